@@ -1,0 +1,266 @@
+#!/usr/bin/env python3
+"""Benchmark of the MI355X hot paths (driver contract: one JSON line on rank 0).
+
+Headline (BASELINE.json configs[1], "C2"): PairHMM forward algorithm on
+1,000,000 synthetic (read, haplotype) pairs per GPU, read length 101,
+haplotype length uniform in [150, 300], fp32 pass + fp64 rescue, inputs
+resident in HBM.  A step = one full pass of the hot path over the batch:
+schedule (device radix sort into 4-pair wave groups) -> fp32 forward kernel ->
+fp64 rescue kernel.  `value` = total cells (sum of R*H) of all ranks * steps /
+max-over-ranks wall time, in GCUPS.
+
+Multi-GPU: one process per GPU (torch.distributed.run); every rank processes
+its own 1M-pair shard (weak scaling, static partition, no data-path
+collective — SURVEY.md §8e).  torch.distributed is used only for the barrier
+and the max-over-ranks timing reduction.
+
+Also reported (not the headline): banded-SW ksw_extend2 GCUPS on C3-shaped
+synthetic extension tasks (2x151 bp reads, bwa defaults) and on the fixed
+qlen=151/tlen=251 variant, cells counted by the kernel exactly as ksw_extend2
+evaluates them; and the CPU baseline (the oracle restatement, OpenMP) on a
+bounded sample, rank 0 / N=1 only.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "falcon-genome_amd"))
+import fcship  # noqa: E402  (after torch: one HIP runtime per process)
+
+METRIC = "PairHMM GCUPS + banded-SW GCUPS per GPU; end-to-end htc regions/sec at 8 GPUs"
+FLOPS_PER_CELL = 11          # M 5 + I 3 + D 3 (FMA = 2)
+FP32_VECTOR_PEAK_TF = 157.3  # MI355X_MICROARCH.md chip table (spec)
+HBM_PEAK_GBS = 8000.0
+
+
+def phmm_dev_batch(p: "fcship.PhmmPairs", dev):
+    keep = {}
+    for k in ("read_bases", "read_bq", "read_iq", "read_dq", "read_gcp", "read_off", "read_len", "hap_bases",
+              "hap_off", "hap_len", "pair_read", "pair_hap"):
+        keep[k] = torch.from_numpy(np.ascontiguousarray(getattr(p, k))).to(dev)
+    b = p.to_struct()
+    for k, t in keep.items():
+        setattr(b, k, t.data_ptr())
+    return b, keep
+
+
+def bsw_dev_batch(t: "fcship.BswTasks", dev):
+    keep = {}
+    for k in ("qbuf", "qoff", "qlen", "tbuf", "toff", "tlen", "h0", "w"):
+        keep[k] = torch.from_numpy(np.ascontiguousarray(getattr(t, k))).to(dev)
+    b = t.to_struct()
+    for k, v in keep.items():
+        setattr(b, k, v.data_ptr())
+    return b, keep
+
+
+def load_traffic(name):
+    """Per-launch HBM bytes of a kernel from a committed rocprofv3 PMC summary."""
+    path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    try:
+        with open(path) as f:
+            return json.load(f).get(name)
+    except (OSError, ValueError):
+        return None
+
+
+def bench_phmm(args, dev, rank, world):
+    p = fcship.synth_phmm(args.seed + 7919 * rank, args.pairs, R=101, hmin=150, hmax=300)
+    cells = p.cells()
+    b, keep = phmm_dev_batch(p, dev)
+    out = torch.empty(p.n_pairs, dtype=torch.float64, device=dev)
+    plan = fcship.C.c_void_p()
+    fcship.check(fcship.lib.fcs_phmm_plan_create(dev.index, p.n_pairs, fcship.C.byref(plan)))
+    opts = fcship.phmm_opts(device=dev.index)
+    stream = torch.cuda.current_stream(dev)
+    sp = stream.cuda_stream
+    B, O = fcship.C.byref(b), fcship.C.byref(opts)
+
+    def step(ev=None):
+        if ev is not None:
+            ev[0].record(stream)
+        fcship.check(fcship.lib.fcs_phmm_dev_schedule(plan, B, sp))
+        if ev is not None:
+            ev[1].record(stream)
+        fcship.check(fcship.lib.fcs_phmm_dev_forward(plan, B, out.data_ptr(), O, sp))
+        if ev is not None:
+            ev[2].record(stream)
+        fcship.check(fcship.lib.fcs_phmm_dev_rescue(plan, B, out.data_ptr(), O, sp))
+        if ev is not None:
+            ev[3].record(stream)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        torch.distributed.barrier()
+    torch.cuda.synchronize(dev)
+    evs = [[torch.cuda.Event(enable_timing=True) for _ in range(4)] for _ in range(args.steps)]
+    t0 = time.perf_counter()
+    for k in range(args.steps):
+        step(evs[k])
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        torch.distributed.barrier()
+    t1 = time.perf_counter()
+    elapsed = torch.tensor([t1 - t0], dtype=torch.float64, device=dev)
+    if world > 1:
+        torch.distributed.all_reduce(elapsed, op=torch.distributed.ReduceOp.MAX)
+    elapsed = float(elapsed.item())
+    sched_ms = float(np.mean([e[0].elapsed_time(e[1]) for e in evs]))
+    fwd_ms = float(np.mean([e[1].elapsed_time(e[2]) for e in evs]))
+    resc_ms = float(np.mean([e[2].elapsed_time(e[3]) for e in evs]))
+    nres = fcship.C.c_int64()
+    fcship.check(fcship.lib.fcs_phmm_plan_rescue_count(plan, sp, fcship.C.byref(nres)))
+    res = out.cpu().numpy()
+    fcship.lib.fcs_phmm_plan_destroy(plan)
+    del keep
+    return dict(p=p, cells=cells, elapsed=elapsed, sched_ms=sched_ms, fwd_ms=fwd_ms, resc_ms=resc_ms,
+                n_rescued=int(nres.value), out=res)
+
+
+def bench_bsw(args, dev, tasks, reps=3):
+    b, keep = bsw_dev_batch(tasks, dev)
+    res = torch.empty((tasks.n, 6), dtype=torch.int32, device=dev)
+    cells = torch.empty(tasks.n, dtype=torch.int64, device=dev)
+    params = fcship.bsw_params()
+    stream = torch.cuda.current_stream(dev)
+    run = lambda: fcship.check(fcship.lib.fcs_bsw_extend_dev(fcship.C.byref(b), fcship.C.byref(params),  # noqa
+                                                             res.data_ptr(), cells.data_ptr(), dev.index,
+                                                             stream.cuda_stream))
+    run()
+    torch.cuda.synchronize(dev)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record(stream)
+    for _ in range(reps):
+        run()
+    e1.record(stream)
+    torch.cuda.synchronize(dev)
+    ms = e0.elapsed_time(e1) / reps
+    ncell = int(cells.sum().item())
+    del keep
+    return dict(ms=ms, cells=ncell, gcups=ncell / (ms * 1e-3) / 1e9, tasks=tasks.n,
+                bytes=int(tasks.qbuf.size + tasks.tbuf.size + 24 * tasks.n))
+
+
+def cpu_baseline_phmm(p, budget_s, threads):
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import oracle_lib  # test infrastructure: CPU baseline leg only
+    n_done, cells, chunk, t_used = 0, 0, 4000, 0.0
+    while t_used < budget_s and n_done < p.n_pairs:
+        hi = min(p.n_pairs, n_done + chunk)
+        sub = fcship.PhmmPairs(p.read_bases, p.read_bq, p.read_iq, p.read_dq, p.read_gcp, p.read_off, p.read_len,
+                               p.hap_bases, p.hap_off, p.hap_len, p.pair_read[n_done:hi], p.pair_hap[n_done:hi])
+        t0 = time.perf_counter()
+        oracle_lib.phmm_batch(sub, threads=threads)
+        t_used += time.perf_counter() - t0
+        cells += sub.cells()
+        n_done = hi
+    return dict(value=cells / t_used / 1e9, unit="GCUPS", cores=threads, kind="port",
+                sample=f"first {n_done} of the {p.n_pairs} C2 pairs ({cells / 1e9:.2f} G cells, {t_used:.1f} s), "
+                       f"scalar C oracle restatement (GKL float + double rescue), OpenMP {threads} threads")
+
+
+def cpu_baseline_bsw(tasks, budget_s, threads):
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import oracle_lib
+    n = tasks.n
+    t0 = time.perf_counter()
+    _, cells = oracle_lib.ksw_extend2_batch(tasks, fcship.default_mat(), threads=threads)
+    dt = time.perf_counter() - t0
+    return dict(value=int(cells.sum()) / dt / 1e9, unit="GCUPS", cores=threads, kind="port",
+                sample=f"{n} C3 extension tasks, scalar C ksw_extend2 restatement, OpenMP {threads} threads")
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--pairs", type=int, default=1_000_000)
+    ap.add_argument("--seed", type=int, default=20261015)
+    ap.add_argument("--bsw-reads", type=int, default=500_000)
+    ap.add_argument("--no-bsw", action="store_true")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-budget", type=float, default=12.0)
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dev = torch.device("cuda", local)
+    torch.cuda.set_device(dev)
+    if world > 1:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        torch.distributed.init_process_group("nccl", device_id=dev)
+
+    ph = bench_phmm(args, dev, rank, world)
+    total_cells = ph["cells"] * world * args.steps
+    value = total_cells / ph["elapsed"] / 1e9
+    fwd_s = ph["fwd_ms"] * 1e-3
+    achieved_tf = FLOPS_PER_CELL * ph["cells"] / fwd_s / 1e12
+    traffic = load_traffic("phmm_kernel<float,false,false>")
+    p = ph["p"]
+    alg_bytes = int(5 * p.read_len.sum() + p.hap_len.sum() + 4 * p.n_pairs + 8 * p.n_pairs)
+
+    line = {
+        "metric": METRIC,
+        "value": round(value, 3),
+        "unit": "GCUPS",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(ph["elapsed"] / args.steps * 1e3, 3),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "fp32 (fp64 rescue)",
+        "data": "synthetic (seeded C2 generator: hap uniform ACGT, read = hap substring with 1% subs / 0.1% indels, "
+                "base Q U[10,40], ins/del GOP 45, GCP 10)",
+        "config": {"workload": "C2: PairHMM, 1M pairs per GPU, read len 101, hap len U[150,300], fp32 + fp64 rescue",
+                   "pairs_per_gpu": p.n_pairs, "cells_per_gpu": ph["cells"], "parallelism": f"static shard x{world}"},
+        "stages_ms": {"schedule": round(ph["sched_ms"], 3), "forward_fp32": round(ph["fwd_ms"], 3),
+                      "rescue_fp64": round(ph["resc_ms"], 3)},
+        "rescued_pairs": ph["n_rescued"],
+        "roofline": {"bound": "valu", "achieved": round(achieved_tf, 3), "peak": FP32_VECTOR_PEAK_TF,
+                     "unit": "TFLOP/s", "frac": round(achieved_tf / FP32_VECTOR_PEAK_TF, 4),
+                     "traffic": traffic,
+                     "kernel": "phmm_kernel<float> (fp32 forward)",
+                     "kernel_gcups": round(ph["cells"] / fwd_s / 1e9, 3),
+                     "algorithmic_bytes_per_launch": alg_bytes,
+                     "algorithmic_hbm_GBs": round(alg_bytes / fwd_s / 1e9, 2),
+                     "hbm_frac": round(alg_bytes / fwd_s / 1e9 / HBM_PEAK_GBS, 5)},
+    }
+
+    if not args.no_bsw and rank == 0:
+        c3 = fcship.synth_bsw(args.seed, args.bsw_reads, read_len=151, ref_len=10_000_000, w=100)
+        fx = fcship.synth_bsw(args.seed, max(1, args.bsw_reads // 4), read_len=151, ref_len=10_000_000, w=100,
+                              mode=1, fixed_q=151, fixed_t=251)
+        r3 = bench_bsw(args, dev, c3)
+        rf = bench_bsw(args, dev, fx)
+        line["bsw"] = {"workload": "C3: ksw_extend2 left/right seed extensions of 2x151 bp reads, bwa defaults",
+                       "c3_gcups": round(r3["gcups"], 3), "c3_tasks": r3["tasks"], "c3_ms": round(r3["ms"], 3),
+                       "fixed_151x251_gcups": round(rf["gcups"], 3), "fixed_tasks": rf["tasks"],
+                       "int_ops_per_cell": 12}
+        if world == 1 and not args.no_cpu_baseline:
+            line["bsw"]["cpu_baseline"] = cpu_baseline_bsw(
+                fcship.synth_bsw(args.seed + 1, 20000, read_len=151, ref_len=10_000_000), 0,
+                min(16, os.cpu_count() or 1))
+
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        line["cpu_baseline"] = cpu_baseline_phmm(p, args.cpu_budget, min(16, os.cpu_count() or 1))
+
+    if rank == 0:
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        torch.distributed.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,431 @@
+// BWA-MEM banded Smith-Waterman (ksw_extend2 / ksw_global2) on gfx950.
+//
+// Algorithm: bwa ksw.c, reached from
+// /root/reference/src/workers/BWAWorker.cpp:134-166 (bwa-flow --offload).
+//
+// Mapping (DESIGN.md §Banded SW): one 64-lane wave per extension task.  Lane l
+// owns query columns j = l + 64*k (k < NS slots) and keeps bwa's eh[j] = {h, e}
+// for those columns in registers, so the "stale eh[] beyond the band" that bwa
+// re-reads when the band grows is reproduced exactly.  Target rows are processed
+// in bwa's order, one row per iteration:
+//   * M and E need only the lane's own column;
+//   * F(i,j) = max(F0 - (j-beg)e, max_{beg<=k<j} (t_k - (j-1-k)e)),
+//     t_k = max(M_k - (o_ins+e_ins), 0), is an exclusive max-plus prefix scan
+//     over the lanes (both E and F open from M in ksw, so the row has no other
+//     dependency) — 6 DPP steps + one wave shift per slot;
+//   * eh[j].h <- H(i, j-1) is a one-lane DPP shift of the row's H;
+//   * row max / arg-max (ties to the larger j), z-drop, and the beg/end band
+//     trimming are wave ballots + scalar bit scans, so all control flow is
+//     wave-uniform and every integer matches bwa bit for bit.
+#include <hip/hip_runtime.h>
+
+#include "fcship_internal.h"
+
+namespace fcs {
+
+static constexpr int kMinusInf = -0x40000000;       // ksw.c MINUS_INF
+static constexpr int kScanNeg = (-2147483647 - 1) + (1 << 24);  // below any reachable scan value
+
+__device__ __forceinline__ unsigned long long ballot64(bool v) { return __ballot(v); }
+
+// Exclusive prefix max of u across slots (column order), seeded with carry.
+template <int NS>
+__device__ __forceinline__ void excl_scan(const int (&u)[NS], int carry, int (&ex)[NS]) {
+#pragma unroll
+  for (int k = 0; k < NS; ++k) {
+    const int incl = wave_incl_max(u[k], kScanNeg);
+    int e = dpp_wave_shr1_i(carry, incl);
+    ex[k] = max(e, carry);
+    carry = max(carry, read_lane(incl, 63));
+  }
+}
+
+// Query profile for column j: bytes mat[t*5 + q_j] for t = 0..3 packed, and t = 4.
+__device__ __forceinline__ int prof_score(int lo, int hi, int tb) {
+  return tb < 4 ? (int)(int8_t)(lo >> (tb << 3)) : hi;
+}
+
+template <int NS>
+__device__ void extend_task(const BswDevBatch& b, const BswParams& p, long long task, uint8_t* __restrict__ tl,
+                            int32_t* __restrict__ res, int64_t* __restrict__ cells_out) {
+  const int lane = lane_id();
+  const int qlen = b.qlen[task], tlen = b.tlen[task], h0 = b.h0[task];
+  int w = b.w[task];
+  const uint8_t* __restrict__ q = b.qbuf + b.qoff[task];
+  const uint8_t* __restrict__ tg = b.tbuf + b.toff[task];
+  for (int i = lane; i < tlen; i += 64) tl[i] = tg[i];
+
+  const int oe_del = p.o_del + p.e_del, oe_ins = p.o_ins + p.e_ins;
+  const int e_del = p.e_del, e_ins = p.e_ins;
+  int H[NS], E[NS], plo[NS], phi[NS];
+  const int h1v = h0 > oe_ins ? h0 - oe_ins : 0;
+#pragma unroll
+  for (int k = 0; k < NS; ++k) {
+    const int j = lane + 64 * k;
+    const int qb = j < qlen ? (int)q[j] : 4;
+    plo[k] = (p.mat[0 * 5 + qb] & 0xFF) | ((p.mat[1 * 5 + qb] & 0xFF) << 8) | ((p.mat[2 * 5 + qb] & 0xFF) << 16) |
+             ((p.mat[3 * 5 + qb] & 0xFF) << 24);
+    phi[k] = p.mat[4 * 5 + qb];
+    int hv = 0;
+    if (j == 0) hv = h0;
+    else if (j == 1 && j <= qlen) hv = h1v;
+    else if (j >= 2 && j <= qlen) hv = max(h1v - (j - 1) * e_ins, 0);
+    H[k] = hv;
+    E[k] = 0;
+  }
+  {
+    int max_ins = (int)((double)(qlen * p.max_mat + p.end_bonus - p.o_ins) / e_ins + 1.);
+    max_ins = max_ins > 1 ? max_ins : 1;
+    w = w < max_ins ? w : max_ins;
+    int max_del = (int)((double)(qlen * p.max_mat + p.end_bonus - p.o_del) / e_del + 1.);
+    max_del = max_del > 1 ? max_del : 1;
+    w = w < max_del ? w : max_del;
+  }
+  __syncthreads();
+
+  int mx = h0, max_i = -1, max_j = -1, max_ie = -1, gscore = -1, max_off = 0;
+  int beg = 0, end = qlen;
+  long long ncell = 0;
+  for (int i = 0; i < tlen; ++i) {
+    const int tb = first_lane((int)tl[i]);
+    if (beg < i - w) beg = i - w;
+    if (end > i + w + 1) end = i + w + 1;
+    if (end > qlen) end = qlen;
+    int h1 = 0;
+    if (beg == 0) {
+      h1 = h0 - (p.o_del + e_del * (i + 1));
+      if (h1 < 0) h1 = 0;
+    }
+    if (beg >= end) {
+      // empty row: bwa still stores eh[end] = {h1, 0}; j == beg here.
+#pragma unroll
+      for (int k = 0; k < NS; ++k)
+        if (lane + 64 * k == end) { H[k] = h1; E[k] = 0; }
+      if (beg == qlen) {
+        max_ie = gscore > h1 ? max_ie : i;
+        gscore = gscore > h1 ? gscore : h1;
+      }
+      break;  // row max is 0
+    }
+    ncell += end - beg;
+    int M[NS], u[NS], ex[NS], h[NS];
+#pragma unroll
+    for (int k = 0; k < NS; ++k) {
+      const int j = lane + 64 * k;
+      const bool inb = j >= beg && j < end;
+      const int sc = prof_score(plo[k], phi[k], tb);
+      M[k] = H[k] ? H[k] + sc : 0;
+      const int t = max(M[k] - oe_ins, 0);
+      u[k] = inb ? t + j * e_ins : kScanNeg;
+    }
+    excl_scan<NS>(u, (beg - 1) * e_ins, ex);
+    int rowmax = -1;
+#pragma unroll
+    for (int k = 0; k < NS; ++k) {
+      const int j = lane + 64 * k;
+      const bool inb = j >= beg && j < end;
+      const int f = ex[k] - (j - 1) * e_ins;
+      const int hh = max(max(M[k], E[k]), f);
+      h[k] = inb ? hh : -1;
+      rowmax = max(rowmax, h[k]);
+    }
+    const int m = wave_max(rowmax);
+    // arg-max, ties to the larger j
+    int mj = -1;
+#pragma unroll
+    for (int k = NS - 1; k >= 0; --k) {
+      const unsigned long long bm = ballot64(h[k] == m);
+      if (mj < 0 && bm) mj = 64 * k + 63 - __builtin_clzll(bm);
+    }
+    // eh update over [beg, end]
+    int carry_h = h1;
+    unsigned long long nz[NS];
+#pragma unroll
+    for (int k = 0; k < NS; ++k) {
+      const int j = lane + 64 * k;
+      const int hs = dpp_wave_shr1_i(carry_h, h[k]);
+      const int lastk = read_lane(h[k], 63);
+      const int t = max(M[k] - oe_del, 0);
+      const int en = max(E[k] - e_del, t);
+      if (j >= beg && j <= end) {
+        H[k] = (j == beg) ? h1 : hs;
+        E[k] = (j == end) ? 0 : en;
+      }
+      carry_h = lastk;
+      nz[k] = ballot64(j >= beg && j <= end && (H[k] != 0 || E[k] != 0));
+    }
+    if (end == qlen) {
+      // h1 after the loop = H(i, qlen-1), now stored at eh[qlen].h
+      int hl = 0;
+#pragma unroll
+      for (int k = 0; k < NS; ++k)
+        if ((end >> 6) == k) hl = read_lane(H[k], end & 63);
+      max_ie = gscore > hl ? max_ie : i;
+      gscore = gscore > hl ? gscore : hl;
+    }
+    if (m == 0) break;
+    if (m > mx) {
+      mx = m, max_i = i, max_j = mj;
+      const int d = mj > i ? mj - i : i - mj;
+      max_off = max_off > d ? max_off : d;
+    } else if (p.zdrop > 0) {
+      if (i - max_i > mj - max_j) {
+        if (mx - m - ((i - max_i) - (mj - max_j)) * e_del > p.zdrop) break;
+      } else {
+        if (mx - m - ((mj - max_j) - (i - max_i)) * e_ins > p.zdrop) break;
+      }
+    }
+    // band trimming: first non-zero in [beg, end), last non-zero in [beg', end]
+    int nb = end, last = -1;
+#pragma unroll
+    for (int k = 0; k < NS; ++k) {
+      unsigned long long bm = nz[k];
+      if (nb == end) {
+        unsigned long long bb = bm;
+        const int eb = end - 64 * k;
+        if (eb >= 0 && eb < 64) bb &= ~(1ull << eb);
+        if (bb) nb = 64 * k + __builtin_ctzll(bb);
+      }
+      if (bm) last = 64 * k + 63 - __builtin_clzll(bm);
+    }
+    beg = nb;
+    if (last >= 0) end = last + 2 < qlen ? last + 2 : qlen;
+    else end = beg + 1 < qlen ? beg + 1 : qlen;
+  }
+  if (lane == 0) {
+    int32_t* r = res + 6 * task;
+    r[0] = mx;
+    r[1] = max_j + 1;
+    r[2] = max_i + 1;
+    r[3] = max_ie + 1;
+    r[4] = gscore;
+    r[5] = max_off;
+    if (cells_out) cells_out[task] = ncell;
+  }
+}
+
+template <int MAXNS>
+__global__ __launch_bounds__(64) void bsw_extend_kernel(const BswDevBatch b, const BswParams p, int32_t* __restrict__ res,
+                                                        int64_t* __restrict__ cells) {
+  extern __shared__ __align__(16) unsigned char tl[];
+  for (long long task = blockIdx.x; task < b.n; task += gridDim.x) {
+    const int qlen = b.qlen[task];
+    const int ns = (qlen + 1 + 63) >> 6;
+    if (MAXNS <= 4) {
+      switch (ns) {
+        case 0:
+        case 1: extend_task<1>(b, p, task, tl, res, cells); break;
+        case 2: extend_task<2>(b, p, task, tl, res, cells); break;
+        case 3: extend_task<3>(b, p, task, tl, res, cells); break;
+        default: extend_task<4>(b, p, task, tl, res, cells); break;
+      }
+    } else {
+      if (ns <= 8) extend_task<8>(b, p, task, tl, res, cells);
+      else extend_task<16>(b, p, task, tl, res, cells);
+    }
+    __syncthreads();
+  }
+}
+
+int launch_bsw_extend(const BswDevBatch& b, const BswParams& p, int max_qlen, int max_tlen, int32_t* res,
+                      int64_t* cells, hipStream_t s) {
+  if (b.n <= 0) return FCS_OK;
+  if (max_qlen > 1023) return fail(FCS_ERR_UNSUPPORTED, "[E::fcship] ksw_extend2: qlen > 1023 unsupported");
+  const size_t lds = (size_t)((max_tlen + 64 + 15) / 16) * 16;
+  if (lds > 64 * 1024) return fail(FCS_ERR_UNSUPPORTED, "[E::fcship] ksw_extend2: tlen too large");
+  long long grid = b.n;
+  const long long cap = 256LL * 64;
+  if (grid > cap) grid = cap;
+  if (max_qlen <= 255)
+    hipLaunchKernelGGL(bsw_extend_kernel<4>, dim3((unsigned)grid), dim3(64), lds, s, b, p, res, cells);
+  else
+    hipLaunchKernelGGL(bsw_extend_kernel<16>, dim3((unsigned)grid), dim3(64), lds, s, b, p, res, cells);
+  FCS_HIP_CHECK(hipGetLastError());
+  return FCS_OK;
+}
+
+// ---------------------------------------------------------------- ksw_global2
+template <int NS>
+__device__ void global_task(const BswDevBatch& b, const BswParams& p, long long task, uint8_t* __restrict__ tl,
+                            int32_t* __restrict__ scores, uint8_t* __restrict__ zbuf, const int64_t* __restrict__ zoff) {
+  const int lane = lane_id();
+  const int qlen = b.qlen[task], tlen = b.tlen[task], w = b.w[task];
+  const uint8_t* __restrict__ q = b.qbuf + b.qoff[task];
+  const uint8_t* __restrict__ tg = b.tbuf + b.toff[task];
+  for (int i = lane; i < tlen; i += 64) tl[i] = tg[i];
+  const int oe_del = p.o_del + p.e_del, oe_ins = p.o_ins + p.e_ins;
+  const int e_del = p.e_del, e_ins = p.e_ins;
+  const int n_col = qlen < 2 * w + 1 ? qlen : 2 * w + 1;
+  uint8_t* __restrict__ z = zbuf ? zbuf + zoff[task] : nullptr;
+  int H[NS], E[NS], plo[NS], phi[NS];
+#pragma unroll
+  for (int k = 0; k < NS; ++k) {
+    const int j = lane + 64 * k;
+    const int qb = j < qlen ? (int)q[j] : 4;
+    plo[k] = (p.mat[0 * 5 + qb] & 0xFF) | ((p.mat[1 * 5 + qb] & 0xFF) << 8) | ((p.mat[2 * 5 + qb] & 0xFF) << 16) |
+             ((p.mat[3 * 5 + qb] & 0xFF) << 24);
+    phi[k] = p.mat[4 * 5 + qb];
+    int hv = kMinusInf;
+    if (j == 0) hv = 0;
+    else if (j <= qlen && j <= w) hv = -(p.o_ins + e_ins * j);
+    H[k] = hv;
+    E[k] = kMinusInf;
+  }
+  __syncthreads();
+  for (int i = 0; i < tlen; ++i) {
+    const int tb = first_lane((int)tl[i]);
+    const int beg = i > w ? i - w : 0;
+    const int end = i + w + 1 < qlen ? i + w + 1 : qlen;
+    const int h1 = beg == 0 ? -(p.o_del + e_del * (i + 1)) : kMinusInf;
+    int M[NS], u[NS], ex[NS];
+#pragma unroll
+    for (int k = 0; k < NS; ++k) {
+      const int j = lane + 64 * k;
+      const bool inb = j >= beg && j < end;
+      M[k] = H[k] + prof_score(plo[k], phi[k], tb);
+      u[k] = inb ? (M[k] - oe_ins) + j * e_ins : kScanNeg;
+    }
+    // F0 = MINUS_INF enters as a virtual column beg-1
+    excl_scan<NS>(u, kMinusInf + (beg - 1) * e_ins, ex);
+    int carry_h = h1;
+#pragma unroll
+    for (int k = 0; k < NS; ++k) {
+      const int j = lane + 64 * k;
+      const bool inb = j >= beg && j < end;
+      const int f = ex[k] - (j - 1) * e_ins;
+      const int m = M[k], e = E[k];
+      int d = m >= e ? 0 : 1;
+      int hh = m >= e ? m : e;
+      d = hh >= f ? d : 2;
+      hh = hh >= f ? hh : f;
+      int t = m - oe_del;
+      const int e2 = e - e_del;
+      d |= e2 > t ? 1 << 2 : 0;
+      const int en = e2 > t ? e2 : t;
+      t = m - oe_ins;
+      const int f2 = f - e_ins;
+      d |= f2 > t ? 2 << 4 : 0;
+      if (z && inb) z[(long long)i * n_col + (j - beg)] = (uint8_t)d;
+      const int hsrc = inb ? hh : 0;
+      const int hs = dpp_wave_shr1_i(carry_h, hsrc);
+      carry_h = read_lane(hsrc, 63);
+      // bwa writes eh[end] = {h1, MINUS_INF} even when the band is empty
+      // (beg >= end, h1 then still holds its row-start value).
+      if ((j >= beg && j <= end) || j == end) {
+        H[k] = (j == beg || beg >= end) ? h1 : hs;
+        E[k] = (j == end) ? kMinusInf : en;
+      }
+    }
+  }
+  // score = eh[qlen].h
+  int sc = 0;
+#pragma unroll
+  for (int k = 0; k < NS; ++k)
+    if ((qlen >> 6) == k) sc = read_lane(H[k], qlen & 63);
+  if (lane == 0) scores[task] = sc;
+}
+
+template <int MAXNS>
+__global__ __launch_bounds__(64) void bsw_global_kernel(const BswDevBatch b, const BswParams p, int32_t* __restrict__ scores,
+                                                        uint8_t* __restrict__ zbuf, const int64_t* __restrict__ zoff) {
+  extern __shared__ __align__(16) unsigned char tl[];
+  for (long long task = blockIdx.x; task < b.n; task += gridDim.x) {
+    const int qlen = b.qlen[task];
+    const int ns = (qlen + 1 + 63) >> 6;
+    if (MAXNS <= 4) {
+      switch (ns) {
+        case 0:
+        case 1: global_task<1>(b, p, task, tl, scores, zbuf, zoff); break;
+        case 2: global_task<2>(b, p, task, tl, scores, zbuf, zoff); break;
+        case 3: global_task<3>(b, p, task, tl, scores, zbuf, zoff); break;
+        default: global_task<4>(b, p, task, tl, scores, zbuf, zoff); break;
+      }
+    } else {
+      if (ns <= 8) global_task<8>(b, p, task, tl, scores, zbuf, zoff);
+      else global_task<16>(b, p, task, tl, scores, zbuf, zoff);
+    }
+    __syncthreads();
+  }
+}
+
+// One lane per task walks the direction bytes back from (tlen-1, last column).
+__global__ void bsw_traceback_kernel(const BswDevBatch b, const uint8_t* __restrict__ zbuf,
+                                     const int64_t* __restrict__ zoff, uint32_t* __restrict__ cigar,
+                                     const int64_t* __restrict__ cigar_off, const int32_t* __restrict__ cigar_cap,
+                                     int32_t* __restrict__ n_cigar) {
+  const long long task = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (task >= b.n) return;
+  const int qlen = b.qlen[task], tlen = b.tlen[task], w = b.w[task];
+  const int n_col = qlen < 2 * w + 1 ? qlen : 2 * w + 1;
+  const uint8_t* z = zbuf + zoff[task];
+  const long long zsize = (long long)n_col * (tlen > 0 ? tlen : 0);
+  uint32_t* cg = cigar + cigar_off[task];
+  const int cap = cigar_cap[task];
+  int n = 0, which = 0, curop = -1;
+  uint32_t curlen = 0;
+  int i = tlen - 1;
+  int k = (i + w + 1 < qlen ? i + w + 1 : qlen) - 1;
+  // ops are produced last-to-first as runs; each finished run is stored, the
+  // array is reversed at the end (bwa push_cigar + reverse).
+  auto push = [&](int op, int len) {
+    if (op == curop) {
+      curlen += (uint32_t)len;
+    } else {
+      if (curop >= 0) {
+        if (n < cap) cg[n] = curlen << 4 | (uint32_t)curop;
+        ++n;
+      }
+      curop = op;
+      curlen = (uint32_t)len;
+    }
+  };
+  while (i >= 0 && k >= 0) {
+    // cells outside the written band read as 0 (zeroed matrix, bounded index;
+    // see oracle/ksw_oracle.c header) instead of bwa's undefined read
+    const long long zi = (long long)i * n_col + (k - (i > w ? i - w : 0));
+    which = (zi >= 0 && zi < zsize) ? (z[zi] >> (which << 1) & 3) : 0;
+    if (which == 0) push(0, 1), --i, --k;
+    else if (which == 1) push(2, 1), --i;
+    else push(1, 1), --k;
+  }
+  if (i >= 0) push(2, i + 1);
+  if (k >= 0) push(1, k + 1);
+  if (curop >= 0) {
+    if (n < cap) cg[n] = curlen << 4 | (uint32_t)curop;
+    ++n;
+  }
+  const int nn = n < cap ? n : cap;
+  for (int a = 0; a < nn >> 1; ++a) {
+    const uint32_t t = cg[a];
+    cg[a] = cg[nn - 1 - a];
+    cg[nn - 1 - a] = t;
+  }
+  n_cigar[task] = n;
+}
+
+int launch_bsw_global(const BswDevBatch& b, const BswParams& p, int max_qlen, int max_tlen, int32_t* scores,
+                      uint8_t* zbuf, int64_t zbytes, const int64_t* zoff, uint32_t* cigar, const int64_t* cigar_off,
+                      const int32_t* cigar_cap, int32_t* n_cigar, hipStream_t s) {
+  if (b.n <= 0) return FCS_OK;
+  if (max_qlen > 1023) return fail(FCS_ERR_UNSUPPORTED, "[E::fcship] ksw_global2: qlen > 1023 unsupported");
+  if (zbuf && zbytes > 0) FCS_HIP_CHECK(hipMemsetAsync(zbuf, 0, (size_t)zbytes, s));
+  const size_t lds = (size_t)((max_tlen + 64 + 15) / 16) * 16;
+  if (lds > 64 * 1024) return fail(FCS_ERR_UNSUPPORTED, "[E::fcship] ksw_global2: tlen too large");
+  long long grid = b.n;
+  const long long cap = 256LL * 64;
+  if (grid > cap) grid = cap;
+  if (max_qlen <= 255)
+    hipLaunchKernelGGL(bsw_global_kernel<4>, dim3((unsigned)grid), dim3(64), lds, s, b, p, scores, zbuf, zoff);
+  else
+    hipLaunchKernelGGL(bsw_global_kernel<16>, dim3((unsigned)grid), dim3(64), lds, s, b, p, scores, zbuf, zoff);
+  FCS_HIP_CHECK(hipGetLastError());
+  if (cigar) {
+    const long long nb = (b.n + 63) / 64;
+    hipLaunchKernelGGL(bsw_traceback_kernel, dim3((unsigned)nb), dim3(64), 0, s, b, zbuf, zoff, cigar, cigar_off,
+                       cigar_cap, n_cigar);
+    FCS_HIP_CHECK(hipGetLastError());
+  }
+  return FCS_OK;
+}
+
+}  // namespace fcs

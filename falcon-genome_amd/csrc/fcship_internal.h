@@ -1,0 +1,151 @@
+// Internal definitions shared by the gfx950 kernels and the C-ABI layer.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include <string>
+
+#include "fcship.h"
+
+namespace fcs {
+
+// ------------------------------------------------------------ error plumbing
+void set_error(const std::string& msg);
+int fail(int code, const std::string& msg);
+#define FCS_HIP_CHECK(expr)                                                                  \
+  do {                                                                                       \
+    hipError_t _e = (expr);                                                                  \
+    if (_e != hipSuccess)                                                                    \
+      return ::fcs::fail(FCS_ERR_DEVICE, std::string("[E::fcship] ") + #expr + ": " +        \
+                                             hipGetErrorString(_e));                         \
+  } while (0)
+
+// ------------------------------------------------------------ DPP cross-lane
+// CDNA (gfx9) DPP controls.  row = 16 lanes.
+enum : int {
+  kDppRowShr1 = 0x111,
+  kDppRowShr2 = 0x112,
+  kDppRowShr4 = 0x114,
+  kDppRowShr8 = 0x118,
+  kDppWaveShr1 = 0x138,
+  kDppRowBcast15 = 0x142,
+  kDppRowBcast31 = 0x143,
+};
+
+// src taken from lane-1 within each 16-lane row; lane 0 of a row keeps `old`.
+__device__ __forceinline__ int dpp_row_shr1_i(int old, int src) {
+  return __builtin_amdgcn_update_dpp(old, src, kDppRowShr1, 0xF, 0xF, false);
+}
+__device__ __forceinline__ float dpp_row_shr1_f(float old, float src) {
+  return __int_as_float(
+      __builtin_amdgcn_update_dpp(__float_as_int(old), __float_as_int(src), kDppRowShr1, 0xF, 0xF, false));
+}
+__device__ __forceinline__ double dpp_row_shr1_d(double old, double src) {
+  const long long o = __double_as_longlong(old), s = __double_as_longlong(src);
+  const int lo = __builtin_amdgcn_update_dpp((int)o, (int)s, kDppRowShr1, 0xF, 0xF, false);
+  const int hi = __builtin_amdgcn_update_dpp((int)(o >> 32), (int)(s >> 32), kDppRowShr1, 0xF, 0xF, false);
+  return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
+}
+template <typename T> __device__ __forceinline__ T dpp_row_shr1(T old, T src);
+template <> __device__ __forceinline__ float dpp_row_shr1<float>(float old, float src) { return dpp_row_shr1_f(old, src); }
+template <> __device__ __forceinline__ double dpp_row_shr1<double>(double old, double src) { return dpp_row_shr1_d(old, src); }
+
+// Whole-wave shift by one lane: lane l gets src of lane l-1, lane 0 keeps `old`.
+__device__ __forceinline__ int dpp_wave_shr1_i(int old, int src) {
+  return __builtin_amdgcn_update_dpp(old, src, kDppWaveShr1, 0xF, 0xF, false);
+}
+
+// Inclusive max-scan over the 64 lanes of a wave (lane order), identity `neg`.
+__device__ __forceinline__ int wave_incl_max(int v, int neg) {
+  v = max(v, __builtin_amdgcn_update_dpp(neg, v, kDppRowShr1, 0xF, 0xF, false));
+  v = max(v, __builtin_amdgcn_update_dpp(neg, v, kDppRowShr2, 0xF, 0xF, false));
+  v = max(v, __builtin_amdgcn_update_dpp(neg, v, kDppRowShr4, 0xF, 0xF, false));
+  v = max(v, __builtin_amdgcn_update_dpp(neg, v, kDppRowShr8, 0xF, 0xF, false));
+  v = max(v, __builtin_amdgcn_update_dpp(neg, v, kDppRowBcast15, 0xA, 0xF, false));
+  v = max(v, __builtin_amdgcn_update_dpp(neg, v, kDppRowBcast31, 0xC, 0xF, false));
+  return v;
+}
+
+__device__ __forceinline__ int lane_id() { return (int)__lane_id(); }
+
+__device__ __forceinline__ int read_lane(int v, int lane) { return __builtin_amdgcn_readlane(v, lane); }
+__device__ __forceinline__ int first_lane(int v) { return __builtin_amdgcn_readfirstlane(v); }
+
+// Max over the wave, result uniform.
+__device__ __forceinline__ int wave_max(int v) {
+  return read_lane(wave_incl_max(v, INT32_MIN), 63);
+}
+
+// ------------------------------------------------------------ PairHMM tables
+// Host-computed (fcship_tables.cpp) GKL Context<T> tables, uploaded once per device.
+template <typename T>
+struct PhmmTables {
+  const T* ph2pr;   // [128] 10^(-q/10)
+  const T* dmatch;  // [128] 1 - ph2pr[q]          (prior on match)
+  const T* dmis;    // [128] ph2pr[q] / 3          (prior on mismatch)
+  const T* mm;      // [kMmEntries] matchToMatch(max,min) for quals 0..127
+  T init_const;     // 2^120 (float) / 2^1020 (double)
+  T log10_init;     // log10f(2^120) / log10(2^1020), host libm
+};
+constexpr int kMmEntries = (127 * 128) / 2 + 128;  // index (mx*(mx+1))/2 + mn, mx <= 127
+
+// Raw device-side view of an fcs_phmm_batch.
+struct PhmmDevBatch {
+  const uint8_t *rb, *bq, *iq, *dq, *gq;
+  const int64_t* read_off;
+  const int32_t* read_len;
+  const uint8_t* hb;
+  const int64_t* hap_off;
+  const int32_t* hap_len;
+  const int32_t* pair_read;
+  const int32_t* pair_hap;
+  int64_t n_pairs;
+};
+
+// Per-device state shared by all calls (tables).
+struct DeviceTables {
+  bool ready = false;
+  float* f_tabs = nullptr;   // ph2pr | dmatch | dmis | mm
+  double* d_tabs = nullptr;
+  PhmmTables<float> tf;
+  PhmmTables<double> td;
+};
+int get_device_tables(int device, DeviceTables** out);
+
+// Host table builder (fcship_tables.cpp).
+void build_phmm_tables_f(float* ph2pr, float* dmatch, float* dmis, float* mm);
+void build_phmm_tables_d(double* ph2pr, double* dmatch, double* dmis, double* mm);
+
+// ------------------------------------------------------------ kernel launchers
+int launch_phmm_keys(const PhmmDevBatch& b, uint32_t* keys, int32_t* idx, hipStream_t s);
+int launch_phmm_forward(const PhmmDevBatch& b, const int32_t* order, int64_t count, int max_hap_len,
+                        const DeviceTables& t, bool exact, double* out, int32_t* rescue_list,
+                        unsigned long long* rescue_count, float thr, bool use_rescue, hipStream_t s);
+int launch_phmm_rescue(const PhmmDevBatch& b, const int32_t* list, const unsigned long long* count_dev,
+                       int64_t max_count, int max_hap_len, const DeviceTables& t, bool exact, double* out,
+                       hipStream_t s);
+
+struct BswDevBatch {
+  const uint8_t* qbuf;
+  const int64_t* qoff;
+  const int32_t* qlen;
+  const uint8_t* tbuf;
+  const int64_t* toff;
+  const int32_t* tlen;
+  const int32_t* h0;
+  const int32_t* w;
+  int64_t n;
+};
+struct BswParams {
+  int8_t mat[25];
+  int32_t o_del, e_del, o_ins, e_ins, end_bonus, zdrop;
+  int32_t max_mat;
+};
+int launch_bsw_extend(const BswDevBatch& b, const BswParams& p, int max_qlen, int max_tlen, int32_t* res,
+                      int64_t* cells, hipStream_t s);
+int launch_bsw_global(const BswDevBatch& b, const BswParams& p, int max_qlen, int max_tlen, int32_t* scores,
+                      uint8_t* zbuf, int64_t zbytes, const int64_t* zoff, uint32_t* cigar, const int64_t* cigar_off,
+                      const int32_t* cigar_cap, int32_t* n_cigar, hipStream_t s);
+
+}  // namespace fcs

@@ -1,0 +1,262 @@
+/*
+ * fcship.h — C-ABI of the MI355X (gfx950) hot-path library libfcship.so.
+ *
+ * This is the drop-in boundary for the two dynamic-programming hot paths that
+ * the reference's `fcs-genome` CLI reaches only through external processes:
+ *
+ *   PairHMM forward algorithm (htc / mutect2)
+ *     reference call-out : HTCWorker::setup builds `java -jar GATK HaplotypeCaller
+ *                          ... --native-pair-hmm-threads=N`
+ *                          (/root/reference/src/workers/HTCWorker.cpp:51-85),
+ *                          Mutect2Worker::setup (/root/reference/src/workers/Mutect2Worker.cpp:109-192),
+ *                          FPGA offload via the Blaze NAM daemon started by
+ *                          BackgroundExecutor (/root/reference/src/worker-htc.cpp:100-112,
+ *                          /root/reference/src/worker-mutect2.cpp:153-165).
+ *     interface replaced : GKL IntelPairHmm.computeLikelihoodsNative(ReadDataHolder[],
+ *                          HaplotypeDataHolder[], double[] likelihoods) [EXT, not
+ *                          vendored]; see fcs_phmm_compute.
+ *
+ *   BWA-MEM banded Smith-Waterman (align)
+ *     reference call-out : BWAWorker::setup builds `bwa-flow mem ... --offload
+ *                          --use_fpga --fpga_path=<root>/fpga/sw.xclbin`
+ *                          (/root/reference/src/workers/BWAWorker.cpp:134-166;
+ *                          config keys /root/reference/src/config.cpp:297-300).
+ *     interface replaced : bwa ksw.c ksw_extend2() / ksw_global2() [EXT, not
+ *                          vendored]; see fcs_ksw_extend2 / fcs_ksw_global2 (same
+ *                          argument lists) and the batched fcs_bsw_* entry points.
+ *
+ * Conventions:
+ *   - every function returns FCS_OK (0) or a negative FCS_ERR_* code; the
+ *     message of the last failure on the calling thread is fcs_last_error();
+ *   - no C++ exceptions cross the boundary;
+ *   - the caller owns every buffer; nothing is retained after a synchronous
+ *     return;
+ *   - entry points are thread-safe; each (thread, device) pair uses its own
+ *     HIP stream for the synchronous host-pointer calls;
+ *   - `device` selects the GPU (the Executor's GPU slot);
+ *   - the *_dev entry points take DEVICE pointers and a hipStream_t (passed as
+ *     void*), enqueue work and return without synchronising.
+ *
+ * Nothing here falls back to the CPU: if no gfx950 device is present the
+ * calls fail with FCS_ERR_DEVICE.
+ */
+#ifndef FCSHIP_H
+#define FCSHIP_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define FCS_OK 0
+#define FCS_ERR_INVALID (-1)     /* bad argument */
+#define FCS_ERR_DEVICE (-2)      /* no device / HIP runtime failure */
+#define FCS_ERR_NOMEM (-3)       /* allocation failure */
+#define FCS_ERR_UNSUPPORTED (-4) /* outside the supported envelope (e.g. m != 5) */
+
+/* ------------------------------------------------------------------ common */
+int fcs_device_count(void);
+const char* fcs_last_error(void);
+const char* fcs_version(void);
+/* Build/ABI self-description: number of symbols this library exports that are
+ * declared in this header (used by the loader test). */
+int fcs_abi_symbol_count(void);
+
+/* ----------------------------------------------------------------- PairHMM */
+/* One read: bases + the four per-base quality arrays GATK hands to the PairHMM
+ * (base quality, insertion GOP, deletion GOP, gap-continuation penalty), all
+ * already preprocessed by the caller exactly as for GKL (quals are used &127). */
+typedef struct {
+  const uint8_t* bases;
+  const uint8_t* base_q;
+  const uint8_t* ins_q;
+  const uint8_t* del_q;
+  const uint8_t* gcp;
+  int32_t len;
+} fcs_phmm_read;
+
+typedef struct {
+  const uint8_t* bases;
+  int32_t len;
+} fcs_phmm_hap;
+
+typedef struct {
+  int32_t device;           /* GPU ordinal */
+  int32_t use_fp64_rescue;  /* 1: recompute pairs whose fp32 result < rescue_threshold in fp64 (GKL) */
+  float rescue_threshold;   /* GKL MIN_ACCEPTED = 1e-28f */
+  int32_t exact_order;      /* 1: no FMA contraction, GKL operation order (bitwise vs the fp32 oracle);
+                               0: FMA-contracted fast path (default) */
+} fcs_phmm_opts;
+
+/* Defaults: device 0, rescue on, 1e-28f, fast path. */
+void fcs_phmm_opts_default(fcs_phmm_opts* o);
+
+/* Replacement for GKL computeLikelihoodsNative: every read against every
+ * haplotype, log10 likelihoods written read-major:
+ * out_log10[r * n_haps + h].  Host pointers, synchronous. */
+int fcs_phmm_compute(const fcs_phmm_read* reads, int32_t n_reads, const fcs_phmm_hap* haps,
+                     int32_t n_haps, double* out_log10, const fcs_phmm_opts* opts);
+
+/* Flat structure-of-arrays pair batch.  Read k occupies
+ * [read_off[k], read_off[k] + read_len[k]) of each of the five read byte
+ * arrays; hap k occupies [hap_off[k], hap_off[k] + hap_len[k]) of hap_bases;
+ * pair p is (pair_read[p], pair_hap[p]).  max_read_len / max_hap_len must bound
+ * every length (they size on-chip buffers). */
+typedef struct {
+  const uint8_t* read_bases;
+  const uint8_t* read_bq;
+  const uint8_t* read_iq;
+  const uint8_t* read_dq;
+  const uint8_t* read_gcp;
+  const int64_t* read_off;
+  const int32_t* read_len;
+  int64_t n_reads;
+  const uint8_t* hap_bases;
+  const int64_t* hap_off;
+  const int32_t* hap_len;
+  int64_t n_haps;
+  const int32_t* pair_read;
+  const int32_t* pair_hap;
+  int64_t n_pairs;
+  int64_t read_bytes; /* total bytes in each read byte array */
+  int64_t hap_bytes;  /* total bytes in hap_bases */
+  int32_t max_read_len;
+  int32_t max_hap_len;
+} fcs_phmm_batch;
+
+/* Host-pointer batch (synchronous): out_log10[p] for every pair. */
+int fcs_phmm_compute_pairs(const fcs_phmm_batch* b, double* out_log10, const fcs_phmm_opts* opts);
+
+/* Device-resident path.  A plan owns the scratch (schedule, sort temp storage,
+ * rescue list) for batches up to max_pairs pairs. */
+typedef struct fcs_phmm_plan fcs_phmm_plan;
+int fcs_phmm_plan_create(int32_t device, int64_t max_pairs, fcs_phmm_plan** plan);
+int fcs_phmm_plan_destroy(fcs_phmm_plan* plan);
+/* Stage 1: order pairs into 4-pair wave groups by (read len, hap len). */
+int fcs_phmm_dev_schedule(fcs_phmm_plan* plan, const fcs_phmm_batch* dev_batch, void* stream);
+/* Stage 2: fp32 forward pass over the schedule; writes out_log10 for pairs
+ * that pass the rescue threshold and queues the others. */
+int fcs_phmm_dev_forward(fcs_phmm_plan* plan, const fcs_phmm_batch* dev_batch, double* dev_out_log10,
+                         const fcs_phmm_opts* opts, void* stream);
+/* Stage 3: fp64 rescue pass over the queued pairs (no-op if none). */
+int fcs_phmm_dev_rescue(fcs_phmm_plan* plan, const fcs_phmm_batch* dev_batch, double* dev_out_log10,
+                        const fcs_phmm_opts* opts, void* stream);
+/* Stages 1-3 back to back. */
+int fcs_phmm_dev_run(fcs_phmm_plan* plan, const fcs_phmm_batch* dev_batch, double* dev_out_log10,
+                     const fcs_phmm_opts* opts, void* stream);
+/* Number of pairs the last forward pass queued for rescue (synchronises the stream). */
+int fcs_phmm_plan_rescue_count(fcs_phmm_plan* plan, void* stream, int64_t* count);
+
+/* -------------------------------------------------------------- banded SW */
+typedef struct {
+  int32_t qlen, tlen, h0, w;
+  const uint8_t* query;  /* bases coded 0..4 (A,C,G,T,N) as in bwa */
+  const uint8_t* target;
+} fcs_bsw_task;
+
+typedef struct {
+  int8_t mat[25]; /* 5x5 scoring matrix, row = target base, col = query base */
+  int32_t o_del, e_del, o_ins, e_ins, end_bonus, zdrop;
+} fcs_bsw_params;
+
+typedef struct {
+  int32_t score, qle, tle, gtle, gscore, max_off;
+} fcs_bsw_result;
+
+/* bwa defaults: a=1, b=4 (N scores -1), o=6, e=1, end_bonus=5, zdrop=100. */
+void fcs_bsw_params_default(fcs_bsw_params* p);
+
+/* Batched ksw_extend2 (host pointers, synchronous). */
+int fcs_bsw_extend(const fcs_bsw_task* tasks, int32_t n, const fcs_bsw_params* params,
+                   fcs_bsw_result* results, int32_t device);
+
+/* Packed structure-of-arrays extension batch (device or host pointers
+ * depending on the entry point).  Task k: query bytes
+ * qbuf[qoff[k] .. +qlen[k]), target bytes tbuf[toff[k] .. +tlen[k]). */
+typedef struct {
+  const uint8_t* qbuf;
+  const int64_t* qoff;
+  const int32_t* qlen;
+  const uint8_t* tbuf;
+  const int64_t* toff;
+  const int32_t* tlen;
+  const int32_t* h0;
+  const int32_t* w;
+  int64_t n;
+  int64_t qbytes;
+  int64_t tbytes;
+  int32_t max_qlen;
+  int32_t max_tlen;
+} fcs_bsw_batch;
+
+/* Device path: res = 6 int32 per task (score, qle, tle, gtle, gscore,
+ * max_off); cells (nullable) = evaluated cells per task (int64). */
+int fcs_bsw_extend_dev(const fcs_bsw_batch* dev_batch, const fcs_bsw_params* params, int32_t* dev_res,
+                       int64_t* dev_cells, int32_t device, void* stream);
+
+/* Host-pointer packed batch (synchronous). */
+int fcs_bsw_extend_batch(const fcs_bsw_batch* host_batch, const fcs_bsw_params* params, int32_t* res,
+                         int64_t* cells, int32_t device);
+
+/* Batched ksw_global2 (host pointers, synchronous).  Task k uses tasks[k].w as
+ * the band and ignores h0.  scores[k] = global score; CIGAR ops of task k are
+ * written to cigar_arena[cigar_off[k] .. cigar_off[k] + cigar_cap[k]) and the
+ * true op count to n_cigar[k] (FCS_ERR_INVALID if any count exceeds its cap;
+ * qlen + tlen always suffices). */
+int fcs_bsw_global(const fcs_bsw_task* tasks, int32_t n, const fcs_bsw_params* params, int32_t* scores,
+                   uint32_t* cigar_arena, const int64_t* cigar_off, const int32_t* cigar_cap,
+                   int32_t* n_cigar, int32_t device);
+
+/* Signature twins of bwa's ksw.c entry points, running on GPU `device` 0 (or
+ * the device set by fcs_set_default_device).  m must be 5.  They return the
+ * score exactly as bwa does; because a global score can be negative, failure
+ * is signalled by FCS_KSW_FAILED (INT32_MIN) plus fcs_last_error().
+ * fcs_ksw_global2 returns the CIGAR in *cigar allocated with malloc(), as bwa
+ * does (caller frees). */
+#define FCS_KSW_FAILED (-2147483647 - 1)
+int fcs_ksw_extend2(int qlen, const uint8_t* query, int tlen, const uint8_t* target, int m,
+                    const int8_t* mat, int o_del, int e_del, int o_ins, int e_ins, int w,
+                    int end_bonus, int zdrop, int h0, int* qle, int* tle, int* gtle, int* gscore,
+                    int* max_off);
+int fcs_ksw_global2(int qlen, const uint8_t* query, int tlen, const uint8_t* target, int m,
+                    const int8_t* mat, int o_del, int e_del, int o_ins, int e_ins, int w,
+                    int* n_cigar, uint32_t** cigar);
+int fcs_set_default_device(int32_t device);
+
+/* ---------------------------------------------- synthetic workload builders */
+/* Seeded generators for the benchmark configurations (BASELINE.json C2/C3).
+ * Deterministic for a given seed.  Callers size the buffers with the *_sizes
+ * functions first. */
+
+/* C2: n_pairs independent pairs, read length R, hap length uniform in
+ * [hmin, hmax]; read = hap substring with 1% substitutions and 0.1% 1-3 bp
+ * indels; base_q uniform [10,40], ins_q = del_q = 45, gcp = 10.  One read and
+ * one hap per pair (pair p = (p, p)).  Reads may come out shorter than R when
+ * the source window runs off the hap; lengths are written to read_len. */
+int fcs_synth_phmm_sizes(uint64_t seed, int64_t n_pairs, int32_t R, int32_t hmin, int32_t hmax,
+                         int64_t* read_bytes, int64_t* hap_bytes);
+int fcs_synth_phmm(uint64_t seed, int64_t n_pairs, int32_t R, int32_t hmin, int32_t hmax,
+                   uint8_t* read_bases, uint8_t* read_bq, uint8_t* read_iq, uint8_t* read_dq,
+                   uint8_t* read_gcp, int64_t* read_off, int32_t* read_len, uint8_t* hap_bases,
+                   int64_t* hap_off, int32_t* hap_len);
+
+/* C3: reads of length read_len sampled from a random reference of ref_len
+ * bases (0.5% substitutions, 0.05% indels), one seed per read; emits the left
+ * (reversed) and right extension tasks a bwa-mem seed produces, with
+ * tlen = min(qlen + w, available reference).  mode 1 instead emits fixed
+ * qlen=fixed_q / tlen=fixed_t tasks (clean GCUPS variant).  Returns the task
+ * count in *n_tasks (≤ 2 * n_reads). */
+int fcs_synth_bsw_sizes(uint64_t seed, int64_t n_reads, int32_t read_len, int64_t ref_len, int32_t w,
+                        int32_t mode, int32_t fixed_q, int32_t fixed_t, int64_t* n_tasks,
+                        int64_t* qbytes, int64_t* tbytes);
+int fcs_synth_bsw(uint64_t seed, int64_t n_reads, int32_t read_len, int64_t ref_len, int32_t w,
+                  int32_t mode, int32_t fixed_q, int32_t fixed_t, uint8_t* qbuf, int64_t* qoff,
+                  int32_t* qlen, uint8_t* tbuf, int64_t* toff, int32_t* tlen, int32_t* h0,
+                  int32_t* wv, int64_t* n_tasks);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* FCSHIP_H */

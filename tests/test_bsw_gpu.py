@@ -1,0 +1,160 @@
+"""GPU parity: banded Smith-Waterman HIP kernels vs the ksw.c oracle.
+
+Bar: bit-exact — every integer of every ksw_extend2 result (score, qle, tle,
+gtle, gscore, max_off), the evaluated cell count, and every ksw_global2 score
+and CIGAR must equal the oracle's.
+"""
+import numpy as np
+import pytest
+
+import fcship
+import oracle_lib
+
+pytestmark = pytest.mark.gpu
+
+
+def related_pair(rng, qlen, tlen, sub=0.03, indel=0.01, n_frac=0.0):
+    t = rng.integers(0, 4, tlen).astype(np.uint8)
+    q = []
+    i = 0
+    while len(q) < qlen:
+        u = rng.random()
+        if u < indel / 2:
+            q.append(int(rng.integers(0, 4)))
+            continue
+        if u < indel:
+            i += 1
+            continue
+        b = int(t[i % tlen]) if tlen else int(rng.integers(0, 4))
+        if rng.random() < sub:
+            b = (b + 1 + int(rng.integers(0, 3))) & 3
+        q.append(b)
+        i += 1
+    q = np.array(q[:qlen], np.uint8)
+    if n_frac:
+        q[rng.random(qlen) < n_frac] = 4
+        t[rng.random(tlen) < n_frac] = 4
+    return q, t
+
+
+def random_tasks(seed, n, qmax=260, wmax=120):
+    rng = np.random.default_rng(seed)
+    items = []
+    for k in range(n):
+        qlen = int(rng.integers(0, qmax + 1)) if k % 7 else int(rng.integers(1, 40))
+        tlen = max(0, qlen + int(rng.integers(-20, 120)))
+        kind = k % 4
+        if kind == 0:
+            q, t = related_pair(rng, qlen, tlen)
+        elif kind == 1:  # unrelated: band trimming / early termination
+            q = rng.integers(0, 4, qlen).astype(np.uint8)
+            t = rng.integers(0, 4, tlen).astype(np.uint8)
+        elif kind == 2:  # related prefix, then junk: z-drop
+            q, t = related_pair(rng, qlen, tlen, sub=0.01)
+            cut = int(rng.integers(0, max(1, min(qlen, tlen))))
+            t[cut:] = rng.integers(0, 4, tlen - cut)
+        else:
+            q, t = related_pair(rng, qlen, tlen, sub=0.05, indel=0.03, n_frac=0.02)
+        h0 = int(rng.integers(1, 80))
+        w = int(rng.integers(0, wmax + 1)) if k % 3 else 100
+        items.append((q, t, h0, w))
+    return fcship.make_tasks(items)
+
+
+def assert_extend_equal(tasks, params_kw=None, mat=None):
+    params_kw = params_kw or {}
+    m = fcship.default_mat() if mat is None else np.asarray(mat, np.int8)
+    res, cells = fcship.bsw_extend_batch(tasks, fcship.bsw_params(mat=m, **params_kw))
+    ref, rcells = oracle_lib.ksw_extend2_batch(tasks, m, **params_kw)
+    bad = np.flatnonzero((res != ref).any(axis=1) | (cells != rcells))
+    if bad.size:
+        k = int(bad[0])
+        raise AssertionError(f"{bad.size}/{tasks.n} tasks differ; task {k} qlen={tasks.qlen[k]} tlen={tasks.tlen[k]} "
+                             f"h0={tasks.h0[k]} w={tasks.w[k]}: gpu={res[k]}/{cells[k]} ref={ref[k]}/{rcells[k]}")
+
+
+def test_extend_random(gpu):
+    assert_extend_equal(random_tasks(1, 600))
+
+
+def test_extend_zdrop_and_penalties(gpu):
+    t = random_tasks(2, 300, qmax=180)
+    assert_extend_equal(t, dict(o_del=5, e_del=2, o_ins=4, e_ins=3, end_bonus=0, zdrop=20))
+    assert_extend_equal(t, dict(zdrop=0))
+
+
+def test_extend_random_matrix(gpu):
+    rng = np.random.default_rng(5)
+    mat = rng.integers(-5, 4, 25).astype(np.int8)
+    mat[[0, 6, 12, 18]] = rng.integers(1, 4, 4)
+    assert_extend_equal(random_tasks(3, 200, qmax=150), mat=mat)
+
+
+def test_extend_long_queries(gpu):
+    # qlen > 255 selects the wide (up to 16 slots per lane) kernel
+    assert_extend_equal(random_tasks(4, 40, qmax=900, wmax=400))
+
+
+def test_extend_c3_synthetic(gpu):
+    assert_extend_equal(fcship.synth_bsw(20261015, 2000, ref_len=2_000_000))
+    assert_extend_equal(fcship.synth_bsw(20261015, 300, ref_len=2_000_000, mode=1))
+
+
+def test_ksw_extend2_twin(gpu):
+    rng = np.random.default_rng(9)
+    q, t = related_pair(rng, 120, 200)
+    got = fcship.ksw_extend2(q, t, 25, 100)
+    ref, _ = oracle_lib.ksw_extend2(q, t, 25, 100, fcship.default_mat())
+    assert got == ref
+
+
+def global_tasks(seed, n):
+    rng = np.random.default_rng(seed)
+    items = []
+    for k in range(n):
+        qlen = int(rng.integers(0, 200))
+        tlen = max(0, qlen + int(rng.integers(-8, 9)))
+        q, t = related_pair(rng, qlen, tlen, sub=0.03, indel=0.02, n_frac=0.01 if k % 5 == 0 else 0.0)
+        w = int(rng.integers(0, 25)) if k % 4 else int(rng.integers(50, 300))
+        items.append((q, t, 1, w))
+    return fcship.make_tasks(items)
+
+
+def test_global_scores_and_cigars(gpu):
+    t = global_tasks(6, 400)
+    scores, cigars = fcship.bsw_global(t)
+    m = fcship.default_mat()
+    for k in range(t.n):
+        q, tg, _, w = t.task(k)
+        rs, rc = oracle_lib.ksw_global2(q, tg, w, m)
+        assert scores[k] == rs, f"task {k}: score {scores[k]} != {rs}"
+        assert np.array_equal(cigars[k], rc), f"task {k}: {fcship.cigar_str(cigars[k])} != {fcship.cigar_str(rc)}"
+
+
+def test_global_score_only_and_twin(gpu):
+    t = global_tasks(8, 50)
+    scores, _ = fcship.bsw_global(t, with_cigar=False)
+    m = fcship.default_mat()
+    for k in range(t.n):
+        q, tg, _, w = t.task(k)
+        assert scores[k] == oracle_lib.ksw_global2(q, tg, w, m)[0]
+    q, tg, _, w = t.task(3)
+    sc, ops = fcship.ksw_global2(q, tg, w)
+    rs, rc = oracle_lib.ksw_global2(q, tg, w, m)
+    assert sc == rs and np.array_equal(ops, rc)
+
+
+def test_golden_fixtures_gpu(gpu):
+    import json
+    import os
+    with open(os.path.join(os.path.dirname(__file__), "golden", "ksw_golden.json")) as f:
+        g = json.load(f)
+    mat = np.array(g["mat"], np.int8)
+    t = fcship.make_tasks([(c["q"], c["t"], c["h0"], c["w"]) for c in g["extend"]])
+    res, cells = fcship.bsw_extend_batch(t, fcship.bsw_params(mat=mat))
+    assert res.tolist() == [c["out"] for c in g["extend"]]
+    assert cells.tolist() == [c["cells"] for c in g["extend"]]
+    t = fcship.make_tasks([(c["q"], c["t"], 1, c["w"]) for c in g["global"]])
+    scores, cigars = fcship.bsw_global(t, fcship.bsw_params(mat=mat))
+    assert scores.tolist() == [c["score"] for c in g["global"]]
+    assert [list(map(int, x)) for x in cigars] == [c["cigar"] for c in g["global"]]

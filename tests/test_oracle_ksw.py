@@ -1,0 +1,192 @@
+"""Pins the ksw_extend2 / ksw_global2 oracle (CPU, no GPU needed).
+
+The reference holds no SW golden vectors (parity unpinned), so
+the C restatement is checked against hand-traced known answers, a second,
+independently written Python restatement of ksw_extend2 (list-based, from
+SURVEY.md Appendix A.2), an unbanded Gotoh DP for ksw_global2 scores, CIGAR
+self-consistency, and the committed golden fixtures.
+"""
+import json
+import os
+
+import numpy as np
+
+import oracle_lib
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+
+
+def default_mat():
+    m = np.full((5, 5), -1, np.int8)
+    for i in range(4):
+        for j in range(4):
+            m[i, j] = 1 if i == j else -4
+    return m.ravel()
+
+
+MAT = default_mat()
+
+
+def py_extend(q, t, h0, w, mat=MAT, o_del=6, e_del=1, o_ins=6, e_ins=1, end_bonus=5, zdrop=100):
+    """Independent list-based restatement of bwa ksw_extend2."""
+    qlen, tlen = len(q), len(t)
+    H = [0] * (qlen + 1)
+    E = [0] * (qlen + 1)
+    H[0] = h0
+    if qlen >= 1:
+        H[1] = max(h0 - o_ins - e_ins, 0)
+    j = 2
+    while j <= qlen and H[j - 1] > e_ins:
+        H[j] = H[j - 1] - e_ins
+        j += 1
+    mx = int(max(mat.max(), 0))
+    w = min(w, max(int((qlen * mx + end_bonus - o_ins) / e_ins + 1.0), 1),
+            max(int((qlen * mx + end_bonus - o_del) / e_del + 1.0), 1))
+    best, bi, bj, bie, gs, moff = h0, -1, -1, -1, -1, 0
+    beg, end, cells = 0, qlen, 0
+    for i in range(tlen):
+        beg = max(beg, i - w)
+        end = min(end, i + w + 1, qlen)
+        h1 = max(h0 - (o_del + e_del * (i + 1)), 0) if beg == 0 else 0
+        f, m, mj = 0, 0, -1
+        jj = beg
+        for jj in range(beg, end):
+            M = H[jj] + int(mat[t[i] * 5 + q[jj]]) if H[jj] else 0
+            e = E[jj]
+            H[jj] = h1
+            h = max(M, e, f)
+            h1 = h
+            if h >= m:
+                m, mj = h, jj
+            E[jj] = max(e - e_del, max(M - o_del - e_del, 0))
+            f = max(f - e_ins, max(M - o_ins - e_ins, 0))
+        j_after = end if end > beg else beg
+        cells += max(end - beg, 0)
+        H[end], E[end] = h1, 0
+        if j_after == qlen:
+            if not gs > h1:
+                bie, gs = i, h1
+        if m == 0:
+            break
+        if m > best:
+            best, bi, bj = m, i, mj
+            moff = max(moff, abs(mj - i))
+        elif zdrop > 0:
+            if i - bi > mj - bj:
+                if best - m - ((i - bi) - (mj - bj)) * e_del > zdrop:
+                    break
+            elif best - m - ((mj - bj) - (i - bi)) * e_ins > zdrop:
+                break
+        nb = beg
+        while nb < end and H[nb] == 0 and E[nb] == 0:
+            nb += 1
+        beg = nb
+        ne = end
+        while ne >= beg and H[ne] == 0 and E[ne] == 0:
+            ne -= 1
+        end = min(ne + 2, qlen)
+    return (best, bj + 1, bi + 1, bie + 1, gs, moff), cells
+
+
+def test_known_answers():
+    q = [0, 1, 2, 3, 0, 1, 2, 3, 0, 1]
+    assert oracle_lib.ksw_extend2(q, q, 5, 100, MAT)[0] == (15, 10, 10, 10, 15, 0)
+    assert oracle_lib.ksw_extend2(q, [], 5, 100, MAT)[0] == (5, 0, 0, 0, -1, 0)
+    # all-mismatch, hand traced row by row: the extension never beats h0
+    assert oracle_lib.ksw_extend2([0, 0, 0, 0], [1, 1, 1, 1], 10, 100, MAT)[0] == (10, 0, 0, 3, 0, 0)
+    # global: identity and a single deletion
+    sc, cig = oracle_lib.ksw_global2([0, 1, 2, 3], [0, 1, 2, 3], 10, MAT)
+    assert sc == 4 and list(cig) == [4 << 4 | 0]
+    # hand traced: at cell (3,2) M and E tie at -4 and ksw prefers M (m >= e),
+    # so the deleted target base is the FIRST '2': 2M1D4M, score 6 - (6+1)
+    sc, cig = oracle_lib.ksw_global2([0, 1, 2, 3, 0, 1], [0, 1, 2, 2, 3, 0, 1], 10, MAT)
+    assert sc == 6 - 7 and [(int(c) >> 4, int(c) & 15) for c in cig] == [(2, 0), (1, 2), (4, 0)]
+
+
+def rand_pair(rng, qlen, tlen, related):
+    t = rng.integers(0, 4, tlen)
+    if related:
+        q = t[:qlen].copy() if qlen <= tlen else np.concatenate([t, rng.integers(0, 4, qlen - tlen)])
+        m = rng.random(qlen) < 0.05
+        q[m] = rng.integers(0, 5, m.sum())
+    else:
+        q = rng.integers(0, 5, qlen)
+    return q.astype(np.uint8), t.astype(np.uint8)
+
+
+def test_extend_matches_independent_restatement():
+    rng = np.random.default_rng(11)
+    for k in range(250):
+        qlen, tlen = int(rng.integers(0, 70)), int(rng.integers(0, 110))
+        q, t = rand_pair(rng, qlen, tlen, k % 3 != 0)
+        h0, w = int(rng.integers(1, 60)), int(rng.integers(0, 40))
+        kw = dict(zdrop=int(rng.integers(0, 30)), end_bonus=int(rng.integers(0, 6)))
+        ref, cells = oracle_lib.ksw_extend2(q, t, h0, w, MAT, **kw)
+        got, gcells = py_extend(list(q), list(t), h0, w, **kw)
+        assert ref == got and cells == gcells, (k, ref, got)
+
+
+def gotoh_global(q, t, mat=MAT, o_del=6, e_del=1, o_ins=6, e_ins=1):
+    """Unbanded global DP with ksw's M-based gap opening (no band)."""
+    NEG = -10 ** 9
+    qlen, tlen = len(q), len(t)
+    H = [[NEG] * (qlen + 1) for _ in range(tlen + 1)]
+    E = [[NEG] * (qlen + 1) for _ in range(tlen + 1)]
+    F = [[NEG] * (qlen + 1) for _ in range(tlen + 1)]
+    Mx = [[NEG] * (qlen + 1) for _ in range(tlen + 1)]
+    H[0][0] = 0
+    for j in range(1, qlen + 1):
+        H[0][j] = -(o_ins + e_ins * j)
+    for i in range(1, tlen + 1):
+        H[i][0] = -(o_del + e_del * i)
+    for i in range(1, tlen + 1):
+        for j in range(1, qlen + 1):
+            Mx[i][j] = H[i - 1][j - 1] + int(mat[t[i - 1] * 5 + q[j - 1]])
+            E[i][j] = max(Mx[i - 1][j] - o_del - e_del if i > 1 else NEG, E[i - 1][j] - e_del,
+                          H[i - 1][j] - o_del - e_del if j == 0 or i == 1 else NEG)
+            F[i][j] = max(Mx[i][j - 1] - o_ins - e_ins if j > 1 else NEG, F[i][j - 1] - e_ins,
+                          H[i][j - 1] - o_ins - e_ins if j == 1 else NEG)
+            H[i][j] = max(Mx[i][j], E[i][j], F[i][j])
+    return H[tlen][qlen]
+
+
+def cigar_score(cig, q, t, mat=MAT, o_del=6, e_del=1, o_ins=6, e_ins=1):
+    s, i, j = 0, 0, 0
+    for c in cig:
+        n, op = int(c) >> 4, int(c) & 15
+        if op == 0:
+            for _ in range(n):
+                s += int(mat[t[i] * 5 + q[j]])
+                i += 1
+                j += 1
+        elif op == 1:
+            s -= o_ins + e_ins * n
+            j += n
+        else:
+            s -= o_del + e_del * n
+            i += n
+    assert i == len(t) and j == len(q)
+    return s
+
+
+def test_global_score_vs_unbanded_dp_and_cigar_consistency():
+    rng = np.random.default_rng(12)
+    for k in range(120):
+        qlen = int(rng.integers(1, 30))
+        tlen = max(1, qlen + int(rng.integers(-4, 5)))
+        q, t = rand_pair(rng, qlen, tlen, True)
+        sc, cig = oracle_lib.ksw_global2(q, t, 64, MAT)
+        assert sc == gotoh_global(list(q), list(t)), k
+        assert cigar_score(cig, list(q), list(t)) == sc, k
+
+
+def test_golden_fixtures():
+    with open(os.path.join(HERE, "golden", "ksw_golden.json")) as f:
+        g = json.load(f)
+    mat = np.array(g["mat"], np.int8)
+    for c in g["extend"]:
+        ref, cells = oracle_lib.ksw_extend2(c["q"], c["t"], c["h0"], c["w"], mat)
+        assert list(ref) == c["out"] and cells == c["cells"]
+    for c in g["global"]:
+        sc, cig = oracle_lib.ksw_global2(c["q"], c["t"], c["w"], mat)
+        assert sc == c["score"] and list(map(int, cig)) == c["cigar"]

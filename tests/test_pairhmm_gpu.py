@@ -1,0 +1,185 @@
+"""GPU parity: PairHMM HIP kernels vs the CPU oracle (GKL semantics).
+
+Bar (north_star): log10 likelihoods within 1e-5 relative of the GKL-semantics
+oracle for the default FMA path; the exact_order path keeps GKL's operation
+order and must agree to within 2 float ulps of the final log10 (the only
+difference left is device vs host log10f).
+"""
+import numpy as np
+import pytest
+
+import fcship
+import oracle_lib
+
+pytestmark = pytest.mark.gpu
+
+RTOL = 1e-5
+
+
+def ulp32(x):
+    x = np.abs(np.asarray(x, np.float64)).astype(np.float32)
+    return (np.nextafter(x, np.float32(np.inf)) - x).astype(np.float64)
+
+
+def rand_read(rng, R, alphabet=b"ACGT", n_frac=0.0):
+    b = rng.choice(np.frombuffer(alphabet, np.uint8), R)
+    if n_frac:
+        b[rng.random(R) < n_frac] = ord("N")
+    bq = rng.integers(0, 60, R).astype(np.uint8)
+    iq = rng.integers(10, 60, R).astype(np.uint8)
+    dq = rng.integers(10, 60, R).astype(np.uint8)
+    gq = rng.integers(5, 40, R).astype(np.uint8)
+    return (b, bq, iq, dq, gq)
+
+
+def mutate(rng, hap, R, sub=0.02):
+    start = int(rng.integers(0, max(1, len(hap) - R + 1)))
+    r = np.array(hap[start:start + R], np.uint8)
+    if r.size < R:
+        r = np.concatenate([r, rng.choice(np.frombuffer(b"ACGT", np.uint8), R - r.size)])
+    m = rng.random(R) < sub
+    r[m] = rng.choice(np.frombuffer(b"ACGT", np.uint8), int(m.sum()))
+    return r
+
+
+def random_batch(seed, n_reads, n_haps, rlo, rhi, hlo, hhi, n_frac=0.01, related=True):
+    rng = np.random.default_rng(seed)
+    haps = []
+    for _ in range(n_haps):
+        h = rng.choice(np.frombuffer(b"ACGT", np.uint8), int(rng.integers(hlo, hhi + 1)))
+        h[rng.random(h.size) < n_frac] = ord("N")
+        haps.append(h)
+    reads = []
+    for i in range(n_reads):
+        R = int(rng.integers(rlo, rhi + 1))
+        rd = list(rand_read(rng, R, n_frac=n_frac))
+        if related:
+            rd[0] = mutate(rng, haps[i % n_haps], R)
+        reads.append(tuple(rd))
+    return reads, haps
+
+
+def check_parity(p, gpu_out, exact):
+    ref, used_d = oracle_lib.phmm_batch(p)
+    assert np.all(np.isfinite(gpu_out) == np.isfinite(ref)), "finite mask differs"
+    fin = np.isfinite(ref)
+    g, r = gpu_out[fin], ref[fin]
+    if exact:
+        # float-pass pairs: bitwise forward sums, so only log10f rounding may differ
+        tol = np.where(used_d[fin], 1e-12 * np.abs(r) + 1e-12, 2 * ulp32(r) + 2 * ulp32(36.123599))
+        bad = np.abs(g - r) > tol
+    else:
+        bad = np.abs(g - r) > RTOL * np.abs(r)
+    if bad.any():
+        i = np.flatnonzero(bad)[:5]
+        raise AssertionError(f"{bad.sum()} / {bad.size} mismatches; gpu={g[i]} ref={r[i]} rescued={used_d[fin][i]}")
+    assert np.all(gpu_out[~fin] == ref[~fin])
+    return used_d
+
+
+@pytest.mark.parametrize("exact", [True, False])
+def test_small_handmade(gpu, exact):
+    reads = [(b"ACGT", b"\x1e\x1e\x1e\x1e", b"\x2d" * 4, b"\x2d" * 4, b"\x0a" * 4),
+             (b"ACGTACGTTT", bytes([20] * 10), bytes([45] * 10), bytes([45] * 10), bytes([10] * 10)),
+             (b"NNAC", bytes([30, 10, 0, 40]), bytes([45] * 4), bytes([45] * 4), bytes([10] * 4))]
+    haps = [b"ACGT", b"TTACGTACGTTTAA", b"A", b"NCGTNACG"]
+    p = fcship.make_pairs(reads, haps)
+    out = fcship.phmm_compute_pairs(p, exact=exact)
+    check_parity(p, out, exact)
+
+
+@pytest.mark.parametrize("exact", [True, False])
+def test_random_lengths(gpu, exact):
+    # ragged R and H: short reads (< one 16-row stripe), R not a multiple of 16,
+    # haps shorter than a stripe, long haps; N bases on both sides; quals past 127
+    reads, haps = random_batch(7 + exact, 60, 7, 1, 200, 1, 420)
+    p = fcship.make_pairs(reads, haps)
+    p.read_bq[::17] = 200  # masked & 127 like GKL
+    out = fcship.phmm_compute_pairs(p, exact=exact)
+    check_parity(p, out, exact)
+
+
+def test_dense_read_major(gpu):
+    reads, haps = random_batch(11, 9, 5, 30, 120, 50, 200)
+    dense = fcship.phmm_compute(reads, haps)
+    p = fcship.make_pairs(reads, haps)
+    ref, _ = oracle_lib.phmm_batch(p)
+    np.testing.assert_allclose(dense.ravel(), ref, rtol=RTOL)
+    assert dense.shape == (9, 5)
+
+
+@pytest.mark.parametrize("exact", [True, False])
+def test_rescue_path(gpu, exact):
+    # unrelated, high-quality reads underflow the fp32 pass -> fp64 rescue
+    reads, haps = random_batch(3, 40, 4, 90, 150, 150, 300, n_frac=0.0, related=False)
+    reads = [(r[0], np.full(r[0].size, 40, np.uint8), np.full(r[0].size, 60, np.uint8),
+              np.full(r[0].size, 60, np.uint8), r[4]) for r in reads]
+    p = fcship.make_pairs(reads, haps)
+    out = fcship.phmm_compute_pairs(p, exact=exact)
+    used = check_parity(p, out, exact)
+    assert used.sum() > 0, "test must exercise the fp64 rescue"
+
+
+def test_no_rescue_option(gpu):
+    reads, haps = random_batch(5, 8, 2, 100, 101, 200, 200, related=False)
+    p = fcship.make_pairs(reads, haps)
+    out = fcship.phmm_compute_pairs(p, rescue=False)
+    raw = np.array([oracle_lib.phmm_prob_f(reads[i // 2], haps[i % 2]) for i in range(p.n_pairs)], np.float32)
+    with np.errstate(divide="ignore"):
+        exp = (np.log10(raw.astype(np.float32)) - np.float32(np.log10(np.float32(2.0 ** 120)))).astype(np.float64)
+    fin = np.isfinite(exp)
+    np.testing.assert_allclose(out[fin], exp[fin], rtol=RTOL)
+
+
+def test_degenerate(gpu):
+    reads = [(b"", b"", b"", b"", b""), (b"ACG", b"\x14" * 3, b"\x2d" * 3, b"\x2d" * 3, b"\x0a" * 3)]
+    haps = [b"", b"ACGT"]
+    p = fcship.make_pairs(reads, haps)
+    out = fcship.phmm_compute_pairs(p)
+    assert np.isneginf(out[0]) and np.isneginf(out[1]) and np.isneginf(out[2])
+    assert np.isfinite(out[3])
+
+
+def test_synthetic_c2_sample(gpu):
+    p = fcship.synth_phmm(20261015, 3000)
+    out = fcship.phmm_compute_pairs(p)
+    check_parity(p, out, exact=False)
+
+
+def test_device_path_matches_host_path(gpu):
+    torch = pytest.importorskip("torch")
+    p = fcship.synth_phmm(99, 777, R=64, hmin=20, hmax=90)
+    host = fcship.phmm_compute_pairs(p)
+    dev = {k: torch.from_numpy(getattr(p, k)).cuda() for k in
+           ("read_bases", "read_bq", "read_iq", "read_dq", "read_gcp", "read_off", "read_len", "hap_bases",
+            "hap_off", "hap_len", "pair_read", "pair_hap")}
+    b = p.to_struct()
+    for k, t in dev.items():
+        setattr(b, k, t.data_ptr())
+    out = torch.empty(p.n_pairs, dtype=torch.float64, device="cuda")
+    plan = fcship.C.c_void_p()
+    fcship.check(fcship.lib.fcs_phmm_plan_create(0, p.n_pairs, fcship.C.byref(plan)))
+    try:
+        o = fcship.phmm_opts()
+        s = torch.cuda.current_stream().cuda_stream
+        fcship.check(fcship.lib.fcs_phmm_dev_run(plan, fcship.C.byref(b), out.data_ptr(), fcship.C.byref(o), s))
+        torch.cuda.synchronize()
+    finally:
+        fcship.lib.fcs_phmm_plan_destroy(plan)
+    np.testing.assert_array_equal(out.cpu().numpy(), host)
+
+
+def test_golden_fixtures_gpu(gpu):
+    import json
+    import os
+    with open(os.path.join(os.path.dirname(__file__), "golden", "phmm_golden.json")) as f:
+        g = json.load(f)
+    reads = [tuple(bytes(c[k]) for k in ("bases", "bq", "iq", "dq", "gcp")) for c in g["cases"]]
+    haps = [bytes(c["hap"]) for c in g["cases"]]
+    p = fcship.make_pairs(reads, haps, pairs=[(i, i) for i in range(len(reads))])
+    exp = np.array([c["log10"] for c in g["cases"]])
+    for exact in (True, False):
+        out = fcship.phmm_compute_pairs(p, exact=exact)
+        fin = np.isfinite(exp)
+        assert np.array_equal(np.isfinite(out), fin)
+        np.testing.assert_allclose(out[fin], exp[fin], rtol=1e-6 if exact else RTOL)

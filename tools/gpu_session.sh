@@ -1,0 +1,37 @@
+#!/bin/bash
+# One bounded GPU session on the gpurun box: parity tests, smoke, bench, and
+# rocprofv3 kernel-trace / PMC passes.  Every GPU step has its own time limit
+# and the script stops at the first failing step (no retries).
+# usage: tools/gpu_session.sh TAG [tests] [smoke] [bench] [prof] [pmc]
+set -u
+TAG=$1; shift
+ROOT=${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}
+OUT=$ROOT/gpurun_out/$TAG
+mkdir -p "$OUT"
+cd "$ROOT"
+export TMPDIR=/tmp
+run() {  # name seconds cmd...
+  local name=$1 secs=$2; shift 2
+  echo "== $name ($(date +%T))" | tee -a "$OUT/session.log"
+  timeout -k 10 "$secs" "$@" > "$OUT/$name.log" 2>&1
+  local rc=$?
+  echo "== $name rc=$rc" | tee -a "$OUT/session.log"
+  tail -3 "$OUT/$name.log" | tee -a "$OUT/session.log"
+  if [ $rc -ne 0 ]; then echo "STOP after $name" | tee -a "$OUT/session.log"; exit $rc; fi
+}
+for step in "$@"; do
+  case $step in
+    tests) run pytest_gpu 900 python -m pytest tests -m gpu -q -p no:cacheprovider ;;
+    smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
+    bench) run bench 900 python bench.py ;;
+    benchq) run benchq 600 python bench.py --steps 3 --warmup 1 --no-cpu-baseline ;;
+    prof) run prof 900 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o run --output-format csv -- \
+            python3 "$ROOT/bench.py" --steps 3 --warmup 1 --no-cpu-baseline ;;
+    pmc) run pmc 900 rocprofv3 --pmc FETCH_SIZE -d "$OUT/pmc_fetch" -o run --output-format csv -- \
+            python3 "$ROOT/bench.py" --steps 1 --warmup 0 --no-cpu-baseline --no-bsw &&
+         run pmc2 900 rocprofv3 --pmc WRITE_SIZE -d "$OUT/pmc_write" -o run --output-format csv -- \
+            python3 "$ROOT/bench.py" --steps 1 --warmup 0 --no-cpu-baseline --no-bsw ;;
+    *) echo "unknown step $step"; exit 2 ;;
+  esac
+done
+echo "== session done" | tee -a "$OUT/session.log"
