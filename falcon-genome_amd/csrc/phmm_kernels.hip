@@ -9,125 +9,198 @@
 //     16-lane DPP row ("segment");
 //   * inside a segment, lane l owns read row 16*s + l of stripe s and the
 //     segment sweeps anti-diagonals: at step t lane l computes column t - l;
-//   * the up-neighbour values (row r-1) arrive by DPP row_shr:1 from lane l-1;
-//     lane 0 of the segment gets them from the segment's LDS boundary ring,
-//     which lane 15 filled with the previous stripe's last row (and which holds
-//     row 0 = {M=0, I=0, D=INITIAL_CONSTANT/H} plus the hap bases for stripe 0);
-//     the DPP `old` operand delivers the LDS value to lane 0 for free;
-//   * the diagonal values (r-1, c-1) are the previous step's up values and the
-//     left values (r, c-1) are the lane's own previous outputs, so a cell costs
-//     four DPP moves, one select for the emission prior and 8 FP ops;
-//   * idle cells (c <= 0) compute exact zeros by construction, so no per-step
-//     predicates are needed; the lane holding the last read row sums M and I
-//     in column order like GKL's vector kernel.
-// The file is compiled with -ffp-contract=off: the EXACT variant evaluates GKL's
-// operation order bit-for-bit, the fast variant uses explicit fma().
+//   * up-neighbour values (row r-1, same column) arrive by DPP row_shr:1 from
+//     lane l-1; lane 0 gets them through the DPP `old` operand from the
+//     segment's LDS boundary ring, which lane 15 filled with the previous
+//     stripe's last row (M, I: 8 bytes per column).  D of that row is not
+//     stored: lane 0 re-derives it from the M stream with the same operation
+//     lane 15 used, so it is bit-identical;
+//   * diagonal values (r-1, c-1) are the previous step's up values and left
+//     values (r, c-1) the lane's own previous outputs;
+//   * the hap base of column t reaches lane 0 by DPP row_newbcast from a
+//     register that holds 16 consecutive hap bytes (one LDS read per 16 steps),
+//     and moves down the segment with the M/I/D values;
+//   * idle cells (c <= 0) compute exact zeros by construction, so the step has
+//     no predicates; the lane holding the read's last row sums M and I in
+//     column order like GKL's vector kernel.
+// Steps are unrolled in blocks of 16 (the DPP broadcast lane is an immediate),
+// the ring is read four steps ahead and the next stripe's row parameters are
+// gathered while the current stripe runs.
+// Compiled with -ffp-contract=off: the EXACT variant keeps GKL's operation
+// order bit-for-bit, the fast variant uses explicit fma().
 #include <hip/hip_runtime.h>
+
+#include <utility>
 
 #include "fcship_internal.h"
 
 namespace fcs {
 
-template <typename T> struct alignas(16) PhSlot;
-template <> struct alignas(16) PhSlot<float> {
-  float M, I, D;
-  int hb;
-};
-template <> struct alignas(16) PhSlot<double> {
-  double M, I, D;
-  int hb;
-  int pad;
+template <typename T> struct alignas(2 * sizeof(T)) PhRing {
+  T M, I;
 };
 
 __device__ __forceinline__ float fma_t(float a, float b, float c) { return fmaf(a, b, c); }
 __device__ __forceinline__ double fma_t(double a, double b, double c) { return fma(a, b, c); }
 
-// One stripe of one segment: steps 0..tend.  buf points at the segment's
-// boundary ring, slot index = column + 16.
-template <typename T, bool EXACT, bool SUM>
-__device__ __forceinline__ void phmm_stripe(PhSlot<T>* __restrict__ buf, const int sl, const int tend, const T e1,
-                                            const T e3, const T mm, const T gm, const T mx, const T xx, const T my,
-                                            const T yy, const int rbase, const int lim, T& accM, T& accI) {
-  T Mo = 0, Io = 0, Do = 0, Mp = 0, Ip = 0, Dp = 0;
-  int ho = 0;
-  PhSlot<T> nx = buf[16];
-#pragma unroll 2
-  for (int t = 0; t <= tend; ++t) {
-    const PhSlot<T> cur = nx;
-    nx = buf[t + 17];
-    const T Mu = dpp_row_shr1<T>(cur.M, Mo);
-    const T Iu = dpp_row_shr1<T>(cur.I, Io);
-    const T Du = dpp_row_shr1<T>(cur.D, Do);
-    const int hu = dpp_row_shr1_i(cur.hb, ho);
-    const T prior = (hu == rbase || hu == 'N') ? e1 : e3;
-    T Mn, In, Dn;
-    if constexpr (EXACT) {
-      Mn = ((Mp * mm + Ip * gm) + Dp * gm) * prior;
-      In = Mu * mx + Iu * xx;
-      Dn = Mo * my + Do * yy;
-    } else {
-      Mn = prior * fma_t(Mp, mm, fma_t(Ip, gm, Dp * gm));
-      In = fma_t(Mu, mx, Iu * xx);
-      Dn = fma_t(Mo, my, Do * yy);
-    }
-    if (sl == 15) {
-      PhSlot<T> o;
-      o.M = Mn;
-      o.I = In;
-      o.D = Dn;
-      o.hb = hu;
-      buf[t + 1] = o;
-    }
-    if constexpr (SUM) {
-      if (t <= lim) {
-        accM += Mn;
-        accI += In;
-      }
-    }
-    Mp = Mu;
-    Ip = Iu;
-    Dp = Du;
-    Mo = Mn;
-    Io = In;
-    Do = Dn;
-    ho = hu;
-  }
+// Lane S of each 16-lane row broadcast to its row (gfx90a+ DPP row_newbcast).
+template <int S> __device__ __forceinline__ int row_bcast_i(int v) {
+  return __builtin_amdgcn_update_dpp(0, v, 0x150 + S, 0xF, 0xF, false);
+}
+template <int S> __device__ __forceinline__ float row_bcast(float v) { return __int_as_float(row_bcast_i<S>(__float_as_int(v))); }
+template <int S> __device__ __forceinline__ double row_bcast(double v) {
+  const long long x = __double_as_longlong(v);
+  const int lo = row_bcast_i<S>((int)x), hi = row_bcast_i<S>((int)(x >> 32));
+  return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
 }
 
 template <typename T>
-__device__ __forceinline__ void load_row(const PhmmDevBatch& b, const PhmmTables<T>& tab, bool valid, int64_t pos,
-                                         T& e1, T& e3, T& mm, T& gm, T& mx, T& xx, T& my, T& yy, int& rbase) {
-  e1 = e3 = mm = gm = mx = xx = my = yy = (T)0;
-  rbase = -1;
+struct RowP {
+  T e1, e3, mm, gm, mx, xx, my, yy;
+  int rbase;
+};
+
+template <typename T>
+struct LaneState {
+  T Mo, Io, Do;  // own outputs of the previous step: cell (r, c-1)
+  T Mp, Ip, Dp;  // up values of the previous step:   cell (r-1, c-1)
+  T Mq, Dq;      // boundary-row stream seen by lane 0: M, D of (r-1, c-1)
+  int ho;        // hap base of the previous step's column
+};
+
+// One anti-diagonal step at t = t0 + S.
+template <typename T, bool EXACT, bool SUM, int S>
+__device__ __forceinline__ void phmm_step(LaneState<T>& L, PhRing<T> (&pf)[4], const int Q, const RowP<T>& p,
+                                          const T myp, const T yyp, PhRing<T>* __restrict__ ring, const int t0,
+                                          const bool top, const int lim, T& accM, T& accI) {
+  const int t = t0 + S;
+  const PhRing<T> cur = pf[S & 3];
+  pf[S & 3] = ring[t + 20];  // column t + 4, four steps ahead
+  T dq;
+  if constexpr (EXACT) dq = L.Mq * myp + L.Dq * yyp;
+  else dq = fma_t(L.Mq, myp, L.Dq * yyp);
+  L.Mq = cur.M;
+  L.Dq = dq;
+  const int hb0 = row_bcast_i<S>(Q);
+  const T Mu = dpp_row_shr1<T>(cur.M, L.Mo);
+  const T Iu = dpp_row_shr1<T>(cur.I, L.Io);
+  const T Du = dpp_row_shr1<T>(dq, L.Do);
+  const int hu = dpp_row_shr1_i(hb0, L.ho);
+  const T prior = (hu == p.rbase || hu == 'N') ? p.e1 : p.e3;
+  T Mn, In, Dn;
+  if constexpr (EXACT) {
+    Mn = ((L.Mp * p.mm + L.Ip * p.gm) + L.Dp * p.gm) * prior;
+    In = Mu * p.mx + Iu * p.xx;
+    Dn = L.Mo * p.my + L.Do * p.yy;
+  } else {
+    Mn = prior * fma_t(L.Mp, p.mm, fma_t(L.Ip, p.gm, L.Dp * p.gm));
+    In = fma_t(Mu, p.mx, Iu * p.xx);
+    Dn = fma_t(L.Mo, p.my, L.Do * p.yy);
+  }
+  if (top) {
+    PhRing<T> o;
+    o.M = Mn;
+    o.I = In;
+    ring[t + 1] = o;  // column t - 15
+  }
+  if constexpr (SUM) {
+    if (t <= lim) {
+      accM += Mn;
+      accI += In;
+    }
+  }
+  L.Mp = Mu;
+  L.Ip = Iu;
+  L.Dp = Du;
+  L.Mo = Mn;
+  L.Io = In;
+  L.Do = Dn;
+  L.ho = hu;
+}
+
+template <typename T, bool EXACT, bool SUM>
+__device__ __forceinline__ void phmm_block(LaneState<T>& L, PhRing<T> (&pf)[4], const int Q, const RowP<T>& p,
+                                           const T myp, const T yyp, PhRing<T>* __restrict__ ring, const int t0,
+                                           const bool top, const int lim, T& accM, T& accI) {
+  [&]<int... S>(std::integer_sequence<int, S...>) {
+    (phmm_step<T, EXACT, SUM, S>(L, pf, Q, p, myp, yyp, ring, t0, top, lim, accM, accI), ...);
+  }(std::make_integer_sequence<int, 16>{});
+}
+
+struct RawRow {
+  int rb, bq, iq, dq, gq;
+};
+
+__device__ __forceinline__ RawRow load_raw(const PhmmDevBatch& b, bool valid, int64_t pos) {
+  RawRow r{-1, 0, 0, 0, 0};
   if (valid) {
-    rbase = b.rb[pos];
-    const int q = b.bq[pos] & 127, qi = b.iq[pos] & 127, qd = b.dq[pos] & 127, qc = b.gq[pos] & 127;
-    e1 = tab.dmatch[q];
-    e3 = (rbase == 'N') ? e1 : tab.dmis[q];
-    const int hi = qi > qd ? qi : qd, lo = qi > qd ? qd : qi;
-    mm = tab.mm[((hi * (hi + 1)) >> 1) + lo];
-    gm = tab.dmatch[qc];
-    mx = tab.ph2pr[qi];
-    xx = tab.ph2pr[qc];
-    my = tab.ph2pr[qd];
-    yy = tab.ph2pr[qc];
+    r.rb = b.rb[pos];
+    r.bq = b.bq[pos];
+    r.iq = b.iq[pos];
+    r.dq = b.dq[pos];
+    r.gq = b.gq[pos];
+  }
+  return r;
+}
+
+template <typename T>
+__device__ __forceinline__ RowP<T> row_params(const PhmmTables<T>& tab, const RawRow& r) {
+  RowP<T> p;
+  if (r.rb < 0) {
+    p.e1 = p.e3 = p.mm = p.gm = p.mx = p.xx = p.my = p.yy = (T)0;
+    p.rbase = -1;
+    return p;
+  }
+  const int q = r.bq & 127, qi = r.iq & 127, qd = r.dq & 127, qc = r.gq & 127;
+  p.rbase = r.rb;
+  p.e1 = tab.dmatch[q];
+  p.e3 = (r.rb == 'N') ? p.e1 : tab.dmis[q];
+  const int hi = qi > qd ? qi : qd, lo = qi > qd ? qd : qi;
+  p.mm = tab.mm[((hi * (hi + 1)) >> 1) + lo];
+  p.gm = tab.dmatch[qc];
+  p.mx = tab.ph2pr[qi];
+  p.xx = tab.ph2pr[qc];
+  p.my = tab.ph2pr[qd];
+  p.yy = tab.ph2pr[qc];
+  return p;
+}
+
+// Runs one stripe: nblk blocks of 16 steps; the next stripe's parameters are
+// gathered after the first block (their bytes were requested at stripe start).
+template <typename T, bool EXACT, bool SUM>
+__device__ __forceinline__ void phmm_stripe(LaneState<T>& L, const RowP<T>& p, const T myp, const T yyp,
+                                            PhRing<T>* __restrict__ ring, const unsigned char* __restrict__ hapl,
+                                            const int sl, const int nblk, const int lim, T& accM, T& accI,
+                                            const PhmmTables<T>& tab, const RawRow& nraw, RowP<T>& np) {
+  const bool top = sl == 15;
+  PhRing<T> pf[4];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) pf[k] = ring[16 + k];
+  int Q = hapl[sl];
+  int Qn = hapl[16 + sl];
+  phmm_block<T, EXACT, SUM>(L, pf, Q, p, myp, yyp, ring, 0, top, lim, accM, accI);
+  np = row_params<T>(tab, nraw);
+  for (int blk = 1; blk < nblk; ++blk) {
+    Q = Qn;
+    Qn = hapl[16 * (blk + 1) + sl];
+    phmm_block<T, EXACT, SUM>(L, pf, Q, p, myp, yyp, ring, 16 * blk, top, lim, accM, accI);
   }
 }
 
-// FINAL_DOUBLE=false: fp32 pass (rescue queueing); true: fp64 pass.
 template <typename T, bool EXACT, bool RESCUE_PASS>
 __global__ __launch_bounds__(64) void phmm_kernel(const PhmmDevBatch b, const int32_t* __restrict__ order,
                                                   const unsigned long long* __restrict__ count_dev,
-                                                  long long count_host, const int nslot, const PhmmTables<T> tab,
-                                                  double* __restrict__ out, int32_t* __restrict__ rescue_list,
+                                                  long long count_host, const int nslot, const int nhap,
+                                                  const PhmmTables<T> tab, double* __restrict__ out,
+                                                  int32_t* __restrict__ rescue_list,
                                                   unsigned long long* __restrict__ rescue_count, const float thr,
                                                   const int use_rescue) {
   extern __shared__ __align__(16) unsigned char smem_raw[];
-  PhSlot<T>* const slots = reinterpret_cast<PhSlot<T>*>(smem_raw);
   const int lane = threadIdx.x;
   const int seg = lane >> 4;
   const int sl = lane & 15;
-  PhSlot<T>* const buf = slots + seg * nslot;
+  PhRing<T>* const ring = reinterpret_cast<PhRing<T>*>(smem_raw) + seg * nslot;
+  unsigned char* const hapl = smem_raw + (size_t)4 * nslot * sizeof(PhRing<T>) + seg * nhap;
   const long long count = count_dev ? (long long)(*count_dev) : count_host;
   const long long ngroups = (count + 3) >> 2;
 
@@ -150,42 +223,42 @@ __global__ __launch_bounds__(64) void phmm_kernel(const PhmmDevBatch b, const in
     const int nstr_max = wave_max(nstr);
     if (nstr_max == 0) continue;
 
-    // Boundary ring <- row 0: M = I = 0, D = INITIAL_CONSTANT / H for c in [0, H],
-    // hap base of column c (1-based) in .hb.
-    const T init = active ? tab.init_const / (T)H : (T)0;
+    // Boundary ring <- row 0 (M = I = 0; its D = INITIAL_CONSTANT / H is
+    // injected through lane 0's D stream) and the hap bytes by column.
     __syncthreads();
     for (int s = sl; s < nslot; s += 16) {
-      const int c = s - 16;
-      PhSlot<T> v{};
+      PhRing<T> v;
       v.M = 0;
       v.I = 0;
-      v.D = (active && c >= 0 && c <= H) ? init : (T)0;
-      v.hb = (active && c >= 1 && c <= H) ? (int)b.hb[ho + c - 1] : 0;
-      buf[s] = v;
+      ring[s] = v;
     }
+    for (int c = sl; c < nhap; c += 16)
+      hapl[c] = (active && c >= 1 && c <= H) ? b.hb[ho + c - 1] : (unsigned char)0;
     __syncthreads();
 
-    // Row parameters of stripe 0; the next stripe's are loaded one stripe ahead.
-    T e1, e3, mm, gm, mx, xx, my, yy;
-    int rbase;
-    load_row<T>(b, tab, active && sl < R, ro + sl, e1, e3, mm, gm, mx, xx, my, yy, rbase);
+    const T init = active ? tab.init_const / (T)H : (T)0;
+    RowP<T> prm = row_params<T>(tab, load_raw(b, active && sl < R, ro + sl));
     T accM = 0, accI = 0;
     const int sum_stripe = active ? (R - 1) >> 4 : -1;
     const int sum_lane = active ? (R - 1) & 15 : -1;
+    T myp = 0, yyp = 1;  // row 0: D(0, c) = init for every c
     for (int st = 0; st < nstr_max; ++st) {
       const int nrow = (st + 1) * 16 + sl;
-      T n_e1, n_e3, n_mm, n_gm, n_mx, n_xx, n_my, n_yy;
-      int n_rbase;
-      load_row<T>(b, tab, active && nrow < R, ro + nrow, n_e1, n_e3, n_mm, n_gm, n_mx, n_xx, n_my, n_yy, n_rbase);
-
+      const RawRow nraw = load_raw(b, active && nrow < R, ro + nrow);
+      RowP<T> nprm;
+      LaneState<T> L;
+      L.Mo = L.Io = L.Do = L.Mp = L.Ip = L.Dp = L.Mq = (T)0;
+      L.Dq = (st == 0) ? init : (T)0;
+      L.ho = 0;
       const bool seg_sums = (st == sum_stripe);
       const int any_sum = wave_max(seg_sums ? 1 : 0);
       if (any_sum) {
-        // Do all live segments finish here?  Then stop at the last summing column.
+        // If no live segment continues past this stripe, stop after the last summed column.
         const int cont = wave_max((active && nstr > st + 1) ? 1 : 0);
         const int lim = (seg_sums && sl == sum_lane) ? sl + H : -1;
         const int tend = cont ? Hmax + 15 : wave_max(seg_sums ? sum_lane + H : 0);
-        phmm_stripe<T, EXACT, true>(buf, sl, tend, e1, e3, mm, gm, mx, xx, my, yy, rbase, lim, accM, accI);
+        phmm_stripe<T, EXACT, true>(L, prm, myp, yyp, ring, hapl, sl, (tend + 16) >> 4, lim, accM, accI, tab, nraw,
+                                    nprm);
         if (seg_sums && sl == sum_lane) {
           const T sum = accM + accI;
           if constexpr (RESCUE_PASS) {
@@ -201,17 +274,13 @@ __global__ __launch_bounds__(64) void phmm_kernel(const PhmmDevBatch b, const in
           }
         }
       } else {
-        phmm_stripe<T, EXACT, false>(buf, sl, Hmax + 15, e1, e3, mm, gm, mx, xx, my, yy, rbase, -1, accM, accI);
+        phmm_stripe<T, EXACT, false>(L, prm, myp, yyp, ring, hapl, sl, (Hmax + 31) >> 4, -1, accM, accI, tab, nraw,
+                                     nprm);
       }
-      e1 = n_e1;
-      e3 = n_e3;
-      mm = n_mm;
-      gm = n_gm;
-      mx = n_mx;
-      xx = n_xx;
-      my = n_my;
-      yy = n_yy;
-      rbase = n_rbase;
+      // lane 0 of the next stripe derives D of this stripe's last row (lane 15)
+      myp = row_bcast<15>(prm.my);
+      yyp = row_bcast<15>(prm.yy);
+      prm = nprm;
     }
   }
 }
@@ -228,12 +297,10 @@ __global__ void phmm_keys_kernel(const PhmmDevBatch b, uint32_t* __restrict__ ke
   idx[p] = (int32_t)p;
 }
 
-static int nslot_for(int max_hap_len) {
-  // >= Hmax + 33 slots; slot count = 4 (mod 16) so the four segment rings start
-  // on different LDS bank groups (ds_read_b128 lane groups mix segments).
-  int n = ((max_hap_len + 33 + 15) / 16) * 16 + 4;
-  return n;
-}
+// Ring slots = column + 16 for columns -16 .. Hmax + 34 (block round-up plus
+// the four-step read-ahead); hap bytes by column 0 .. 16 * (blocks + 1).
+static int nslot_for(int max_hap_len) { return ((max_hap_len + 51 + 15) / 16) * 16; }
+static int nhap_for(int max_hap_len) { return ((max_hap_len + 15 + 16) / 16 + 1) * 16; }
 
 int launch_phmm_keys(const PhmmDevBatch& b, uint32_t* keys, int32_t* idx, hipStream_t s) {
   if (b.n_pairs <= 0) return FCS_OK;
@@ -250,17 +317,19 @@ static int launch_one(const PhmmDevBatch& b, const int32_t* order, const unsigne
                       double* out, int32_t* rescue_list, unsigned long long* rescue_count, float thr,
                       bool use_rescue, hipStream_t s) {
   const int nslot = nslot_for(max_hap_len);
-  const size_t lds = (size_t)4 * nslot * sizeof(PhSlot<T>);
+  const int nhap = nhap_for(max_hap_len);
+  const size_t lds = (size_t)4 * nslot * sizeof(PhRing<T>) + (size_t)4 * nhap;
   if (lds > 160 * 1024)
     return fail(FCS_ERR_UNSUPPORTED, "[E::fcship] max_hap_len too large for the LDS boundary ring");
   auto kern = phmm_kernel<T, EXACT, RESCUE>;
-  if (lds > 64 * 1024) FCS_HIP_CHECK(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+  if (lds > 64 * 1024)
+    FCS_HIP_CHECK(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
   long long grid = max_groups;
   const long long cap = 256LL * 64;  // grid-stride beyond this
   if (grid > cap) grid = cap;
   if (grid < 1) grid = 1;
-  hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(64), lds, s, b, order, count_dev, count_host, nslot, tab, out,
-                     rescue_list, rescue_count, thr, use_rescue ? 1 : 0);
+  hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(64), lds, s, b, order, count_dev, count_host, nslot, nhap, tab,
+                     out, rescue_list, rescue_count, thr, use_rescue ? 1 : 0);
   FCS_HIP_CHECK(hipGetLastError());
   return FCS_OK;
 }

@@ -178,8 +178,13 @@ def test_golden_fixtures_gpu(gpu):
     haps = [bytes(c["hap"]) for c in g["cases"]]
     p = fcship.make_pairs(reads, haps, pairs=[(i, i) for i in range(len(reads))])
     exp = np.array([c["log10"] for c in g["cases"]])
+    resc = np.array([c["rescued"] for c in g["cases"]])
+    fin = np.isfinite(exp)
     for exact in (True, False):
         out = fcship.phmm_compute_pairs(p, exact=exact)
-        fin = np.isfinite(exp)
         assert np.array_equal(np.isfinite(out), fin)
-        np.testing.assert_allclose(out[fin], exp[fin], rtol=1e-6 if exact else RTOL)
+        if exact:  # bitwise sums; device vs host log10f may differ by an ulp at ~36
+            tol = np.where(resc, 1e-12 * np.abs(exp) + 1e-12, 2 * ulp32(exp) + 2 * ulp32(36.123599))
+            assert np.all(np.abs(out[fin] - exp[fin]) <= tol[fin])
+        else:
+            np.testing.assert_allclose(out[fin], exp[fin], rtol=RTOL)
