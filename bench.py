@@ -131,9 +131,10 @@ def bench_bsw(args, dev, tasks, reps=3):
     cells = torch.empty(tasks.n, dtype=torch.int64, device=dev)
     params = fcship.bsw_params()
     stream = torch.cuda.current_stream(dev)
-    run = lambda: fcship.check(fcship.lib.fcs_bsw_extend_dev(fcship.C.byref(b), fcship.C.byref(params),  # noqa
-                                                             res.data_ptr(), cells.data_ptr(), dev.index,
-                                                             stream.cuda_stream))
+    plan = fcship.C.c_void_p()
+    fcship.check(fcship.lib.fcs_bsw_plan_create(dev.index, tasks.n, fcship.C.byref(plan)))
+    run = lambda: fcship.check(fcship.lib.fcs_bsw_extend_plan(plan, fcship.C.byref(b), fcship.C.byref(params),  # noqa
+                                                              res.data_ptr(), cells.data_ptr(), stream.cuda_stream))
     run()
     torch.cuda.synchronize(dev)
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -144,6 +145,7 @@ def bench_bsw(args, dev, tasks, reps=3):
     torch.cuda.synchronize(dev)
     ms = e0.elapsed_time(e1) / reps
     ncell = int(cells.sum().item())
+    fcship.lib.fcs_bsw_plan_destroy(plan)
     del keep
     return dict(ms=ms, cells=ncell, gcups=ncell / (ms * 1e-3) / 1e9, tasks=tasks.n,
                 bytes=int(tasks.qbuf.size + tasks.tbuf.size + 24 * tasks.n))

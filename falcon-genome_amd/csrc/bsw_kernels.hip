@@ -206,9 +206,12 @@ __device__ void extend_task(const BswDevBatch& b, const BswParams& p, long long 
 
 template <int MAXNS>
 __global__ __launch_bounds__(64) void bsw_extend_kernel(const BswDevBatch b, const BswParams p, int32_t* __restrict__ res,
-                                                        int64_t* __restrict__ cells) {
+                                                        int64_t* __restrict__ cells, const int32_t* __restrict__ order,
+                                                        const int64_t* __restrict__ bounds) {
   extern __shared__ __align__(16) unsigned char tl[];
-  for (long long task = blockIdx.x; task < b.n; task += gridDim.x) {
+  const long long lo = bounds[7], hi = bounds[8];
+  for (long long pos = lo + blockIdx.x; pos < hi; pos += gridDim.x) {
+    const long long task = order[pos];
     const int qlen = b.qlen[task];
     const int ns = (qlen + 1 + 63) >> 6;
     if (MAXNS <= 4) {
@@ -227,8 +230,8 @@ __global__ __launch_bounds__(64) void bsw_extend_kernel(const BswDevBatch b, con
   }
 }
 
-int launch_bsw_extend(const BswDevBatch& b, const BswParams& p, int max_qlen, int max_tlen, int32_t* res,
-                      int64_t* cells, hipStream_t s) {
+int launch_bsw_extend_wide(const BswDevBatch& b, const BswParams& p, int max_qlen, int max_tlen, int32_t* res,
+                           int64_t* cells, const int32_t* order, const int64_t* bounds, hipStream_t s) {
   if (b.n <= 0) return FCS_OK;
   if (max_qlen > 1023) return fail(FCS_ERR_UNSUPPORTED, "[E::fcship] ksw_extend2: qlen > 1023 unsupported");
   const size_t lds = (size_t)((max_tlen + 64 + 15) / 16) * 16;
@@ -237,9 +240,9 @@ int launch_bsw_extend(const BswDevBatch& b, const BswParams& p, int max_qlen, in
   const long long cap = 256LL * 64;
   if (grid > cap) grid = cap;
   if (max_qlen <= 255)
-    hipLaunchKernelGGL(bsw_extend_kernel<4>, dim3((unsigned)grid), dim3(64), lds, s, b, p, res, cells);
+    hipLaunchKernelGGL(bsw_extend_kernel<4>, dim3((unsigned)grid), dim3(64), lds, s, b, p, res, cells, order, bounds);
   else
-    hipLaunchKernelGGL(bsw_extend_kernel<16>, dim3((unsigned)grid), dim3(64), lds, s, b, p, res, cells);
+    hipLaunchKernelGGL(bsw_extend_kernel<16>, dim3((unsigned)grid), dim3(64), lds, s, b, p, res, cells, order, bounds);
   FCS_HIP_CHECK(hipGetLastError());
   return FCS_OK;
 }

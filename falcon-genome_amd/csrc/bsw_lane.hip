@@ -1,0 +1,291 @@
+// ksw_extend2 with one task per LANE (gfx950), for the bwa-typical envelope:
+// qlen <= 151, every score fits in int16, mat entries in [-16, 15].
+//
+// Algorithm: bwa ksw.c ksw_extend2, reached from
+// /root/reference/src/workers/BWAWorker.cpp:134-166.
+//
+// Mapping (DESIGN.md §Banded SW, "lane kernel"): the wave takes 64 tasks of
+// similar (qlen, tlen) from the device-sorted schedule; each lane runs bwa's
+// row loop verbatim for its own task.  bwa's eh[] lives in registers as
+// packed int16 pairs (h | e << 16), indexed by compile-time column numbers in
+// a fully unrolled column loop, so the band bookkeeping (including the stale
+// eh[] entries that bwa re-reads when the band grows) is reproduced exactly.
+// Per cell: 2 ops for the profile score (5-bit fields selected by the query
+// code), then bwa's max/add chain; no cross-lane traffic at all.  A 16-column
+// chunk is skipped when it lies outside the band of every live lane (one
+// wave-wide min/max per row), and lanes whose task ended idle under EXEC.
+#include <hip/hip_runtime.h>
+
+#include <utility>
+
+#include "fcship_internal.h"
+
+namespace fcs {
+
+__device__ __forceinline__ int wave_min_i(int v) { return -wave_max(-v); }
+
+// registers holding the per-column query offsets (q * 5), six 5-bit fields each
+template <int NC> constexpr int QW = (NC + 5) / 6;
+
+// Signed 5-bit field at bit offset `off` of `pack`.
+__device__ __forceinline__ int field5(uint32_t pack, uint32_t off) {
+  return ((int)((pack >> off) << 27)) >> 27;
+}
+
+struct LaneRow {
+  int beg, end, h1, f, m, mj, first, last;
+  uint32_t pack;
+};
+
+template <int J, int NC>
+__device__ __forceinline__ void lane_cell(uint32_t (&eh)[NC], const uint32_t (&qr)[QW<NC>], LaneRow& r, const bool work,
+                                          const int e_del, const int oe_del, const int e_ins, const int oe_ins) {
+  if (work && J >= r.beg && J < r.end) {
+    const uint32_t x = eh[J];
+    const int hp = (int)(x & 0xFFFFu);
+    const int e = (int)(x >> 16);
+    const uint32_t qo = (qr[J / 6] >> (5 * (J % 6))) & 31u;
+    const int s = field5(r.pack, qo);
+    const int M = hp ? hp + s : 0;
+    const int h = max(max(M, e), r.f);
+    r.mj = (h >= r.m) ? J : r.mj;  // ties go to the larger j
+    r.m = max(r.m, h);
+    const int en = max(max(e - e_del, M - oe_del), 0);
+    r.f = max(max(r.f - e_ins, M - oe_ins), 0);
+    const uint32_t xn = (uint32_t)r.h1 | ((uint32_t)en << 16);
+    eh[J] = xn;
+    r.h1 = h;
+    if (xn != 0u) {
+      r.last = J;
+      if (r.first > NC) r.first = J;
+    }
+  } else if (work && J == r.end) {
+    eh[J] = (uint32_t)r.h1;  // eh[end] = {h1, 0}
+    if (r.h1 != 0) r.last = J;
+  }
+}
+
+template <int C, int NC>
+__device__ __forceinline__ void lane_chunk(uint32_t (&eh)[NC], const uint32_t (&qr)[QW<NC>], LaneRow& r, const bool work,
+                                           const int cmin, const int cmax, const int e_del, const int oe_del,
+                                           const int e_ins, const int oe_ins) {
+  constexpr int L = (NC - 16 * C) < 16 ? (NC - 16 * C) : 16;  // last chunk may be partial
+  if (16 * C <= cmax && 16 * C + L - 1 >= cmin) {
+    [&]<int... S>(std::integer_sequence<int, S...>) {
+      (lane_cell<16 * C + S, NC>(eh, qr, r, work, e_del, oe_del, e_ins, oe_ins), ...);
+    }(std::make_integer_sequence<int, L>{});
+  }
+}
+
+template <int NC>
+__global__ __launch_bounds__(64, 2) void bsw_lane_kernel(const BswDevBatch b, const BswParams p,
+                                                      const int32_t* __restrict__ order,
+                                                      const int64_t* __restrict__ bounds, const int bucket,
+                                                      int32_t* __restrict__ res, int64_t* __restrict__ cells_out) {
+  const long long lo = bounds[bucket], hi = bounds[bucket + 1];
+  const long long base = lo + 64LL * blockIdx.x;
+  if (base >= hi) return;
+  const int lane = threadIdx.x;
+  const long long k = base + lane;
+  const bool has = k < hi;
+  const long long task = has ? order[k] : 0;
+  int qlen = 0, tlen = 0, h0 = 1, w = 0;
+  const uint8_t* __restrict__ q = b.qbuf;
+  const uint8_t* __restrict__ tg = b.tbuf;
+  if (has) {
+    qlen = b.qlen[task];
+    tlen = b.tlen[task];
+    h0 = b.h0[task];
+    w = b.w[task];
+    q = b.qbuf + b.qoff[task];
+    tg = b.tbuf + b.toff[task];
+  }
+  const int e_del = p.e_del, e_ins = p.e_ins, oe_del = p.o_del + p.e_del, oe_ins = p.o_ins + p.e_ins;
+
+  uint32_t qr[QW<NC>];
+#pragma unroll
+  for (int c = 0; c < QW<NC>; ++c) {
+    uint32_t v = 0;
+#pragma unroll
+    for (int z = 0; z < 6; ++z) {
+      const int j = 6 * c + z;
+      const uint32_t qb = (j < qlen) ? (uint32_t)q[j] : 4u;
+      if (j < NC) v |= (qb * 5u) << (5 * z);
+    }
+    qr[c] = v;
+  }
+  uint32_t eh[NC];
+  const int h1v = h0 > oe_ins ? h0 - oe_ins : 0;
+#pragma unroll
+  for (int j = 0; j < NC; ++j) {
+    int hv = 0;
+    if (j == 0) hv = h0;
+    else if (j == 1) hv = (j <= qlen) ? h1v : 0;
+    else hv = (j <= qlen) ? max(h1v - (j - 1) * e_ins, 0) : 0;
+    eh[j] = (uint32_t)hv;
+  }
+  {
+    int max_ins = (int)((double)(qlen * p.max_mat + p.end_bonus - p.o_ins) / e_ins + 1.);
+    max_ins = max_ins > 1 ? max_ins : 1;
+    w = w < max_ins ? w : max_ins;
+    int max_del = (int)((double)(qlen * p.max_mat + p.end_bonus - p.o_del) / e_del + 1.);
+    max_del = max_del > 1 ? max_del : 1;
+    w = w < max_del ? w : max_del;
+  }
+
+  int mx = h0, max_i = -1, max_j = -1, max_ie = -1, gscore = -1, max_off = 0;
+  int ncell = 0;  // <= qlen * tlen < 2^31 in this envelope
+  bool done = !has;
+  LaneRow r;
+  r.beg = 0;
+  r.end = qlen;
+  int tcur = (tlen > 0) ? tg[0] : 0;
+  int tnext = (tlen > 1) ? tg[1] : 0;
+  for (int i = 0;; ++i) {
+    const bool alive = !done && i < tlen;
+    if (__ballot(alive) == 0ull) break;
+    const int tb = tcur;
+    tcur = tnext;
+    tnext = (alive && i + 2 < tlen) ? tg[i + 2] : 0;
+    if (alive) {
+      if (r.beg < i - w) r.beg = i - w;
+      if (r.end > i + w + 1) r.end = i + w + 1;
+      if (r.end > qlen) r.end = qlen;
+      r.h1 = 0;
+      if (r.beg == 0) {
+        r.h1 = h0 - (p.o_del + e_del * (i + 1));
+        if (r.h1 < 0) r.h1 = 0;
+      }
+    }
+    if constexpr (NC >= 96) {
+      // keep the per-column query offsets packed (re-extracted per cell)
+      // instead of letting the compiler hoist NC unpacked copies out of the
+      // row loop: that doubles the register file and halves occupancy
+#pragma unroll
+      for (int c = 0; c < QW<NC>; ++c) asm volatile("" : "+v"(qr[c]));
+    }
+    const bool empty = alive && r.beg >= r.end;
+    const bool work = alive && !empty;
+    const int cmin = wave_min_i(work ? r.beg : (1 << 20));
+    const int cmax = wave_max(work ? r.end : -1);
+    r.pack = tb == 0 ? (uint32_t)p.matpack[0]
+           : tb == 1 ? (uint32_t)p.matpack[1]
+           : tb == 2 ? (uint32_t)p.matpack[2]
+           : tb == 3 ? (uint32_t)p.matpack[3] : (uint32_t)p.matpack[4];
+    r.f = 0;
+    r.m = 0;
+    r.mj = -1;
+    r.first = NC + 1;
+    r.last = -1;
+    [&]<int... C>(std::integer_sequence<int, C...>) {
+      (lane_chunk<C, NC>(eh, qr, r, work, cmin, cmax, e_del, oe_del, e_ins, oe_ins), ...);
+    }(std::make_integer_sequence<int, (NC + 15) / 16>{});
+    if (empty) {
+      // bwa still stores eh[end] = {h1, 0}; the loop index equals beg here
+#pragma unroll
+      for (int j = 0; j < NC; ++j)
+        if (j == r.end) eh[j] = (uint32_t)r.h1;
+      if (r.beg == qlen) {
+        max_ie = gscore > r.h1 ? max_ie : i;
+        gscore = gscore > r.h1 ? gscore : r.h1;
+      }
+      done = true;
+    }
+    if (work) {
+      ncell += r.end - r.beg;
+      if (r.end == qlen) {
+        max_ie = gscore > r.h1 ? max_ie : i;
+        gscore = gscore > r.h1 ? gscore : r.h1;
+      }
+      if (r.m == 0) {
+        done = true;
+      } else if (r.m > mx) {
+        mx = r.m, max_i = i, max_j = r.mj;
+        const int d = r.mj > i ? r.mj - i : i - r.mj;
+        max_off = max_off > d ? max_off : d;
+      } else if (p.zdrop > 0) {
+        if (i - max_i > r.mj - max_j) {
+          if (mx - r.m - ((i - max_i) - (r.mj - max_j)) * e_del > p.zdrop) done = true;
+        } else {
+          if (mx - r.m - ((r.mj - max_j) - (i - max_i)) * e_ins > p.zdrop) done = true;
+        }
+      }
+      if (!done) {
+        r.beg = (r.first <= NC) ? r.first : r.end;
+        r.end = (r.last >= 0) ? min(r.last + 2, qlen) : min(r.beg + 1, qlen);
+      }
+    }
+  }
+  if (has) {
+    int32_t* o = res + 6 * task;
+    o[0] = mx;
+    o[1] = max_j + 1;
+    o[2] = max_i + 1;
+    o[3] = max_ie + 1;
+    o[4] = gscore;
+    o[5] = max_off;
+    if (cells_out) cells_out[task] = ncell;
+  }
+}
+
+// Bucket of a task: 0..6 = lane kernel with 16/32/48/64/96/128/152 register
+// columns (152 = bwa reads up to 151 bp), 7 = wave-per-task kernel (long queries or out-of-int16 scores).
+__device__ __forceinline__ int bsw_bucket(int qlen, int h0, const BswParams& p) {
+  if (!p.lane_ok || h0 <= 0 || (long long)h0 + (long long)qlen * p.max_mat >= 32000) return 7;
+  const int need = qlen + 1;
+  if (need <= 16) return 0;
+  if (need <= 32) return 1;
+  if (need <= 48) return 2;
+  if (need <= 64) return 3;
+  if (need <= 96) return 4;
+  if (need <= 128) return 5;
+  if (need <= 152) return 6;
+  return 7;
+}
+
+__global__ void bsw_keys_kernel(const BswDevBatch b, const BswParams p, uint32_t* __restrict__ keys,
+                                int32_t* __restrict__ idx) {
+  const long long k = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (k >= b.n) return;
+  const int qlen = b.qlen[k], tlen = b.tlen[k];
+  const uint32_t bk = (uint32_t)bsw_bucket(qlen, b.h0[k], p);
+  keys[k] = (bk << 28) | ((uint32_t)min(max(qlen, 0), 1023) << 18) | (uint32_t)min(max(tlen, 0), 262143);
+  idx[k] = (int32_t)k;
+}
+
+// bounds[c] = first sorted position whose bucket >= c, c = 0..8.
+__global__ void bsw_bounds_kernel(const uint32_t* __restrict__ keys, long long n, int64_t* __restrict__ bounds) {
+  const long long k = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (k > n) return;
+  const int cur = (k < n) ? (int)(keys[k] >> 28) : 8;
+  const int prev = (k > 0) ? (int)(keys[k - 1] >> 28) : -1;
+  for (int c = prev + 1; c <= cur; ++c) bounds[c] = k;
+}
+
+int launch_bsw_extend_sorted(const BswDevBatch& b, const BswParams& p, int max_qlen, int max_tlen, int32_t* res,
+                             int64_t* cells, const BswWorkspace& ws, hipStream_t s) {
+  if (b.n <= 0) return FCS_OK;
+  if (b.n > ws.cap) return fail(FCS_ERR_INVALID, "[E::fcship] SW batch larger than its plan");
+  const int bs = 256;
+  const unsigned nb = (unsigned)((b.n + bs - 1) / bs);
+  hipLaunchKernelGGL(bsw_keys_kernel, dim3(nb), dim3(bs), 0, s, b, p, ws.keys_in, ws.idx_in);
+  FCS_HIP_CHECK(hipGetLastError());
+  size_t tmp = ws.tmp_bytes;
+  FCS_HIP_CHECK(hipcub_sort_pairs(ws.tmp, tmp, ws.keys_in, ws.keys_out, ws.idx_in, ws.idx_out, (int)b.n, s));
+  hipLaunchKernelGGL(bsw_bounds_kernel, dim3((unsigned)((b.n + 1 + bs - 1) / bs)), dim3(bs), 0, s, ws.keys_out,
+                     (long long)b.n, ws.bounds);
+  FCS_HIP_CHECK(hipGetLastError());
+  const unsigned g = (unsigned)((b.n + 63) / 64);
+  hipLaunchKernelGGL(bsw_lane_kernel<16>, dim3(g), dim3(64), 0, s, b, p, ws.idx_out, ws.bounds, 0, res, cells);
+  hipLaunchKernelGGL(bsw_lane_kernel<32>, dim3(g), dim3(64), 0, s, b, p, ws.idx_out, ws.bounds, 1, res, cells);
+  hipLaunchKernelGGL(bsw_lane_kernel<48>, dim3(g), dim3(64), 0, s, b, p, ws.idx_out, ws.bounds, 2, res, cells);
+  hipLaunchKernelGGL(bsw_lane_kernel<64>, dim3(g), dim3(64), 0, s, b, p, ws.idx_out, ws.bounds, 3, res, cells);
+  hipLaunchKernelGGL(bsw_lane_kernel<96>, dim3(g), dim3(64), 0, s, b, p, ws.idx_out, ws.bounds, 4, res, cells);
+  hipLaunchKernelGGL(bsw_lane_kernel<128>, dim3(g), dim3(64), 0, s, b, p, ws.idx_out, ws.bounds, 5, res, cells);
+  hipLaunchKernelGGL(bsw_lane_kernel<152>, dim3(g), dim3(64), 0, s, b, p, ws.idx_out, ws.bounds, 6, res, cells);
+  FCS_HIP_CHECK(hipGetLastError());
+  // bucket 7: wave-per-task kernel over the sorted tail
+  return launch_bsw_extend_wide(b, p, max_qlen, max_tlen, res, cells, ws.idx_out, ws.bounds, s);
+}
+
+}  // namespace fcs

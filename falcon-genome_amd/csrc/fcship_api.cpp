@@ -88,7 +88,42 @@ BswParams to_params(const fcs_bsw_params* p) {
   int mx = 0;
   for (int i = 0; i < 25; ++i) mx = std::max<int>(mx, p->mat[i]);
   q.max_mat = mx;
+  q.lane_ok = 1;
+  for (int t = 0; t < 5; ++t) {
+    uint32_t pk = 0;
+    for (int c = 0; c < 5; ++c) {
+      const int v = p->mat[t * 5 + c];
+      if (v < -16 || v > 15) q.lane_ok = 0;
+      pk |= ((uint32_t)v & 31u) << (5 * c);
+    }
+    q.matpack[t] = (int32_t)pk;
+  }
   return q;
+}
+
+// Workspace for one SW schedule of up to cap tasks.  Stream-ordered
+// allocation when `stream_alloc`, so the *_dev entry point stays asynchronous.
+int ws_alloc(BswWorkspace& ws, int64_t cap, hipStream_t s, bool stream_alloc) {
+  ws.cap = cap;
+  const size_t n = (size_t)std::max<int64_t>(cap, 1);
+  size_t tmp = 0;
+  FCS_HIP_CHECK(hipcub_sort_pairs(nullptr, tmp, nullptr, nullptr, nullptr, nullptr, (int)n, s));
+  ws.tmp_bytes = std::max<size_t>(tmp, 16);
+  void** bufs[6] = {(void**)&ws.keys_in, (void**)&ws.keys_out, (void**)&ws.idx_in, (void**)&ws.idx_out,
+                    (void**)&ws.bounds, &ws.tmp};
+  const size_t sz[6] = {4 * n, 4 * n, 4 * n, 4 * n, 9 * sizeof(int64_t), ws.tmp_bytes};
+  for (int i = 0; i < 6; ++i) {
+    if (stream_alloc) FCS_HIP_CHECK(hipMallocAsync(bufs[i], sz[i], s));
+    else FCS_HIP_CHECK(hipMalloc(bufs[i], sz[i]));
+  }
+  return FCS_OK;
+}
+
+void ws_free(BswWorkspace& ws, hipStream_t s, bool stream_alloc) {
+  void* bufs[6] = {ws.keys_in, ws.keys_out, ws.idx_in, ws.idx_out, ws.bounds, ws.tmp};
+  for (void* b : bufs)
+    if (b) (void)(stream_alloc ? hipFreeAsync(b, s) : hipFree(b));
+  ws = BswWorkspace();
 }
 
 int check_params(const fcs_bsw_params* p) {
@@ -99,6 +134,11 @@ int check_params(const fcs_bsw_params* p) {
 }
 
 }  // namespace
+
+hipError_t hipcub_sort_pairs(void* tmp, size_t& bytes, const uint32_t* kin, uint32_t* kout, const int32_t* vin,
+                             int32_t* vout, int n, hipStream_t s) {
+  return hipcub::DeviceRadixSort::SortPairs(tmp, bytes, kin, kout, vin, vout, n, 0, 32, s);
+}
 
 int get_device_tables(int device, DeviceTables** out) {
   std::lock_guard<std::mutex> lk(g_dev_mu);
@@ -130,7 +170,12 @@ int get_device_tables(int device, DeviceTables** out) {
 
 using namespace fcs;
 
-// ------------------------------------------------------------------ plan
+// ------------------------------------------------------------------ plans
+struct fcs_bsw_plan {
+  int device = 0;
+  BswWorkspace ws;
+};
+
 struct fcs_phmm_plan {
   int device = 0;
   int64_t max_pairs = 0;
@@ -491,9 +536,55 @@ int fcs_bsw_extend_dev(const fcs_bsw_batch* b, const fcs_bsw_params* params, int
   if ((rc = check_params(params))) return rc;
   if (b->n > 0 && !res) return fail(FCS_ERR_INVALID, "[E::fcs_bsw_extend_dev] null result buffer");
   if ((rc = check_device(device))) return rc;
+  if (b->n == 0) return FCS_OK;
   FCS_HIP_CHECK(hipSetDevice(device));
-  return launch_bsw_extend(bsw_dev(b), to_params(params), std::max(b->max_qlen, 0), std::max(b->max_tlen, 0), res,
-                           cells, (hipStream_t)stream);
+  hipStream_t s = (hipStream_t)stream;
+  BswWorkspace ws;
+  if ((rc = ws_alloc(ws, b->n, s, true))) {
+    ws_free(ws, s, true);
+    return rc;
+  }
+  rc = launch_bsw_extend_sorted(bsw_dev(b), to_params(params), std::max(b->max_qlen, 0), std::max(b->max_tlen, 0),
+                                res, cells, ws, s);
+  ws_free(ws, s, true);
+  return rc;
+}
+
+int fcs_bsw_plan_create(int32_t device, int64_t max_tasks, fcs_bsw_plan** plan) {
+  if (!plan || max_tasks < 0) return fail(FCS_ERR_INVALID, "[E::fcs_bsw_plan_create] bad arguments");
+  int rc = check_device(device);
+  if (rc) return rc;
+  FCS_HIP_CHECK(hipSetDevice(device));
+  std::unique_ptr<fcs_bsw_plan> p(new fcs_bsw_plan());
+  p->device = device;
+  if ((rc = ws_alloc(p->ws, max_tasks, nullptr, false))) {
+    ws_free(p->ws, nullptr, false);
+    return rc;
+  }
+  *plan = p.release();
+  return FCS_OK;
+}
+
+int fcs_bsw_plan_destroy(fcs_bsw_plan* plan) {
+  if (!plan) return FCS_OK;
+  (void)hipSetDevice(plan->device);
+  ws_free(plan->ws, nullptr, false);
+  delete plan;
+  return FCS_OK;
+}
+
+int fcs_bsw_extend_plan(fcs_bsw_plan* plan, const fcs_bsw_batch* b, const fcs_bsw_params* params, int32_t* res,
+                        int64_t* cells, void* stream) {
+  if (!plan) return fail(FCS_ERR_INVALID, "[E::fcs_bsw_extend_plan] null plan");
+  int rc = check_bsw_batch(b);
+  if (rc) return rc;
+  if ((rc = check_params(params))) return rc;
+  if (b->n > plan->ws.cap) return fail(FCS_ERR_INVALID, "[E::fcs_bsw_extend_plan] batch exceeds plan");
+  if (b->n > 0 && !res) return fail(FCS_ERR_INVALID, "[E::fcs_bsw_extend_plan] null result buffer");
+  if (b->n == 0) return FCS_OK;
+  FCS_HIP_CHECK(hipSetDevice(plan->device));
+  return launch_bsw_extend_sorted(bsw_dev(b), to_params(params), std::max(b->max_qlen, 0), std::max(b->max_tlen, 0),
+                                  res, cells, plan->ws, (hipStream_t)stream);
 }
 
 int fcs_bsw_extend_batch(const fcs_bsw_batch* b, const fcs_bsw_params* params, int32_t* res, int64_t* cells,
@@ -732,6 +823,6 @@ int fcs_ksw_global2(int qlen, const uint8_t* query, int tlen, const uint8_t* tar
   return score;
 }
 
-int fcs_abi_symbol_count(void) { return 26; }
+int fcs_abi_symbol_count(void) { return 29; }
 
 }  // extern "C"

@@ -141,9 +141,28 @@ struct BswParams {
   int8_t mat[25];
   int32_t o_del, e_del, o_ins, e_ins, end_bonus, zdrop;
   int32_t max_mat;
+  int32_t matpack[5];  // row t: mat[t*5+q] as signed 5-bit fields at bit 5*q
+  int32_t lane_ok;     // every mat entry fits a signed 5-bit field
 };
-int launch_bsw_extend(const BswDevBatch& b, const BswParams& p, int max_qlen, int max_tlen, int32_t* res,
-                      int64_t* cells, hipStream_t s);
+// Device scratch of one SW launch sequence (sort keys, schedule, bucket bounds).
+struct BswWorkspace {
+  int64_t cap = 0;
+  uint32_t* keys_in = nullptr;
+  uint32_t* keys_out = nullptr;
+  int32_t* idx_in = nullptr;
+  int32_t* idx_out = nullptr;
+  int64_t* bounds = nullptr;  // [9]
+  void* tmp = nullptr;
+  size_t tmp_bytes = 0;
+};
+hipError_t hipcub_sort_pairs(void* tmp, size_t& bytes, const uint32_t* kin, uint32_t* kout, const int32_t* vin,
+                             int32_t* vout, int n, hipStream_t s);
+// Sorted schedule: lane-per-task kernels for buckets 0..6, wave-per-task for 7.
+int launch_bsw_extend_sorted(const BswDevBatch& b, const BswParams& p, int max_qlen, int max_tlen, int32_t* res,
+                             int64_t* cells, const BswWorkspace& ws, hipStream_t s);
+// Wave-per-task kernel over sorted positions [bounds[7], bounds[8]).
+int launch_bsw_extend_wide(const BswDevBatch& b, const BswParams& p, int max_qlen, int max_tlen, int32_t* res,
+                           int64_t* cells, const int32_t* order, const int64_t* bounds, hipStream_t s);
 int launch_bsw_global(const BswDevBatch& b, const BswParams& p, int max_qlen, int max_tlen, int32_t* scores,
                       uint8_t* zbuf, int64_t zbytes, const int64_t* zoff, uint32_t* cigar, const int64_t* cigar_off,
                       const int32_t* cigar_cap, int32_t* n_cigar, hipStream_t s);

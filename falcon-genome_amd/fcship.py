@@ -129,6 +129,10 @@ _sig("fcs_bsw_extend", C.c_int, [C.POINTER(BswTask), C.c_int32, C.POINTER(BswPar
 _sig("fcs_bsw_extend_dev", C.c_int, [C.POINTER(BswBatch), C.POINTER(BswParams), C.c_void_p, C.c_void_p,
                                      C.c_int32, C.c_void_p])
 _sig("fcs_bsw_extend_batch", C.c_int, [C.POINTER(BswBatch), C.POINTER(BswParams), i32p, i64p, C.c_int32])
+_sig("fcs_bsw_plan_create", C.c_int, [C.c_int32, C.c_int64, C.POINTER(C.c_void_p)])
+_sig("fcs_bsw_plan_destroy", C.c_int, [C.c_void_p])
+_sig("fcs_bsw_extend_plan", C.c_int, [C.c_void_p, C.POINTER(BswBatch), C.POINTER(BswParams), C.c_void_p, C.c_void_p,
+                                      C.c_void_p])
 _sig("fcs_bsw_global", C.c_int, [C.POINTER(BswTask), C.c_int32, C.POINTER(BswParams), i32p, u32p, i64p, i32p,
                                  i32p, C.c_int32])
 _sig("fcs_ksw_extend2", C.c_int, [C.c_int, u8p, C.c_int, u8p, C.c_int, i8p, C.c_int, C.c_int, C.c_int, C.c_int,

@@ -195,6 +195,15 @@ typedef struct {
 int fcs_bsw_extend_dev(const fcs_bsw_batch* dev_batch, const fcs_bsw_params* params, int32_t* dev_res,
                        int64_t* dev_cells, int32_t device, void* stream);
 
+/* Reusable device scratch for fcs_bsw_extend_plan (schedule sort buffers for
+ * batches of up to max_tasks tasks); fcs_bsw_extend_dev allocates the same
+ * scratch stream-ordered on every call instead. */
+typedef struct fcs_bsw_plan fcs_bsw_plan;
+int fcs_bsw_plan_create(int32_t device, int64_t max_tasks, fcs_bsw_plan** plan);
+int fcs_bsw_plan_destroy(fcs_bsw_plan* plan);
+int fcs_bsw_extend_plan(fcs_bsw_plan* plan, const fcs_bsw_batch* dev_batch, const fcs_bsw_params* params,
+                        int32_t* dev_res, int64_t* dev_cells, void* stream);
+
 /* Host-pointer packed batch (synchronous). */
 int fcs_bsw_extend_batch(const fcs_bsw_batch* host_batch, const fcs_bsw_params* params, int32_t* res,
                          int64_t* cells, int32_t device);
