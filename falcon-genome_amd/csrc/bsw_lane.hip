@@ -16,6 +16,7 @@
 // wave-wide min/max per row), and lanes whose task ended idle under EXEC.
 #include <hip/hip_runtime.h>
 
+#include <type_traits>
 #include <utility>
 
 #include "fcship_internal.h"
@@ -32,14 +33,49 @@ __device__ __forceinline__ int field5(uint32_t pack, uint32_t off) {
   return ((int)((pack >> off) << 27)) >> 27;
 }
 
+// Words of the per-row "eh[j] != 0" bitmap (bit j for column j).
+template <int NC> constexpr int NZW = (NC + 31) / 32;
+
+template <int NC>
 struct LaneRow {
-  int beg, end, h1, f, m, mj, first, last;
+  int beg, end, h1, f;
+  uint32_t key;  // max over the row of (h << 16 | j): row max and its arg-max, ties to the larger j
   uint32_t pack;
+  uint32_t nz[NZW<NC>];
 };
 
-template <int J, int NC>
-__device__ __forceinline__ void lane_cell(uint32_t (&eh)[NC], const uint32_t (&qr)[QW<NC>], LaneRow& r, const bool work,
-                                          const int e_del, const int oe_del, const int e_ins, const int oe_ins) {
+// One in-band cell (bwa's inner-loop body).
+template <int J, int NC, bool SYM>
+__device__ __forceinline__ void lane_cell_body(uint32_t (&eh)[NC], const uint32_t (&qr)[QW<NC>], LaneRow<NC>& r,
+                                               const int e_del, const int oe_del, const int e_ins, const int oe_ins) {
+  const uint32_t x = eh[J];
+  const int hp = (int)(x & 0xFFFFu);
+  const int e = (int)(x >> 16);
+  const uint32_t qo = (qr[J / 6] >> (5 * (J % 6))) & 31u;
+  const int s = field5(r.pack, qo);
+  const int M = hp ? hp + s : 0;
+  const int h = max(max(M, e), r.f);
+  r.key = max(r.key, ((uint32_t)h << 16) | (uint32_t)J);
+  int en, fn;
+  if constexpr (SYM) {
+    const int mo = M - oe_del;
+    en = max(max(e - e_del, mo), 0);
+    fn = max(max(r.f - e_del, mo), 0);
+  } else {
+    en = max(max(e - e_del, M - oe_del), 0);
+    fn = max(max(r.f - e_ins, M - oe_ins), 0);
+  }
+  r.f = fn;
+  const uint32_t xn = (uint32_t)r.h1 | ((uint32_t)en << 16);
+  eh[J] = xn;
+  r.h1 = h;
+  r.nz[J / 32] |= min(xn, 1u) << (J % 32);
+}
+
+template <int J, int NC, bool SYM>
+__device__ __forceinline__ void lane_cell(uint32_t (&eh)[NC], const uint32_t (&qr)[QW<NC>], LaneRow<NC>& r,
+                                          const bool work, const int e_del, const int oe_del, const int e_ins,
+                                          const int oe_ins) {
   if (work && J >= r.beg && J < r.end) {
     const uint32_t x = eh[J];
     const int hp = (int)(x & 0xFFFFu);
@@ -48,36 +84,51 @@ __device__ __forceinline__ void lane_cell(uint32_t (&eh)[NC], const uint32_t (&q
     const int s = field5(r.pack, qo);
     const int M = hp ? hp + s : 0;
     const int h = max(max(M, e), r.f);
-    r.mj = (h >= r.m) ? J : r.mj;  // ties go to the larger j
-    r.m = max(r.m, h);
-    const int en = max(max(e - e_del, M - oe_del), 0);
-    r.f = max(max(r.f - e_ins, M - oe_ins), 0);
+    r.key = max(r.key, ((uint32_t)h << 16) | (uint32_t)J);
+    int en, fn;
+    if constexpr (SYM) {  // o_del == o_ins and e_del == e_ins (bwa defaults)
+      const int mo = M - oe_del;
+      en = max(max(e - e_del, mo), 0);
+      fn = max(max(r.f - e_del, mo), 0);
+    } else {
+      en = max(max(e - e_del, M - oe_del), 0);
+      fn = max(max(r.f - e_ins, M - oe_ins), 0);
+    }
+    r.f = fn;
     const uint32_t xn = (uint32_t)r.h1 | ((uint32_t)en << 16);
     eh[J] = xn;
     r.h1 = h;
-    if (xn != 0u) {
-      r.last = J;
-      if (r.first > NC) r.first = J;
-    }
+    r.nz[J / 32] |= min(xn, 1u) << (J % 32);
   } else if (work && J == r.end) {
     eh[J] = (uint32_t)r.h1;  // eh[end] = {h1, 0}
-    if (r.h1 != 0) r.last = J;
+    r.nz[J / 32] |= min((uint32_t)r.h1, 1u) << (J % 32);
   }
 }
 
-template <int C, int NC>
-__device__ __forceinline__ void lane_chunk(uint32_t (&eh)[NC], const uint32_t (&qr)[QW<NC>], LaneRow& r, const bool work,
-                                           const int cmin, const int cmax, const int e_del, const int oe_del,
-                                           const int e_ins, const int oe_ins) {
+template <int C, int NC, bool SYM>
+__device__ __forceinline__ void lane_chunk(uint32_t (&eh)[NC], const uint32_t (&qr)[QW<NC>], LaneRow<NC>& r,
+                                           const bool work, const int cmin, const int cmax, const int e_del,
+                                           const int oe_del, const int e_ins, const int oe_ins) {
   constexpr int L = (NC - 16 * C) < 16 ? (NC - 16 * C) : 16;  // last chunk may be partial
   if (16 * C <= cmax && 16 * C + L - 1 >= cmin) {
-    [&]<int... S>(std::integer_sequence<int, S...>) {
-      (lane_cell<16 * C + S, NC>(eh, qr, r, work, e_del, oe_del, e_ins, oe_ins), ...);
-    }(std::make_integer_sequence<int, L>{});
+    // Fast path when the whole chunk lies strictly inside the band of every
+    // live lane (no per-column band test, no eh[end] write in this chunk).
+    const bool inside = !work || (r.beg <= 16 * C && 16 * C + L - 1 < r.end);
+    if (__ballot(!inside) == 0ull) {
+      if (work) {
+        [&]<int... S>(std::integer_sequence<int, S...>) {
+          (lane_cell_body<16 * C + S, NC, SYM>(eh, qr, r, e_del, oe_del, e_ins, oe_ins), ...);
+        }(std::make_integer_sequence<int, L>{});
+      }
+    } else {
+      [&]<int... S>(std::integer_sequence<int, S...>) {
+        (lane_cell<16 * C + S, NC, SYM>(eh, qr, r, work, e_del, oe_del, e_ins, oe_ins), ...);
+      }(std::make_integer_sequence<int, L>{});
+    }
   }
 }
 
-template <int NC>
+template <int NC, bool SYM>
 __global__ __launch_bounds__(64, 2) void bsw_lane_kernel(const BswDevBatch b, const BswParams p,
                                                       const int32_t* __restrict__ order,
                                                       const int64_t* __restrict__ bounds, const int bucket,
@@ -136,7 +187,7 @@ __global__ __launch_bounds__(64, 2) void bsw_lane_kernel(const BswDevBatch b, co
   int mx = h0, max_i = -1, max_j = -1, max_ie = -1, gscore = -1, max_off = 0;
   int ncell = 0;  // <= qlen * tlen < 2^31 in this envelope
   bool done = !has;
-  LaneRow r;
+  LaneRow<NC> r;
   r.beg = 0;
   r.end = qlen;
   int tcur = (tlen > 0) ? tg[0] : 0;
@@ -173,12 +224,11 @@ __global__ __launch_bounds__(64, 2) void bsw_lane_kernel(const BswDevBatch b, co
            : tb == 2 ? (uint32_t)p.matpack[2]
            : tb == 3 ? (uint32_t)p.matpack[3] : (uint32_t)p.matpack[4];
     r.f = 0;
-    r.m = 0;
-    r.mj = -1;
-    r.first = NC + 1;
-    r.last = -1;
+    r.key = 0;
+#pragma unroll
+    for (int k = 0; k < NZW<NC>; ++k) r.nz[k] = 0;
     [&]<int... C>(std::integer_sequence<int, C...>) {
-      (lane_chunk<C, NC>(eh, qr, r, work, cmin, cmax, e_del, oe_del, e_ins, oe_ins), ...);
+      (lane_chunk<C, NC, SYM>(eh, qr, r, work, cmin, cmax, e_del, oe_del, e_ins, oe_ins), ...);
     }(std::make_integer_sequence<int, (NC + 15) / 16>{});
     if (empty) {
       // bwa still stores eh[end] = {h1, 0}; the loop index equals beg here
@@ -197,22 +247,32 @@ __global__ __launch_bounds__(64, 2) void bsw_lane_kernel(const BswDevBatch b, co
         max_ie = gscore > r.h1 ? max_ie : i;
         gscore = gscore > r.h1 ? gscore : r.h1;
       }
-      if (r.m == 0) {
+      const int m = (int)(r.key >> 16), mj = (int)(r.key & 0xFFFFu);
+      if (m == 0) {
         done = true;
-      } else if (r.m > mx) {
-        mx = r.m, max_i = i, max_j = r.mj;
-        const int d = r.mj > i ? r.mj - i : i - r.mj;
+      } else if (m > mx) {
+        mx = m, max_i = i, max_j = mj;
+        const int d = mj > i ? mj - i : i - mj;
         max_off = max_off > d ? max_off : d;
       } else if (p.zdrop > 0) {
-        if (i - max_i > r.mj - max_j) {
-          if (mx - r.m - ((i - max_i) - (r.mj - max_j)) * e_del > p.zdrop) done = true;
+        if (i - max_i > mj - max_j) {
+          if (mx - m - ((i - max_i) - (mj - max_j)) * e_del > p.zdrop) done = true;
         } else {
-          if (mx - r.m - ((r.mj - max_j) - (i - max_i)) * e_ins > p.zdrop) done = true;
+          if (mx - m - ((mj - max_j) - (i - max_i)) * e_ins > p.zdrop) done = true;
         }
       }
       if (!done) {
-        r.beg = (r.first <= NC) ? r.first : r.end;
-        r.end = (r.last >= 0) ? min(r.last + 2, qlen) : min(r.beg + 1, qlen);
+        // bwa's trims: first non-zero eh in [beg, end) (else end), last non-zero
+        // in [beg', end]; the bitmap holds exactly the entries written this row
+        int first = -1, last = -1;
+#pragma unroll
+        for (int k = 0; k < NZW<NC>; ++k) {
+          const uint32_t wbits = r.nz[k];
+          if (first < 0 && wbits) first = 32 * k + __builtin_ctz(wbits);
+          if (wbits) last = 32 * k + 31 - __builtin_clz(wbits);
+        }
+        r.beg = (first >= 0) ? first : r.end;
+        r.end = (last >= 0) ? min(last + 2, qlen) : min(r.beg + 1, qlen);
       }
     }
   }
@@ -276,13 +336,21 @@ int launch_bsw_extend_sorted(const BswDevBatch& b, const BswParams& p, int max_q
                      (long long)b.n, ws.bounds);
   FCS_HIP_CHECK(hipGetLastError());
   const unsigned g = (unsigned)((b.n + 63) / 64);
-  hipLaunchKernelGGL(bsw_lane_kernel<16>, dim3(g), dim3(64), 0, s, b, p, ws.idx_out, ws.bounds, 0, res, cells);
-  hipLaunchKernelGGL(bsw_lane_kernel<32>, dim3(g), dim3(64), 0, s, b, p, ws.idx_out, ws.bounds, 1, res, cells);
-  hipLaunchKernelGGL(bsw_lane_kernel<48>, dim3(g), dim3(64), 0, s, b, p, ws.idx_out, ws.bounds, 2, res, cells);
-  hipLaunchKernelGGL(bsw_lane_kernel<64>, dim3(g), dim3(64), 0, s, b, p, ws.idx_out, ws.bounds, 3, res, cells);
-  hipLaunchKernelGGL(bsw_lane_kernel<96>, dim3(g), dim3(64), 0, s, b, p, ws.idx_out, ws.bounds, 4, res, cells);
-  hipLaunchKernelGGL(bsw_lane_kernel<128>, dim3(g), dim3(64), 0, s, b, p, ws.idx_out, ws.bounds, 5, res, cells);
-  hipLaunchKernelGGL(bsw_lane_kernel<152>, dim3(g), dim3(64), 0, s, b, p, ws.idx_out, ws.bounds, 6, res, cells);
+  const bool sym = p.o_del == p.o_ins && p.e_del == p.e_ins;
+  auto lanes = [&](auto sym_tag) {
+    constexpr bool SYM = decltype(sym_tag)::value;
+    hipLaunchKernelGGL((bsw_lane_kernel<16, SYM>), dim3(g), dim3(64), 0, s, b, p, ws.idx_out, ws.bounds, 0, res, cells);
+    hipLaunchKernelGGL((bsw_lane_kernel<32, SYM>), dim3(g), dim3(64), 0, s, b, p, ws.idx_out, ws.bounds, 1, res, cells);
+    hipLaunchKernelGGL((bsw_lane_kernel<48, SYM>), dim3(g), dim3(64), 0, s, b, p, ws.idx_out, ws.bounds, 2, res, cells);
+    hipLaunchKernelGGL((bsw_lane_kernel<64, SYM>), dim3(g), dim3(64), 0, s, b, p, ws.idx_out, ws.bounds, 3, res, cells);
+    hipLaunchKernelGGL((bsw_lane_kernel<96, SYM>), dim3(g), dim3(64), 0, s, b, p, ws.idx_out, ws.bounds, 4, res, cells);
+    hipLaunchKernelGGL((bsw_lane_kernel<128, SYM>), dim3(g), dim3(64), 0, s, b, p, ws.idx_out, ws.bounds, 5, res,
+                       cells);
+    hipLaunchKernelGGL((bsw_lane_kernel<152, SYM>), dim3(g), dim3(64), 0, s, b, p, ws.idx_out, ws.bounds, 6, res,
+                       cells);
+  };
+  if (sym) lanes(std::true_type{});
+  else lanes(std::false_type{});
   FCS_HIP_CHECK(hipGetLastError());
   // bucket 7: wave-per-task kernel over the sorted tail
   return launch_bsw_extend_wide(b, p, max_qlen, max_tlen, res, cells, ws.idx_out, ws.bounds, s);
