@@ -16,6 +16,7 @@
 // wave-wide min/max per row), and lanes whose task ended idle under EXEC.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <type_traits>
 #include <utility>
 
@@ -128,14 +129,11 @@ __device__ __forceinline__ void lane_chunk(uint32_t (&eh)[NC], const uint32_t (&
   }
 }
 
+// 64 consecutive tasks of the sorted schedule, starting at `base`.
 template <int NC, bool SYM>
-__global__ __launch_bounds__(64, 2) void bsw_lane_kernel(const BswDevBatch b, const BswParams p,
-                                                      const int32_t* __restrict__ order,
-                                                      const int64_t* __restrict__ bounds, const int bucket,
-                                                      int32_t* __restrict__ res, int64_t* __restrict__ cells_out) {
-  const long long lo = bounds[bucket], hi = bounds[bucket + 1];
-  const long long base = lo + 64LL * blockIdx.x;
-  if (base >= hi) return;
+__device__ __forceinline__ void lane_wave(const BswDevBatch& b, const BswParams& p, const int32_t* __restrict__ order,
+                                          const long long base, const long long hi, int32_t* __restrict__ res,
+                                          int64_t* __restrict__ cells_out) {
   const int lane = threadIdx.x;
   const long long k = base + lane;
   const bool has = k < hi;
@@ -288,6 +286,18 @@ __global__ __launch_bounds__(64, 2) void bsw_lane_kernel(const BswDevBatch b, co
   }
 }
 
+// One launch per bucket; the grid strides over the bucket's range so empty
+// buckets cost a few hundred idle workgroups, not n/64.
+template <int NC, bool SYM>
+__global__ __launch_bounds__(64, 2) void bsw_lane_kernel(const BswDevBatch b, const BswParams p,
+                                                      const int32_t* __restrict__ order,
+                                                      const int64_t* __restrict__ bounds, const int bucket,
+                                                      int32_t* __restrict__ res, int64_t* __restrict__ cells_out) {
+  const long long lo = bounds[bucket], hi = bounds[bucket + 1];
+  for (long long base = lo + 64LL * blockIdx.x; base < hi; base += 64LL * gridDim.x)
+    lane_wave<NC, SYM>(b, p, order, base, hi, res, cells_out);
+}
+
 // Bucket of a task: 0..6 = lane kernel with 16/32/48/64/96/128/152 register
 // columns (152 = bwa reads up to 151 bp), 7 = wave-per-task kernel (long queries or out-of-int16 scores).
 __device__ __forceinline__ int bsw_bucket(int qlen, int h0, const BswParams& p) {
@@ -335,7 +345,9 @@ int launch_bsw_extend_sorted(const BswDevBatch& b, const BswParams& p, int max_q
   hipLaunchKernelGGL(bsw_bounds_kernel, dim3((unsigned)((b.n + 1 + bs - 1) / bs)), dim3(bs), 0, s, ws.keys_out,
                      (long long)b.n, ws.bounds);
   FCS_HIP_CHECK(hipGetLastError());
-  const unsigned g = (unsigned)((b.n + 63) / 64);
+  // 8192 workgroups = 4 rounds of the 2048 resident waves (2 per SIMD): caps
+  // the cost of an empty bucket and still leaves the dispatcher a tail to balance
+  const unsigned g = (unsigned)std::min<long long>((b.n + 63) / 64, 8192);
   const bool sym = p.o_del == p.o_ins && p.e_del == p.e_ins;
   auto lanes = [&](auto sym_tag) {
     constexpr bool SYM = decltype(sym_tag)::value;
