@@ -242,7 +242,7 @@ def main():
 
     if not args.no_bsw and rank == 0:
         c3 = fcship.synth_bsw(args.seed, args.bsw_reads, read_len=151, ref_len=10_000_000, w=100)
-        fx = fcship.synth_bsw(args.seed, max(1, args.bsw_reads // 4), read_len=151, ref_len=10_000_000, w=100,
+        fx = fcship.synth_bsw(args.seed, max(1, args.bsw_reads * 2), read_len=151, ref_len=10_000_000, w=100,
                               mode=1, fixed_q=151, fixed_t=251)
         r3 = bench_bsw(args, dev, c3)
         rf = bench_bsw(args, dev, fx)

@@ -349,23 +349,31 @@ int launch_bsw_extend_sorted(const BswDevBatch& b, const BswParams& p, int max_q
   // the cost of an empty bucket and still leaves the dispatcher a tail to balance
   const unsigned g = (unsigned)std::min<long long>((b.n + 63) / 64, 8192);
   const bool sym = p.o_del == p.o_ins && p.e_del == p.e_ins;
+  // The eight bucket kernels are independent (disjoint task ranges).  A bwa
+  // batch spreads over all of them, so each alone is ~one round of waves and
+  // its tail would idle the chip: fork them over kForkStreams streams,
+  // largest columns first, so small buckets fill the large ones' tails.
+  hipStream_t fs[kForkStreams];
+  if (const int rc = fork_streams(s, fs); rc != FCS_OK) return rc;
   auto lanes = [&](auto sym_tag) {
     constexpr bool SYM = decltype(sym_tag)::value;
-    hipLaunchKernelGGL((bsw_lane_kernel<16, SYM>), dim3(g), dim3(64), 0, s, b, p, ws.idx_out, ws.bounds, 0, res, cells);
-    hipLaunchKernelGGL((bsw_lane_kernel<32, SYM>), dim3(g), dim3(64), 0, s, b, p, ws.idx_out, ws.bounds, 1, res, cells);
-    hipLaunchKernelGGL((bsw_lane_kernel<48, SYM>), dim3(g), dim3(64), 0, s, b, p, ws.idx_out, ws.bounds, 2, res, cells);
-    hipLaunchKernelGGL((bsw_lane_kernel<64, SYM>), dim3(g), dim3(64), 0, s, b, p, ws.idx_out, ws.bounds, 3, res, cells);
-    hipLaunchKernelGGL((bsw_lane_kernel<96, SYM>), dim3(g), dim3(64), 0, s, b, p, ws.idx_out, ws.bounds, 4, res, cells);
-    hipLaunchKernelGGL((bsw_lane_kernel<128, SYM>), dim3(g), dim3(64), 0, s, b, p, ws.idx_out, ws.bounds, 5, res,
-                       cells);
-    hipLaunchKernelGGL((bsw_lane_kernel<152, SYM>), dim3(g), dim3(64), 0, s, b, p, ws.idx_out, ws.bounds, 6, res,
-                       cells);
+    const int32_t* o = ws.idx_out;
+    const int64_t* bd = ws.bounds;
+    hipLaunchKernelGGL((bsw_lane_kernel<152, SYM>), dim3(g), dim3(64), 0, fs[0], b, p, o, bd, 6, res, cells);
+    hipLaunchKernelGGL((bsw_lane_kernel<128, SYM>), dim3(g), dim3(64), 0, fs[1], b, p, o, bd, 5, res, cells);
+    hipLaunchKernelGGL((bsw_lane_kernel<96, SYM>), dim3(g), dim3(64), 0, fs[2], b, p, o, bd, 4, res, cells);
+    hipLaunchKernelGGL((bsw_lane_kernel<64, SYM>), dim3(g), dim3(64), 0, fs[3], b, p, o, bd, 3, res, cells);
+    hipLaunchKernelGGL((bsw_lane_kernel<48, SYM>), dim3(g), dim3(64), 0, fs[3], b, p, o, bd, 2, res, cells);
+    hipLaunchKernelGGL((bsw_lane_kernel<32, SYM>), dim3(g), dim3(64), 0, fs[2], b, p, o, bd, 1, res, cells);
+    hipLaunchKernelGGL((bsw_lane_kernel<16, SYM>), dim3(g), dim3(64), 0, fs[1], b, p, o, bd, 0, res, cells);
   };
   if (sym) lanes(std::true_type{});
   else lanes(std::false_type{});
   FCS_HIP_CHECK(hipGetLastError());
   // bucket 7: wave-per-task kernel over the sorted tail
-  return launch_bsw_extend_wide(b, p, max_qlen, max_tlen, res, cells, ws.idx_out, ws.bounds, s);
+  const int rc = launch_bsw_extend_wide(b, p, max_qlen, max_tlen, res, cells, ws.idx_out, ws.bounds, fs[0]);
+  if (rc != FCS_OK) return rc;
+  return join_streams(s, fs);
 }
 
 }  // namespace fcs

@@ -52,6 +52,54 @@ hipStream_t thread_stream(int device) {
   return s;
 }
 
+struct ForkSet {
+  hipStream_t side[kForkStreams - 1] = {};
+  hipEvent_t fork = nullptr;
+  hipEvent_t join[kForkStreams - 1] = {};
+};
+
+// Side streams and events of the calling thread on the current device.
+ForkSet* fork_set() {
+  int device = 0;
+  if (hipGetDevice(&device) != hipSuccess) return nullptr;
+  static thread_local std::map<int, ForkSet> sets;
+  auto it = sets.find(device);
+  if (it != sets.end()) return &it->second;
+  ForkSet f;
+  if (hipEventCreateWithFlags(&f.fork, hipEventDisableTiming) != hipSuccess) return nullptr;
+  for (int i = 0; i < kForkStreams - 1; ++i)
+    if (hipStreamCreateWithFlags(&f.side[i], hipStreamNonBlocking) != hipSuccess ||
+        hipEventCreateWithFlags(&f.join[i], hipEventDisableTiming) != hipSuccess)
+      return nullptr;
+  return &(sets[device] = f);
+}
+
+}  // namespace
+
+int fork_streams(hipStream_t s, hipStream_t (&fs)[kForkStreams]) {
+  ForkSet* f = fork_set();
+  if (!f) return fail(FCS_ERR_DEVICE, "[E::fcship] cannot create side streams");
+  FCS_HIP_CHECK(hipEventRecord(f->fork, s));
+  fs[0] = s;
+  for (int i = 0; i < kForkStreams - 1; ++i) {
+    FCS_HIP_CHECK(hipStreamWaitEvent(f->side[i], f->fork, 0));
+    fs[i + 1] = f->side[i];
+  }
+  return FCS_OK;
+}
+
+int join_streams(hipStream_t s, const hipStream_t (&fs)[kForkStreams]) {
+  ForkSet* f = fork_set();
+  if (!f) return fail(FCS_ERR_DEVICE, "[E::fcship] cannot create side streams");
+  for (int i = 0; i < kForkStreams - 1; ++i) {
+    FCS_HIP_CHECK(hipEventRecord(f->join[i], fs[i + 1]));
+    FCS_HIP_CHECK(hipStreamWaitEvent(s, f->join[i], 0));
+  }
+  return FCS_OK;
+}
+
+namespace {
+
 // RAII device buffer for the synchronous paths.
 struct DevBuf {
   void* p = nullptr;

@@ -117,6 +117,15 @@ int get_device_tables(int device, DeviceTables** out);
 void build_phmm_tables_f(float* ph2pr, float* dmatch, float* dmis, float* mm);
 void build_phmm_tables_d(double* ph2pr, double* dmatch, double* dmis, double* mm);
 
+// ------------------------------------------------------------ stream fork/join
+// fs[0] = s itself; fs[1..] are per-(thread, device) side streams that wait
+// for everything already queued on s.  join_streams makes s wait for them.
+// Both are pure stream-ordered event operations (no host sync), so they also
+// work inside a hipGraph stream capture.
+constexpr int kForkStreams = 4;
+int fork_streams(hipStream_t s, hipStream_t (&fs)[kForkStreams]);
+int join_streams(hipStream_t s, const hipStream_t (&fs)[kForkStreams]);
+
 // ------------------------------------------------------------ kernel launchers
 int launch_phmm_keys(const PhmmDevBatch& b, uint32_t* keys, int32_t* idx, hipStream_t s);
 int launch_phmm_forward(const PhmmDevBatch& b, const int32_t* order, int64_t count, int max_hap_len,
