@@ -236,8 +236,10 @@ int launch_bsw_extend_wide(const BswDevBatch& b, const BswParams& p, int max_qle
   if (max_qlen > 1023) return fail(FCS_ERR_UNSUPPORTED, "[E::fcship] ksw_extend2: qlen > 1023 unsupported");
   const size_t lds = (size_t)((max_tlen + 64 + 15) / 16) * 16;
   if (lds > 64 * 1024) return fail(FCS_ERR_UNSUPPORTED, "[E::fcship] ksw_extend2: tlen too large");
+  // grid-stride over the sorted tail; 2048 waves (2 per SIMD) fill the chip,
+  // and an empty tail (the common bwa case) costs only that many exits
   long long grid = b.n;
-  const long long cap = 256LL * 64;
+  const long long cap = 2048;
   if (grid > cap) grid = cap;
   if (max_qlen <= 255)
     hipLaunchKernelGGL(bsw_extend_kernel<4>, dim3((unsigned)grid), dim3(64), lds, s, b, p, res, cells, order, bounds);
@@ -414,8 +416,10 @@ int launch_bsw_global(const BswDevBatch& b, const BswParams& p, int max_qlen, in
   if (zbuf && zbytes > 0) FCS_HIP_CHECK(hipMemsetAsync(zbuf, 0, (size_t)zbytes, s));
   const size_t lds = (size_t)((max_tlen + 64 + 15) / 16) * 16;
   if (lds > 64 * 1024) return fail(FCS_ERR_UNSUPPORTED, "[E::fcship] ksw_global2: tlen too large");
+  // grid-stride over the sorted tail; 2048 waves (2 per SIMD) fill the chip,
+  // and an empty tail (the common bwa case) costs only that many exits
   long long grid = b.n;
-  const long long cap = 256LL * 64;
+  const long long cap = 2048;
   if (grid > cap) grid = cap;
   if (max_qlen <= 255)
     hipLaunchKernelGGL(bsw_global_kernel<4>, dim3((unsigned)grid), dim3(64), lds, s, b, p, scores, zbuf, zoff);

@@ -29,10 +29,24 @@ __device__ __forceinline__ int wave_min_i(int v) { return -wave_max(-v); }
 // registers holding the per-column query offsets (q * 5), six 5-bit fields each
 template <int NC> constexpr int QW = (NC + 5) / 6;
 
-// Signed 5-bit field at bit offset `off` of `pack`.
-__device__ __forceinline__ int field5(uint32_t pack, uint32_t off) {
-  return ((int)((pack >> off) << 27)) >> 27;
+// Signed 5-bit field at bit offset `off` of `pack` (one v_bfe_i32).
+__device__ __forceinline__ int field5(uint32_t pack, uint32_t off) { return __builtin_amdgcn_sbfe(pack, off, 5); }
+
+// nz | (x != 0) << sh as v_min_u32 + v_lshl_or_b32 (the compiler's own
+// cmp/cndmask/or form costs one more VALU op per cell).
+template <int SH>
+__device__ __forceinline__ uint32_t or_nz_bit(uint32_t nz, uint32_t x) {
+  uint32_t t, r;
+  asm("v_min_u32 %0, %1, 1" : "=v"(t) : "v"(x));
+  asm("v_lshl_or_b32 %0, %1, %2, %3" : "=v"(r) : "v"(t), "i"(SH), "v"(nz));
+  return r;
 }
+
+// bwa's `M = M ? M + q[j] : 0` as min(hp + s, 32 hp): identical whenever hp > 0
+// (s <= 15 < 31 hp), and <= 0 when hp == 0, where every consumer (max with
+// e, f >= 0; max(M - oe, 0)) treats it exactly like 0.  No VCC select, so no
+// VALU-writes-VCC hazard nops either.
+__device__ __forceinline__ int diag_m(int hp, int s) { return min(hp + s, hp << 5); }
 
 // Words of the per-row "eh[j] != 0" bitmap (bit j for column j).
 template <int NC> constexpr int NZW = (NC + 31) / 32;
@@ -45,20 +59,26 @@ struct LaneRow {
   uint32_t nz[NZW<NC>];
 };
 
-// One in-band cell (bwa's inner-loop body).
-template <int J, int NC, bool SYM>
-__device__ __forceinline__ void lane_cell_body(uint32_t (&eh)[NC], const uint32_t (&qr)[QW<NC>], LaneRow<NC>& r,
-                                               const int e_del, const int oe_del, const int e_ins, const int oe_ins) {
+// bwa's inner-loop body for column J.  MASKED = false: every working lane has
+// J inside [beg, end).  MASKED = true (a chunk crossing some lane's band
+// edge): the body runs unconditionally and bit J of `bm` (low half: J in
+// [beg, end); high half: J in [beg, end]) selects what it may change, with
+// sign-extended 1-bit masks and bit-selects instead of branches: eh[J] only
+// for J in [beg, end] (at J == end bwa stores {h1, 0}), h1 / f / the row key
+// only for J in [beg, end).  Lanes not working this row have bm = 0.
+template <int J, int NC, bool SYM, bool MASKED>
+__device__ __forceinline__ void lane_cell(uint32_t (&eh)[NC], const uint32_t (&qr)[QW<NC>], LaneRow<NC>& r,
+                                          const uint32_t bm, const int e_del, const int oe_del, const int e_ins,
+                                          const int oe_ins) {
   const uint32_t x = eh[J];
   const int hp = (int)(x & 0xFFFFu);
   const int e = (int)(x >> 16);
-  const uint32_t qo = (qr[J / 6] >> (5 * (J % 6))) & 31u;
+  const uint32_t qo = __builtin_amdgcn_ubfe(qr[J / 6], 5 * (J % 6), 5);
   const int s = field5(r.pack, qo);
-  const int M = hp ? hp + s : 0;
+  const int M = diag_m(hp, s);
   const int h = max(max(M, e), r.f);
-  r.key = max(r.key, ((uint32_t)h << 16) | (uint32_t)J);
   int en, fn;
-  if constexpr (SYM) {
+  if constexpr (SYM) {  // o_del == o_ins and e_del == e_ins (bwa defaults)
     const int mo = M - oe_del;
     en = max(max(e - e_del, mo), 0);
     fn = max(max(r.f - e_del, mo), 0);
@@ -66,44 +86,32 @@ __device__ __forceinline__ void lane_cell_body(uint32_t (&eh)[NC], const uint32_
     en = max(max(e - e_del, M - oe_del), 0);
     fn = max(max(r.f - e_ins, M - oe_ins), 0);
   }
-  r.f = fn;
-  const uint32_t xn = (uint32_t)r.h1 | ((uint32_t)en << 16);
-  eh[J] = xn;
-  r.h1 = h;
-  r.nz[J / 32] |= min(xn, 1u) << (J % 32);
-}
-
-template <int J, int NC, bool SYM>
-__device__ __forceinline__ void lane_cell(uint32_t (&eh)[NC], const uint32_t (&qr)[QW<NC>], LaneRow<NC>& r,
-                                          const bool work, const int e_del, const int oe_del, const int e_ins,
-                                          const int oe_ins) {
-  if (work && J >= r.beg && J < r.end) {
-    const uint32_t x = eh[J];
-    const int hp = (int)(x & 0xFFFFu);
-    const int e = (int)(x >> 16);
-    const uint32_t qo = (qr[J / 6] >> (5 * (J % 6))) & 31u;
-    const int s = field5(r.pack, qo);
-    const int M = hp ? hp + s : 0;
-    const int h = max(max(M, e), r.f);
+  if constexpr (!MASKED) {
     r.key = max(r.key, ((uint32_t)h << 16) | (uint32_t)J);
-    int en, fn;
-    if constexpr (SYM) {  // o_del == o_ins and e_del == e_ins (bwa defaults)
-      const int mo = M - oe_del;
-      en = max(max(e - e_del, mo), 0);
-      fn = max(max(r.f - e_del, mo), 0);
-    } else {
-      en = max(max(e - e_del, M - oe_del), 0);
-      fn = max(max(r.f - e_ins, M - oe_ins), 0);
-    }
     r.f = fn;
     const uint32_t xn = (uint32_t)r.h1 | ((uint32_t)en << 16);
     eh[J] = xn;
     r.h1 = h;
-    r.nz[J / 32] |= min(xn, 1u) << (J % 32);
-  } else if (work && J == r.end) {
-    eh[J] = (uint32_t)r.h1;  // eh[end] = {h1, 0}
-    r.nz[J / 32] |= min((uint32_t)r.h1, 1u) << (J % 32);
+    r.nz[J / 32] = or_nz_bit<J % 32>(r.nz[J / 32], xn);
+  } else {
+    const uint32_t ms = (uint32_t)__builtin_amdgcn_sbfe(bm, J % 16, 1);       // J in [beg, end)
+    const uint32_t mx = (uint32_t)__builtin_amdgcn_sbfe(bm, 16 + J % 16, 1);  // J in [beg, end]
+    // a masked-off h contributes (0 << 16 | J): below any positive row max,
+    // and a zero row max ends the task before its arg-max is used
+    r.key = max(r.key, (((uint32_t)h & ms) << 16) | (uint32_t)J);
+    r.f = (int)(((uint32_t)fn & ms) | ((uint32_t)r.f & ~ms));
+    const uint32_t xn = (uint32_t)r.h1 | (((uint32_t)en & ms) << 16);
+    const uint32_t xo = (xn & mx) | (x & ~mx);
+    eh[J] = xo;
+    r.h1 = (int)(((uint32_t)h & ms) | ((uint32_t)r.h1 & ~ms));
+    r.nz[J / 32] = or_nz_bit<J % 32>(r.nz[J / 32], xo);  // bits outside [beg, end] are masked after the row
   }
+}
+
+// Bits [lo, hi) of a 16-column chunk starting at column c0, clamped.
+__device__ __forceinline__ uint32_t chunk_bits(int lo, int hi, int c0) {
+  const int a = min(max(lo - c0, 0), 16), b = min(max(hi - c0, 0), 16);
+  return ((1u << b) - 1u) & ~((1u << a) - 1u);
 }
 
 template <int C, int NC, bool SYM>
@@ -118,12 +126,14 @@ __device__ __forceinline__ void lane_chunk(uint32_t (&eh)[NC], const uint32_t (&
     if (__ballot(!inside) == 0ull) {
       if (work) {
         [&]<int... S>(std::integer_sequence<int, S...>) {
-          (lane_cell_body<16 * C + S, NC, SYM>(eh, qr, r, e_del, oe_del, e_ins, oe_ins), ...);
+          (lane_cell<16 * C + S, NC, SYM, false>(eh, qr, r, 0u, e_del, oe_del, e_ins, oe_ins), ...);
         }(std::make_integer_sequence<int, L>{});
       }
     } else {
+      const uint32_t bm =
+          work ? (chunk_bits(r.beg, r.end, 16 * C) | (chunk_bits(r.beg, r.end + 1, 16 * C) << 16)) : 0u;
       [&]<int... S>(std::integer_sequence<int, S...>) {
-        (lane_cell<16 * C + S, NC, SYM>(eh, qr, r, work, e_del, oe_del, e_ins, oe_ins), ...);
+        (lane_cell<16 * C + S, NC, SYM, true>(eh, qr, r, bm, e_del, oe_del, e_ins, oe_ins), ...);
       }(std::make_integer_sequence<int, L>{});
     }
   }
@@ -261,11 +271,14 @@ __device__ __forceinline__ void lane_wave(const BswDevBatch& b, const BswParams&
       }
       if (!done) {
         // bwa's trims: first non-zero eh in [beg, end) (else end), last non-zero
-        // in [beg', end]; the bitmap holds exactly the entries written this row
+        // in [beg', end]; bits are kept for [beg, end] only, the entries bwa wrote this row
         int first = -1, last = -1;
 #pragma unroll
         for (int k = 0; k < NZW<NC>; ++k) {
-          const uint32_t wbits = r.nz[k];
+          // keep bits of [beg, end] only (masked chunks also set bits for untouched entries)
+          const int a = min(max(r.beg - 32 * k, 0), 32), z = min(max(r.end + 1 - 32 * k, 0), 32);
+          const uint32_t keep = (z >= 32 ? ~0u : ((1u << z) - 1u)) & (a >= 32 ? 0u : ~((1u << a) - 1u));
+          const uint32_t wbits = r.nz[k] & keep;
           if (first < 0 && wbits) first = 32 * k + __builtin_ctz(wbits);
           if (wbits) last = 32 * k + 31 - __builtin_clz(wbits);
         }

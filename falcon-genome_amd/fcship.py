@@ -20,7 +20,7 @@ except ImportError:  # pragma: no cover - torch is optional plumbing
     torch = None
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "libfcship.so")
+LIB_PATH = os.environ.get("FCSHIP_LIB") or os.path.join(HERE, "libfcship.so")  # override: A/B builds
 HEADER_PATH = os.path.join(os.path.dirname(HERE), "include", "fcship.h")
 
 if not os.path.exists(LIB_PATH):

@@ -1,0 +1,44 @@
+"""SW-only timing for profiling runs: the two ksw_extend2 workloads of bench.py
+(C3 seed extensions and the fixed 151x251 case), nothing else on the GPU.
+
+usage: python tools/bsw_bench.py [--reads N] [--which c3|fixed|both]
+"""
+import argparse
+import json
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, "falcon-genome_amd"))
+
+import torch  # noqa: E402  (first: one HIP runtime per process)
+
+import bench  # noqa: E402
+import fcship  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--reads", type=int, default=500_000)
+    ap.add_argument("--seed", type=int, default=20261015)
+    ap.add_argument("--which", default="both", choices=["c3", "fixed", "both"])
+    ap.add_argument("--reps", type=int, default=3)
+    args = ap.parse_args()
+    dev = torch.device("cuda", 0)
+    torch.cuda.set_device(dev)
+    out = {}
+    if args.which in ("c3", "both"):
+        t = fcship.synth_bsw(args.seed, args.reads, read_len=151, ref_len=10_000_000, w=100)
+        r = bench.bench_bsw(args, dev, t, reps=args.reps)
+        out["c3"] = {k: (round(v, 3) if isinstance(v, float) else v) for k, v in r.items()}
+    if args.which in ("fixed", "both"):
+        t = fcship.synth_bsw(args.seed, 2 * args.reads, read_len=151, ref_len=10_000_000, w=100, mode=1,
+                             fixed_q=151, fixed_t=251)
+        r = bench.bench_bsw(args, dev, t, reps=args.reps)
+        out["fixed"] = {k: (round(v, 3) if isinstance(v, float) else v) for k, v in r.items()}
+    print(json.dumps(out))
+
+
+if __name__ == "__main__":
+    main()
