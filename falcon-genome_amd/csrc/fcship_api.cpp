@@ -497,43 +497,74 @@ int fcs_phmm_compute(const fcs_phmm_read* reads, int32_t n_reads, const fcs_phmm
     return fail(FCS_ERR_INVALID, "[E::fcs_phmm_compute] bad arguments");
   if ((int64_t)n_reads * n_haps == 0) return FCS_OK;
   if (!out_log10) return fail(FCS_ERR_INVALID, "[E::fcs_phmm_compute] null output");
-  std::vector<int64_t> roff(n_reads), hoff(n_haps);
-  std::vector<int32_t> rlen(n_reads), hlen(n_haps);
-  int64_t rt = 0, ht = 0;
-  for (int32_t r = 0; r < n_reads; ++r) {
-    if (reads[r].len < 0 || (reads[r].len > 0 && (!reads[r].bases || !reads[r].base_q || !reads[r].ins_q ||
-                                                  !reads[r].del_q || !reads[r].gcp)))
-      return fail(FCS_ERR_INVALID, "[E::fcs_phmm_compute] malformed read");
-    roff[r] = rt;
-    rlen[r] = reads[r].len;
-    rt += reads[r].len;
-  }
-  for (int32_t h = 0; h < n_haps; ++h) {
-    if (haps[h].len < 0 || (haps[h].len > 0 && !haps[h].bases))
-      return fail(FCS_ERR_INVALID, "[E::fcs_phmm_compute] malformed haplotype");
-    hoff[h] = ht;
-    hlen[h] = haps[h].len;
-    ht += haps[h].len;
-  }
-  std::vector<uint8_t> rb(rt), bq(rt), iq(rt), dq(rt), gq(rt), hb(ht);
-  for (int32_t r = 0; r < n_reads; ++r) {
-    const size_t L = reads[r].len;
-    if (!L) continue;
-    std::memcpy(&rb[roff[r]], reads[r].bases, L);
-    std::memcpy(&bq[roff[r]], reads[r].base_q, L);
-    std::memcpy(&iq[roff[r]], reads[r].ins_q, L);
-    std::memcpy(&dq[roff[r]], reads[r].del_q, L);
-    std::memcpy(&gq[roff[r]], reads[r].gcp, L);
-  }
-  for (int32_t h = 0; h < n_haps; ++h)
-    if (haps[h].len) std::memcpy(&hb[hoff[h]], haps[h].bases, haps[h].len);
-  const int64_t np = (int64_t)n_reads * n_haps;
-  std::vector<int32_t> pr(np), ph(np);
-  for (int32_t r = 0, k = 0; r < n_reads; ++r)
-    for (int32_t h = 0; h < n_haps; ++h, ++k) {
-      pr[k] = r;
-      ph[k] = h;
+  fcs_phmm_region r{reads, n_reads, haps, n_haps, out_log10};
+  return fcs_phmm_compute_regions(&r, 1, opts);
+}
+
+// Many active regions in one device pass: the regions' reads and haplotypes
+// are concatenated into one SoA batch whose pair list is region-major and
+// read-major within a region, so the flat result splits back into each
+// region's read-major matrix by a running offset.
+int fcs_phmm_compute_regions(const fcs_phmm_region* regions, int32_t n_regions, const fcs_phmm_opts* opts) {
+  if (n_regions < 0 || (n_regions > 0 && !regions))
+    return fail(FCS_ERR_INVALID, "[E::fcs_phmm_compute_regions] bad arguments");
+  int64_t nr = 0, nh = 0, np = 0, rt = 0, ht = 0;
+  for (int32_t g = 0; g < n_regions; ++g) {
+    const fcs_phmm_region& R = regions[g];
+    if (R.n_reads < 0 || R.n_haps < 0 || (R.n_reads > 0 && !R.reads) || (R.n_haps > 0 && !R.haps))
+      return fail(FCS_ERR_INVALID, "[E::fcs_phmm_compute_regions] malformed region");
+    const int64_t pairs = (int64_t)R.n_reads * R.n_haps;
+    if (pairs > 0 && !R.out_log10) return fail(FCS_ERR_INVALID, "[E::fcs_phmm_compute_regions] null region output");
+    for (int32_t r = 0; r < R.n_reads; ++r) {
+      const fcs_phmm_read& x = R.reads[r];
+      if (x.len < 0 || (x.len > 0 && (!x.bases || !x.base_q || !x.ins_q || !x.del_q || !x.gcp)))
+        return fail(FCS_ERR_INVALID, "[E::fcs_phmm_compute_regions] malformed read");
+      rt += x.len;
     }
+    for (int32_t h = 0; h < R.n_haps; ++h) {
+      if (R.haps[h].len < 0 || (R.haps[h].len > 0 && !R.haps[h].bases))
+        return fail(FCS_ERR_INVALID, "[E::fcs_phmm_compute_regions] malformed haplotype");
+      ht += R.haps[h].len;
+    }
+    nr += R.n_reads;
+    nh += R.n_haps;
+    np += pairs;
+  }
+  if (np == 0) return FCS_OK;
+  if (nr > INT32_MAX || nh > INT32_MAX)
+    return fail(FCS_ERR_INVALID, "[E::fcs_phmm_compute_regions] more than 2^31 reads or haplotypes");
+  std::vector<int64_t> roff(nr), hoff(nh);
+  std::vector<int32_t> rlen(nr), hlen(nh), pr(np), ph(np);
+  std::vector<uint8_t> rb(rt), bq(rt), iq(rt), dq(rt), gq(rt), hb(ht);
+  int64_t ri = 0, hi = 0, pi = 0, ro = 0, ho = 0;
+  for (int32_t g = 0; g < n_regions; ++g) {
+    const fcs_phmm_region& R = regions[g];
+    const int64_t r0 = ri, h0 = hi;
+    for (int32_t r = 0; r < R.n_reads; ++r, ++ri) {
+      const fcs_phmm_read& x = R.reads[r];
+      roff[ri] = ro;
+      rlen[ri] = x.len;
+      if (x.len) {
+        std::memcpy(&rb[ro], x.bases, x.len);
+        std::memcpy(&bq[ro], x.base_q, x.len);
+        std::memcpy(&iq[ro], x.ins_q, x.len);
+        std::memcpy(&dq[ro], x.del_q, x.len);
+        std::memcpy(&gq[ro], x.gcp, x.len);
+      }
+      ro += x.len;
+    }
+    for (int32_t h = 0; h < R.n_haps; ++h, ++hi) {
+      hoff[hi] = ho;
+      hlen[hi] = R.haps[h].len;
+      if (R.haps[h].len) std::memcpy(&hb[ho], R.haps[h].bases, R.haps[h].len);
+      ho += R.haps[h].len;
+    }
+    for (int32_t r = 0; r < R.n_reads; ++r)
+      for (int32_t h = 0; h < R.n_haps; ++h, ++pi) {
+        pr[pi] = (int32_t)(r0 + r);
+        ph[pi] = (int32_t)(h0 + h);
+      }
+  }
   fcs_phmm_batch b{};
   b.read_bases = rb.data();
   b.read_bq = bq.data();
@@ -542,17 +573,27 @@ int fcs_phmm_compute(const fcs_phmm_read* reads, int32_t n_reads, const fcs_phmm
   b.read_gcp = gq.data();
   b.read_off = roff.data();
   b.read_len = rlen.data();
-  b.n_reads = n_reads;
+  b.n_reads = nr;
   b.hap_bases = hb.data();
   b.hap_off = hoff.data();
   b.hap_len = hlen.data();
-  b.n_haps = n_haps;
+  b.n_haps = nh;
   b.pair_read = pr.data();
   b.pair_hap = ph.data();
   b.n_pairs = np;
   b.read_bytes = rt;
   b.hap_bytes = ht;
-  return fcs_phmm_compute_pairs(&b, out_log10, opts);
+  if (n_regions == 1) return fcs_phmm_compute_pairs(&b, regions[0].out_log10, opts);
+  std::vector<double> flat(np);
+  const int rc = fcs_phmm_compute_pairs(&b, flat.data(), opts);
+  if (rc) return rc;
+  int64_t off = 0;
+  for (int32_t g = 0; g < n_regions; ++g) {
+    const int64_t pairs = (int64_t)regions[g].n_reads * regions[g].n_haps;
+    if (pairs) std::memcpy(regions[g].out_log10, flat.data() + off, 8 * (size_t)pairs);
+    off += pairs;
+  }
+  return FCS_OK;
 }
 
 // ------------------------------------------------------------------ banded SW
@@ -871,6 +912,6 @@ int fcs_ksw_global2(int qlen, const uint8_t* query, int tlen, const uint8_t* tar
   return score;
 }
 
-int fcs_abi_symbol_count(void) { return 29; }
+int fcs_abi_symbol_count(void) { return 30; }
 
 }  // extern "C"

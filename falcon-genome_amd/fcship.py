@@ -61,6 +61,11 @@ class PhmmHap(C.Structure):
     _fields_ = [("bases", u8p), ("len", C.c_int32)]
 
 
+class PhmmRegion(C.Structure):
+    _fields_ = [("reads", C.POINTER(PhmmRead)), ("n_reads", C.c_int32), ("haps", C.POINTER(PhmmHap)),
+                ("n_haps", C.c_int32), ("out_log10", f64p)]
+
+
 class PhmmOpts(C.Structure):
     _fields_ = [("device", C.c_int32), ("use_fp64_rescue", C.c_int32), ("rescue_threshold", C.c_float),
                 ("exact_order", C.c_int32)]
@@ -112,6 +117,7 @@ _sig("fcs_abi_symbol_count", C.c_int, [])
 _sig("fcs_phmm_opts_default", None, [C.POINTER(PhmmOpts)])
 _sig("fcs_phmm_compute", C.c_int, [C.POINTER(PhmmRead), C.c_int32, C.POINTER(PhmmHap), C.c_int32, f64p,
                                    C.POINTER(PhmmOpts)])
+_sig("fcs_phmm_compute_regions", C.c_int, [C.POINTER(PhmmRegion), C.c_int32, C.POINTER(PhmmOpts)])
 _sig("fcs_phmm_compute_pairs", C.c_int, [C.POINTER(PhmmBatch), f64p, C.POINTER(PhmmOpts)])
 _sig("fcs_phmm_plan_create", C.c_int, [C.c_int32, C.c_int64, C.POINTER(C.c_void_p)])
 _sig("fcs_phmm_plan_destroy", C.c_int, [C.c_void_p])
@@ -267,6 +273,35 @@ def phmm_compute(reads, haps, **kw) -> np.ndarray:
     o = phmm_opts(**kw)
     check(lib.fcs_phmm_compute(R, len(reads), H, len(haps), out.ctypes.data_as(f64p), C.byref(o)))
     return out
+
+
+def phmm_compute_regions(regions, **kw) -> list:
+    """Active-region batching: regions = [(reads, haps), ...] with reads as
+    (bases, base_q, ins_q, del_q, gcp) tuples; one device pass for all, returns
+    one [n_reads, n_haps] log10 matrix per region."""
+    keep, outs = [], []
+
+    def u8(x):
+        a = np.ascontiguousarray(np.frombuffer(bytes(x), dtype=np.uint8) if not isinstance(x, np.ndarray)
+                                 else x.astype(np.uint8))
+        keep.append(a)
+        return a.ctypes.data_as(u8p)
+    G = (PhmmRegion * max(len(regions), 1))()
+    for g, (reads, haps) in enumerate(regions):
+        R = (PhmmRead * max(len(reads), 1))()
+        for i, r in enumerate(reads):
+            R[i] = PhmmRead(u8(r[0]), u8(r[1]), u8(r[2]), u8(r[3]), u8(r[4]), len(r[0]))
+        H = (PhmmHap * max(len(haps), 1))()
+        for i, h in enumerate(haps):
+            H[i] = PhmmHap(u8(h), len(h))
+        out = np.zeros((len(reads), len(haps)), dtype=np.float64)
+        keep += [R, H]
+        outs.append(out)
+        G[g] = PhmmRegion(C.cast(R, C.POINTER(PhmmRead)), len(reads), C.cast(H, C.POINTER(PhmmHap)), len(haps),
+                          out.ctypes.data_as(f64p))
+    o = phmm_opts(**kw)
+    check(lib.fcs_phmm_compute_regions(G, len(regions), C.byref(o)))
+    return outs
 
 
 def synth_phmm(seed: int, n_pairs: int, R: int = 101, hmin: int = 150, hmax: int = 300) -> PhmmPairs:

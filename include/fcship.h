@@ -98,6 +98,22 @@ void fcs_phmm_opts_default(fcs_phmm_opts* o);
 int fcs_phmm_compute(const fcs_phmm_read* reads, int32_t n_reads, const fcs_phmm_hap* haps,
                      int32_t n_haps, double* out_log10, const fcs_phmm_opts* opts);
 
+/* One active region: its reads x haplotypes matrix, written read-major to
+ * out_log10[r * n_haps + h] (the per-region call GATK's
+ * PairHMMLikelihoodCalculationEngine makes [EXT]). */
+typedef struct {
+  const fcs_phmm_read* reads;
+  int32_t n_reads;
+  const fcs_phmm_hap* haps;
+  int32_t n_haps;
+  double* out_log10;
+} fcs_phmm_region;
+
+/* Active-region batching: many regions in one device
+ * pass, each region's result identical to fcs_phmm_compute on that region
+ * alone.  Host pointers, synchronous. */
+int fcs_phmm_compute_regions(const fcs_phmm_region* regions, int32_t n_regions, const fcs_phmm_opts* opts);
+
 /* Flat structure-of-arrays pair batch.  Read k occupies
  * [read_off[k], read_off[k] + read_len[k]) of each of the five read byte
  * arrays; hap k occupies [hap_off[k], hap_off[k] + hap_len[k]) of hap_bases;

@@ -188,3 +188,28 @@ def test_golden_fixtures_gpu(gpu):
             assert np.all(np.abs(out[fin] - exp[fin]) <= tol[fin])
         else:
             np.testing.assert_allclose(out[fin], exp[fin], rtol=RTOL)
+
+
+def test_region_batching_equals_per_region(gpu):
+    """Active-region batching (fcs_phmm_compute_regions):
+    every region's matrix is bitwise the one fcs_phmm_compute gives for that
+    region alone, and within RTOL of the oracle; empty regions are allowed."""
+    rng = np.random.default_rng(77)
+    regions = []
+    for g in range(23):
+        nr, nh = int(rng.integers(0, 12)), int(rng.integers(0, 5))
+        if g == 5:
+            nr = 0
+        if g == 9:
+            nh = 0
+        reads, haps = random_batch(1000 + g, max(nr, 1), max(nh, 1), 30, 151, 60, 320)
+        regions.append((reads[:nr], haps[:nh]))
+    outs = fcship.phmm_compute_regions(regions)
+    for (reads, haps), out in zip(regions, outs):
+        assert out.shape == (len(reads), len(haps))
+        if out.size == 0:
+            continue
+        alone = fcship.phmm_compute(reads, haps)
+        assert np.array_equal(out, alone)
+        ref = np.array([[oracle_lib.phmm_log10(r, h)[0] for h in haps] for r in reads])
+        np.testing.assert_allclose(out, ref, rtol=RTOL)
