@@ -1,0 +1,585 @@
+#include "aligner.h"
+
+#include <algorithm>
+#include <cmath>
+#include <cstring>
+#include <fstream>
+#include <iostream>
+#include <map>
+
+#include "common.h"
+#include "config.h"
+#include "executor.h"
+#include "fcship.h"
+
+namespace fcsg {
+
+namespace {
+
+uint8_t code_of(char c) {
+  switch (c) {
+    case 'A': case 'a': return 0;
+    case 'C': case 'c': return 1;
+    case 'G': case 'g': return 2;
+    case 'T': case 't': return 3;
+    default: return 4;
+  }
+}
+
+std::vector<uint8_t> encode(const std::string& s) {
+  std::vector<uint8_t> o(s.size());
+  for (size_t i = 0; i < s.size(); ++i) o[i] = code_of(s[i]);
+  return o;
+}
+
+std::string revcomp(const std::string& s) {
+  std::string o(s.rbegin(), s.rend());
+  for (char& c : o) c = c == 'A' ? 'T' : c == 'C' ? 'G' : c == 'G' ? 'C' : c == 'T' ? 'A' : 'N';
+  return o;
+}
+
+// bwa's infer_bw (bwamem.c): band implied by a score over lengths l1, l2.
+int infer_bw(int l1, int l2, int score, int a, int q, int r) {
+  int w = (int)((double)(std::min(l1, l2) * a - score - q) / r + 2.);
+  if (w < std::abs(l1 - l2)) w = std::abs(l1 - l2);
+  return w;
+}
+
+// One read's alignment in progress.
+struct Aln {
+  int read = -1;
+  bool rev = false, mapped = false;
+  int contig = -1;
+  int mapq = 0;
+  std::string seq;            // oriented query bases (revcomp for reverse)
+  std::vector<uint8_t> q;     // codes of seq
+  std::vector<uint8_t> qual;  // oriented quals
+  int64_t seed_r = 0;         // contig offset of the seed start
+  int seed_q = 0, seed_len = 0;
+  int score = 0, truesc = 0;
+  int qb = 0, qe = 0;
+  int64_t rb = 0, re = 0;
+  int w_left = 0, w_right = 0;
+  std::vector<uint32_t> cigar;
+  int nm = 0;
+  std::string md;
+};
+
+}  // namespace
+
+KmerIndex::KmerIndex(const Reference& ref, int k) : k_(k) {
+  if (k < 8 || k > 31) throw invalidParam("seed length must be in [8, 31]");
+  uint64_t g = 0;
+  std::vector<std::pair<uint64_t, uint64_t>> kv;
+  for (const Contig& c : ref.contigs) {
+    starts_.push_back(g);
+    const int64_t L = (int64_t)c.seq.size();
+    uint64_t key = 0;
+    int valid = 0;
+    const uint64_t mask = (k == 32) ? ~0ull : ((1ull << (2 * k)) - 1);
+    for (int64_t p = 0; p < L; ++p) {
+      const uint8_t b = code_of(c.seq[p]);
+      if (b > 3) {
+        valid = 0;
+        key = 0;
+        continue;
+      }
+      key = ((key << 2) | b) & mask;
+      if (++valid >= k) kv.emplace_back(key, g + (uint64_t)(p - k + 1));
+    }
+    g += (uint64_t)L;
+  }
+  starts_.push_back(g);
+  std::sort(kv.begin(), kv.end());
+  keys_.resize(kv.size());
+  pos_.resize(kv.size());
+  for (size_t i = 0; i < kv.size(); ++i) {
+    keys_[i] = kv[i].first;
+    pos_[i] = kv[i].second;
+  }
+}
+
+std::pair<const uint64_t*, const uint64_t*> KmerIndex::lookup(uint64_t key) const {
+  auto lo = std::lower_bound(keys_.begin(), keys_.end(), key);
+  auto hi = std::upper_bound(lo, keys_.end(), key);
+  return {pos_.data() + (lo - keys_.begin()), pos_.data() + (hi - keys_.begin())};
+}
+
+int KmerIndex::contig_of(uint64_t g, int64_t& off) const {
+  const auto it = std::upper_bound(starts_.begin(), starts_.end(), g);
+  const int c = (int)(it - starts_.begin()) - 1;
+  off = (int64_t)(g - starts_[c]);
+  return c;
+}
+
+AlignStats align_reads(const Reference& ref, const KmerIndex& idx, const std::vector<std::string>& names,
+                       const std::vector<std::string>& seqs, const std::vector<std::string>& quals,
+                       const AlignOptions& opt, std::vector<BamRecord>& out) {
+  AlignStats st;
+  const uint64_t t0 = now_us();
+  fcs_bsw_params P;
+  fcs_bsw_params_default(&P);
+  const int a = 1;  // match score of the default matrix
+  const int k = idx.k();
+  const uint64_t kmask = (1ull << (2 * k)) - 1;
+  std::vector<Aln> alns(seqs.size());
+
+  // ---- seeds and the best chain per read
+  for (size_t r = 0; r < seqs.size(); ++r) {
+    Aln& A = alns[r];
+    A.read = (int)r;
+    ++st.reads;
+    struct Best {
+      int hits = 0;
+      int64_t diag = 0;
+      int qp = 0;
+      uint64_t g = 0;
+    } best[2], second;  // best per strand
+    int best_hits = 0, second_hits = 0;
+    bool best_rev = false;
+    for (int strand = 0; strand < 2; ++strand) {
+      const std::string s = strand ? revcomp(seqs[r]) : seqs[r];
+      const std::vector<uint8_t> c = encode(s);
+      std::map<int64_t, std::pair<int, std::pair<int, uint64_t>>> diag;  // diag → (hits, (first qp, g))
+      for (int qp = 0; qp + k <= (int)c.size(); qp += opt.seed_step) {
+        uint64_t key = 0;
+        bool ok = true;
+        for (int i = 0; i < k && ok; ++i) {
+          if (c[qp + i] > 3) ok = false;
+          key = ((key << 2) | c[qp + i]) & kmask;
+        }
+        if (!ok) continue;
+        const auto [b, e] = idx.lookup(key);
+        if (e - b == 0 || e - b > opt.max_occ) continue;
+        for (const uint64_t* p = b; p != e; ++p) {
+          const int64_t d = (int64_t)*p - qp;
+          auto& x = diag[d];
+          if (x.first++ == 0) x.second = {qp, *p};
+        }
+      }
+      // cluster diagonals within +-8 (indels shift them)
+      int64_t cl_start = 0, cl_prev = 0;
+      int cl_hits = 0;
+      std::pair<int, uint64_t> cl_seed{0, 0};
+      int cl_seed_hits = -1;
+      auto close = [&](void) {
+        if (cl_hits == 0) return;
+        if (cl_hits > best[strand].hits) best[strand] = {cl_hits, cl_start, cl_seed.first, cl_seed.second};
+        if (cl_hits > best_hits) {
+          second_hits = best_hits;
+          best_hits = cl_hits;
+          best_rev = strand;
+        } else if (cl_hits > second_hits) {
+          second_hits = cl_hits;
+        }
+      };
+      for (const auto& [d, x] : diag) {
+        if (cl_hits == 0 || d - cl_prev > 8) {
+          close();
+          cl_start = d;
+          cl_hits = 0;
+          cl_seed_hits = -1;
+        }
+        cl_hits += x.first;
+        if (x.first > cl_seed_hits) {
+          cl_seed_hits = x.first;
+          cl_seed = x.second;
+        }
+        cl_prev = d;
+      }
+      close();
+    }
+    (void)second;
+    if (best_hits == 0) continue;
+    const Best& B = best[best_rev ? 1 : 0];
+    A.rev = best_rev;
+    A.seq = best_rev ? revcomp(seqs[r]) : seqs[r];
+    A.q = encode(A.seq);
+    A.qual.resize(A.seq.size());
+    for (size_t i = 0; i < A.seq.size(); ++i) {
+      const size_t j = best_rev ? A.seq.size() - 1 - i : i;
+      A.qual[i] = (uint8_t)(j < quals[r].size() ? std::max(0, quals[r][j] - 33) : 30);
+    }
+    int64_t off = 0;
+    A.contig = idx.contig_of(B.g, off);
+    const std::string& R = ref.contigs[A.contig].seq;
+    // grow the k-mer hit to a maximal exact match
+    int qs = B.qp, qe = B.qp + k;
+    int64_t rs = off;
+    while (qs > 0 && rs > 0 && A.q[qs - 1] < 4 && A.q[qs - 1] == code_of(R[rs - 1])) --qs, --rs;
+    while (qe < (int)A.q.size() && rs + (qe - qs) < (int64_t)R.size() && A.q[qe] < 4 &&
+           A.q[qe] == code_of(R[rs + (qe - qs)]))
+      ++qe;
+    A.seed_q = qs;
+    A.seed_len = qe - qs;
+    A.seed_r = rs;
+    A.mapped = true;
+    A.mapq = second_hits >= best_hits ? 0 : std::min(60, (int)std::lround(60.0 * (best_hits - second_hits) / best_hits));
+  }
+
+  auto run_ext = [&](std::vector<fcs_bsw_task>& tasks, std::vector<fcs_bsw_result>& res) {
+    res.resize(tasks.size());
+    if (tasks.empty()) return;
+    const uint64_t g0 = now_us();
+    if (fcs_bsw_extend(tasks.data(), (int32_t)tasks.size(), &P, res.data(), opt.gpu) != FCS_OK)
+      throw failedCommand(std::string(fcs_last_error()));
+    st.gpu_seconds += (now_us() - g0) / 1e6;
+    st.ext_tasks += (int64_t)tasks.size();
+  };
+
+  // ---- left extensions (reversed prefix vs reversed reference), band retry
+  std::vector<std::vector<uint8_t>> lq(alns.size()), lt(alns.size());
+  {
+    std::vector<int> who;
+    std::vector<fcs_bsw_task> tasks;
+    std::vector<fcs_bsw_result> res;
+    for (Aln& A : alns) {
+      if (!A.mapped) continue;
+      A.score = A.truesc = A.seed_len * a;
+      A.qb = A.seed_q;
+      A.rb = A.seed_r;
+      if (A.seed_q == 0) continue;
+      const std::string& R = ref.contigs[A.contig].seq;
+      const int64_t tl = std::min<int64_t>(A.seed_r, A.seed_q + opt.w);
+      auto& q = lq[A.read];
+      auto& t = lt[A.read];
+      q.assign(A.q.rend() - A.seed_q, A.q.rend());
+      t.resize(tl);
+      for (int64_t i = 0; i < tl; ++i) t[i] = code_of(R[A.seed_r - 1 - i]);
+      who.push_back(A.read);
+    }
+    std::vector<int> w_of(alns.size(), opt.w);
+    std::vector<int> todo = who;
+    for (int pass = 0; pass < 2 && !todo.empty(); ++pass) {
+      tasks.clear();
+      for (int r : todo)
+        tasks.push_back({(int32_t)lq[r].size(), (int32_t)lt[r].size(), alns[r].seed_len * a, w_of[r], lq[r].data(),
+                         lt[r].data()});
+      run_ext(tasks, res);
+      std::vector<int> again;
+      for (size_t i = 0; i < todo.size(); ++i) {
+        Aln& A = alns[todo[i]];
+        const fcs_bsw_result& x = res[i];
+        const int prev = A.score;
+        A.score = x.score;
+        A.w_left = w_of[A.read];
+        if (x.gscore <= 0 || x.gscore <= A.score - P.end_bonus) {  // local
+          A.qb = A.seed_q - x.qle;
+          A.rb = A.seed_r - x.tle;
+          A.truesc = A.score;
+        } else {  // to-end
+          A.qb = 0;
+          A.rb = A.seed_r - x.gtle;
+          A.truesc = x.gscore;
+        }
+        const int w = w_of[A.read];
+        if (pass == 0 && A.score != prev && x.max_off >= (w >> 1) + (w >> 2)) {
+          w_of[A.read] = w << 1;
+          again.push_back(A.read);
+        }
+      }
+      todo = again;
+    }
+  }
+  // ---- right extensions (h0 = score after the left extension)
+  {
+    std::vector<int> who;
+    std::vector<fcs_bsw_task> tasks;
+    std::vector<fcs_bsw_result> res;
+    std::vector<int> sc0(alns.size(), 0), w_of(alns.size(), opt.w), left_true(alns.size(), 0);
+    for (Aln& A : alns) {
+      if (!A.mapped) continue;
+      const int qe = A.seed_q + A.seed_len;
+      A.qe = qe;
+      A.re = A.seed_r + A.seed_len;
+      if (qe == (int)A.q.size()) continue;
+      const std::string& R = ref.contigs[A.contig].seq;
+      auto& q = lq[A.read];
+      auto& t = lt[A.read];
+      q.assign(A.q.begin() + qe, A.q.end());
+      const int64_t tl = std::min<int64_t>((int64_t)R.size() - A.re, (int64_t)q.size() + opt.w);
+      t.resize(std::max<int64_t>(tl, 0));
+      for (int64_t i = 0; i < tl; ++i) t[i] = code_of(R[A.re + i]);
+      sc0[A.read] = A.score;
+      left_true[A.read] = A.truesc;
+      who.push_back(A.read);
+    }
+    std::vector<int> todo = who;
+    for (int pass = 0; pass < 2 && !todo.empty(); ++pass) {
+      tasks.clear();
+      for (int r : todo)
+        tasks.push_back({(int32_t)lq[r].size(), (int32_t)lt[r].size(), sc0[r], w_of[r], lq[r].data(), lt[r].data()});
+      run_ext(tasks, res);
+      std::vector<int> again;
+      for (size_t i = 0; i < todo.size(); ++i) {
+        Aln& A = alns[todo[i]];
+        const fcs_bsw_result& x = res[i];
+        const int prev = A.score;
+        const int qe0 = A.seed_q + A.seed_len;
+        const int64_t re0 = A.seed_r + A.seed_len;
+        A.score = x.score;
+        A.w_right = w_of[A.read];
+        // each try recomputes the right part from the left result (sc0)
+        if (x.gscore <= 0 || x.gscore <= A.score - P.end_bonus) {  // local
+          A.qe = qe0 + x.qle;
+          A.re = re0 + x.tle;
+          A.truesc = left_true[A.read] + A.score - sc0[A.read];
+        } else {  // to-end
+          A.qe = (int)A.q.size();
+          A.re = re0 + x.gtle;
+          A.truesc = left_true[A.read] + x.gscore - sc0[A.read];
+        }
+        const int w = w_of[A.read];
+        if (pass == 0 && A.score != prev && x.max_off >= (w >> 1) + (w >> 2)) {
+          w_of[A.read] = w << 1;
+          again.push_back(A.read);
+        }
+      }
+      todo = again;
+    }
+  }
+
+  // ---- global alignment for the CIGAR (bwa_gen_cigar2 with band inference / widening)
+  {
+    std::vector<int> todo;
+    std::vector<int> w2(alns.size(), 0), last_sc(alns.size(), INT32_MIN), tries(alns.size(), 0);
+    std::vector<std::vector<uint8_t>> gq(alns.size()), gt(alns.size());
+    for (Aln& A : alns) {
+      if (!A.mapped) continue;
+      if (A.qe <= A.qb || A.re <= A.rb) {
+        A.mapped = false;
+        continue;
+      }
+      const std::string& R = ref.contigs[A.contig].seq;
+      gq[A.read].assign(A.q.begin() + A.qb, A.q.begin() + A.qe);
+      gt[A.read].resize(A.re - A.rb);
+      for (int64_t i = A.rb; i < A.re; ++i) gt[A.read][i - A.rb] = code_of(R[i]);
+      const int l1 = A.qe - A.qb, l2 = (int)(A.re - A.rb);
+      int w = std::max(infer_bw(l1, l2, A.truesc, a, P.o_del, P.e_del), infer_bw(l1, l2, A.truesc, a, P.o_ins, P.e_ins));
+      const int wmax = std::max(A.w_left, A.w_right) ? std::max(A.w_left, A.w_right) : opt.w;
+      if (w > opt.w) w = std::min(w, wmax);
+      w2[A.read] = w;
+      todo.push_back(A.read);
+    }
+    while (!todo.empty()) {
+      std::vector<fcs_bsw_task> tasks;
+      std::vector<int64_t> off;
+      std::vector<int32_t> cap;
+      int64_t tot = 0;
+      for (int r : todo) {
+        w2[r] = std::min(w2[r], opt.w << 2);
+        tasks.push_back({(int32_t)gq[r].size(), (int32_t)gt[r].size(), 0, w2[r], gq[r].data(), gt[r].data()});
+        off.push_back(tot);
+        cap.push_back((int32_t)(gq[r].size() + gt[r].size() + 1));
+        tot += cap.back();
+      }
+      std::vector<int32_t> scores(tasks.size()), ncig(tasks.size());
+      std::vector<uint32_t> arena((size_t)std::max<int64_t>(tot, 1));
+      const uint64_t g0 = now_us();
+      if (fcs_bsw_global(tasks.data(), (int32_t)tasks.size(), &P, scores.data(), arena.data(), off.data(), cap.data(),
+                         ncig.data(), opt.gpu) != FCS_OK)
+        throw failedCommand(std::string(fcs_last_error()));
+      st.gpu_seconds += (now_us() - g0) / 1e6;
+      st.global_tasks += (int64_t)tasks.size();
+      std::vector<int> again;
+      for (size_t i = 0; i < todo.size(); ++i) {
+        Aln& A = alns[todo[i]];
+        A.cigar.assign(arena.begin() + off[i], arena.begin() + off[i] + ncig[i]);
+        const int sc = scores[i];
+        const bool stop = sc == last_sc[A.read] || w2[A.read] == opt.w << 2;
+        last_sc[A.read] = sc;
+        if (!stop && ++tries[A.read] < 3 && sc < A.truesc - a) {
+          w2[A.read] <<= 1;
+          again.push_back(A.read);
+        }
+      }
+      todo = again;
+    }
+  }
+
+  // ---- records
+  for (Aln& A : alns) {
+    BamRecord rec;
+    rec.name = names[A.read];
+    rec.set_aux_string("RG", opt.rg);
+    if (!A.mapped || A.cigar.empty()) {
+      rec.flag = kUnmapped;
+      rec.seq = seqs[A.read];
+      rec.qual.resize(rec.seq.size());
+      for (size_t i = 0; i < rec.seq.size(); ++i)
+        rec.qual[i] = (uint8_t)(i < quals[A.read].size() ? std::max(0, quals[A.read][i] - 33) : 30);
+      out.push_back(std::move(rec));
+      continue;
+    }
+    ++st.mapped;
+    std::vector<uint32_t> cig;
+    if (A.qb > 0) cig.push_back(cigar_pack((uint32_t)A.qb, kS));
+    for (uint32_t c : A.cigar) {
+      // ksw ops: 0 = M, 1 = I, 2 = D
+      const uint32_t op = c & 0xf;
+      cig.push_back(cigar_pack(c >> 4, op == 0 ? kM : op == 1 ? kI : kD));
+    }
+    if (A.qe < (int)A.q.size()) cig.push_back(cigar_pack((uint32_t)(A.q.size() - A.qe), kS));
+    // NM / MD over the aligned part
+    const std::string& R = ref.contigs[A.contig].seq;
+    int nm = 0, run = 0;
+    std::string md;
+    int qi = A.qb;
+    int64_t ri = A.rb;
+    for (uint32_t c : A.cigar) {
+      const uint32_t len = c >> 4, op = c & 0xf;
+      if (op == 0) {
+        for (uint32_t j = 0; j < len; ++j, ++qi, ++ri) {
+          if (A.q[qi] != code_of(R[ri]) || A.q[qi] > 3) {
+            ++nm;
+            md += std::to_string(run);
+            md += R[ri];
+            run = 0;
+          } else {
+            ++run;
+          }
+        }
+      } else if (op == 1) {
+        nm += (int)len;
+        qi += (int)len;
+      } else {
+        nm += (int)len;
+        md += std::to_string(run) + "^" + R.substr(ri, len);
+        run = 0;
+        ri += len;
+      }
+    }
+    md += std::to_string(run);
+    rec.ref_id = A.contig;
+    rec.pos = (int32_t)A.rb;
+    rec.mapq = (uint8_t)A.mapq;
+    rec.flag = A.rev ? kReverse : 0;
+    rec.cigar = cig;
+    rec.seq = A.seq;
+    rec.qual = A.qual;
+    rec.set_aux_int("NM", nm);
+    rec.set_aux_string("MD", md);
+    rec.set_aux_int("AS", A.truesc);
+    out.push_back(std::move(rec));
+  }
+  st.seconds = (now_us() - t0) / 1e6;
+  return st;
+}
+
+// ------------------------------------------------------------------ align command
+namespace {
+
+bool read_fastq(std::ifstream& in, std::string& name, std::string& seq, std::string& qual) {
+  std::string plus;
+  if (!std::getline(in, name)) return false;
+  if (name.empty() || name[0] != '@') throw formatError("FASTQ record does not start with '@'");
+  name = name.substr(1);
+  const size_t ws = name.find_first_of(" \t");
+  if (ws != std::string::npos) name.resize(ws);
+  if (name.size() > 2 && name[name.size() - 2] == '/') name.resize(name.size() - 2);  // /1, /2
+  if (!std::getline(in, seq) || !std::getline(in, plus) || !std::getline(in, qual))
+    throw formatError("truncated FASTQ record " + name);
+  if (qual.size() != seq.size()) throw formatError("FASTQ quality length differs for " + name);
+  return true;
+}
+
+}  // namespace
+
+int align_main(int argc, char** argv) {
+  std::string ref_path, fq1, fq2, output, rg = "sample", sp = "sample", pl = "illumina", lb = "sample";
+  bool force = false;
+  for (int i = 1; i < argc; ++i) {
+    const std::string a = argv[i];
+    auto val = [&]() -> std::string {
+      if (i + 1 >= argc) throw invalidParam(a + " needs a value");
+      return argv[++i];
+    };
+    if (a == "-h" || a == "--help") {
+      std::cerr << "'fcs-genome align' options:\n  -r, --ref arg\n  -1, --fastq1 arg\n  -2, --fastq2 arg\n"
+                   "  -o, --output arg\n  -R, --rg arg\n  -S, --sp arg\n  -P, --pl arg\n  -L, --lb arg\n"
+                   "  -l, --align-only\n  -f, --force\n";
+      throw helpRequest();
+    } else if (a == "-r" || a == "--ref") ref_path = val();
+    else if (a == "-1" || a == "--fastq1") fq1 = val();
+    else if (a == "-2" || a == "--fastq2") fq2 = val();
+    else if (a == "-o" || a == "--output") output = val();
+    else if (a == "-R" || a == "--rg") rg = val();
+    else if (a == "-S" || a == "--sp") sp = val();
+    else if (a == "-P" || a == "--pl") pl = val();
+    else if (a == "-L" || a == "--lb") lb = val();
+    else if (a == "-f" || a == "--force") force = true;
+    else if (a == "-l" || a == "--align-only" || a == "--disable-merge") continue;
+    else throw invalidParam(a);
+  }
+  if (ref_path.empty()) throw invalidParam("--ref is required");
+  if (fq1.empty()) throw invalidParam("--fastq1 is required");
+  if (output.empty()) throw invalidParam("--output is required");
+  if (!is_regular_file(ref_path)) throw fileNotFound(ref_path);
+  if (!is_regular_file(fq1)) throw fileNotFound(fq1);
+  if (!fq2.empty() && !is_regular_file(fq2)) throw fileNotFound(fq2);
+  if (!force && path_exists(output)) throw invalidParam("output " + output + " exists (use -f)");
+  const std::vector<int> gpus = conf().gpu_devices();
+  if (gpus.empty()) throw failedCommand("[E::fcs-genome] no GPU visible (gpu.devices); the GPU path has no CPU fallback");
+
+  const Reference ref = load_fasta(ref_path);
+  AlignOptions opt;
+  opt.gpu = gpus[0];
+  opt.rg = rg;
+  opt.chunk_size = conf().get_int("bwa.chunk_size");
+  const KmerIndex idx(ref, opt.k);
+  std::vector<BamRecord> recs;
+  AlignStats tot;
+  for (int mate = 0; mate < (fq2.empty() ? 1 : 2); ++mate) {
+    std::ifstream in(mate ? fq2 : fq1);
+    std::vector<std::string> names, seqs, quals;
+    std::string n, s, q;
+    auto flush = [&] {
+      if (names.empty()) return;
+      const size_t first = recs.size();
+      const AlignStats st = align_reads(ref, idx, names, seqs, quals, opt, recs);
+      if (!fq2.empty())
+        for (size_t i = first; i < recs.size(); ++i) recs[i].flag |= kPaired | (mate ? kRead2 : kRead1);
+      tot.reads += st.reads;
+      tot.mapped += st.mapped;
+      tot.seconds += st.seconds;
+      tot.gpu_seconds += st.gpu_seconds;
+      tot.ext_tasks += st.ext_tasks;
+      tot.global_tasks += st.global_tasks;
+      names.clear();
+      seqs.clear();
+      quals.clear();
+    };
+    while (read_fastq(in, n, s, q)) {
+      names.push_back(n);
+      seqs.push_back(s);
+      quals.push_back(q);
+      if ((int)names.size() >= opt.chunk_size) flush();
+    }
+    flush();
+  }
+  std::stable_sort(recs.begin(), recs.end(), [](const BamRecord& x, const BamRecord& y) {
+    const uint32_t a = (uint32_t)x.ref_id, b = (uint32_t)y.ref_id;  // unmapped (-1) last
+    return a != b ? a < b : x.pos < y.pos;
+  });
+  BamHeader h;
+  h.text = "@HD\tVN:1.6\tSO:coordinate\n";
+  for (const Contig& c : ref.contigs) {
+    h.names.push_back(c.name);
+    h.lengths.push_back((int64_t)c.seq.size());
+    h.text += "@SQ\tSN:" + c.name + "\tLN:" + std::to_string(c.seq.size()) + "\n";
+  }
+  h.text += "@RG\tID:" + rg + "\tSM:" + sp + "\tPL:" + pl + "\tLB:" + lb + "\n";
+  h.text += "@PG\tID:fcs-genome\tPN:fcs-genome align\n";
+  {
+    BamWriter w(output, h);
+    for (const BamRecord& r : recs) w.write(r);
+    w.close();
+  }
+  bam_index_build(output);
+  std::cerr << "[fcs-genome align] " << tot.reads << " reads, " << tot.mapped << " mapped, " << tot.ext_tasks
+            << " extension tasks, " << tot.global_tasks << " global alignments, " << tot.seconds << " s (GPU calls "
+            << tot.gpu_seconds << " s)" << std::endl;
+  return 0;
+}
+
+}  // namespace fcsg

@@ -1,0 +1,233 @@
+#include "bgzf.h"
+
+#include <zlib.h>
+
+#include <cstring>
+
+#include "common.h"
+
+namespace fcsg {
+
+const uint8_t kBgzfEof[28] = {0x1f, 0x8b, 0x08, 0x04, 0, 0, 0, 0, 0, 0xff, 0x06, 0, 0x42, 0x43,
+                              0x02, 0,    0x1b, 0,    3, 0, 0, 0, 0, 0, 0,    0, 0, 0};
+
+namespace {
+
+void put16(uint8_t* p, uint32_t v) {
+  p[0] = (uint8_t)v;
+  p[1] = (uint8_t)(v >> 8);
+}
+void put32(uint8_t* p, uint32_t v) {
+  for (int i = 0; i < 4; ++i) p[i] = (uint8_t)(v >> (8 * i));
+}
+uint32_t get16(const uint8_t* p) { return (uint32_t)p[0] | ((uint32_t)p[1] << 8); }
+uint32_t get32(const uint8_t* p) {
+  return (uint32_t)p[0] | ((uint32_t)p[1] << 8) | ((uint32_t)p[2] << 16) | ((uint32_t)p[3] << 24);
+}
+
+// One BGZF member for n <= kBgzfMaxBlock input bytes.
+std::vector<uint8_t> make_block(const uint8_t* data, size_t n, int level) {
+  std::vector<uint8_t> out(kBgzfMaxBlock + 64);
+  for (int attempt = 0; attempt < 2; ++attempt) {
+    z_stream zs{};
+    if (deflateInit2(&zs, attempt ? 0 : level, Z_DEFLATED, -15, 8, Z_DEFAULT_STRATEGY) != Z_OK)
+      throw internalError("[E::bgzf] deflateInit2 failed");
+    zs.next_in = const_cast<uint8_t*>(data);
+    zs.avail_in = (uInt)n;
+    zs.next_out = out.data() + 18;
+    zs.avail_out = (uInt)(kBgzfMaxBlock - 18 - 8);
+    const int rc = deflate(&zs, Z_FINISH);
+    const size_t clen = zs.total_out;
+    deflateEnd(&zs);
+    if (rc != Z_STREAM_END) {
+      if (attempt == 0) continue;  // incompressible: store (level 0) instead
+      throw internalError("[E::bgzf] block does not fit in 64 KiB");
+    }
+    const size_t bsize = 18 + clen + 8;
+    static const uint8_t hdr[16] = {0x1f, 0x8b, 0x08, 0x04, 0, 0, 0, 0, 0, 0xff, 0x06, 0, 0x42, 0x43, 0x02, 0};
+    std::memcpy(out.data(), hdr, 16);
+    put16(out.data() + 16, (uint32_t)(bsize - 1));
+    put32(out.data() + 18 + clen, (uint32_t)crc32(crc32(0L, Z_NULL, 0), data, (uInt)n));
+    put32(out.data() + 18 + clen + 4, (uint32_t)n);
+    out.resize(bsize);
+    return out;
+  }
+  return {};
+}
+
+}  // namespace
+
+// ------------------------------------------------------------------ writer
+BgzfWriter::BgzfWriter(const std::string& path, int level) : level_(level) {
+  f_ = std::fopen(path.c_str(), "wb");
+  if (!f_) throw fileNotFound(path + " (cannot open for writing)");
+  buf_.reserve(kBgzfMaxBlock);
+}
+
+BgzfWriter::~BgzfWriter() {
+  try {
+    close();
+  } catch (...) {
+  }
+}
+
+void BgzfWriter::emit_block(const uint8_t* data, size_t n) {
+  const std::vector<uint8_t> blk = make_block(data, n, level_);
+  if (std::fwrite(blk.data(), 1, blk.size(), f_) != blk.size()) throw internalError("[E::bgzf] write failed");
+  coff_ += blk.size();
+}
+
+void BgzfWriter::write(const void* data, size_t n) {
+  const uint8_t* p = static_cast<const uint8_t*>(data);
+  while (n > 0) {
+    const size_t take = std::min(n, kBgzfBlockData - buf_.size());
+    buf_.insert(buf_.end(), p, p + take);
+    p += take;
+    n -= take;
+    if (buf_.size() >= kBgzfBlockData) flush();
+  }
+}
+
+void BgzfWriter::flush() {
+  if (buf_.empty()) return;
+  emit_block(buf_.data(), buf_.size());
+  buf_.clear();
+}
+
+void BgzfWriter::close() {
+  if (closed_ || !f_) return;
+  flush();
+  std::fwrite(kBgzfEof, 1, sizeof kBgzfEof, f_);
+  std::fclose(f_);
+  f_ = nullptr;
+  closed_ = true;
+}
+
+// ------------------------------------------------------------------ reader
+BgzfReader::BgzfReader(const std::string& path) {
+  f_ = std::fopen(path.c_str(), "rb");
+  if (!f_) throw fileNotFound(path);
+}
+
+BgzfReader::~BgzfReader() {
+  if (f_) std::fclose(f_);
+}
+
+bool BgzfReader::load_block() {
+  for (;;) {
+    block_coff_ = next_coff_;
+    if (std::fseek(f_, (long)block_coff_, SEEK_SET) != 0) return false;
+    uint8_t h[18];
+    const size_t got = std::fread(h, 1, 18, f_);
+    if (got == 0) return false;
+    if (got < 18 || h[0] != 0x1f || h[1] != 0x8b || h[2] != 8 || !(h[3] & 4))
+      throw formatError("not a BGZF block at offset " + std::to_string(block_coff_));
+    const uint32_t xlen = get16(h + 10);
+    // find the BC subfield (it is the only one we write; others are skipped)
+    std::vector<uint8_t> extra(xlen);
+    std::memcpy(extra.data(), h + 12, std::min<uint32_t>(xlen, 6));
+    if (xlen > 6 && std::fread(extra.data() + 6, 1, xlen - 6, f_) != xlen - 6) throw formatError("truncated BGZF header");
+    uint32_t bsize = 0;
+    for (uint32_t k = 0; k + 4 <= xlen;) {
+      const uint32_t slen = get16(&extra[k + 2]);
+      if (extra[k] == 66 && extra[k + 1] == 67 && slen == 2) bsize = get16(&extra[k + 4]) + 1;
+      k += 4 + slen;
+    }
+    if (bsize == 0) throw formatError("gzip member without BGZF BC field");
+    std::vector<uint8_t> comp(bsize);
+    std::fseek(f_, (long)block_coff_, SEEK_SET);
+    if (std::fread(comp.data(), 1, bsize, f_) != bsize) throw formatError("truncated BGZF block");
+    const size_t hdr = 12 + xlen;
+    const uint32_t isize = get32(&comp[bsize - 4]);
+    const uint32_t crc = get32(&comp[bsize - 8]);
+    block_.assign(isize, 0);
+    if (isize > 0) {
+      z_stream zs{};
+      if (inflateInit2(&zs, -15) != Z_OK) throw internalError("[E::bgzf] inflateInit2 failed");
+      zs.next_in = comp.data() + hdr;
+      zs.avail_in = (uInt)(bsize - hdr - 8);
+      zs.next_out = block_.data();
+      zs.avail_out = isize;
+      const int rc = inflate(&zs, Z_FINISH);
+      inflateEnd(&zs);
+      if (rc != Z_STREAM_END || zs.total_out != isize) throw formatError("corrupt BGZF block payload");
+      if ((uint32_t)crc32(crc32(0L, Z_NULL, 0), block_.data(), isize) != crc) throw formatError("BGZF CRC mismatch");
+    }
+    next_coff_ = block_coff_ + bsize;
+    pos_ = 0;
+    if (isize == 0) {
+      saw_eof_ = true;  // empty block (EOF marker, or an empty block mid-file): keep going
+      continue;
+    }
+    return true;
+  }
+}
+
+size_t BgzfReader::read(void* out, size_t n) {
+  uint8_t* o = static_cast<uint8_t*>(out);
+  size_t done = 0;
+  while (done < n) {
+    if (pos_ >= block_.size() && !load_block()) break;
+    const size_t take = std::min(n - done, block_.size() - pos_);
+    std::memcpy(o + done, block_.data() + pos_, take);
+    pos_ += take;
+    done += take;
+  }
+  return done;
+}
+
+bool BgzfReader::read_exact(void* out, size_t n) {
+  const size_t got = read(out, n);
+  if (got == 0 && n > 0) return false;
+  if (got != n) throw formatError("truncated BGZF data");
+  return true;
+}
+
+bool BgzfReader::getline(std::string& line) {
+  line.clear();
+  bool any = false;
+  for (;;) {
+    if (pos_ >= block_.size() && !load_block()) return any;
+    any = true;
+    const uint8_t* s = block_.data() + pos_;
+    const uint8_t* e = block_.data() + block_.size();
+    const uint8_t* nl = static_cast<const uint8_t*>(std::memchr(s, '\n', e - s));
+    if (nl) {
+      line.append(reinterpret_cast<const char*>(s), nl - s);
+      pos_ += (nl - s) + 1;
+      return true;
+    }
+    line.append(reinterpret_cast<const char*>(s), e - s);
+    pos_ = block_.size();
+  }
+}
+
+void BgzfReader::seek(uint64_t voff) {
+  next_coff_ = voff >> 16;
+  block_.clear();
+  pos_ = 0;
+  if (!load_block()) throw formatError("seek past end of BGZF file");
+  pos_ = (size_t)(voff & 0xffff);
+}
+
+std::vector<uint8_t> bgzf_compress(const uint8_t* data, size_t n, int level) {
+  std::vector<uint8_t> out;
+  for (size_t k = 0; k < n; k += kBgzfBlockData) {
+    const std::vector<uint8_t> b = make_block(data + k, std::min(kBgzfBlockData, n - k), level);
+    out.insert(out.end(), b.begin(), b.end());
+  }
+  out.insert(out.end(), kBgzfEof, kBgzfEof + sizeof kBgzfEof);
+  return out;
+}
+
+bool is_bgzf_file(const std::string& path) {
+  FILE* f = std::fopen(path.c_str(), "rb");
+  if (!f) return false;
+  uint8_t h[16];
+  const bool ok = std::fread(h, 1, 16, f) == 16 && h[0] == 0x1f && h[1] == 0x8b && (h[3] & 4) && h[12] == 66 &&
+                  h[13] == 67;
+  std::fclose(f);
+  return ok;
+}
+
+}  // namespace fcsg

@@ -1,0 +1,75 @@
+// BGZF (blocked gzip) reader and writer on zlib — the container of BAM,
+// bgzipped VCF and tabix indexes (the reference shells
+// out to bgzip/tabix/samtools for these, src/worker-htc.cpp:153-176).
+//
+// Block layout (SAM/BAM spec §4.1): a gzip member with FEXTRA carrying the
+// 'BC' subfield (BSIZE = block size - 1), raw-deflate payload of at most 64 KiB,
+// CRC32 and ISIZE.  Files end with the fixed 28-byte empty block.  A virtual
+// offset is (compressed block start << 16) | offset inside the block.
+#pragma once
+
+#include <cstdint>
+#include <cstdio>
+#include <string>
+#include <vector>
+
+namespace fcsg {
+
+constexpr size_t kBgzfMaxBlock = 0x10000;   // max uncompressed bytes per block
+constexpr size_t kBgzfBlockData = 0xff00;   // what the writer packs per block (as htslib)
+extern const uint8_t kBgzfEof[28];
+
+class BgzfWriter {
+ public:
+  explicit BgzfWriter(const std::string& path, int level = 6);
+  ~BgzfWriter();
+  BgzfWriter(const BgzfWriter&) = delete;
+  BgzfWriter& operator=(const BgzfWriter&) = delete;
+
+  void write(const void* data, size_t n);
+  void write(const std::string& s) { write(s.data(), s.size()); }
+  // Ends the current block so the next write starts a new one (BAM header, index points).
+  void flush();
+  // Virtual offset of the next byte written.
+  uint64_t tell() const { return (coff_ << 16) | (uint64_t)buf_.size(); }
+  void close();  // flush + EOF block
+
+ private:
+  void emit_block(const uint8_t* data, size_t n);
+  FILE* f_ = nullptr;
+  int level_;
+  std::vector<uint8_t> buf_;
+  uint64_t coff_ = 0;  // compressed offset of the block being filled
+  bool closed_ = false;
+};
+
+class BgzfReader {
+ public:
+  explicit BgzfReader(const std::string& path);
+  ~BgzfReader();
+  BgzfReader(const BgzfReader&) = delete;
+  BgzfReader& operator=(const BgzfReader&) = delete;
+
+  // Reads up to n bytes; returns bytes read (0 at end of data).
+  size_t read(void* out, size_t n);
+  // Reads exactly n bytes or throws formatError (false when at clean EOF before any byte).
+  bool read_exact(void* out, size_t n);
+  bool getline(std::string& line);  // text mode ('\n' stripped)
+  uint64_t tell() const { return (block_coff_ << 16) | (uint64_t)pos_; }
+  void seek(uint64_t voff);
+  bool saw_eof_marker() const { return saw_eof_; }
+
+ private:
+  bool load_block();  // false at end of file
+  FILE* f_ = nullptr;
+  std::vector<uint8_t> block_;
+  size_t pos_ = 0;
+  uint64_t block_coff_ = 0, next_coff_ = 0;
+  bool saw_eof_ = false;
+};
+
+// Whole-buffer helpers (tests, small files).
+std::vector<uint8_t> bgzf_compress(const uint8_t* data, size_t n, int level = 6);
+bool is_bgzf_file(const std::string& path);
+
+}  // namespace fcsg

@@ -1,0 +1,495 @@
+#include "caller.h"
+
+#include <algorithm>
+#include <cmath>
+#include <cstdio>
+#include <map>
+#include <memory>
+#include <tuple>
+
+#include "bam.h"
+#include "common.h"
+#include "fcship.h"
+#include "gatk_prep.h"
+
+namespace fcsg {
+
+void CallerStats::add(const CallerStats& o) {
+  reads += o.reads;
+  regions += o.regions;
+  pairs += o.pairs;
+  cells += o.cells;
+  calls += o.calls;
+  device_passes += o.device_passes;
+  seconds += o.seconds;
+  phmm_seconds += o.phmm_seconds;
+}
+
+namespace {
+
+struct Read {
+  int32_t pos = 0;
+  int64_t end = 0;
+  std::vector<uint32_t> cigar;
+  std::string seq;
+  std::vector<uint8_t> qual;
+  int mapq = 0;
+  std::string bi, bd;
+};
+
+void load_reads(const std::string& bam, const std::string& chrom, int64_t beg, int64_t end, const CallerOptions& opt,
+                std::vector<Read>& out) {
+  BamReader rd(bam);
+  const int tid = rd.header().ref_index(chrom);
+  if (tid < 0) return;
+  if (is_regular_file(bam + ".bai")) {
+    const uint64_t off = BamIndex(bam + ".bai").seek_offset(tid, beg);
+    if (off) rd.seek(off);
+  }
+  BamRecord r;
+  while (rd.next(r)) {
+    if (r.ref_id < tid) continue;
+    if (r.ref_id > tid || r.pos >= end) break;
+    if (r.flag & (kUnmapped | kSecondary | kQcFail | kDuplicate | kSupplementary)) continue;
+    if (r.mapq < opt.min_mapq || r.cigar.empty() || r.qual.size() != r.seq.size()) continue;
+    const int64_t e = r.end();
+    if (e <= beg) continue;
+    Read x;
+    x.pos = r.pos;
+    x.end = e;
+    x.cigar = std::move(r.cigar);
+    x.seq = std::move(r.seq);
+    x.qual = std::move(r.qual);
+    x.mapq = r.mapq;
+    r.get_aux_string("BI", x.bi);
+    r.get_aux_string("BD", x.bd);
+    out.push_back(std::move(x));
+  }
+}
+
+struct Allele {
+  int64_t pos;  // 0-based anchor
+  std::string ref, alt;
+  bool operator<(const Allele& o) const { return std::tie(pos, ref, alt) < std::tie(o.pos, o.ref, o.alt); }
+  int64_t ref_end() const { return pos + (int64_t)ref.size(); }
+};
+
+struct Pileup {
+  int64_t wb = 0;
+  std::vector<int> depth, events;
+  std::map<Allele, int> support;
+};
+
+// Walks every read's CIGAR once: depth, mismatch/indel events and allele support.
+void build_pileup(const std::string& ref, const std::vector<Read>& reads, int min_bq, Pileup& pu) {
+  const int64_t n = (int64_t)pu.depth.size();
+  auto in = [&](int64_t p) { return p >= pu.wb && p < pu.wb + n; };
+  for (const Read& rd : reads) {
+    int64_t rp = rd.pos;
+    size_t q = 0;
+    for (uint32_t c : rd.cigar) {
+      const uint32_t len = cigar_len(c);
+      switch (cigar_op(c)) {
+        case kM: case kEq: case kX:
+          for (uint32_t k = 0; k < len; ++k, ++rp, ++q) {
+            if (!in(rp) || rd.qual[q] < min_bq) continue;
+            ++pu.depth[rp - pu.wb];
+            const char b = rd.seq[q];
+            if (b != ref[rp] && ref[rp] != 'N' && b != 'N') {
+              ++pu.events[rp - pu.wb];
+              ++pu.support[{rp, std::string(1, ref[rp]), std::string(1, b)}];
+            }
+          }
+          break;
+        case kI:
+          if (rp > rd.pos && in(rp - 1)) {
+            ++pu.events[rp - 1 - pu.wb];
+            ++pu.support[{rp - 1, std::string(1, ref[rp - 1]), ref[rp - 1] + rd.seq.substr(q, len)}];
+          }
+          q += len;
+          break;
+        case kD:
+          if (rp > rd.pos && in(rp - 1) && rp + len <= (int64_t)ref.size()) {
+            ++pu.events[rp - 1 - pu.wb];
+            ++pu.support[{rp - 1, ref.substr(rp - 1, len + 1), std::string(1, ref[rp - 1])}];
+          }
+          for (uint32_t k = 0; k < len; ++k, ++rp)
+            if (in(rp)) ++pu.depth[rp - pu.wb];
+          break;
+        case kN: rp += len; break;
+        case kS: q += len; break;
+        default: break;
+      }
+    }
+  }
+}
+
+// Query slice [qs, qe) of the read whose bases align inside [rb, re) (inserted
+// bases go with their left anchor); soft clips excluded.  false if empty.
+bool clip_to_window(const Read& rd, int64_t rb, int64_t re, size_t& qs, size_t& qe) {
+  int64_t rp = rd.pos, anchor = rd.pos - 1;
+  size_t q = 0;
+  bool started = false;
+  qs = qe = 0;
+  auto take = [&](int64_t a, size_t qi) {
+    if (a >= rb && a < re) {
+      if (!started) {
+        qs = qi;
+        started = true;
+      }
+      qe = qi + 1;
+    }
+  };
+  for (uint32_t c : rd.cigar) {
+    const uint32_t len = cigar_len(c);
+    switch (cigar_op(c)) {
+      case kM: case kEq: case kX:
+        for (uint32_t k = 0; k < len; ++k, ++rp, ++q) {
+          anchor = rp;
+          take(rp, q);
+        }
+        break;
+      case kI:
+        for (uint32_t k = 0; k < len; ++k, ++q) take(anchor, q);
+        break;
+      case kD: case kN: rp += len; anchor = rp - 1; break;
+      case kS: q += len; break;
+      default: break;
+    }
+  }
+  return started && qe > qs;
+}
+
+struct Region {
+  int64_t beg = 0, end = 0;  // reference window [beg, end)
+  std::vector<Allele> cands;
+  std::vector<std::string> haps;
+  std::vector<uint32_t> hap_mask;  // bit c: haplotype carries candidate c
+  std::vector<PreparedRead> reads[2];  // [0] sample / tumor, [1] normal
+  std::vector<double> lik[2];          // read-major log10 likelihoods
+};
+
+void build_haplotypes(const std::string& ref, Region& g) {
+  const int k = (int)g.cands.size();
+  for (uint32_t mask = 0; mask < (1u << k); ++mask) {
+    std::vector<const Allele*> on;
+    for (int c = 0; c < k; ++c)
+      if (mask >> c & 1) on.push_back(&g.cands[c]);
+    std::sort(on.begin(), on.end(), [](const Allele* a, const Allele* b) { return a->pos < b->pos; });
+    bool ok = true;
+    for (size_t i = 1; i < on.size(); ++i)
+      if (on[i]->pos < on[i - 1]->ref_end()) ok = false;  // overlapping alleles cannot share a haplotype
+    if (!ok) continue;
+    std::string h;
+    int64_t p = g.beg;
+    for (const Allele* a : on) {
+      h.append(ref, p, a->pos - p);
+      h += a->alt;
+      p = a->ref_end();
+    }
+    h.append(ref, p, g.end - p);
+    g.haps.push_back(std::move(h));
+    g.hap_mask.push_back(mask);
+  }
+}
+
+double log10_add(double a, double b) {
+  const double m = std::max(a, b);
+  if (m == -INFINITY) return m;
+  return m + std::log10(std::pow(10.0, a - m) + std::pow(10.0, b - m));
+}
+
+// Per read: best log10 likelihood among haplotypes with / without candidate c.
+void allele_lik(const Region& g, int s, int c, std::vector<double>& la, std::vector<double>& lr) {
+  const size_t nr = g.reads[s].size(), nh = g.haps.size();
+  la.assign(nr, -INFINITY);
+  lr.assign(nr, -INFINITY);
+  for (size_t r = 0; r < nr; ++r)
+    for (size_t h = 0; h < nh; ++h) {
+      const double v = g.lik[s][r * nh + h];
+      if (g.hap_mask[h] >> c & 1) la[r] = std::max(la[r], v);
+      else lr[r] = std::max(lr[r], v);
+    }
+}
+
+void dump_region(std::FILE* f, const Region& g, int s) {
+  const int32_t nr = (int32_t)g.reads[s].size(), nh = (int32_t)g.haps.size();
+  std::fwrite("RGN1", 1, 4, f);
+  std::fwrite(&nr, 4, 1, f);
+  std::fwrite(&nh, 4, 1, f);
+  for (const PreparedRead& r : g.reads[s]) {
+    const int32_t L = (int32_t)r.bases.size();
+    std::fwrite(&L, 4, 1, f);
+    for (const auto* v : {&r.bases, &r.base_q, &r.ins_q, &r.del_q, &r.gcp}) std::fwrite(v->data(), 1, L, f);
+  }
+  for (const std::string& h : g.haps) {
+    const int32_t L = (int32_t)h.size();
+    std::fwrite(&L, 4, 1, f);
+    std::fwrite(h.data(), 1, L, f);
+  }
+  std::fwrite(g.lik[s].data(), 8, g.lik[s].size(), f);
+}
+
+// One device pass over a batch of regions (both read sets in Mutect2 mode).
+void run_phmm(std::vector<std::unique_ptr<Region>>& batch, const CallerOptions& opt, CallerStats& st, std::FILE* dump) {
+  std::vector<std::vector<fcs_phmm_read>> rv;
+  std::vector<std::vector<fcs_phmm_hap>> hv(batch.size());
+  std::vector<fcs_phmm_region> regs;
+  rv.reserve(2 * batch.size());
+  for (size_t i = 0; i < batch.size(); ++i) {
+    Region& g = *batch[i];
+    for (const std::string& h : g.haps) hv[i].push_back({reinterpret_cast<const uint8_t*>(h.data()), (int32_t)h.size()});
+    for (int s = 0; s < 2; ++s) {
+      g.lik[s].assign(g.reads[s].size() * g.haps.size(), 0.0);
+      if (g.reads[s].empty()) continue;
+      rv.emplace_back();
+      for (const PreparedRead& r : g.reads[s]) {
+        rv.back().push_back({r.bases.data(), r.base_q.data(), r.ins_q.data(), r.del_q.data(), r.gcp.data(),
+                             (int32_t)r.bases.size()});
+        for (const std::string& h : g.haps) st.cells += (int64_t)r.bases.size() * (int64_t)h.size();
+      }
+      regs.push_back({rv.back().data(), (int32_t)rv.back().size(), hv[i].data(), (int32_t)hv[i].size(),
+                      g.lik[s].data()});
+      st.pairs += (int64_t)g.reads[s].size() * (int64_t)g.haps.size();
+    }
+  }
+  fcs_phmm_opts o;
+  fcs_phmm_opts_default(&o);
+  o.device = opt.gpu;
+  o.use_fp64_rescue = opt.fp64_rescue ? 1 : 0;
+  const uint64_t t0 = now_us();
+  const int rc = fcs_phmm_compute_regions(regs.data(), (int32_t)regs.size(), &o);
+  st.phmm_seconds += (now_us() - t0) / 1e6;
+  ++st.device_passes;
+  if (rc != FCS_OK) throw failedCommand(std::string(fcs_last_error()));
+  if (dump)
+    for (const auto& g : batch)
+      for (int s = 0; s < 2; ++s)
+        if (!g->reads[s].empty()) dump_region(dump, *g, s);
+}
+
+// Germline diploid genotyping of each candidate allele of a region.
+void genotype_germline(const Region& g, const CallerOptions& opt, int64_t own_beg, int64_t own_end,
+                       const std::string& chrom, std::vector<VcfRecord>& calls) {
+  static const double prior[3] = {std::log10(1.0 - 1.5e-3), std::log10(1e-3), std::log10(5e-4)};
+  std::vector<double> la, lr;
+  for (size_t c = 0; c < g.cands.size(); ++c) {
+    const Allele& a = g.cands[c];
+    if (a.pos < own_beg || a.pos >= own_end) continue;
+    allele_lik(g, 0, (int)c, la, lr);
+    double gl[3] = {0, 0, 0};
+    int ad_ref = 0, ad_alt = 0;
+    for (size_t r = 0; r < la.size(); ++r) {
+      gl[0] += lr[r];
+      gl[2] += la[r];
+      gl[1] += log10_add(la[r], lr[r]) - std::log10(2.0);
+      if (la[r] - lr[r] > 0.2) ++ad_alt;
+      else if (lr[r] - la[r] > 0.2) ++ad_ref;
+    }
+    double post[3], mx = -INFINITY;
+    for (int k = 0; k < 3; ++k) mx = std::max(mx, post[k] = gl[k] + prior[k]);
+    double norm = -INFINITY;
+    for (int k = 0; k < 3; ++k) norm = log10_add(norm, post[k]);
+    const int gt = (int)(std::max_element(post, post + 3) - post);
+    const double qual = std::min(-10.0 * (post[0] - norm), 9999.0);
+    if (gt == 0 || qual < opt.min_qual) continue;
+    const double glmax = std::max({gl[0], gl[1], gl[2]});
+    int pl[3];
+    for (int k = 0; k < 3; ++k) pl[k] = (int)std::lround(-10.0 * (gl[k] - glmax));
+    int sorted[3] = {pl[0], pl[1], pl[2]};
+    std::sort(sorted, sorted + 3);
+    const int gq = std::min(99, sorted[1]);
+    VcfRecord rec;
+    rec.chrom = chrom;
+    rec.pos = a.pos + 1;
+    rec.ref = a.ref;
+    rec.alts = {a.alt};
+    rec.qual = qual;
+    rec.info = "DP=" + std::to_string(la.size());
+    rec.format = "GT:AD:DP:GQ:PL";
+    rec.samples = {std::string(gt == 1 ? "0/1" : "1/1") + ":" + std::to_string(ad_ref) + "," + std::to_string(ad_alt) +
+                   ":" + std::to_string(la.size()) + ":" + std::to_string(gq) + ":" + std::to_string(pl[0]) + "," +
+                   std::to_string(pl[1]) + "," + std::to_string(pl[2])};
+    calls.push_back(rec);
+  }
+}
+
+// Mutect2-style tumor/normal test of each candidate allele.
+void genotype_somatic(const Region& g, const CallerOptions& opt, int64_t own_beg, int64_t own_end,
+                      const std::string& chrom, std::vector<VcfRecord>& calls) {
+  std::vector<double> ta, tr, na, nr;
+  for (size_t c = 0; c < g.cands.size(); ++c) {
+    const Allele& a = g.cands[c];
+    if (a.pos < own_beg || a.pos >= own_end) continue;
+    allele_lik(g, 0, (int)c, ta, tr);
+    allele_lik(g, 1, (int)c, na, nr);
+    int t_alt = 0, t_ref = 0, n_alt = 0, n_ref = 0;
+    for (size_t r = 0; r < ta.size(); ++r) {
+      if (ta[r] - tr[r] > 0.2) ++t_alt;
+      else if (tr[r] - ta[r] > 0.2) ++t_ref;
+    }
+    for (size_t r = 0; r < na.size(); ++r) {
+      if (na[r] - nr[r] > 0.2) ++n_alt;
+      else if (nr[r] - na[r] > 0.2) ++n_ref;
+    }
+    if (t_alt == 0) continue;
+    const double f = std::max(1e-3, (double)t_alt / std::max(1, t_alt + t_ref));
+    double tlod = 0, nlod = 0;
+    for (size_t r = 0; r < ta.size(); ++r)
+      tlod += log10_add(std::log10(f) + ta[r], std::log10(1.0 - f) + tr[r]) - tr[r];
+    for (size_t r = 0; r < na.size(); ++r) nlod += nr[r] - (log10_add(na[r], nr[r]) - std::log10(2.0));
+    if (tlod < opt.tlod || nlod < opt.nlod) continue;
+    VcfRecord rec;
+    rec.chrom = chrom;
+    rec.pos = a.pos + 1;
+    rec.ref = a.ref;
+    rec.alts = {a.alt};
+    char info[96];
+    std::snprintf(info, sizeof info, "TLOD=%.2f;NLOD=%.2f", tlod, nlod);
+    rec.info = info;
+    rec.format = "GT:AD:AF";
+    char taf[32];
+    std::snprintf(taf, sizeof taf, "%.3f", f);
+    rec.samples = {"0/1:" + std::to_string(t_ref) + "," + std::to_string(t_alt) + ":" + taf,
+                   "0/0:" + std::to_string(n_ref) + "," + std::to_string(n_alt) + ":0.000"};
+    calls.push_back(rec);
+  }
+}
+
+}  // namespace
+
+CallerStats call_intervals(const Reference& ref, const std::string& bam, const std::string& normal_bam,
+                           const std::vector<Interval>& intervals, const CallerOptions& opt, VcfWriter& out) {
+  CallerStats st;
+  const uint64_t t0 = now_us();
+  std::FILE* dump = opt.dump_path.empty() ? nullptr : std::fopen(opt.dump_path.c_str(), "ab");
+  std::vector<VcfRecord> calls;
+  std::vector<std::unique_ptr<Region>> pending;
+  std::vector<std::tuple<int64_t, int64_t, std::string>> own;  // per pending region: owned range + chrom
+  auto flush = [&] {
+    if (pending.empty()) return;
+    run_phmm(pending, opt, st, dump);
+    for (size_t i = 0; i < pending.size(); ++i) {
+      const auto& [ob, oe, chrom] = own[i];
+      if (opt.somatic) genotype_somatic(*pending[i], opt, ob, oe, chrom, calls);
+      else genotype_germline(*pending[i], opt, ob, oe, chrom, calls);
+    }
+    pending.clear();
+    own.clear();
+  };
+  for (const Interval& iv : intervals) {
+    const int ci = ref.index(iv.chrom);
+    if (ci < 0) throw invalidParam("interval contig " + iv.chrom + " is not in the reference");
+    const std::string& seq = ref.contigs[ci].seq;
+    const int64_t L = (int64_t)seq.size();
+    const int64_t own_beg = std::max<int64_t>(0, iv.lb - 1), own_end = std::min<int64_t>(L, iv.ub);
+    if (own_beg >= own_end) continue;
+    const int64_t wb = std::max<int64_t>(0, own_beg - opt.max_region), we = std::min<int64_t>(L, own_end + opt.max_region);
+    std::vector<Read> reads[2];
+    load_reads(bam, iv.chrom, wb, we, opt, reads[0]);
+    if (opt.somatic) load_reads(normal_bam, iv.chrom, wb, we, opt, reads[1]);
+    st.reads += (int64_t)(reads[0].size() + reads[1].size());
+    Pileup pu;
+    pu.wb = wb;
+    pu.depth.assign(we - wb, 0);
+    pu.events.assign(we - wb, 0);
+    build_pileup(seq, reads[0], opt.min_base_quality, pu);
+    if (opt.somatic) build_pileup(seq, reads[1], opt.min_base_quality, pu);
+    // ---- active sites → regions
+    std::vector<int64_t> sites;
+    for (int64_t p = wb; p < we; ++p) {
+      const int ev = pu.events[p - wb], dp = std::max(1, pu.depth[p - wb]);
+      if (ev >= 2 && ev >= opt.active_fraction * dp) sites.push_back(p);
+    }
+    size_t i = 0;
+    while (i < sites.size()) {
+      size_t j = i;
+      while (j + 1 < sites.size() && sites[j + 1] <= sites[j] + opt.padding) ++j;
+      const int64_t first = sites[i], last = sites[j];
+      i = j + 1;
+      if (first < own_beg || first >= own_end) continue;  // another shard owns this region
+      for (int64_t rb = std::max<int64_t>(0, first - opt.padding); rb < std::min<int64_t>(L, last + opt.padding + 1);
+           rb += opt.max_region) {
+        auto g = std::make_unique<Region>();
+        g->beg = rb;
+        g->end = std::min<int64_t>({L, last + opt.padding + 1, rb + opt.max_region});
+        // candidates: supported by >= 2 reads and a fraction of the depth
+        std::vector<std::pair<int, Allele>> cs;
+        for (auto it = pu.support.lower_bound({g->beg, "", ""}); it != pu.support.end() && it->first.pos < g->end; ++it) {
+          const int dp = std::max(1, pu.depth[it->first.pos - wb]);
+          if (it->first.ref_end() > g->end) continue;
+          if (it->second >= 2 && it->second >= (opt.somatic ? 0.05 : 0.1) * dp) cs.emplace_back(it->second, it->first);
+        }
+        if (cs.empty()) continue;
+        std::stable_sort(cs.begin(), cs.end(), [](const auto& a, const auto& b) { return a.first > b.first; });
+        if ((int)cs.size() > kMaxCandidates) cs.resize(kMaxCandidates);
+        for (auto& c : cs) g->cands.push_back(c.second);
+        std::sort(g->cands.begin(), g->cands.end());
+        build_haplotypes(seq, *g);
+        // reads clipped to the window, GATK-prepared, deterministic downsampling
+        for (int s = 0; s < (opt.somatic ? 2 : 1); ++s) {
+          std::vector<const Read*> ov;
+          for (const Read& rd : reads[s])
+            if (rd.pos < g->end && rd.end > g->beg) ov.push_back(&rd);
+          const size_t cap = (size_t)opt.max_reads_per_region;
+          const double stride = ov.size() > cap ? (double)ov.size() / cap : 1.0;
+          for (double x = 0; (size_t)x < ov.size() && g->reads[s].size() < cap; x += stride) {
+            const Read& rd = *ov[(size_t)x];
+            size_t qs, qe;
+            if (!clip_to_window(rd, g->beg, g->end, qs, qe) || qe - qs < 20) continue;
+            std::vector<uint8_t> q(rd.qual.begin() + qs, rd.qual.begin() + qe);
+            PreparedRead pr;
+            gatk_prepare_read(rd.seq.substr(qs, qe - qs), q, rd.bi.empty() ? "" : rd.bi.substr(qs, qe - qs),
+                              rd.bd.empty() ? "" : rd.bd.substr(qs, qe - qs), rd.mapq, pr,
+                              opt.base_quality_threshold);
+            g->reads[s].push_back(std::move(pr));
+          }
+        }
+        if (g->reads[0].empty()) continue;
+        ++st.regions;
+        pending.push_back(std::move(g));
+        own.emplace_back(own_beg, own_end, iv.chrom);
+        if ((int)pending.size() >= opt.batch_regions) flush();
+      }
+    }
+    flush();
+  }
+  flush();
+  if (dump) std::fclose(dump);
+  std::stable_sort(calls.begin(), calls.end(), [&](const VcfRecord& a, const VcfRecord& b) {
+    const int ia = ref.index(a.chrom), ib = ref.index(b.chrom);
+    return ia != ib ? ia < ib : a.pos < b.pos;
+  });
+  for (const VcfRecord& r : calls) out.write(r);
+  st.calls = (int64_t)calls.size();
+  st.seconds = (now_us() - t0) / 1e6;
+  return st;
+}
+
+VcfHeader caller_vcf_header(const Reference& ref, const std::vector<std::string>& samples, bool somatic,
+                            const std::string& ref_path) {
+  VcfHeader h;
+  for (const Contig& c : ref.contigs) h.contigs.emplace_back(c.name, (int64_t)c.seq.size());
+  h.samples = samples;
+  h.reference = ref_path;
+  h.source = somatic ? "fcs-genome mutect2 (GPU PairHMM)" : "fcs-genome htc (GPU PairHMM)";
+  if (somatic) {
+    h.meta = {"##INFO=<ID=TLOD,Number=1,Type=Float,Description=\"Log10 likelihood ratio of the variant in the tumor\">",
+              "##INFO=<ID=NLOD,Number=1,Type=Float,Description=\"Log10 likelihood ratio of the normal being reference\">",
+              "##FORMAT=<ID=GT,Number=1,Type=String,Description=\"Genotype\">",
+              "##FORMAT=<ID=AD,Number=R,Type=Integer,Description=\"Allelic depths (informative reads)\">",
+              "##FORMAT=<ID=AF,Number=A,Type=Float,Description=\"Allele fraction\">",
+              "##FILTER=<ID=PASS,Description=\"All filters passed\">"};
+  } else {
+    h.meta = {"##INFO=<ID=DP,Number=1,Type=Integer,Description=\"Reads in the active region\">",
+              "##FORMAT=<ID=GT,Number=1,Type=String,Description=\"Genotype\">",
+              "##FORMAT=<ID=AD,Number=R,Type=Integer,Description=\"Allelic depths (informative reads)\">",
+              "##FORMAT=<ID=DP,Number=1,Type=Integer,Description=\"Read depth\">",
+              "##FORMAT=<ID=GQ,Number=1,Type=Integer,Description=\"Genotype quality\">",
+              "##FORMAT=<ID=PL,Number=G,Type=Integer,Description=\"Phred-scaled genotype likelihoods\">",
+              "##FILTER=<ID=PASS,Description=\"All filters passed\">"};
+  }
+  return h;
+}
+
+}  // namespace fcsg

@@ -1,0 +1,62 @@
+// Caller side of the PairHMM for `fcs-genome htc` / `mutect2` (SURVEY.md §8f
+// row f2): per interval shard, find active regions from the pileup, build
+// candidate haplotypes, prepare reads the GATK way (gatk_prep.h), send many
+// regions per device pass through fcs_phmm_compute_regions (the hot path,
+// include/fcship.h), scatter the read-major likelihood matrices back and
+// genotype from them.
+//
+// What stands in for GATK here [EXT, not in /root/reference]: haplotypes come
+// from the candidate alleles seen in the reads (every combination of up to
+// kMaxCandidates alleles per region) instead of GATK's local de-Bruijn
+// assembly, genotypes from the standard diploid read-likelihood model
+// (GATK's GenotypingEngine with the default heterozygosity prior), and the
+// Mutect2 mode from the tumor/normal LOD test (TLOD >= 6.3, NLOD >= 2.2).  The
+// likelihoods themselves are GKL's PairHMM, bit-for-bit the hot-path kernels.
+#pragma once
+
+#include <cstdint>
+#include <string>
+#include <vector>
+
+#include "fasta.h"
+#include "intervals.h"
+#include "vcf.h"
+
+namespace fcsg {
+
+constexpr int kMaxCandidates = 4;  // haplotypes = all 2^k allele combinations
+
+struct CallerOptions {
+  int gpu = 0;
+  bool somatic = false;  // Mutect2 mode (tumor BAM + normal BAM)
+  int min_base_quality = 10;
+  int base_quality_threshold = 18;
+  int min_mapq = 20;
+  double active_fraction = 0.15;
+  int padding = 50;
+  int max_region = 300;
+  int max_reads_per_region = 250;
+  int batch_regions = 4096;
+  bool fp64_rescue = true;
+  double min_qual = 30.0;  // stand_call_conf
+  double tlod = 6.3, nlod = 2.2;
+  std::string dump_path;  // if set: append every region's PairHMM inputs/outputs here (tests)
+};
+
+struct CallerStats {
+  int64_t reads = 0, regions = 0, pairs = 0, cells = 0, calls = 0, device_passes = 0;
+  double seconds = 0, phmm_seconds = 0;
+  void add(const CallerStats& o);
+};
+
+// Calls variants of `bam` (tumor BAM in Mutect2 mode, with `normal_bam`) on
+// the intervals; records with POS inside an interval are written to `out` in
+// coordinate order.
+CallerStats call_intervals(const Reference& ref, const std::string& bam, const std::string& normal_bam,
+                           const std::vector<Interval>& intervals, const CallerOptions& opt, VcfWriter& out);
+
+// Header of the caller's VCF (FORMAT/INFO definitions, contigs, samples).
+VcfHeader caller_vcf_header(const Reference& ref, const std::vector<std::string>& samples, bool somatic,
+                            const std::string& ref_path);
+
+}  // namespace fcsg

@@ -1,0 +1,217 @@
+// extern "C" hooks of libfcsgenome.so for the Python tests (tests/test_host_*.py):
+// the host pieces with exact expected outputs — GATK read preparation,
+// interval partitioning, BGZF, BAM record coding, BAI/TBI building, the
+// executor's stage/error semantics.  Not part of the hot-path ABI (include/fcship.h).
+#include <cstring>
+#include <functional>
+#include <string>
+
+#include "bam.h"
+#include "bgzf.h"
+#include "common.h"
+#include "config.h"
+#include "executor.h"
+#include "fasta.h"
+#include "gatk_prep.h"
+#include "intervals.h"
+#include "vcf.h"
+
+using namespace fcsg;
+
+namespace {
+thread_local std::string g_err;
+int guard(const std::function<void()>& fn) {
+  try {
+    fn();
+    return 0;
+  } catch (const std::exception& e) {
+    g_err = e.what();
+    return -1;
+  }
+}
+int copy_out(const std::string& s, char* buf, int cap) {
+  if ((int)s.size() + 1 > cap) return -(int)s.size() - 1;
+  std::memcpy(buf, s.c_str(), s.size() + 1);
+  return (int)s.size();
+}
+}  // namespace
+
+extern "C" {
+
+const char* fcsg_last_error() { return g_err.c_str(); }
+
+int fcsg_prepare_read(const char* bases, const uint8_t* quals, int len, const char* bi, const char* bd, int mapq,
+                      int threshold, uint8_t* bq, uint8_t* iq, uint8_t* dq, uint8_t* gcp) {
+  return guard([&] {
+    PreparedRead pr;
+    gatk_prepare_read(std::string(bases, len), std::vector<uint8_t>(quals, quals + len), bi ? std::string(bi) : "",
+                      bd ? std::string(bd) : "", mapq, pr, threshold);
+    std::memcpy(bq, pr.base_q.data(), len);
+    std::memcpy(iq, pr.ins_q.data(), len);
+    std::memcpy(dq, pr.del_q.data(), len);
+    std::memcpy(gcp, pr.gcp.data(), len);
+  });
+}
+
+// "shard\tchrom\tlb\tub\n" lines of the init_contig_intv partition of a .dict.
+int fcsg_partition_dict(const char* dict_path, int ncontigs, int skip_pseudo, char* buf, int cap) {
+  int rc = 0;
+  const int g = guard([&] {
+    const auto parts = partition_contigs(read_dict(dict_path), ncontigs, skip_pseudo != 0);
+    std::string s;
+    for (size_t k = 0; k < parts.size(); ++k)
+      for (const Interval& iv : parts[k])
+        s += std::to_string(k) + "\t" + iv.chrom + "\t" + std::to_string(iv.lb) + "\t" + std::to_string(iv.ub) + "\n";
+    rc = copy_out(s, buf, cap);
+  });
+  return g ? g : rc;
+}
+
+int fcsg_bgzf_compress_file(const char* in, const char* out) {
+  return guard([&] { bgzip_file(in, out); });
+}
+
+// Decompress a BGZF file with the library's reader (tests compare with Python's gzip).
+int fcsg_bgzf_decompress_file(const char* in, const char* out) {
+  return guard([&] {
+    BgzfReader r(in);
+    std::string all;
+    char buf[1 << 16];
+    for (size_t n; (n = r.read(buf, sizeof buf)) > 0;) all.append(buf, n);
+    write_file(out, all);
+  });
+}
+
+// BAM → SAM-like text (one line per record) with the library's reader.
+int fcsg_bam_to_text(const char* bam, const char* out) {
+  return guard([&] {
+    BamReader r(bam);
+    std::string s;
+    for (size_t i = 0; i < r.header().names.size(); ++i)
+      s += "@SQ\t" + r.header().names[i] + "\t" + std::to_string(r.header().lengths[i]) + "\n";
+    BamRecord rec;
+    while (r.next(rec)) {
+      std::string q;
+      for (uint8_t x : rec.qual) q += (char)(x + 33);
+      std::string md;
+      int64_t nm = -1;
+      rec.get_aux_string("MD", md);
+      rec.get_aux_int("NM", nm);
+      s += rec.name + "\t" + std::to_string(rec.flag) + "\t" + std::to_string(rec.ref_id) + "\t" +
+           std::to_string(rec.pos) + "\t" + std::to_string(rec.mapq) + "\t" + cigar_string(rec.cigar) + "\t" + rec.seq +
+           "\t" + (q.empty() ? "*" : q) + "\t" + md + "\t" + std::to_string(nm) + "\n";
+    }
+    write_file(out, s);
+  });
+}
+
+// SAM-like text (name flag ref_id pos mapq cigar seq qual) → BAM with the library's writer.
+int fcsg_text_to_bam(const char* text, const char* bam, const char* names_csv, const char* lengths_csv) {
+  return guard([&] {
+    BamHeader h;
+    std::string nm = names_csv, ln = lengths_csv;
+    for (size_t p = 0; p < nm.size();) {
+      const size_t e = std::min(nm.find(',', p), nm.size());
+      h.names.push_back(nm.substr(p, e - p));
+      p = e + 1;
+    }
+    for (size_t p = 0; p < ln.size();) {
+      const size_t e = std::min(ln.find(',', p), ln.size());
+      h.lengths.push_back(std::stoll(ln.substr(p, e - p)));
+      p = e + 1;
+    }
+    for (size_t i = 0; i < h.names.size(); ++i)
+      h.text += "@SQ\tSN:" + h.names[i] + "\tLN:" + std::to_string(h.lengths[i]) + "\n";
+    BamWriter w(bam, h);
+    std::string body = read_file(text);
+    size_t p = 0;
+    while (p < body.size()) {
+      const size_t e = std::min(body.find('\n', p), body.size());
+      const std::string line = body.substr(p, e - p);
+      p = e + 1;
+      if (line.empty()) continue;
+      std::vector<std::string> f;
+      for (size_t a = 0; a <= line.size();) {
+        const size_t b = std::min(line.find('\t', a), line.size());
+        f.push_back(line.substr(a, b - a));
+        a = b + 1;
+      }
+      if (f.size() < 8) throw formatError("text record needs 8 fields");
+      BamRecord r;
+      r.name = f[0];
+      r.flag = (uint16_t)std::stoi(f[1]);
+      r.ref_id = std::stoi(f[2]);
+      r.pos = std::stoi(f[3]);
+      r.mapq = (uint8_t)std::stoi(f[4]);
+      r.cigar = parse_cigar(f[5]);
+      r.seq = f[6];
+      if (f[7] != "*")
+        for (char c : f[7]) r.qual.push_back((uint8_t)(c - 33));
+      w.write(r);
+    }
+    w.close();
+  });
+}
+
+int fcsg_bam_index(const char* bam) {
+  return guard([&] { bam_index_build(bam); });
+}
+
+int fcsg_bam_seek_offset(const char* bai, int tid, long long beg, unsigned long long* off) {
+  return guard([&] { *off = BamIndex(bai).seek_offset(tid, beg); });
+}
+
+int fcsg_vcf_concat(const char* const* inputs, int n, const char* output) {
+  return guard([&] { vcf_concat(std::vector<std::string>(inputs, inputs + n), output); });
+}
+
+int fcsg_tabix(const char* vcf_gz) {
+  return guard([&] { tabix_index_vcf(vcf_gz); });
+}
+
+unsigned fcsg_reg2bin(long long beg, long long end) { return reg2bin(beg, end); }
+
+// Runs an executor with n_tasks shell-command workers (cmd per task, %d = task
+// index) over n_threads threads and GPU slots gpus_csv; writes the per-task
+// FCS_GPU_DEVICE seen by each command into its own output.  Returns the
+// exception class on failure: 0 ok, 4 failedCommand, 1 other; findError text in buf.
+int fcsg_run_stage(const char* cmd_fmt, int n_tasks, int n_threads, const char* gpus_csv, const char* log_dir,
+                   char* buf, int cap) {
+  try {
+    conf().init("");
+    conf().set("log_dir", log_dir);
+    std::vector<int> gpus;
+    std::string g = gpus_csv;
+    for (size_t p = 0; p < g.size();) {
+      const size_t e = std::min(g.find(',', p), g.size());
+      if (e > p) gpus.push_back(std::stoi(g.substr(p, e - p)));
+      p = e + 1;
+    }
+    class Cmd : public Worker {
+     public:
+      explicit Cmd(std::string c) : Worker(1, 1, {}, "test stage") { cmd_ = std::move(c); }
+    };
+    Executor ex("test", n_threads, gpus);
+    for (int i = 0; i < n_tasks; ++i) {
+      char c[4096];
+      std::snprintf(c, sizeof c, cmd_fmt, i);
+      ex.addTask(std::make_shared<Cmd>(c), "");
+    }
+    ex.run();
+    copy_out("", buf, cap);
+    return 0;
+  } catch (const failedCommand&) {
+    copy_out(g_err, buf, cap);
+    return 4;
+  } catch (const std::exception& e) {
+    g_err = e.what();
+    copy_out(g_err, buf, cap);
+    return 1;
+  }
+}
+
+int fcsg_find_error(const char* const* logs, int n, char* buf, int cap) {
+  return copy_out(LogUtils::findError(std::vector<std::string>(logs, logs + n)), buf, cap);
+}
+
+}  // extern "C"

@@ -1,0 +1,91 @@
+#include "common.h"
+
+#include <dirent.h>
+#include <sys/stat.h>
+#include <unistd.h>
+
+#include <algorithm>
+#include <cerrno>
+#include <cstdio>
+#include <cstring>
+#include <fstream>
+#include <sstream>
+
+namespace fcsg {
+
+bool path_exists(const std::string& p) {
+  struct stat st;
+  return ::stat(p.c_str(), &st) == 0;
+}
+
+bool is_regular_file(const std::string& p) {
+  struct stat st;
+  return ::stat(p.c_str(), &st) == 0 && S_ISREG(st.st_mode);
+}
+
+bool is_directory(const std::string& p) {
+  struct stat st;
+  return ::stat(p.c_str(), &st) == 0 && S_ISDIR(st.st_mode);
+}
+
+void create_dir(const std::string& p) {
+  if (p.empty()) return;
+  std::string cur;
+  std::stringstream ss(p);
+  std::string part;
+  if (p[0] == '/') cur = "/";
+  while (std::getline(ss, part, '/')) {
+    if (part.empty()) continue;
+    cur += part + "/";
+    if (::mkdir(cur.c_str(), 0755) != 0 && errno != EEXIST)
+      throw internalError("[E::fcsg] cannot create directory " + cur + ": " + std::strerror(errno));
+  }
+}
+
+void remove_path(const std::string& p) {
+  if (is_directory(p)) {
+    if (DIR* d = ::opendir(p.c_str())) {
+      while (dirent* e = ::readdir(d)) {
+        const std::string n = e->d_name;
+        if (n == "." || n == "..") continue;
+        remove_path(p + "/" + n);
+      }
+      ::closedir(d);
+    }
+    ::rmdir(p.c_str());
+  } else {
+    ::unlink(p.c_str());
+  }
+}
+
+std::vector<std::string> list_dir(const std::string& p, const std::string& suffix) {
+  std::vector<std::string> out;
+  if (DIR* d = ::opendir(p.c_str())) {
+    while (dirent* e = ::readdir(d)) {
+      const std::string n = e->d_name;
+      if (n == "." || n == "..") continue;
+      if (!suffix.empty() && (n.size() < suffix.size() || n.compare(n.size() - suffix.size(), suffix.size(), suffix)))
+        continue;
+      out.push_back(p + "/" + n);
+    }
+    ::closedir(d);
+  }
+  std::sort(out.begin(), out.end());
+  return out;
+}
+
+std::string read_file(const std::string& p) {
+  std::ifstream in(p, std::ios::binary);
+  if (!in) throw fileNotFound(p);
+  std::ostringstream ss;
+  ss << in.rdbuf();
+  return ss.str();
+}
+
+void write_file(const std::string& p, const std::string& data) {
+  std::ofstream out(p, std::ios::binary);
+  if (!out) throw fileNotFound(p + " (cannot write)");
+  out << data;
+}
+
+}  // namespace fcsg

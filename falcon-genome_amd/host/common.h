@@ -1,0 +1,80 @@
+// Shared host-side definitions of the fcs-genome orchestrator (SURVEY.md §8f
+// row f1): the error types the reference's drivers throw and catch
+// (/root/reference/include/fcs-genome/common.h:27-67), file-name helpers
+// (get_contig_fname, :232-245) and timing.
+#pragma once
+
+#include <chrono>
+#include <cstdint>
+#include <iomanip>
+#include <sstream>
+#include <stdexcept>
+#include <string>
+#include <vector>
+
+namespace fcsg {
+
+// Exit codes of `fcs-genome` (reference main.cpp: helpRequest → 0 after help,
+// invalidParam/pathEmpty/fileNotFound → 1, failedCommand → 4, internal → 3).
+class helpRequest : public std::runtime_error {
+ public:
+  helpRequest() : std::runtime_error("") {}
+};
+class silentExit : public std::runtime_error {
+ public:
+  silentExit() : std::runtime_error("") {}
+};
+class invalidParam : public std::runtime_error {
+ public:
+  explicit invalidParam(const std::string& what) : std::runtime_error("Invalid parameter: " + what) {}
+};
+class fileNotFound : public std::runtime_error {
+ public:
+  explicit fileNotFound(const std::string& what) : std::runtime_error("Cannot find " + what) {}
+};
+class failedCommand : public std::runtime_error {
+ public:
+  explicit failedCommand(const std::string& what) : std::runtime_error(what) {}
+};
+class internalError : public std::runtime_error {
+ public:
+  explicit internalError(const std::string& what) : std::runtime_error(what) {}
+};
+class pathEmpty : public std::runtime_error {
+ public:
+  explicit pathEmpty(const std::string& what) : std::runtime_error("Path of " + what + " is empty") {}
+};
+class formatError : public std::runtime_error {
+ public:
+  explicit formatError(const std::string& what) : std::runtime_error("[E::fcsg] " + what) {}
+};
+
+inline uint64_t now_us() {
+  return (uint64_t)std::chrono::duration_cast<std::chrono::microseconds>(
+             std::chrono::steady_clock::now().time_since_epoch())
+      .count();
+}
+
+// <base>/<prefix><contig as 6 digits>.<ext> — the reference's per-shard file naming.
+inline std::string get_contig_fname(const std::string& base, int contig, const std::string& ext = "bam",
+                                    const std::string& prefix = "part-") {
+  std::ostringstream ss;
+  ss << base << "/" << prefix << std::setw(6) << std::setfill('0') << contig << "." << ext;
+  return ss.str();
+}
+
+inline std::string basename_of(const std::string& path) {
+  const size_t k = path.find_last_of('/');
+  return k == std::string::npos ? path : path.substr(k + 1);
+}
+
+bool path_exists(const std::string& p);
+bool is_regular_file(const std::string& p);
+bool is_directory(const std::string& p);
+void create_dir(const std::string& p);   // mkdir -p
+void remove_path(const std::string& p);  // rm -rf
+std::vector<std::string> list_dir(const std::string& p, const std::string& suffix = "");
+std::string read_file(const std::string& p);
+void write_file(const std::string& p, const std::string& data);
+
+}  // namespace fcsg

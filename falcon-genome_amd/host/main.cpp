@@ -1,0 +1,330 @@
+// fcs-genome command line: the reference's CLI surface
+// for the GPU-backed commands — `htc`, `mutect2`, `align` — with its option
+// names (src/worker-htc.cpp:25-33, src/worker-mutect2.cpp:26-40,
+// src/worker-align.cpp:29-42), config keys (`conf`) and exit codes
+// (src/main.cpp:165-240: help 0, bad option 1/2, missing file 3, failed
+// stage 4, other error -1), plus `synth` for the synthetic C1/C4/C5 inputs.
+#include <cstring>
+#include <iostream>
+#include <map>
+#include <memory>
+#include <string>
+#include <vector>
+
+#include "common.h"
+#include "config.h"
+#include "executor.h"
+#include "fcship.h"
+#include "intervals.h"
+#include "synth.h"
+#include "workers.h"
+
+namespace fcsg {
+
+int align_main(int argc, char** argv);  // align.cpp
+
+namespace {
+
+// Minimal boost::program_options stand-in: long/short options with values or flags.
+class Args {
+ public:
+  struct Opt {
+    std::string lng, shrt, help;
+    bool flag, required;
+  };
+  void add(const std::string& lng, const std::string& shrt, bool flag, bool required, const std::string& help) {
+    opts_.push_back({lng, shrt, help, flag, required});
+  }
+  void parse(int argc, char** argv) {
+    for (int i = 1; i < argc; ++i) {
+      std::string a = argv[i];
+      if (a == "-h" || a == "--help") throw helpRequest();
+      const Opt* o = nullptr;
+      std::string val;
+      bool has_val = false;
+      for (const Opt& x : opts_) {
+        if (a == "--" + x.lng || (!x.shrt.empty() && a == "-" + x.shrt)) o = &x;
+        else if (a.rfind("--" + x.lng + "=", 0) == 0) {
+          o = &x;
+          val = a.substr(x.lng.size() + 3);
+          has_val = true;
+        }
+        if (o) break;
+      }
+      if (!o) throw invalidParam(a);
+      if (o->flag) {
+        vals_[o->lng].push_back("1");
+        continue;
+      }
+      if (!has_val) {
+        if (i + 1 >= argc) throw invalidParam(a + " needs a value");
+        val = argv[++i];
+      }
+      vals_[o->lng].push_back(val);
+    }
+    for (const Opt& x : opts_)
+      if (x.required && !vals_.count(x.lng)) throw invalidParam("--" + x.lng + " is required");
+  }
+  bool has(const std::string& k) const { return vals_.count(k) > 0; }
+  std::string get(const std::string& k, const std::string& def = "") const {
+    auto it = vals_.find(k);
+    if (it == vals_.end()) return def;
+    if (it->second.back().empty()) throw pathEmpty(k);
+    return it->second.back();
+  }
+  std::vector<std::string> all(const std::string& k) const {
+    auto it = vals_.find(k);
+    return it == vals_.end() ? std::vector<std::string>{} : it->second;
+  }
+  std::string help() const {
+    std::string s;
+    for (const Opt& x : opts_)
+      s += "  " + (x.shrt.empty() ? std::string("    ") : "-" + x.shrt + ", ") + "--" + x.lng +
+           (x.flag ? "" : " arg") + "\t" + x.help + "\n";
+    return s;
+  }
+
+ private:
+  std::vector<Opt> opts_;
+  std::map<std::string, std::vector<std::string>> vals_;
+};
+
+void common_opts(Args& a) {
+  a.add("force", "f", true, false, "overwrite output files if they exist");
+  a.add("extra-options", "O", false, false, "extra options for the command");
+}
+
+std::vector<int> slots() {
+  std::vector<int> g = conf().gpu_devices();
+  if (g.empty()) throw failedCommand("[E::fcs-genome] no GPU visible (gpu.devices); the GPU path has no CPU fallback");
+  return g;
+}
+
+// Shards of the run: -L list (one file for all shards) or the reference's 32 interval parts.
+std::vector<std::vector<std::string>> shard_intervals(const std::string& ref, const std::string& intv_list) {
+  const int n = conf().get_int("gatk.ncontigs");
+  std::vector<std::vector<std::string>> out(n);
+  if (!intv_list.empty()) {
+    // split the user's list into n shard files, contig order preserved
+    const auto iv = read_interval_list(intv_list);
+    std::vector<std::pair<std::string, int64_t>> pseudo;  // (name, length) of each listed interval
+    for (const Interval& i : iv) pseudo.emplace_back(i.chrom, i.ub - i.lb + 1);
+    const auto parts = partition_contigs(pseudo, n, false);
+    const std::string dir = conf().temp_dir() + "/intv_user";
+    create_dir(dir);
+    for (int k = 0; k < n; ++k) {
+      std::vector<Interval> shifted;
+      for (const Interval& p : parts[k]) {
+        // map back: pseudo-contig i starts at iv[i].lb
+        for (const Interval& src : iv)
+          if (src.chrom == p.chrom && p.lb - 1 + src.lb <= src.ub) {
+            shifted.push_back({src.chrom, src.lb + p.lb - 1, src.lb + p.ub - 1});
+            break;
+          }
+      }
+      const std::string path = get_contig_fname(dir, k, "list", "part-");
+      write_interval_list(path, shifted);
+      out[k].push_back(path);
+    }
+    return out;
+  }
+  const auto paths = init_contig_intv(ref, n, conf().temp_dir(), conf().get_bool("gatk.skip_pseudo_chr"));
+  for (int k = 0; k < n; ++k) out[k].push_back(paths[k]);
+  return out;
+}
+
+int htc_main(int argc, char** argv) {
+  Args a;
+  common_opts(a);
+  a.add("ref", "r", false, true, "reference genome path");
+  a.add("input", "i", false, true, "input BAM file");
+  a.add("output", "o", false, true, "output VCF file (<output>.gz + .tbi are written too)");
+  a.add("produce-vcf", "v", true, false, "produce VCF (the only mode: GVCF blocks are not emitted)");
+  a.add("intervalList", "L", false, false, "interval list file");
+  a.add("sample-id", "", false, false, "sample id for log files");
+  a.add("skip-concat", "s", true, false, "(deprecated) produce a set of VCF files instead of one");
+  a.add("gatk4", "g", true, false, "accepted for compatibility");
+  a.add("dump-regions", "", false, false, "debug: write every region's PairHMM inputs/outputs to <path>.<shard>");
+  try {
+    a.parse(argc, argv);
+  } catch (helpRequest&) {
+    std::cerr << "'fcs-genome htc' options:\n" << a.help();
+    throw;
+  }
+  const std::string ref = a.get("ref"), input = a.get("input"), output = a.get("output");
+  const bool force = a.has("force");
+  const std::string sample_id = a.get("sample-id");
+  std::vector<std::string> extra = a.all("extra-options");
+  if (a.has("dump-regions")) extra.push_back("--dump-regions " + a.get("dump-regions"));
+  const std::vector<int> gpus = slots();
+  const std::string out_dir = conf().temp_dir() + "/htc";
+  create_dir(out_dir);
+  const auto shards = shard_intervals(ref, a.get("intervalList"));
+  BackgroundExecutor warm("gpu-warmup", std::make_shared<DeviceWarmupWorker>(gpus));
+  Executor ex("Haplotype Caller", conf().get_int("gatk.htc.nprocs", "gatk.nprocs"), gpus);
+  std::vector<std::string> parts;
+  warm.wait();
+  if (warm.status() != 0) throw failedCommand(std::string("[E::fcs-genome] GPU warm-up failed: ") + fcs_last_error());
+  for (size_t k = 0; k < shards.size(); ++k) {
+    const std::string part = get_contig_fname(out_dir, (int)k, "vcf");
+    parts.push_back(part);
+    ex.addTask(std::make_shared<HTCWorker>(ref, shards[k], input, part, extra, (int)k, true, true), sample_id);
+  }
+  const std::string plain = output;
+  ex.addTask(std::make_shared<VCFConcatWorker>(parts, plain), sample_id, true);
+  if (!a.has("skip-concat")) {
+    if (!force && path_exists(plain + ".gz")) throw invalidParam("output " + plain + ".gz exists (use -f)");
+    ex.addTask(std::make_shared<ZIPWorker>(plain, plain + ".gz", force), sample_id, true);
+    ex.addTask(std::make_shared<TabixWorker>(plain + ".gz"), sample_id, true);
+  }
+  ex.run();
+  return 0;
+}
+
+int mutect2_main(int argc, char** argv) {
+  Args a;
+  common_opts(a);
+  a.add("ref", "r", false, true, "reference genome path");
+  a.add("normal", "n", false, true, "input normal BAM file");
+  a.add("tumor", "t", false, true, "input tumor BAM file");
+  a.add("output", "o", false, true, "output VCF file");
+  a.add("intervalList", "L", false, false, "interval list file");
+  a.add("normal_name", "a", false, false, "normal sample name");
+  a.add("tumor_name", "b", false, false, "tumor sample name");
+  a.add("sample-id", "", false, false, "sample id for log file");
+  for (const char* k : {"dbsnp", "cosmic", "germline", "panels_of_normals", "contamination_table", "filtered_vcf"})
+    a.add(k, "", false, false, "accepted for compatibility (not used by the GPU caller)");
+  try {
+    a.parse(argc, argv);
+  } catch (helpRequest&) {
+    std::cerr << "'fcs-genome mutect2' options:\n" << a.help();
+    throw;
+  }
+  const std::string ref = a.get("ref"), output = a.get("output");
+  const std::vector<int> gpus = slots();
+  const std::string out_dir = conf().temp_dir() + "/mutect2";
+  create_dir(out_dir);
+  const auto shards = shard_intervals(ref, a.get("intervalList"));
+  Executor ex("Mutect2", conf().get_int("gatk.mutect2.nprocs", "gatk.nprocs"), gpus);
+  std::vector<std::string> parts;
+  const std::string sample_id = a.get("sample-id");
+  for (size_t k = 0; k < shards.size(); ++k) {
+    const std::string part = get_contig_fname(out_dir, (int)k, "vcf");
+    parts.push_back(part);
+    ex.addTask(std::make_shared<Mutect2Worker>(ref, shards[k], a.get("normal"), a.get("tumor"), part,
+                                               a.all("extra-options"), (int)k, true),
+               sample_id);
+  }
+  ex.addTask(std::make_shared<VCFConcatWorker>(parts, output), sample_id, true);
+  ex.addTask(std::make_shared<ZIPWorker>(output, output + ".gz", true), sample_id, true);
+  ex.addTask(std::make_shared<TabixWorker>(output + ".gz"), sample_id, true);
+  ex.run();
+  return 0;
+}
+
+int synth_main(int argc, char** argv) {
+  Args a;
+  a.add("output", "o", false, true, "output directory");
+  a.add("contigs", "c", false, false, "name:length[,name:length...] (default chr20:1000000)");
+  a.add("coverage", "x", false, false, "sample coverage (default 30)");
+  a.add("seed", "s", false, false, "seed (default 20261015)");
+  a.add("max-reads", "n", false, false, "keep only the first N reads by position (C1: 1000)");
+  a.add("tumor", "T", true, false, "also write tumor.bam with somatic variants (C5)");
+  a.add("tumor-coverage", "", false, false, "tumor coverage (default 40)");
+  a.add("somatic-af", "", false, false, "somatic allele fraction (default 0.3)");
+  a.parse(argc, argv);
+  SynthSpec sp;
+  if (a.has("contigs")) {
+    sp.contigs.clear();
+    std::string s = a.get("contigs");
+    size_t p = 0;
+    while (p < s.size()) {
+      const size_t e = std::min(s.find(',', p), s.size());
+      const std::string tok = s.substr(p, e - p);
+      const size_t c = tok.find(':');
+      if (c == std::string::npos) throw invalidParam("--contigs " + s);
+      sp.contigs.emplace_back(tok.substr(0, c), std::stoll(tok.substr(c + 1)));
+      p = e + 1;
+    }
+  }
+  if (a.has("coverage")) sp.coverage = std::stod(a.get("coverage"));
+  if (a.has("seed")) sp.seed = std::stoull(a.get("seed"));
+  if (a.has("max-reads")) sp.max_reads = std::stoll(a.get("max-reads"));
+  if (a.has("tumor")) sp.somatic_rate = 1e-4;
+  if (a.has("tumor-coverage")) sp.tumor_coverage = std::stod(a.get("tumor-coverage"));
+  if (a.has("somatic-af")) sp.somatic_af = std::stod(a.get("somatic-af"));
+  const SynthOutputs o = synth_dataset(sp, a.get("output"));
+  std::cout << "{\"ref\": \"" << o.ref_fasta << "\", \"bam\": \"" << o.bam << "\", \"fastq\": \"" << o.fastq
+            << "\", \"truth\": \"" << o.truth_vcf << "\", \"tumor_bam\": \"" << o.tumor_bam
+            << "\", \"reads\": " << o.n_reads << ", \"tumor_reads\": " << o.n_tumor_reads
+            << ", \"variants\": " << o.variants.size() << "}" << std::endl;
+  return 0;
+}
+
+int print_help() {
+  std::cout << "Falcon Genome Analysis Toolkit (MI355X / gfx950 build)\n"
+               "Usage: fcs-genome [command] <options>\n\nCommands:\n"
+               "  align           align FASTQ reads into a sorted BAM (GPU banded SW)\n"
+               "  htc             variant calling, HaplotypeCaller-style (GPU PairHMM)\n"
+               "  mutect2         somatic variant calling, tumor/normal (GPU PairHMM)\n"
+               "  conf            print configuration keys\n"
+               "  synth           write synthetic reference/BAM/FASTQ/truth inputs\n";
+  return 0;
+}
+
+}  // namespace
+}  // namespace fcsg
+
+int main(int argc, char** argv) {
+  using namespace fcsg;
+  if (argc < 2) {
+    print_help();
+    return 1;
+  }
+  std::string cmd = argv[1];
+  for (char& c : cmd) c = (char)std::tolower((unsigned char)c);
+  int ret = 0;
+  std::string root;
+  {
+    std::string self = argv[0];
+    const size_t k = self.find_last_of('/');
+    root = k == std::string::npos ? "." : self.substr(0, k) + "/..";
+  }
+  try {
+    conf().init(root);
+    if (cmd == "htc") ret = htc_main(argc - 1, argv + 1);
+    else if (cmd == "mutect2") ret = mutect2_main(argc - 1, argv + 1);
+    else if (cmd == "align" || cmd == "al") ret = align_main(argc - 1, argv + 1);
+    else if (cmd == "synth") ret = synth_main(argc - 1, argv + 1);
+    else if (cmd == "conf") {
+      std::cerr << "fcs-genome configuration options:\n" << conf().dump();
+      ret = 1;  // the reference exits through silentExit here
+    } else if (cmd == "--version") {
+      std::cout << "fcs-genome (gfx950) / " << fcs_version() << std::endl;
+    } else {
+      print_help();
+      ret = 1;
+    }
+    remove_path(conf().temp_dir());
+  } catch (helpRequest&) {
+    ret = 0;
+  } catch (invalidParam& e) {
+    std::cerr << "[fcs-genome] ERROR: Failed to parse arguments: invalid option " << e.what() << std::endl;
+    ret = 1;
+  } catch (pathEmpty& e) {
+    std::cerr << "[fcs-genome] ERROR: Failed to parse arguments: option " << e.what() << " cannot be empty" << std::endl;
+    ret = 1;
+  } catch (fileNotFound& e) {
+    std::cerr << "[fcs-genome] ERROR: " << e.what() << std::endl;
+    ret = 3;
+  } catch (silentExit&) {
+    ret = 1;
+  } catch (failedCommand& e) {
+    if (*e.what()) std::cerr << e.what() << std::endl;
+    ret = 4;
+  } catch (std::runtime_error& e) {
+    std::cerr << "[fcs-genome] ERROR: Encountered an error: " << e.what() << std::endl;
+    ret = -1;
+  }
+  return ret;
+}

@@ -1,0 +1,177 @@
+#include "workers.h"
+
+#include <map>
+#include <mutex>
+
+#include "common.h"
+#include "config.h"
+#include "fcship.h"
+#include "intervals.h"
+#include "vcf.h"
+
+namespace fcsg {
+
+std::shared_ptr<const Reference> load_reference_cached(const std::string& path) {
+  static std::mutex mu;
+  static std::map<std::string, std::shared_ptr<const Reference>> cache;
+  std::lock_guard<std::mutex> g(mu);
+  auto it = cache.find(path);
+  if (it != cache.end()) return it->second;
+  auto ref = std::make_shared<const Reference>(load_fasta(path));
+  cache[path] = ref;
+  return ref;
+}
+
+CallerOptions caller_options_from_config(int gpu) {
+  const Config& c = conf();
+  CallerOptions o;
+  o.gpu = gpu < 0 ? 0 : gpu;
+  o.min_base_quality = c.get_int("htc.min_base_quality");
+  o.base_quality_threshold = c.get_int("htc.base_quality_threshold");
+  o.min_mapq = c.get_int("htc.min_mapq");
+  o.active_fraction = std::stod(c.get_string("htc.active_fraction"));
+  o.padding = c.get_int("htc.padding");
+  o.max_region = c.get_int("htc.max_region");
+  o.max_reads_per_region = c.get_int("htc.max_reads_per_region");
+  o.batch_regions = c.get_int("gpu.phmm.batch_regions");
+  o.fp64_rescue = c.get_bool("gpu.phmm.rescue");
+  o.tlod = std::stod(c.get_string("mutect2.tlod"));
+  o.nlod = std::stod(c.get_string("mutect2.nlod"));
+  if (o.padding < 0 || o.max_region < 1 || o.batch_regions < 1 || o.max_reads_per_region < 1)
+    throw invalidParam("htc.padding / htc.max_region / gpu.phmm.batch_regions / htc.max_reads_per_region");
+  return o;
+}
+
+static std::vector<Interval> read_all(const std::vector<std::string>& paths) {
+  std::vector<Interval> out;
+  for (const std::string& p : paths) {
+    const auto iv = read_interval_list(p);
+    out.insert(out.end(), iv.begin(), iv.end());
+  }
+  return out;
+}
+
+// ------------------------------------------------------------------ HTC
+HTCWorker::HTCWorker(std::string ref_path, std::vector<std::string> intv_paths, std::string input_path,
+                     std::string output_path, std::vector<std::string> extra_opts, int contig, bool flag_vcf,
+                     bool flag_f, bool /*flag_gatk*/)
+    : Worker(1, 1, std::move(extra_opts), "Haplotype Caller"),
+      ref_path_(std::move(ref_path)),
+      input_path_(std::move(input_path)),
+      output_path_(std::move(output_path)),
+      intv_paths_(std::move(intv_paths)),
+      contig_(contig),
+      flag_vcf_(flag_vcf),
+      flag_f_(flag_f) {}
+
+void HTCWorker::check() {
+  if (!is_regular_file(ref_path_)) throw fileNotFound(ref_path_);
+  if (!is_regular_file(input_path_)) throw fileNotFound(input_path_);
+  for (const std::string& p : intv_paths_)
+    if (!is_regular_file(p)) throw fileNotFound(p);
+  if (!flag_f_ && path_exists(output_path_)) throw invalidParam("output " + output_path_ + " exists (use -f)");
+}
+
+int HTCWorker::run(TaskContext& ctx) {
+  auto ref = load_reference_cached(ref_path_);
+  CallerOptions opt = caller_options_from_config(ctx.gpu);
+  auto it = extra_opts_.find("--dump-regions");
+  if (it != extra_opts_.end() && !it->second.empty()) opt.dump_path = it->second[0] + "." + std::to_string(contig_);
+  const VcfHeader h = caller_vcf_header(*ref, {"sample"}, false, ref_path_);
+  VcfWriter out(output_path_, h);
+  stats_ = call_intervals(*ref, input_path_, "", read_all(intv_paths_), opt, out);
+  out.close();
+  if (ctx.log)
+    std::fprintf(ctx.log,
+                 "[fcs-genome htc] shard %d gpu %d: %lld reads, %lld regions, %lld pairs, %lld cells, %lld calls, "
+                 "%.3f s (PairHMM %.3f s, %lld device passes)\n",
+                 contig_, ctx.gpu, (long long)stats_.reads, (long long)stats_.regions, (long long)stats_.pairs,
+                 (long long)stats_.cells, (long long)stats_.calls, stats_.seconds, stats_.phmm_seconds,
+                 (long long)stats_.device_passes);
+  return 0;
+}
+
+// ------------------------------------------------------------------ Mutect2
+Mutect2Worker::Mutect2Worker(std::string ref_path, std::vector<std::string> intv_paths, std::string normal_path,
+                             std::string tumor_path, std::string output_path, std::vector<std::string> extra_opts,
+                             int contig, bool flag_f)
+    : Worker(1, 1, std::move(extra_opts), "Mutect2"),
+      ref_path_(std::move(ref_path)),
+      normal_path_(std::move(normal_path)),
+      tumor_path_(std::move(tumor_path)),
+      output_path_(std::move(output_path)),
+      intv_paths_(std::move(intv_paths)),
+      contig_(contig),
+      flag_f_(flag_f) {}
+
+void Mutect2Worker::check() {
+  for (const std::string* p : {&ref_path_, &normal_path_, &tumor_path_})
+    if (!is_regular_file(*p)) throw fileNotFound(*p);
+  for (const std::string& p : intv_paths_)
+    if (!is_regular_file(p)) throw fileNotFound(p);
+  if (!flag_f_ && path_exists(output_path_)) throw invalidParam("output " + output_path_ + " exists (use -f)");
+}
+
+int Mutect2Worker::run(TaskContext& ctx) {
+  auto ref = load_reference_cached(ref_path_);
+  CallerOptions opt = caller_options_from_config(ctx.gpu);
+  opt.somatic = true;
+  const VcfHeader h = caller_vcf_header(*ref, {"TUMOR", "NORMAL"}, true, ref_path_);
+  VcfWriter out(output_path_, h);
+  stats_ = call_intervals(*ref, tumor_path_, normal_path_, read_all(intv_paths_), opt, out);
+  out.close();
+  if (ctx.log)
+    std::fprintf(ctx.log, "[fcs-genome mutect2] shard %d gpu %d: %lld reads, %lld regions, %lld calls, %.3f s\n",
+                 contig_, ctx.gpu, (long long)stats_.reads, (long long)stats_.regions, (long long)stats_.calls,
+                 stats_.seconds);
+  return 0;
+}
+
+// ------------------------------------------------------------------ VCF tail
+VCFConcatWorker::VCFConcatWorker(std::vector<std::string> inputs, std::string output)
+    : Worker(1, 1, {}, "VCF concat"), inputs_(std::move(inputs)), output_(std::move(output)) {}
+
+void VCFConcatWorker::check() {
+  if (inputs_.empty()) throw invalidParam("no VCF to concatenate");
+}
+
+int VCFConcatWorker::run(TaskContext&) {
+  vcf_concat(inputs_, output_);
+  return 0;
+}
+
+ZIPWorker::ZIPWorker(std::string input, std::string output, bool)
+    : Worker(1, 1, {}, "bgzip"), input_(std::move(input)), output_(std::move(output)) {}
+
+void ZIPWorker::check() {}
+
+int ZIPWorker::run(TaskContext&) {
+  bgzip_file(input_, output_);
+  return 0;
+}
+
+TabixWorker::TabixWorker(std::string path) : Worker(1, 1, {}, "tabix"), path_(std::move(path)) {}
+
+int TabixWorker::run(TaskContext&) {
+  tabix_index_vcf(path_);
+  return 0;
+}
+
+DeviceWarmupWorker::DeviceWarmupWorker(std::vector<int> gpus) : Worker(1, 1, {}, "GPU warm-up"), gpus_(std::move(gpus)) {}
+
+int DeviceWarmupWorker::run(TaskContext&) {
+  // a 1x1 PairHMM call per device builds and uploads its GKL tables
+  static const uint8_t b[1] = {'A'}, q[1] = {30}, g[1] = {10}, iq[1] = {45};
+  const fcs_phmm_read r{b, q, iq, iq, g, 1};
+  const fcs_phmm_hap h{b, 1};
+  double out = 0;
+  for (int d : gpus_) {
+    fcs_phmm_opts o;
+    fcs_phmm_opts_default(&o);
+    o.device = d;
+    if (fcs_phmm_compute(&r, 1, &h, 1, &out, &o) != FCS_OK) return 1;
+  }
+  return 0;
+}
+
+}  // namespace fcsg

@@ -1,0 +1,101 @@
+// Workers of the GPU-backed commands (reference: include/fcs-genome/workers/*.h).
+// HTCWorker / Mutect2Worker keep the reference's constructor arguments
+// (src/workers/HTCWorker.cpp:17-47, Mutect2Worker.cpp:17-107) but run the
+// caller in-process on the task's GPU slot instead of launching GATK;
+// VCFConcatWorker / ZIPWorker / TabixWorker are the same tail as
+// src/worker-htc.cpp:153-176, done natively instead of via bcftools/bgzip/tabix.
+#pragma once
+
+#include <memory>
+#include <string>
+#include <vector>
+
+#include "caller.h"
+#include "executor.h"
+#include "fasta.h"
+
+namespace fcsg {
+
+// Process-wide reference cache (shard tasks of one run share the genome).
+std::shared_ptr<const Reference> load_reference_cached(const std::string& path);
+
+class HTCWorker : public Worker {
+ public:
+  HTCWorker(std::string ref_path, std::vector<std::string> intv_paths, std::string input_path,
+            std::string output_path, std::vector<std::string> extra_opts, int contig, bool flag_vcf, bool flag_f,
+            bool flag_gatk = false);
+  void check() override;
+  int run(TaskContext& ctx) override;
+  CallerStats stats() const { return stats_; }
+
+ private:
+  std::string ref_path_, input_path_, output_path_;
+  std::vector<std::string> intv_paths_;
+  int contig_;
+  bool flag_vcf_, flag_f_;
+  CallerStats stats_;
+};
+
+class Mutect2Worker : public Worker {
+ public:
+  Mutect2Worker(std::string ref_path, std::vector<std::string> intv_paths, std::string normal_path,
+                std::string tumor_path, std::string output_path, std::vector<std::string> extra_opts, int contig,
+                bool flag_f);
+  void check() override;
+  int run(TaskContext& ctx) override;
+  CallerStats stats() const { return stats_; }
+
+ private:
+  std::string ref_path_, normal_path_, tumor_path_, output_path_;
+  std::vector<std::string> intv_paths_;
+  int contig_;
+  bool flag_f_;
+  CallerStats stats_;
+};
+
+class VCFConcatWorker : public Worker {
+ public:
+  VCFConcatWorker(std::vector<std::string> inputs, std::string output);
+  void check() override;
+  int run(TaskContext& ctx) override;
+
+ private:
+  std::vector<std::string> inputs_;
+  std::string output_;
+};
+
+class ZIPWorker : public Worker {
+ public:
+  ZIPWorker(std::string input, std::string output, bool flag_f = true);
+  void check() override;
+  int run(TaskContext& ctx) override;
+
+ private:
+  std::string input_, output_;
+};
+
+class TabixWorker : public Worker {
+ public:
+  explicit TabixWorker(std::string path);
+  int run(TaskContext& ctx) override;
+
+ private:
+  std::string path_;
+};
+
+// Loads libfcship's per-device tables on every GPU slot before the shard
+// tasks start (the role the Blaze NAM daemon plays for the FPGA:
+// src/worker-htc.cpp:100-112).  Run by a BackgroundExecutor.
+class DeviceWarmupWorker : public Worker {
+ public:
+  explicit DeviceWarmupWorker(std::vector<int> gpus);
+  int run(TaskContext& ctx) override;
+
+ private:
+  std::vector<int> gpus_;
+};
+
+// Applies the caller's config keys (htc.*, mutect2.*, gpu.*) to options.
+CallerOptions caller_options_from_config(int gpu);
+
+}  // namespace fcsg

@@ -1,0 +1,138 @@
+"""End-to-end GPU runs of the fcs-genome commands on synthetic data (SURVEY.md
+§8f rows f1-f4): `htc` and `mutect2` recover the spiked variants, every
+PairHMM likelihood the caller used matches the CPU oracle (the caller dumps
+its region batches with --dump-regions), and `align` places the synthetic
+reads where the generator drew them.  Recall / precision bars are this
+build's own (the reference's caller is GATK [EXT]; parity unpinned beyond the
+PairHMM values)."""
+import os
+import struct
+
+import numpy as np
+import pytest
+
+import host_lib as H
+import oracle_lib
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def data(tmp_path_factory):
+    d = tmp_path_factory.mktemp("e2e")
+    p = H.run_cli("synth", "-o", d, "-c", "chr20:250000,chr21:100000", "-x", "30", "--tumor", "--seed", "11")
+    assert p.returncode == 0, p.stderr
+    return d
+
+
+def truth(d, somatic):
+    out = set()
+    for ln in (d / "truth.vcf").read_text().splitlines():
+        if ln.startswith("#"):
+            continue
+        f = ln.split("\t")
+        if ("SOMATIC" in f[7]) == somatic:
+            out.add((f[0], int(f[1]), f[3], f[4]))
+    return out
+
+
+def calls(vcf):
+    out = set()
+    for ln in open(vcf).read().splitlines():
+        if ln.startswith("#"):
+            continue
+        f = ln.split("\t")
+        out.add((f[0], int(f[1]), f[3], f[4]))
+    return out
+
+
+def read_dump(path):
+    regions = []
+    b = open(path, "rb").read()
+    p = 0
+    while p < len(b):
+        assert b[p:p + 4] == b"RGN1"
+        nr, nh = struct.unpack_from("<ii", b, p + 4)
+        p += 12
+        reads = []
+        for _ in range(nr):
+            L = struct.unpack_from("<i", b, p)[0]
+            p += 4
+            reads.append(tuple(np.frombuffer(b[p + k * L: p + (k + 1) * L], np.uint8).copy() for k in range(5)))
+            p += 5 * L
+        haps = []
+        for _ in range(nh):
+            L = struct.unpack_from("<i", b, p)[0]
+            haps.append(np.frombuffer(b[p + 4: p + 4 + L], np.uint8).copy())
+            p += 4 + L
+        lik = np.frombuffer(b[p: p + 8 * nr * nh], np.float64).reshape(nr, nh).copy()
+        p += 8 * nr * nh
+        regions.append((reads, haps, lik))
+    return regions
+
+
+ENV = {"FCS_GATK_NCONTIGS": "6", "FCS_GATK_NPROCS": "3", "FCS_GPU_DEVICES": "0"}
+
+
+def test_htc_end_to_end(gpu, data, tmp_path):
+    out = tmp_path / "htc.vcf"
+    dump = tmp_path / "dump"
+    p = H.run_cli("htc", "-r", data / "ref.fasta", "-i", data / "sample.bam", "-o", out, "--dump-regions", dump,
+                  env=ENV, cwd=tmp_path)
+    assert p.returncode == 0, p.stderr[-3000:]
+    assert (tmp_path / "htc.vcf.gz").exists() and (tmp_path / "htc.vcf.gz.tbi").exists()
+    import gzip
+    assert gzip.decompress((tmp_path / "htc.vcf.gz").read_bytes()).decode() == out.read_text()
+    t, c = truth(data, False), calls(out)
+    tp = len(t & c)
+    snv_t = {v for v in t if len(v[2]) == len(v[3]) == 1}
+    assert len(snv_t & c) / len(snv_t) >= 0.95, (len(snv_t & c), len(snv_t))
+    assert tp / len(t) >= 0.9, (tp, len(t))
+    assert tp / max(1, len(c)) >= 0.95, (tp, len(c))
+    # every PairHMM value the caller used equals the oracle's (sampled pairs)
+    rng = np.random.default_rng(0)
+    dumps = sorted(tmp_path.glob("dump.*"))
+    assert dumps
+    checked = 0
+    for f in dumps:
+        for reads, haps, lik in read_dump(f):
+            for _ in range(3):
+                r, h = int(rng.integers(len(reads))), int(rng.integers(len(haps)))
+                ref, _ = oracle_lib.phmm_log10(reads[r], haps[h])
+                assert abs(lik[r, h] - ref) <= 1e-5 * abs(ref), (lik[r, h], ref)
+                checked += 1
+    assert checked >= 100
+
+
+def test_mutect2_end_to_end(gpu, data, tmp_path):
+    out = tmp_path / "m2.vcf"
+    p = H.run_cli("mutect2", "-r", data / "ref.fasta", "-t", data / "tumor.bam", "-n", data / "sample.bam", "-o", out,
+                  env=ENV, cwd=tmp_path)
+    assert p.returncode == 0, p.stderr[-3000:]
+    som, germ, c = truth(data, True), truth(data, False), calls(out)
+    assert som, "the synthetic tumor has somatic variants"
+    assert len(som & c) / len(som) >= 0.8, (len(som & c), len(som))
+    assert len(germ & c) <= 0.02 * len(germ)  # germline sites are rejected by the normal
+
+
+def test_align_end_to_end(gpu, data, tmp_path):
+    out = tmp_path / "aln.bam"
+    p = H.run_cli("align", "-r", data / "ref.fasta", "-1", data / "sample.fastq", "-o", out, env=ENV, cwd=tmp_path)
+    assert p.returncode == 0, p.stderr[-3000:]
+    assert os.path.exists(str(out) + ".bai")
+    _, _, truth_recs = H.read_bam(data / "sample.bam")
+    names, _, recs = H.read_bam(out)
+    want = {r["name"]: r for r in truth_recs}
+    same_pos = same_cig = mapped = 0
+    for r in recs:
+        if r["flag"] & 4:
+            continue
+        mapped += 1
+        w = want[r["name"]]
+        same_pos += (r["ref_id"], r["pos"]) == (w["ref_id"], w["pos"])
+        same_cig += r["cigar"] == w["cigar"]
+        assert (r["flag"] & 16) == (w["flag"] & 16)
+        assert r["seq"] == w["seq"]
+    assert mapped / len(recs) >= 0.99
+    assert same_pos / mapped >= 0.97, (same_pos, mapped)
+    assert same_cig / mapped >= 0.9, (same_cig, mapped)
