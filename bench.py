@@ -151,6 +151,60 @@ def bench_bsw(args, dev, tasks, reps=3):
                 bytes=int(tasks.qbuf.size + tasks.tbuf.size + 24 * tasks.n))
 
 
+def bench_e2e(args, rank, local):
+    """End-to-end fcs-genome commands on this rank's own synthetic genome
+    (C4/C5-shaped: chr1-like random reference, 30x sample, 40x tumor with
+    somatic variants; weak scaling, one GPU per rank).  Wall time of each
+    command as a user runs it (process start, BAM decode, pileup, PairHMM on
+    the GPU, VCF tail)."""
+    import re
+    import shutil
+    import subprocess
+    import tempfile
+    exe = os.path.join(ROOT, "falcon-genome_amd", "bin", "fcs-genome")
+    work = tempfile.mkdtemp(prefix=f"fcs-e2e-{rank}-")
+    env = dict(os.environ, FCS_GPU_DEVICES=str(local), FCS_LOG_DIR=os.path.join(work, "log"),
+               FCS_TEMP_DIR=work, FCS_GATK_NPROCS="16")
+    try:
+        L = int(args.e2e_mbp * 1e6)
+        subprocess.run([exe, "synth", "-o", work + "/d", "-c", f"chr1:{L}", "-x", "30", "--tumor",
+                        "--seed", str(args.seed + rank)], env=env, check=True, capture_output=True)
+        out = {"data": f"synthetic chr1-like {args.e2e_mbp:g} Mbp per GPU, sample 30x, tumor 40x (+1e-4 somatic)"}
+
+        def timed(name, cmd):
+            shutil.rmtree(env["FCS_LOG_DIR"], ignore_errors=True)
+            t0 = time.perf_counter()
+            r = subprocess.run([exe, *cmd], env=env, capture_output=True, text=True, cwd=work)
+            dt = time.perf_counter() - t0
+            if r.returncode != 0:
+                raise RuntimeError(f"fcs-genome {name} failed ({r.returncode}): {r.stderr[-2000:]}")
+            logs = ""
+            for f in (os.listdir(env["FCS_LOG_DIR"]) if os.path.isdir(env["FCS_LOG_DIR"]) else []):
+                if ".part-" not in f:
+                    logs += open(os.path.join(env["FCS_LOG_DIR"], f)).read()
+            return dt, logs, r.stderr
+        d = work + "/d"
+        dt, logs, _ = timed("htc", ["htc", "-r", d + "/ref.fasta", "-i", d + "/sample.bam", "-o", work + "/htc.vcf"])
+        reg = sum(int(x) for x in re.findall(r"(\d+) regions", logs))
+        pairs = sum(int(x) for x in re.findall(r"(\d+) pairs", logs))
+        cells = sum(int(x) for x in re.findall(r"(\d+) cells", logs))
+        out["htc"] = {"regions": reg, "pairs": pairs, "cells": cells, "seconds": round(dt, 3),
+                      "regions_per_s": round(reg / dt, 1)}
+        dt, logs, _ = timed("mutect2", ["mutect2", "-r", d + "/ref.fasta", "-t", d + "/tumor.bam", "-n",
+                                        d + "/sample.bam", "-o", work + "/m2.vcf"])
+        reg = sum(int(x) for x in re.findall(r"(\d+) regions", logs))
+        out["mutect2"] = {"regions": reg, "seconds": round(dt, 3), "regions_per_s": round(reg / dt, 1)}
+        dt, _, err = timed("align", ["align", "-r", d + "/ref.fasta", "-1", d + "/sample.fastq", "-o",
+                                     work + "/aln.bam"])
+        m = re.search(r"(\d+) reads, (\d+) mapped, (\d+) extension tasks", err)
+        n = int(m.group(1)) if m else 0
+        out["align"] = {"reads": n, "ext_tasks": int(m.group(3)) if m else 0, "seconds": round(dt, 3),
+                        "reads_per_s": round(n / dt, 1)}
+        return out
+    finally:
+        shutil.rmtree(work, ignore_errors=True)
+
+
 def cpu_baseline_phmm(p, budget_s, threads):
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     import oracle_lib  # test infrastructure: CPU baseline leg only
@@ -191,6 +245,8 @@ def main():
     ap.add_argument("--no-bsw", action="store_true")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-budget", type=float, default=12.0)
+    ap.add_argument("--no-e2e", action="store_true")
+    ap.add_argument("--e2e-mbp", type=float, default=4.0)
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -257,6 +313,19 @@ def main():
 
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         line["cpu_baseline"] = cpu_baseline_phmm(p, args.cpu_budget, min(16, os.cpu_count() or 1))
+
+    if not args.no_e2e:
+        e2e = bench_e2e(args, rank, local)
+        if world > 1:  # whole-job rates: units of all ranks over the slowest rank's time
+            for k, unit in (("htc", "regions"), ("mutect2", "regions"), ("align", "reads")):
+                t = torch.tensor([e2e[k][unit], e2e[k]["seconds"]], dtype=torch.float64, device=dev)
+                tot = t.clone()
+                torch.distributed.all_reduce(tot[:1])
+                torch.distributed.all_reduce(tot[1:], op=torch.distributed.ReduceOp.MAX)
+                e2e[k][unit] = int(tot[0].item())
+                e2e[k]["seconds"] = round(tot[1].item(), 3)
+                e2e[k][unit + "_per_s"] = round(tot[0].item() / tot[1].item(), 1)
+        line["e2e"] = e2e
 
     if rank == 0:
         print(json.dumps(line), flush=True)
