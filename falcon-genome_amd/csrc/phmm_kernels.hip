@@ -44,11 +44,30 @@ template <typename T> struct alignas(2 * sizeof(T)) PhRing {
 __device__ __forceinline__ float fma_t(float a, float b, float c) { return fmaf(a, b, c); }
 __device__ __forceinline__ double fma_t(double a, double b, double c) { return fma(a, b, c); }
 
+__device__ __forceinline__ unsigned char base_code(unsigned char b) {
+  return b == 'A' ? 0 : b == 'C' ? 1 : b == 'G' ? 2 : b == 'T' ? 3 : b == 'N' ? 4 : 5;
+}
+__device__ __forceinline__ int base_mask(int rb) {
+  const int c = base_code((unsigned char)rb);
+  // N matches every hap code; a byte outside A/C/G/T/N equals no A/C/G/T hap
+  // byte, so it matches only N (code 4) — bit-select groups have no code 5
+  return c == 4 ? 0x7F : c == 5 ? 0x10 : (1 << c) | 0x10;
+}
+__device__ __forceinline__ float sel_bits(uint32_t m, float a, float b) {
+  return __uint_as_float((__float_as_uint(a) & m) | (__float_as_uint(b) & ~m));
+}
+__device__ __forceinline__ double sel_bits(uint32_t m, double a, double b) {
+  const unsigned long long mm = ((unsigned long long)m << 32) | m;
+  return __longlong_as_double((long long)(((unsigned long long)__double_as_longlong(a) & mm) |
+                                          ((unsigned long long)__double_as_longlong(b) & ~mm)));
+}
+
 template <typename T>
 struct RowP {
   T e1, e3, my, yy;  // own row: emission priors, deletion transitions
   T mm, gm, mx, xx;  // row below: match/gap-to-match, insertion transitions
-  int rbase;
+  int rbase;  // read base byte (byte-compare groups)
+  int rmask;  // bit k set: hap code k (A,C,G,T,N = 0..4) matches this row's read base
 };
 
 template <typename T>
@@ -59,7 +78,7 @@ struct LaneState {
 };
 
 // One anti-diagonal step at t = t0 + S.
-template <typename T, bool EXACT, bool SUM, int S>
+template <typename T, bool EXACT, bool SUM, bool BC, int S>
 __device__ __forceinline__ void phmm_step(LaneState<T>& L, PhRing<T> (&pf)[4], int (&hq)[4],
                                           const unsigned char* __restrict__ hapl, const RowP<T>& p,
                                           PhRing<T>* __restrict__ ring, const int t0, const int sl, const bool top,
@@ -71,7 +90,12 @@ __device__ __forceinline__ void phmm_step(LaneState<T>& L, PhRing<T> (&pf)[4], i
   hq[S & 3] = hapl[t + 20 - sl];  // this lane's hap base for column t + 4 - l
   const T Xu = dpp_row_shr1<T>(cur.X, L.Xo);
   const T I = dpp_row_shr1<T>(cur.I, L.Io);
-  const T prior = (hb == p.rbase || hb == 'N') ? p.e1 : p.e3;
+  T prior;
+  if constexpr (BC) {  // group with bytes outside A/C/G/T/N: GKL's byte compare
+    prior = (hb == p.rbase || hb == 'N') ? p.e1 : p.e3;
+  } else {  // hap codes: one bit extract + one bit select, no compare/VCC
+    prior = sel_bits((uint32_t)__builtin_amdgcn_sbfe(p.rmask, hb, 1), p.e1, p.e3);
+  }
   const T M = L.Xp * prior;
   T D, Xn, In;
   if constexpr (EXACT) {
@@ -102,13 +126,13 @@ __device__ __forceinline__ void phmm_step(LaneState<T>& L, PhRing<T> (&pf)[4], i
   L.Do = D;
 }
 
-template <typename T, bool EXACT, bool SUM>
+template <typename T, bool EXACT, bool SUM, bool BC>
 __device__ __forceinline__ void phmm_block(LaneState<T>& L, PhRing<T> (&pf)[4], int (&hq)[4],
                                            const unsigned char* __restrict__ hapl, const RowP<T>& p,
                                            PhRing<T>* __restrict__ ring, const int t0, const int sl, const bool top,
                                            const int lim, T& accM, T& accI) {
   [&]<int... S>(std::integer_sequence<int, S...>) {
-    (phmm_step<T, EXACT, SUM, S>(L, pf, hq, hapl, p, ring, t0, sl, top, lim, accM, accI), ...);
+    (phmm_step<T, EXACT, SUM, BC, S>(L, pf, hq, hapl, p, ring, t0, sl, top, lim, accM, accI), ...);
   }(std::make_integer_sequence<int, 16>{});
 }
 
@@ -139,9 +163,11 @@ __device__ __forceinline__ RowP<T> row_params(const PhmmTables<T>& tab, const Ra
   RowP<T> p;
   p.e1 = p.e3 = p.my = p.yy = p.mm = p.gm = p.mx = p.xx = (T)0;
   p.rbase = -1;
+  p.rmask = -1;
   if (r.rb < 0) return p;
   const int q = r.bq & 127, qd = r.dq & 127, qc = r.gq & 127;
   p.rbase = r.rb;
+  p.rmask = base_mask(r.rb);
   p.e1 = tab.dmatch[q];
   p.e3 = (r.rb == 'N') ? p.e1 : tab.dmis[q];
   p.my = tab.ph2pr[qd];
@@ -157,7 +183,7 @@ __device__ __forceinline__ RowP<T> row_params(const PhmmTables<T>& tab, const Ra
 
 // One stripe: nblk blocks of 16 steps; the next stripe's parameters are
 // gathered after the first block (their bytes were requested at stripe start).
-template <typename T, bool EXACT, bool SUM>
+template <typename T, bool EXACT, bool SUM, bool BC>
 __device__ __forceinline__ void phmm_stripe(const RowP<T>& p, PhRing<T>* __restrict__ ring,
                                             const unsigned char* __restrict__ hapl, const int sl, const int nblk,
                                             const int lim, T& accM, T& accI, const PhmmTables<T>& tab,
@@ -172,10 +198,10 @@ __device__ __forceinline__ void phmm_stripe(const RowP<T>& p, PhRing<T>* __restr
     pf[k] = ring[16 + k];
     hq[k] = hapl[16 + k - sl];
   }
-  phmm_block<T, EXACT, SUM>(L, pf, hq, hapl, p, ring, 0, sl, top, lim, accM, accI);
+  phmm_block<T, EXACT, SUM, BC>(L, pf, hq, hapl, p, ring, 0, sl, top, lim, accM, accI);
   np = row_params<T>(tab, nraw);
   for (int blk = 1; blk < nblk; ++blk)
-    phmm_block<T, EXACT, SUM>(L, pf, hq, hapl, p, ring, 16 * blk, sl, top, lim, accM, accI);
+    phmm_block<T, EXACT, SUM, BC>(L, pf, hq, hapl, p, ring, 16 * blk, sl, top, lim, accM, accI);
 }
 
 template <typename T, bool EXACT, bool RESCUE_PASS>
@@ -218,14 +244,28 @@ __global__ __launch_bounds__(64) void phmm_kernel(const PhmmDevBatch b, const in
     const T init = active ? tab.init_const / (T)H : (T)0;
     const T x0 = active ? init * tab.dmatch[b.gq[ro] & 127] : (T)0;
     __syncthreads();
+    // Hap bytes go to LDS as codes A,C,G,T,N = 0..4 (6 = padding) for the
+    // bit-select prior.  A hap byte outside A/C/G/T/N anywhere in the wave's
+    // pairs switches the group to raw bytes and GKL's byte compare (read
+    // bytes outside the set are exact on the code path: they match only N).
+    bool other = false;
     for (int s = sl; s < nslot; s += 16) {
       const int c = s - 16;
       PhRing<T> v;
       v.X = (c >= 0 && c <= H) ? x0 : (T)0;
       v.I = 0;
       ring[s] = v;
-      hapl[s] = (active && c >= 1 && c <= H) ? b.hb[ho + c - 1] : (unsigned char)0;
+      const bool in = active && c >= 1 && c <= H;
+      const unsigned char code = in ? base_code(b.hb[ho + c - 1]) : (unsigned char)6;
+      other |= code == 5;
+      hapl[s] = code;
     }
+    const bool bytecmp = __ballot(other) != 0ull;
+    if (bytecmp)
+      for (int s = sl; s < nslot; s += 16) {
+        const int c = s - 16;
+        hapl[s] = (active && c >= 1 && c <= H) ? b.hb[ho + c - 1] : (unsigned char)0;
+      }
     __syncthreads();
 
     RowP<T> prm = row_params<T>(tab, load_raw(b, active ? R : 0, ro, sl));
@@ -242,7 +282,10 @@ __global__ __launch_bounds__(64) void phmm_kernel(const PhmmDevBatch b, const in
         const int cont = wave_max((active && nstr > st + 1) ? 1 : 0);
         const int lim = (seg_sums && sl == sum_lane) ? sl + H : -1;
         const int tend = cont ? Hmax + 15 : wave_max(seg_sums ? sum_lane + H : 0);
-        phmm_stripe<T, EXACT, true>(prm, ring, hapl, sl, (tend + 16) >> 4, lim, accM, accI, tab, nraw, nprm);
+        if (bytecmp)
+          phmm_stripe<T, EXACT, true, true>(prm, ring, hapl, sl, (tend + 16) >> 4, lim, accM, accI, tab, nraw, nprm);
+        else
+          phmm_stripe<T, EXACT, true, false>(prm, ring, hapl, sl, (tend + 16) >> 4, lim, accM, accI, tab, nraw, nprm);
         if (seg_sums && sl == sum_lane) {
           const T sum = accM + accI;
           if constexpr (RESCUE_PASS) {
@@ -258,7 +301,10 @@ __global__ __launch_bounds__(64) void phmm_kernel(const PhmmDevBatch b, const in
           }
         }
       } else {
-        phmm_stripe<T, EXACT, false>(prm, ring, hapl, sl, (Hmax + 31) >> 4, -1, accM, accI, tab, nraw, nprm);
+        if (bytecmp)
+          phmm_stripe<T, EXACT, false, true>(prm, ring, hapl, sl, (Hmax + 31) >> 4, -1, accM, accI, tab, nraw, nprm);
+        else
+          phmm_stripe<T, EXACT, false, false>(prm, ring, hapl, sl, (Hmax + 31) >> 4, -1, accM, accI, tab, nraw, nprm);
       }
       prm = nprm;
     }

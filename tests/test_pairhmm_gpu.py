@@ -213,3 +213,25 @@ def test_region_batching_equals_per_region(gpu):
         assert np.array_equal(out, alone)
         ref = np.array([[oracle_lib.phmm_log10(r, h)[0] for h in haps] for r in reads])
         np.testing.assert_allclose(out, ref, rtol=RTOL)
+
+
+@pytest.mark.parametrize("exact", [True, False])
+def test_bytes_outside_acgtn(gpu, exact):
+    """GKL compares bases as bytes ('N' a wildcard on either side): groups
+    with IUPAC / lower-case bytes take the byte-compare path, the rest the
+    hap-code bit-select path; both must match the oracle."""
+    reads, haps = random_batch(31, 24, 6, 40, 130, 60, 220)
+    rng = np.random.default_rng(5)
+    alphabet = np.frombuffer(b"ACGTNRYacgtMK", np.uint8)
+    for k in (0, 3, 7):  # a few reads and haps with odd bytes; others stay ACGTN
+        r = list(reads[k])
+        b = r[0].copy()
+        m = rng.random(b.size) < 0.2
+        b[m] = rng.choice(alphabet, int(m.sum()))
+        r[0] = b
+        reads[k] = tuple(r)
+    h = haps[2].copy()
+    h[::7] = ord("R")
+    haps[2] = h
+    p = fcship.make_pairs(reads, haps)
+    check_parity(p, fcship.phmm_compute_pairs(p, exact=exact), exact)
