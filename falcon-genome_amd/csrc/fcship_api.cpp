@@ -234,7 +234,8 @@ struct fcs_phmm_plan {
   void* sort_tmp = nullptr;
   size_t sort_tmp_bytes = 0;
   int32_t* rescue_list = nullptr;
-  unsigned long long* rescue_count = nullptr;
+  unsigned long long* rescue_count = nullptr;  // [0] rescue count, then int64 class bounds[7]
+  int64_t* bounds = nullptr;
   int64_t scheduled = -1;  // n_pairs of the last schedule
 };
 
@@ -329,8 +330,9 @@ int fcs_phmm_plan_create(int32_t device, int64_t max_pairs, fcs_phmm_plan** plan
   FCS_HIP_CHECK(hipMalloc(&p->idx_in, n * 4));
   FCS_HIP_CHECK(hipMalloc(&p->idx_out, n * 4));
   FCS_HIP_CHECK(hipMalloc(&p->rescue_list, n * 4));
-  FCS_HIP_CHECK(hipMalloc(&p->rescue_count, sizeof(unsigned long long)));
-  FCS_HIP_CHECK(hipMemset(p->rescue_count, 0, sizeof(unsigned long long)));
+  FCS_HIP_CHECK(hipMalloc(&p->rescue_count, 8 * sizeof(unsigned long long)));
+  FCS_HIP_CHECK(hipMemset(p->rescue_count, 0, 8 * sizeof(unsigned long long)));
+  p->bounds = reinterpret_cast<int64_t*>(p->rescue_count + 1);
   size_t tmp = 0;
   FCS_HIP_CHECK(hipcub::DeviceRadixSort::SortPairs(nullptr, tmp, p->keys_in, p->keys_out, p->idx_in, p->idx_out,
                                                     (int)n, 0, 32));
@@ -369,6 +371,7 @@ int fcs_phmm_dev_schedule(fcs_phmm_plan* plan, const fcs_phmm_batch* b, void* st
     FCS_HIP_CHECK(hipcub::DeviceRadixSort::SortPairs(plan->sort_tmp, tmp, plan->keys_in, plan->keys_out,
                                                       plan->idx_in, plan->idx_out, (int)b->n_pairs, 0, 32, s));
   }
+  if ((rc = launch_phmm_bounds(plan->keys_out, b->n_pairs, plan->bounds, s))) return rc;
   plan->scheduled = b->n_pairs;
   return FCS_OK;
 }
@@ -387,7 +390,7 @@ int fcs_phmm_dev_forward(fcs_phmm_plan* plan, const fcs_phmm_batch* b, double* o
   if (rc) return rc;
   hipStream_t s = (hipStream_t)stream;
   FCS_HIP_CHECK(hipMemsetAsync(plan->rescue_count, 0, sizeof(unsigned long long), s));
-  return launch_phmm_forward(to_dev(b), plan->idx_out, b->n_pairs, std::max(b->max_hap_len, 1), *t,
+  return launch_phmm_forward(to_dev(b), plan->idx_out, b->n_pairs, std::max(b->max_hap_len, 1), plan->bounds, *t,
                              opts->exact_order != 0, out, plan->rescue_list, plan->rescue_count,
                              opts->rescue_threshold, opts->use_fp64_rescue != 0, s);
 }

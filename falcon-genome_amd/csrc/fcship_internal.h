@@ -128,8 +128,10 @@ int join_streams(hipStream_t s, const hipStream_t (&fs)[kForkStreams]);
 
 // ------------------------------------------------------------ kernel launchers
 int launch_phmm_keys(const PhmmDevBatch& b, uint32_t* keys, int32_t* idx, hipStream_t s);
+// bounds: device int64[7] from launch_phmm_bounds over the sorted keys.
+int launch_phmm_bounds(const uint32_t* sorted_keys, int64_t n, int64_t* bounds, hipStream_t s);
 int launch_phmm_forward(const PhmmDevBatch& b, const int32_t* order, int64_t count, int max_hap_len,
-                        const DeviceTables& t, bool exact, double* out, int32_t* rescue_list,
+                        const int64_t* bounds, const DeviceTables& t, bool exact, double* out, int32_t* rescue_list,
                         unsigned long long* rescue_count, float thr, bool use_rescue, hipStream_t s);
 int launch_phmm_rescue(const PhmmDevBatch& b, const int32_t* list, const unsigned long long* count_dev,
                        int64_t max_count, int max_hap_len, const DeviceTables& t, bool exact, double* out,

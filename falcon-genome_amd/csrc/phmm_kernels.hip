@@ -31,6 +31,8 @@
 // order bit-for-bit, the fast variant uses explicit fma().
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
+
 #include <utility>
 
 #include "fcship_internal.h"
@@ -207,7 +209,8 @@ __device__ __forceinline__ void phmm_stripe(const RowP<T>& p, PhRing<T>* __restr
 template <typename T, bool EXACT, bool RESCUE_PASS>
 __global__ __launch_bounds__(64) void phmm_kernel(const PhmmDevBatch b, const int32_t* __restrict__ order,
                                                   const unsigned long long* __restrict__ count_dev,
-                                                  long long count_host, const int nslot, const PhmmTables<T> tab,
+                                                  long long count_host, const int64_t* __restrict__ bounds,
+                                                  const int cls, const int nslot, const PhmmTables<T> tab,
                                                   double* __restrict__ out, int32_t* __restrict__ rescue_list,
                                                   unsigned long long* __restrict__ rescue_count, const float thr,
                                                   const int use_rescue) {
@@ -217,7 +220,12 @@ __global__ __launch_bounds__(64) void phmm_kernel(const PhmmDevBatch b, const in
   const int sl = lane & 15;
   PhRing<T>* const ring = reinterpret_cast<PhRing<T>*>(smem_raw) + seg * nslot;
   unsigned char* const hapl = smem_raw + (size_t)4 * nslot * sizeof(PhRing<T>) + seg * nslot;
-  const long long count = count_dev ? (long long)(*count_dev) : count_host;
+  // forward pass: this launch's hap-length class of the sorted schedule; rescue: the device-side list count
+  long long count = count_dev ? (long long)(*count_dev) : count_host;
+  if (bounds) {
+    order += bounds[cls];
+    count = bounds[cls + 1] - bounds[cls];
+  }
   const long long ngroups = (count + 3) >> 2;
 
   for (long long g = blockIdx.x; g < ngroups; g += gridDim.x) {
@@ -311,22 +319,44 @@ __global__ __launch_bounds__(64) void phmm_kernel(const PhmmDevBatch b, const in
   }
 }
 
-// Sort keys: descending (stripe count, hap length) -> ascending key order.
+// Slots (ring entries and hap bytes) = column + 16 for columns -16 .. Hmax + 34:
+// stripes run to Hmax + 15 rounded up to a 16-step block, plus four steps of
+// read-ahead.
+static __host__ __device__ int nslot_for(int max_hap_len) { return ((max_hap_len + 51 + 15) / 16) * 16; }
+
+// Hap-length classes of the forward pass: class c < kPhmmClasses - 1 holds
+// pairs with nslot_for(H) <= 224 + 32c (LDS 8.1 .. 12.7 KB per wave), the last
+// class everything longer.  Each class is its own launch with LDS sized to the
+// class, so short haplotypes run at 4 waves per SIMD instead of the 3 that the
+// longest haplotype of the batch would allow.
+constexpr int kPhmmClasses = 6;
+__host__ __device__ inline int phmm_class(int H) {
+  const int c = (nslot_for(H) - 224 + 31) / 32;
+  return c < 0 ? 0 : c > kPhmmClasses - 1 ? kPhmmClasses - 1 : c;
+}
+
+// Sort keys: class descending, then stripe count and hap length descending,
+// as ascending keys — each class is a contiguous range, longest work first.
 __global__ void phmm_keys_kernel(const PhmmDevBatch b, uint32_t* __restrict__ keys, int32_t* __restrict__ idx) {
   const long long p = (long long)blockIdx.x * blockDim.x + threadIdx.x;
   if (p >= b.n_pairs) return;
   const int R = b.read_len[b.pair_read[p]];
   const int H = b.hap_len[b.pair_hap[p]];
-  const uint32_t ns = (uint32_t)min((R + 15) >> 4, 0xFFFF);
+  const uint32_t ns = (uint32_t)min((R + 15) >> 4, 0xFFF);
   const uint32_t hh = (uint32_t)min(max(H, 0), 0xFFFF);
-  keys[p] = ((0xFFFFu - ns) << 16) | (0xFFFFu - hh);
+  const uint32_t rc = (uint32_t)(kPhmmClasses - 1 - phmm_class(max(H, 0)));
+  keys[p] = (rc << 28) | ((0xFFFu - ns) << 16) | (0xFFFFu - hh);
   idx[p] = (int32_t)p;
 }
 
-// Slots (ring entries and hap bytes) = column + 16 for columns -16 .. Hmax + 34:
-// stripes run to Hmax + 15 rounded up to a 16-step block, plus four steps of
-// read-ahead.
-static int nslot_for(int max_hap_len) { return ((max_hap_len + 51 + 15) / 16) * 16; }
+// bounds[j] = first sorted position of reversed class j (j = 0: the longest class); bounds[kPhmmClasses] = n.
+__global__ void phmm_bounds_kernel(const uint32_t* __restrict__ keys, long long n, int64_t* __restrict__ bounds) {
+  const long long k = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (k > n) return;
+  const int cur = (k < n) ? (int)(keys[k] >> 28) : kPhmmClasses;
+  const int prev = (k > 0) ? (int)(keys[k - 1] >> 28) : -1;
+  for (int j = prev + 1; j <= cur; ++j) bounds[j] = k;
+}
 
 int launch_phmm_keys(const PhmmDevBatch& b, uint32_t* keys, int32_t* idx, hipStream_t s) {
   if (b.n_pairs <= 0) return FCS_OK;
@@ -337,12 +367,19 @@ int launch_phmm_keys(const PhmmDevBatch& b, uint32_t* keys, int32_t* idx, hipStr
   return FCS_OK;
 }
 
+int launch_phmm_bounds(const uint32_t* sorted_keys, int64_t n, int64_t* bounds, hipStream_t s) {
+  const int bs = 256;
+  hipLaunchKernelGGL(phmm_bounds_kernel, dim3((unsigned)((n + 1 + bs - 1) / bs)), dim3(bs), 0, s, sorted_keys,
+                     (long long)n, bounds);
+  FCS_HIP_CHECK(hipGetLastError());
+  return FCS_OK;
+}
+
 template <typename T, bool EXACT, bool RESCUE>
 static int launch_one(const PhmmDevBatch& b, const int32_t* order, const unsigned long long* count_dev,
-                      long long count_host, long long max_groups, int max_hap_len, const PhmmTables<T>& tab,
-                      double* out, int32_t* rescue_list, unsigned long long* rescue_count, float thr,
-                      bool use_rescue, hipStream_t s) {
-  const int nslot = nslot_for(max_hap_len);
+                      long long count_host, const int64_t* bounds, int cls, int nslot, long long max_groups,
+                      const PhmmTables<T>& tab, double* out, int32_t* rescue_list, unsigned long long* rescue_count,
+                      float thr, bool use_rescue, hipStream_t s) {
   const size_t lds = (size_t)4 * nslot * (sizeof(PhRing<T>) + 1);
   if (lds > 160 * 1024)
     return fail(FCS_ERR_UNSUPPORTED, "[E::fcship] max_hap_len too large for the LDS boundary ring");
@@ -353,22 +390,35 @@ static int launch_one(const PhmmDevBatch& b, const int32_t* order, const unsigne
   const long long cap = 256LL * 64;  // grid-stride beyond this
   if (grid > cap) grid = cap;
   if (grid < 1) grid = 1;
-  hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(64), lds, s, b, order, count_dev, count_host, nslot, tab, out,
-                     rescue_list, rescue_count, thr, use_rescue ? 1 : 0);
+  hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(64), lds, s, b, order, count_dev, count_host, bounds, cls, nslot,
+                     tab, out, rescue_list, rescue_count, thr, use_rescue ? 1 : 0);
   FCS_HIP_CHECK(hipGetLastError());
   return FCS_OK;
 }
 
 int launch_phmm_forward(const PhmmDevBatch& b, const int32_t* order, int64_t count, int max_hap_len,
-                        const DeviceTables& t, bool exact, double* out, int32_t* rescue_list,
+                        const int64_t* bounds, const DeviceTables& t, bool exact, double* out, int32_t* rescue_list,
                         unsigned long long* rescue_count, float thr, bool use_rescue, hipStream_t s) {
   if (count <= 0) return FCS_OK;
   const long long groups = (count + 3) / 4;
-  if (exact)
-    return launch_one<float, true, false>(b, order, nullptr, count, groups, max_hap_len, t.tf, out, rescue_list,
-                                          rescue_count, thr, use_rescue, s);
-  return launch_one<float, false, false>(b, order, nullptr, count, groups, max_hap_len, t.tf, out, rescue_list,
-                                         rescue_count, thr, use_rescue, s);
+  const int ns_max = nslot_for(max_hap_len);
+  const int c_max = phmm_class(max_hap_len);
+  // One launch per hap-length class (ranges from the device-side bounds), forked
+  // over streams so a class's tail overlaps the next class; classes above the
+  // batch's longest haplotype are empty and not launched.
+  hipStream_t fs[kForkStreams];
+  if (const int rc = fork_streams(s, fs); rc != FCS_OK) return rc;
+  for (int j = kPhmmClasses - 1 - c_max; j < kPhmmClasses; ++j) {
+    const int c = kPhmmClasses - 1 - j;
+    const int ns = (c == kPhmmClasses - 1) ? ns_max : std::min(224 + 32 * c, ns_max);
+    hipStream_t st = fs[j % kForkStreams];
+    const int rc = exact ? launch_one<float, true, false>(b, order, nullptr, count, bounds, j, ns, groups, t.tf, out,
+                                                           rescue_list, rescue_count, thr, use_rescue, st)
+                         : launch_one<float, false, false>(b, order, nullptr, count, bounds, j, ns, groups, t.tf, out,
+                                                            rescue_list, rescue_count, thr, use_rescue, st);
+    if (rc != FCS_OK) return rc;
+  }
+  return join_streams(s, fs);
 }
 
 int launch_phmm_rescue(const PhmmDevBatch& b, const int32_t* list, const unsigned long long* count_dev,
@@ -380,10 +430,10 @@ int launch_phmm_rescue(const PhmmDevBatch& b, const int32_t* list, const unsigne
   long long groups = (max_count + 3) / 4;
   if (groups > 2048) groups = 2048;
   if (exact)
-    return launch_one<double, true, true>(b, list, count_dev, 0, groups, max_hap_len, t.td, out, nullptr, nullptr,
-                                          0.f, false, s);
-  return launch_one<double, false, true>(b, list, count_dev, 0, groups, max_hap_len, t.td, out, nullptr, nullptr, 0.f,
-                                         false, s);
+    return launch_one<double, true, true>(b, list, count_dev, 0, nullptr, 0, nslot_for(max_hap_len), groups, t.td, out,
+                                          nullptr, nullptr, 0.f, false, s);
+  return launch_one<double, false, true>(b, list, count_dev, 0, nullptr, 0, nslot_for(max_hap_len), groups, t.td, out,
+                                         nullptr, nullptr, 0.f, false, s);
 }
 
 }  // namespace fcs
