@@ -35,6 +35,7 @@ import fcship  # noqa: E402  (after torch: one HIP runtime per process)
 
 METRIC = "PairHMM GCUPS + banded-SW GCUPS per GPU; end-to-end htc regions/sec at 8 GPUs"
 FLOPS_PER_CELL = 11          # M 5 + I 3 + D 3 (FMA = 2)
+VALU_LANE_INSTR_PEAK = 256 * 4 * 32 * 2.4e9  # lane-instructions/s: one wave64 VALU op per 2 cycles per SIMD
 FP32_VECTOR_PEAK_TF = 157.3  # MI355X_MICROARCH.md chip table (spec)
 HBM_PEAK_GBS = 8000.0
 
@@ -289,7 +290,11 @@ def main():
         "roofline": {"bound": "valu", "achieved": round(achieved_tf, 3), "peak": FP32_VECTOR_PEAK_TF,
                      "unit": "TFLOP/s", "frac": round(achieved_tf / FP32_VECTOR_PEAK_TF, 4),
                      "traffic": traffic,
-                     "kernel": "phmm_kernel<float> (fp32 forward)",
+                     "kernel": "phmm_kernel<float,false,false>: fp32 forward pass = one launch per hap-length "
+                               "class, overlapped on 4 streams; achieved = algorithmic FLOPs / pass time (HIP events "
+                               "on the launch stream; rocprof pass span in profiles/r1/r1c_phmm_summary.json)",
+                     "valu_instr_per_cell": 12.0,
+                     "valu_issue_frac": round(ph["cells"] / fwd_s * 12.0 / VALU_LANE_INSTR_PEAK, 4),
                      "kernel_gcups": round(ph["cells"] / fwd_s / 1e9, 3),
                      "algorithmic_bytes_per_launch": alg_bytes,
                      "algorithmic_hbm_GBs": round(alg_bytes / fwd_s / 1e9, 2),
@@ -305,7 +310,12 @@ def main():
         line["bsw"] = {"workload": "C3: ksw_extend2 left/right seed extensions of 2x151 bp reads, bwa defaults",
                        "c3_gcups": round(r3["gcups"], 3), "c3_tasks": r3["tasks"], "c3_ms": round(r3["ms"], 3),
                        "fixed_151x251_gcups": round(rf["gcups"], 3), "fixed_tasks": rf["tasks"],
-                       "int_ops_per_cell": 12}
+                       "roofline": {"bound": "valu", "valu_instr_per_cell": 16,
+                                    "achieved": round(r3["gcups"] * 16 / 1e3, 3), "peak": VALU_LANE_INSTR_PEAK / 1e12,
+                                    "unit": "T lane-instr/s", "frac": round(r3["gcups"] * 16e9 / VALU_LANE_INSTR_PEAK, 4),
+                                    "fixed_frac": round(rf["gcups"] * 16e9 / VALU_LANE_INSTR_PEAK, 4),
+                                    "note": "16 = VALU instructions of the lane kernel's in-band cell (ISA count); "
+                                            "peak = 256 CU x 4 SIMD x 32 lanes x 2.4 GHz"}}
         if world == 1 and not args.no_cpu_baseline:
             line["bsw"]["cpu_baseline"] = cpu_baseline_bsw(
                 fcship.synth_bsw(args.seed + 1, 20000, read_len=151, ref_len=10_000_000), 0,

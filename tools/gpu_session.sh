@@ -24,13 +24,13 @@ for step in "$@"; do
     tests) run pytest_gpu 900 python -m pytest tests -m gpu -q -p no:cacheprovider ;;
     smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench) run bench 900 python bench.py ;;
-    benchq) run benchq 600 python bench.py --steps 3 --warmup 1 --no-cpu-baseline ;;
+    benchq) run benchq 600 python bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-e2e ;;
     prof) run prof 900 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o run --output-format csv -- \
-            python3 "$ROOT/bench.py" --steps 3 --warmup 1 --no-cpu-baseline ;;
+            python3 "$ROOT/bench.py" --steps 3 --warmup 1 --no-cpu-baseline --no-e2e ;;
     pmc) run pmc 900 rocprofv3 --pmc FETCH_SIZE -d "$OUT/pmc_fetch" -o run --output-format csv -- \
-            python3 "$ROOT/bench.py" --steps 1 --warmup 0 --no-cpu-baseline --no-bsw &&
+            python3 "$ROOT/bench.py" --steps 1 --warmup 0 --no-cpu-baseline --no-bsw --no-e2e &&
          run pmc2 900 rocprofv3 --pmc WRITE_SIZE -d "$OUT/pmc_write" -o run --output-format csv -- \
-            python3 "$ROOT/bench.py" --steps 1 --warmup 0 --no-cpu-baseline --no-bsw ;;
+            python3 "$ROOT/bench.py" --steps 1 --warmup 0 --no-cpu-baseline --no-bsw --no-e2e ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac
 done
