@@ -55,9 +55,26 @@ template <int NC>
 struct LaneRow {
   int beg, end, h1, f;
   uint32_t key;  // max over the row of (h << 16 | j): row max and its arg-max, ties to the larger j
+  uint32_t kpend;  // key candidate of the even column of a pair, folded with the odd one by one v_max3
   uint32_t pack;
   uint32_t nz[NZW<NC>];
 };
+
+// m ? a : b per bit (v_bfi_b32); m is all-ones or zero here.  Inline asm so
+// the compiler does not turn it back into compare + v_cndmask.
+__device__ __forceinline__ uint32_t bfi(uint32_t m, uint32_t a, uint32_t b) {
+  uint32_t r;
+  asm("v_bfi_b32 %0, %1, %2, %3" : "=v"(r) : "v"(m), "v"(a), "v"(b));
+  return r;
+}
+
+// Row key update in pairs of columns: even J parks its candidate, odd J folds
+// both with one v_max3 (chunks hold an even number of columns).
+template <int J, int NC>
+__device__ __forceinline__ void fold_key(LaneRow<NC>& r, uint32_t k) {
+  if constexpr (J % 2 == 0) r.kpend = k;
+  else r.key = max(max(r.key, r.kpend), k);
+}
 
 // bwa's inner-loop body for column J.  MASKED = false: every working lane has
 // J inside [beg, end).  MASKED = true (a chunk crossing some lane's band
@@ -87,7 +104,7 @@ __device__ __forceinline__ void lane_cell(uint32_t (&eh)[NC], const uint32_t (&q
     fn = max(max(r.f - e_ins, M - oe_ins), 0);
   }
   if constexpr (!MASKED) {
-    r.key = max(r.key, ((uint32_t)h << 16) | (uint32_t)J);
+    fold_key<J>(r, ((uint32_t)h << 16) | (uint32_t)J);
     r.f = fn;
     const uint32_t xn = (uint32_t)r.h1 | ((uint32_t)en << 16);
     eh[J] = xn;
@@ -98,12 +115,12 @@ __device__ __forceinline__ void lane_cell(uint32_t (&eh)[NC], const uint32_t (&q
     const uint32_t mx = (uint32_t)__builtin_amdgcn_sbfe(bm, 16 + J % 16, 1);  // J in [beg, end]
     // a masked-off h contributes (0 << 16 | J): below any positive row max,
     // and a zero row max ends the task before its arg-max is used
-    r.key = max(r.key, (((uint32_t)h & ms) << 16) | (uint32_t)J);
-    r.f = (int)(((uint32_t)fn & ms) | ((uint32_t)r.f & ~ms));
+    fold_key<J>(r, (((uint32_t)h & ms) << 16) | (uint32_t)J);
+    r.f = (int)bfi(ms, (uint32_t)fn, (uint32_t)r.f);
     const uint32_t xn = (uint32_t)r.h1 | (((uint32_t)en & ms) << 16);
-    const uint32_t xo = (xn & mx) | (x & ~mx);
+    const uint32_t xo = bfi(mx, xn, x);
     eh[J] = xo;
-    r.h1 = (int)(((uint32_t)h & ms) | ((uint32_t)r.h1 & ~ms));
+    r.h1 = (int)bfi(ms, (uint32_t)h, (uint32_t)r.h1);
     r.nz[J / 32] = or_nz_bit<J % 32>(r.nz[J / 32], xo);  // bits outside [beg, end] are masked after the row
   }
 }
@@ -119,6 +136,7 @@ __device__ __forceinline__ void lane_chunk(uint32_t (&eh)[NC], const uint32_t (&
                                            const bool work, const int cmin, const int cmax, const int e_del,
                                            const int oe_del, const int e_ins, const int oe_ins) {
   constexpr int L = (NC - 16 * C) < 16 ? (NC - 16 * C) : 16;  // last chunk may be partial
+  static_assert(L % 2 == 0, "fold_key pairs columns within a chunk");
   if (16 * C <= cmax && 16 * C + L - 1 >= cmin) {
     // Fast path when the whole chunk lies strictly inside the band of every
     // live lane (no per-column band test, no eh[end] write in this chunk).
