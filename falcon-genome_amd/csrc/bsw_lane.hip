@@ -11,7 +11,7 @@
 // a fully unrolled column loop, so the band bookkeeping (including the stale
 // eh[] entries that bwa re-reads when the band grows) is reproduced exactly.
 // Per cell: 2 ops for the profile score (5-bit fields selected by the query
-// code), then bwa's max/add chain; no cross-lane traffic at all.  A 16-column
+// code), then bwa's max/add chain; no cross-lane traffic at all.  A kCW-column
 // chunk is skipped when it lies outside the band of every live lane (one
 // wave-wide min/max per row), and lanes whose task ended idle under EXEC.
 #include <hip/hip_runtime.h>
@@ -25,6 +25,10 @@
 namespace fcs {
 
 __device__ __forceinline__ int wave_min_i(int v) { return -wave_max(-v); }
+
+// Columns per chunk: the unit of the per-row band skip and of the
+// fast (inside every lane's band) vs masked (some lane's band edge) choice.
+constexpr int kCW = 8;
 
 // registers holding the per-column query offsets (q * 5), six 5-bit fields each
 template <int NC> constexpr int QW = (NC + 5) / 6;
@@ -111,8 +115,8 @@ __device__ __forceinline__ void lane_cell(uint32_t (&eh)[NC], const uint32_t (&q
     r.h1 = h;
     r.nz[J / 32] = or_nz_bit<J % 32>(r.nz[J / 32], xn);
   } else {
-    const uint32_t ms = (uint32_t)__builtin_amdgcn_sbfe(bm, J % 16, 1);       // J in [beg, end)
-    const uint32_t mx = (uint32_t)__builtin_amdgcn_sbfe(bm, 16 + J % 16, 1);  // J in [beg, end]
+    const uint32_t ms = (uint32_t)__builtin_amdgcn_sbfe(bm, J % kCW, 1);        // J in [beg, end)
+    const uint32_t mx = (uint32_t)__builtin_amdgcn_sbfe(bm, kCW + J % kCW, 1);  // J in [beg, end]
     // a masked-off h contributes (0 << 16 | J): below any positive row max,
     // and a zero row max ends the task before its arg-max is used
     fold_key<J>(r, (((uint32_t)h & ms) << 16) | (uint32_t)J);
@@ -125,9 +129,9 @@ __device__ __forceinline__ void lane_cell(uint32_t (&eh)[NC], const uint32_t (&q
   }
 }
 
-// Bits [lo, hi) of a 16-column chunk starting at column c0, clamped.
+// Bits [lo, hi) of a kCW-column chunk starting at column c0, clamped.
 __device__ __forceinline__ uint32_t chunk_bits(int lo, int hi, int c0) {
-  const int a = min(max(lo - c0, 0), 16), b = min(max(hi - c0, 0), 16);
+  const int a = min(max(lo - c0, 0), kCW), b = min(max(hi - c0, 0), kCW);
   return ((1u << b) - 1u) & ~((1u << a) - 1u);
 }
 
@@ -135,23 +139,23 @@ template <int C, int NC, bool SYM>
 __device__ __forceinline__ void lane_chunk(uint32_t (&eh)[NC], const uint32_t (&qr)[QW<NC>], LaneRow<NC>& r,
                                            const bool work, const int cmin, const int cmax, const int e_del,
                                            const int oe_del, const int e_ins, const int oe_ins) {
-  constexpr int L = (NC - 16 * C) < 16 ? (NC - 16 * C) : 16;  // last chunk may be partial
+  constexpr int L = (NC - kCW * C) < kCW ? (NC - kCW * C) : kCW;  // last chunk may be partial
   static_assert(L % 2 == 0, "fold_key pairs columns within a chunk");
-  if (16 * C <= cmax && 16 * C + L - 1 >= cmin) {
+  if (kCW * C <= cmax && kCW * C + L - 1 >= cmin) {
     // Fast path when the whole chunk lies strictly inside the band of every
     // live lane (no per-column band test, no eh[end] write in this chunk).
-    const bool inside = !work || (r.beg <= 16 * C && 16 * C + L - 1 < r.end);
+    const bool inside = !work || (r.beg <= kCW * C && kCW * C + L - 1 < r.end);
     if (__ballot(!inside) == 0ull) {
       if (work) {
         [&]<int... S>(std::integer_sequence<int, S...>) {
-          (lane_cell<16 * C + S, NC, SYM, false>(eh, qr, r, 0u, e_del, oe_del, e_ins, oe_ins), ...);
+          (lane_cell<kCW * C + S, NC, SYM, false>(eh, qr, r, 0u, e_del, oe_del, e_ins, oe_ins), ...);
         }(std::make_integer_sequence<int, L>{});
       }
     } else {
       const uint32_t bm =
-          work ? (chunk_bits(r.beg, r.end, 16 * C) | (chunk_bits(r.beg, r.end + 1, 16 * C) << 16)) : 0u;
+          work ? (chunk_bits(r.beg, r.end, kCW * C) | (chunk_bits(r.beg, r.end + 1, kCW * C) << kCW)) : 0u;
       [&]<int... S>(std::integer_sequence<int, S...>) {
-        (lane_cell<16 * C + S, NC, SYM, true>(eh, qr, r, bm, e_del, oe_del, e_ins, oe_ins), ...);
+        (lane_cell<kCW * C + S, NC, SYM, true>(eh, qr, r, bm, e_del, oe_del, e_ins, oe_ins), ...);
       }(std::make_integer_sequence<int, L>{});
     }
   }
@@ -255,7 +259,7 @@ __device__ __forceinline__ void lane_wave(const BswDevBatch& b, const BswParams&
     for (int k = 0; k < NZW<NC>; ++k) r.nz[k] = 0;
     [&]<int... C>(std::integer_sequence<int, C...>) {
       (lane_chunk<C, NC, SYM>(eh, qr, r, work, cmin, cmax, e_del, oe_del, e_ins, oe_ins), ...);
-    }(std::make_integer_sequence<int, (NC + 15) / 16>{});
+    }(std::make_integer_sequence<int, (NC + kCW - 1) / kCW>{});
     if (empty) {
       // bwa still stores eh[end] = {h1, 0}; the loop index equals beg here
 #pragma unroll
