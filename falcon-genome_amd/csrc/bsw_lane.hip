@@ -352,9 +352,16 @@ __global__ void bsw_keys_kernel(const BswDevBatch b, const BswParams p, uint32_t
                                 int32_t* __restrict__ idx) {
   const long long k = (long long)blockIdx.x * blockDim.x + threadIdx.x;
   if (k >= b.n) return;
-  const int qlen = b.qlen[k], tlen = b.tlen[k];
-  const uint32_t bk = (uint32_t)bsw_bucket(qlen, b.h0[k], p);
-  keys[k] = (bk << 28) | ((uint32_t)min(max(qlen, 0), 1023) << 18) | (uint32_t)min(max(tlen, 0), 262143);
+  const int qlen = b.qlen[k], tlen = b.tlen[k], h0 = b.h0[k];
+  const uint32_t bk = (uint32_t)bsw_bucket(qlen, h0, p);
+  // Rows a task is expected to run: an extension that keeps matching peaks
+  // near row qlen with score ~h0 + qlen*max_mat and then decays by e_del per
+  // row until the row max hits 0 (bwa's m == 0 exit), capped by tlen.  Tasks
+  // of a wave sorted by this run about as long as each other, so fewer lanes
+  // idle behind the wave's longest task.
+  const long long est = min((long long)tlen, (long long)qlen +
+                                                 ((long long)h0 + (long long)qlen * p.max_mat) / max(p.e_del, 1) + 1);
+  keys[k] = (bk << 28) | ((uint32_t)min(max(qlen, 0), 1023) << 18) | (uint32_t)min(max(est, 0LL), 262143LL);
   idx[k] = (int32_t)k;
 }
 
