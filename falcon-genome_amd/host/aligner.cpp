@@ -6,6 +6,7 @@
 #include <fstream>
 #include <iostream>
 #include <map>
+#include <thread>
 
 #include "common.h"
 #include "config.h"
@@ -43,6 +44,22 @@ int infer_bw(int l1, int l2, int score, int a, int q, int r) {
   int w = (int)((double)(std::min(l1, l2) * a - score - q) / r + 2.);
   if (w < std::abs(l1 - l2)) w = std::abs(l1 - l2);
   return w;
+}
+
+// Static split of [0, n) over up to `threads` std::threads.
+template <typename F>
+void parallel_for(size_t n, int threads, F&& fn) {
+  const size_t nt = std::max<size_t>(1, std::min<size_t>((size_t)std::max(threads, 1), n / 256 + 1));
+  if (nt == 1) {
+    for (size_t i = 0; i < n; ++i) fn(i);
+    return;
+  }
+  std::vector<std::thread> th;
+  for (size_t t = 0; t < nt; ++t)
+    th.emplace_back([&, t] {
+      for (size_t i = n * t / nt; i < n * (t + 1) / nt; ++i) fn(i);
+    });
+  for (auto& x : th) x.join();
 }
 
 // One read's alignment in progress.
@@ -124,23 +141,24 @@ AlignStats align_reads(const Reference& ref, const KmerIndex& idx, const std::ve
   const uint64_t kmask = (1ull << (2 * k)) - 1;
   std::vector<Aln> alns(seqs.size());
 
-  // ---- seeds and the best chain per read
-  for (size_t r = 0; r < seqs.size(); ++r) {
+  // ---- seeds and the best chain per read (host threads over reads)
+  st.reads = (int64_t)seqs.size();
+  auto seed_read = [&](size_t r) {
     Aln& A = alns[r];
     A.read = (int)r;
-    ++st.reads;
-    struct Best {
-      int hits = 0;
-      int64_t diag = 0;
-      int qp = 0;
-      uint64_t g = 0;
-    } best[2], second;  // best per strand
-    int best_hits = 0, second_hits = 0;
+    struct Hit {
+      int64_t d;
+      int qp;
+      uint64_t g;
+    };
+    std::vector<Hit> hits;
+    int best_hits = 0, second_hits = 0, best_qp = 0;
+    uint64_t best_g = 0;
     bool best_rev = false;
     for (int strand = 0; strand < 2; ++strand) {
       const std::string s = strand ? revcomp(seqs[r]) : seqs[r];
       const std::vector<uint8_t> c = encode(s);
-      std::map<int64_t, std::pair<int, std::pair<int, uint64_t>>> diag;  // diag → (hits, (first qp, g))
+      hits.clear();
       for (int qp = 0; qp + k <= (int)c.size(); qp += opt.seed_step) {
         uint64_t key = 0;
         bool ok = true;
@@ -151,47 +169,39 @@ AlignStats align_reads(const Reference& ref, const KmerIndex& idx, const std::ve
         if (!ok) continue;
         const auto [b, e] = idx.lookup(key);
         if (e - b == 0 || e - b > opt.max_occ) continue;
-        for (const uint64_t* p = b; p != e; ++p) {
-          const int64_t d = (int64_t)*p - qp;
-          auto& x = diag[d];
-          if (x.first++ == 0) x.second = {qp, *p};
-        }
+        for (const uint64_t* p = b; p != e; ++p) hits.push_back({(int64_t)*p - qp, qp, *p});
       }
-      // cluster diagonals within +-8 (indels shift them)
-      int64_t cl_start = 0, cl_prev = 0;
-      int cl_hits = 0;
-      std::pair<int, uint64_t> cl_seed{0, 0};
-      int cl_seed_hits = -1;
-      auto close = [&](void) {
-        if (cl_hits == 0) return;
-        if (cl_hits > best[strand].hits) best[strand] = {cl_hits, cl_start, cl_seed.first, cl_seed.second};
-        if (cl_hits > best_hits) {
+      // chains: diagonals within 8 of the previous one (indels shift them);
+      // a chain's seed is its earliest hit on its most supported diagonal
+      std::sort(hits.begin(), hits.end(), [](const Hit& x, const Hit& y) { return x.d != y.d ? x.d < y.d : x.qp < y.qp; });
+      size_t i = 0;
+      while (i < hits.size()) {
+        size_t j = i;
+        int n = 0, dn_best = 0;
+        const Hit* seed = &hits[i];
+        while (j < hits.size() && (j == i || hits[j].d - hits[j - 1].d <= 8)) {
+          size_t e = j;
+          while (e < hits.size() && hits[e].d == hits[j].d) ++e;  // one diagonal
+          if ((int)(e - j) > dn_best) {
+            dn_best = (int)(e - j);
+            seed = &hits[j];
+          }
+          n += (int)(e - j);
+          j = e;
+        }
+        if (n > best_hits) {
           second_hits = best_hits;
-          best_hits = cl_hits;
+          best_hits = n;
           best_rev = strand;
-        } else if (cl_hits > second_hits) {
-          second_hits = cl_hits;
+          best_qp = seed->qp;
+          best_g = seed->g;
+        } else if (n > second_hits) {
+          second_hits = n;
         }
-      };
-      for (const auto& [d, x] : diag) {
-        if (cl_hits == 0 || d - cl_prev > 8) {
-          close();
-          cl_start = d;
-          cl_hits = 0;
-          cl_seed_hits = -1;
-        }
-        cl_hits += x.first;
-        if (x.first > cl_seed_hits) {
-          cl_seed_hits = x.first;
-          cl_seed = x.second;
-        }
-        cl_prev = d;
+        i = j;
       }
-      close();
     }
-    (void)second;
-    if (best_hits == 0) continue;
-    const Best& B = best[best_rev ? 1 : 0];
+    if (best_hits == 0) return;
     A.rev = best_rev;
     A.seq = best_rev ? revcomp(seqs[r]) : seqs[r];
     A.q = encode(A.seq);
@@ -201,10 +211,10 @@ AlignStats align_reads(const Reference& ref, const KmerIndex& idx, const std::ve
       A.qual[i] = (uint8_t)(j < quals[r].size() ? std::max(0, quals[r][j] - 33) : 30);
     }
     int64_t off = 0;
-    A.contig = idx.contig_of(B.g, off);
+    A.contig = idx.contig_of(best_g, off);
     const std::string& R = ref.contigs[A.contig].seq;
     // grow the k-mer hit to a maximal exact match
-    int qs = B.qp, qe = B.qp + k;
+    int qs = best_qp, qe = best_qp + k;
     int64_t rs = off;
     while (qs > 0 && rs > 0 && A.q[qs - 1] < 4 && A.q[qs - 1] == code_of(R[rs - 1])) --qs, --rs;
     while (qe < (int)A.q.size() && rs + (qe - qs) < (int64_t)R.size() && A.q[qe] < 4 &&
@@ -215,7 +225,8 @@ AlignStats align_reads(const Reference& ref, const KmerIndex& idx, const std::ve
     A.seed_r = rs;
     A.mapped = true;
     A.mapq = second_hits >= best_hits ? 0 : std::min(60, (int)std::lround(60.0 * (best_hits - second_hits) / best_hits));
-  }
+  };
+  parallel_for(seqs.size(), opt.threads, seed_read);
 
   auto run_ext = [&](std::vector<fcs_bsw_task>& tasks, std::vector<fcs_bsw_result>& res) {
     res.resize(tasks.size());
@@ -397,9 +408,13 @@ AlignStats align_reads(const Reference& ref, const KmerIndex& idx, const std::ve
     }
   }
 
-  // ---- records
-  for (Aln& A : alns) {
-    BamRecord rec;
+  // ---- records (host threads; one slot per read keeps the input order)
+  const size_t base = out.size();
+  out.resize(base + alns.size());
+  std::vector<char> mapped_flag(alns.size(), 0);
+  parallel_for(alns.size(), opt.threads, [&](size_t ai) {
+    Aln& A = alns[ai];
+    BamRecord& rec = out[base + ai];
     rec.name = names[A.read];
     rec.set_aux_string("RG", opt.rg);
     if (!A.mapped || A.cigar.empty()) {
@@ -408,10 +423,9 @@ AlignStats align_reads(const Reference& ref, const KmerIndex& idx, const std::ve
       rec.qual.resize(rec.seq.size());
       for (size_t i = 0; i < rec.seq.size(); ++i)
         rec.qual[i] = (uint8_t)(i < quals[A.read].size() ? std::max(0, quals[A.read][i] - 33) : 30);
-      out.push_back(std::move(rec));
-      continue;
+      return;
     }
-    ++st.mapped;
+    mapped_flag[ai] = 1;
     std::vector<uint32_t> cig;
     if (A.qb > 0) cig.push_back(cigar_pack((uint32_t)A.qb, kS));
     for (uint32_t c : A.cigar) {
@@ -460,8 +474,8 @@ AlignStats align_reads(const Reference& ref, const KmerIndex& idx, const std::ve
     rec.set_aux_int("NM", nm);
     rec.set_aux_string("MD", md);
     rec.set_aux_int("AS", A.truesc);
-    out.push_back(std::move(rec));
-  }
+  });
+  for (char m : mapped_flag) st.mapped += m;
   st.seconds = (now_us() - t0) / 1e6;
   return st;
 }
@@ -526,6 +540,10 @@ int align_main(int argc, char** argv) {
   opt.gpu = gpus[0];
   opt.rg = rg;
   opt.chunk_size = conf().get_int("bwa.chunk_size");
+  {
+    const int nt = conf().get_int("bwa.nt");
+    opt.threads = nt > 0 ? nt : (int)std::min(16u, std::max(1u, std::thread::hardware_concurrency()));
+  }
   const KmerIndex idx(ref, opt.k);
   std::vector<BamRecord> recs;
   AlignStats tot;

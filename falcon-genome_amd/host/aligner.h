@@ -31,6 +31,7 @@ struct AlignOptions {
   int max_occ = 64;      // ignore k-mers with more hits
   int w = 100;           // band width
   int chunk_size = 100000;
+  int threads = 16;        // host threads for seeding / task building (bwa.nt)
   std::string rg = "sample", sample = "sample", platform = "illumina", library = "sample";
 };
 

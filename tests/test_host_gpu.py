@@ -136,3 +136,17 @@ def test_align_end_to_end(gpu, data, tmp_path):
     assert mapped / len(recs) >= 0.99
     assert same_pos / mapped >= 0.97, (same_pos, mapped)
     assert same_cig / mapped >= 0.9, (same_cig, mapped)
+
+
+def test_htc_gpu_slots_do_not_change_calls(gpu, data, tmp_path):
+    """Shards dealt over two GPU slots (both on device 0 here — the dealing
+    rule is the same as over two devices) and more concurrent tasks give the
+    same VCF as one slot: shards are independent, no exchange step."""
+    outs = []
+    for devs, nprocs in (("0", "1"), ("0,0", "4")):
+        out = tmp_path / f"htc_{nprocs}.vcf"
+        env = dict(ENV, FCS_GPU_DEVICES=devs, FCS_GATK_NPROCS=nprocs)
+        p = H.run_cli("htc", "-r", data / "ref.fasta", "-i", data / "sample.bam", "-o", out, env=env, cwd=tmp_path)
+        assert p.returncode == 0, p.stderr[-3000:]
+        outs.append([ln for ln in out.read_text().splitlines() if not ln.startswith("##source")])
+    assert outs[0] == outs[1]
