@@ -209,7 +209,7 @@ __global__ __launch_bounds__(64) void bsw_extend_kernel(const BswDevBatch b, con
                                                         int64_t* __restrict__ cells, const int32_t* __restrict__ order,
                                                         const int64_t* __restrict__ bounds) {
   extern __shared__ __align__(16) unsigned char tl[];
-  const long long lo = bounds[7], hi = bounds[8];
+  const long long lo = bounds[kBswWideBucket], hi = bounds[kBswWideBucket + 1];
   for (long long pos = lo + blockIdx.x; pos < hi; pos += gridDim.x) {
     const long long task = order[pos];
     const int qlen = b.qlen[task];

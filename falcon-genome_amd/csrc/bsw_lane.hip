@@ -52,6 +52,12 @@ __device__ __forceinline__ uint32_t or_nz_bit(uint32_t nz, uint32_t x) {
 // VALU-writes-VCC hazard nops either.
 __device__ __forceinline__ int diag_m(int hp, int s) { return min(hp + s, hp << 5); }
 
+// Registers holding bwa's eh[] for NC columns: one per column (h | e << 16),
+// or, when every score of the task fits a byte (B8), one per column pair
+// (h0 | e0 << 8 | h1 << 16 | e1 << 24) — half the register file, so the
+// 152-column kernel runs 3 waves per SIMD instead of 2.
+template <int NC, bool B8> constexpr int EhN = B8 ? NC / 2 : NC;
+
 // Words of the per-row "eh[j] != 0" bitmap (bit j for column j).
 template <int NC> constexpr int NZW = (NC + 31) / 32;
 
@@ -60,6 +66,7 @@ struct LaneRow {
   int beg, end, h1, f;
   uint32_t key;  // max over the row of (h << 16 | j): row max and its arg-max, ties to the larger j
   uint32_t kpend;  // key candidate of the even column of a pair, folded with the odd one by one v_max3
+  uint32_t xst;    // byte-packed layout: the even column's new 16-bit entry, stored with the odd one
   uint32_t pack;
   uint32_t nz[NZW<NC>];
 };
@@ -80,6 +87,15 @@ __device__ __forceinline__ void fold_key(LaneRow<NC>& r, uint32_t k) {
   else r.key = max(max(r.key, r.kpend), k);
 }
 
+// New entry of column J: direct, or (B8) parked for the even column and
+// stored with the odd one as one register (chunks hold whole pairs).
+template <int J, int NC, bool B8>
+__device__ __forceinline__ void eh_store(uint32_t (&eh)[(EhN<NC, B8>)], LaneRow<NC>& r, uint32_t v) {
+  if constexpr (!B8) eh[J] = v;
+  else if constexpr (J % 2 == 0) r.xst = v;
+  else eh[J / 2] = r.xst | (v << 16);
+}
+
 // bwa's inner-loop body for column J.  MASKED = false: every working lane has
 // J inside [beg, end).  MASKED = true (a chunk crossing some lane's band
 // edge): the body runs unconditionally and bit J of `bm` (low half: J in
@@ -87,13 +103,24 @@ __device__ __forceinline__ void fold_key(LaneRow<NC>& r, uint32_t k) {
 // sign-extended 1-bit masks and bit-selects instead of branches: eh[J] only
 // for J in [beg, end] (at J == end bwa stores {h1, 0}), h1 / f / the row key
 // only for J in [beg, end).  Lanes not working this row have bm = 0.
-template <int J, int NC, bool SYM, bool MASKED>
-__device__ __forceinline__ void lane_cell(uint32_t (&eh)[NC], const uint32_t (&qr)[QW<NC>], LaneRow<NC>& r,
+template <int J, int NC, bool SYM, bool MASKED, bool B8>
+__device__ __forceinline__ void lane_cell(uint32_t (&eh)[(EhN<NC, B8>)], const uint32_t (&qr)[QW<NC>], LaneRow<NC>& r,
                                           const uint32_t bm, const int e_del, const int oe_del, const int e_ins,
                                           const int oe_ins) {
-  const uint32_t x = eh[J];
-  const int hp = (int)(x & 0xFFFFu);
-  const int e = (int)(x >> 16);
+  constexpr int ES = B8 ? 8 : 16;  // bit offset of e inside a column entry
+  uint32_t x;                      // this column's entry (h | e << ES)
+  int hp, e;
+  if constexpr (B8) {
+    constexpr int sh = 16 * (J % 2);
+    const uint32_t w = eh[J / 2];
+    hp = (int)((w >> sh) & 0xFFu);
+    e = (int)((w >> (sh + 8)) & 0xFFu);
+    x = (w >> sh) & 0xFFFFu;
+  } else {
+    x = eh[J];
+    hp = (int)(x & 0xFFFFu);
+    e = (int)(x >> 16);
+  }
   const uint32_t qo = __builtin_amdgcn_ubfe(qr[J / 6], 5 * (J % 6), 5);
   const int s = field5(r.pack, qo);
   const int M = diag_m(hp, s);
@@ -110,8 +137,8 @@ __device__ __forceinline__ void lane_cell(uint32_t (&eh)[NC], const uint32_t (&q
   if constexpr (!MASKED) {
     fold_key<J>(r, ((uint32_t)h << 16) | (uint32_t)J);
     r.f = fn;
-    const uint32_t xn = (uint32_t)r.h1 | ((uint32_t)en << 16);
-    eh[J] = xn;
+    const uint32_t xn = (uint32_t)r.h1 | ((uint32_t)en << ES);
+    eh_store<J, NC, B8>(eh, r, xn);
     r.h1 = h;
     r.nz[J / 32] = or_nz_bit<J % 32>(r.nz[J / 32], xn);
   } else {
@@ -121,9 +148,9 @@ __device__ __forceinline__ void lane_cell(uint32_t (&eh)[NC], const uint32_t (&q
     // and a zero row max ends the task before its arg-max is used
     fold_key<J>(r, (((uint32_t)h & ms) << 16) | (uint32_t)J);
     r.f = (int)bfi(ms, (uint32_t)fn, (uint32_t)r.f);
-    const uint32_t xn = (uint32_t)r.h1 | (((uint32_t)en & ms) << 16);
+    const uint32_t xn = (uint32_t)r.h1 | (((uint32_t)en & ms) << ES);
     const uint32_t xo = bfi(mx, xn, x);
-    eh[J] = xo;
+    eh_store<J, NC, B8>(eh, r, xo);
     r.h1 = (int)bfi(ms, (uint32_t)h, (uint32_t)r.h1);
     r.nz[J / 32] = or_nz_bit<J % 32>(r.nz[J / 32], xo);  // bits outside [beg, end] are masked after the row
   }
@@ -135,8 +162,8 @@ __device__ __forceinline__ uint32_t chunk_bits(int lo, int hi, int c0) {
   return ((1u << b) - 1u) & ~((1u << a) - 1u);
 }
 
-template <int C, int NC, bool SYM>
-__device__ __forceinline__ void lane_chunk(uint32_t (&eh)[NC], const uint32_t (&qr)[QW<NC>], LaneRow<NC>& r,
+template <int C, int NC, bool SYM, bool B8>
+__device__ __forceinline__ void lane_chunk(uint32_t (&eh)[(EhN<NC, B8>)], const uint32_t (&qr)[QW<NC>], LaneRow<NC>& r,
                                            const bool work, const int cmin, const int cmax, const int e_del,
                                            const int oe_del, const int e_ins, const int oe_ins) {
   constexpr int L = (NC - kCW * C) < kCW ? (NC - kCW * C) : kCW;  // last chunk may be partial
@@ -148,21 +175,21 @@ __device__ __forceinline__ void lane_chunk(uint32_t (&eh)[NC], const uint32_t (&
     if (__ballot(!inside) == 0ull) {
       if (work) {
         [&]<int... S>(std::integer_sequence<int, S...>) {
-          (lane_cell<kCW * C + S, NC, SYM, false>(eh, qr, r, 0u, e_del, oe_del, e_ins, oe_ins), ...);
+          (lane_cell<kCW * C + S, NC, SYM, false, B8>(eh, qr, r, 0u, e_del, oe_del, e_ins, oe_ins), ...);
         }(std::make_integer_sequence<int, L>{});
       }
     } else {
       const uint32_t bm =
           work ? (chunk_bits(r.beg, r.end, kCW * C) | (chunk_bits(r.beg, r.end + 1, kCW * C) << kCW)) : 0u;
       [&]<int... S>(std::integer_sequence<int, S...>) {
-        (lane_cell<kCW * C + S, NC, SYM, true>(eh, qr, r, bm, e_del, oe_del, e_ins, oe_ins), ...);
+        (lane_cell<kCW * C + S, NC, SYM, true, B8>(eh, qr, r, bm, e_del, oe_del, e_ins, oe_ins), ...);
       }(std::make_integer_sequence<int, L>{});
     }
   }
 }
 
 // 64 consecutive tasks of the sorted schedule, starting at `base`.
-template <int NC, bool SYM>
+template <int NC, bool SYM, bool B8>
 __device__ __forceinline__ void lane_wave(const BswDevBatch& b, const BswParams& p, const int32_t* __restrict__ order,
                                           const long long base, const long long hi, int32_t* __restrict__ res,
                                           int64_t* __restrict__ cells_out) {
@@ -195,7 +222,7 @@ __device__ __forceinline__ void lane_wave(const BswDevBatch& b, const BswParams&
     }
     qr[c] = v;
   }
-  uint32_t eh[NC];
+  uint32_t eh[(EhN<NC, B8>)];
   const int h1v = h0 > oe_ins ? h0 - oe_ins : 0;
 #pragma unroll
   for (int j = 0; j < NC; ++j) {
@@ -203,7 +230,12 @@ __device__ __forceinline__ void lane_wave(const BswDevBatch& b, const BswParams&
     if (j == 0) hv = h0;
     else if (j == 1) hv = (j <= qlen) ? h1v : 0;
     else hv = (j <= qlen) ? max(h1v - (j - 1) * e_ins, 0) : 0;
-    eh[j] = (uint32_t)hv;
+    if constexpr (B8) {
+      if (j % 2 == 0) eh[j / 2] = (uint32_t)hv;
+      else eh[j / 2] |= (uint32_t)hv << 16;
+    } else {
+      eh[j] = (uint32_t)hv;
+    }
   }
   {
     int max_ins = (int)((double)(qlen * p.max_mat + p.end_bonus - p.o_ins) / e_ins + 1.);
@@ -258,13 +290,20 @@ __device__ __forceinline__ void lane_wave(const BswDevBatch& b, const BswParams&
 #pragma unroll
     for (int k = 0; k < NZW<NC>; ++k) r.nz[k] = 0;
     [&]<int... C>(std::integer_sequence<int, C...>) {
-      (lane_chunk<C, NC, SYM>(eh, qr, r, work, cmin, cmax, e_del, oe_del, e_ins, oe_ins), ...);
+      (lane_chunk<C, NC, SYM, B8>(eh, qr, r, work, cmin, cmax, e_del, oe_del, e_ins, oe_ins), ...);
     }(std::make_integer_sequence<int, (NC + kCW - 1) / kCW>{});
     if (empty) {
       // bwa still stores eh[end] = {h1, 0}; the loop index equals beg here
 #pragma unroll
       for (int j = 0; j < NC; ++j)
-        if (j == r.end) eh[j] = (uint32_t)r.h1;
+        if (j == r.end) {
+          if constexpr (B8) {
+            const uint32_t m16 = (j % 2) ? 0xFFFF0000u : 0xFFFFu;
+            eh[j / 2] = (eh[j / 2] & ~m16) | (((uint32_t)r.h1 << (16 * (j % 2))) & m16);
+          } else {
+            eh[j] = (uint32_t)r.h1;
+          }
+        }
       if (r.beg == qlen) {
         max_ie = gscore > r.h1 ? max_ie : i;
         gscore = gscore > r.h1 ? gscore : r.h1;
@@ -323,29 +362,34 @@ __device__ __forceinline__ void lane_wave(const BswDevBatch& b, const BswParams&
 
 // One launch per bucket; the grid strides over the bucket's range so empty
 // buckets cost a few hundred idle workgroups, not n/64.
-template <int NC, bool SYM>
-__global__ __launch_bounds__(64, 2) void bsw_lane_kernel(const BswDevBatch b, const BswParams p,
+template <int NC, bool SYM, bool B8>
+__global__ __launch_bounds__(64, B8 ? 3 : 2) void bsw_lane_kernel(const BswDevBatch b, const BswParams p,
                                                       const int32_t* __restrict__ order,
                                                       const int64_t* __restrict__ bounds, const int bucket,
                                                       int32_t* __restrict__ res, int64_t* __restrict__ cells_out) {
   const long long lo = bounds[bucket], hi = bounds[bucket + 1];
   for (long long base = lo + 64LL * blockIdx.x; base < hi; base += 64LL * gridDim.x)
-    lane_wave<NC, SYM>(b, p, order, base, hi, res, cells_out);
+    lane_wave<NC, SYM, B8>(b, p, order, base, hi, res, cells_out);
 }
 
-// Bucket of a task: 0..6 = lane kernel with 16/32/48/64/96/128/152 register
-// columns (152 = bwa reads up to 151 bp), 7 = wave-per-task kernel (long queries or out-of-int16 scores).
+// Bucket of a task: 0..6 = 16-bit lane kernels with 16/32/48/64/96/128/152
+// register columns (152 = bwa reads up to 151 bp); 7..9 = byte-packed lane
+// kernels with 96/128/152 columns for tasks whose scores all fit a byte (the
+// register saving buys a third wave per SIMD there; at <= 64 columns the
+// 16-bit layout already runs 3-4 waves and is cheaper per cell);
+// kBswWideBucket = wave-per-task kernel (long queries, scores beyond int16,
+// matrices beyond 5 bits).
 __device__ __forceinline__ int bsw_bucket(int qlen, int h0, const BswParams& p) {
-  if (!p.lane_ok || h0 <= 0 || (long long)h0 + (long long)qlen * p.max_mat >= 32000) return 7;
+  const long long bound = (long long)h0 + (long long)qlen * p.max_mat;  // no cell can score more
+  if (!p.lane_ok || h0 <= 0 || bound >= 32000) return kBswWideBucket;
   const int need = qlen + 1;
   if (need <= 16) return 0;
   if (need <= 32) return 1;
   if (need <= 48) return 2;
   if (need <= 64) return 3;
-  if (need <= 96) return 4;
-  if (need <= 128) return 5;
-  if (need <= 152) return 6;
-  return 7;
+  const int c = need <= 96 ? 4 : need <= 128 ? 5 : need <= 152 ? 6 : -1;
+  if (c < 0) return kBswWideBucket;
+  return bound < 256 ? c + 3 : c;
 }
 
 __global__ void bsw_keys_kernel(const BswDevBatch b, const BswParams p, uint32_t* __restrict__ keys,
@@ -365,11 +409,11 @@ __global__ void bsw_keys_kernel(const BswDevBatch b, const BswParams p, uint32_t
   idx[k] = (int32_t)k;
 }
 
-// bounds[c] = first sorted position whose bucket >= c, c = 0..8.
+// bounds[c] = first sorted position whose bucket >= c, c = 0..kBswWideBucket + 1.
 __global__ void bsw_bounds_kernel(const uint32_t* __restrict__ keys, long long n, int64_t* __restrict__ bounds) {
   const long long k = (long long)blockIdx.x * blockDim.x + threadIdx.x;
   if (k > n) return;
-  const int cur = (k < n) ? (int)(keys[k] >> 28) : 8;
+  const int cur = (k < n) ? (int)(keys[k] >> 28) : kBswWideBucket + 1;
   const int prev = (k > 0) ? (int)(keys[k - 1] >> 28) : -1;
   for (int c = prev + 1; c <= cur; ++c) bounds[c] = k;
 }
@@ -399,15 +443,20 @@ int launch_bsw_extend_sorted(const BswDevBatch& b, const BswParams& p, int max_q
   if (const int rc = fork_streams(s, fs); rc != FCS_OK) return rc;
   auto lanes = [&](auto sym_tag) {
     constexpr bool SYM = decltype(sym_tag)::value;
-    const int32_t* o = ws.idx_out;
-    const int64_t* bd = ws.bounds;
-    hipLaunchKernelGGL((bsw_lane_kernel<152, SYM>), dim3(g), dim3(64), 0, fs[0], b, p, o, bd, 6, res, cells);
-    hipLaunchKernelGGL((bsw_lane_kernel<128, SYM>), dim3(g), dim3(64), 0, fs[1], b, p, o, bd, 5, res, cells);
-    hipLaunchKernelGGL((bsw_lane_kernel<96, SYM>), dim3(g), dim3(64), 0, fs[2], b, p, o, bd, 4, res, cells);
-    hipLaunchKernelGGL((bsw_lane_kernel<64, SYM>), dim3(g), dim3(64), 0, fs[3], b, p, o, bd, 3, res, cells);
-    hipLaunchKernelGGL((bsw_lane_kernel<48, SYM>), dim3(g), dim3(64), 0, fs[3], b, p, o, bd, 2, res, cells);
-    hipLaunchKernelGGL((bsw_lane_kernel<32, SYM>), dim3(g), dim3(64), 0, fs[2], b, p, o, bd, 1, res, cells);
-    hipLaunchKernelGGL((bsw_lane_kernel<16, SYM>), dim3(g), dim3(64), 0, fs[1], b, p, o, bd, 0, res, cells);
+    auto go = [&](auto kern, hipStream_t st, int bucket) {
+      hipLaunchKernelGGL(kern, dim3(g), dim3(64), 0, st, b, p, ws.idx_out, ws.bounds, bucket, res, cells);
+    };
+    // widest first, so the small buckets fill the large ones' tails
+    go(bsw_lane_kernel<152, SYM, true>, fs[0], 9);
+    go(bsw_lane_kernel<128, SYM, true>, fs[1], 8);
+    go(bsw_lane_kernel<96, SYM, true>, fs[2], 7);
+    go(bsw_lane_kernel<152, SYM, false>, fs[3], 6);
+    go(bsw_lane_kernel<128, SYM, false>, fs[0], 5);
+    go(bsw_lane_kernel<96, SYM, false>, fs[1], 4);
+    go(bsw_lane_kernel<64, SYM, false>, fs[2], 3);
+    go(bsw_lane_kernel<48, SYM, false>, fs[3], 2);
+    go(bsw_lane_kernel<32, SYM, false>, fs[2], 1);
+    go(bsw_lane_kernel<16, SYM, false>, fs[1], 0);
   };
   if (sym) lanes(std::true_type{});
   else lanes(std::false_type{});

@@ -159,7 +159,7 @@ int ws_alloc(BswWorkspace& ws, int64_t cap, hipStream_t s, bool stream_alloc) {
   ws.tmp_bytes = std::max<size_t>(tmp, 16);
   void** bufs[6] = {(void**)&ws.keys_in, (void**)&ws.keys_out, (void**)&ws.idx_in, (void**)&ws.idx_out,
                     (void**)&ws.bounds, &ws.tmp};
-  const size_t sz[6] = {4 * n, 4 * n, 4 * n, 4 * n, 9 * sizeof(int64_t), ws.tmp_bytes};
+  const size_t sz[6] = {4 * n, 4 * n, 4 * n, 4 * n, (kBswWideBucket + 2) * sizeof(int64_t), ws.tmp_bytes};
   for (int i = 0; i < 6; ++i) {
     if (stream_alloc) FCS_HIP_CHECK(hipMallocAsync(bufs[i], sz[i], s));
     else FCS_HIP_CHECK(hipMalloc(bufs[i], sz[i]));

@@ -155,6 +155,8 @@ struct BswParams {
   int32_t matpack[5];  // row t: mat[t*5+q] as signed 5-bit fields at bit 5*q
   int32_t lane_ok;     // every mat entry fits a signed 5-bit field
 };
+// SW schedule buckets: 0..9 lane-per-task kernels (bsw_lane.hip), 10 = wave-per-task.
+constexpr int kBswWideBucket = 10;
 // Device scratch of one SW launch sequence (sort keys, schedule, bucket bounds).
 struct BswWorkspace {
   int64_t cap = 0;
@@ -162,7 +164,7 @@ struct BswWorkspace {
   uint32_t* keys_out = nullptr;
   int32_t* idx_in = nullptr;
   int32_t* idx_out = nullptr;
-  int64_t* bounds = nullptr;  // [9]
+  int64_t* bounds = nullptr;  // [kBswWideBucket + 2]
   void* tmp = nullptr;
   size_t tmp_bytes = 0;
 };
@@ -171,7 +173,7 @@ hipError_t hipcub_sort_pairs(void* tmp, size_t& bytes, const uint32_t* kin, uint
 // Sorted schedule: lane-per-task kernels for buckets 0..6, wave-per-task for 7.
 int launch_bsw_extend_sorted(const BswDevBatch& b, const BswParams& p, int max_qlen, int max_tlen, int32_t* res,
                              int64_t* cells, const BswWorkspace& ws, hipStream_t s);
-// Wave-per-task kernel over sorted positions [bounds[7], bounds[8]).
+// Wave-per-task kernel over sorted positions [bounds[kBswWideBucket], bounds[kBswWideBucket + 1]).
 int launch_bsw_extend_wide(const BswDevBatch& b, const BswParams& p, int max_qlen, int max_tlen, int32_t* res,
                            int64_t* cells, const int32_t* order, const int64_t* bounds, hipStream_t s);
 int launch_bsw_global(const BswDevBatch& b, const BswParams& p, int max_qlen, int max_tlen, int32_t* scores,

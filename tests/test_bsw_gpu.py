@@ -158,3 +158,18 @@ def test_golden_fixtures_gpu(gpu):
     scores, cigars = fcship.bsw_global(t, fcship.bsw_params(mat=mat))
     assert scores.tolist() == [c["score"] for c in g["global"]]
     assert [list(map(int, x)) for x in cigars] == [c["cigar"] for c in g["global"]]
+
+
+def test_extend_byte_and_word_buckets(gpu):
+    """Tasks of 65..151 query bases go to the byte-packed lane kernels when
+    every score fits a byte (h0 + qlen * max(mat) < 256) and to the 16-bit
+    ones otherwise; mixed in one batch, both must be bit-exact."""
+    rng = np.random.default_rng(17)
+    items = []
+    for k in range(400):
+        qlen = int(rng.integers(65, 152))
+        tlen = qlen + int(rng.integers(-10, 110))
+        q, t = related_pair(rng, qlen, max(tlen, 1), sub=0.02, indel=0.01)
+        h0 = int(rng.integers(1, 256 - qlen)) if k % 2 else int(rng.integers(256 - qlen, 400))
+        items.append((q, t, h0, 100 if k % 3 else int(rng.integers(5, 60))))
+    assert_extend_equal(fcship.make_tasks(items))
