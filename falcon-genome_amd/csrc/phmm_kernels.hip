@@ -64,6 +64,13 @@ __device__ __forceinline__ double sel_bits(uint32_t m, double a, double b) {
                                           ((unsigned long long)__double_as_longlong(b) & ~mm)));
 }
 
+// Last-row accumulation as a plain VALU add: left to the compiler, the two
+// running sums get packed into v_pk_add_f32 with register moves around them.
+__device__ __forceinline__ void acc_add(float& a, float x) { asm("v_add_f32 %0, %1, %2" : "=v"(a) : "v"(a), "v"(x)); }
+__device__ __forceinline__ void acc_add(double& a, double x) {
+  asm("v_add_f64 %0, %1, %2" : "=v"(a) : "v"(a), "v"(x));
+}
+
 template <typename T>
 struct RowP {
   T e1, e3, my, yy;  // own row: emission priors, deletion transitions
@@ -80,7 +87,7 @@ struct LaneState {
 };
 
 // One anti-diagonal step at t = t0 + S.
-template <typename T, bool EXACT, bool SUM, bool BC, int S>
+template <typename T, bool EXACT, bool SUM, bool BC, bool COND, int S>
 __device__ __forceinline__ void phmm_step(LaneState<T>& L, PhRing<T> (&pf)[4], int (&hq)[4],
                                           const unsigned char* __restrict__ hapl, const RowP<T>& p,
                                           PhRing<T>* __restrict__ ring, const int t0, const int sl, const bool top,
@@ -116,9 +123,16 @@ __device__ __forceinline__ void phmm_step(LaneState<T>& L, PhRing<T> (&pf)[4], i
     ring[t + 1] = o;  // column t - 15
   }
   if constexpr (SUM) {
-    if (t <= lim) {
-      accM += M;
-      accI += I;
+    // The summing lane runs the last row with my = yy = 1, so its D is the
+    // running sum of M over the columns to its left, in GKL's order; only I
+    // needs an add.  Blocks wholly inside every summing lane's columns add
+    // unconditionally (other lanes' sums are discarded); the tail block
+    // compares and takes sum M = D + M at the last column.
+    if constexpr (!COND) {
+      acc_add(accI, I);
+    } else {
+      if (t <= lim) acc_add(accI, I);
+      if (t == lim) accM = D + M;
     }
   }
   L.Xp = Xu;
@@ -128,13 +142,13 @@ __device__ __forceinline__ void phmm_step(LaneState<T>& L, PhRing<T> (&pf)[4], i
   L.Do = D;
 }
 
-template <typename T, bool EXACT, bool SUM, bool BC>
+template <typename T, bool EXACT, bool SUM, bool BC, bool COND>
 __device__ __forceinline__ void phmm_block(LaneState<T>& L, PhRing<T> (&pf)[4], int (&hq)[4],
                                            const unsigned char* __restrict__ hapl, const RowP<T>& p,
                                            PhRing<T>* __restrict__ ring, const int t0, const int sl, const bool top,
                                            const int lim, T& accM, T& accI) {
   [&]<int... S>(std::integer_sequence<int, S...>) {
-    (phmm_step<T, EXACT, SUM, BC, S>(L, pf, hq, hapl, p, ring, t0, sl, top, lim, accM, accI), ...);
+    (phmm_step<T, EXACT, SUM, BC, COND, S>(L, pf, hq, hapl, p, ring, t0, sl, top, lim, accM, accI), ...);
   }(std::make_integer_sequence<int, 16>{});
 }
 
@@ -188,8 +202,8 @@ __device__ __forceinline__ RowP<T> row_params(const PhmmTables<T>& tab, const Ra
 template <typename T, bool EXACT, bool SUM, bool BC>
 __device__ __forceinline__ void phmm_stripe(const RowP<T>& p, PhRing<T>* __restrict__ ring,
                                             const unsigned char* __restrict__ hapl, const int sl, const int nblk,
-                                            const int lim, T& accM, T& accI, const PhmmTables<T>& tab,
-                                            const RawRow& nraw, RowP<T>& np) {
+                                            const int lim, const int ulim, T& accM, T& accI,
+                                            const PhmmTables<T>& tab, const RawRow& nraw, RowP<T>& np) {
   const bool top = sl == 15;
   LaneState<T> L;
   L.Mo = L.Do = L.Xp = L.Xo = L.Io = (T)0;
@@ -200,10 +214,19 @@ __device__ __forceinline__ void phmm_stripe(const RowP<T>& p, PhRing<T>* __restr
     pf[k] = ring[16 + k];
     hq[k] = hapl[16 + k - sl];
   }
-  phmm_block<T, EXACT, SUM, BC>(L, pf, hq, hapl, p, ring, 0, sl, top, lim, accM, accI);
+  // ulim: the smallest last-column step of the summing lanes (wave-uniform);
+  // blocks that end before it need no compare
+  if (!SUM || 15 < ulim)
+    phmm_block<T, EXACT, SUM, BC, false>(L, pf, hq, hapl, p, ring, 0, sl, top, lim, accM, accI);
+  else
+    phmm_block<T, EXACT, SUM, BC, true>(L, pf, hq, hapl, p, ring, 0, sl, top, lim, accM, accI);
   np = row_params<T>(tab, nraw);
-  for (int blk = 1; blk < nblk; ++blk)
-    phmm_block<T, EXACT, SUM, BC>(L, pf, hq, hapl, p, ring, 16 * blk, sl, top, lim, accM, accI);
+  for (int blk = 1; blk < nblk; ++blk) {
+    if (!SUM || 16 * blk + 15 < ulim)
+      phmm_block<T, EXACT, SUM, BC, false>(L, pf, hq, hapl, p, ring, 16 * blk, sl, top, lim, accM, accI);
+    else
+      phmm_block<T, EXACT, SUM, BC, true>(L, pf, hq, hapl, p, ring, 16 * blk, sl, top, lim, accM, accI);
+  }
 }
 
 template <typename T, bool EXACT, bool RESCUE_PASS>
@@ -289,11 +312,15 @@ __global__ __launch_bounds__(64) void phmm_kernel(const PhmmDevBatch b, const in
         // If no live segment continues past this stripe, stop after the last summed column.
         const int cont = wave_max((active && nstr > st + 1) ? 1 : 0);
         const int lim = (seg_sums && sl == sum_lane) ? sl + H : -1;
+        const int ulim = -wave_max((seg_sums && sl == sum_lane) ? -(sl + H) : -0x7FFFFFFF);
+        accM = accI = 0;  // a sum lives within its stripe; drop what unconditional blocks added before
         const int tend = cont ? Hmax + 15 : wave_max(seg_sums ? sum_lane + H : 0);
+        RowP<T> sp = prm;  // the last row's D feeds only rows past R: reuse it as the M sum
+        if (lim >= 0) sp.my = sp.yy = (T)1;
         if (bytecmp)
-          phmm_stripe<T, EXACT, true, true>(prm, ring, hapl, sl, (tend + 16) >> 4, lim, accM, accI, tab, nraw, nprm);
+          phmm_stripe<T, EXACT, true, true>(sp, ring, hapl, sl, (tend + 16) >> 4, lim, ulim, accM, accI, tab, nraw, nprm);
         else
-          phmm_stripe<T, EXACT, true, false>(prm, ring, hapl, sl, (tend + 16) >> 4, lim, accM, accI, tab, nraw, nprm);
+          phmm_stripe<T, EXACT, true, false>(sp, ring, hapl, sl, (tend + 16) >> 4, lim, ulim, accM, accI, tab, nraw, nprm);
         if (seg_sums && sl == sum_lane) {
           const T sum = accM + accI;
           if constexpr (RESCUE_PASS) {
@@ -310,9 +337,9 @@ __global__ __launch_bounds__(64) void phmm_kernel(const PhmmDevBatch b, const in
         }
       } else {
         if (bytecmp)
-          phmm_stripe<T, EXACT, false, true>(prm, ring, hapl, sl, (Hmax + 31) >> 4, -1, accM, accI, tab, nraw, nprm);
+          phmm_stripe<T, EXACT, false, true>(prm, ring, hapl, sl, (Hmax + 31) >> 4, -1, -1, accM, accI, tab, nraw, nprm);
         else
-          phmm_stripe<T, EXACT, false, false>(prm, ring, hapl, sl, (Hmax + 31) >> 4, -1, accM, accI, tab, nraw, nprm);
+          phmm_stripe<T, EXACT, false, false>(prm, ring, hapl, sl, (Hmax + 31) >> 4, -1, -1, accM, accI, tab, nraw, nprm);
       }
       prm = nprm;
     }
