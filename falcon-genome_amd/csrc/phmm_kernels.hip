@@ -73,7 +73,7 @@ __device__ __forceinline__ void acc_add(double& a, double x) {
 
 template <typename T>
 struct RowP {
-  T e1, e3, my, yy;  // own row: emission priors, deletion transitions
+  T e1, e3, my, yy;  // own row: emission priors, deletion transitions (my * gm of the row below unless EXACT)
   T mm, gm, mx, xx;  // row below: match/gap-to-match, insertion transitions
   int rbase;  // read base byte (byte-compare groups)
   int rmask;  // bit k set: hap code k (A,C,G,T,N = 0..4) matches this row's read base
@@ -112,8 +112,8 @@ __device__ __forceinline__ void phmm_step(LaneState<T>& L, PhRing<T> (&pf)[4], i
     Xn = (M * p.mm + I * p.gm) + D * p.gm;
     In = M * p.mx + I * p.xx;
   } else {
-    D = fma_t(L.Mo, p.my, L.Do * p.yy);
-    Xn = fma_t(M, p.mm, fma_t(I, p.gm, D * p.gm));
+    D = fma_t(L.Mo, p.my, L.Do * p.yy);  // D' = gm * D (row_params)
+    Xn = fma_t(M, p.mm, fma_t(I, p.gm, D));
     In = fma_t(M, p.mx, I * p.xx);
   }
   if (top) {
@@ -174,7 +174,10 @@ __device__ __forceinline__ RawRow load_raw(const PhmmDevBatch& b, int R, int64_t
   return r;
 }
 
-template <typename T>
+// EXACT = false folds the row below's gap-to-match into the deletion
+// recurrence: the lane carries D' = gm * D (my' = my * gm), so X = M*mm +
+// I*gm + D*gm takes two FMAs instead of three.
+template <typename T, bool EXACT>
 __device__ __forceinline__ RowP<T> row_params(const PhmmTables<T>& tab, const RawRow& r) {
   RowP<T> p;
   p.e1 = p.e3 = p.my = p.yy = p.mm = p.gm = p.mx = p.xx = (T)0;
@@ -194,6 +197,7 @@ __device__ __forceinline__ RowP<T> row_params(const PhmmTables<T>& tab, const Ra
   p.gm = tab.dmatch[nc];
   p.mx = tab.ph2pr[ni];
   p.xx = tab.ph2pr[nc];
+  if constexpr (!EXACT) p.my = p.my * p.gm;
   return p;
 }
 
@@ -220,7 +224,7 @@ __device__ __forceinline__ void phmm_stripe(const RowP<T>& p, PhRing<T>* __restr
     phmm_block<T, EXACT, SUM, BC, false>(L, pf, hq, hapl, p, ring, 0, sl, top, lim, accM, accI);
   else
     phmm_block<T, EXACT, SUM, BC, true>(L, pf, hq, hapl, p, ring, 0, sl, top, lim, accM, accI);
-  np = row_params<T>(tab, nraw);
+  np = row_params<T, EXACT>(tab, nraw);
   for (int blk = 1; blk < nblk; ++blk) {
     if (!SUM || 16 * blk + 15 < ulim)
       phmm_block<T, EXACT, SUM, BC, false>(L, pf, hq, hapl, p, ring, 16 * blk, sl, top, lim, accM, accI);
@@ -309,7 +313,7 @@ __global__ __launch_bounds__(64, (sizeof(T) == 4 && !EXACT) ? 4 : 1) void phmm_k
       }
     __syncthreads();
 
-    RowP<T> prm = row_params<T>(tab, load_raw(b, active ? R : 0, ro, sl));
+    RowP<T> prm = row_params<T, EXACT>(tab, load_raw(b, active ? R : 0, ro, sl));
     T accM = 0, accI = 0;
     const int sum_stripe = active ? (R - 1) >> 4 : -1;
     const int sum_lane = active ? (R - 1) & 15 : -1;
