@@ -26,15 +26,31 @@ namespace fcs {
 
 __device__ __forceinline__ int wave_min_i(int v) { return -wave_max(-v); }
 
+#ifdef FCS_BSW_STATS
+// Diagnostic build only (tools/bsw_stats.py): per-bucket counters of waves,
+// rows, fast / masked chunks and columns, useful lane-cells, working lane-rows.
+__device__ unsigned long long g_bsw_stats[16][8];
+__shared__ unsigned long long s_bsw_stats[8];
+#define BSW_STAT(k, v) \
+  do {                  \
+    if (threadIdx.x == 0) s_bsw_stats[k] += (v); \
+  } while (0)
+#else
+#define BSW_STAT(k, v) \
+  do {                  \
+  } while (0)
+#endif
+
 // Columns per chunk: the unit of the per-row band skip and of the
 // fast (inside every lane's band) vs masked (some lane's band edge) choice.
 constexpr int kCW = 8;
 
-// registers holding the per-column query offsets (q * 5), six 5-bit fields each
-template <int NC> constexpr int QW = (NC + 5) / 6;
-
-// Signed 5-bit field at bit offset `off` of `pack` (one v_bfe_i32).
-__device__ __forceinline__ int field5(uint32_t pack, uint32_t off) { return __builtin_amdgcn_sbfe(pack, off, 5); }
+// Query profile by byte permute: the row's score table is two registers
+// (s0 bytes = mat[tb][A, C, G, T], s1 byte 0 = mat[tb][N]) and every group of
+// four columns has a selector dword in LDS (byte k = 4 + q for q in A..T, 0
+// for N), so one v_perm_b32 yields the four columns' scores as signed bytes,
+// which the h + s add reads in place (SDWA byte select).
+template <int NC> constexpr int QG = NC / 4;  // selector dwords per lane
 
 // nz | (x != 0) << sh as v_min_u32 + v_lshl_or_b32 (the compiler's own
 // cmp/cndmask/or form costs one more VALU op per cell).
@@ -67,7 +83,9 @@ struct LaneRow {
   uint32_t key;  // max over the row of (h << 16 | j): row max and its arg-max, ties to the larger j
   uint32_t kpend;  // key candidate of the even column of a pair, folded with the odd one by one v_max3
   uint32_t xst;    // byte-packed layout: the even column's new 16-bit entry, stored with the odd one
-  uint32_t pack;
+  uint32_t s0, s1;  // this row's score table (see QG)
+  uint32_t sc;      // scores of the current four columns, one signed byte each
+  uint32_t qn[kCW / 4], qx[kCW / 4];  // selectors of this chunk / the next (prefetched)
   uint32_t nz[NZW<NC>];
 };
 
@@ -102,9 +120,10 @@ __device__ __forceinline__ void eh_store(uint32_t (&eh)[(EhN<NC, B8>)], LaneRow<
 // [beg, end); high half: J in [beg, end]) selects what it may change, with
 // sign-extended 1-bit masks and bit-selects instead of branches: eh[J] only
 // for J in [beg, end] (at J == end bwa stores {h1, 0}), h1 / f / the row key
-// only for J in [beg, end).  Lanes not working this row have bm = 0.
+// only for J in [beg, end).  Lanes not working this row compute garbage they
+// never read again.
 template <int J, int NC, bool SYM, bool MASKED, bool B8>
-__device__ __forceinline__ void lane_cell(uint32_t (&eh)[(EhN<NC, B8>)], const uint32_t (&qr)[QW<NC>], LaneRow<NC>& r,
+__device__ __forceinline__ void lane_cell(uint32_t (&eh)[(EhN<NC, B8>)], const uint32_t* __restrict__ qs, LaneRow<NC>& r,
                                           const uint32_t bm, const int e_del, const int oe_del, const int e_ins,
                                           const int oe_ins) {
   constexpr int ES = B8 ? 8 : 16;  // bit offset of e inside a column entry
@@ -121,8 +140,8 @@ __device__ __forceinline__ void lane_cell(uint32_t (&eh)[(EhN<NC, B8>)], const u
     hp = (int)(x & 0xFFFFu);
     e = (int)(x >> 16);
   }
-  const uint32_t qo = __builtin_amdgcn_ubfe(qr[J / 6], 5 * (J % 6), 5);
-  const int s = field5(r.pack, qo);
+  if constexpr (J % 4 == 0) r.sc = __builtin_amdgcn_perm(r.s0, r.s1, r.qn[(J % kCW) / 4]);
+  const int s = (int)(int8_t)(uint8_t)(r.sc >> (8 * (J % 4)));
   const int M = diag_m(hp, s);
   const int h = max(max(M, e), r.f);
   int en, fn;
@@ -162,29 +181,60 @@ __device__ __forceinline__ uint32_t chunk_bits(int lo, int hi, int c0) {
   return ((1u << b) - 1u) & ~((1u << a) - 1u);
 }
 
+// Passes the chunk's inputs through an empty asm on each path.  Without it
+// the compiler hoists the two paths' common head (every column's score and
+// unpacking) above the fast/masked branch, keeping a chunk of temporaries
+// live at once: spills in the 152-column kernels.
+__device__ __forceinline__ void opaque(uint32_t& x) { asm volatile("" : "+v"(x)); }
+
+template <int C, int L, int NC, bool B8>
+__device__ __forceinline__ void opaque_chunk(uint32_t (&eh)[(EhN<NC, B8>)], LaneRow<NC>& r) {
+  constexpr int j0 = kCW * C, j1 = kCW * C + L - 1;
+  constexpr int e0 = B8 ? j0 / 2 : j0, e1 = B8 ? j1 / 2 : j1;
+  [&]<int... K>(std::integer_sequence<int, K...>) {
+    (opaque(eh[e0 + K]), ...);
+  }(std::make_integer_sequence<int, e1 - e0 + 1>{});
+  opaque(r.s0);
+  opaque(r.s1);
+}
+
 template <int C, int NC, bool SYM, bool B8>
-__device__ __forceinline__ void lane_chunk(uint32_t (&eh)[(EhN<NC, B8>)], const uint32_t (&qr)[QW<NC>], LaneRow<NC>& r,
-                                           const bool work, const int cmin, const int cmax, const int e_del,
+__device__ __forceinline__ void lane_chunk(uint32_t (&eh)[(EhN<NC, B8>)], const uint32_t* __restrict__ qs, LaneRow<NC>& r,
+                                           const int cmin, const int cmax, const int bmax,
+                                           const int emin, const int e_del,
                                            const int oe_del, const int e_ins, const int oe_ins) {
   constexpr int L = (NC - kCW * C) < kCW ? (NC - kCW * C) : kCW;  // last chunk may be partial
   static_assert(L % 2 == 0, "fold_key pairs columns within a chunk");
   if (kCW * C <= cmax && kCW * C + L - 1 >= cmin) {
+    // selectors of the next chunk: in flight while this one computes
+    if constexpr (kCW * (C + 1) < NC) {
+#pragma unroll
+      for (int k = 0; k < kCW / 4; ++k) r.qx[k] = qs[64 * ((kCW / 4) * (C + 1) + k)];
+    }
     // Fast path when the whole chunk lies strictly inside the band of every
-    // live lane (no per-column band test, no eh[end] write in this chunk).
-    const bool inside = !work || (r.beg <= kCW * C && kCW * C + L - 1 < r.end);
-    if (__ballot(!inside) == 0ull) {
-      if (work) {
-        [&]<int... S>(std::integer_sequence<int, S...>) {
-          (lane_cell<kCW * C + S, NC, SYM, false, B8>(eh, qr, r, 0u, e_del, oe_del, e_ins, oe_ins), ...);
-        }(std::make_integer_sequence<int, L>{});
-      }
-    } else {
-      const uint32_t bm =
-          work ? (chunk_bits(r.beg, r.end, kCW * C) | (chunk_bits(r.beg, r.end + 1, kCW * C) << kCW)) : 0u;
+    // live lane (no per-column band test, no eh[end] write in this chunk):
+    // a scalar test against the wave's largest beg and smallest end.
+    if (bmax <= kCW * C && kCW * C + L - 1 < emin) {
+      // Lanes not working this row run the body too: a lane that is done
+      // never reads its state again, and an empty row ends its task (its
+      // row-start h1 is kept aside).  No EXEC branch, so no join copies.
+      BSW_STAT(2, 1);
+      BSW_STAT(4, L);
+      opaque_chunk<C, L, NC, B8>(eh, r);
       [&]<int... S>(std::integer_sequence<int, S...>) {
-        (lane_cell<kCW * C + S, NC, SYM, true, B8>(eh, qr, r, bm, e_del, oe_del, e_ins, oe_ins), ...);
+        (lane_cell<kCW * C + S, NC, SYM, false, B8>(eh, qs, r, 0u, e_del, oe_del, e_ins, oe_ins), ...);
+      }(std::make_integer_sequence<int, L>{});
+    } else {
+      BSW_STAT(3, 1);
+      BSW_STAT(5, L);
+      opaque_chunk<C, L, NC, B8>(eh, r);
+      const uint32_t bm = chunk_bits(r.beg, r.end, kCW * C) | (chunk_bits(r.beg, r.end + 1, kCW * C) << kCW);
+      [&]<int... S>(std::integer_sequence<int, S...>) {
+        (lane_cell<kCW * C + S, NC, SYM, true, B8>(eh, qs, r, bm, e_del, oe_del, e_ins, oe_ins), ...);
       }(std::make_integer_sequence<int, L>{});
     }
+#pragma unroll
+    for (int k = 0; k < kCW / 4; ++k) r.qn[k] = r.qx[k];
   }
 }
 
@@ -192,7 +242,8 @@ __device__ __forceinline__ void lane_chunk(uint32_t (&eh)[(EhN<NC, B8>)], const 
 template <int NC, bool SYM, bool B8>
 __device__ __forceinline__ void lane_wave(const BswDevBatch& b, const BswParams& p, const int32_t* __restrict__ order,
                                           const long long base, const long long hi, int32_t* __restrict__ res,
-                                          int64_t* __restrict__ cells_out) {
+                                          int64_t* __restrict__ cells_out, uint32_t* __restrict__ qsel,
+                                          const uint32_t* __restrict__ mtab) {
   const int lane = threadIdx.x;
   const long long k = base + lane;
   const bool has = k < hi;
@@ -210,17 +261,18 @@ __device__ __forceinline__ void lane_wave(const BswDevBatch& b, const BswParams&
   }
   const int e_del = p.e_del, e_ins = p.e_ins, oe_del = p.o_del + p.e_del, oe_ins = p.o_ins + p.e_ins;
 
-  uint32_t qr[QW<NC>];
+  // this lane's query selectors (columns past qlen score as N)
+  uint32_t* __restrict__ qs = qsel + lane;
 #pragma unroll
-  for (int c = 0; c < QW<NC>; ++c) {
+  for (int g = 0; g < QG<NC>; ++g) {
     uint32_t v = 0;
 #pragma unroll
-    for (int z = 0; z < 6; ++z) {
-      const int j = 6 * c + z;
+    for (int z = 0; z < 4; ++z) {
+      const int j = 4 * g + z;
       const uint32_t qb = (j < qlen) ? (uint32_t)q[j] : 4u;
-      if (j < NC) v |= (qb * 5u) << (5 * z);
+      v |= (qb < 4u ? 4u + qb : 0u) << (8 * z);
     }
-    qr[c] = v;
+    qs[64 * g] = v;
   }
   uint32_t eh[(EhN<NC, B8>)];
   const int h1v = h0 > oe_ins ? h0 - oe_ins : 0;
@@ -270,43 +322,39 @@ __device__ __forceinline__ void lane_wave(const BswDevBatch& b, const BswParams&
         if (r.h1 < 0) r.h1 = 0;
       }
     }
-    if constexpr (NC >= 96) {
-      // keep the per-column query offsets packed (re-extracted per cell)
-      // instead of letting the compiler hoist NC unpacked copies out of the
-      // row loop: that doubles the register file and halves occupancy
-#pragma unroll
-      for (int c = 0; c < QW<NC>; ++c) asm volatile("" : "+v"(qr[c]));
-    }
     const bool empty = alive && r.beg >= r.end;
     const bool work = alive && !empty;
+    const int h1_row = r.h1;
+    BSW_STAT(1, 1);
+    BSW_STAT(7, __popcll(__ballot(work)));
     const int cmin = wave_min_i(work ? r.beg : (1 << 20));
     const int cmax = wave_max(work ? r.end : -1);
-    r.pack = tb == 0 ? (uint32_t)p.matpack[0]
-           : tb == 1 ? (uint32_t)p.matpack[1]
-           : tb == 2 ? (uint32_t)p.matpack[2]
-           : tb == 3 ? (uint32_t)p.matpack[3] : (uint32_t)p.matpack[4];
+    const int bmax = wave_max(work ? r.beg : -1);
+    const int emin = wave_min_i(work ? r.end : (1 << 20));
+    {
+      const uint2 t2 = reinterpret_cast<const uint2*>(mtab)[min((unsigned)tb, 4u)];
+      r.s0 = t2.x;
+      r.s1 = t2.y;
+    }
+    {
+      // selectors of the row's first chunk (the wave's leftmost band column)
+      const int c0 = min(max(cmin, 0), NC - 1) / kCW;
+#pragma unroll
+      for (int k = 0; k < kCW / 4; ++k) r.qn[k] = qs[64 * ((kCW / 4) * c0 + k)];
+    }
     r.f = 0;
     r.key = 0;
 #pragma unroll
     for (int k = 0; k < NZW<NC>; ++k) r.nz[k] = 0;
     [&]<int... C>(std::integer_sequence<int, C...>) {
-      (lane_chunk<C, NC, SYM, B8>(eh, qr, r, work, cmin, cmax, e_del, oe_del, e_ins, oe_ins), ...);
+      (lane_chunk<C, NC, SYM, B8>(eh, qs, r, cmin, cmax, bmax, emin, e_del, oe_del, e_ins, oe_ins), ...);
     }(std::make_integer_sequence<int, (NC + kCW - 1) / kCW>{});
     if (empty) {
-      // bwa still stores eh[end] = {h1, 0}; the loop index equals beg here
-#pragma unroll
-      for (int j = 0; j < NC; ++j)
-        if (j == r.end) {
-          if constexpr (B8) {
-            const uint32_t m16 = (j % 2) ? 0xFFFF0000u : 0xFFFFu;
-            eh[j / 2] = (eh[j / 2] & ~m16) | (((uint32_t)r.h1 << (16 * (j % 2))) & m16);
-          } else {
-            eh[j] = (uint32_t)r.h1;
-          }
-        }
+      // bwa stores eh[end] = {h1, 0} and stops (beg >= end ends the row loop
+      // for good), so only the to-end score of this row matters
       if (r.beg == qlen) {
-        max_ie = gscore > r.h1 ? max_ie : i;
-        gscore = gscore > r.h1 ? gscore : r.h1;
+        max_ie = gscore > h1_row ? max_ie : i;
+        gscore = gscore > h1_row ? gscore : h1_row;
       }
       done = true;
     }
@@ -348,6 +396,14 @@ __device__ __forceinline__ void lane_wave(const BswDevBatch& b, const BswParams&
       }
     }
   }
+#ifdef FCS_BSW_STATS
+  {
+    int tot = ncell;
+    for (int o = 32; o > 0; o >>= 1) tot += __shfl_xor(tot, o);
+    BSW_STAT(6, tot);
+    BSW_STAT(0, 1);
+  }
+#endif
   if (has) {
     int32_t* o = res + 6 * task;
     o[0] = mx;
@@ -368,9 +424,38 @@ __global__ __launch_bounds__(64, B8 ? 3 : 2) void bsw_lane_kernel(const BswDevBa
                                                       const int64_t* __restrict__ bounds, const int bucket,
                                                       int32_t* __restrict__ res, int64_t* __restrict__ cells_out) {
   const long long lo = bounds[bucket], hi = bounds[bucket + 1];
+  __shared__ uint32_t qsel[QG<NC> * 64];  // [group][lane] query selectors
+  __shared__ uint2 mtab[5];               // score table of target base t (s0, s1)
+  if (threadIdx.x < 5) {
+    const int t = threadIdx.x;
+    uint32_t s0 = 0;
+    for (int c = 0; c < 4; ++c) s0 |= (uint32_t)(uint8_t)p.mat[t * 5 + c] << (8 * c);
+    mtab[t] = make_uint2(s0, (uint32_t)(uint8_t)p.mat[t * 5 + 4]);
+  }
+  __syncthreads();
+#ifdef FCS_BSW_STATS
+  if (threadIdx.x < 8) s_bsw_stats[threadIdx.x] = 0;
+  __syncthreads();
+#endif
   for (long long base = lo + 64LL * blockIdx.x; base < hi; base += 64LL * gridDim.x)
-    lane_wave<NC, SYM, B8>(b, p, order, base, hi, res, cells_out);
+    lane_wave<NC, SYM, B8>(b, p, order, base, hi, res, cells_out, qsel, reinterpret_cast<const uint32_t*>(mtab));
+#ifdef FCS_BSW_STATS
+  __syncthreads();
+  if (threadIdx.x < 8) atomicAdd(&g_bsw_stats[bucket][threadIdx.x], s_bsw_stats[threadIdx.x]);
+#endif
 }
+
+#ifdef FCS_BSW_STATS
+extern "C" int fcs_bsw_stats_read(unsigned long long* out, int reset) {
+  if (hipDeviceSynchronize() != hipSuccess) return -1;
+  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_bsw_stats), sizeof(g_bsw_stats)) != hipSuccess) return -1;
+  if (reset) {
+    static const unsigned long long z[16][8] = {};
+    if (hipMemcpyToSymbol(HIP_SYMBOL(g_bsw_stats), z, sizeof(z)) != hipSuccess) return -1;
+  }
+  return 0;
+}
+#endif
 
 // Bucket of a task: 0..6 = 16-bit lane kernels with 16/32/48/64/96/128/152
 // register columns (152 = bwa reads up to 151 bp); 7..9 = byte-packed lane
