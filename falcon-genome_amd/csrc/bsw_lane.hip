@@ -462,12 +462,16 @@ extern "C" int fcs_bsw_stats_read(unsigned long long* out, int reset) {
 // kernels with 96/128/152 columns for tasks whose scores all fit a byte (the
 // register saving buys a third wave per SIMD there; at <= 64 columns the
 // 16-bit layout already runs 3-4 waves and is cheaper per cell);
-// kBswWideBucket = wave-per-task kernel (long queries, scores beyond int16,
-// matrices beyond 5 bits).
-__device__ __forceinline__ int bsw_bucket(int qlen, int h0, const BswParams& p) {
+// kBswPairBucket0..+4 = two-tasks-per-lane kernels (bsw_pair.hip) with
+// 32/64/96/128/152 columns for tasks whose biased scores fit a byte and whose
+// query and target hold no N (`acgt`); kBswWideBucket = wave-per-task kernel
+// (long queries, scores beyond int16, matrices beyond 5 bits).
+__device__ __forceinline__ int bsw_bucket(int qlen, int h0, bool acgt, const BswParams& p) {
   const long long bound = (long long)h0 + (long long)qlen * p.max_mat;  // no cell can score more
-  if (!p.lane_ok || h0 <= 0 || bound >= 32000) return kBswWideBucket;
   const int need = qlen + 1;
+  if (p.pair_ok && acgt && h0 > 0 && need <= 152 && bound + p.pair_cg - 1 <= 255)
+    return kBswPairBucket0 + (need <= 32 ? 0 : need <= 64 ? 1 : need <= 96 ? 2 : need <= 128 ? 3 : 4);
+  if (!p.lane_ok || h0 <= 0 || bound >= 32000) return kBswWideBucket;
   if (need <= 16) return 0;
   if (need <= 32) return 1;
   if (need <= 48) return 2;
@@ -477,12 +481,37 @@ __device__ __forceinline__ int bsw_bucket(int qlen, int h0, const BswParams& p) 
   return bound < 256 ? c + 3 : c;
 }
 
+// No base outside A/C/G/T (code >= 4) among the n query bytes at s: aligned
+// 16-byte loads (the caller's buffers come from hipMalloc, so an aligned block
+// holding one of the task's bytes lies inside the allocation), edge bytes masked.
+__device__ __forceinline__ bool bsw_query_acgt(const uint8_t* s, int n) {
+  if (n <= 0) return true;
+  const uintptr_t b = (uintptr_t)s, e = b + (uintptr_t)n, a0 = b & ~(uintptr_t)15;
+  uint32_t any = 0;
+  for (uintptr_t blk = a0; blk < e; blk += 16) {
+    const uint4 v = *reinterpret_cast<const uint4*>(blk);
+    const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const uintptr_t d = blk + 4 * q;
+      uint32_t keep = 0xFFFFFFFFu;
+      if (d < b) keep = b - d >= 4 ? 0u : ~0u << (8 * (b - d));
+      if (d + 4 > e) keep &= d >= e ? 0u : ~0u >> (8 * (d + 4 - e));
+      any |= w[q] & keep;
+    }
+  }
+  return (any & 0xFCFCFCFCu) == 0;
+}
+
 __global__ void bsw_keys_kernel(const BswDevBatch b, const BswParams p, uint32_t* __restrict__ keys,
                                 int32_t* __restrict__ idx) {
   const long long k = (long long)blockIdx.x * blockDim.x + threadIdx.x;
   if (k >= b.n) return;
   const int qlen = b.qlen[k], tlen = b.tlen[k], h0 = b.h0[k];
-  const uint32_t bk = (uint32_t)bsw_bucket(qlen, h0, p);
+  // the pair kernels score target N rows from their table but take queries
+  // without N only (a query N would need a fifth score per column)
+  const bool acgt = p.pair_ok && qlen < 152 && bsw_query_acgt(b.qbuf + b.qoff[k], qlen);
+  const uint32_t bk = (uint32_t)bsw_bucket(qlen, h0, acgt, p);
   // Rows a task is expected to run: an extension that keeps matching peaks
   // near row qlen with score ~h0 + qlen*max_mat and then decays by e_del per
   // row until the row max hits 0 (bwa's m == 0 exit), capped by tlen.  Tasks
@@ -490,7 +519,10 @@ __global__ void bsw_keys_kernel(const BswDevBatch b, const BswParams p, uint32_t
   // idle behind the wave's longest task.
   const long long est = min((long long)tlen, (long long)qlen +
                                                  ((long long)h0 + (long long)qlen * p.max_mat) / max(p.e_del, 1) + 1);
-  keys[k] = (bk << 28) | ((uint32_t)min(max(qlen, 0), 1023) << 18) | (uint32_t)min(max(est, 0LL), 262143LL);
+  // longest first inside a bucket (the sort is ascending): the last waves of a
+  // launch are the short ones, so the launch's tail is short
+  keys[k] = (bk << 28) | ((1023u - (uint32_t)min(max(qlen, 0), 1023)) << 18) |
+            (262143u - (uint32_t)min(max(est, 0LL), 262143LL));
   idx[k] = (int32_t)k;
 }
 
@@ -508,8 +540,7 @@ int launch_bsw_extend_sorted(const BswDevBatch& b, const BswParams& p, int max_q
   if (b.n <= 0) return FCS_OK;
   if (b.n > ws.cap) return fail(FCS_ERR_INVALID, "[E::fcship] SW batch larger than its plan");
   const int bs = 256;
-  const unsigned nb = (unsigned)((b.n + bs - 1) / bs);
-  hipLaunchKernelGGL(bsw_keys_kernel, dim3(nb), dim3(bs), 0, s, b, p, ws.keys_in, ws.idx_in);
+  hipLaunchKernelGGL(bsw_keys_kernel, dim3((unsigned)((b.n + bs - 1) / bs)), dim3(bs), 0, s, b, p, ws.keys_in, ws.idx_in);
   FCS_HIP_CHECK(hipGetLastError());
   size_t tmp = ws.tmp_bytes;
   FCS_HIP_CHECK(hipcub_sort_pairs(ws.tmp, tmp, ws.keys_in, ws.keys_out, ws.idx_in, ws.idx_out, (int)b.n, s));
@@ -543,10 +574,15 @@ int launch_bsw_extend_sorted(const BswDevBatch& b, const BswParams& p, int max_q
     go(bsw_lane_kernel<32, SYM, false>, fs[2], 1);
     go(bsw_lane_kernel<16, SYM, false>, fs[1], 0);
   };
+  // two-tasks-per-lane kernels first: they carry the bwa-typical tasks
+  if (const int rc = launch_bsw_pair(b, p, res, cells, ws.idx_out, ws.bounds,
+                                     (unsigned)std::min<long long>((b.n + 127) / 128, 8192), fs);
+      rc != FCS_OK)
+    return rc;
   if (sym) lanes(std::true_type{});
   else lanes(std::false_type{});
   FCS_HIP_CHECK(hipGetLastError());
-  // bucket 7: wave-per-task kernel over the sorted tail
+  // wave-per-task kernel over the sorted tail
   const int rc = launch_bsw_extend_wide(b, p, max_qlen, max_tlen, res, cells, ws.idx_out, ws.bounds, fs[0]);
   if (rc != FCS_OK) return rc;
   return join_streams(s, fs);

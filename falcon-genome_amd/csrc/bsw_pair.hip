@@ -1,0 +1,488 @@
+// ksw_extend2 with TWO tasks per lane in packed 16-bit arithmetic (gfx950
+// VOP3P), for the bwa-typical envelope: qlen <= 151, every score of the task
+// below 256 after the score bias, no N in the query, h0 > 0.
+//
+// Algorithm: bwa ksw.c ksw_extend2, reached from
+// /root/reference/src/workers/BWAWorker.cpp:134-166.  Same row loop, band
+// bookkeeping, z-drop and trims as the one-task lane kernel (bsw_lane.hip);
+// what changes is the data layout of a cell, so that every VALU op of the
+// cell body works on two tasks at once (task A = low 16 bits, B = high).
+//
+// Layout:
+//  * bwa's eh[j] of both tasks in ONE register: bytes [eA, hA, eB, hB].
+//  * Values are carried in the "x256" domain: a 16-bit half holds v << 8.
+//    Unpacking is one AND (h) and one packed shift (e); repacking the new
+//    entry {h1, e'} of both tasks is one v_perm_b32.
+//  * Scores: one v_perm_b32 per two columns turns the per-lane selector
+//    dword [qA_j, qA_j+1, 4+qB_j, 4+qB_j+1] and the row's two 4-byte score
+//    tables (mat[t][0..3] + bias, t = this row's target base of A / B, N
+//    included) into
+//    the four biased scores; v_pk_mad_u16 (x256, which also drops the other
+//    column's byte) or AND+add puts them in the x256 domain on top of h.
+//  * bwa's `M = M ? M + q : 0` is min(h + s', gate) - bias with
+//    gate = sat(C * h) (0 iff h == 0, above any h + s' otherwise), all
+//    saturating packed ops; every later max / saturating subtract is exactly
+//    bwa's max(., 0) arithmetic.
+//  * Row max and arg-max: packed max of (h << 8 | j); ties go to the larger j
+//    as in bwa.  Trims: a 16-column bitmap per task half (v_pk_min + lshl_or).
+//
+// Band edges without per-cell predicates:
+//  * left: every eh[] entry left of a task's `beg` is kept at zero (bwa's
+//    trims only skip zero entries; the one entry a band cut (i - w) leaves
+//    behind per row is zeroed in the row it leaves the band).  Zero inputs
+//    make zero outputs, so the chain (h1, f) enters `beg` as zero exactly as
+//    bwa restarts it; only chunks holding a cut column mask their inputs.
+//  * right: chunks reaching some task's `end` run with per-half masks: no
+//    e' at j == end (bwa stores {h1, 0}), entries beyond `end` keep their
+//    stale values (bwa re-reads them when the band grows), and h1 at `end` is
+//    captured for the to-end score.
+#include <hip/hip_runtime.h>
+
+#include <utility>
+
+#include "fcship_internal.h"
+
+namespace fcs {
+
+#ifdef FCS_BSW_STATS
+// Diagnostic build only (tools/bsw_stats.py): per pair bucket, counters of
+// waves, rows, fast / masked chunks, useful cells, working and alive task-rows,
+// and the row band union width.
+__device__ unsigned long long g_pair_stats[5][8];
+__shared__ unsigned long long s_pair_stats[8];
+#define PAIR_STAT(k, v) \
+  do {                  \
+    if (threadIdx.x == 0) s_pair_stats[k] += (v); \
+  } while (0)
+extern "C" int fcs_bsw_pair_stats_read(unsigned long long* out, int reset) {
+  if (hipDeviceSynchronize() != hipSuccess) return -1;
+  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_pair_stats), sizeof(g_pair_stats)) != hipSuccess) return -1;
+  if (reset) {
+    static const unsigned long long z[5][8] = {};
+    if (hipMemcpyToSymbol(HIP_SYMBOL(g_pair_stats), z, sizeof(z)) != hipSuccess) return -1;
+  }
+  return 0;
+}
+#else
+#define PAIR_STAT(k, v) \
+  do {                  \
+  } while (0)
+#endif
+
+namespace {
+
+// ---------------------------------------------------------------- packed ops
+// Clang vector builtins (not inline asm) wherever a pattern exists, so the
+// hazard recognizer sees real instructions and inserts no defensive s_nop.
+typedef uint16_t u16x2 __attribute__((ext_vector_type(2)));
+typedef int16_t i16x2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ u16x2 V(uint32_t x) { return __builtin_bit_cast(u16x2, x); }
+__device__ __forceinline__ uint32_t U(u16x2 x) { return __builtin_bit_cast(uint32_t, x); }
+
+__device__ __forceinline__ uint32_t pk_max(uint32_t a, uint32_t b) { return U(__builtin_elementwise_max(V(a), V(b))); }
+__device__ __forceinline__ uint32_t pk_min(uint32_t a, uint32_t b) { return U(__builtin_elementwise_min(V(a), V(b))); }
+// max(a - s, 0) per half (v_pk_sub_u16 clamp)
+__device__ __forceinline__ uint32_t pk_subs(uint32_t a, uint32_t s) {
+  return U(__builtin_elementwise_sub_sat(V(a), V(s)));
+}
+__device__ __forceinline__ uint32_t pk_add(uint32_t a, uint32_t b) { return U(V(a) + V(b)); }
+// a * s + c per half (mod 2^16): v_pk_mad_u16 (s must not be a compile-time
+// power of two, or the compiler splits it into a shift and an add)
+__device__ __forceinline__ uint32_t pk_mad(uint32_t a, uint32_t s, uint32_t c) { return U(V(a) * V(s) + V(c)); }
+// min(a * s, 65535) per half: no builtin for a saturating multiply-add
+__device__ __forceinline__ uint32_t pk_gate(uint32_t a, uint32_t s) {
+  uint32_t r;
+  asm("v_pk_mad_u16 %0, %1, %2, 0 op_sel_hi:[1,1,0] clamp" : "=v"(r) : "v"(a), "s"(s));
+  return r;
+}
+__device__ __forceinline__ uint32_t pk_shl8(uint32_t a) { return U(V(a) << (u16x2)(8)); }
+// (a != 0) per half as 0 / 1, with `one` a runtime 0x00010001 (a literal 1
+// turns min(a, 1) into compare + select)
+__device__ __forceinline__ uint32_t pk_nz(uint32_t a, uint32_t one) { return pk_min(a, one); }
+// all-ones per half where (signed) a < b
+__device__ __forceinline__ uint32_t pk_lt(uint32_t a, uint32_t b) {
+  const i16x2 d = __builtin_bit_cast(i16x2, a) - __builtin_bit_cast(i16x2, b);
+  return __builtin_bit_cast(uint32_t, d >> (i16x2)(15));
+}
+__device__ __forceinline__ uint32_t pbfi(uint32_t m, uint32_t a, uint32_t b) { return (m & a) | (~m & b); }
+__device__ __forceinline__ void opq(uint32_t& x) { asm volatile("" : "+v"(x)); }
+
+__device__ __forceinline__ uint32_t pack2(int a, int b) { return ((uint32_t)a & 0xFFFFu) | ((uint32_t)b << 16); }
+
+// ---------------------------------------------------------------- layout
+constexpr int kPW = 8;  // columns per chunk (skip / fast / masked unit)
+template <int NC> constexpr int PCH = (NC + kPW - 1) / kPW;  // chunks
+template <int NC> constexpr int PNZ = (NC + 15) / 16;        // bitmap words
+
+// Wave-uniform constants of the cell body (x256 domain, both halves).
+struct PairK {
+  uint32_t k256;       // 0x0100 | 0x0100 << 16
+  uint32_t one;        // 0x0001 | 0x0001 << 16
+  uint32_t cg;         // gate multiplier C = max biased score + 1
+  uint32_t bias;       // score bias << 8
+  uint32_t oed, ed, oei, ei;  // (o + e) << 8 and e << 8 of deletions / insertions
+};
+
+template <int NC>
+struct PairRow {
+  uint32_t F, H1, KEY, CAP;
+  uint32_t tabA, tabB;       // biased score tables of this row's target bases
+  uint32_t BEGM1, END, ENDX;  // per half: beg - 1, end, end + 1
+  uint32_t O;                // scores of the current column pair
+  uint4 sel, seln;           // selector dwords of this chunk / the next
+  uint32_t nz[PNZ<NC>];
+};
+
+// bwa's inner-loop body for column J of both tasks.  MODE bit 0: mask the
+// inputs left of beg (a band-cut column is in this chunk); bit 1: right-edge
+// masks (some task's end is in or left of this chunk).
+template <int J, int NC, bool SYM, int MODE>
+__device__ __forceinline__ void pair_cell(uint32_t (&eh)[NC], PairRow<NC>& r, const PairK& k) {
+  constexpr uint32_t JJ = (uint32_t)J | ((uint32_t)J << 16);
+  const uint32_t w0 = eh[J];
+  uint32_t w = w0;
+  if constexpr (MODE & 1) w &= pk_lt(r.BEGM1, JJ);  // J >= beg
+  const uint32_t HP = w & 0xFF00FF00u;
+  const uint32_t E = pk_shl8(w);
+  uint32_t t;
+  if constexpr (J % 2 == 0) {
+    constexpr int g = (J % kPW) / 2;
+    const uint32_t sl = g == 0 ? r.sel.x : g == 1 ? r.sel.y : g == 2 ? r.sel.z : r.sel.w;
+    r.O = __builtin_amdgcn_perm(r.tabB, r.tabA, sl);
+    t = pk_mad(r.O, k.k256, HP);
+  } else {
+    t = pk_add(r.O & 0xFF00FF00u, HP);
+  }
+  const uint32_t M = pk_subs(pk_min(t, pk_gate(HP, k.cg)), k.bias);
+  const uint32_t H = pk_max(pk_max(M, E), r.F);
+  const uint32_t MOd = pk_subs(M, k.oed);
+  uint32_t EN = pk_max(pk_subs(E, k.ed), MOd);
+  const uint32_t MOi = SYM ? MOd : pk_subs(M, k.oei);
+  const uint32_t Fn = pk_max(pk_subs(r.F, k.ei), MOi);
+  uint32_t Hk = H, wst;
+  if constexpr (MODE & 2) {
+    const uint32_t mE = pk_lt(JJ, r.END);   // J < end
+    const uint32_t mX = pk_lt(JJ, r.ENDX);  // J <= end
+    EN &= mE;
+    Hk &= mE;
+    r.CAP = pbfi(mX ^ mE, r.H1, r.CAP);  // J == end: bwa's eh[end].h = h1
+    wst = pbfi(mX, __builtin_amdgcn_perm(r.H1, EN, 0x07030501u), w0);
+  } else {
+    wst = __builtin_amdgcn_perm(r.H1, EN, 0x07030501u);
+  }
+  eh[J] = wst;
+  r.KEY = pk_max(r.KEY, Hk | JJ);
+  r.nz[J / 16] |= pk_nz(wst, k.one) << (J % 16);
+  r.H1 = H;
+  r.F = Fn;
+}
+
+template <int C, int NC>
+__device__ __forceinline__ void pair_opaque(uint32_t (&eh)[NC], PairRow<NC>& r) {
+  constexpr int j0 = kPW * C, L = (NC - j0) < kPW ? (NC - j0) : kPW;
+  [&]<int... K>(std::integer_sequence<int, K...>) __attribute__((always_inline)) {
+    (opq(eh[j0 + K]), ...);
+  }(std::make_integer_sequence<int, L>{});
+  opq(r.tabA);
+  opq(r.tabB);
+}
+
+template <int C, int NC, bool SYM>
+__device__ __forceinline__ void pair_chunk(uint32_t (&eh)[NC], const uint4* __restrict__ qs, PairRow<NC>& r,
+                                           const PairK& k, const int cmin, const int cmax, const int emin,
+                                           const int cut_lo, const int cut_hi) {
+  constexpr int j0 = kPW * C, L = (NC - j0) < kPW ? (NC - j0) : kPW;
+  static_assert(L % 2 == 0, "column pairs share one score perm");
+  if (j0 > cmax || j0 + L - 1 < cmin) return;
+  if constexpr (C + 1 < PCH<NC>) r.seln = qs[64 * (C + 1)];
+  const bool right = j0 + L - 1 >= emin;
+  const bool left = j0 <= cut_hi && j0 + L - 1 >= cut_lo;
+  pair_opaque<C, NC>(eh, r);
+  // two bodies only (fast, fully masked): every extra variant of the unrolled
+  // chunk costs instruction-cache footprint shared by the concurrent buckets
+  if (!right && !left) {
+    PAIR_STAT(2, 1);
+    [&]<int... S>(std::integer_sequence<int, S...>) __attribute__((always_inline)) {
+      (pair_cell<j0 + S, NC, SYM, 0>(eh, r, k), ...);
+    }(std::make_integer_sequence<int, L>{});
+  } else {
+    PAIR_STAT(3, 1);
+    [&]<int... S>(std::integer_sequence<int, S...>) __attribute__((always_inline)) {
+      (pair_cell<j0 + S, NC, SYM, 3>(eh, r, k), ...);
+    }(std::make_integer_sequence<int, L>{});
+  }
+  r.sel = r.seln;
+}
+
+// bwa's per-task scalar state.
+struct PairTask {
+  long long id;
+  const uint8_t* tg;
+  int qlen, tlen, h0, w;
+  int beg, end;
+  int mx, max_i, max_j, max_ie, gscore, max_off, ncell;
+  int tcur, tnext;
+  bool done;
+};
+
+__device__ __forceinline__ void task_load(PairTask& T, const BswDevBatch& b, const BswParams& p, const int32_t* order,
+                                          long long k, long long hi) {
+  T.done = k >= hi;
+  T.id = T.done ? -1 : order[k];
+  T.qlen = T.tlen = T.w = 0;
+  T.h0 = 1;
+  T.tg = b.tbuf;
+  if (!T.done) {
+    T.qlen = b.qlen[T.id];
+    T.tlen = b.tlen[T.id];
+    T.h0 = b.h0[T.id];
+    T.w = b.w[T.id];
+    T.tg = b.tbuf + b.toff[T.id];
+  }
+  int max_ins = (int)((double)(T.qlen * p.max_mat + p.end_bonus - p.o_ins) / p.e_ins + 1.);
+  max_ins = max_ins > 1 ? max_ins : 1;
+  T.w = T.w < max_ins ? T.w : max_ins;
+  int max_del = (int)((double)(T.qlen * p.max_mat + p.end_bonus - p.o_del) / p.e_del + 1.);
+  max_del = max_del > 1 ? max_del : 1;
+  T.w = T.w < max_del ? T.w : max_del;
+  T.beg = 0;
+  T.end = T.qlen;
+  T.mx = T.h0;
+  T.max_i = T.max_j = T.max_ie = -1;
+  T.gscore = -1;
+  T.max_off = 0;
+  T.ncell = 0;
+  T.tcur = (T.tlen > 0) ? T.tg[0] : 0;
+  T.tnext = (T.tlen > 1) ? T.tg[1] : 0;
+}
+
+// Row start: bwa's band update and h1.  Returns h1 (0 for a task not working).
+__device__ __forceinline__ int task_row_begin(PairTask& T, const BswParams& p, int i, bool alive, bool& work,
+                                              bool& empty) {
+  int h1 = 0;
+  if (alive) {
+    if (T.beg < i - T.w) T.beg = i - T.w;
+    if (T.end > i + T.w + 1) T.end = i + T.w + 1;
+    if (T.end > T.qlen) T.end = T.qlen;
+    if (T.beg == 0) {
+      h1 = T.h0 - (p.o_del + p.e_del * (i + 1));
+      if (h1 < 0) h1 = 0;
+    }
+  }
+  empty = alive && T.beg >= T.end;
+  work = alive && !empty;
+  return h1;
+}
+
+// Row end: bwa's to-end score, row max / z-drop, and trims from the bitmap
+// half `hs` (0 or 16) of the nz words.
+template <int NC>
+__device__ __forceinline__ void task_row_end(PairTask& T, const BswParams& p, int i, bool work, bool empty, int h1_row,
+                                             uint32_t key, int cap, const uint32_t (&nz)[PNZ<NC>], int hs,
+                                             int wlo, int whi) {
+  if (empty) {
+    if (T.beg == T.qlen) {
+      T.max_ie = T.gscore > h1_row ? T.max_ie : i;
+      T.gscore = T.gscore > h1_row ? T.gscore : h1_row;
+    }
+    T.done = true;
+  }
+  if (!work) return;
+  T.ncell += T.end - T.beg;
+  if (T.end == T.qlen) {
+    T.max_ie = T.gscore > cap ? T.max_ie : i;
+    T.gscore = T.gscore > cap ? T.gscore : cap;
+  }
+  const int m = (int)(key >> 8), mj = (int)(key & 0xFFu);
+  if (m == 0) {
+    T.done = true;
+  } else if (m > T.mx) {
+    T.mx = m, T.max_i = i, T.max_j = mj;
+    const int d = mj > i ? mj - i : i - mj;
+    T.max_off = T.max_off > d ? T.max_off : d;
+  } else if (p.zdrop > 0) {
+    if (i - T.max_i > mj - T.max_j) {
+      if (T.mx - m - ((i - T.max_i) - (mj - T.max_j)) * p.e_del > p.zdrop) T.done = true;
+    } else {
+      if (T.mx - m - ((mj - T.max_j) - (i - T.max_i)) * p.e_ins > p.zdrop) T.done = true;
+    }
+  }
+  if (T.done) return;
+  // bwa's trims over the entries written this row, [beg, end]
+  int first = -1, last = -1;
+#pragma unroll
+  for (int k = 0; k < PNZ<NC>; ++k) {
+    if (16 * k + 15 < wlo || 16 * k > whi) continue;  // wave-uniform: outside every band
+    const int a = min(max(T.beg - 16 * k, 0), 16), z = min(max(T.end + 1 - 16 * k, 0), 16);
+    const uint32_t keep = ((1u << z) - 1u) & ~((1u << a) - 1u);
+    const uint32_t wb = (nz[k] >> hs) & keep;
+    if (first < 0 && wb) first = 16 * k + __builtin_ctz(wb);
+    if (wb) last = 16 * k + 31 - __builtin_clz(wb);
+  }
+  T.beg = (first >= 0) ? first : T.end;
+  T.end = (last >= 0) ? min(last + 2, T.qlen) : min(T.beg + 1, T.qlen);
+}
+
+__device__ __forceinline__ int pair_eh_init(const PairTask& T, int j, int h1v, int e_ins) {
+  if (j == 0) return T.h0;
+  if (j > T.qlen) return 0;
+  if (j == 1) return h1v;
+  return max(h1v - (j - 1) * e_ins, 0);
+}
+
+// 128 consecutive tasks of the sorted schedule (lane l: 2l and 2l + 1), from `base`.
+template <int NC, bool SYM>
+__device__ __forceinline__ void pair_wave(const BswDevBatch& b, const BswParams& p, const int32_t* __restrict__ order,
+                                          const long long base, const long long hi, int32_t* __restrict__ res,
+                                          int64_t* __restrict__ cells_out, uint4* __restrict__ qsel,
+                                          const uint32_t* __restrict__ ptab) {
+  const int lane = threadIdx.x;
+  PairTask A, B;
+  task_load(A, b, p, order, base + 2 * lane, hi);
+  task_load(B, b, p, order, base + 2 * lane + 1, hi);
+
+  // selector dwords [qA_j, qA_j+1, 4 + qB_j, 4 + qB_j+1], four per chunk
+  uint4* __restrict__ qs = qsel + lane;
+  {
+    const uint8_t* qa = A.done ? b.qbuf : b.qbuf + b.qoff[A.id];
+    const uint8_t* qb = B.done ? b.qbuf : b.qbuf + b.qoff[B.id];
+#pragma unroll
+    for (int c = 0; c < PCH<NC>; ++c) {
+      uint32_t v[4];
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const int j = kPW * c + 2 * g;
+        const uint32_t a0 = j < A.qlen ? qa[j] & 3u : 0u, a1 = j + 1 < A.qlen ? qa[j + 1] & 3u : 0u;
+        const uint32_t b0 = j < B.qlen ? qb[j] & 3u : 0u, b1 = j + 1 < B.qlen ? qb[j + 1] & 3u : 0u;
+        v[g] = a0 | (a1 << 8) | ((4u + b0) << 16) | ((4u + b1) << 24);
+      }
+      qs[64 * c] = make_uint4(v[0], v[1], v[2], v[3]);
+    }
+  }
+  const PairK k{(uint32_t)p.pair_k256, (uint32_t)p.pair_one, ((uint32_t)p.pair_cg) * 0x10001u, ((uint32_t)p.pair_bias << 8) * 0x10001u,
+                ((uint32_t)(p.o_del + p.e_del) << 8) * 0x10001u, ((uint32_t)p.e_del << 8) * 0x10001u,
+                ((uint32_t)(p.o_ins + p.e_ins) << 8) * 0x10001u, ((uint32_t)p.e_ins << 8) * 0x10001u};
+
+  uint32_t eh[NC];
+  {
+    const int oe_ins = p.o_ins + p.e_ins;
+    const int h1a = A.h0 > oe_ins ? A.h0 - oe_ins : 0, h1b = B.h0 > oe_ins ? B.h0 - oe_ins : 0;
+#pragma unroll
+    for (int j = 0; j < NC; ++j)
+      eh[j] = ((uint32_t)pair_eh_init(A, j, h1a, p.e_ins) << 8) | ((uint32_t)pair_eh_init(B, j, h1b, p.e_ins) << 24);
+  }
+  // wave range of band widths (the band-cut column of row i is i - 1 - w)
+  const int wlo_w = -wave_max(-min(A.done ? (1 << 20) : A.w, B.done ? (1 << 20) : B.w));
+  const int whi_w = wave_max(max(A.done ? -1 : A.w, B.done ? -1 : B.w));
+
+  PairRow<NC> r;
+  for (int i = 0;; ++i) {
+    const bool aliveA = !A.done && i < A.tlen, aliveB = !B.done && i < B.tlen;
+    if (__ballot(aliveA || aliveB) == 0ull) break;
+    const int tA = A.tcur, tB = B.tcur;
+    A.tcur = A.tnext;
+    B.tcur = B.tnext;
+    A.tnext = (aliveA && i + 2 < A.tlen) ? A.tg[i + 2] : 0;
+    B.tnext = (aliveB && i + 2 < B.tlen) ? B.tg[i + 2] : 0;
+    bool workA, emptyA, workB, emptyB;
+    const int h1A = task_row_begin(A, p, i, aliveA, workA, emptyA);
+    const int h1B = task_row_begin(B, p, i, aliveB, workB, emptyB);
+    const int cmin = -wave_max(-min(workA ? A.beg : (1 << 20), workB ? B.beg : (1 << 20)));
+    const int cmax = wave_max(max(workA ? A.end : -1, workB ? B.end : -1));
+    const int emin = -wave_max(-min(workA ? A.end : (1 << 20), workB ? B.end : (1 << 20)));
+    PAIR_STAT(1, 1);
+    PAIR_STAT(5, __popcll(__ballot(workA)) + __popcll(__ballot(workB)));
+    PAIR_STAT(6, __popcll(__ballot(aliveA)) + __popcll(__ballot(aliveB)));
+    PAIR_STAT(7, cmax >= cmin ? cmax - cmin + 1 : 0);
+    r.tabA = ptab[min(tA, 4)];
+    r.tabB = ptab[min(tB, 4)];
+    r.F = 0;
+    r.H1 = ((uint32_t)h1A << 8) | ((uint32_t)h1B << 24);
+    r.KEY = 0;
+    r.CAP = 0;
+    r.BEGM1 = pack2(A.beg - 1, B.beg - 1);
+    r.END = pack2(A.end, B.end);
+    r.ENDX = pack2(A.end + 1, B.end + 1);
+#pragma unroll
+    for (int q = 0; q < PNZ<NC>; ++q) r.nz[q] = 0;
+    if (cmax >= 0) r.sel = qs[64 * (min(max(cmin, 0), NC - 1) / kPW)];
+    // band-cut columns of this row (zeroed as they leave the band)
+    const int cut_lo = i - 1 - whi_w, cut_hi = i - 1 - wlo_w;
+    [&]<int... C>(std::integer_sequence<int, C...>) __attribute__((always_inline)) {
+      (pair_chunk<C, NC, SYM>(eh, qs, r, k, cmin, cmax, emin, cut_lo, cut_hi), ...);
+    }(std::make_integer_sequence<int, PCH<NC>>{});
+    task_row_end<NC>(A, p, i, workA, emptyA, h1A, r.KEY & 0xFFFFu, (int)((r.CAP >> 8) & 0xFFu), r.nz, 0, cmin, cmax);
+    task_row_end<NC>(B, p, i, workB, emptyB, h1B, r.KEY >> 16, (int)(r.CAP >> 24), r.nz, 16, cmin, cmax);
+  }
+#ifdef FCS_BSW_STATS
+  {
+    int tot = A.ncell + B.ncell;
+    for (int o = 32; o > 0; o >>= 1) tot += __shfl_xor(tot, o);
+    PAIR_STAT(4, tot);
+    PAIR_STAT(0, 1);
+  }
+#endif
+  auto emit = [&](const PairTask& T) __attribute__((always_inline)) {
+    if (T.id < 0) return;
+    int32_t* o = res + 6 * T.id;
+    o[0] = T.mx;
+    o[1] = T.max_j + 1;
+    o[2] = T.max_i + 1;
+    o[3] = T.max_ie + 1;
+    o[4] = T.gscore;
+    o[5] = T.max_off;
+    if (cells_out) cells_out[T.id] = T.ncell;
+  };
+  emit(A);
+  emit(B);
+}
+
+}  // namespace
+
+template <int NC, bool SYM>
+__global__ __launch_bounds__(64, NC <= 32 ? 4 : NC <= 64 ? 3 : 2) void bsw_pair_kernel(
+    const BswDevBatch b, const BswParams p, const int32_t* __restrict__ order, const int64_t* __restrict__ bounds,
+    const int bucket, int32_t* __restrict__ res, int64_t* __restrict__ cells_out) {
+  const long long lo = bounds[bucket], hi = bounds[bucket + 1];
+  __shared__ uint4 qsel[PCH<NC> * 64];  // [chunk][lane] selector dwords
+  __shared__ uint32_t ptab[5];          // biased scores mat[t][0..3] + bias, t = A, C, G, T, N
+  if (threadIdx.x < 5) {
+    const int t = threadIdx.x;
+    uint32_t v = 0;
+    for (int c = 0; c < 4; ++c) v |= (uint32_t)(uint8_t)(p.mat[t * 5 + c] + p.pair_bias) << (8 * c);
+    ptab[t] = v;
+  }
+  __syncthreads();
+#ifdef FCS_BSW_STATS
+  if (threadIdx.x < 8) s_pair_stats[threadIdx.x] = 0;
+  __syncthreads();
+#endif
+  for (long long base = lo + 128LL * blockIdx.x; base < hi; base += 128LL * gridDim.x)
+    pair_wave<NC, SYM>(b, p, order, base, hi, res, cells_out, qsel, ptab);
+#ifdef FCS_BSW_STATS
+  __syncthreads();
+  if (threadIdx.x < 8) atomicAdd(&g_pair_stats[bucket - kBswPairBucket0][threadIdx.x], s_pair_stats[threadIdx.x]);
+#endif
+}
+
+int launch_bsw_pair(const BswDevBatch& b, const BswParams& p, int32_t* res, int64_t* cells, const int32_t* order,
+                    const int64_t* bounds, unsigned grid, const hipStream_t (&fs)[kForkStreams]) {
+  const bool sym = p.o_del == p.o_ins && p.e_del == p.e_ins;
+  auto lanes = [&](auto sym_tag) {
+    constexpr bool SYM = decltype(sym_tag)::value;
+    auto go = [&](auto kern, hipStream_t st, int bucket) {
+      hipLaunchKernelGGL(kern, dim3(grid), dim3(64), 0, st, b, p, order, bounds, bucket, res, cells);
+    };
+    go(bsw_pair_kernel<152, SYM>, fs[0], kBswPairBucket0 + 4);
+    go(bsw_pair_kernel<128, SYM>, fs[1], kBswPairBucket0 + 3);
+    go(bsw_pair_kernel<96, SYM>, fs[2], kBswPairBucket0 + 2);
+    go(bsw_pair_kernel<64, SYM>, fs[3], kBswPairBucket0 + 1);
+    go(bsw_pair_kernel<32, SYM>, fs[2], kBswPairBucket0 + 0);
+  };
+  if (sym) lanes(std::true_type{});
+  else lanes(std::false_type{});
+  FCS_HIP_CHECK(hipGetLastError());
+  return FCS_OK;
+}
+
+}  // namespace fcs

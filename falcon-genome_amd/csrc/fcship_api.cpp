@@ -146,6 +146,14 @@ BswParams to_params(const fcs_bsw_params* p) {
     }
     q.matpack[t] = (int32_t)pk;
   }
+  int mn4 = 0, mx4 = 0;
+  for (int t = 0; t < 5; ++t)  // target rows A..N, query columns A..T (the pair kernel's tables)
+    for (int c = 0; c < 4; ++c) mn4 = std::min<int>(mn4, p->mat[t * 5 + c]), mx4 = std::max<int>(mx4, p->mat[t * 5 + c]);
+  q.pair_bias = -mn4;
+  q.pair_cg = mx4 + q.pair_bias + 1;
+  q.pair_ok = q.pair_cg <= 128 ? 1 : 0;
+  q.pair_k256 = 0x01000100;
+  q.pair_one = 0x00010001;
   return q;
 }
 
