@@ -575,10 +575,7 @@ int launch_bsw_extend_sorted(const BswDevBatch& b, const BswParams& p, int max_q
     go(bsw_lane_kernel<16, SYM, false>, fs[1], 0);
   };
   // two-tasks-per-lane kernels first: they carry the bwa-typical tasks
-  if (const int rc = launch_bsw_pair(b, p, res, cells, ws.idx_out, ws.bounds,
-                                     (unsigned)std::min<long long>((b.n + 127) / 128, 8192), fs);
-      rc != FCS_OK)
-    return rc;
+  if (const int rc = launch_bsw_pair(b, p, res, cells, ws.idx_out, ws.bounds, fs[0]); rc != FCS_OK) return rc;
   if (sym) lanes(std::true_type{});
   else lanes(std::false_type{});
   FCS_HIP_CHECK(hipGetLastError());

@@ -105,7 +105,6 @@ __device__ __forceinline__ uint32_t pk_lt(uint32_t a, uint32_t b) {
   return __builtin_bit_cast(uint32_t, d >> (i16x2)(15));
 }
 __device__ __forceinline__ uint32_t pbfi(uint32_t m, uint32_t a, uint32_t b) { return (m & a) | (~m & b); }
-__device__ __forceinline__ void opq(uint32_t& x) { asm volatile("" : "+v"(x)); }
 
 __device__ __forceinline__ uint32_t pack2(int a, int b) { return ((uint32_t)a & 0xFFFFu) | ((uint32_t)b << 16); }
 
@@ -127,27 +126,26 @@ template <int NC>
 struct PairRow {
   uint32_t F, H1, KEY, CAP;
   uint32_t tabA, tabB;       // biased score tables of this row's target bases
-  uint32_t BEGM1, END, ENDX;  // per half: beg - 1, end, end + 1
+  uint32_t BEGM1, END;       // per half: beg - 1, end
   uint32_t O;                // scores of the current column pair
-  uint4 sel, seln;           // selector dwords of this chunk / the next
+  uint4 sel[2];              // selector dwords, double-buffered by chunk parity
   uint32_t nz[PNZ<NC>];
 };
 
-// bwa's inner-loop body for column J of both tasks.  MODE bit 0: mask the
-// inputs left of beg (a band-cut column is in this chunk); bit 1: right-edge
-// masks (some task's end is in or left of this chunk).
-template <int J, int NC, bool SYM, int MODE>
+// bwa's inner-loop body for column J of both tasks, the same code for every
+// chunk.  Edge chunks wrap it in pair_chunk's pre-pass (inputs outside
+// [beg, end) zeroed) and post-pass (entries beyond end restored).
+template <int J, int NC, bool SYM>
 __device__ __forceinline__ void pair_cell(uint32_t (&eh)[NC], PairRow<NC>& r, const PairK& k) {
   constexpr uint32_t JJ = (uint32_t)J | ((uint32_t)J << 16);
-  const uint32_t w0 = eh[J];
-  uint32_t w = w0;
-  if constexpr (MODE & 1) w &= pk_lt(r.BEGM1, JJ);  // J >= beg
+  const uint32_t w = eh[J];
   const uint32_t HP = w & 0xFF00FF00u;
   const uint32_t E = pk_shl8(w);
   uint32_t t;
   if constexpr (J % 2 == 0) {
     constexpr int g = (J % kPW) / 2;
-    const uint32_t sl = g == 0 ? r.sel.x : g == 1 ? r.sel.y : g == 2 ? r.sel.z : r.sel.w;
+    const uint4& cs = r.sel[(J / kPW) & 1];
+    const uint32_t sl = g == 0 ? cs.x : g == 1 ? cs.y : g == 2 ? cs.z : cs.w;
     r.O = __builtin_amdgcn_perm(r.tabB, r.tabA, sl);
     t = pk_mad(r.O, k.k256, HP);
   } else {
@@ -156,37 +154,26 @@ __device__ __forceinline__ void pair_cell(uint32_t (&eh)[NC], PairRow<NC>& r, co
   const uint32_t M = pk_subs(pk_min(t, pk_gate(HP, k.cg)), k.bias);
   const uint32_t H = pk_max(pk_max(M, E), r.F);
   const uint32_t MOd = pk_subs(M, k.oed);
-  uint32_t EN = pk_max(pk_subs(E, k.ed), MOd);
+  const uint32_t EN = pk_max(pk_subs(E, k.ed), MOd);
   const uint32_t MOi = SYM ? MOd : pk_subs(M, k.oei);
   const uint32_t Fn = pk_max(pk_subs(r.F, k.ei), MOi);
-  uint32_t Hk = H, wst;
-  if constexpr (MODE & 2) {
-    const uint32_t mE = pk_lt(JJ, r.END);   // J < end
-    const uint32_t mX = pk_lt(JJ, r.ENDX);  // J <= end
-    EN &= mE;
-    Hk &= mE;
-    r.CAP = pbfi(mX ^ mE, r.H1, r.CAP);  // J == end: bwa's eh[end].h = h1
-    wst = pbfi(mX, __builtin_amdgcn_perm(r.H1, EN, 0x07030501u), w0);
-  } else {
-    wst = __builtin_amdgcn_perm(r.H1, EN, 0x07030501u);
-  }
+  const uint32_t wst = __builtin_amdgcn_perm(r.H1, EN, 0x07030501u);
   eh[J] = wst;
-  r.KEY = pk_max(r.KEY, Hk | JJ);
+  r.KEY = pk_max(r.KEY, H | JJ);
   r.nz[J / 16] |= pk_nz(wst, k.one) << (J % 16);
   r.H1 = H;
   r.F = Fn;
 }
 
-template <int C, int NC>
-__device__ __forceinline__ void pair_opaque(uint32_t (&eh)[NC], PairRow<NC>& r) {
-  constexpr int j0 = kPW * C, L = (NC - j0) < kPW ? (NC - j0) : kPW;
-  [&]<int... K>(std::integer_sequence<int, K...>) __attribute__((always_inline)) {
-    (opq(eh[j0 + K]), ...);
-  }(std::make_integer_sequence<int, L>{});
-  opq(r.tabA);
-  opq(r.tabB);
-}
-
+// One kPW-column chunk of the row.  A chunk some task's band edge touches
+// (its end, or a band-cut column on the left) runs the same cell body with
+// its inputs outside [beg, end) zeroed first.  Zero inputs make the body
+// compute exactly bwa's edge behaviour: left of beg zeros (so h1 = f = 0
+// enter beg), at end the entry {h1, 0} bwa stores, and beyond end only the
+// decaying f chain, which stays below the row max (f <= max M - (o + e)), so
+// the row's arg-max is unaffected.  The post-pass then puts back the stale
+// entries beyond end that bwa leaves untouched, and takes h1 at end (for the
+// to-end score).  Bits of the trims' bitmap beyond end are masked per row.
 template <int C, int NC, bool SYM>
 __device__ __forceinline__ void pair_chunk(uint32_t (&eh)[NC], const uint4* __restrict__ qs, PairRow<NC>& r,
                                            const PairK& k, const int cmin, const int cmax, const int emin,
@@ -194,24 +181,31 @@ __device__ __forceinline__ void pair_chunk(uint32_t (&eh)[NC], const uint4* __re
   constexpr int j0 = kPW * C, L = (NC - j0) < kPW ? (NC - j0) : kPW;
   static_assert(L % 2 == 0, "column pairs share one score perm");
   if (j0 > cmax || j0 + L - 1 < cmin) return;
-  if constexpr (C + 1 < PCH<NC>) r.seln = qs[64 * (C + 1)];
-  const bool right = j0 + L - 1 >= emin;
-  const bool left = j0 <= cut_hi && j0 + L - 1 >= cut_lo;
-  pair_opaque<C, NC>(eh, r);
-  // two bodies only (fast, fully masked): every extra variant of the unrolled
-  // chunk costs instruction-cache footprint shared by the concurrent buckets
-  if (!right && !left) {
-    PAIR_STAT(2, 1);
-    [&]<int... S>(std::integer_sequence<int, S...>) __attribute__((always_inline)) {
-      (pair_cell<j0 + S, NC, SYM, 0>(eh, r, k), ...);
-    }(std::make_integer_sequence<int, L>{});
-  } else {
+  if constexpr (C + 1 < PCH<NC>) r.sel[(C + 1) & 1] = qs[64 * (C + 1)];
+  const bool edge = j0 + L - 1 >= emin || (j0 <= cut_hi && j0 + L - 1 >= cut_lo);
+  uint32_t keep[L];
+  if (edge) {
     PAIR_STAT(3, 1);
     [&]<int... S>(std::integer_sequence<int, S...>) __attribute__((always_inline)) {
-      (pair_cell<j0 + S, NC, SYM, 3>(eh, r, k), ...);
+      ((keep[S] = eh[j0 + S],
+        eh[j0 + S] &= pk_lt((uint32_t)(j0 + S) * 0x10001u, r.END) & pk_lt(r.BEGM1, (uint32_t)(j0 + S) * 0x10001u)),
+       ...);
+    }(std::make_integer_sequence<int, L>{});
+  } else {
+    PAIR_STAT(2, 1);
+  }
+  [&]<int... S>(std::integer_sequence<int, S...>) __attribute__((always_inline)) {
+    (pair_cell<j0 + S, NC, SYM>(eh, r, k), ...);
+  }(std::make_integer_sequence<int, L>{});
+  if (edge) {
+    uint32_t mx = pk_lt((uint32_t)(j0 - 1) * 0x10001u, r.END);  // column j0 <= end
+    [&]<int... S>(std::integer_sequence<int, S...>) __attribute__((always_inline)) {
+      ((r.CAP = pbfi(mx & ~pk_lt((uint32_t)(j0 + S) * 0x10001u, r.END), eh[j0 + S], r.CAP),  // j == end
+        eh[j0 + S] = pbfi(mx, eh[j0 + S], keep[S]),                                          // j > end: stale
+        mx = pk_lt((uint32_t)(j0 + S) * 0x10001u, r.END)),
+       ...);
     }(std::make_integer_sequence<int, L>{});
   }
-  r.sel = r.seln;
 }
 
 // bwa's per-task scalar state.
@@ -402,10 +396,9 @@ __device__ __forceinline__ void pair_wave(const BswDevBatch& b, const BswParams&
     r.CAP = 0;
     r.BEGM1 = pack2(A.beg - 1, B.beg - 1);
     r.END = pack2(A.end, B.end);
-    r.ENDX = pack2(A.end + 1, B.end + 1);
 #pragma unroll
     for (int q = 0; q < PNZ<NC>; ++q) r.nz[q] = 0;
-    if (cmax >= 0) r.sel = qs[64 * (min(max(cmin, 0), NC - 1) / kPW)];
+    if (cmax >= 0) r.sel[0] = r.sel[1] = qs[64 * (min(max(cmin, 0), NC - 1) / kPW)];
     // band-cut columns of this row (zeroed as they leave the band)
     const int cut_lo = i - 1 - whi_w, cut_hi = i - 1 - wlo_w;
     [&]<int... C>(std::integer_sequence<int, C...>) __attribute__((always_inline)) {
@@ -439,48 +432,65 @@ __device__ __forceinline__ void pair_wave(const BswDevBatch& b, const BswParams&
 
 }  // namespace
 
-template <int NC, bool SYM>
-__global__ __launch_bounds__(64, NC <= 32 ? 4 : NC <= 64 ? 3 : 2) void bsw_pair_kernel(
-    const BswDevBatch b, const BswParams p, const int32_t* __restrict__ order, const int64_t* __restrict__ bounds,
-    const int bucket, int32_t* __restrict__ res, int64_t* __restrict__ cells_out) {
-  const long long lo = bounds[bucket], hi = bounds[bucket + 1];
-  __shared__ uint4 qsel[PCH<NC> * 64];  // [chunk][lane] selector dwords
-  __shared__ uint32_t ptab[5];          // biased scores mat[t][0..3] + bias, t = A, C, G, T, N
-  if (threadIdx.x < 5) {
-    const int t = threadIdx.x;
-    uint32_t v = 0;
-    for (int c = 0; c < 4; ++c) v |= (uint32_t)(uint8_t)(p.mat[t * 5 + c] + p.pair_bias) << (8 * c);
-    ptab[t] = v;
+// All five pair buckets in ONE launch, one 128-task wave per workgroup, in
+// longest-first order: workgroup w takes the w-th wave of the concatenation
+// [152 | 128 | 96 | 64 | 32 columns] (each bucket already sorted longest
+// first).  The dispatcher hands out workgroups in order, so the long waves
+// start first and the short ones fill the tail (LPT packing); separate
+// per-bucket launches over streams left ~1/3 of the wave slots idle at the
+// end of a C3 batch.  Registers / LDS are sized for the widest path (2 waves
+// per SIMD for every bucket).
+template <bool SYM>
+__global__ __launch_bounds__(64, 2) void bsw_pair_kernel(const BswDevBatch b, const BswParams p,
+                                                         const int32_t* __restrict__ order,
+                                                         const int64_t* __restrict__ bounds,
+                                                         int32_t* __restrict__ res, int64_t* __restrict__ cells_out) {
+  __shared__ uint4 qsel[PCH<152> * 64];  // [chunk][lane] selector dwords
+  __shared__ uint32_t ptab[5];           // biased scores mat[t][0..3] + bias, t = A, C, G, T, N
+  long long t = blockIdx.x;
+  int slot = -1;
+  long long lo = 0, hi = 0;
+  for (int s = 4; s >= 0; --s) {  // widest bucket first
+    const long long blo = bounds[kBswPairBucket0 + s], bhi = bounds[kBswPairBucket0 + s + 1];
+    const long long nw = (bhi - blo + 127) / 128;
+    if (t < nw) {
+      slot = s, lo = blo + 128 * t, hi = bhi;
+      break;
+    }
+    t -= nw;
   }
-  __syncthreads();
+  if (slot < 0) return;
+  if (threadIdx.x < 5) {
+    const int tb = threadIdx.x;
+    uint32_t v = 0;
+    for (int c = 0; c < 4; ++c) v |= (uint32_t)(uint8_t)(p.mat[tb * 5 + c] + p.pair_bias) << (8 * c);
+    ptab[tb] = v;
+  }
 #ifdef FCS_BSW_STATS
   if (threadIdx.x < 8) s_pair_stats[threadIdx.x] = 0;
-  __syncthreads();
 #endif
-  for (long long base = lo + 128LL * blockIdx.x; base < hi; base += 128LL * gridDim.x)
-    pair_wave<NC, SYM>(b, p, order, base, hi, res, cells_out, qsel, ptab);
+  __syncthreads();
+  switch (slot) {
+    case 4: pair_wave<152, SYM>(b, p, order, lo, hi, res, cells_out, qsel, ptab); break;
+    case 3: pair_wave<128, SYM>(b, p, order, lo, hi, res, cells_out, qsel, ptab); break;
+    case 2: pair_wave<96, SYM>(b, p, order, lo, hi, res, cells_out, qsel, ptab); break;
+    case 1: pair_wave<64, SYM>(b, p, order, lo, hi, res, cells_out, qsel, ptab); break;
+    default: pair_wave<32, SYM>(b, p, order, lo, hi, res, cells_out, qsel, ptab); break;
+  }
 #ifdef FCS_BSW_STATS
   __syncthreads();
-  if (threadIdx.x < 8) atomicAdd(&g_pair_stats[bucket - kBswPairBucket0][threadIdx.x], s_pair_stats[threadIdx.x]);
+  if (threadIdx.x < 8) atomicAdd(&g_pair_stats[slot][threadIdx.x], s_pair_stats[threadIdx.x]);
 #endif
 }
 
 int launch_bsw_pair(const BswDevBatch& b, const BswParams& p, int32_t* res, int64_t* cells, const int32_t* order,
-                    const int64_t* bounds, unsigned grid, const hipStream_t (&fs)[kForkStreams]) {
-  const bool sym = p.o_del == p.o_ins && p.e_del == p.e_ins;
-  auto lanes = [&](auto sym_tag) {
-    constexpr bool SYM = decltype(sym_tag)::value;
-    auto go = [&](auto kern, hipStream_t st, int bucket) {
-      hipLaunchKernelGGL(kern, dim3(grid), dim3(64), 0, st, b, p, order, bounds, bucket, res, cells);
-    };
-    go(bsw_pair_kernel<152, SYM>, fs[0], kBswPairBucket0 + 4);
-    go(bsw_pair_kernel<128, SYM>, fs[1], kBswPairBucket0 + 3);
-    go(bsw_pair_kernel<96, SYM>, fs[2], kBswPairBucket0 + 2);
-    go(bsw_pair_kernel<64, SYM>, fs[3], kBswPairBucket0 + 1);
-    go(bsw_pair_kernel<32, SYM>, fs[2], kBswPairBucket0 + 0);
-  };
-  if (sym) lanes(std::true_type{});
-  else lanes(std::false_type{});
+                    const int64_t* bounds, hipStream_t s) {
+  // upper bound of the waves over the five buckets; the rest exit at once
+  const unsigned grid = (unsigned)((b.n + 127) / 128 + 5);
+  if (p.o_del == p.o_ins && p.e_del == p.e_ins)
+    hipLaunchKernelGGL(bsw_pair_kernel<true>, dim3(grid), dim3(64), 0, s, b, p, order, bounds, res, cells);
+  else
+    hipLaunchKernelGGL(bsw_pair_kernel<false>, dim3(grid), dim3(64), 0, s, b, p, order, bounds, res, cells);
   FCS_HIP_CHECK(hipGetLastError());
   return FCS_OK;
 }

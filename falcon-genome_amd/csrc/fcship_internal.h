@@ -180,9 +180,9 @@ hipError_t hipcub_sort_pairs(void* tmp, size_t& bytes, const uint32_t* kin, uint
 // Sorted schedule: lane-per-task kernels for buckets 0..6, wave-per-task for 7.
 int launch_bsw_extend_sorted(const BswDevBatch& b, const BswParams& p, int max_qlen, int max_tlen, int32_t* res,
                              int64_t* cells, const BswWorkspace& ws, hipStream_t s);
-// Pair kernels over buckets kBswPairBucket0..+4, launched on the fork streams.
+// Pair kernel over buckets kBswPairBucket0..+4 (one launch, longest waves first).
 int launch_bsw_pair(const BswDevBatch& b, const BswParams& p, int32_t* res, int64_t* cells, const int32_t* order,
-                    const int64_t* bounds, unsigned grid, const hipStream_t (&fs)[kForkStreams]);
+                    const int64_t* bounds, hipStream_t s);
 // Wave-per-task kernel over sorted positions [bounds[kBswWideBucket], bounds[kBswWideBucket + 1]).
 int launch_bsw_extend_wide(const BswDevBatch& b, const BswParams& p, int max_qlen, int max_tlen, int32_t* res,
                            int64_t* cells, const int32_t* order, const int64_t* bounds, hipStream_t s);
