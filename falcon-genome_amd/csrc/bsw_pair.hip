@@ -99,10 +99,20 @@ __device__ __forceinline__ uint32_t pk_shl8(uint32_t a) { return U(V(a) << (u16x
 // (a != 0) per half as 0 / 1, with `one` a runtime 0x00010001 (a literal 1
 // turns min(a, 1) into compare + select)
 __device__ __forceinline__ uint32_t pk_nz(uint32_t a, uint32_t one) { return pk_min(a, one); }
-// all-ones per half where (signed) a < b
+// all-ones per half where (signed) a < b.  The shift is inline asm: as a
+// builtin, LLVM turns the sign extraction back into compares + selects.
 __device__ __forceinline__ uint32_t pk_lt(uint32_t a, uint32_t b) {
-  const i16x2 d = __builtin_bit_cast(i16x2, a) - __builtin_bit_cast(i16x2, b);
-  return __builtin_bit_cast(uint32_t, d >> (i16x2)(15));
+  const uint32_t d = __builtin_bit_cast(uint32_t, __builtin_bit_cast(i16x2, a) - __builtin_bit_cast(i16x2, b));
+  uint32_t r;
+  asm("v_pk_ashrrev_i16 %0, 15, %1 op_sel_hi:[0,1]" : "=v"(r) : "v"(d));
+  return r;
+}
+// Returns x through a volatile asm: values derived from the result cannot be
+// computed before the enclosing conditional block, so the edge passes stay
+// behind their branch instead of being speculated into every chunk.
+__device__ __forceinline__ uint32_t launder(uint32_t x) {
+  asm volatile("" : "+v"(x));
+  return x;
 }
 __device__ __forceinline__ uint32_t pbfi(uint32_t m, uint32_t a, uint32_t b) { return (m & a) | (~m & b); }
 
@@ -182,15 +192,21 @@ __device__ __forceinline__ void pair_chunk(uint32_t (&eh)[NC], const uint4* __re
   static_assert(L % 2 == 0, "column pairs share one score perm");
   if (j0 > cmax || j0 + L - 1 < cmin) return;
   if constexpr (C + 1 < PCH<NC>) r.sel[(C + 1) & 1] = qs[64 * (C + 1)];
-  const bool edge = j0 + L - 1 >= emin || (j0 <= cut_hi && j0 + L - 1 >= cut_lo);
+  const bool right = j0 + L - 1 >= emin, left = j0 <= cut_hi && j0 + L - 1 >= cut_lo;
+  const bool edge = right || left;
   uint32_t keep[L];
   if (edge) {
     PAIR_STAT(3, 1);
+    const uint32_t endv = launder(r.END);
     [&]<int... S>(std::integer_sequence<int, S...>) __attribute__((always_inline)) {
-      ((keep[S] = eh[j0 + S],
-        eh[j0 + S] &= pk_lt((uint32_t)(j0 + S) * 0x10001u, r.END) & pk_lt(r.BEGM1, (uint32_t)(j0 + S) * 0x10001u)),
-       ...);
+      ((keep[S] = eh[j0 + S], eh[j0 + S] &= pk_lt((uint32_t)(j0 + S) * 0x10001u, endv)), ...);  // j < end
     }(std::make_integer_sequence<int, L>{});
+    if (left) {
+      const uint32_t begv = launder(r.BEGM1);
+      [&]<int... S>(std::integer_sequence<int, S...>) __attribute__((always_inline)) {
+        ((eh[j0 + S] &= pk_lt(begv, (uint32_t)(j0 + S) * 0x10001u)), ...);  // j >= beg
+      }(std::make_integer_sequence<int, L>{});
+    }
   } else {
     PAIR_STAT(2, 1);
   }
@@ -198,11 +214,24 @@ __device__ __forceinline__ void pair_chunk(uint32_t (&eh)[NC], const uint4* __re
     (pair_cell<j0 + S, NC, SYM>(eh, r, k), ...);
   }(std::make_integer_sequence<int, L>{});
   if (edge) {
-    uint32_t mx = pk_lt((uint32_t)(j0 - 1) * 0x10001u, r.END);  // column j0 <= end
+    const uint32_t endv = launder(r.END);
+    // bitmap bits of this chunk beyond end (restored stale entries) cleared
+    {
+      constexpr int o = j0 % 16;
+      const int endA = (int)(endv & 0xFFFFu), endB = (int)(endv >> 16);
+      const uint32_t ka = __builtin_amdgcn_ubfe(~0u, 0, (uint32_t)min(max(endA + 1 - j0, 0), L));
+      const uint32_t kb = __builtin_amdgcn_ubfe(~0u, 0, (uint32_t)min(max(endB + 1 - j0, 0), L));
+      constexpr uint32_t cm = ((1u << L) - 1u) * 0x10001u << o;
+      r.nz[j0 / 16] &= ~cm | (ka << o) | (kb << (16 + o));
+    }
+    uint32_t mx = pk_lt((uint32_t)(j0 - 1) * 0x10001u, endv);  // column j0 <= end
     [&]<int... S>(std::integer_sequence<int, S...>) __attribute__((always_inline)) {
-      ((r.CAP = pbfi(mx & ~pk_lt((uint32_t)(j0 + S) * 0x10001u, r.END), eh[j0 + S], r.CAP),  // j == end
-        eh[j0 + S] = pbfi(mx, eh[j0 + S], keep[S]),                                          // j > end: stale
-        mx = pk_lt((uint32_t)(j0 + S) * 0x10001u, r.END)),
+      (([&] __attribute__((always_inline)) {
+         const uint32_t me = pk_lt((uint32_t)(j0 + S) * 0x10001u, endv);  // j < end
+         r.CAP = pbfi(mx ^ me, eh[j0 + S], r.CAP);                          // j == end: {h1, 0}
+         eh[j0 + S] = pbfi(mx, eh[j0 + S], keep[S]);                        // j > end: stale entry back
+         mx = me;
+       }()),
        ...);
     }(std::make_integer_sequence<int, L>{});
   }
@@ -302,19 +331,27 @@ __device__ __forceinline__ void task_row_end(PairTask& T, const BswParams& p, in
     }
   }
   if (T.done) return;
-  // bwa's trims over the entries written this row, [beg, end]
-  int first = -1, last = -1;
+  // bwa's trims: beg = first non-zero entry, end = last non-zero entry + 2.
+  // The bitmap holds no bit left of beg (those entries are zero) and none
+  // beyond end (edge chunks clear them), so these are the lowest and highest
+  // set bits: v_ffbl over 32-column words, the highest via bit reverse.
+  constexpr int NM = (PNZ<NC> + 1) / 2;
+  uint32_t fc = ~0u, lc = ~0u;
 #pragma unroll
-  for (int k = 0; k < PNZ<NC>; ++k) {
-    if (16 * k + 15 < wlo || 16 * k > whi) continue;  // wave-uniform: outside every band
-    const int a = min(max(T.beg - 16 * k, 0), 16), z = min(max(T.end + 1 - 16 * k, 0), 16);
-    const uint32_t keep = ((1u << z) - 1u) & ~((1u << a) - 1u);
-    const uint32_t wb = (nz[k] >> hs) & keep;
-    if (first < 0 && wb) first = 16 * k + __builtin_ctz(wb);
-    if (wb) last = 16 * k + 31 - __builtin_clz(wb);
+  for (int m = 0; m < NM; ++m) {
+    if (32 * m + 31 < wlo || 32 * m > whi) continue;  // wave-uniform: outside every band
+    const uint32_t lo = nz[2 * m], hi = (2 * m + 1 < PNZ<NC>) ? nz[2 * m + 1] : 0u;
+    const uint32_t w = __builtin_amdgcn_perm(hi, lo, hs ? 0x07060302u : 0x05040100u);
+    fc = min(fc, (uint32_t)__builtin_ctzg(w, -1) | (uint32_t)(m << 5));
+    lc = min(lc, (uint32_t)__builtin_ctzg(__builtin_bitreverse32(w), -1) | (uint32_t)((NM - 1 - m) << 5));
   }
-  T.beg = (first >= 0) ? first : T.end;
-  T.end = (last >= 0) ? min(last + 2, T.qlen) : min(T.beg + 1, T.qlen);
+  if (fc != ~0u) {
+    T.beg = (int)fc;
+    T.end = min(32 * (NM - 1 - (int)(lc >> 5)) + 31 - (int)(lc & 31u) + 2, T.qlen);
+  } else {
+    T.beg = T.end;
+    T.end = min(T.beg + 1, T.qlen);
+  }
 }
 
 __device__ __forceinline__ int pair_eh_init(const PairTask& T, int j, int h1v, int e_ins) {
