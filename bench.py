@@ -224,6 +224,31 @@ def cpu_baseline_phmm(p, budget_s, threads):
                        f"scalar C oracle restatement (GKL float + double rescue), OpenMP {threads} threads")
 
 
+def bsw_roofline(r3, rf):
+    """SW roofline: VALU issue.  achieved = cells/s x the lane-instructions per
+    cell measured by rocprofv3 (SQ_INSTS_VALU, profiles/pmc_bsw.json, same
+    workloads) against 256 CU x 4 SIMD x 32 lanes x 2.4 GHz; the body of one
+    cell of the pair kernel is 9.75 lane-instructions (19.5 packed VOP3P/VOP2
+    per two tasks).  HBM: algorithmic bytes qlen + tlen + 24 per task."""
+    path = os.path.join(ROOT, "profiles", "pmc_bsw.json")
+    meas = json.load(open(path)) if os.path.exists(path) else {}
+    per3 = meas.get("c3", {}).get("valu_lane_instr_per_cell")
+    perf = meas.get("fixed", {}).get("valu_lane_instr_per_cell")
+    out = {"bound": "valu", "unit": "T lane-instr/s", "peak": round(VALU_LANE_INSTR_PEAK / 1e12, 3),
+           "kernel": "bsw_pair_kernel (two ksw_extend2 tasks per lane, packed 16-bit VOP3P)",
+           "body_instr_per_cell": 9.75,
+           "hbm_GBs": round(r3["bytes"] / (r3["ms"] * 1e-3) / 1e9, 2),
+           "hbm_frac": round(r3["bytes"] / (r3["ms"] * 1e-3) / 1e9 / HBM_PEAK_GBS, 5)}
+    if per3:
+        ach = r3["gcups"] * 1e9 * per3
+        out.update(achieved=round(ach / 1e12, 3), frac=round(ach / VALU_LANE_INSTR_PEAK, 4),
+                   valu_instr_per_cell=per3, valu_source=meas.get("source"))
+    if perf:
+        out["fixed_frac"] = round(rf["gcups"] * 1e9 * perf / VALU_LANE_INSTR_PEAK, 4)
+        out["fixed_valu_instr_per_cell"] = perf
+    return out
+
+
 def cpu_baseline_bsw(tasks, budget_s, threads):
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     import oracle_lib
@@ -310,12 +335,7 @@ def main():
         line["bsw"] = {"workload": "C3: ksw_extend2 left/right seed extensions of 2x151 bp reads, bwa defaults",
                        "c3_gcups": round(r3["gcups"], 3), "c3_tasks": r3["tasks"], "c3_ms": round(r3["ms"], 3),
                        "fixed_151x251_gcups": round(rf["gcups"], 3), "fixed_tasks": rf["tasks"],
-                       "roofline": {"bound": "valu", "valu_instr_per_cell": 16,
-                                    "achieved": round(r3["gcups"] * 16 / 1e3, 3), "peak": VALU_LANE_INSTR_PEAK / 1e12,
-                                    "unit": "T lane-instr/s", "frac": round(r3["gcups"] * 16e9 / VALU_LANE_INSTR_PEAK, 4),
-                                    "fixed_frac": round(rf["gcups"] * 16e9 / VALU_LANE_INSTR_PEAK, 4),
-                                    "note": "16 = VALU instructions of the lane kernel's in-band cell (ISA count); "
-                                            "peak = 256 CU x 4 SIMD x 32 lanes x 2.4 GHz"}}
+                       "roofline": bsw_roofline(r3, rf)}
         if world == 1 and not args.no_cpu_baseline:
             line["bsw"]["cpu_baseline"] = cpu_baseline_bsw(
                 fcship.synth_bsw(args.seed + 1, 20000, read_len=151, ref_len=10_000_000), 0,

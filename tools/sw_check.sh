@@ -31,4 +31,10 @@ if [[ "${2:-}" == *stall* ]]; then
   timeout -k 10 120 rocprofv3 --pmc SQC_ICACHE_MISSES SQC_ICACHE_HITS SQC_ICACHE_REQ -d $O/pmc3 -o run --output-format csv -- python3 tools/bsw_bench.py --which c3 --reps 1 > $O/pmc3.log 2>&1 || exit 1
   python3 tools/pmc_kernels.py $O/pmc3 bsw_
 fi
+if [[ "${2:-}" == *valu* ]]; then
+  export TMPDIR=/tmp
+  for w in c3 fixed; do
+    timeout -k 10 120 rocprofv3 --pmc SQ_INSTS_VALU -d $O/valu_$w -o run --output-format csv -- python3 tools/bsw_bench.py --which $w --reps 1 > $O/valu_$w.log 2>&1 || exit 1
+  done
+fi
 exit 0
