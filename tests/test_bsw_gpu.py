@@ -173,3 +173,74 @@ def test_extend_byte_and_word_buckets(gpu):
         h0 = int(rng.integers(1, 256 - qlen)) if k % 2 else int(rng.integers(256 - qlen, 400))
         items.append((q, t, h0, 100 if k % 3 else int(rng.integers(5, 60))))
     assert_extend_equal(fcship.make_tasks(items))
+
+
+def pair_tasks(seed, n, qmax=151, wlo=1, whi=40, h0max=60, target_n=0.0):
+    """Tasks inside the two-tasks-per-lane envelope (no query N, qlen <= 151)
+    with narrow bands, so band cuts (i - w) and right edges move every row."""
+    rng = np.random.default_rng(seed)
+    items = []
+    for k in range(n):
+        qlen = int(rng.integers(0, qmax + 1))
+        tlen = max(0, qlen + int(rng.integers(-30, 110)))
+        q, t = related_pair(rng, qlen, tlen, sub=0.02 + 0.05 * (k % 3 == 0), indel=0.01 + 0.03 * (k % 5 == 0))
+        if target_n and tlen:
+            t[rng.random(tlen) < target_n] = 4
+        if k % 4 == 1:  # junk tail: z-drop and trims
+            cut = int(rng.integers(0, max(1, min(qlen, tlen))))
+            t[cut:] = rng.integers(0, 4, tlen - cut)
+        items.append((q, t, int(rng.integers(1, h0max + 1)), int(rng.integers(wlo, whi + 1))))
+    return fcship.make_tasks(items)
+
+
+def test_pair_kernel_narrow_bands(gpu):
+    """Band cuts every row (small w): the left-edge zeroing of the pair kernel."""
+    assert_extend_equal(pair_tasks(31, 1500, wlo=1, whi=12))
+    assert_extend_equal(pair_tasks(32, 1500, wlo=10, whi=60))
+
+
+def test_pair_kernel_asymmetric_gaps_and_target_n(gpu):
+    t = pair_tasks(33, 1200, target_n=0.03)
+    assert_extend_equal(t, dict(o_del=4, e_del=2, o_ins=7, e_ins=1, end_bonus=3, zdrop=40))
+    assert_extend_equal(t, dict(o_del=6, e_del=1, o_ins=6, e_ins=1, end_bonus=5, zdrop=0))
+
+
+def test_pair_kernel_score_envelope_boundary(gpu):
+    """h0 + qlen * max(mat) + (pair score bias) straddling 255: the tasks below go
+    to the pair kernel, the ones above to the 16-bit lane kernel; both exact."""
+    rng = np.random.default_rng(34)
+    items = []
+    for k in range(800):
+        qlen = int(rng.integers(20, 152))
+        q, t = related_pair(rng, qlen, qlen + int(rng.integers(0, 100)), sub=0.01)
+        edge = 255 - qlen - 4  # default mat: max 1, bias 4 -> h0 + qlen + 4 <= 255 stays in the pair kernel
+        h0 = max(1, edge + int(rng.integers(-3, 4)))
+        items.append((q, t, h0, 100))
+    assert_extend_equal(fcship.make_tasks(items))
+
+
+def test_pair_kernel_matrices(gpu):
+    rng = np.random.default_rng(35)
+    for trial in range(3):
+        mat = rng.integers(-6, 0, 25).astype(np.int8)
+        mat[[0, 6, 12, 18]] = rng.integers(1, 5, 4)
+        mat[4::5] = -1
+        mat[20:25] = -1
+        assert_extend_equal(pair_tasks(36 + trial, 600, qmax=60, h0max=30, target_n=0.02), mat=mat)
+
+
+def test_pair_kernel_mixed_lengths_in_a_wave(gpu):
+    """Few tasks per query length, so the 128 tasks of a wave differ in qlen,
+    band and row count (lanes finish at different rows)."""
+    rng = np.random.default_rng(37)
+    items = []
+    for k in range(700):
+        qlen = int(rng.integers(0, 152))
+        tlen = int(rng.integers(0, 260))
+        q, t = related_pair(rng, qlen, tlen, sub=0.03)
+        items.append((q, t, int(rng.integers(1, 50)), int(rng.integers(1, 120))))
+    assert_extend_equal(fcship.make_tasks(items))
+
+
+def test_pair_kernel_c3_batch(gpu):
+    assert_extend_equal(fcship.synth_bsw(20261016, 20000, ref_len=4_000_000))
