@@ -167,8 +167,10 @@ __device__ __forceinline__ void pair_cell(uint32_t (&eh)[NC], PairRow<NC>& r, co
   const uint32_t EN = pk_max(pk_subs(E, k.ed), MOd);
   const uint32_t MOi = SYM ? MOd : pk_subs(M, k.oei);
   const uint32_t Fn = pk_max(pk_subs(r.F, k.ei), MOi);
-  const uint32_t wst = __builtin_amdgcn_perm(r.H1, EN, 0x07030501u);
-  eh[J] = wst;
+  // in place (tied operand), so no chunk path moves eh[] between registers;
+  // edge chunks copy the entries they must restore in their pre-pass
+  asm("v_perm_b32 %0, %1, %2, %3" : "+v"(eh[J]) : "v"(r.H1), "v"(EN), "s"(0x07030501u));
+  const uint32_t wst = eh[J];
   r.KEY = pk_max(r.KEY, H | JJ);
   r.nz[J / 16] |= pk_nz(wst, k.one) << (J % 16);
   r.H1 = H;
@@ -186,14 +188,14 @@ __device__ __forceinline__ void pair_cell(uint32_t (&eh)[NC], PairRow<NC>& r, co
 // to-end score).  Bits of the trims' bitmap beyond end are masked per row.
 template <int C, int NC, bool SYM>
 __device__ __forceinline__ void pair_chunk(uint32_t (&eh)[NC], const uint4* __restrict__ qs, PairRow<NC>& r,
-                                           const PairK& k, const int cmin, const int cmax, const int emin,
-                                           const int cut_lo, const int cut_hi) {
+                                           const PairK& k, const uint32_t proc, const uint32_t edges,
+                                           const uint32_t cuts) {
   constexpr int j0 = kPW * C, L = (NC - j0) < kPW ? (NC - j0) : kPW;
   static_assert(L % 2 == 0, "column pairs share one score perm");
-  if (j0 > cmax || j0 + L - 1 < cmin) return;
+  if (!((proc >> C) & 1u)) return;
   if constexpr (C + 1 < PCH<NC>) r.sel[(C + 1) & 1] = qs[64 * (C + 1)];
-  const bool right = j0 + L - 1 >= emin, left = j0 <= cut_hi && j0 + L - 1 >= cut_lo;
-  const bool edge = right || left;
+  const bool left = (cuts >> C) & 1u;
+  const bool edge = (edges >> C) & 1u;
   uint32_t keep[L];
   if (edge) {
     PAIR_STAT(3, 1);
@@ -437,9 +439,24 @@ __device__ __forceinline__ void pair_wave(const BswDevBatch& b, const BswParams&
     for (int q = 0; q < PNZ<NC>; ++q) r.nz[q] = 0;
     if (cmax >= 0) r.sel[0] = r.sel[1] = qs[64 * (min(max(cmin, 0), NC - 1) / kPW)];
     // band-cut columns of this row (zeroed as they leave the band)
-    const int cut_lo = i - 1 - whi_w, cut_hi = i - 1 - wlo_w;
+    // chunk classes of this row as wave-uniform bit masks (bit C = chunk C):
+    // processed = overlaps [cmin, cmax]; edge = reaches some end (>= emin) or
+    // holds a band-cut column [i - 1 - max w, i - 1 - min w]
+    uint32_t proc = 0, edges = 0, cuts = 0;
+    if (cmax >= cmin) {
+      const int cf = max(cmin, 0) / kPW, cl = min(cmax, NC - 1) / kPW;
+      proc = (cl >= 31 ? ~0u : (2u << cl) - 1u) & ~((1u << cf) - 1u);
+      const int ef = max(emin, 0) / kPW;  // first chunk whose last column >= emin
+      edges = proc & ~((1u << min(ef, 31)) - 1u);
+      const int cut_lo = i - 1 - whi_w, cut_hi = i - 1 - wlo_w;
+      if (cut_hi >= 0) {
+        const int kf = max(cut_lo, 0) / kPW, kl = min(cut_hi, NC - 1) / kPW;
+        cuts = proc & (kl >= 31 ? ~0u : (2u << kl) - 1u) & ~((1u << kf) - 1u);
+      }
+      edges |= cuts;
+    }
     [&]<int... C>(std::integer_sequence<int, C...>) __attribute__((always_inline)) {
-      (pair_chunk<C, NC, SYM>(eh, qs, r, k, cmin, cmax, emin, cut_lo, cut_hi), ...);
+      (pair_chunk<C, NC, SYM>(eh, qs, r, k, proc, edges, cuts), ...);
     }(std::make_integer_sequence<int, PCH<NC>>{});
     task_row_end<NC>(A, p, i, workA, emptyA, h1A, r.KEY & 0xFFFFu, (int)((r.CAP >> 8) & 0xFFu), r.nz, 0, cmin, cmax);
     task_row_end<NC>(B, p, i, workB, emptyB, h1B, r.KEY >> 16, (int)(r.CAP >> 24), r.nz, 16, cmin, cmax);
