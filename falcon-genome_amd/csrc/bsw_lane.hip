@@ -464,12 +464,13 @@ extern "C" int fcs_bsw_stats_read(unsigned long long* out, int reset) {
 // 16-bit layout already runs 3-4 waves and is cheaper per cell);
 // kBswPairBucket0..+4 = two-tasks-per-lane kernels (bsw_pair.hip) with
 // 32/64/96/128/152 columns for tasks whose biased scores fit a byte and whose
-// query and target hold no N (`acgt`); kBswWideBucket = wave-per-task kernel
+// query holds no N (`acgt`), with tlen < 1024 (the pair kernel's 16-bit row
+// bookkeeping); kBswWideBucket = wave-per-task kernel
 // (long queries, scores beyond int16, matrices beyond 5 bits).
-__device__ __forceinline__ int bsw_bucket(int qlen, int h0, bool acgt, const BswParams& p) {
+__device__ __forceinline__ int bsw_bucket(int qlen, int tlen, int h0, bool acgt, const BswParams& p) {
   const long long bound = (long long)h0 + (long long)qlen * p.max_mat;  // no cell can score more
   const int need = qlen + 1;
-  if (p.pair_ok && acgt && h0 > 0 && need <= 152 && bound + p.pair_cg - 1 <= 255)
+  if (p.pair_ok && acgt && h0 > 0 && need <= 152 && tlen < 1024 && bound + p.pair_cg - 1 <= 255)
     return kBswPairBucket0 + (need <= 32 ? 0 : need <= 64 ? 1 : need <= 96 ? 2 : need <= 128 ? 3 : 4);
   if (!p.lane_ok || h0 <= 0 || bound >= 32000) return kBswWideBucket;
   if (need <= 16) return 0;
@@ -511,7 +512,7 @@ __global__ void bsw_keys_kernel(const BswDevBatch b, const BswParams p, uint32_t
   // the pair kernels score target N rows from their table but take queries
   // without N only (a query N would need a fifth score per column)
   const bool acgt = p.pair_ok && qlen < 152 && bsw_query_acgt(b.qbuf + b.qoff[k], qlen);
-  const uint32_t bk = (uint32_t)bsw_bucket(qlen, h0, acgt, p);
+  const uint32_t bk = (uint32_t)bsw_bucket(qlen, tlen, h0, acgt, p);
   // Rows a task is expected to run: an extension that keeps matching peaks
   // near row qlen with score ~h0 + qlen*max_mat and then decays by e_del per
   // row until the row max hits 0 (bwa's m == 0 exit), capped by tlen.  Tasks

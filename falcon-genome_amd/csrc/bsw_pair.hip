@@ -281,80 +281,28 @@ __device__ __forceinline__ void task_load(PairTask& T, const BswDevBatch& b, con
   T.tnext = (T.tlen > 1) ? T.tg[1] : 0;
 }
 
-// Row start: bwa's band update and h1.  Returns h1 (0 for a task not working).
-__device__ __forceinline__ int task_row_begin(PairTask& T, const BswParams& p, int i, bool alive, bool& work,
-                                              bool& empty) {
-  int h1 = 0;
-  if (alive) {
-    if (T.beg < i - T.w) T.beg = i - T.w;
-    if (T.end > i + T.w + 1) T.end = i + T.w + 1;
-    if (T.end > T.qlen) T.end = T.qlen;
-    if (T.beg == 0) {
-      h1 = T.h0 - (p.o_del + p.e_del * (i + 1));
-      if (h1 < 0) h1 = 0;
-    }
-  }
-  empty = alive && T.beg >= T.end;
-  work = alive && !empty;
-  return h1;
+// ---------------------------------------------------------------- bookkeeping
+// bwa's per-row scalar logic for both tasks at once: every field is a pair of
+// signed 16-bit halves (task A low, B high) and every condition an all-ones
+// half mask, so the row start / end costs the same as for one task.  The
+// envelope keeps every value in range (tlen < 1024, e_del, e_ins <= 16).
+__device__ __forceinline__ i16x2 SI(uint32_t x) { return __builtin_bit_cast(i16x2, x); }
+__device__ __forceinline__ uint32_t SU(i16x2 x) { return __builtin_bit_cast(uint32_t, x); }
+__device__ __forceinline__ uint32_t s_add(uint32_t a, uint32_t b) { return SU(SI(a) + SI(b)); }
+__device__ __forceinline__ uint32_t s_sub(uint32_t a, uint32_t b) { return SU(SI(a) - SI(b)); }
+__device__ __forceinline__ uint32_t s_mul(uint32_t a, uint32_t b) { return SU(SI(a) * SI(b)); }
+__device__ __forceinline__ uint32_t s_max(uint32_t a, uint32_t b) { return SU(__builtin_elementwise_max(SI(a), SI(b))); }
+__device__ __forceinline__ uint32_t s_min(uint32_t a, uint32_t b) { return SU(__builtin_elementwise_min(SI(a), SI(b))); }
+// all-ones per half where a == b (one = 0x00010001 at run time)
+__device__ __forceinline__ uint32_t s_eq(uint32_t a, uint32_t b, uint32_t one) {
+  return U(V(pk_min(a ^ b, one)) - V(one));
 }
 
-// Row end: bwa's to-end score, row max / z-drop, and trims from the bitmap
-// half `hs` (0 or 16) of the nz words.
-template <int NC>
-__device__ __forceinline__ void task_row_end(PairTask& T, const BswParams& p, int i, bool work, bool empty, int h1_row,
-                                             uint32_t key, int cap, const uint32_t (&nz)[PNZ<NC>], int hs,
-                                             int wlo, int whi) {
-  if (empty) {
-    if (T.beg == T.qlen) {
-      T.max_ie = T.gscore > h1_row ? T.max_ie : i;
-      T.gscore = T.gscore > h1_row ? T.gscore : h1_row;
-    }
-    T.done = true;
-  }
-  if (!work) return;
-  T.ncell += T.end - T.beg;
-  if (T.end == T.qlen) {
-    T.max_ie = T.gscore > cap ? T.max_ie : i;
-    T.gscore = T.gscore > cap ? T.gscore : cap;
-  }
-  const int m = (int)(key >> 8), mj = (int)(key & 0xFFu);
-  if (m == 0) {
-    T.done = true;
-  } else if (m > T.mx) {
-    T.mx = m, T.max_i = i, T.max_j = mj;
-    const int d = mj > i ? mj - i : i - mj;
-    T.max_off = T.max_off > d ? T.max_off : d;
-  } else if (p.zdrop > 0) {
-    if (i - T.max_i > mj - T.max_j) {
-      if (T.mx - m - ((i - T.max_i) - (mj - T.max_j)) * p.e_del > p.zdrop) T.done = true;
-    } else {
-      if (T.mx - m - ((mj - T.max_j) - (i - T.max_i)) * p.e_ins > p.zdrop) T.done = true;
-    }
-  }
-  if (T.done) return;
-  // bwa's trims: beg = first non-zero entry, end = last non-zero entry + 2.
-  // The bitmap holds no bit left of beg (those entries are zero) and none
-  // beyond end (edge chunks clear them), so these are the lowest and highest
-  // set bits: v_ffbl over 32-column words, the highest via bit reverse.
-  constexpr int NM = (PNZ<NC> + 1) / 2;
-  uint32_t fc = ~0u, lc = ~0u;
-#pragma unroll
-  for (int m = 0; m < NM; ++m) {
-    if (32 * m + 31 < wlo || 32 * m > whi) continue;  // wave-uniform: outside every band
-    const uint32_t lo = nz[2 * m], hi = (2 * m + 1 < PNZ<NC>) ? nz[2 * m + 1] : 0u;
-    const uint32_t w = __builtin_amdgcn_perm(hi, lo, hs ? 0x07060302u : 0x05040100u);
-    fc = min(fc, (uint32_t)__builtin_ctzg(w, -1) | (uint32_t)(m << 5));
-    lc = min(lc, (uint32_t)__builtin_ctzg(__builtin_bitreverse32(w), -1) | (uint32_t)((NM - 1 - m) << 5));
-  }
-  if (fc != ~0u) {
-    T.beg = (int)fc;
-    T.end = min(32 * (NM - 1 - (int)(lc >> 5)) + 31 - (int)(lc & 31u) + 2, T.qlen);
-  } else {
-    T.beg = T.end;
-    T.end = min(T.beg + 1, T.qlen);
-  }
-}
+struct PairState {
+  uint32_t QLEN, TLEN, W, H0, BEG, END;
+  uint32_t MX, MAXI, MAXJ, MAXIE, GS, MOFF, DONE;
+  uint32_t NCA, NCB;  // evaluated cells (32-bit per task)
+};
 
 __device__ __forceinline__ int pair_eh_init(const PairTask& T, int j, int h1v, int e_ins) {
   if (j == 0) return T.h0;
@@ -408,37 +356,63 @@ __device__ __forceinline__ void pair_wave(const BswDevBatch& b, const BswParams&
   const int wlo_w = -wave_max(-min(A.done ? (1 << 20) : A.w, B.done ? (1 << 20) : B.w));
   const int whi_w = wave_max(max(A.done ? -1 : A.w, B.done ? -1 : B.w));
 
+  PairState S;
+  S.QLEN = pack2(A.qlen, B.qlen);
+  S.TLEN = pack2(A.tlen, B.tlen);
+  S.W = pack2(A.w, B.w);
+  S.H0 = pack2(A.h0, B.h0);
+  S.BEG = 0;
+  S.END = S.QLEN;
+  S.MX = S.H0;
+  S.MAXI = S.MAXJ = S.MAXIE = S.GS = 0xFFFFFFFFu;  // -1, -1
+  S.MOFF = 0;
+  S.DONE = (A.done ? 0xFFFFu : 0u) | (B.done ? 0xFFFF0000u : 0u);
+  S.NCA = S.NCB = 0;
+  const uint8_t* __restrict__ tgA = A.tg;
+  const uint8_t* __restrict__ tgB = B.tg;
+  const int tlenA = A.tlen, tlenB = B.tlen;
+  uint32_t TB = (uint32_t)A.tcur | ((uint32_t)A.tnext << 8) | ((uint32_t)B.tcur << 16) | ((uint32_t)B.tnext << 24);
+  const uint32_t ONE = k.one, ED1 = (uint32_t)p.e_del * 0x10001u, EI1 = (uint32_t)p.e_ins * 0x10001u;
+  const uint32_t ZD2 = (uint32_t)min(p.zdrop, 32767) * 0x10001u;
+
   PairRow<NC> r;
   for (int i = 0;; ++i) {
-    const bool aliveA = !A.done && i < A.tlen, aliveB = !B.done && i < B.tlen;
-    if (__ballot(aliveA || aliveB) == 0ull) break;
-    const int tA = A.tcur, tB = B.tcur;
-    A.tcur = A.tnext;
-    B.tcur = B.tnext;
-    A.tnext = (aliveA && i + 2 < A.tlen) ? A.tg[i + 2] : 0;
-    B.tnext = (aliveB && i + 2 < B.tlen) ? B.tg[i + 2] : 0;
-    bool workA, emptyA, workB, emptyB;
-    const int h1A = task_row_begin(A, p, i, aliveA, workA, emptyA);
-    const int h1B = task_row_begin(B, p, i, aliveB, workB, emptyB);
-    const int cmin = -wave_max(-min(workA ? A.beg : (1 << 20), workB ? B.beg : (1 << 20)));
-    const int cmax = wave_max(max(workA ? A.end : -1, workB ? B.end : -1));
-    const int emin = -wave_max(-min(workA ? A.end : (1 << 20), workB ? B.end : (1 << 20)));
+    const uint32_t I2 = (uint32_t)i * 0x10001u;
+    const uint32_t ALIVE = ~S.DONE & pk_lt(I2, S.TLEN);
+    if (__ballot(ALIVE != 0u) == 0ull) break;
+    const uint32_t tA = TB & 0xFFu, tB = (TB >> 16) & 0xFFu;
+    {
+      const uint32_t nA = ((ALIVE & 0xFFFFu) && i + 2 < tlenA) ? tgA[i + 2] : 0u;
+      const uint32_t nB = ((ALIVE >> 16) && i + 2 < tlenB) ? tgB[i + 2] : 0u;
+      TB = ((TB >> 8) & 0x00FF00FFu) | (nA << 8) | (nB << 24);
+    }
+    // bwa's band: beg = max(beg, i - w), end = min(end, i + w + 1, qlen)
+    S.BEG = s_max(S.BEG, s_sub(I2, S.W));
+    S.END = s_min(S.END, s_min(s_add(s_add(I2, ONE), S.W), S.QLEN));
+    // h1 of the row start: max(h0 - (o_del + e_del (i + 1)), 0) where beg == 0
+    const uint32_t ode = (uint32_t)min(p.o_del + p.e_del * (i + 1), 65535) * 0x10001u;
+    const uint32_t H1r = pk_subs(S.H0, ode) & pk_lt(S.BEG, ONE);
+    const uint32_t WORK = ALIVE & pk_lt(S.BEG, S.END);
+    const uint32_t EMPTY = ALIVE ^ WORK;  // beg >= end: bwa stores eh[end] and stops
+    const int begA = (int)(int16_t)(S.BEG & 0xFFFFu), begB = (int)(int16_t)(S.BEG >> 16);
+    const int endA = (int)(int16_t)(S.END & 0xFFFFu), endB = (int)(int16_t)(S.END >> 16);
+    const bool workA = WORK & 1u, workB = (WORK >> 16) & 1u;
+    const int cmin = -wave_max(-min(workA ? begA : (1 << 20), workB ? begB : (1 << 20)));
+    const int cmax = wave_max(max(workA ? endA : -1, workB ? endB : -1));
+    const int emin = -wave_max(-min(workA ? endA : (1 << 20), workB ? endB : (1 << 20)));
     PAIR_STAT(1, 1);
-    PAIR_STAT(5, __popcll(__ballot(workA)) + __popcll(__ballot(workB)));
-    PAIR_STAT(6, __popcll(__ballot(aliveA)) + __popcll(__ballot(aliveB)));
     PAIR_STAT(7, cmax >= cmin ? cmax - cmin + 1 : 0);
-    r.tabA = ptab[min(tA, 4)];
-    r.tabB = ptab[min(tB, 4)];
+    r.tabA = ptab[min(tA, 4u)];
+    r.tabB = ptab[min(tB, 4u)];
     r.F = 0;
-    r.H1 = ((uint32_t)h1A << 8) | ((uint32_t)h1B << 24);
+    r.H1 = pk_shl8(H1r);
     r.KEY = 0;
     r.CAP = 0;
-    r.BEGM1 = pack2(A.beg - 1, B.beg - 1);
-    r.END = pack2(A.end, B.end);
+    r.BEGM1 = s_sub(S.BEG, ONE);
+    r.END = S.END;
 #pragma unroll
     for (int q = 0; q < PNZ<NC>; ++q) r.nz[q] = 0;
     if (cmax >= 0) r.sel[0] = r.sel[1] = qs[64 * (min(max(cmin, 0), NC - 1) / kPW)];
-    // band-cut columns of this row (zeroed as they leave the band)
     // chunk classes of this row as wave-uniform bit masks (bit C = chunk C):
     // processed = overlaps [cmin, cmax]; edge = reaches some end (>= emin) or
     // holds a band-cut column [i - 1 - max w, i - 1 - min w]
@@ -458,30 +432,91 @@ __device__ __forceinline__ void pair_wave(const BswDevBatch& b, const BswParams&
     [&]<int... C>(std::integer_sequence<int, C...>) __attribute__((always_inline)) {
       (pair_chunk<C, NC, SYM>(eh, qs, r, k, proc, edges, cuts), ...);
     }(std::make_integer_sequence<int, PCH<NC>>{});
-    task_row_end<NC>(A, p, i, workA, emptyA, h1A, r.KEY & 0xFFFFu, (int)((r.CAP >> 8) & 0xFFu), r.nz, 0, cmin, cmax);
-    task_row_end<NC>(B, p, i, workB, emptyB, h1B, r.KEY >> 16, (int)(r.CAP >> 24), r.nz, 16, cmin, cmax);
+
+    // ---- row end (bwa's order): to-end score, cells, m == 0, new max or z-drop, trims
+    const uint32_t M8 = U(V(r.KEY) >> (u16x2)(8)), MJ = r.KEY & 0x00FF00FFu;
+    // to-end score: a working row reaching qlen (h1 at end) or an empty row with beg == qlen
+    const uint32_t CAND = pbfi(WORK, U(V(r.CAP) >> (u16x2)(8)), H1r);
+    const uint32_t GATE = (WORK & s_eq(S.END, S.QLEN, ONE)) | (EMPTY & s_eq(S.BEG, S.QLEN, ONE));
+    const uint32_t UPD = GATE & ~pk_lt(CAND, S.GS);  // ties go to the later row
+    S.GS = pbfi(UPD, CAND, S.GS);
+    S.MAXIE = pbfi(UPD, I2, S.MAXIE);
+    {
+      const uint32_t dc = s_sub(S.END, S.BEG) & WORK;
+      S.NCA += dc & 0xFFFFu;
+      S.NCB += dc >> 16;
+    }
+    const uint32_t ZERO = WORK & s_eq(M8, 0u, ONE);
+    const uint32_t NEWMAX = WORK & pk_lt(S.MX, M8);
+    uint32_t DROP = 0;
+    if (p.zdrop > 0) {
+      // (i - max_i) - (mj - max_j) > 0: mx - m - d e_del > zdrop; else mx - m + d e_ins > zdrop
+      const uint32_t D = s_sub(s_sub(I2, S.MAXI), s_sub(MJ, S.MAXJ));
+      const uint32_t base = s_sub(S.MX, M8);
+      const uint32_t val = pbfi(pk_lt(0u, D), s_sub(base, s_mul(D, ED1)), s_add(base, s_mul(D, EI1)));
+      DROP = WORK & ~NEWMAX & ~ZERO & pk_lt(ZD2, val);
+    }
+    S.MOFF = pbfi(NEWMAX, s_max(S.MOFF, s_max(s_sub(MJ, I2), s_sub(I2, MJ))), S.MOFF);
+    S.MX = pbfi(NEWMAX, M8, S.MX);
+    S.MAXI = pbfi(NEWMAX, I2, S.MAXI);
+    S.MAXJ = pbfi(NEWMAX, MJ, S.MAXJ);
+    S.DONE |= EMPTY | ZERO | DROP;
+    const uint32_t TRIM = WORK & ~S.DONE;
+    if (__ballot(TRIM != 0u)) {
+      // bwa's trims: beg = first non-zero entry, end = last non-zero entry + 2.
+      // The bitmap holds no bit left of beg (those entries are zero) and none
+      // beyond end (edge chunks clear them), so these are the lowest and highest
+      // set bits: v_ffbl over 32-column words, the highest via bit reverse.
+      constexpr int NM = (PNZ<NC> + 1) / 2;
+      uint32_t fa = ~0u, la = ~0u, fb = ~0u, lb = ~0u;
+#pragma unroll
+      for (int m = 0; m < NM; ++m) {
+        if (32 * m + 31 < cmin || 32 * m > cmax) continue;  // wave-uniform: outside every band
+        const uint32_t lo = r.nz[2 * m], hi = (2 * m + 1 < PNZ<NC>) ? r.nz[2 * m + 1] : 0u;
+        const uint32_t wa = __builtin_amdgcn_perm(hi, lo, 0x05040100u), wb = __builtin_amdgcn_perm(hi, lo, 0x07060302u);
+        fa = min(fa, (uint32_t)__builtin_ctzg(wa, -1) | (uint32_t)(m << 5));
+        la = min(la, (uint32_t)__builtin_ctzg(__builtin_bitreverse32(wa), -1) | (uint32_t)((NM - 1 - m) << 5));
+        fb = min(fb, (uint32_t)__builtin_ctzg(wb, -1) | (uint32_t)(m << 5));
+        lb = min(lb, (uint32_t)__builtin_ctzg(__builtin_bitreverse32(wb), -1) | (uint32_t)((NM - 1 - m) << 5));
+      }
+      auto trim = [&](uint32_t f, uint32_t l, int endv, int qlen, int& nb, int& ne) __attribute__((always_inline)) {
+        if (f != ~0u) {
+          nb = (int)f;
+          ne = min(32 * (NM - 1 - (int)(l >> 5)) + 31 - (int)(l & 31u) + 2, qlen);
+        } else {
+          nb = endv;
+          ne = min(endv + 1, qlen);
+        }
+      };
+      int nba, nea, nbb, neb;
+      trim(fa, la, endA, A.qlen, nba, nea);
+      trim(fb, lb, endB, B.qlen, nbb, neb);
+      S.BEG = pbfi(TRIM, pack2(nba, nbb), S.BEG);
+      S.END = pbfi(TRIM, pack2(nea, neb), S.END);
+    }
   }
 #ifdef FCS_BSW_STATS
   {
-    int tot = A.ncell + B.ncell;
+    int tot = (int)(S.NCA + S.NCB);
     for (int o = 32; o > 0; o >>= 1) tot += __shfl_xor(tot, o);
     PAIR_STAT(4, tot);
     PAIR_STAT(0, 1);
   }
 #endif
-  auto emit = [&](const PairTask& T) __attribute__((always_inline)) {
-    if (T.id < 0) return;
-    int32_t* o = res + 6 * T.id;
-    o[0] = T.mx;
-    o[1] = T.max_j + 1;
-    o[2] = T.max_i + 1;
-    o[3] = T.max_ie + 1;
-    o[4] = T.gscore;
-    o[5] = T.max_off;
-    if (cells_out) cells_out[T.id] = T.ncell;
+  auto emit = [&](long long id, int h, uint32_t nc) __attribute__((always_inline)) {
+    if (id < 0) return;
+    auto f = [&](uint32_t x) { return (int)(int16_t)(h ? (x >> 16) : (x & 0xFFFFu)); };
+    int32_t* o = res + 6 * id;
+    o[0] = f(S.MX);
+    o[1] = f(S.MAXJ) + 1;
+    o[2] = f(S.MAXI) + 1;
+    o[3] = f(S.MAXIE) + 1;
+    o[4] = f(S.GS);
+    o[5] = f(S.MOFF);
+    if (cells_out) cells_out[id] = nc;
   };
-  emit(A);
-  emit(B);
+  emit(A.id, 0, S.NCA);
+  emit(B.id, 1, S.NCB);
 }
 
 }  // namespace

@@ -151,7 +151,8 @@ BswParams to_params(const fcs_bsw_params* p) {
     for (int c = 0; c < 4; ++c) mn4 = std::min<int>(mn4, p->mat[t * 5 + c]), mx4 = std::max<int>(mx4, p->mat[t * 5 + c]);
   q.pair_bias = -mn4;
   q.pair_cg = mx4 + q.pair_bias + 1;
-  q.pair_ok = q.pair_cg <= 128 ? 1 : 0;
+  // the pair kernel's 16-bit z-drop arithmetic: |row distance| * e stays below 2^15
+  q.pair_ok = (q.pair_cg <= 128 && p->e_del <= 16 && p->e_ins <= 16) ? 1 : 0;
   q.pair_k256 = 0x01000100;
   q.pair_one = 0x00010001;
   return q;
