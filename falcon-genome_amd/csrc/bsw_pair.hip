@@ -107,6 +107,19 @@ __device__ __forceinline__ uint32_t pk_lt(uint32_t a, uint32_t b) {
   asm("v_pk_ashrrev_i16 %0, 15, %1 op_sel_hi:[0,1]" : "=v"(r) : "v"(d));
   return r;
 }
+// In-place updates of eh[] entries (tied operands): every path through a
+// chunk leaves an entry in its own register, so chunk joins need no copies.
+__device__ __forceinline__ void and_in_place(uint32_t& x, uint32_t m) { asm("v_and_b32 %0, %0, %1" : "+v"(x) : "v"(m)); }
+// A copy in a register of its own (the entry's register stays with eh[]).
+__device__ __forceinline__ uint32_t vcopy(uint32_t x) {
+  uint32_t r;
+  asm("v_mov_b32 %0, %1" : "=v"(r) : "v"(x));
+  return r;
+}
+// x = m ? x : k per bit
+__device__ __forceinline__ void bfi_in_place(uint32_t& x, uint32_t m, uint32_t k) {
+  asm("v_bfi_b32 %0, %1, %0, %2" : "+v"(x) : "v"(m), "v"(k));
+}
 // Returns x through a volatile asm: values derived from the result cannot be
 // computed before the enclosing conditional block, so the edge passes stay
 // behind their branch instead of being speculated into every chunk.
@@ -201,12 +214,12 @@ __device__ __forceinline__ void pair_chunk(uint32_t (&eh)[NC], const uint4* __re
     PAIR_STAT(3, 1);
     const uint32_t endv = launder(r.END);
     [&]<int... S>(std::integer_sequence<int, S...>) __attribute__((always_inline)) {
-      ((keep[S] = eh[j0 + S], eh[j0 + S] &= pk_lt((uint32_t)(j0 + S) * 0x10001u, endv)), ...);  // j < end
+      ((keep[S] = vcopy(eh[j0 + S]), and_in_place(eh[j0 + S], pk_lt((uint32_t)(j0 + S) * 0x10001u, endv))), ...);  // j < end
     }(std::make_integer_sequence<int, L>{});
     if (left) {
       const uint32_t begv = launder(r.BEGM1);
       [&]<int... S>(std::integer_sequence<int, S...>) __attribute__((always_inline)) {
-        ((eh[j0 + S] &= pk_lt(begv, (uint32_t)(j0 + S) * 0x10001u)), ...);  // j >= beg
+        (and_in_place(eh[j0 + S], pk_lt(begv, (uint32_t)(j0 + S) * 0x10001u)), ...);  // j >= beg
       }(std::make_integer_sequence<int, L>{});
     }
   } else {
@@ -231,7 +244,7 @@ __device__ __forceinline__ void pair_chunk(uint32_t (&eh)[NC], const uint4* __re
       (([&] __attribute__((always_inline)) {
          const uint32_t me = pk_lt((uint32_t)(j0 + S) * 0x10001u, endv);  // j < end
          r.CAP = pbfi(mx ^ me, eh[j0 + S], r.CAP);                          // j == end: {h1, 0}
-         eh[j0 + S] = pbfi(mx, eh[j0 + S], keep[S]);                        // j > end: stale entry back
+         bfi_in_place(eh[j0 + S], mx, keep[S]);                             // j > end: stale entry back
          mx = me;
        }()),
        ...);

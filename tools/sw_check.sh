@@ -26,7 +26,7 @@ if [[ "${2:-}" == *pmc* ]]; then
 fi
 if [[ "${2:-}" == *stall* ]]; then
   export TMPDIR=/tmp
-  timeout -k 10 120 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_ACTIVE_INST_VALU SQ_WAIT_INST_ANY SQ_WAIT_ANY SQ_INSTS_VALU SQ_IFETCH SQ_BUSY_CYCLES -d $O/pmc2 -o run --output-format csv -- python3 tools/bsw_bench.py --which c3 --reps 1 > $O/pmc2.log 2>&1 || exit 1
+  timeout -k 10 120 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_ACTIVE_INST_VALU SQ_WAIT_INST_ANY SQ_WAIT_ANY SQ_INSTS_VALU SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_SCA SQ_ACTIVE_INST_MISC -d $O/pmc2 -o run --output-format csv -- python3 tools/bsw_bench.py --which c3 --reps 1 > $O/pmc2.log 2>&1 || exit 1
   python3 tools/pmc_kernels.py $O/pmc2 bsw_
   timeout -k 10 120 rocprofv3 --pmc SQC_ICACHE_MISSES SQC_ICACHE_HITS SQC_ICACHE_REQ -d $O/pmc3 -o run --output-format csv -- python3 tools/bsw_bench.py --which c3 --reps 1 > $O/pmc3.log 2>&1 || exit 1
   python3 tools/pmc_kernels.py $O/pmc3 bsw_
