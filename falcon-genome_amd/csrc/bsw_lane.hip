@@ -416,32 +416,97 @@ __device__ __forceinline__ void lane_wave(const BswDevBatch& b, const BswParams&
   }
 }
 
-// One launch per bucket; the grid strides over the bucket's range so empty
-// buckets cost a few hundred idle workgroups, not n/64.
-template <int NC, bool SYM, bool B8>
-__global__ __launch_bounds__(64, B8 ? 3 : 2) void bsw_lane_kernel(const BswDevBatch b, const BswParams p,
-                                                      const int32_t* __restrict__ order,
-                                                      const int64_t* __restrict__ bounds, const int bucket,
-                                                      int32_t* __restrict__ res, int64_t* __restrict__ cells_out) {
-  const long long lo = bounds[bucket], hi = bounds[bucket + 1];
-  __shared__ uint32_t qsel[QG<NC> * 64];  // [group][lane] query selectors
-  __shared__ uint2 mtab[5];               // score table of target base t (s0, s1)
-  if (threadIdx.x < 5) {
-    const int t = threadIdx.x;
-    uint32_t s0 = 0;
-    for (int c = 0; c < 4; ++c) s0 |= (uint32_t)(uint8_t)p.mat[t * 5 + c] << (8 * c);
-    mtab[t] = make_uint2(s0, (uint32_t)(uint8_t)p.mat[t * 5 + 4]);
+}  // namespace fcs
+
+#include "bsw_pair.h"
+
+namespace fcs {
+
+// Wave classes of the single extension launch, in dispatch order: workgroup w
+// takes the w-th wave of the concatenation of these buckets' sorted ranges
+// (64 tasks per lane wave, 128 per pair wave).  Widest columns first, and at
+// equal width the one-task-per-lane waves (the longest per wave) before the
+// pair waves, so the dispatcher packs longest-first (LPT) and short waves fill
+// the tail.  Empty buckets contribute no waves; the grid is an upper bound
+// (n / 64 + one per class), and the surplus workgroups come last and exit at
+// once, in the tail.  One launch instead of one per bucket: concurrent
+// near-empty bucket launches on side streams slowed the pair waves of a bwa
+// batch by 1-5%.
+constexpr int kExtClasses = 15;
+__constant__ const int8_t kExtOrder[kExtClasses] = {
+    9, 6, kBswPairBucket0 + 4,      // 152 columns: byte lane, lane, pair
+    8, 5, kBswPairBucket0 + 3,      // 128
+    7, 4, kBswPairBucket0 + 2,      // 96
+    kBswPairBucket0 + 1, 3, 2,      // 64, 64, 48
+    kBswPairBucket0, 1, 0};         // 32, 32, 16
+
+template <bool SYM>
+__global__ __launch_bounds__(64, 2) void bsw_ext_kernel(const BswDevBatch b, const BswParams p,
+                                                       const int32_t* __restrict__ order,
+                                                       const int64_t* __restrict__ bounds, int32_t* __restrict__ res,
+                                                       int64_t* __restrict__ cells_out) {
+  // pair waves: [chunk][lane] selector uint4s + 5 table dwords; lane waves:
+  // [group][lane] selector dwords + 5 uint2 tables (the same bytes)
+  constexpr int kSel = PCH<152> * 64;
+  static_assert(QG<152> * 64 * 4 <= kSel * 16, "lane selectors fit the pair selector area");
+  __shared__ uint4 smem[kSel + 3];
+  long long t = blockIdx.x;
+  int bucket = -1;
+  long long lo = 0, hi = 0;
+  for (int s = 0; s < kExtClasses; ++s) {
+    const int c = kExtOrder[s];
+    const int per = c >= kBswPairBucket0 ? 128 : 64;
+    const long long blo = bounds[c], bhi = bounds[c + 1];
+    const long long nw = (bhi - blo + per - 1) / per;
+    if (t < nw) {
+      bucket = c, lo = blo + per * t, hi = bhi;
+      break;
+    }
+    t -= nw;
   }
-  __syncthreads();
+  if (bucket < 0) return;
+  const bool pair = bucket >= kBswPairBucket0;
+  if (threadIdx.x < 5) {
+    const int tb = threadIdx.x;
+    if (pair) {
+      uint32_t v = 0;
+      for (int c = 0; c < 4; ++c) v |= (uint32_t)(uint8_t)(p.mat[tb * 5 + c] + p.pair_bias) << (8 * c);
+      reinterpret_cast<uint32_t*>(smem + kSel)[tb] = v;
+    } else {
+      uint32_t s0 = 0;
+      for (int c = 0; c < 4; ++c) s0 |= (uint32_t)(uint8_t)p.mat[tb * 5 + c] << (8 * c);
+      reinterpret_cast<uint2*>(smem + kSel)[tb] = make_uint2(s0, (uint32_t)(uint8_t)p.mat[tb * 5 + 4]);
+    }
+  }
 #ifdef FCS_BSW_STATS
-  if (threadIdx.x < 8) s_bsw_stats[threadIdx.x] = 0;
-  __syncthreads();
+  if (threadIdx.x < 8) s_bsw_stats[threadIdx.x] = 0, s_pair_stats[threadIdx.x] = 0;
 #endif
-  for (long long base = lo + 64LL * blockIdx.x; base < hi; base += 64LL * gridDim.x)
-    lane_wave<NC, SYM, B8>(b, p, order, base, hi, res, cells_out, qsel, reinterpret_cast<const uint32_t*>(mtab));
+  __syncthreads();
+  uint32_t* const qsel = reinterpret_cast<uint32_t*>(smem);
+  const uint32_t* const tab = reinterpret_cast<const uint32_t*>(smem + kSel);
+  switch (bucket) {
+    case kBswPairBucket0 + 4: pair_wave<152, SYM>(b, p, order, lo, hi, res, cells_out, smem, tab); break;
+    case kBswPairBucket0 + 3: pair_wave<128, SYM>(b, p, order, lo, hi, res, cells_out, smem, tab); break;
+    case kBswPairBucket0 + 2: pair_wave<96, SYM>(b, p, order, lo, hi, res, cells_out, smem, tab); break;
+    case kBswPairBucket0 + 1: pair_wave<64, SYM>(b, p, order, lo, hi, res, cells_out, smem, tab); break;
+    case kBswPairBucket0: pair_wave<32, SYM>(b, p, order, lo, hi, res, cells_out, smem, tab); break;
+    case 9: lane_wave<152, SYM, true>(b, p, order, lo, hi, res, cells_out, qsel, tab); break;
+    case 8: lane_wave<128, SYM, true>(b, p, order, lo, hi, res, cells_out, qsel, tab); break;
+    case 7: lane_wave<96, SYM, true>(b, p, order, lo, hi, res, cells_out, qsel, tab); break;
+    case 6: lane_wave<152, SYM, false>(b, p, order, lo, hi, res, cells_out, qsel, tab); break;
+    case 5: lane_wave<128, SYM, false>(b, p, order, lo, hi, res, cells_out, qsel, tab); break;
+    case 4: lane_wave<96, SYM, false>(b, p, order, lo, hi, res, cells_out, qsel, tab); break;
+    case 3: lane_wave<64, SYM, false>(b, p, order, lo, hi, res, cells_out, qsel, tab); break;
+    case 2: lane_wave<48, SYM, false>(b, p, order, lo, hi, res, cells_out, qsel, tab); break;
+    case 1: lane_wave<32, SYM, false>(b, p, order, lo, hi, res, cells_out, qsel, tab); break;
+    default: lane_wave<16, SYM, false>(b, p, order, lo, hi, res, cells_out, qsel, tab); break;
+  }
 #ifdef FCS_BSW_STATS
   __syncthreads();
-  if (threadIdx.x < 8) atomicAdd(&g_bsw_stats[bucket][threadIdx.x], s_bsw_stats[threadIdx.x]);
+  if (threadIdx.x < 8) {
+    if (pair) atomicAdd(&g_pair_stats[bucket - kBswPairBucket0][threadIdx.x], s_pair_stats[threadIdx.x]);
+    else atomicAdd(&g_bsw_stats[bucket][threadIdx.x], s_bsw_stats[threadIdx.x]);
+  }
 #endif
 }
 
@@ -462,7 +527,7 @@ extern "C" int fcs_bsw_stats_read(unsigned long long* out, int reset) {
 // kernels with 96/128/152 columns for tasks whose scores all fit a byte (the
 // register saving buys a third wave per SIMD there; at <= 64 columns the
 // 16-bit layout already runs 3-4 waves and is cheaper per cell);
-// kBswPairBucket0..+4 = two-tasks-per-lane kernels (bsw_pair.hip) with
+// kBswPairBucket0..+4 = two-tasks-per-lane kernels (bsw_pair.h) with
 // 32/64/96/128/152 columns for tasks whose biased scores fit a byte and whose
 // query holds no N (`acgt`), with tlen < 1024 (the pair kernel's 16-bit row
 // bookkeeping); kBswWideBucket = wave-per-task kernel
@@ -548,42 +613,16 @@ int launch_bsw_extend_sorted(const BswDevBatch& b, const BswParams& p, int max_q
   hipLaunchKernelGGL(bsw_bounds_kernel, dim3((unsigned)((b.n + 1 + bs - 1) / bs)), dim3(bs), 0, s, ws.keys_out,
                      (long long)b.n, ws.bounds);
   FCS_HIP_CHECK(hipGetLastError());
-  // 8192 workgroups = 4 rounds of the 2048 resident waves (2 per SIMD): caps
-  // the cost of an empty bucket and still leaves the dispatcher a tail to balance
-  const unsigned g = (unsigned)std::min<long long>((b.n + 63) / 64, 8192);
-  const bool sym = p.o_del == p.o_ins && p.e_del == p.e_ins;
-  // The eight bucket kernels are independent (disjoint task ranges).  A bwa
-  // batch spreads over all of them, so each alone is ~one round of waves and
-  // its tail would idle the chip: fork them over kForkStreams streams,
-  // largest columns first, so small buckets fill the large ones' tails.
-  hipStream_t fs[kForkStreams];
-  if (const int rc = fork_streams(s, fs); rc != FCS_OK) return rc;
-  auto lanes = [&](auto sym_tag) {
-    constexpr bool SYM = decltype(sym_tag)::value;
-    auto go = [&](auto kern, hipStream_t st, int bucket) {
-      hipLaunchKernelGGL(kern, dim3(g), dim3(64), 0, st, b, p, ws.idx_out, ws.bounds, bucket, res, cells);
-    };
-    // widest first, so the small buckets fill the large ones' tails
-    go(bsw_lane_kernel<152, SYM, true>, fs[0], 9);
-    go(bsw_lane_kernel<128, SYM, true>, fs[1], 8);
-    go(bsw_lane_kernel<96, SYM, true>, fs[2], 7);
-    go(bsw_lane_kernel<152, SYM, false>, fs[3], 6);
-    go(bsw_lane_kernel<128, SYM, false>, fs[0], 5);
-    go(bsw_lane_kernel<96, SYM, false>, fs[1], 4);
-    go(bsw_lane_kernel<64, SYM, false>, fs[2], 3);
-    go(bsw_lane_kernel<48, SYM, false>, fs[3], 2);
-    go(bsw_lane_kernel<32, SYM, false>, fs[2], 1);
-    go(bsw_lane_kernel<16, SYM, false>, fs[1], 0);
-  };
-  // two-tasks-per-lane kernels first: they carry the bwa-typical tasks
-  if (const int rc = launch_bsw_pair(b, p, res, cells, ws.idx_out, ws.bounds, fs[0]); rc != FCS_OK) return rc;
-  if (sym) lanes(std::true_type{});
-  else lanes(std::false_type{});
+  // one launch for every pair and lane bucket (an upper bound of their waves)
+  const unsigned grid = (unsigned)((b.n + 63) / 64 + kExtClasses);
+  if (p.o_del == p.o_ins && p.e_del == p.e_ins)
+    hipLaunchKernelGGL(bsw_ext_kernel<true>, dim3(grid), dim3(64), 0, s, b, p, ws.idx_out, ws.bounds, res, cells);
+  else
+    hipLaunchKernelGGL(bsw_ext_kernel<false>, dim3(grid), dim3(64), 0, s, b, p, ws.idx_out, ws.bounds, res, cells);
   FCS_HIP_CHECK(hipGetLastError());
-  // wave-per-task kernel over the sorted tail
-  const int rc = launch_bsw_extend_wide(b, p, max_qlen, max_tlen, res, cells, ws.idx_out, ws.bounds, fs[0]);
-  if (rc != FCS_OK) return rc;
-  return join_streams(s, fs);
+  // wave-per-task kernel over the sorted tail (empty in bwa batches: its grid
+  // of exits runs after the extension launch, not beside it)
+  return launch_bsw_extend_wide(b, p, max_qlen, max_tlen, res, cells, ws.idx_out, ws.bounds, s);
 }
 
 }  // namespace fcs

@@ -36,6 +36,9 @@
 //    e' at j == end (bwa stores {h1, 0}), entries beyond `end` keep their
 //    stale values (bwa re-reads them when the band grows), and h1 at `end` is
 //    captured for the to-end score.
+// Device code only: included by bsw_lane.hip, whose single extension launch
+// (bsw_ext_kernel) runs pair waves and lane waves side by side.
+#pragma once
 #include <hip/hip_runtime.h>
 
 #include <utility>
@@ -533,68 +536,5 @@ __device__ __forceinline__ void pair_wave(const BswDevBatch& b, const BswParams&
 }
 
 }  // namespace
-
-// All five pair buckets in ONE launch, one 128-task wave per workgroup, in
-// longest-first order: workgroup w takes the w-th wave of the concatenation
-// [152 | 128 | 96 | 64 | 32 columns] (each bucket already sorted longest
-// first).  The dispatcher hands out workgroups in order, so the long waves
-// start first and the short ones fill the tail (LPT packing); separate
-// per-bucket launches over streams left ~1/3 of the wave slots idle at the
-// end of a C3 batch.  Registers / LDS are sized for the widest path (2 waves
-// per SIMD for every bucket).
-template <bool SYM>
-__global__ __launch_bounds__(64, 2) void bsw_pair_kernel(const BswDevBatch b, const BswParams p,
-                                                         const int32_t* __restrict__ order,
-                                                         const int64_t* __restrict__ bounds,
-                                                         int32_t* __restrict__ res, int64_t* __restrict__ cells_out) {
-  __shared__ uint4 qsel[PCH<152> * 64];  // [chunk][lane] selector dwords
-  __shared__ uint32_t ptab[5];           // biased scores mat[t][0..3] + bias, t = A, C, G, T, N
-  long long t = blockIdx.x;
-  int slot = -1;
-  long long lo = 0, hi = 0;
-  for (int s = 4; s >= 0; --s) {  // widest bucket first
-    const long long blo = bounds[kBswPairBucket0 + s], bhi = bounds[kBswPairBucket0 + s + 1];
-    const long long nw = (bhi - blo + 127) / 128;
-    if (t < nw) {
-      slot = s, lo = blo + 128 * t, hi = bhi;
-      break;
-    }
-    t -= nw;
-  }
-  if (slot < 0) return;
-  if (threadIdx.x < 5) {
-    const int tb = threadIdx.x;
-    uint32_t v = 0;
-    for (int c = 0; c < 4; ++c) v |= (uint32_t)(uint8_t)(p.mat[tb * 5 + c] + p.pair_bias) << (8 * c);
-    ptab[tb] = v;
-  }
-#ifdef FCS_BSW_STATS
-  if (threadIdx.x < 8) s_pair_stats[threadIdx.x] = 0;
-#endif
-  __syncthreads();
-  switch (slot) {
-    case 4: pair_wave<152, SYM>(b, p, order, lo, hi, res, cells_out, qsel, ptab); break;
-    case 3: pair_wave<128, SYM>(b, p, order, lo, hi, res, cells_out, qsel, ptab); break;
-    case 2: pair_wave<96, SYM>(b, p, order, lo, hi, res, cells_out, qsel, ptab); break;
-    case 1: pair_wave<64, SYM>(b, p, order, lo, hi, res, cells_out, qsel, ptab); break;
-    default: pair_wave<32, SYM>(b, p, order, lo, hi, res, cells_out, qsel, ptab); break;
-  }
-#ifdef FCS_BSW_STATS
-  __syncthreads();
-  if (threadIdx.x < 8) atomicAdd(&g_pair_stats[slot][threadIdx.x], s_pair_stats[threadIdx.x]);
-#endif
-}
-
-int launch_bsw_pair(const BswDevBatch& b, const BswParams& p, int32_t* res, int64_t* cells, const int32_t* order,
-                    const int64_t* bounds, hipStream_t s) {
-  // upper bound of the waves over the five buckets; the rest exit at once
-  const unsigned grid = (unsigned)((b.n + 127) / 128 + 5);
-  if (p.o_del == p.o_ins && p.e_del == p.e_ins)
-    hipLaunchKernelGGL(bsw_pair_kernel<true>, dim3(grid), dim3(64), 0, s, b, p, order, bounds, res, cells);
-  else
-    hipLaunchKernelGGL(bsw_pair_kernel<false>, dim3(grid), dim3(64), 0, s, b, p, order, bounds, res, cells);
-  FCS_HIP_CHECK(hipGetLastError());
-  return FCS_OK;
-}
 
 }  // namespace fcs

@@ -154,14 +154,14 @@ struct BswParams {
   int32_t max_mat;
   int32_t matpack[5];  // row t: mat[t*5+q] as signed 5-bit fields at bit 5*q
   int32_t lane_ok;     // every mat entry fits a signed 5-bit field
-  // two-tasks-per-lane kernel (bsw_pair.hip): A/C/G/T scores biased to >= 0
+  // two-tasks-per-lane kernel (bsw_pair.h): A/C/G/T scores biased to >= 0
   int32_t pair_ok;     // the biased A/C/G/T block fits a byte
   int32_t pair_bias;   // -min(0, min mat[t][q]), t < 5, q < 4
   int32_t pair_cg;     // max mat[t][q] (t < 5, q < 4) + pair_bias + 1
-  int32_t pair_k256, pair_one;  // 0x01000100, 0x00010001: runtime constants (see bsw_pair.hip pk_mad / pk_nz)
+  int32_t pair_k256, pair_one;  // 0x01000100, 0x00010001: runtime constants (see bsw_pair.h pk_mad / pk_nz)
 };
 // SW schedule buckets: 0..9 lane-per-task kernels (bsw_lane.hip), 10..14
-// two-tasks-per-lane kernels (bsw_pair.hip), 15 = wave-per-task.
+// two-tasks-per-lane kernels (bsw_pair.h), 15 = wave-per-task.
 constexpr int kBswPairBucket0 = 10;
 constexpr int kBswWideBucket = 15;
 // Device scratch of one SW launch sequence (sort keys, schedule, bucket bounds).
@@ -177,12 +177,10 @@ struct BswWorkspace {
 };
 hipError_t hipcub_sort_pairs(void* tmp, size_t& bytes, const uint32_t* kin, uint32_t* kout, const int32_t* vin,
                              int32_t* vout, int n, hipStream_t s);
-// Sorted schedule: lane-per-task kernels for buckets 0..6, wave-per-task for 7.
+// Sorted schedule: one launch over the lane (0..9) and pair (kBswPairBucket0..+4)
+// buckets, then the wave-per-task kernel over kBswWideBucket.
 int launch_bsw_extend_sorted(const BswDevBatch& b, const BswParams& p, int max_qlen, int max_tlen, int32_t* res,
                              int64_t* cells, const BswWorkspace& ws, hipStream_t s);
-// Pair kernel over buckets kBswPairBucket0..+4 (one launch, longest waves first).
-int launch_bsw_pair(const BswDevBatch& b, const BswParams& p, int32_t* res, int64_t* cells, const int32_t* order,
-                    const int64_t* bounds, hipStream_t s);
 // Wave-per-task kernel over sorted positions [bounds[kBswWideBucket], bounds[kBswWideBucket + 1]).
 int launch_bsw_extend_wide(const BswDevBatch& b, const BswParams& p, int max_qlen, int max_tlen, int32_t* res,
                            int64_t* cells, const int32_t* order, const int64_t* bounds, hipStream_t s);
