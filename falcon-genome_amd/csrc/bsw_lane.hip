@@ -587,8 +587,11 @@ __global__ void bsw_keys_kernel(const BswDevBatch b, const BswParams p, uint32_t
                                                  ((long long)h0 + (long long)qlen * p.max_mat) / max(p.e_del, 1) + 1);
   // longest first inside a bucket (the sort is ascending): the last waves of a
   // launch are the short ones, so the launch's tail is short
-  keys[k] = (bk << 28) | ((1023u - (uint32_t)min(max(qlen, 0), 1023)) << 18) |
-            (262143u - (uint32_t)min(max(est, 0LL), 262143LL));
+  // 24-bit key (three 8-bit radix passes): bucket | 255 - qlen | 4095 - est.
+  // The clamps only touch wave-per-task tasks (pair and lane tasks have
+  // qlen <= 151, and pair tasks tlen < 1024); they change order, never results.
+  keys[k] = (bk << kBswKeyBucketShift) | ((255u - (uint32_t)min(max(qlen, 0), 255)) << 12) |
+            (4095u - (uint32_t)min(max(est, 0LL), 4095LL));
   idx[k] = (int32_t)k;
 }
 
@@ -596,8 +599,8 @@ __global__ void bsw_keys_kernel(const BswDevBatch b, const BswParams p, uint32_t
 __global__ void bsw_bounds_kernel(const uint32_t* __restrict__ keys, long long n, int64_t* __restrict__ bounds) {
   const long long k = (long long)blockIdx.x * blockDim.x + threadIdx.x;
   if (k > n) return;
-  const int cur = (k < n) ? (int)(keys[k] >> 28) : kBswWideBucket + 1;
-  const int prev = (k > 0) ? (int)(keys[k - 1] >> 28) : -1;
+  const int cur = (k < n) ? (int)(keys[k] >> kBswKeyBucketShift) : kBswWideBucket + 1;
+  const int prev = (k > 0) ? (int)(keys[k - 1] >> kBswKeyBucketShift) : -1;
   for (int c = prev + 1; c <= cur; ++c) bounds[c] = k;
 }
 
@@ -609,7 +612,7 @@ int launch_bsw_extend_sorted(const BswDevBatch& b, const BswParams& p, int max_q
   hipLaunchKernelGGL(bsw_keys_kernel, dim3((unsigned)((b.n + bs - 1) / bs)), dim3(bs), 0, s, b, p, ws.keys_in, ws.idx_in);
   FCS_HIP_CHECK(hipGetLastError());
   size_t tmp = ws.tmp_bytes;
-  FCS_HIP_CHECK(hipcub_sort_pairs(ws.tmp, tmp, ws.keys_in, ws.keys_out, ws.idx_in, ws.idx_out, (int)b.n, s));
+  FCS_HIP_CHECK(sort_pairs_u32(ws.tmp, tmp, ws.keys_in, ws.keys_out, ws.idx_in, ws.idx_out, (int)b.n, s, kBswKeyBits));
   hipLaunchKernelGGL(bsw_bounds_kernel, dim3((unsigned)((b.n + 1 + bs - 1) / bs)), dim3(bs), 0, s, ws.keys_out,
                      (long long)b.n, ws.bounds);
   FCS_HIP_CHECK(hipGetLastError());

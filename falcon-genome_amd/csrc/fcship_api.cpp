@@ -6,7 +6,7 @@
 // prefix LogUtils::findError scans task logs for,
 // /root/reference/src/LogUtils.cpp:10-40) retrievable with fcs_last_error().
 #include <hip/hip_runtime.h>
-#include <hipcub/hipcub.hpp>
+#include <rocprim/device/device_radix_sort.hpp>
 
 #include <algorithm>
 #include <cstdlib>
@@ -164,7 +164,7 @@ int ws_alloc(BswWorkspace& ws, int64_t cap, hipStream_t s, bool stream_alloc) {
   ws.cap = cap;
   const size_t n = (size_t)std::max<int64_t>(cap, 1);
   size_t tmp = 0;
-  FCS_HIP_CHECK(hipcub_sort_pairs(nullptr, tmp, nullptr, nullptr, nullptr, nullptr, (int)n, s));
+  FCS_HIP_CHECK(sort_pairs_u32(nullptr, tmp, nullptr, nullptr, nullptr, nullptr, (int)n, s));
   ws.tmp_bytes = std::max<size_t>(tmp, 16);
   void** bufs[6] = {(void**)&ws.keys_in, (void**)&ws.keys_out, (void**)&ws.idx_in, (void**)&ws.idx_out,
                     (void**)&ws.bounds, &ws.tmp};
@@ -192,9 +192,15 @@ int check_params(const fcs_bsw_params* p) {
 
 }  // namespace
 
-hipError_t hipcub_sort_pairs(void* tmp, size_t& bytes, const uint32_t* kin, uint32_t* kout, const int32_t* vin,
-                             int32_t* vout, int n, hipStream_t s) {
-  return hipcub::DeviceRadixSort::SortPairs(tmp, bytes, kin, kout, vin, vout, n, 0, 32, s);
+// Stable LSD radix sort of (32-bit key, index) pairs.  rocPRIM's default picks
+// a block sort + ~20 merge passes for n <= 2^20 (the C2 / C3 batch sizes:
+// 0.16 ms of 7 us launches); a merge-sort limit of 0 forces its onesweep path
+// (histogram + one pass per 8-bit digit) at every size.  Same order either way.
+using SortConfig = rocprim::radix_sort_config<rocprim::default_config, rocprim::default_config,
+                                              rocprim::default_config, 0>;
+hipError_t sort_pairs_u32(void* tmp, size_t& bytes, const uint32_t* kin, uint32_t* kout, const int32_t* vin,
+                          int32_t* vout, int n, hipStream_t s, int end_bit) {
+  return rocprim::radix_sort_pairs<SortConfig>(tmp, bytes, kin, kout, vin, vout, (size_t)n, 0, (unsigned)end_bit, s);
 }
 
 int get_device_tables(int device, DeviceTables** out) {
@@ -343,8 +349,7 @@ int fcs_phmm_plan_create(int32_t device, int64_t max_pairs, fcs_phmm_plan** plan
   FCS_HIP_CHECK(hipMemset(p->rescue_count, 0, 8 * sizeof(unsigned long long)));
   p->bounds = reinterpret_cast<int64_t*>(p->rescue_count + 1);
   size_t tmp = 0;
-  FCS_HIP_CHECK(hipcub::DeviceRadixSort::SortPairs(nullptr, tmp, p->keys_in, p->keys_out, p->idx_in, p->idx_out,
-                                                    (int)n, 0, 32));
+  FCS_HIP_CHECK(sort_pairs_u32(nullptr, tmp, p->keys_in, p->keys_out, p->idx_in, p->idx_out, (int)n, nullptr));
   p->sort_tmp_bytes = std::max<size_t>(tmp, 16);
   FCS_HIP_CHECK(hipMalloc(&p->sort_tmp, p->sort_tmp_bytes));
   *plan = p.release();
@@ -377,8 +382,8 @@ int fcs_phmm_dev_schedule(fcs_phmm_plan* plan, const fcs_phmm_batch* b, void* st
   if (rc) return rc;
   if (b->n_pairs > 0) {
     size_t tmp = plan->sort_tmp_bytes;
-    FCS_HIP_CHECK(hipcub::DeviceRadixSort::SortPairs(plan->sort_tmp, tmp, plan->keys_in, plan->keys_out,
-                                                      plan->idx_in, plan->idx_out, (int)b->n_pairs, 0, 32, s));
+    FCS_HIP_CHECK(sort_pairs_u32(plan->sort_tmp, tmp, plan->keys_in, plan->keys_out, plan->idx_in, plan->idx_out,
+                                 (int)b->n_pairs, s));
   }
   if ((rc = launch_phmm_bounds(plan->keys_out, b->n_pairs, plan->bounds, s))) return rc;
   plan->scheduled = b->n_pairs;

@@ -175,8 +175,12 @@ struct BswWorkspace {
   void* tmp = nullptr;
   size_t tmp_bytes = 0;
 };
-hipError_t hipcub_sort_pairs(void* tmp, size_t& bytes, const uint32_t* kin, uint32_t* kout, const int32_t* vin,
-                             int32_t* vout, int n, hipStream_t s);
+// Stable radix sort of (key, index) pairs over key bits [0, end_bit).
+hipError_t sort_pairs_u32(void* tmp, size_t& bytes, const uint32_t* kin, uint32_t* kout, const int32_t* vin,
+                          int32_t* vout, int n, hipStream_t s, int end_bit = 32);
+// SW schedule keys: bucket in bits [20, 24), below it the in-bucket order.
+constexpr int kBswKeyBucketShift = 20;
+constexpr int kBswKeyBits = 24;
 // Sorted schedule: one launch over the lane (0..9) and pair (kBswPairBucket0..+4)
 // buckets, then the wave-per-task kernel over kBswWideBucket.
 int launch_bsw_extend_sorted(const BswDevBatch& b, const BswParams& p, int max_qlen, int max_tlen, int32_t* res,
