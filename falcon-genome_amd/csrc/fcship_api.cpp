@@ -383,7 +383,7 @@ int fcs_phmm_dev_schedule(fcs_phmm_plan* plan, const fcs_phmm_batch* b, void* st
   if (b->n_pairs > 0) {
     size_t tmp = plan->sort_tmp_bytes;
     FCS_HIP_CHECK(sort_pairs_u32(plan->sort_tmp, tmp, plan->keys_in, plan->keys_out, plan->idx_in, plan->idx_out,
-                                 (int)b->n_pairs, s));
+                                 (int)b->n_pairs, s, kPhmmKeyBits));
   }
   if ((rc = launch_phmm_bounds(plan->keys_out, b->n_pairs, plan->bounds, s))) return rc;
   plan->scheduled = b->n_pairs;

@@ -181,6 +181,9 @@ hipError_t sort_pairs_u32(void* tmp, size_t& bytes, const uint32_t* kin, uint32_
 // SW schedule keys: bucket in bits [20, 24), below it the in-bucket order.
 constexpr int kBswKeyBucketShift = 20;
 constexpr int kBswKeyBits = 24;
+// PairHMM schedule keys: hap-length class in bits [21, 24).
+constexpr int kPhmmKeyClassShift = 21;
+constexpr int kPhmmKeyBits = 24;
 // Sorted schedule: one launch over the lane (0..9) and pair (kBswPairBucket0..+4)
 // buckets, then the wave-per-task kernel over kBswWideBucket.
 int launch_bsw_extend_sorted(const BswDevBatch& b, const BswParams& p, int max_qlen, int max_tlen, int32_t* res,

@@ -371,6 +371,7 @@ static __host__ __device__ int nslot_for(int max_hap_len) { return ((max_hap_len
 // class, so short haplotypes run at 4 waves per SIMD instead of the 3 that the
 // longest haplotype of the batch would allow.
 constexpr int kPhmmClasses = 6;
+static_assert(kPhmmClasses <= 8 && kPhmmKeyClassShift + 3 <= kPhmmKeyBits, "class fits the key");
 __host__ __device__ inline int phmm_class(int H) {
   const int c = (nslot_for(H) - 224 + 31) / 32;
   return c < 0 ? 0 : c > kPhmmClasses - 1 ? kPhmmClasses - 1 : c;
@@ -383,10 +384,13 @@ __global__ void phmm_keys_kernel(const PhmmDevBatch b, uint32_t* __restrict__ ke
   if (p >= b.n_pairs) return;
   const int R = b.read_len[b.pair_read[p]];
   const int H = b.hap_len[b.pair_hap[p]];
-  const uint32_t ns = (uint32_t)min((R + 15) >> 4, 0xFFF);
-  const uint32_t hh = (uint32_t)min(max(H, 0), 0xFFFF);
+  // 24 bits (three 8-bit radix passes): class | 255 - stripes | 8191 - H.  The
+  // clamps (R > 4080, H > 8191) only change the order, never results: a wave
+  // runs its pairs' own shapes (wave max of stripes and H).
+  const uint32_t ns = (uint32_t)min((R + 15) >> 4, 0xFF);
+  const uint32_t hh = (uint32_t)min(max(H, 0), 0x1FFF);
   const uint32_t rc = (uint32_t)(kPhmmClasses - 1 - phmm_class(max(H, 0)));
-  keys[p] = (rc << 28) | ((0xFFFu - ns) << 16) | (0xFFFFu - hh);
+  keys[p] = (rc << kPhmmKeyClassShift) | ((0xFFu - ns) << 13) | (0x1FFFu - hh);
   idx[p] = (int32_t)p;
 }
 
@@ -394,8 +398,8 @@ __global__ void phmm_keys_kernel(const PhmmDevBatch b, uint32_t* __restrict__ ke
 __global__ void phmm_bounds_kernel(const uint32_t* __restrict__ keys, long long n, int64_t* __restrict__ bounds) {
   const long long k = (long long)blockIdx.x * blockDim.x + threadIdx.x;
   if (k > n) return;
-  const int cur = (k < n) ? (int)(keys[k] >> 28) : kPhmmClasses;
-  const int prev = (k > 0) ? (int)(keys[k - 1] >> 28) : -1;
+  const int cur = (k < n) ? (int)(keys[k] >> kPhmmKeyClassShift) : kPhmmClasses;
+  const int prev = (k > 0) ? (int)(keys[k - 1] >> kPhmmKeyClassShift) : -1;
   for (int j = prev + 1; j <= cur; ++j) bounds[j] = k;
 }
 
