@@ -31,6 +31,10 @@ for step in "$@"; do
             python3 "$ROOT/bench.py" --steps 1 --warmup 0 --no-cpu-baseline --no-bsw --no-e2e &&
          run pmc2 900 rocprofv3 --pmc WRITE_SIZE -d "$OUT/pmc_write" -o run --output-format csv -- \
             python3 "$ROOT/bench.py" --steps 1 --warmup 0 --no-cpu-baseline --no-bsw --no-e2e ;;
+    bswpmc) run bswpmc_c3 300 rocprofv3 --pmc SQ_INSTS_VALU -d "$OUT/bswpmc_c3" -o run --output-format csv -- \
+            python3 "$ROOT/tools/bsw_bench.py" --which c3 --reps 1 &&
+            run bswpmc_fixed 300 rocprofv3 --pmc SQ_INSTS_VALU -d "$OUT/bswpmc_fixed" -o run --output-format csv -- \
+            python3 "$ROOT/tools/bsw_bench.py" --which fixed --reps 1 ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac
 done
