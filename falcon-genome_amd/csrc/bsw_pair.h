@@ -338,20 +338,40 @@ __device__ __forceinline__ void pair_wave(const BswDevBatch& b, const BswParams&
   task_load(A, b, p, order, base + 2 * lane, hi);
   task_load(B, b, p, order, base + 2 * lane + 1, hi);
 
-  // selector dwords [qA_j, qA_j+1, 4 + qB_j, 4 + qB_j+1], four per chunk
+  // selector dwords [qA_j, qA_j+1, 4 + qB_j, 4 + qB_j+1], four per chunk.
+  // Each query is read as the aligned dwords that cover it (every load issued
+  // before any use: one memory round trip per wave instead of one per chunk),
+  // realigned to column 0 by v_alignbyte, and cut at qlen (columns past qlen
+  // read as code 0, as bwa never scores them).
   uint4* __restrict__ qs = qsel + lane;
   {
+    constexpr int NQ = PCH<NC> * 2;  // query words: 4 columns each
     const uint8_t* qa = A.done ? b.qbuf : b.qbuf + b.qoff[A.id];
     const uint8_t* qb = B.done ? b.qbuf : b.qbuf + b.qoff[B.id];
+    const uint32_t* wa = reinterpret_cast<const uint32_t*>((uintptr_t)qa & ~(uintptr_t)3);
+    const uint32_t* wb = reinterpret_cast<const uint32_t*>((uintptr_t)qb & ~(uintptr_t)3);
+    const int oa = (int)((uintptr_t)qa & 3), ob = (int)((uintptr_t)qb & 3);
+    uint32_t WA[NQ + 1], WB[NQ + 1];
+#pragma unroll
+    for (int w = 0; w <= NQ; ++w) {
+      // aligned dwords holding some query byte (they lie inside the hipMalloc'd buffer)
+      WA[w] = 4 * w < oa + A.qlen ? wa[w] : 0u;
+      WB[w] = 4 * w < ob + B.qlen ? wb[w] : 0u;
+    }
+    auto cut = [](uint32_t v, int rem) __attribute__((always_inline)) {  // bytes >= rem zeroed
+      return rem >= 4 ? v : rem <= 0 ? 0u : v & ((1u << (8 * rem)) - 1u);
+    };
 #pragma unroll
     for (int c = 0; c < PCH<NC>; ++c) {
       uint32_t v[4];
 #pragma unroll
-      for (int g = 0; g < 4; ++g) {
-        const int j = kPW * c + 2 * g;
-        const uint32_t a0 = j < A.qlen ? qa[j] & 3u : 0u, a1 = j + 1 < A.qlen ? qa[j + 1] & 3u : 0u;
-        const uint32_t b0 = j < B.qlen ? qb[j] & 3u : 0u, b1 = j + 1 < B.qlen ? qb[j + 1] & 3u : 0u;
-        v[g] = a0 | (a1 << 8) | ((4u + b0) << 16) | ((4u + b1) << 24);
+      for (int h = 0; h < 2; ++h) {
+        const int w = 2 * c + h;
+        const uint32_t qa4 = cut(__builtin_amdgcn_alignbyte(WA[w + 1], WA[w], (uint32_t)oa), A.qlen - 4 * w);
+        const uint32_t qb4 = cut(__builtin_amdgcn_alignbyte(WB[w + 1], WB[w], (uint32_t)ob), B.qlen - 4 * w);
+        // columns 4w, 4w+1 and 4w+2, 4w+3: [qA_j, qA_j+1, qB_j, qB_j+1] & 3, B + 4
+        v[2 * h] = (__builtin_amdgcn_perm(qb4, qa4, 0x05040100u) & 0x03030303u) | 0x04040000u;
+        v[2 * h + 1] = (__builtin_amdgcn_perm(qb4, qa4, 0x07060302u) & 0x03030303u) | 0x04040000u;
       }
       qs[64 * c] = make_uint4(v[0], v[1], v[2], v[3]);
     }
@@ -388,6 +408,9 @@ __device__ __forceinline__ void pair_wave(const BswDevBatch& b, const BswParams&
   const uint8_t* __restrict__ tgB = B.tg;
   const int tlenA = A.tlen, tlenB = B.tlen;
   uint32_t TB = (uint32_t)A.tcur | ((uint32_t)A.tnext << 8) | ((uint32_t)B.tcur << 16) | ((uint32_t)B.tnext << 24);
+  // target bytes of row i + 2, loaded during row i - 1: a whole row of cells
+  // hides the load (loaded and used in the same row, it stalled every row: +4%)
+  uint32_t PND = (tlenA > 2 ? (uint32_t)tgA[2] : 0u) | ((tlenB > 2 ? (uint32_t)tgB[2] : 0u) << 8);
   const uint32_t ONE = k.one, ED1 = (uint32_t)p.e_del * 0x10001u, EI1 = (uint32_t)p.e_ins * 0x10001u;
   const uint32_t ZD2 = (uint32_t)min(p.zdrop, 32767) * 0x10001u;
 
@@ -397,10 +420,11 @@ __device__ __forceinline__ void pair_wave(const BswDevBatch& b, const BswParams&
     const uint32_t ALIVE = ~S.DONE & pk_lt(I2, S.TLEN);
     if (__ballot(ALIVE != 0u) == 0ull) break;
     const uint32_t tA = TB & 0xFFu, tB = (TB >> 16) & 0xFFu;
+    TB = ((TB >> 8) & 0x00FF00FFu) | ((PND & 0xFFu) << 8) | ((PND >> 8) << 24);
     {
-      const uint32_t nA = ((ALIVE & 0xFFFFu) && i + 2 < tlenA) ? tgA[i + 2] : 0u;
-      const uint32_t nB = ((ALIVE >> 16) && i + 2 < tlenB) ? tgB[i + 2] : 0u;
-      TB = ((TB >> 8) & 0x00FF00FFu) | (nA << 8) | (nB << 24);
+      const uint32_t nA = ((ALIVE & 0xFFFFu) && i + 3 < tlenA) ? tgA[i + 3] : 0u;
+      const uint32_t nB = ((ALIVE >> 16) && i + 3 < tlenB) ? tgB[i + 3] : 0u;
+      PND = nA | (nB << 8);
     }
     // bwa's band: beg = max(beg, i - w), end = min(end, i + w + 1, qlen)
     S.BEG = s_max(S.BEG, s_sub(I2, S.W));
