@@ -293,17 +293,31 @@ __global__ __launch_bounds__(64, (sizeof(T) == 4 && !EXACT) ? 4 : 1) void phmm_k
     // bit-select prior.  A hap byte outside A/C/G/T/N anywhere in the wave's
     // pairs switches the group to raw bytes and GKL's byte compare (read
     // bytes outside the set are exact on the code path: they match only N).
+    // Eight slots per lane per batch: all eight byte loads are issued before
+    // any is used, so a haplotype costs ~3 memory round trips, not one per slot.
     bool other = false;
-    for (int s = sl; s < nslot; s += 16) {
-      const int c = s - 16;
-      PhRing<T> v;
-      v.X = (c >= 0 && c <= H) ? x0 : (T)0;
-      v.I = 0;
-      ring[s] = v;
-      const bool in = active && c >= 1 && c <= H;
-      const unsigned char code = in ? base_code(b.hb[ho + c - 1]) : (unsigned char)6;
-      other |= code == 5;
-      hapl[s] = code;
+    constexpr int kHB = 8;
+    for (int s0 = sl; s0 < nslot; s0 += 16 * kHB) {
+      unsigned char raw[kHB];
+#pragma unroll
+      for (int u = 0; u < kHB; ++u) {
+        const int c = s0 + 16 * u - 16;
+        raw[u] = (active && c >= 1 && c <= H && c + 16 < nslot) ? b.hb[ho + c - 1] : (unsigned char)0;
+      }
+#pragma unroll
+      for (int u = 0; u < kHB; ++u) {
+        const int s = s0 + 16 * u, c = s - 16;
+        if (s < nslot) {
+          PhRing<T> v;
+          v.X = (c >= 0 && c <= H) ? x0 : (T)0;
+          v.I = 0;
+          ring[s] = v;
+          const bool in = active && c >= 1 && c <= H;
+          const unsigned char code = in ? base_code(raw[u]) : (unsigned char)6;
+          other |= code == 5;
+          hapl[s] = code;
+        }
+      }
     }
     const bool bytecmp = __ballot(other) != 0ull;
     if (bytecmp)
