@@ -586,12 +586,19 @@ __global__ void bsw_keys_kernel(const BswDevBatch b, const BswParams p, uint32_t
   const long long est = min((long long)tlen, (long long)qlen +
                                                  ((long long)h0 + (long long)qlen * p.max_mat) / max(p.e_del, 1) + 1);
   // longest first inside a bucket (the sort is ascending): the last waves of a
-  // launch are the short ones, so the launch's tail is short
-  // 24-bit key (three 8-bit radix passes): bucket | 255 - qlen | 4095 - est.
-  // The clamps only touch wave-per-task tasks (pair and lane tasks have
-  // qlen <= 151, and pair tasks tlen < 1024); they change order, never results.
-  keys[k] = (bk << kBswKeyBucketShift) | ((255u - (uint32_t)min(max(qlen, 0), 255)) << 12) |
-            (4095u - (uint32_t)min(max(est, 0LL), 4095LL));
+  // launch are the short ones, so the launch's tail is short.  24-bit key (three
+  // 8-bit radix passes): bucket | qlen / 4 | h0 | rows beyond qlen / 4, each
+  // descending.  h0 right after the (coarse) query length groups tasks whose
+  // band of nonzero cells grows alike (its width follows the running score),
+  // so a wave's band union wastes fewer lane-columns: C3 +4% over ordering by
+  // exact qlen then rows (gpurun_out/k1, k2).  The clamps only touch
+  // wave-per-task tasks; the order never changes results.
+  {
+    const uint32_t q = 63u - (uint32_t)(min(max(qlen, 0), 255) >> 2);
+    const uint32_t h = 255u - (uint32_t)min(max(h0, 0), 255);
+    const uint32_t e = 63u - (uint32_t)(min(max(est - (long long)qlen, 0LL), 255LL) >> 2);
+    keys[k] = (bk << kBswKeyBucketShift) | (q << 14) | (h << 6) | e;
+  }
   idx[k] = (int32_t)k;
 }
 
