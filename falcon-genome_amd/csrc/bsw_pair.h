@@ -441,6 +441,14 @@ __device__ __forceinline__ void pair_wave(const BswDevBatch& b, const BswParams&
     const int cmax = wave_max(max(workA ? endA : -1, workB ? endB : -1));
     const int emin = -wave_max(-min(workA ? endA : (1 << 20), workB ? endB : (1 << 20)));
     PAIR_STAT(1, 1);
+#ifdef FCS_BSW_STATS
+    {  // task-rows of the wave that still work / are alive in this row
+      int wk = (int)(WORK & 1u) + (int)((WORK >> 16) & 1u), al = (int)(ALIVE & 1u) + (int)((ALIVE >> 16) & 1u);
+      for (int o = 32; o > 0; o >>= 1) wk += __shfl_xor(wk, o), al += __shfl_xor(al, o);
+      PAIR_STAT(5, wk);
+      PAIR_STAT(6, al);
+    }
+#endif
     PAIR_STAT(7, cmax >= cmin ? cmax - cmin + 1 : 0);
     r.tabA = ptab[min(tA, 4u)];
     r.tabB = ptab[min(tB, 4u)];
