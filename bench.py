@@ -317,7 +317,7 @@ def main():
                      "traffic": traffic,
                      "kernel": "phmm_kernel<float,false,false>: fp32 forward pass = one launch per hap-length "
                                "class, overlapped on 4 streams; achieved = algorithmic FLOPs / pass time (HIP events "
-                               "on the launch stream; rocprof pass span in profiles/r1/r1h_phmm_summary.json)",
+                               "on the launch stream; rocprof pass span in profiles/r1/r1j_phmm_summary.json)",
                      "valu_instr_per_cell": 12.0,
                      "valu_issue_frac": round(ph["cells"] / fwd_s * 12.0 / VALU_LANE_INSTR_PEAK, 4),
                      "kernel_gcups": round(ph["cells"] / fwd_s / 1e9, 3),
