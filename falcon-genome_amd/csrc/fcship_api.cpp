@@ -346,7 +346,13 @@ int fcs_phmm_plan_create(int32_t device, int64_t max_pairs, fcs_phmm_plan** plan
   FCS_HIP_CHECK(hipMalloc(&p->idx_out, n * 4));
   FCS_HIP_CHECK(hipMalloc(&p->rescue_list, n * 4));
   FCS_HIP_CHECK(hipMalloc(&p->rescue_count, 8 * sizeof(unsigned long long)));
+  // hipMemset runs on the null stream, which does not order against the
+  // non-blocking streams the plan is used on: without the synchronize it could
+  // land after a later schedule had written the class bounds next to the count
+  // (zeroing them, so class launches computed nothing).  Waited for here; the
+  // count and the bounds are rewritten stream-ordered on every run anyway.
   FCS_HIP_CHECK(hipMemset(p->rescue_count, 0, 8 * sizeof(unsigned long long)));
+  FCS_HIP_CHECK(hipStreamSynchronize(nullptr));
   p->bounds = reinterpret_cast<int64_t*>(p->rescue_count + 1);
   size_t tmp = 0;
   FCS_HIP_CHECK(sort_pairs_u32(nullptr, tmp, p->keys_in, p->keys_out, p->idx_in, p->idx_out, (int)n, nullptr));

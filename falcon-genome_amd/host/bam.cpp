@@ -14,18 +14,22 @@ namespace {
 
 const char kSeqNt16[] = "=ACMGRSVTWYHKDBN";
 
-uint8_t nt16_code(char c) {
-  static uint8_t tab[256];
-  static bool init = false;
-  if (!init) {
+struct Nt16Table {
+  uint8_t tab[256];
+  Nt16Table() {
     for (int i = 0; i < 256; ++i) tab[i] = 15;
     for (int k = 0; k < 16; ++k) {
       tab[(uint8_t)kSeqNt16[k]] = (uint8_t)k;
       tab[(uint8_t)std::tolower(kSeqNt16[k])] = (uint8_t)k;
     }
-    init = true;
   }
-  return tab[(uint8_t)c];
+};
+
+// Built once by a function-local static (thread-safe initialisation): the
+// aligner's record builders call this from several threads.
+uint8_t nt16_code(char c) {
+  static const Nt16Table t;
+  return t.tab[(uint8_t)c];
 }
 
 template <typename T>
