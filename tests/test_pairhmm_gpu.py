@@ -235,3 +235,42 @@ def test_bytes_outside_acgtn(gpu, exact):
     haps[2] = h
     p = fcship.make_pairs(reads, haps)
     check_parity(p, fcship.phmm_compute_pairs(p, exact=exact), exact)
+
+
+def test_concurrent_region_calls_match_serial(gpu):
+    """The Executor's shard tasks call the synchronous region API from several
+    host threads on one device at once (each on its own non-blocking stream).
+    Every concurrent result must equal the serial one bitwise: a device write
+    that is not ordered on the caller's stream (round 1: the plan's null-stream
+    memset of the class bounds) shows up here as a mismatch."""
+    import threading
+    rng = np.random.default_rng(4242)
+    jobs = []
+    for j in range(8):
+        regions = []
+        for g in range(int(rng.integers(3, 9))):
+            nr, nh = int(rng.integers(1, 10)), int(rng.integers(1, 5))
+            reads, haps = random_batch(7000 + 31 * j + g, nr, nh, 40, 151, 60, 420)
+            regions.append((reads, haps))
+        jobs.append(regions)
+    serial = [fcship.phmm_compute_regions(r) for r in jobs]
+    got = [None] * len(jobs)
+    errors = []
+
+    def worker(k):
+        try:
+            for j in range(k, len(jobs), 4):
+                for _ in range(3):
+                    outs = fcship.phmm_compute_regions(jobs[j])
+                    if not all(np.array_equal(a, b) for a, b in zip(outs, serial[j])):
+                        got[j] = outs
+        except Exception as e:  # surfaced below on the main thread
+            errors.append(e)
+
+    threads = [threading.Thread(target=worker, args=(k,)) for k in range(4)]
+    for t in threads:
+        t.start()
+    for t in threads:
+        t.join()
+    assert not errors, errors
+    assert all(g is None for g in got), [j for j, g in enumerate(got) if g is not None]
