@@ -384,30 +384,54 @@ CallerStats call_intervals(const Reference& ref, const std::string& bam, const s
     const int64_t L = (int64_t)seq.size();
     const int64_t own_beg = std::max<int64_t>(0, iv.lb - 1), own_end = std::min<int64_t>(L, iv.ub);
     if (own_beg >= own_end) continue;
-    const int64_t wb = std::max<int64_t>(0, own_beg - opt.max_region), we = std::min<int64_t>(L, own_end + opt.max_region);
+    // Active-site clusters (sites chained while the gap is <= padding) are the
+    // connected components of the whole contig's site graph, so every shard
+    // that sees a cluster must see all of it: the window around the shard's
+    // own range grows until no cluster overlapping that range comes within
+    // `padding` of a window edge (a site beyond the edge could chain on, and
+    // the cluster's regions reach `padding` past its end sites).  Then the
+    // regions, their candidates and reads, and so the likelihoods and calls,
+    // do not depend on where gatk.ncontigs put the shard boundaries.
+    int64_t ext_l = opt.max_region, ext_r = opt.max_region, wb = 0, we = 0;
     std::vector<Read> reads[2];
-    load_reads(bam, iv.chrom, wb, we, opt, reads[0]);
-    if (opt.somatic) load_reads(normal_bam, iv.chrom, wb, we, opt, reads[1]);
-    st.reads += (int64_t)(reads[0].size() + reads[1].size());
     Pileup pu;
-    pu.wb = wb;
-    pu.depth.assign(we - wb, 0);
-    pu.events.assign(we - wb, 0);
-    build_pileup(seq, reads[0], opt.min_base_quality, pu);
-    if (opt.somatic) build_pileup(seq, reads[1], opt.min_base_quality, pu);
-    // ---- active sites → regions
-    std::vector<int64_t> sites;
-    for (int64_t p = wb; p < we; ++p) {
-      const int ev = pu.events[p - wb], dp = std::max(1, pu.depth[p - wb]);
-      if (ev >= 2 && ev >= opt.active_fraction * dp) sites.push_back(p);
+    std::vector<std::pair<int64_t, int64_t>> clusters;  // [first site, last site] overlapping the own range
+    for (;;) {
+      wb = std::max<int64_t>(0, own_beg - ext_l);
+      we = std::min<int64_t>(L, own_end + ext_r);
+      reads[0].clear();
+      reads[1].clear();
+      load_reads(bam, iv.chrom, wb, we, opt, reads[0]);
+      if (opt.somatic) load_reads(normal_bam, iv.chrom, wb, we, opt, reads[1]);
+      pu = Pileup();
+      pu.wb = wb;
+      pu.depth.assign(we - wb, 0);
+      pu.events.assign(we - wb, 0);
+      build_pileup(seq, reads[0], opt.min_base_quality, pu);
+      if (opt.somatic) build_pileup(seq, reads[1], opt.min_base_quality, pu);
+      std::vector<int64_t> sites;
+      for (int64_t p = wb; p < we; ++p) {
+        const int ev = pu.events[p - wb], dp = std::max(1, pu.depth[p - wb]);
+        if (ev >= 2 && ev >= opt.active_fraction * dp) sites.push_back(p);
+      }
+      clusters.clear();
+      bool grow_l = false, grow_r = false;
+      for (size_t i = 0; i < sites.size();) {
+        size_t j = i;
+        while (j + 1 < sites.size() && sites[j + 1] <= sites[j] + opt.padding) ++j;
+        const int64_t first = sites[i], last = sites[j];
+        i = j + 1;
+        if (last < own_beg || first >= own_end) continue;  // no site in this shard's range
+        if (wb > 0 && first < wb + 2 * opt.padding) grow_l = true;
+        if (we < L && last + 2 * opt.padding >= we) grow_r = true;
+        clusters.emplace_back(first, last);
+      }
+      if (!grow_l && !grow_r) break;
+      if (grow_l) ext_l *= 2;
+      if (grow_r) ext_r *= 2;
     }
-    size_t i = 0;
-    while (i < sites.size()) {
-      size_t j = i;
-      while (j + 1 < sites.size() && sites[j + 1] <= sites[j] + opt.padding) ++j;
-      const int64_t first = sites[i], last = sites[j];
-      i = j + 1;
-      if (first < own_beg || first >= own_end) continue;  // another shard owns this region
+    st.reads += (int64_t)(reads[0].size() + reads[1].size());
+    for (const auto& [first, last] : clusters) {
       for (int64_t rb = std::max<int64_t>(0, first - opt.padding); rb < std::min<int64_t>(L, last + opt.padding + 1);
            rb += opt.max_region) {
         auto g = std::make_unique<Region>();
@@ -423,6 +447,11 @@ CallerStats call_intervals(const Reference& ref, const std::string& bam, const s
         if (cs.empty()) continue;
         std::stable_sort(cs.begin(), cs.end(), [](const auto& a, const auto& b) { return a.first > b.first; });
         if ((int)cs.size() > kMaxCandidates) cs.resize(kMaxCandidates);
+        // a region none of whose candidates lies in the own range can produce no
+        // call here (the neighbouring shard computes it)
+        if (std::none_of(cs.begin(), cs.end(),
+                         [&](const auto& c) { return c.second.pos >= own_beg && c.second.pos < own_end; }))
+          continue;
         for (auto& c : cs) g->cands.push_back(c.second);
         std::sort(g->cands.begin(), g->cands.end());
         build_haplotypes(seq, *g);

@@ -232,6 +232,7 @@ int synth_main(int argc, char** argv) {
   a.add("tumor", "T", true, false, "also write tumor.bam with somatic variants (C5)");
   a.add("tumor-coverage", "", false, false, "tumor coverage (default 40)");
   a.add("somatic-af", "", false, false, "somatic allele fraction (default 0.3)");
+  a.add("spike", "", false, false, "chr:pos[,chr:pos...] plant three het SNVs at pos-30, pos, pos+30 (1-based)");
   a.parse(argc, argv);
   SynthSpec sp;
   if (a.has("contigs")) {
@@ -244,6 +245,17 @@ int synth_main(int argc, char** argv) {
       const size_t c = tok.find(':');
       if (c == std::string::npos) throw invalidParam("--contigs " + s);
       sp.contigs.emplace_back(tok.substr(0, c), std::stoll(tok.substr(c + 1)));
+      p = e + 1;
+    }
+  }
+  if (a.has("spike")) {
+    std::string s = a.get("spike");
+    for (size_t p = 0; p < s.size();) {
+      const size_t e = std::min(s.find(',', p), s.size());
+      const std::string tok = s.substr(p, e - p);
+      const size_t c = tok.rfind(':');
+      if (c == std::string::npos) throw invalidParam("--spike " + s);
+      sp.spikes.emplace_back(tok.substr(0, c), std::stoll(tok.substr(c + 1)) - 1);
       p = e + 1;
     }
   }

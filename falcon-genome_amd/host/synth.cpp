@@ -206,6 +206,28 @@ SynthOutputs synth_dataset(const SynthSpec& spec, const std::string& dir) {
     }
   }
 
+  for (const auto& [chrom, centre] : spec.spikes) {
+    const int c = ref.index(chrom);
+    if (c < 0 || centre < 200 || centre + 200 >= (int64_t)ref.contigs[c].seq.size())
+      throw invalidParam("--spike " + chrom + ":" + std::to_string(centre) + " is not inside a contig");
+    auto& vs = per[c];
+    vs.erase(std::remove_if(vs.begin(), vs.end(),
+                            [&](const SynthVariant& v) { return v.pos + 100 >= centre && v.pos <= centre + 100; }),
+             vs.end());
+    Rng r(spec.seed, 0x3000 + (uint64_t)centre);
+    for (int64_t d : {-30, 0, 30}) {
+      SynthVariant v;
+      v.chrom = chrom;
+      v.pos = centre + d;
+      v.ref = std::string(1, ref.contigs[c].seq[v.pos]);
+      v.alt = std::string(1, other_base(r, ref.contigs[c].seq[v.pos]));
+      v.gt = 1;
+      v.af = 0.5;
+      vs.push_back(v);
+    }
+    std::sort(vs.begin(), vs.end(), [](const SynthVariant& a, const SynthVariant& b) { return a.pos < b.pos; });
+  }
+
   // ---- reads
   BamHeader hdr;
   hdr.text = "@HD\tVN:1.6\tSO:coordinate\n";

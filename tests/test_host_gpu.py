@@ -17,10 +17,16 @@ import oracle_lib
 pytestmark = pytest.mark.gpu
 
 
+SPIKE = "chr20:109380"
+
+
 @pytest.fixture(scope="module")
 def data(tmp_path_factory):
     d = tmp_path_factory.mktemp("e2e")
-    p = H.run_cli("synth", "-o", d, "-c", "chr20:250000,chr21:100000", "-x", "30", "--tumor", "--seed", "11")
+    # the spiked cluster straddles the 10th/11th shard boundary of gatk.ncontigs = 32
+    # (ceil(350000 / 32) = 10938 positions per shard: chr20:109380 | 109381)
+    p = H.run_cli("synth", "-o", d, "-c", "chr20:250000,chr21:100000", "-x", "30", "--tumor", "--seed", "11",
+                  "--spike", SPIKE)
     assert p.returncode == 0, p.stderr
     return d
 
@@ -150,3 +156,21 @@ def test_htc_gpu_slots_do_not_change_calls(gpu, data, tmp_path):
         assert p.returncode == 0, p.stderr[-3000:]
         outs.append([ln for ln in out.read_text().splitlines() if not ln.startswith("##source")])
     assert outs[0] == outs[1]
+
+
+def test_htc_shard_boundaries_do_not_change_calls(gpu, data, tmp_path):
+    """a variant cluster cut by a gatk.ncontigs boundary is called the
+    same as with the boundary elsewhere — every shard whose range a cluster
+    touches sees the whole cluster (caller.cpp window growth) and emits only the
+    calls inside its own range."""
+    outs = {}
+    for n in ("1", "6", "32"):
+        out = tmp_path / f"htc_n{n}.vcf"
+        p = H.run_cli("htc", "-r", data / "ref.fasta", "-i", data / "sample.bam", "-o", out,
+                      env=dict(ENV, FCS_GATK_NCONTIGS=n), cwd=tmp_path)
+        assert p.returncode == 0, p.stderr[-3000:]
+        outs[n] = [ln for ln in out.read_text().splitlines() if not ln.startswith("##")]
+    assert outs["1"] == outs["6"] == outs["32"]
+    spiked = {("chr20", 109380 + d) for d in (-30, 0, 30)}
+    called = {(f[0], int(f[1])) for f in (ln.split("\t") for ln in outs["32"] if not ln.startswith("#"))}
+    assert spiked <= called, spiked - called
