@@ -9,6 +9,7 @@
 #include <rocprim/device/device_radix_sort.hpp>
 
 #include <algorithm>
+#include <cmath>
 #include <cstdlib>
 #include <cstring>
 #include <map>
@@ -100,28 +101,59 @@ int join_streams(hipStream_t s, const hipStream_t (&fs)[kForkStreams]) {
 
 namespace {
 
-// RAII device buffer for the synchronous paths.
-struct DevBuf {
-  void* p = nullptr;
-  ~DevBuf() {
-    if (p) (void)hipFree(p);
+// Aligned sub-allocations of one staging buffer.
+struct Layout {
+  size_t total = 0;
+  size_t add(size_t bytes) {
+    const size_t o = total;
+    total += (bytes + 255) & ~(size_t)255;
+    return o;
   }
-  int alloc(size_t bytes) {
-    if (bytes == 0) bytes = 16;
-    if (hipMalloc(&p, bytes) != hipSuccess) {
-      p = nullptr;
-      return fail(FCS_ERR_NOMEM, "[E::fcship] hipMalloc failed");
-    }
-    return FCS_OK;
-  }
-  template <typename T> T* as() const { return static_cast<T*>(p); }
 };
 
-int upload(DevBuf& d, const void* src, size_t bytes, hipStream_t s) {
-  int rc = d.alloc(bytes);
-  if (rc) return rc;
-  if (bytes && src) FCS_HIP_CHECK(hipMemcpyAsync(d.p, src, bytes, hipMemcpyHostToDevice, s));
-  return FCS_OK;
+}  // namespace
+
+// Per-(thread, device) state of the synchronous host-pointer entry points:
+// the thread's stream, a PairHMM plan and an SW plan grown to the largest
+// batch seen, one device arena for the batch's inputs and outputs and one
+// pinned host arena it is staged through (one H2D and one D2H copy per call).
+// After warm-up a call allocates nothing: no hipMalloc/hipFree (hipFree
+// synchronises the whole device, so per-call frees serialised the Executor's
+// concurrent shard threads on one GPU) and no null-stream operation.
+struct Session {
+  int device = 0;
+  hipStream_t s = nullptr;
+  fcs_phmm_plan* phmm = nullptr;
+  fcs_bsw_plan* bsw = nullptr;
+  void* dev = nullptr;
+  size_t dev_cap = 0;
+  void* host = nullptr;
+  size_t host_cap = 0;
+  ~Session();
+  int ensure_dev(size_t bytes);
+  int ensure_host(size_t bytes);
+  int ensure_phmm(int64_t pairs);
+  int ensure_bsw(int64_t tasks);
+  template <typename T> T* d(size_t off) const { return reinterpret_cast<T*>(static_cast<char*>(dev) + off); }
+  template <typename T> T* h(size_t off) const { return reinterpret_cast<T*>(static_cast<char*>(host) + off); }
+};
+
+namespace {
+
+size_t grown(size_t need, size_t cap) { return std::max(need + need / 4, std::min<size_t>(2 * cap, need + (1u << 30))); }
+
+// The calling thread's session on `device` (created on first use).
+Session* session(int device) {
+  static thread_local std::map<int, std::unique_ptr<Session>> sessions;
+  auto& slot = sessions[device];
+  if (!slot) {
+    hipStream_t s = thread_stream(device);
+    if (!s) return nullptr;
+    slot.reset(new Session());
+    slot->device = device;
+    slot->s = s;
+  }
+  return slot.get();
 }
 
 BswParams to_params(const fcs_bsw_params* p) {
@@ -254,6 +286,76 @@ struct fcs_phmm_plan {
   int64_t scheduled = -1;  // n_pairs of the last schedule
 };
 
+namespace fcs {
+
+Session::~Session() {
+  (void)hipSetDevice(device);
+  if (s) (void)hipStreamSynchronize(s);
+  fcs_phmm_plan_destroy(phmm);
+  fcs_bsw_plan_destroy(bsw);
+  if (dev) (void)hipFree(dev);
+  if (host) (void)hipHostFree(host);
+}
+
+int Session::ensure_dev(size_t bytes) {
+  if (bytes <= dev_cap) return FCS_OK;
+  FCS_HIP_CHECK(hipStreamSynchronize(s));
+  if (dev) (void)hipFree(dev);
+  dev = nullptr;
+  dev_cap = 0;
+  const size_t cap = grown(bytes, dev_cap);
+  if (hipMalloc(&dev, cap) != hipSuccess) {
+    dev = nullptr;
+    return fail(FCS_ERR_NOMEM, "[E::fcship] hipMalloc of " + std::to_string(cap) + " bytes failed");
+  }
+  dev_cap = cap;
+  return FCS_OK;
+}
+
+int Session::ensure_host(size_t bytes) {
+  if (bytes <= host_cap) return FCS_OK;
+  FCS_HIP_CHECK(hipStreamSynchronize(s));
+  if (host) (void)hipHostFree(host);
+  host = nullptr;
+  host_cap = 0;
+  const size_t cap = grown(bytes, host_cap);
+  if (hipHostMalloc(&host, cap, hipHostMallocDefault) != hipSuccess) {
+    host = nullptr;
+    return fail(FCS_ERR_NOMEM, "[E::fcship] hipHostMalloc of " + std::to_string(cap) + " bytes failed");
+  }
+  host_cap = cap;
+  return FCS_OK;
+}
+
+int Session::ensure_phmm(int64_t pairs) {
+  if (phmm && phmm->max_pairs >= pairs) return FCS_OK;
+  FCS_HIP_CHECK(hipStreamSynchronize(s));
+  fcs_phmm_plan_destroy(phmm);
+  phmm = nullptr;
+  return fcs_phmm_plan_create(device, (int64_t)grown((size_t)pairs, 0), &phmm);
+}
+
+int Session::ensure_bsw(int64_t tasks) {
+  if (bsw && bsw->ws.cap >= tasks) return FCS_OK;
+  FCS_HIP_CHECK(hipStreamSynchronize(s));
+  fcs_bsw_plan_destroy(bsw);
+  bsw = nullptr;
+  return fcs_bsw_plan_create(device, (int64_t)grown((size_t)tasks, 0), &bsw);
+}
+
+// FCSHIP_TEST_FAULT=drop_schedule: the PairHMM schedule publishes empty class
+// ranges, as the round-1 null-stream memset race once did, so the forward
+// pass computes nothing (tests/test_pairhmm_gpu.py checks it is reported).
+static bool fault_drop_schedule() {
+  static const bool on = [] {
+    const char* e = std::getenv("FCSHIP_TEST_FAULT");
+    return e && std::strcmp(e, "drop_schedule") == 0;
+  }();
+  return on;
+}
+
+}  // namespace fcs
+
 static PhmmDevBatch to_dev(const fcs_phmm_batch* b) {
   PhmmDevBatch d;
   d.rb = b->read_bases;
@@ -346,13 +448,11 @@ int fcs_phmm_plan_create(int32_t device, int64_t max_pairs, fcs_phmm_plan** plan
   FCS_HIP_CHECK(hipMalloc(&p->idx_out, n * 4));
   FCS_HIP_CHECK(hipMalloc(&p->rescue_list, n * 4));
   FCS_HIP_CHECK(hipMalloc(&p->rescue_count, 8 * sizeof(unsigned long long)));
-  // hipMemset runs on the null stream, which does not order against the
-  // non-blocking streams the plan is used on: without the synchronize it could
-  // land after a later schedule had written the class bounds next to the count
-  // (zeroing them, so class launches computed nothing).  Waited for here; the
-  // count and the bounds are rewritten stream-ordered on every run anyway.
-  FCS_HIP_CHECK(hipMemset(p->rescue_count, 0, 8 * sizeof(unsigned long long)));
-  FCS_HIP_CHECK(hipStreamSynchronize(nullptr));
+  // Nothing is initialised here: every run writes the class bounds (the bounds
+  // kernel stores all kPhmmClasses + 1 of them) and zeroes the rescue count on
+  // the caller's stream.  (Round 1 zeroed them with a null-stream hipMemset,
+  // which does not order against the non-blocking streams the plan runs on and
+  // once landed after a schedule, so class launches computed nothing.)
   p->bounds = reinterpret_cast<int64_t*>(p->rescue_count + 1);
   size_t tmp = 0;
   FCS_HIP_CHECK(sort_pairs_u32(nullptr, tmp, p->keys_in, p->keys_out, p->idx_in, p->idx_out, (int)n, nullptr));
@@ -392,6 +492,7 @@ int fcs_phmm_dev_schedule(fcs_phmm_plan* plan, const fcs_phmm_batch* b, void* st
                                  (int)b->n_pairs, s, kPhmmKeyBits));
   }
   if ((rc = launch_phmm_bounds(plan->keys_out, b->n_pairs, plan->bounds, s))) return rc;
+  if (fault_drop_schedule()) FCS_HIP_CHECK(hipMemsetAsync(plan->bounds, 0, 7 * sizeof(int64_t), s));
   plan->scheduled = b->n_pairs;
   return FCS_OK;
 }
@@ -448,6 +549,86 @@ int fcs_phmm_plan_rescue_count(fcs_phmm_plan* plan, void* stream, int64_t* count
   return FCS_OK;
 }
 
+}  // extern "C"
+
+namespace {
+
+// Host side of one synchronous PairHMM pass: `fill` writes the batch's SoA
+// arrays into the session's pinned staging at the offsets of `off` (order of
+// PhmmStage), then one H2D copy, schedule + forward + rescue on the thread's
+// stream into an output pre-filled with NaN, one D2H copy, and a check that
+// every pair's result was written (a pair the schedule or a class launch
+// skipped would otherwise go downstream as garbage).  Returns the results in
+// pinned memory (valid until the thread's next call).
+struct PhmmStage {
+  int64_t n_reads = 0, n_haps = 0, n_pairs = 0, read_bytes = 0, hap_bytes = 0;
+  int32_t max_read_len = 0, max_hap_len = 0;
+};
+enum { kRb, kBq, kIq, kDq, kGq, kRo, kRl, kHb, kHo, kHl, kPr, kPh, kNArr };
+
+template <typename Fill>
+int phmm_staged(const PhmmStage& g, const fcs_phmm_opts& opts, Fill&& fill, const double** host_out) {
+  int rc = check_device(opts.device);
+  if (rc) return rc;
+  FCS_HIP_CHECK(hipSetDevice(opts.device));
+  Session* S = session(opts.device);
+  if (!S) return fail(FCS_ERR_DEVICE, "[E::fcship] stream creation failed");
+  const size_t RB = (size_t)g.read_bytes, HB = (size_t)g.hap_bytes, nr = (size_t)g.n_reads, nh = (size_t)g.n_haps,
+               np = (size_t)g.n_pairs;
+  Layout L;
+  size_t off[kNArr];
+  for (int k = kRb; k <= kGq; ++k) off[k] = L.add(RB);
+  off[kRo] = L.add(8 * nr);
+  off[kRl] = L.add(4 * nr);
+  off[kHb] = L.add(HB);
+  off[kHo] = L.add(8 * nh);
+  off[kHl] = L.add(4 * nh);
+  off[kPr] = L.add(4 * np);
+  off[kPh] = L.add(4 * np);
+  const size_t in_bytes = L.total, out_off = L.add(8 * np);
+  if ((rc = S->ensure_host(L.total)) || (rc = S->ensure_dev(L.total)) || (rc = S->ensure_phmm(g.n_pairs))) return rc;
+  fill(S, off);
+  hipStream_t s = S->s;
+  FCS_HIP_CHECK(hipMemcpyAsync(S->dev, S->host, in_bytes, hipMemcpyHostToDevice, s));
+  fcs_phmm_batch d{};
+  d.read_bases = S->d<uint8_t>(off[kRb]);
+  d.read_bq = S->d<uint8_t>(off[kBq]);
+  d.read_iq = S->d<uint8_t>(off[kIq]);
+  d.read_dq = S->d<uint8_t>(off[kDq]);
+  d.read_gcp = S->d<uint8_t>(off[kGq]);
+  d.read_off = S->d<int64_t>(off[kRo]);
+  d.read_len = S->d<int32_t>(off[kRl]);
+  d.n_reads = g.n_reads;
+  d.hap_bases = S->d<uint8_t>(off[kHb]);
+  d.hap_off = S->d<int64_t>(off[kHo]);
+  d.hap_len = S->d<int32_t>(off[kHl]);
+  d.n_haps = g.n_haps;
+  d.pair_read = S->d<int32_t>(off[kPr]);
+  d.pair_hap = S->d<int32_t>(off[kPh]);
+  d.n_pairs = g.n_pairs;
+  d.read_bytes = g.read_bytes;
+  d.hap_bytes = g.hap_bytes;
+  d.max_read_len = g.max_read_len;
+  d.max_hap_len = g.max_hap_len;
+  double* dout = S->d<double>(out_off);
+  FCS_HIP_CHECK(hipMemsetAsync(dout, 0xFF, 8 * np, s));  // all-ones = NaN: "not written"
+  if ((rc = fcs_phmm_dev_run(S->phmm, &d, dout, &opts, s))) return rc;
+  double* hout = S->h<double>(out_off);
+  FCS_HIP_CHECK(hipMemcpyAsync(hout, dout, 8 * np, hipMemcpyDeviceToHost, s));
+  FCS_HIP_CHECK(hipStreamSynchronize(s));
+  int64_t missing = 0;
+  for (size_t k = 0; k < np; ++k) missing += std::isnan(hout[k]);
+  if (missing)
+    return fail(FCS_ERR_DEVICE, "[E::fcship] PairHMM: " + std::to_string(missing) + " of " + std::to_string(np) +
+                                    " results were not written by the device pass");
+  *host_out = hout;
+  return FCS_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
 int fcs_phmm_compute_pairs(const fcs_phmm_batch* b, double* out_log10, const fcs_phmm_opts* opts_in) {
   int rc = check_batch_shape(b);
   if (rc) return rc;
@@ -457,7 +638,12 @@ int fcs_phmm_compute_pairs(const fcs_phmm_batch* b, double* out_log10, const fcs
   if (b->n_pairs == 0) return FCS_OK;
   if (!out_log10) return fail(FCS_ERR_INVALID, "[E::fcs_phmm_compute_pairs] null output");
   // Validate indices and lengths on the host (the device path trusts its caller).
-  int32_t maxr = 0, maxh = 0;
+  PhmmStage g;
+  g.n_reads = b->n_reads;
+  g.n_haps = b->n_haps;
+  g.n_pairs = b->n_pairs;
+  g.read_bytes = b->read_bytes;
+  g.hap_bytes = b->hap_bytes;
   for (int64_t p = 0; p < b->n_pairs; ++p) {
     const int32_t ri = b->pair_read[p], hi = b->pair_hap[p];
     if (ri < 0 || ri >= b->n_reads || hi < 0 || hi >= b->n_haps)
@@ -466,51 +652,32 @@ int fcs_phmm_compute_pairs(const fcs_phmm_batch* b, double* out_log10, const fcs
   for (int64_t r = 0; r < b->n_reads; ++r) {
     if (b->read_len[r] < 0 || b->read_off[r] < 0 || b->read_off[r] + b->read_len[r] > b->read_bytes)
       return fail(FCS_ERR_INVALID, "[E::fcs_phmm_compute_pairs] read extent outside read arrays");
-    maxr = std::max(maxr, b->read_len[r]);
+    g.max_read_len = std::max(g.max_read_len, b->read_len[r]);
   }
   for (int64_t h = 0; h < b->n_haps; ++h) {
     if (b->hap_len[h] < 0 || b->hap_off[h] < 0 || b->hap_off[h] + b->hap_len[h] > b->hap_bytes)
       return fail(FCS_ERR_INVALID, "[E::fcs_phmm_compute_pairs] hap extent outside hap array");
-    maxh = std::max(maxh, b->hap_len[h]);
+    g.max_hap_len = std::max(g.max_hap_len, b->hap_len[h]);
   }
-  if ((rc = check_device(opts.device))) return rc;
-  FCS_HIP_CHECK(hipSetDevice(opts.device));
-  hipStream_t s = thread_stream(opts.device);
-  if (!s) return fail(FCS_ERR_DEVICE, "[E::fcship] stream creation failed");
-  DevBuf rb, bq, iq, dq, gq, ro, rl, hb, ho, hl, pr, ph, out;
-  const size_t RB = (size_t)b->read_bytes, HB = (size_t)b->hap_bytes;
-  if ((rc = upload(rb, b->read_bases, RB, s)) || (rc = upload(bq, b->read_bq, RB, s)) ||
-      (rc = upload(iq, b->read_iq, RB, s)) || (rc = upload(dq, b->read_dq, RB, s)) ||
-      (rc = upload(gq, b->read_gcp, RB, s)) || (rc = upload(ro, b->read_off, 8 * (size_t)b->n_reads, s)) ||
-      (rc = upload(rl, b->read_len, 4 * (size_t)b->n_reads, s)) || (rc = upload(hb, b->hap_bases, HB, s)) ||
-      (rc = upload(ho, b->hap_off, 8 * (size_t)b->n_haps, s)) ||
-      (rc = upload(hl, b->hap_len, 4 * (size_t)b->n_haps, s)) ||
-      (rc = upload(pr, b->pair_read, 4 * (size_t)b->n_pairs, s)) ||
-      (rc = upload(ph, b->pair_hap, 4 * (size_t)b->n_pairs, s)) || (rc = out.alloc(8 * (size_t)b->n_pairs)))
-    return rc;
-  fcs_phmm_batch d = *b;
-  d.read_bases = rb.as<uint8_t>();
-  d.read_bq = bq.as<uint8_t>();
-  d.read_iq = iq.as<uint8_t>();
-  d.read_dq = dq.as<uint8_t>();
-  d.read_gcp = gq.as<uint8_t>();
-  d.read_off = ro.as<int64_t>();
-  d.read_len = rl.as<int32_t>();
-  d.hap_bases = hb.as<uint8_t>();
-  d.hap_off = ho.as<int64_t>();
-  d.hap_len = hl.as<int32_t>();
-  d.pair_read = pr.as<int32_t>();
-  d.pair_hap = ph.as<int32_t>();
-  d.max_read_len = maxr;
-  d.max_hap_len = maxh;
-  fcs_phmm_plan* plan = nullptr;
-  rc = fcs_phmm_plan_create(opts.device, b->n_pairs, &plan);
+  const size_t RB = (size_t)b->read_bytes, HB = (size_t)b->hap_bytes, nr = (size_t)b->n_reads,
+               nh = (size_t)b->n_haps, np = (size_t)b->n_pairs;
+  const double* res = nullptr;
+  rc = phmm_staged(g, opts, [&](Session* S, const size_t* off) {
+    std::memcpy(S->h<void>(off[kRb]), b->read_bases, RB);
+    std::memcpy(S->h<void>(off[kBq]), b->read_bq, RB);
+    std::memcpy(S->h<void>(off[kIq]), b->read_iq, RB);
+    std::memcpy(S->h<void>(off[kDq]), b->read_dq, RB);
+    std::memcpy(S->h<void>(off[kGq]), b->read_gcp, RB);
+    std::memcpy(S->h<void>(off[kRo]), b->read_off, 8 * nr);
+    std::memcpy(S->h<void>(off[kRl]), b->read_len, 4 * nr);
+    std::memcpy(S->h<void>(off[kHb]), b->hap_bases, HB);
+    std::memcpy(S->h<void>(off[kHo]), b->hap_off, 8 * nh);
+    std::memcpy(S->h<void>(off[kHl]), b->hap_len, 4 * nh);
+    std::memcpy(S->h<void>(off[kPr]), b->pair_read, 4 * np);
+    std::memcpy(S->h<void>(off[kPh]), b->pair_hap, 4 * np);
+  }, &res);
   if (rc) return rc;
-  std::unique_ptr<fcs_phmm_plan, int (*)(fcs_phmm_plan*)> guard(plan, fcs_phmm_plan_destroy);
-  rc = fcs_phmm_dev_run(plan, &d, out.as<double>(), &opts, s);
-  if (rc) return rc;
-  FCS_HIP_CHECK(hipMemcpyAsync(out_log10, out.p, 8 * (size_t)b->n_pairs, hipMemcpyDeviceToHost, s));
-  FCS_HIP_CHECK(hipStreamSynchronize(s));
+  std::memcpy(out_log10, res, 8 * np);
   return FCS_OK;
 }
 
@@ -525,15 +692,15 @@ int fcs_phmm_compute(const fcs_phmm_read* reads, int32_t n_reads, const fcs_phmm
 }
 
 // Many active regions in one device pass: the regions' reads and haplotypes
-// are concatenated into one SoA batch whose pair list is region-major and
-// read-major within a region, so the flat result splits back into each
-// region's read-major matrix by a running offset.
-int fcs_phmm_compute_regions(const fcs_phmm_region* regions, int32_t n_regions, const fcs_phmm_opts* opts) {
+// are concatenated (straight into the pinned staging) into one SoA batch whose
+// pair list is region-major and read-major within a region, so the flat
+// result splits back into each region's read-major matrix by a running offset.
+int fcs_phmm_compute_regions(const fcs_phmm_region* regions, int32_t n_regions, const fcs_phmm_opts* opts_in) {
   if (n_regions < 0 || (n_regions > 0 && !regions))
     return fail(FCS_ERR_INVALID, "[E::fcs_phmm_compute_regions] bad arguments");
-  int64_t nr = 0, nh = 0, np = 0, rt = 0, ht = 0;
-  for (int32_t g = 0; g < n_regions; ++g) {
-    const fcs_phmm_region& R = regions[g];
+  PhmmStage g;
+  for (int32_t k = 0; k < n_regions; ++k) {
+    const fcs_phmm_region& R = regions[k];
     if (R.n_reads < 0 || R.n_haps < 0 || (R.n_reads > 0 && !R.reads) || (R.n_haps > 0 && !R.haps))
       return fail(FCS_ERR_INVALID, "[E::fcs_phmm_compute_regions] malformed region");
     const int64_t pairs = (int64_t)R.n_reads * R.n_haps;
@@ -542,79 +709,68 @@ int fcs_phmm_compute_regions(const fcs_phmm_region* regions, int32_t n_regions, 
       const fcs_phmm_read& x = R.reads[r];
       if (x.len < 0 || (x.len > 0 && (!x.bases || !x.base_q || !x.ins_q || !x.del_q || !x.gcp)))
         return fail(FCS_ERR_INVALID, "[E::fcs_phmm_compute_regions] malformed read");
-      rt += x.len;
+      g.read_bytes += x.len;
+      g.max_read_len = std::max(g.max_read_len, x.len);
     }
     for (int32_t h = 0; h < R.n_haps; ++h) {
       if (R.haps[h].len < 0 || (R.haps[h].len > 0 && !R.haps[h].bases))
         return fail(FCS_ERR_INVALID, "[E::fcs_phmm_compute_regions] malformed haplotype");
-      ht += R.haps[h].len;
+      g.hap_bytes += R.haps[h].len;
+      g.max_hap_len = std::max(g.max_hap_len, R.haps[h].len);
     }
-    nr += R.n_reads;
-    nh += R.n_haps;
-    np += pairs;
+    g.n_reads += R.n_reads;
+    g.n_haps += R.n_haps;
+    g.n_pairs += pairs;
   }
-  if (np == 0) return FCS_OK;
-  if (nr > INT32_MAX || nh > INT32_MAX)
-    return fail(FCS_ERR_INVALID, "[E::fcs_phmm_compute_regions] more than 2^31 reads or haplotypes");
-  std::vector<int64_t> roff(nr), hoff(nh);
-  std::vector<int32_t> rlen(nr), hlen(nh), pr(np), ph(np);
-  std::vector<uint8_t> rb(rt), bq(rt), iq(rt), dq(rt), gq(rt), hb(ht);
-  int64_t ri = 0, hi = 0, pi = 0, ro = 0, ho = 0;
-  for (int32_t g = 0; g < n_regions; ++g) {
-    const fcs_phmm_region& R = regions[g];
-    const int64_t r0 = ri, h0 = hi;
-    for (int32_t r = 0; r < R.n_reads; ++r, ++ri) {
-      const fcs_phmm_read& x = R.reads[r];
-      roff[ri] = ro;
-      rlen[ri] = x.len;
-      if (x.len) {
-        std::memcpy(&rb[ro], x.bases, x.len);
-        std::memcpy(&bq[ro], x.base_q, x.len);
-        std::memcpy(&iq[ro], x.ins_q, x.len);
-        std::memcpy(&dq[ro], x.del_q, x.len);
-        std::memcpy(&gq[ro], x.gcp, x.len);
+  if (g.n_pairs == 0) return FCS_OK;
+  if (g.n_reads > INT32_MAX || g.n_haps > INT32_MAX || g.n_pairs > INT32_MAX)
+    return fail(FCS_ERR_INVALID, "[E::fcs_phmm_compute_regions] more than 2^31 reads, haplotypes or pairs");
+  fcs_phmm_opts opts;
+  if (opts_in) opts = *opts_in;
+  else fcs_phmm_opts_default(&opts);
+  const double* res = nullptr;
+  const int rc = phmm_staged(g, opts, [&](Session* S, const size_t* off) {
+    uint8_t *rb = S->h<uint8_t>(off[kRb]), *bq = S->h<uint8_t>(off[kBq]), *iq = S->h<uint8_t>(off[kIq]),
+            *dq = S->h<uint8_t>(off[kDq]), *gq = S->h<uint8_t>(off[kGq]), *hb = S->h<uint8_t>(off[kHb]);
+    int64_t *roff = S->h<int64_t>(off[kRo]), *hoff = S->h<int64_t>(off[kHo]);
+    int32_t *rlen = S->h<int32_t>(off[kRl]), *hlen = S->h<int32_t>(off[kHl]), *pr = S->h<int32_t>(off[kPr]),
+            *ph = S->h<int32_t>(off[kPh]);
+    int64_t ri = 0, hi = 0, pi = 0, ro = 0, ho = 0;
+    for (int32_t k = 0; k < n_regions; ++k) {
+      const fcs_phmm_region& R = regions[k];
+      const int64_t r0 = ri, h0 = hi;
+      for (int32_t r = 0; r < R.n_reads; ++r, ++ri) {
+        const fcs_phmm_read& x = R.reads[r];
+        roff[ri] = ro;
+        rlen[ri] = x.len;
+        if (x.len) {
+          std::memcpy(rb + ro, x.bases, x.len);
+          std::memcpy(bq + ro, x.base_q, x.len);
+          std::memcpy(iq + ro, x.ins_q, x.len);
+          std::memcpy(dq + ro, x.del_q, x.len);
+          std::memcpy(gq + ro, x.gcp, x.len);
+        }
+        ro += x.len;
       }
-      ro += x.len;
-    }
-    for (int32_t h = 0; h < R.n_haps; ++h, ++hi) {
-      hoff[hi] = ho;
-      hlen[hi] = R.haps[h].len;
-      if (R.haps[h].len) std::memcpy(&hb[ho], R.haps[h].bases, R.haps[h].len);
-      ho += R.haps[h].len;
-    }
-    for (int32_t r = 0; r < R.n_reads; ++r)
-      for (int32_t h = 0; h < R.n_haps; ++h, ++pi) {
-        pr[pi] = (int32_t)(r0 + r);
-        ph[pi] = (int32_t)(h0 + h);
+      for (int32_t h = 0; h < R.n_haps; ++h, ++hi) {
+        hoff[hi] = ho;
+        hlen[hi] = R.haps[h].len;
+        if (R.haps[h].len) std::memcpy(hb + ho, R.haps[h].bases, R.haps[h].len);
+        ho += R.haps[h].len;
       }
-  }
-  fcs_phmm_batch b{};
-  b.read_bases = rb.data();
-  b.read_bq = bq.data();
-  b.read_iq = iq.data();
-  b.read_dq = dq.data();
-  b.read_gcp = gq.data();
-  b.read_off = roff.data();
-  b.read_len = rlen.data();
-  b.n_reads = nr;
-  b.hap_bases = hb.data();
-  b.hap_off = hoff.data();
-  b.hap_len = hlen.data();
-  b.n_haps = nh;
-  b.pair_read = pr.data();
-  b.pair_hap = ph.data();
-  b.n_pairs = np;
-  b.read_bytes = rt;
-  b.hap_bytes = ht;
-  if (n_regions == 1) return fcs_phmm_compute_pairs(&b, regions[0].out_log10, opts);
-  std::vector<double> flat(np);
-  const int rc = fcs_phmm_compute_pairs(&b, flat.data(), opts);
+      for (int32_t r = 0; r < R.n_reads; ++r)
+        for (int32_t h = 0; h < R.n_haps; ++h, ++pi) {
+          pr[pi] = (int32_t)(r0 + r);
+          ph[pi] = (int32_t)(h0 + h);
+        }
+    }
+  }, &res);
   if (rc) return rc;
-  int64_t off = 0;
-  for (int32_t g = 0; g < n_regions; ++g) {
-    const int64_t pairs = (int64_t)regions[g].n_reads * regions[g].n_haps;
-    if (pairs) std::memcpy(regions[g].out_log10, flat.data() + off, 8 * (size_t)pairs);
-    off += pairs;
+  int64_t o = 0;
+  for (int32_t k = 0; k < n_regions; ++k) {
+    const int64_t pairs = (int64_t)regions[k].n_reads * regions[k].n_haps;
+    if (pairs) std::memcpy(regions[k].out_log10, res + o, 8 * (size_t)pairs);
+    o += pairs;
   }
   return FCS_OK;
 }
@@ -722,32 +878,41 @@ int fcs_bsw_extend_batch(const fcs_bsw_batch* b, const fcs_bsw_params* params, i
     if (b->tbuf[i] > 4) return fail(FCS_ERR_INVALID, "[E::fcs_bsw_extend_batch] target base code > 4");
   if ((rc = check_device(device))) return rc;
   FCS_HIP_CHECK(hipSetDevice(device));
-  hipStream_t s = thread_stream(device);
-  if (!s) return fail(FCS_ERR_DEVICE, "[E::fcship] stream creation failed");
-  DevBuf qb, qo, ql, tb, to, tl, h0, w, rs, cl;
+  Session* S = session(device);
+  if (!S) return fail(FCS_ERR_DEVICE, "[E::fcship] stream creation failed");
   const size_t n = (size_t)b->n;
-  if ((rc = upload(qb, b->qbuf, (size_t)b->qbytes, s)) || (rc = upload(qo, b->qoff, 8 * n, s)) ||
-      (rc = upload(ql, b->qlen, 4 * n, s)) || (rc = upload(tb, b->tbuf, (size_t)b->tbytes, s)) ||
-      (rc = upload(to, b->toff, 8 * n, s)) || (rc = upload(tl, b->tlen, 4 * n, s)) ||
-      (rc = upload(h0, b->h0, 4 * n, s)) || (rc = upload(w, b->w, 4 * n, s)) || (rc = rs.alloc(24 * n)) ||
-      (rc = cl.alloc(8 * n)))
+  Layout L;
+  const size_t oq = L.add((size_t)b->qbytes), oqo = L.add(8 * n), oql = L.add(4 * n), ot = L.add((size_t)b->tbytes),
+               oto = L.add(8 * n), otl = L.add(4 * n), oh0 = L.add(4 * n), ow = L.add(4 * n);
+  const size_t in_bytes = L.total, ors = L.add(24 * n), ocl = L.add(8 * n);
+  if ((rc = S->ensure_host(L.total)) || (rc = S->ensure_dev(L.total)) || (rc = S->ensure_bsw(b->n))) return rc;
+  std::memcpy(S->h<void>(oq), b->qbuf, (size_t)b->qbytes);
+  std::memcpy(S->h<void>(oqo), b->qoff, 8 * n);
+  std::memcpy(S->h<void>(oql), b->qlen, 4 * n);
+  std::memcpy(S->h<void>(ot), b->tbuf, (size_t)b->tbytes);
+  std::memcpy(S->h<void>(oto), b->toff, 8 * n);
+  std::memcpy(S->h<void>(otl), b->tlen, 4 * n);
+  std::memcpy(S->h<void>(oh0), b->h0, 4 * n);
+  std::memcpy(S->h<void>(ow), b->w, 4 * n);
+  hipStream_t s = S->s;
+  FCS_HIP_CHECK(hipMemcpyAsync(S->dev, S->host, in_bytes, hipMemcpyHostToDevice, s));
+  BswDevBatch d;
+  d.qbuf = S->d<uint8_t>(oq);
+  d.qoff = S->d<int64_t>(oqo);
+  d.qlen = S->d<int32_t>(oql);
+  d.tbuf = S->d<uint8_t>(ot);
+  d.toff = S->d<int64_t>(oto);
+  d.tlen = S->d<int32_t>(otl);
+  d.h0 = S->d<int32_t>(oh0);
+  d.w = S->d<int32_t>(ow);
+  d.n = b->n;
+  if ((rc = launch_bsw_extend_sorted(d, to_params(params), mq, mt, S->d<int32_t>(ors), S->d<int64_t>(ocl),
+                                     S->bsw->ws, s)))
     return rc;
-  fcs_bsw_batch d = *b;
-  d.qbuf = qb.as<uint8_t>();
-  d.qoff = qo.as<int64_t>();
-  d.qlen = ql.as<int32_t>();
-  d.tbuf = tb.as<uint8_t>();
-  d.toff = to.as<int64_t>();
-  d.tlen = tl.as<int32_t>();
-  d.h0 = h0.as<int32_t>();
-  d.w = w.as<int32_t>();
-  d.max_qlen = mq;
-  d.max_tlen = mt;
-  rc = fcs_bsw_extend_dev(&d, params, rs.as<int32_t>(), cl.as<int64_t>(), device, s);
-  if (rc) return rc;
-  FCS_HIP_CHECK(hipMemcpyAsync(res, rs.p, 24 * n, hipMemcpyDeviceToHost, s));
-  if (cells) FCS_HIP_CHECK(hipMemcpyAsync(cells, cl.p, 8 * n, hipMemcpyDeviceToHost, s));
+  FCS_HIP_CHECK(hipMemcpyAsync(S->h<void>(ors), S->d<void>(ors), ocl + 8 * n - ors, hipMemcpyDeviceToHost, s));
   FCS_HIP_CHECK(hipStreamSynchronize(s));
+  std::memcpy(res, S->h<void>(ors), 24 * n);
+  if (cells) std::memcpy(cells, S->h<void>(ocl), 8 * n);
   return FCS_OK;
 }
 
@@ -825,7 +990,7 @@ int fcs_bsw_global(const fcs_bsw_task* tasks, int32_t n, const fcs_bsw_params* p
     mt = std::max(mt, pk.tlen[k]);
     const int64_t ncol = std::min<int64_t>(pk.qlen[k], 2LL * pk.w[k] + 1);
     zoff[k] = zt;
-    zt += ncol * pk.tlen[k];
+    if (want_cigar) zt += ncol * pk.tlen[k];
     if (want_cigar) {
       if (cigar_cap[k] < 0 || cigar_off[k] < 0) return fail(FCS_ERR_INVALID, "[E::fcs_bsw_global] bad CIGAR extent");
       ct = std::max<int64_t>(ct, cigar_off[k] + cigar_cap[k]);
@@ -837,45 +1002,62 @@ int fcs_bsw_global(const fcs_bsw_task* tasks, int32_t n, const fcs_bsw_params* p
     if (pk.t[i] > 4) return fail(FCS_ERR_INVALID, "[E::fcs_bsw_global] target base code > 4");
   if ((rc = check_device(device))) return rc;
   FCS_HIP_CHECK(hipSetDevice(device));
-  hipStream_t s = thread_stream(device);
-  if (!s) return fail(FCS_ERR_DEVICE, "[E::fcship] stream creation failed");
-  DevBuf qb, qo, ql, tb, to, tl, h0, w, sc, zb, zo, cg, co, cc, nc;
+  Session* S = session(device);
+  if (!S) return fail(FCS_ERR_DEVICE, "[E::fcship] stream creation failed");
   const size_t nn = (size_t)n;
-  if ((rc = upload(qb, pk.q.data(), pk.q.size(), s)) || (rc = upload(qo, pk.qoff.data(), 8 * nn, s)) ||
-      (rc = upload(ql, pk.qlen.data(), 4 * nn, s)) || (rc = upload(tb, pk.t.data(), pk.t.size(), s)) ||
-      (rc = upload(to, pk.toff.data(), 8 * nn, s)) || (rc = upload(tl, pk.tlen.data(), 4 * nn, s)) ||
-      (rc = upload(h0, pk.h0.data(), 4 * nn, s)) || (rc = upload(w, pk.w.data(), 4 * nn, s)) ||
-      (rc = sc.alloc(4 * nn)) || (rc = zb.alloc((size_t)zt)) || (rc = upload(zo, zoff.data(), 8 * nn, s)))
-    return rc;
+  // The direction matrix (and its offsets) only when CIGARs are wanted: a
+  // scores-only batch needs none of it.
+  Layout L;
+  const size_t oq = L.add(pk.q.size()), oqo = L.add(8 * nn), oql = L.add(4 * nn), ot = L.add(pk.t.size()),
+               oto = L.add(8 * nn), otl = L.add(4 * nn), oh0 = L.add(4 * nn), ow = L.add(4 * nn);
+  const size_t ozo = want_cigar ? L.add(8 * nn) : 0, oco = want_cigar ? L.add(8 * nn) : 0,
+               occ = want_cigar ? L.add(4 * nn) : 0;
+  const size_t in_bytes = L.total, osc = L.add(4 * nn), onc = L.add(4 * nn), ocg = L.add(4 * (size_t)ct),
+               ozb = want_cigar ? L.add((size_t)zt) : 0;
+  if ((rc = S->ensure_host(in_bytes + 8 * nn + 4 * (size_t)ct + 1024)) || (rc = S->ensure_dev(L.total))) return rc;
+  std::memcpy(S->h<void>(oq), pk.q.data(), pk.q.size());
+  std::memcpy(S->h<void>(oqo), pk.qoff.data(), 8 * nn);
+  std::memcpy(S->h<void>(oql), pk.qlen.data(), 4 * nn);
+  std::memcpy(S->h<void>(ot), pk.t.data(), pk.t.size());
+  std::memcpy(S->h<void>(oto), pk.toff.data(), 8 * nn);
+  std::memcpy(S->h<void>(otl), pk.tlen.data(), 4 * nn);
+  std::memcpy(S->h<void>(oh0), pk.h0.data(), 4 * nn);
+  std::memcpy(S->h<void>(ow), pk.w.data(), 4 * nn);
   if (want_cigar) {
-    if ((rc = cg.alloc(4 * (size_t)ct)) || (rc = upload(co, cigar_off, 8 * nn, s)) ||
-        (rc = upload(cc, cigar_cap, 4 * nn, s)) || (rc = nc.alloc(4 * nn)))
-      return rc;
+    std::memcpy(S->h<void>(ozo), zoff.data(), 8 * nn);
+    std::memcpy(S->h<void>(oco), cigar_off, 8 * nn);
+    std::memcpy(S->h<void>(occ), cigar_cap, 4 * nn);
   }
+  hipStream_t s = S->s;
+  FCS_HIP_CHECK(hipMemcpyAsync(S->dev, S->host, in_bytes, hipMemcpyHostToDevice, s));
   BswDevBatch d;
-  d.qbuf = qb.as<uint8_t>();
-  d.qoff = qo.as<int64_t>();
-  d.qlen = ql.as<int32_t>();
-  d.tbuf = tb.as<uint8_t>();
-  d.toff = to.as<int64_t>();
-  d.tlen = tl.as<int32_t>();
-  d.h0 = h0.as<int32_t>();
-  d.w = w.as<int32_t>();
+  d.qbuf = S->d<uint8_t>(oq);
+  d.qoff = S->d<int64_t>(oqo);
+  d.qlen = S->d<int32_t>(oql);
+  d.tbuf = S->d<uint8_t>(ot);
+  d.toff = S->d<int64_t>(oto);
+  d.tlen = S->d<int32_t>(otl);
+  d.h0 = S->d<int32_t>(oh0);
+  d.w = S->d<int32_t>(ow);
   d.n = n;
-  rc = launch_bsw_global(d, to_params(params), mq, mt, sc.as<int32_t>(), want_cigar ? zb.as<uint8_t>() : nullptr,
-                         zt, zo.as<int64_t>(), want_cigar ? cg.as<uint32_t>() : nullptr, co.as<int64_t>(),
-                         cc.as<int32_t>(), nc.as<int32_t>(), s);
+  rc = launch_bsw_global(d, to_params(params), mq, mt, S->d<int32_t>(osc), want_cigar ? S->d<uint8_t>(ozb) : nullptr,
+                         zt, want_cigar ? S->d<int64_t>(ozo) : nullptr, want_cigar ? S->d<uint32_t>(ocg) : nullptr,
+                         want_cigar ? S->d<int64_t>(oco) : nullptr, want_cigar ? S->d<int32_t>(occ) : nullptr,
+                         want_cigar ? S->d<int32_t>(onc) : nullptr, s);
   if (rc) return rc;
-  FCS_HIP_CHECK(hipMemcpyAsync(scores, sc.p, 4 * nn, hipMemcpyDeviceToHost, s));
-  if (want_cigar) {
-    FCS_HIP_CHECK(hipMemcpyAsync(n_cigar, nc.p, 4 * nn, hipMemcpyDeviceToHost, s));
-    if (ct) FCS_HIP_CHECK(hipMemcpyAsync(cigar_arena, cg.p, 4 * (size_t)ct, hipMemcpyDeviceToHost, s));
-  }
+  // scores, counts and the CIGAR arena are contiguous in the layout
+  const size_t back = want_cigar ? ocg + 4 * (size_t)ct - osc : 4 * nn;
+  FCS_HIP_CHECK(hipMemcpyAsync(S->h<void>(in_bytes), S->d<void>(osc), back, hipMemcpyDeviceToHost, s));
   FCS_HIP_CHECK(hipStreamSynchronize(s));
-  if (want_cigar)
+  const char* hb = S->h<char>(in_bytes);
+  std::memcpy(scores, hb, 4 * nn);
+  if (want_cigar) {
+    std::memcpy(n_cigar, hb + (onc - osc), 4 * nn);
+    if (ct) std::memcpy(cigar_arena, hb + (ocg - osc), 4 * (size_t)ct);
     for (int32_t k = 0; k < n; ++k)
       if (n_cigar[k] > cigar_cap[k])
         return fail(FCS_ERR_INVALID, "[E::fcs_bsw_global] CIGAR longer than its arena slot");
+  }
   return FCS_OK;
 }
 

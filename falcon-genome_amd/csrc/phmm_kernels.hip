@@ -21,11 +21,11 @@
 //     the previous stripe (8 bytes per column); stripe 0 reads the ring
 //     initialised with row 0 (X = (2^120/H)*gm_1, I = 0);
 //   * each lane reads its hap base for column t - l from an LDS byte array
-//     (LDS pipe, four steps ahead) instead of passing it between lanes;
+//     (LDS pipe, two steps ahead) instead of passing it between lanes;
 //   * idle cells (c <= 0) compute exact zeros by construction, so a step has
 //     no predicates; the lane holding the read's last row sums M and I in
 //     column order like GKL's vector kernel.
-// Steps are unrolled in blocks of 16, the ring is read four steps ahead and the
+// Steps are unrolled in blocks of 16, the ring is read two steps ahead and the
 // next stripe's row parameters are gathered while the current stripe runs.
 // Compiled with -ffp-contract=off: the EXACT variant keeps GKL's operation
 // order bit-for-bit, the fast variant uses explicit fma().
@@ -39,6 +39,14 @@
 
 namespace fcs {
 
+// Ring / hap read-ahead in steps.  Two steps hide the LDS latency (one does
+// not: -8%) and, as a shift register, let every ring read land in the register
+// its DPP `old` operand needs: the four-deep rotation cost two v_mov per step
+// and spilled 2 VGPRs; 2, 3 and 4 measured within 0.5% (gpurun_out/abp2).
+#ifndef FCS_PHMM_PFD
+#define FCS_PHMM_PFD 2
+#endif
+constexpr int PFD = FCS_PHMM_PFD;
 template <typename T> struct alignas(2 * sizeof(T)) PhRing {
   T X, I;
 };
@@ -88,15 +96,20 @@ struct LaneState {
 
 // One anti-diagonal step at t = t0 + S.
 template <typename T, bool EXACT, bool SUM, bool BC, bool COND, int S>
-__device__ __forceinline__ void phmm_step(LaneState<T>& L, PhRing<T> (&pf)[4], int (&hq)[4],
+__device__ __forceinline__ void phmm_step(LaneState<T>& L, PhRing<T> (&pf)[PFD], int (&hq)[PFD],
                                           const unsigned char* __restrict__ hapl, const RowP<T>& p,
                                           PhRing<T>* __restrict__ ring, const int t0, const int sl, const bool top,
                                           const int lim, T& accM, T& accI) {
   const int t = t0 + S;
-  const PhRing<T> cur = pf[S & 3];
-  pf[S & 3] = ring[t + 20];  // lane-0 input for column t + 4
-  const int hb = hq[S & 3];
-  hq[S & 3] = hapl[t + 20 - sl];  // this lane's hap base for column t + 4 - l
+  const PhRing<T> cur = pf[0];
+  const int hb = hq[0];
+#pragma unroll
+  for (int k = 0; k + 1 < PFD; ++k) {
+    pf[k] = pf[k + 1];
+    hq[k] = hq[k + 1];
+  }
+  pf[PFD - 1] = ring[t + 16 + PFD];  // lane-0 input for column t + PFD
+  hq[PFD - 1] = hapl[t + 16 + PFD - sl];  // this lane's hap base for column t + PFD - l
   const T Xu = dpp_row_shr1<T>(cur.X, L.Xo);
   const T I = dpp_row_shr1<T>(cur.I, L.Io);
   T prior;
@@ -143,7 +156,7 @@ __device__ __forceinline__ void phmm_step(LaneState<T>& L, PhRing<T> (&pf)[4], i
 }
 
 template <typename T, bool EXACT, bool SUM, bool BC, bool COND>
-__device__ __forceinline__ void phmm_block(LaneState<T>& L, PhRing<T> (&pf)[4], int (&hq)[4],
+__device__ __forceinline__ void phmm_block(LaneState<T>& L, PhRing<T> (&pf)[PFD], int (&hq)[PFD],
                                            const unsigned char* __restrict__ hapl, const RowP<T>& p,
                                            PhRing<T>* __restrict__ ring, const int t0, const int sl, const bool top,
                                            const int lim, T& accM, T& accI) {
@@ -207,14 +220,14 @@ template <typename T, bool EXACT, bool SUM, bool BC>
 __device__ __forceinline__ void phmm_stripe(const RowP<T>& p, PhRing<T>* __restrict__ ring,
                                             const unsigned char* __restrict__ hapl, const int sl, const int nblk,
                                             const int lim, const int ulim, T& accM, T& accI,
-                                            const PhmmTables<T>& tab, const RawRow& nraw, RowP<T>& np) {
-  const bool top = sl == 15;
+                                            const PhmmTables<T>& tab, const RawRow& nraw, RowP<T>& np,
+                                            const bool top) {
   LaneState<T> L;
   L.Mo = L.Do = L.Xp = L.Xo = L.Io = (T)0;
-  PhRing<T> pf[4];
-  int hq[4];
+  PhRing<T> pf[PFD];
+  int hq[PFD];
 #pragma unroll
-  for (int k = 0; k < 4; ++k) {
+  for (int k = 0; k < PFD; ++k) {
     pf[k] = ring[16 + k];
     hq[k] = hapl[16 + k - sl];
   }
@@ -250,24 +263,31 @@ __global__ __launch_bounds__(64, (sizeof(T) == 4 && !EXACT) ? 4 : 1) void phmm_k
                                                   const int cls, const int nslot, const PhmmTables<T> tab,
                                                   double* __restrict__ out, int32_t* __restrict__ rescue_list,
                                                   unsigned long long* __restrict__ rescue_count, const float thr,
-                                                  const int use_rescue) {
+                                                  const int use_rescue, const int nseg) {
   extern __shared__ __align__(16) unsigned char smem_raw[];
   const int lane = threadIdx.x;
   const int seg = lane >> 4;
   const int sl = lane & 15;
-  PhRing<T>* const ring = reinterpret_cast<PhRing<T>*>(smem_raw + seg * ring_stride<T>(nslot));
-  unsigned char* const hapl = smem_raw + (size_t)4 * ring_stride<T>(nslot) + seg * nslot;
+  // nseg = 4: four pairs per wave, one LDS ring each.  nseg = 1 (haplotypes too
+  // long for four rings in 160 KB): one pair per wave, segments 1..3 idle on
+  // segment 0's ring (they never write it: `top` and the setup are theirs only
+  // when seg < nseg).
+  const bool own_seg = seg < nseg;
+  const int rseg = own_seg ? seg : 0;
+  PhRing<T>* const ring = reinterpret_cast<PhRing<T>*>(smem_raw + rseg * ring_stride<T>(nslot));
+  unsigned char* const hapl = smem_raw + (size_t)nseg * ring_stride<T>(nslot) + rseg * nslot;
+  const bool top = own_seg && sl == 15;
   // forward pass: this launch's hap-length class of the sorted schedule; rescue: the device-side list count
   long long count = count_dev ? (long long)(*count_dev) : count_host;
   if (bounds) {
     order += bounds[cls];
     count = bounds[cls + 1] - bounds[cls];
   }
-  const long long ngroups = (count + 3) >> 2;
+  const long long ngroups = (count + nseg - 1) / nseg;
 
   for (long long g = blockIdx.x; g < ngroups; g += gridDim.x) {
-    const long long idx = g * 4 + seg;
-    const int p = (idx < count) ? order[idx] : -1;
+    const long long idx = g * nseg + seg;
+    const int p = (own_seg && idx < count) ? order[idx] : -1;
     int R = 0, H = 0;
     int64_t ro = 0, ho = 0;
     if (p >= 0) {
@@ -307,7 +327,7 @@ __global__ __launch_bounds__(64, (sizeof(T) == 4 && !EXACT) ? 4 : 1) void phmm_k
 #pragma unroll
       for (int u = 0; u < kHB; ++u) {
         const int s = s0 + 16 * u, c = s - 16;
-        if (s < nslot) {
+        if (own_seg && s < nslot) {
           PhRing<T> v;
           v.X = (c >= 0 && c <= H) ? x0 : (T)0;
           v.I = 0;
@@ -320,7 +340,7 @@ __global__ __launch_bounds__(64, (sizeof(T) == 4 && !EXACT) ? 4 : 1) void phmm_k
       }
     }
     const bool bytecmp = __ballot(other) != 0ull;
-    if (bytecmp)
+    if (bytecmp && own_seg)
       for (int s = sl; s < nslot; s += 16) {
         const int c = s - 16;
         hapl[s] = (active && c >= 1 && c <= H) ? b.hb[ho + c - 1] : (unsigned char)0;
@@ -346,9 +366,9 @@ __global__ __launch_bounds__(64, (sizeof(T) == 4 && !EXACT) ? 4 : 1) void phmm_k
         RowP<T> sp = prm;  // the last row's D feeds only rows past R: reuse it as the M sum
         if (lim >= 0) sp.my = sp.yy = (T)1;
         if (bytecmp)
-          phmm_stripe<T, EXACT, true, true>(sp, ring, hapl, sl, (tend + 16) >> 4, lim, ulim, accM, accI, tab, nraw, nprm);
+          phmm_stripe<T, EXACT, true, true>(sp, ring, hapl, sl, (tend + 16) >> 4, lim, ulim, accM, accI, tab, nraw, nprm, top);
         else
-          phmm_stripe<T, EXACT, true, false>(sp, ring, hapl, sl, (tend + 16) >> 4, lim, ulim, accM, accI, tab, nraw, nprm);
+          phmm_stripe<T, EXACT, true, false>(sp, ring, hapl, sl, (tend + 16) >> 4, lim, ulim, accM, accI, tab, nraw, nprm, top);
         if (seg_sums && sl == sum_lane) {
           const T sum = accM + accI;
           if constexpr (RESCUE_PASS) {
@@ -365,9 +385,9 @@ __global__ __launch_bounds__(64, (sizeof(T) == 4 && !EXACT) ? 4 : 1) void phmm_k
         }
       } else {
         if (bytecmp)
-          phmm_stripe<T, EXACT, false, true>(prm, ring, hapl, sl, (Hmax + 31) >> 4, -1, -1, accM, accI, tab, nraw, nprm);
+          phmm_stripe<T, EXACT, false, true>(prm, ring, hapl, sl, (Hmax + 31) >> 4, -1, -1, accM, accI, tab, nraw, nprm, top);
         else
-          phmm_stripe<T, EXACT, false, false>(prm, ring, hapl, sl, (Hmax + 31) >> 4, -1, -1, accM, accI, tab, nraw, nprm);
+          phmm_stripe<T, EXACT, false, false>(prm, ring, hapl, sl, (Hmax + 31) >> 4, -1, -1, accM, accI, tab, nraw, nprm, top);
       }
       prm = nprm;
     }
@@ -375,7 +395,7 @@ __global__ __launch_bounds__(64, (sizeof(T) == 4 && !EXACT) ? 4 : 1) void phmm_k
 }
 
 // Slots (ring entries and hap bytes) = column + 16 for columns -16 .. Hmax + 34:
-// stripes run to Hmax + 15 rounded up to a 16-step block, plus four steps of
+// stripes run to Hmax + 15 rounded up to a 16-step block, plus up to four steps of
 // read-ahead.
 static __host__ __device__ int nslot_for(int max_hap_len) { return ((max_hap_len + 51 + 15) / 16) * 16; }
 
@@ -434,14 +454,25 @@ int launch_phmm_bounds(const uint32_t* sorted_keys, int64_t n, int64_t* bounds, 
   return FCS_OK;
 }
 
+constexpr size_t kLdsBytes = 160 * 1024;
+
 template <typename T, bool EXACT, bool RESCUE>
 static int launch_one(const PhmmDevBatch& b, const int32_t* order, const unsigned long long* count_dev,
                       long long count_host, const int64_t* bounds, int cls, int nslot, long long max_groups,
                       const PhmmTables<T>& tab, double* out, int32_t* rescue_list, unsigned long long* rescue_count,
                       float thr, bool use_rescue, hipStream_t s) {
-  const size_t lds = (size_t)4 * (ring_stride<T>(nslot) + nslot);
-  if (lds > 160 * 1024)
-    return fail(FCS_ERR_UNSUPPORTED, "[E::fcship] max_hap_len too large for the LDS boundary ring");
+  // Four rings per wave when they fit the 160 KB of LDS, else one (long
+  // haplotypes: fp32 up to ~4.5 kb at four, ~18 kb at one; fp64 ~2.3 / ~9.5 kb).
+  int nseg = 4;
+  size_t lds = (size_t)4 * (ring_stride<T>(nslot) + nslot);
+  if (lds > kLdsBytes) {
+    nseg = 1;
+    lds = (size_t)ring_stride<T>(nslot) + nslot;
+    max_groups *= 4;
+  }
+  if (lds > kLdsBytes)
+    return fail(FCS_ERR_UNSUPPORTED, "[E::fcship] haplotype too long for the LDS boundary ring (max_hap_len " +
+                                         std::to_string(nslot - 67) + ")");
   auto kern = phmm_kernel<T, EXACT, RESCUE>;
   if (lds > 64 * 1024)
     FCS_HIP_CHECK(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
@@ -455,7 +486,7 @@ static int launch_one(const PhmmDevBatch& b, const int32_t* order, const unsigne
   if (grid > cap) grid = cap;
   if (grid < 1) grid = 1;
   hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(64), lds, s, b, order, count_dev, count_host, bounds, cls, nslot,
-                     tab, out, rescue_list, rescue_count, thr, use_rescue ? 1 : 0);
+                     tab, out, rescue_list, rescue_count, thr, use_rescue ? 1 : 0, nseg);
   FCS_HIP_CHECK(hipGetLastError());
   return FCS_OK;
 }

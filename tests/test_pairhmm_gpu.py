@@ -274,3 +274,52 @@ def test_concurrent_region_calls_match_serial(gpu):
         t.join()
     assert not errors, errors
     assert all(g is None for g in got), [j for j, g in enumerate(got) if g is not None]
+
+
+@pytest.mark.parametrize("hlen", [2600, 5200])
+def test_long_haplotypes(gpu, hlen):
+    """a batch with a haplotype longer than four fp64 rings fit in
+    LDS (~2.3 kb) no longer fails; beyond ~4.5 kb the fp32 pass also switches
+    to one pair per wave.  Unrelated high-quality reads make the fp64 rescue
+    fire on the long haplotypes too."""
+    rng = np.random.default_rng(hlen)
+    haps = [rng.choice(np.frombuffer(b"ACGT", np.uint8), n) for n in (hlen, 300, hlen - 7)]
+    reads = []
+    for i in range(12):
+        R = int(rng.integers(90, 152))
+        rd = list(rand_read(rng, R))
+        if i % 2 == 0:
+            rd[0] = mutate(rng, haps[i % 3], R)
+        else:
+            rd[1][:] = 40
+            rd[2][:] = rd[3][:] = 60
+        reads.append(tuple(rd))
+    p = fcship.make_pairs(reads, haps)
+    for exact in (False, True):
+        out = fcship.phmm_compute_pairs(p, exact=exact)
+        used = check_parity(p, out, exact)
+        assert used.sum() > 0, "the fp64 rescue must run on long haplotypes"
+
+
+def test_unwritten_results_are_an_error(gpu, tmp_path):
+    """a schedule that drops pairs (the round-1 null-stream memset
+    race zeroed the class bounds) must fail loudly, not return garbage: the
+    host paths pre-fill outputs with NaN and count what the device left."""
+    import subprocess
+    import sys
+    code = (
+        "import sys; sys.path.insert(0, %r)\n"
+        "import numpy as np, fcship\n"
+        "p = fcship.synth_phmm(7, 256)\n"
+        "try:\n"
+        "    fcship.phmm_compute_pairs(p)\n"
+        "    print('NO ERROR')\n"
+        "except fcship.FcsError as e:\n"
+        "    print('ERR', e)\n"
+    ) % fcship.__file__.rsplit("/", 1)[0]
+    env = dict(__import__("os").environ, FCSHIP_TEST_FAULT="drop_schedule")
+    r = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=120)
+    assert "ERR" in r.stdout and "256 of 256 results were not written" in r.stdout, (r.stdout, r.stderr[-2000:])
+    # and without the fault the same batch is fine
+    p = fcship.synth_phmm(7, 256)
+    assert np.isfinite(fcship.phmm_compute_pairs(p)).all()
