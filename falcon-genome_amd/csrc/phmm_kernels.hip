@@ -394,6 +394,12 @@ __global__ __launch_bounds__(64, (sizeof(T) == 4 && !EXACT) ? 4 : 1) void phmm_k
   }
 }
 
+}  // namespace fcs
+
+#include "phmm2.h"
+
+namespace fcs {
+
 // Slots (ring entries and hap bytes) = column + 16 for columns -16 .. Hmax + 34:
 // stripes run to Hmax + 15 rounded up to a 16-step block, plus up to four steps of
 // read-ahead.
@@ -507,6 +513,22 @@ int launch_phmm_forward(const PhmmDevBatch& b, const int32_t* order, int64_t cou
     const int c = kPhmmClasses - 1 - j;
     const int ns = (c == kPhmmClasses - 1) ? ns_max : std::min(224 + 32 * c, ns_max);
     hipStream_t st = fs[j % kForkStreams];
+#ifndef FCS_PHMM_ONEROW
+    // the two-rows-per-lane kernel (phmm2.h) for the FMA-order pass when its
+    // four rings fit (ring slots >= H + 65, hap bytes + 16)
+    const int ns2 = ns + 16;
+    const size_t lds2 = (size_t)phmm2_lds(ns2);
+    if (!exact && lds2 <= kLdsBytes) {
+      if (lds2 > 64 * 1024)
+        FCS_HIP_CHECK(
+            hipFuncSetAttribute((const void*)phmm2_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds2));
+      const unsigned grid = (unsigned)std::min<long long>(std::max<long long>(groups, 1), 65536);
+      hipLaunchKernelGGL(phmm2_kernel, dim3(grid), dim3(64), lds2, st, b, order, bounds, j, ns2, t.tf, out,
+                         rescue_list, rescue_count, thr, use_rescue ? 1 : 0);
+      FCS_HIP_CHECK(hipGetLastError());
+      continue;
+    }
+#endif
     const int rc = exact ? launch_one<float, true, false>(b, order, nullptr, count, bounds, j, ns, groups, t.tf, out,
                                                            rescue_list, rescue_count, thr, use_rescue, st)
                          : launch_one<float, false, false>(b, order, nullptr, count, bounds, j, ns, groups, t.tf, out,

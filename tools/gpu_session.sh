@@ -35,6 +35,17 @@ for step in "$@"; do
             python3 "$ROOT/tools/bsw_bench.py" --which c3 --reps 1 &&
             run bswpmc_fixed 300 rocprofv3 --pmc SQ_INSTS_VALU -d "$OUT/bswpmc_fixed" -o run --output-format csv -- \
             python3 "$ROOT/tools/bsw_bench.py" --which fixed --reps 1 ;;
+    phmmpmc)  # PairHMM C2 forward pass: SQ issue/stall counters, then HBM bytes (separate passes)
+      run phmmpmc_sq 300 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_BUSY_CYCLES \
+            SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY -d "$OUT/phmmpmc_sq" -o run --output-format csv -- \
+            python3 "$ROOT/tools/phmm_bench.py" --steps 1 --warmup 1 &&
+      run phmmpmc_sq2 300 rocprofv3 --pmc SQ_WAIT_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_INST_CYCLES_SALU \
+            SQ_LDS_BANK_CONFLICT -d "$OUT/phmmpmc_sq2" -o run --output-format csv -- \
+            python3 "$ROOT/tools/phmm_bench.py" --steps 1 --warmup 1 &&
+      run phmmpmc_fetch 300 rocprofv3 --pmc FETCH_SIZE -d "$OUT/phmmpmc_fetch" -o run --output-format csv -- \
+            python3 "$ROOT/tools/phmm_bench.py" --steps 1 --warmup 1 &&
+      run phmmpmc_write 300 rocprofv3 --pmc WRITE_SIZE -d "$OUT/phmmpmc_write" -o run --output-format csv -- \
+            python3 "$ROOT/tools/phmm_bench.py" --steps 1 --warmup 1 ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac
 done
