@@ -61,6 +61,17 @@ def bsw_dev_batch(t: "fcship.BswTasks", dev):
     return b, keep
 
 
+def load_pmc_phmm():
+    """Measured issue counters of the fp32 forward pass (profiles/pmc_phmm.json,
+    written by tools/profile_summary.py from rocprofv3 --pmc passes)."""
+    try:
+        with open(os.path.join(ROOT, "profiles", "pmc_phmm.json")) as f:
+            d = json.load(f)
+        return d["phmm_fwd_fp32"], d.get("source")
+    except (OSError, ValueError, KeyError):
+        return {}, None
+
+
 def load_traffic(name):
     """Per-launch HBM bytes of a kernel from a committed rocprofv3 PMC summary."""
     path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
@@ -289,7 +300,9 @@ def main():
     value = total_cells / ph["elapsed"] / 1e9
     fwd_s = ph["fwd_ms"] * 1e-3
     achieved_tf = FLOPS_PER_CELL * ph["cells"] / fwd_s / 1e12
-    traffic = load_traffic("phmm_kernel<float,false,false>")
+    traffic = load_traffic("phmm_fwd_fp32")
+    pmc, pmc_src = load_pmc_phmm()
+    vipc = pmc.get("valu_lane_instr_per_cell")
     p = ph["p"]
     alg_bytes = int(5 * p.read_len.sum() + p.hap_len.sum() + 4 * p.n_pairs + 8 * p.n_pairs)
 
@@ -315,11 +328,14 @@ def main():
         "roofline": {"bound": "valu", "achieved": round(achieved_tf, 3), "peak": FP32_VECTOR_PEAK_TF,
                      "unit": "TFLOP/s", "frac": round(achieved_tf / FP32_VECTOR_PEAK_TF, 4),
                      "traffic": traffic,
-                     "kernel": "phmm_kernel<float,false,false>: fp32 forward pass = one launch per hap-length "
-                               "class, overlapped on 4 streams; achieved = algorithmic FLOPs / pass time (HIP events "
-                               "on the launch stream; rocprof pass span in profiles/r1/r1j_phmm_summary.json)",
-                     "valu_instr_per_cell": 12.0,
-                     "valu_issue_frac": round(ph["cells"] / fwd_s * 12.0 / VALU_LANE_INSTR_PEAK, 4),
+                     "kernel": "phmm2_kernel (two read rows per lane, packed FP32): fp32 forward pass = one launch "
+                               "per hap-length class, overlapped on 4 streams; achieved = algorithmic FLOPs / pass "
+                               "time (HIP events on the launch stream; rocprof pass span in "
+                               "profiles/r2/r2b_phmm_summary.json)",
+                     "valu_instr_per_cell": vipc,
+                     "valu_issue_frac": (round(ph["cells"] / fwd_s * vipc / VALU_LANE_INSTR_PEAK, 4) if vipc
+                                         else None),
+                     "valu_source": f"profiles/pmc_phmm.json ({pmc_src}: SQ_INSTS_VALU x 64 / cells)",
                      "kernel_gcups": round(ph["cells"] / fwd_s / 1e9, 3),
                      "algorithmic_bytes_per_launch": alg_bytes,
                      "algorithmic_hbm_GBs": round(alg_bytes / fwd_s / 1e9, 2),

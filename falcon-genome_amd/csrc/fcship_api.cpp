@@ -22,6 +22,7 @@
 namespace fcs {
 
 static thread_local std::string g_last_error;
+static thread_local int64_t g_last_rescued = 0;
 void set_error(const std::string& msg) { g_last_error = msg; }
 int fail(int code, const std::string& msg) {
   set_error(msg);
@@ -539,6 +540,12 @@ int fcs_phmm_dev_run(fcs_phmm_plan* plan, const fcs_phmm_batch* b, double* out, 
   return fcs_phmm_dev_rescue(plan, b, out, opts, stream);
 }
 
+int fcs_phmm_last_rescued(int64_t* count) {
+  if (!count) return fail(FCS_ERR_INVALID, "[E::fcs_phmm_last_rescued] null count");
+  *count = g_last_rescued;
+  return FCS_OK;
+}
+
 int fcs_phmm_plan_rescue_count(fcs_phmm_plan* plan, void* stream, int64_t* count) {
   if (!plan || !count) return fail(FCS_ERR_INVALID, "[E::fcs_phmm_plan_rescue_count] bad arguments");
   FCS_HIP_CHECK(hipSetDevice(plan->device));
@@ -615,7 +622,13 @@ int phmm_staged(const PhmmStage& g, const fcs_phmm_opts& opts, Fill&& fill, cons
   if ((rc = fcs_phmm_dev_run(S->phmm, &d, dout, &opts, s))) return rc;
   double* hout = S->h<double>(out_off);
   FCS_HIP_CHECK(hipMemcpyAsync(hout, dout, 8 * np, hipMemcpyDeviceToHost, s));
+  // into the input staging: its H2D copy is stream-ordered before this copy
+  unsigned long long* hres = S->h<unsigned long long>(0);
+  g_last_rescued = 0;
+  if (opts.use_fp64_rescue)
+    FCS_HIP_CHECK(hipMemcpyAsync(hres, S->phmm->rescue_count, sizeof(*hres), hipMemcpyDeviceToHost, s));
   FCS_HIP_CHECK(hipStreamSynchronize(s));
+  if (opts.use_fp64_rescue) g_last_rescued = (int64_t)*hres;
   int64_t missing = 0;
   for (size_t k = 0; k < np; ++k) missing += std::isnan(hout[k]);
   if (missing)
@@ -1117,6 +1130,6 @@ int fcs_ksw_global2(int qlen, const uint8_t* query, int tlen, const uint8_t* tar
   return score;
 }
 
-int fcs_abi_symbol_count(void) { return 30; }
+int fcs_abi_symbol_count(void) { return 31; }
 
 }  // extern "C"

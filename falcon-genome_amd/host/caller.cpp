@@ -21,6 +21,7 @@ void CallerStats::add(const CallerStats& o) {
   cells += o.cells;
   calls += o.calls;
   device_passes += o.device_passes;
+  rescued += o.rescued;
   seconds += o.seconds;
   phmm_seconds += o.phmm_seconds;
 }
@@ -262,6 +263,8 @@ void run_phmm(std::vector<std::unique_ptr<Region>>& batch, const CallerOptions& 
   st.phmm_seconds += (now_us() - t0) / 1e6;
   ++st.device_passes;
   if (rc != FCS_OK) throw failedCommand(std::string(fcs_last_error()));
+  int64_t nres = 0;
+  if (fcs_phmm_last_rescued(&nres) == FCS_OK) st.rescued += nres;
   if (dump)
     for (const auto& g : batch)
       for (int s = 0; s < 2; ++s)

@@ -45,6 +45,7 @@ struct CallerOptions {
 
 struct CallerStats {
   int64_t reads = 0, regions = 0, pairs = 0, cells = 0, calls = 0, device_passes = 0;
+  int64_t rescued = 0;  // pairs the fp64 rescue recomputed (fp32 sum < 1e-28)
   double seconds = 0, phmm_seconds = 0;
   void add(const CallerStats& o);
 };

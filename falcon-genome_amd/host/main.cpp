@@ -194,6 +194,7 @@ int mutect2_main(int argc, char** argv) {
   a.add("sample-id", "", false, false, "sample id for log file");
   for (const char* k : {"dbsnp", "cosmic", "germline", "panels_of_normals", "contamination_table", "filtered_vcf"})
     a.add(k, "", false, false, "accepted for compatibility (not used by the GPU caller)");
+  a.add("dump-regions", "", false, false, "debug: write every region's PairHMM inputs/outputs to <path>.<shard>");
   try {
     a.parse(argc, argv);
   } catch (helpRequest&) {
@@ -208,11 +209,13 @@ int mutect2_main(int argc, char** argv) {
   Executor ex("Mutect2", conf().get_int("gatk.mutect2.nprocs", "gatk.nprocs"), gpus);
   std::vector<std::string> parts;
   const std::string sample_id = a.get("sample-id");
+  std::vector<std::string> extra = a.all("extra-options");
+  if (a.has("dump-regions")) extra.push_back("--dump-regions " + a.get("dump-regions"));
   for (size_t k = 0; k < shards.size(); ++k) {
     const std::string part = get_contig_fname(out_dir, (int)k, "vcf");
     parts.push_back(part);
-    ex.addTask(std::make_shared<Mutect2Worker>(ref, shards[k], a.get("normal"), a.get("tumor"), part,
-                                               a.all("extra-options"), (int)k, true),
+    ex.addTask(std::make_shared<Mutect2Worker>(ref, shards[k], a.get("normal"), a.get("tumor"), part, extra, (int)k,
+                                               true),
                sample_id);
   }
   ex.addTask(std::make_shared<VCFConcatWorker>(parts, output), sample_id, true);
@@ -232,6 +235,7 @@ int synth_main(int argc, char** argv) {
   a.add("tumor", "T", true, false, "also write tumor.bam with somatic variants (C5)");
   a.add("tumor-coverage", "", false, false, "tumor coverage (default 40)");
   a.add("somatic-af", "", false, false, "somatic allele fraction (default 0.3)");
+  a.add("noisy-frac", "", false, false, "fraction of reads drawn with 20% high-quality mismatches (mis-mapped-like)");
   a.add("spike", "", false, false, "chr:pos[,chr:pos...] plant three het SNVs at pos-30, pos, pos+30 (1-based)");
   a.parse(argc, argv);
   SynthSpec sp;
@@ -259,6 +263,7 @@ int synth_main(int argc, char** argv) {
       p = e + 1;
     }
   }
+  if (a.has("noisy-frac")) sp.noisy_frac = std::stod(a.get("noisy-frac"));
   if (a.has("coverage")) sp.coverage = std::stod(a.get("coverage"));
   if (a.has("seed")) sp.seed = std::stoull(a.get("seed"));
   if (a.has("max-reads")) sp.max_reads = std::stoll(a.get("max-reads"));

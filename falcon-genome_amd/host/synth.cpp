@@ -265,6 +265,12 @@ SynthOutputs synth_dataset(const SynthSpec& spec, const std::string& dir) {
         const int64_t s = (int64_t)hr.below(hp.seq.size() - L);
         SimRead sr;
         if (!make_read(hp, s, L, hr, spec.err_rate, sr)) continue;
+        if (spec.noisy_frac > 0 && hr.uniform() < spec.noisy_frac)
+          for (size_t i = 0; i < sr.rec.seq.size(); ++i)
+            if (hr.uniform() < 0.2) {
+              sr.rec.seq[i] = other_base(hr, sr.rec.seq[i]);
+              sr.rec.qual[i] = (uint8_t)(35 + hr.below(6));
+            }
         sr.rec.ref_id = (int32_t)c;
         sr.rec.name = sample + ":" + std::to_string(idx++);
         const bool rev = hr.uniform() < 0.5;

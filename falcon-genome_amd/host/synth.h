@@ -35,6 +35,9 @@ struct SynthSpec {
   double somatic_rate = 0;  // > 0: also write a tumor BAM with somatic variants at somatic_af
   double somatic_af = 0.3;
   double tumor_coverage = 40.0;
+  // reads drawn as if mis-mapped from a paralog: 20% mismatches at Q35-40
+  // (their PairHMM likelihoods underflow the fp32 pass: C5's fp64 rescue)
+  double noisy_frac = 0;
   // planted clusters: three het SNVs at centre - 30, centre, centre + 30
   // (0-based), replacing random variants within 100 bp (shard-boundary tests)
   std::vector<std::pair<std::string, int64_t>> spikes;

@@ -83,11 +83,11 @@ int HTCWorker::run(TaskContext& ctx) {
   out.close();
   if (ctx.log)
     std::fprintf(ctx.log,
-                 "[fcs-genome htc] shard %d gpu %d: %lld reads, %lld regions, %lld pairs, %lld cells, %lld calls, "
-                 "%.3f s (PairHMM %.3f s, %lld device passes)\n",
+                 "[fcs-genome htc] shard %d gpu %d: %lld reads, %lld regions, %lld pairs, %lld cells, %lld rescued, "
+                 "%lld calls, %.3f s (PairHMM %.3f s, %lld device passes)\n",
                  contig_, ctx.gpu, (long long)stats_.reads, (long long)stats_.regions, (long long)stats_.pairs,
-                 (long long)stats_.cells, (long long)stats_.calls, stats_.seconds, stats_.phmm_seconds,
-                 (long long)stats_.device_passes);
+                 (long long)stats_.cells, (long long)stats_.rescued, (long long)stats_.calls, stats_.seconds,
+                 stats_.phmm_seconds, (long long)stats_.device_passes);
   return 0;
 }
 
@@ -116,14 +116,19 @@ int Mutect2Worker::run(TaskContext& ctx) {
   auto ref = load_reference_cached(ref_path_);
   CallerOptions opt = caller_options_from_config(ctx.gpu);
   opt.somatic = true;
+  auto it = extra_opts_.find("--dump-regions");
+  if (it != extra_opts_.end() && !it->second.empty()) opt.dump_path = it->second[0] + "." + std::to_string(contig_);
   const VcfHeader h = caller_vcf_header(*ref, {"TUMOR", "NORMAL"}, true, ref_path_);
   VcfWriter out(output_path_, h);
   stats_ = call_intervals(*ref, tumor_path_, normal_path_, read_all(intv_paths_), opt, out);
   out.close();
   if (ctx.log)
-    std::fprintf(ctx.log, "[fcs-genome mutect2] shard %d gpu %d: %lld reads, %lld regions, %lld calls, %.3f s\n",
-                 contig_, ctx.gpu, (long long)stats_.reads, (long long)stats_.regions, (long long)stats_.calls,
-                 stats_.seconds);
+    std::fprintf(ctx.log,
+                 "[fcs-genome mutect2] shard %d gpu %d: %lld reads, %lld regions, %lld pairs, %lld cells, %lld rescued, "
+                 "%lld calls, %.3f s (PairHMM %.3f s, %lld device passes)\n",
+                 contig_, ctx.gpu, (long long)stats_.reads, (long long)stats_.regions, (long long)stats_.pairs,
+                 (long long)stats_.cells, (long long)stats_.rescued, (long long)stats_.calls, stats_.seconds,
+                 stats_.phmm_seconds, (long long)stats_.device_passes);
   return 0;
 }
 

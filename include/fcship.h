@@ -163,6 +163,9 @@ int fcs_phmm_dev_run(fcs_phmm_plan* plan, const fcs_phmm_batch* dev_batch, doubl
                      const fcs_phmm_opts* opts, void* stream);
 /* Number of pairs the last forward pass queued for rescue (synchronises the stream). */
 int fcs_phmm_plan_rescue_count(fcs_phmm_plan* plan, void* stream, int64_t* count);
+/* Pairs the fp64 rescue recomputed in the calling thread's last synchronous
+ * fcs_phmm_compute / _regions / _pairs call (0 when rescue is off). */
+int fcs_phmm_last_rescued(int64_t* count);
 
 /* -------------------------------------------------------------- banded SW */
 typedef struct {

@@ -174,3 +174,82 @@ def test_htc_shard_boundaries_do_not_change_calls(gpu, data, tmp_path):
     spiked = {("chr20", 109380 + d) for d in (-30, 0, 30)}
     called = {(f[0], int(f[1])) for f in (ln.split("\t") for ln in outs["32"] if not ln.startswith("#"))}
     assert spiked <= called, spiked - called
+
+
+@pytest.fixture(scope="module")
+def data_c5(tmp_path_factory):
+    """C5-shaped tumor/normal pair in which 4% of the reads look mis-mapped
+    (20% high-quality mismatches): their likelihoods against every candidate
+    haplotype fall below the fp32 pass's 1e-28 threshold, so the fp64 rescue
+    runs inside a real mutect2 job."""
+    d = tmp_path_factory.mktemp("c5")
+    p = H.run_cli("synth", "-o", d, "-c", "chr20:200000", "-x", "30", "--tumor", "--seed", "13",
+                  "--noisy-frac", "0.04")
+    assert p.returncode == 0, p.stderr
+    return d
+
+
+def log_totals(logdir, key):
+    import re
+    tot = 0
+    for f in os.listdir(logdir):
+        for m in re.finditer(r"(\d+) " + key, open(os.path.join(logdir, f)).read()):
+            tot += int(m.group(1))
+    return tot
+
+
+def test_mutect2_c5_rescue_and_likelihoods(gpu, data_c5, tmp_path):
+    """mutect2 tumor/normal with the fp32 -> fp64 rescue
+    firing; every sampled likelihood the caller used (tumor and normal
+    regions) equals the oracle within 1e-5, rescued pairs included."""
+    out, dump, logs = tmp_path / "m2.vcf", tmp_path / "dump", tmp_path / "log"
+    p = H.run_cli("mutect2", "-r", data_c5 / "ref.fasta", "-t", data_c5 / "tumor.bam", "-n", data_c5 / "sample.bam",
+                  "-o", out, "--dump-regions", dump, env=dict(ENV, FCS_LOG_DIR=str(logs)), cwd=tmp_path)
+    assert p.returncode == 0, p.stderr[-3000:]
+    rescued = log_totals(logs, "rescued")
+    assert rescued > 0, "the noisy reads must send pairs through the fp64 rescue"
+    som = truth(data_c5, True)
+    assert len(som & calls(out)) / len(som) >= 0.8
+    rng = np.random.default_rng(5)
+    checked = n_resc = 0
+    for f in sorted(tmp_path.glob("dump.*")):
+        for reads, haps, lik in read_dump(f):
+            picks = {(int(rng.integers(len(reads))), int(rng.integers(len(haps)))) for _ in range(3)}
+            # plus every pair whose likelihood is below the fp32 threshold (log10(1e-28) - log10(2^120))
+            picks |= {(int(r), int(h)) for r, h in zip(*np.nonzero(lik < -64.1))}
+            for r, h in picks:
+                ref, used_d = oracle_lib.phmm_log10(reads[r], haps[h])
+                assert abs(lik[r, h] - ref) <= 1e-5 * abs(ref), (lik[r, h], ref, used_d)
+                checked += 1
+                n_resc += used_d
+    assert checked >= 100 and n_resc > 0, (checked, n_resc)
+
+
+def test_htc_c4_proxy_all_devices(gpu, tmp_path):
+    """C4 proxy: htc on a chr1-like 30x genome, the reference's 32 interval
+    shards (gatk.ncontigs) dealt round-robin over every visible GPU
+    (gpu.devices), calls checked against the truth set and the likelihoods of
+    every shard sampled against the oracle.  (2 Mbp, not chr1's 248 Mbp:
+    bench.py's e2e block runs the larger shape.)"""
+    import fcship
+    d = tmp_path / "d"
+    p = H.run_cli("synth", "-o", d, "-c", "chr1:2000000", "-x", "30", "--seed", "17")
+    assert p.returncode == 0, p.stderr
+    devs = ",".join(str(i) for i in range(fcship.device_count()))
+    out, dump, logs = tmp_path / "htc.vcf", tmp_path / "dump", tmp_path / "log"
+    env = dict(ENV, FCS_GATK_NCONTIGS="32", FCS_GATK_NPROCS="8", FCS_GPU_DEVICES=devs, FCS_LOG_DIR=str(logs))
+    p = H.run_cli("htc", "-r", d / "ref.fasta", "-i", d / "sample.bam", "-o", out, "--dump-regions", dump,
+                  env=env, cwd=tmp_path)
+    assert p.returncode == 0, p.stderr[-3000:]
+    t, c = truth(d, False), calls(out)
+    tp = len(t & c)
+    assert tp / len(t) >= 0.9 and tp / max(1, len(c)) >= 0.95, (tp, len(t), len(c))
+    dumps = sorted(tmp_path.glob("dump.*"))
+    assert len(dumps) == 32, len(dumps)  # every shard ran and batched its regions through the GPU
+    rng = np.random.default_rng(1)
+    for f in dumps:
+        for reads, haps, lik in read_dump(f)[:2]:
+            r, h = int(rng.integers(len(reads))), int(rng.integers(len(haps)))
+            ref, _ = oracle_lib.phmm_log10(reads[r], haps[h])
+            assert abs(lik[r, h] - ref) <= 1e-5 * abs(ref)
+    assert log_totals(logs, "regions") > 1000
