@@ -282,7 +282,9 @@ struct fcs_phmm_plan {
   void* sort_tmp = nullptr;
   size_t sort_tmp_bytes = 0;
   int32_t* rescue_list = nullptr;
-  unsigned long long* rescue_count = nullptr;  // [0] rescue count, then int64 class bounds[7]
+  int32_t* fb_list = nullptr;                  // pairs the streamed kernel hands back (bytes outside ACGTN)
+  unsigned long long* rescue_count = nullptr;  // [0] rescue count, [1] fallback count, then int64 class bounds
+  unsigned long long* fb_count = nullptr;
   int64_t* bounds = nullptr;
   int64_t scheduled = -1;  // n_pairs of the last schedule
 };
@@ -448,13 +450,15 @@ int fcs_phmm_plan_create(int32_t device, int64_t max_pairs, fcs_phmm_plan** plan
   FCS_HIP_CHECK(hipMalloc(&p->idx_in, n * 4));
   FCS_HIP_CHECK(hipMalloc(&p->idx_out, n * 4));
   FCS_HIP_CHECK(hipMalloc(&p->rescue_list, n * 4));
-  FCS_HIP_CHECK(hipMalloc(&p->rescue_count, 8 * sizeof(unsigned long long)));
+  FCS_HIP_CHECK(hipMalloc(&p->fb_list, n * 4));
+  FCS_HIP_CHECK(hipMalloc(&p->rescue_count, (2 + kPhmmLaunchClasses + 1) * sizeof(unsigned long long)));
   // Nothing is initialised here: every run writes the class bounds (the bounds
   // kernel stores all kPhmmClasses + 1 of them) and zeroes the rescue count on
   // the caller's stream.  (Round 1 zeroed them with a null-stream hipMemset,
   // which does not order against the non-blocking streams the plan runs on and
   // once landed after a schedule, so class launches computed nothing.)
-  p->bounds = reinterpret_cast<int64_t*>(p->rescue_count + 1);
+  p->fb_count = p->rescue_count + 1;
+  p->bounds = reinterpret_cast<int64_t*>(p->rescue_count + 2);
   size_t tmp = 0;
   FCS_HIP_CHECK(sort_pairs_u32(nullptr, tmp, p->keys_in, p->keys_out, p->idx_in, p->idx_out, (int)n, nullptr));
   p->sort_tmp_bytes = std::max<size_t>(tmp, 16);
@@ -472,6 +476,7 @@ int fcs_phmm_plan_destroy(fcs_phmm_plan* p) {
   (void)hipFree(p->idx_out);
   (void)hipFree(p->sort_tmp);
   (void)hipFree(p->rescue_list);
+  (void)hipFree(p->fb_list);
   (void)hipFree(p->rescue_count);
   delete p;
   return FCS_OK;
@@ -493,7 +498,7 @@ int fcs_phmm_dev_schedule(fcs_phmm_plan* plan, const fcs_phmm_batch* b, void* st
                                  (int)b->n_pairs, s, kPhmmKeyBits));
   }
   if ((rc = launch_phmm_bounds(plan->keys_out, b->n_pairs, plan->bounds, s))) return rc;
-  if (fault_drop_schedule()) FCS_HIP_CHECK(hipMemsetAsync(plan->bounds, 0, 7 * sizeof(int64_t), s));
+  if (fault_drop_schedule()) FCS_HIP_CHECK(hipMemsetAsync(plan->bounds, 0, (kPhmmLaunchClasses + 1) * sizeof(int64_t), s));
   plan->scheduled = b->n_pairs;
   return FCS_OK;
 }
@@ -511,10 +516,10 @@ int fcs_phmm_dev_forward(fcs_phmm_plan* plan, const fcs_phmm_batch* b, double* o
   rc = get_device_tables(plan->device, &t);
   if (rc) return rc;
   hipStream_t s = (hipStream_t)stream;
-  FCS_HIP_CHECK(hipMemsetAsync(plan->rescue_count, 0, sizeof(unsigned long long), s));
+  FCS_HIP_CHECK(hipMemsetAsync(plan->rescue_count, 0, 2 * sizeof(unsigned long long), s));  // rescue + fallback
   return launch_phmm_forward(to_dev(b), plan->idx_out, b->n_pairs, std::max(b->max_hap_len, 1), plan->bounds, *t,
                              opts->exact_order != 0, out, plan->rescue_list, plan->rescue_count,
-                             opts->rescue_threshold, opts->use_fp64_rescue != 0, s);
+                             opts->rescue_threshold, opts->use_fp64_rescue != 0, plan->fb_list, plan->fb_count, s);
 }
 
 int fcs_phmm_dev_rescue(fcs_phmm_plan* plan, const fcs_phmm_batch* b, double* out, const fcs_phmm_opts* opts,

@@ -128,11 +128,14 @@ int join_streams(hipStream_t s, const hipStream_t (&fs)[kForkStreams]);
 
 // ------------------------------------------------------------ kernel launchers
 int launch_phmm_keys(const PhmmDevBatch& b, uint32_t* keys, int32_t* idx, hipStream_t s);
-// bounds: device int64[7] from launch_phmm_bounds over the sorted keys.
+// bounds: device int64[kPhmmLaunchClasses + 1] from launch_phmm_bounds over the sorted keys.
 int launch_phmm_bounds(const uint32_t* sorted_keys, int64_t n, int64_t* bounds, hipStream_t s);
+// fb_list / fb_count: pairs the streamed kernel hands back (haplotype bytes
+// outside A/C/G/T/N), recomputed by the one-row kernel within this call.
 int launch_phmm_forward(const PhmmDevBatch& b, const int32_t* order, int64_t count, int max_hap_len,
                         const int64_t* bounds, const DeviceTables& t, bool exact, double* out, int32_t* rescue_list,
-                        unsigned long long* rescue_count, float thr, bool use_rescue, hipStream_t s);
+                        unsigned long long* rescue_count, float thr, bool use_rescue, int32_t* fb_list,
+                        unsigned long long* fb_count, hipStream_t s);
 int launch_phmm_rescue(const PhmmDevBatch& b, const int32_t* list, const unsigned long long* count_dev,
                        int64_t max_count, int max_hap_len, const DeviceTables& t, bool exact, double* out,
                        hipStream_t s);
@@ -181,9 +184,15 @@ hipError_t sort_pairs_u32(void* tmp, size_t& bytes, const uint32_t* kin, uint32_
 // SW schedule keys: bucket in bits [20, 24), below it the in-bucket order.
 constexpr int kBswKeyBucketShift = 20;
 constexpr int kBswKeyBits = 24;
-// PairHMM schedule keys: hap-length class in bits [21, 24).
-constexpr int kPhmmKeyClassShift = 21;
+// PairHMM schedule keys: launch class in bits [20, 24).  Launch classes
+// 0 .. kStreamClasses-1 run the row-streamed fp32 kernel (phmm_stream.h), the
+// next kPhmmClasses the grouped kernels (phmm2.h / phmm_kernel), each range
+// longest first.
+constexpr int kPhmmKeyClassShift = 20;
 constexpr int kPhmmKeyBits = 24;
+constexpr int kStreamClasses = 4;
+constexpr int kPhmmClasses = 6;
+constexpr int kPhmmLaunchClasses = kStreamClasses + kPhmmClasses;
 // Sorted schedule: one launch over the lane (0..9) and pair (kBswPairBucket0..+4)
 // buckets, then the wave-per-task kernel over kBswWideBucket.
 int launch_bsw_extend_sorted(const BswDevBatch& b, const BswParams& p, int max_qlen, int max_tlen, int32_t* res,

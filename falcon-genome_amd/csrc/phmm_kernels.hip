@@ -32,6 +32,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstdlib>
 
 #include <utility>
 
@@ -397,6 +398,7 @@ __global__ __launch_bounds__(64, (sizeof(T) == 4 && !EXACT) ? 4 : 1) void phmm_k
 }  // namespace fcs
 
 #include "phmm2.h"
+#include "phmm_stream.h"
 
 namespace fcs {
 
@@ -410,35 +412,47 @@ static __host__ __device__ int nslot_for(int max_hap_len) { return ((max_hap_len
 // class everything longer.  Each class is its own launch with LDS sized to the
 // class, so short haplotypes run at 4 waves per SIMD instead of the 3 that the
 // longest haplotype of the batch would allow.
-constexpr int kPhmmClasses = 6;
-static_assert(kPhmmClasses <= 8 && kPhmmKeyClassShift + 3 <= kPhmmKeyBits, "class fits the key");
+static_assert(kPhmmLaunchClasses <= 16 && kPhmmKeyClassShift + 4 <= kPhmmKeyBits, "class fits the key");
 __host__ __device__ inline int phmm_class(int H) {
   const int c = (nslot_for(H) - 224 + 31) / 32;
   return c < 0 ? 0 : c > kPhmmClasses - 1 ? kPhmmClasses - 1 : c;
 }
 
-// Sort keys: class descending, then stripe count and hap length descending,
-// as ascending keys — each class is a contiguous range, longest work first.
+// Sort keys (24 bits, three 8-bit radix passes): a 4-bit launch class, then the
+// in-class order, as ascending keys — each class is a contiguous range and the
+// longest work comes first.  Classes 0 .. kStreamClasses-1 are the row-streamed
+// kernel's (R >= kStreamMinR, longest hap-length class first), the rest the
+// grouped kernels' hap-length classes (longest first).  In-class order:
+// streamed, hap length then read length descending; grouped, stripe count then
+// hap length descending.  The clamps only change the order, never results.
+__host__ __device__ inline int phmm_launch_class(int R, int H, int& stream_cls) {
+  stream_cls = (R >= kStreamMinR && H >= 1) ? stream_class(H) : -1;
+  if (stream_cls >= 0) return kStreamClasses - 1 - stream_cls;
+  return kStreamClasses + kPhmmClasses - 1 - phmm_class(max(H, 0));
+}
+
 __global__ void phmm_keys_kernel(const PhmmDevBatch b, uint32_t* __restrict__ keys, int32_t* __restrict__ idx) {
   const long long p = (long long)blockIdx.x * blockDim.x + threadIdx.x;
   if (p >= b.n_pairs) return;
   const int R = b.read_len[b.pair_read[p]];
   const int H = b.hap_len[b.pair_hap[p]];
-  // 24 bits (three 8-bit radix passes): class | 255 - stripes | 8191 - H.  The
-  // clamps (R > 4080, H > 8191) only change the order, never results: a wave
-  // runs its pairs' own shapes (wave max of stripes and H).
-  const uint32_t ns = (uint32_t)min((R + 15) >> 4, 0xFF);
-  const uint32_t hh = (uint32_t)min(max(H, 0), 0x1FFF);
-  const uint32_t rc = (uint32_t)(kPhmmClasses - 1 - phmm_class(max(H, 0)));
-  keys[p] = (rc << kPhmmKeyClassShift) | ((0xFFu - ns) << 13) | (0x1FFFu - hh);
+  int sc;
+  const uint32_t cf = (uint32_t)phmm_launch_class(R, H, sc);
+  const uint32_t hh = 0xFFFu - (uint32_t)min(max(H, 0), 0xFFF);
+  uint32_t low;
+  if (sc >= 0)
+    low = (hh << 8) | (0xFFu - (uint32_t)min(R >> 4, 0xFF));
+  else
+    low = ((0xFFu - (uint32_t)min((max(R, 0) + 15) >> 4, 0xFF)) << 12) | hh;
+  keys[p] = (cf << kPhmmKeyClassShift) | low;
   idx[p] = (int32_t)p;
 }
 
-// bounds[j] = first sorted position of reversed class j (j = 0: the longest class); bounds[kPhmmClasses] = n.
+// bounds[j] = first sorted position of launch class j; bounds[kPhmmLaunchClasses] = n.
 __global__ void phmm_bounds_kernel(const uint32_t* __restrict__ keys, long long n, int64_t* __restrict__ bounds) {
   const long long k = (long long)blockIdx.x * blockDim.x + threadIdx.x;
   if (k > n) return;
-  const int cur = (k < n) ? (int)(keys[k] >> kPhmmKeyClassShift) : kPhmmClasses;
+  const int cur = (k < n) ? (int)(keys[k] >> kPhmmKeyClassShift) : kPhmmLaunchClasses;
   const int prev = (k > 0) ? (int)(keys[k - 1] >> kPhmmKeyClassShift) : -1;
   for (int j = prev + 1; j <= cur; ++j) bounds[j] = k;
 }
@@ -497,22 +511,88 @@ static int launch_one(const PhmmDevBatch& b, const int32_t* order, const unsigne
   return FCS_OK;
 }
 
+// Pairs per segment stream of the streamed kernel: as many as keep >= ~24K
+// waves in flight for the batch (8 x 3 waves x 256 CUs x 4 SIMDs), at most
+// kStreamMaxK (a stream's quantisation loss is < 1/2 stripe in K pairs).
+// FCSHIP_STREAM_K=k (tests) forces k pairs per stream on any batch size.
+static int stream_pairs_per_segment(int64_t n) {
+  static const int forced = [] {
+    const char* e = std::getenv("FCSHIP_STREAM_K");
+    return e ? std::atoi(e) : 0;
+  }();
+  if (forced > 0) return std::min(forced, kStreamMaxK);
+  const int64_t k = n / (4 * 24576);
+  return (int)std::max<int64_t>(1, std::min<int64_t>(kStreamMaxK, k));
+}
+
 int launch_phmm_forward(const PhmmDevBatch& b, const int32_t* order, int64_t count, int max_hap_len,
                         const int64_t* bounds, const DeviceTables& t, bool exact, double* out, int32_t* rescue_list,
-                        unsigned long long* rescue_count, float thr, bool use_rescue, hipStream_t s) {
+                        unsigned long long* rescue_count, float thr, bool use_rescue, int32_t* fb_list,
+                        unsigned long long* fb_count, hipStream_t s) {
   if (count <= 0) return FCS_OK;
   const long long groups = (count + 3) / 4;
   const int ns_max = nslot_for(max_hap_len);
   const int c_max = phmm_class(max_hap_len);
-  // One launch per hap-length class (ranges from the device-side bounds), forked
+  const int sc_max = stream_class(max_hap_len) < 0 ? kStreamClasses - 1 : stream_class(max_hap_len);
+  // One launch per launch class (ranges from the device-side bounds), forked
   // over streams so a class's tail overlaps the next class; classes above the
   // batch's longest haplotype are empty and not launched.
   hipStream_t fs[kForkStreams];
   if (const int rc = fork_streams(s, fs); rc != FCS_OK) return rc;
+  int fork = 0;
+  for (int j = kStreamClasses - 1 - sc_max; j < kStreamClasses; ++j) {
+    const int sc = kStreamClasses - 1 - j;
+    const int hmax = std::min(stream_class_hmax(sc), max_hap_len);
+    hipStream_t st = fs[fork++ % kForkStreams];
+#ifdef FCS_PHMM_NOSTREAM
+    if (!exact) {  // A/B baseline: the grouped two-row kernel over the stream range
+      const int ns2 = nslot_for(hmax) + 16;
+      const size_t lds2 = (size_t)phmm2_lds(ns2);
+      if (lds2 <= kLdsBytes) {
+        if (lds2 > 64 * 1024)
+          FCS_HIP_CHECK(
+              hipFuncSetAttribute((const void*)phmm2_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds2));
+        hipLaunchKernelGGL(phmm2_kernel, dim3((unsigned)std::min<long long>(std::max<long long>(groups, 1), 65536)),
+                           dim3(64), lds2, st, b, order, bounds, j, ns2, t.tf, out, rescue_list, rescue_count, thr,
+                           use_rescue ? 1 : 0);
+        FCS_HIP_CHECK(hipGetLastError());
+        continue;
+      }
+    }
+#endif
+    if (exact) {  // GKL operation order: the one-row kernel over the same range
+      const int rc = launch_one<float, true, false>(b, order, nullptr, count, bounds, j, nslot_for(hmax), groups, t.tf,
+                                                   out, rescue_list, rescue_count, thr, use_rescue, st);
+      if (rc != FCS_OK) return rc;
+      continue;
+    }
+    const size_t lds = (size_t)stream_lds(hmax);
+    if (lds > kLdsBytes) return fail(FCS_ERR_UNSUPPORTED, "[E::fcship] streamed PairHMM class exceeds LDS");
+    const int K = stream_pairs_per_segment(count);
+    const int w = stream_class_waves(sc);
+    // the range's last pairs run one per segment: about two rounds of the
+    // chip's wave slots (256 CUs x 4 SIMDs x w), so the launch ends on short waves
+    const int tail = 2 * 4 * 1024 * w;
+    const unsigned grid = (unsigned)std::min<long long>(
+        std::max<long long>((count + 4 * K - 1) / (4 * K) + (tail + 3) / 4, 1), 65536);
+    auto launch = [&](auto kern) -> int {
+      if (lds > 64 * 1024)
+        FCS_HIP_CHECK(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+      hipLaunchKernelGGL(kern, dim3(grid), dim3(64), lds, st, b, order, bounds, j, K, tail, stream_nslot(hmax),
+                         stream_hstride(hmax), t.tf, out, rescue_list, rescue_count, thr, use_rescue ? 1 : 0, fb_list,
+                         fb_count);
+      FCS_HIP_CHECK(hipGetLastError());
+      return FCS_OK;
+    };
+    const int rc = w >= 4 ? launch(phmm3_kernel<4>) : w == 3 ? launch(phmm3_kernel<3>)
+                 : w == 2 ? launch(phmm3_kernel<2>) : launch(phmm3_kernel<1>);
+    if (rc != FCS_OK) return rc;
+  }
   for (int j = kPhmmClasses - 1 - c_max; j < kPhmmClasses; ++j) {
     const int c = kPhmmClasses - 1 - j;
+    const int lc = kStreamClasses + j;  // launch class of grouped class c
     const int ns = (c == kPhmmClasses - 1) ? ns_max : std::min(224 + 32 * c, ns_max);
-    hipStream_t st = fs[j % kForkStreams];
+    hipStream_t st = fs[fork++ % kForkStreams];
 #ifndef FCS_PHMM_ONEROW
     // the two-rows-per-lane kernel (phmm2.h) for the FMA-order pass when its
     // four rings fit (ring slots >= H + 65, hap bytes + 16)
@@ -523,19 +603,25 @@ int launch_phmm_forward(const PhmmDevBatch& b, const int32_t* order, int64_t cou
         FCS_HIP_CHECK(
             hipFuncSetAttribute((const void*)phmm2_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds2));
       const unsigned grid = (unsigned)std::min<long long>(std::max<long long>(groups, 1), 65536);
-      hipLaunchKernelGGL(phmm2_kernel, dim3(grid), dim3(64), lds2, st, b, order, bounds, j, ns2, t.tf, out,
+      hipLaunchKernelGGL(phmm2_kernel, dim3(grid), dim3(64), lds2, st, b, order, bounds, lc, ns2, t.tf, out,
                          rescue_list, rescue_count, thr, use_rescue ? 1 : 0);
       FCS_HIP_CHECK(hipGetLastError());
       continue;
     }
 #endif
-    const int rc = exact ? launch_one<float, true, false>(b, order, nullptr, count, bounds, j, ns, groups, t.tf, out,
+    const int rc = exact ? launch_one<float, true, false>(b, order, nullptr, count, bounds, lc, ns, groups, t.tf, out,
                                                            rescue_list, rescue_count, thr, use_rescue, st)
-                         : launch_one<float, false, false>(b, order, nullptr, count, bounds, j, ns, groups, t.tf, out,
+                         : launch_one<float, false, false>(b, order, nullptr, count, bounds, lc, ns, groups, t.tf, out,
                                                             rescue_list, rescue_count, thr, use_rescue, st);
     if (rc != FCS_OK) return rc;
   }
-  return join_streams(s, fs);
+  if (const int rc = join_streams(s, fs); rc != FCS_OK) return rc;
+  if (exact) return FCS_OK;
+  // Pairs the streamed kernel handed back (device-side list): the one-row
+  // kernel with GKL's byte compare, appending to the same rescue list.
+  return launch_one<float, false, false>(b, fb_list, fb_count, 0, nullptr, 0, ns_max,
+                                         std::min<long long>(groups, 2048), t.tf, out, rescue_list, rescue_count, thr,
+                                         use_rescue, s);
 }
 
 int launch_phmm_rescue(const PhmmDevBatch& b, const int32_t* list, const unsigned long long* count_dev,

@@ -1,0 +1,499 @@
+// PairHMM fp32 forward pass with row-streamed segments (included by
+// phmm_kernels.hip after phmm2.h).
+//
+// phmm2_kernel gives each 16-lane segment one pair and runs its rows in
+// stripes of 32 (two rows per lane), so a read of R = 101 rows occupies 128:
+// the last stripe computes 5 useful rows at the price of 32 (C2: 35% of the
+// cell slots idle).  Here a segment runs a STREAM of K pairs back to back:
+// the stream's rows are cut into 32-row stripes regardless of pair
+// boundaries, so a stripe may finish one pair in its low lanes and start the
+// next in its high lanes.  Only the stream's very end is quantised.
+//
+// Per pair the stream holds, in two-row units (lane row a, row b):
+//   [pad if R is even] rows 1..R, V
+// where V is a virtual row R + 1 that sums the last row.  The step is exactly
+// phmm2's (seven packed FP32 ops per two cells, same DPP hand-off and LDS
+// boundary ring); only the per-row constants change:
+//   * row 1 starts the pair: its lane reads the row-0 boundary from a 64-entry
+//     LDS constant Z ({1, 0} at columns >= 0, {0, 0} below) instead of the
+//     lane below / ring, and its emission priors are pre-multiplied by
+//     x0 = (2^120 / H) * gm_1, so M(1, c) = (prior * x0) * 1 = prior * x0
+//     bitwise as in phmm2 (whose ring holds x0 itself);
+//   * the pad row (R even) passes Z through one column later (prior 1, mm 1,
+//     everything else 0), so row 1 sits in a row b and V again in a row b;
+//   * row R hands the row below X = M + I (mm = gm = 1, D killed by my = 0) and
+//     I = 0;
+//   * V (prior 1, my = yy = 1, mm = gm = 1) keeps D = running sum of its M =
+//     sum over c of (M + I)(R, c) in column order, and hands X = M + D: at its
+//     column H + 1 that is sum_{c = 1..H} (M + I)(R, c).  The capture is one
+//     compare-select in the (at most two) 16-step blocks that hold some V
+//     lane's column H + 1 — no per-step accumulator anywhere.
+// Lane 0 of a stripe continues its pair from the segment's LDS ring that lane
+// 15 wrote in the previous stripe, exactly as in phmm2.  A pair spans >= 17
+// units (R >= 33, enforced by the schedule), so a stripe holds at most two
+// pairs of a segment and the segment keeps two hap-code buffers (pair parity).
+// Ring, hap codes and Z are read a few columns past a pair's end and before
+// its start; those columns only feed columns > H or multiply exact zeros, so
+// their content is irrelevant and the arrays are sized to the written ranges.
+// Pairs whose haplotype holds bytes outside A/C/G/T/N (the hap codes cannot
+// express GKL's byte compare) are handed to a fallback list that the one-row
+// kernel recomputes; their streamed results are discarded.
+#pragma once
+
+namespace fcs {
+
+constexpr int kStreamMinR = 33;  // a pair spans >= 17 units: at most two pairs per stripe and segment
+constexpr int kStreamMaxK = 8;   // pairs per segment stream
+// Hap-length bounds of the stream classes: LDS <= 10,240 B per wave (4 waves per
+// SIMD), <= 13,312 B (3, at the 512-byte allocation granularity), <= 20 KB (2),
+// and the 160 KB limit.
+__host__ __device__ constexpr int stream_class_hmax(int c) {
+  return c == 0 ? 224 : c == 1 ? 300 : c == 2 ? 472 : 3700;
+}
+// Waves per SIMD the class's launch bounds ask for (its LDS allows as many).
+__host__ __device__ constexpr int stream_class_waves(int c) { return c == 0 ? 4 : c == 1 ? 3 : c == 2 ? 2 : 1; }
+__host__ __device__ inline int stream_class(int H) {
+  for (int c = 0; c < kStreamClasses; ++c)
+    if (H <= stream_class_hmax(c)) return c;
+  return -1;
+}
+// LDS per wave: Z (64 ring entries) | four rings of hmax + 18 slots (slot =
+// column; a stripe runs to step 16 * ceil((H + 33) / 16) - 1 <= H + 47, so lane
+// 15 writes columns 1 .. hmax + 16) | eight hap-code buffers of hmax + 10 bytes
+// (column c at 3 + (address & 3) + c: whole aligned dwords of the hap bytes are
+// converted in place) | 64 bytes of read-ahead tail.
+__host__ __device__ constexpr int stream_nslot(int hmax) { return hmax + 18; }
+__host__ __device__ constexpr int stream_hstride(int hmax) { return (hmax + 12) & ~3; }
+__host__ __device__ constexpr int stream_lds(int hmax) {
+  return 512 + 4 * 8 * stream_nslot(hmax) + 8 * stream_hstride(hmax) + 64;
+}
+
+// Per-row constants of one half (role: 0 idle, 1 pad, 2 row r < R, 3 row R, 4 V).
+struct SRowC {
+  float e1, e3, my, yy, mm, gm, mx, xx;
+  int mask;
+};
+
+__device__ __forceinline__ SRowC srow_params(const PhmmTables<float>& tab, const RawRow& raw, int role, bool first,
+                                             int H) {
+  SRowC c;
+  if (role == 2 || role == 3) {
+    const RowP<float> q = row_params<float, false>(tab, raw);
+    c.e1 = q.e1;
+    c.e3 = q.e3;
+    c.my = q.my;
+    c.yy = q.yy;
+    c.mm = q.mm;
+    c.gm = q.gm;
+    c.mx = q.mx;
+    c.xx = q.xx;
+    c.mask = q.rmask;
+    if (role == 3) {  // hand X = M + I, I = 0; D is never needed by anyone
+      c.my = 0.f;
+      c.mm = 1.f;
+      c.gm = 1.f;
+      c.mx = 0.f;
+      c.xx = 0.f;
+    }
+    if (first) {  // M(1, c) = prior * x0 (x0 = X(0, c - 1) for c - 1 >= 0)
+      const float x0 = (tab.init_const / (float)H) * tab.dmatch[raw.gq & 127];
+      c.e1 *= x0;
+      c.e3 *= x0;
+    }
+  } else if (role == 4) {  // V: D = running sum of M; X = M + D
+    c.e1 = c.e3 = 1.f;
+    c.my = c.yy = 1.f;
+    c.mm = c.gm = 1.f;
+    c.mx = c.xx = 0.f;
+    c.mask = 0;
+  } else if (role == 1) {  // pad: X = prior * Xp = Z one column on, I = 0, D = 0
+    c.e1 = c.e3 = 1.f;
+    c.my = c.yy = 0.f;
+    c.mm = 1.f;
+    c.gm = 0.f;
+    c.mx = c.xx = 0.f;
+    c.mask = 0;
+  } else {
+    c.e1 = c.e3 = c.my = c.yy = c.mm = c.gm = c.mx = c.xx = 0.f;
+    c.mask = 0;
+  }
+  return c;
+}
+
+__device__ __forceinline__ RowP2 srow_pack(const SRowC& a, const SRowC& b) {
+  RowP2 p;
+  p.e1 = pf2{a.e1, b.e1};
+  p.e3 = pf2{a.e3, b.e3};
+  p.my = pf2{a.my, b.my};
+  p.yy = pf2{a.yy, b.yy};
+  p.mm = pf2{a.mm, b.mm};
+  p.gm = pf2{a.gm, b.gm};
+  p.mx = pf2{a.mx, b.mx};
+  p.xx = pf2{a.xx, b.xx};
+  p.ra = p.rb = 0;
+  p.ma = a.mask;
+  p.mb = b.mask;
+  return p;
+}
+
+// Where one lane sits in a stripe: pair (index k in its segment, batch index
+// p), unit u of the pair, its rows and their roles.
+struct SLane {
+  int k, p, R, H, u;
+  int64_t ro;
+  int role_a, role_b, ra, rb;  // rb = ra + 1; rows are 1-based, 0 = pad
+  bool act;
+};
+
+__device__ __forceinline__ int srole(int r, int R) { return r == 0 ? 1 : r < R ? 2 : r == R ? 3 : 4; }
+
+// One step: phmm2_step without the byte-compare and summing variants; the
+// boundary source is this block's per-lane pointer `rd` (ring or Z) and COND
+// captures the V lanes' X at their column H + 1.
+template <bool COND, bool WRITE, int S>
+__device__ __forceinline__ void pstream_step(Lane2& L, PhRing<float> (&pf)[PFD], int (&hq)[PFD],
+                                             const unsigned char* __restrict__ hp, const PhRing<float>* __restrict__ rd,
+                                             const RowP2& p, const bool start, const bool top, const int t0,
+                                             const int dl, float& acc, const uint32_t wbase) {
+  const int t = t0 + S;
+  const PhRing<float> cur = pf[0];
+  const int hba = hq[0];
+#pragma unroll
+  for (int k = 0; k + 1 < PFD; ++k) {
+    pf[k] = pf[k + 1];
+    hq[k] = hq[k + 1];
+  }
+  pf[PFD - 1] = rd[S];     // boundary input for step t + PFD
+  hq[PFD - 1] = hp[t];     // row a's hap code for column t + PFD - 2l
+  const int hbb = L.hbp;
+  L.hbp = hba;
+  pf2 Xsw = L.Xn, Isw = L.In;
+  Xsw.y = __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(L.Xn.y), kDppRowShr1, 0xF, 0xF, true));
+  Isw.y = __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(L.In.y), kDppRowShr1, 0xF, 0xF, true));
+  Xsw.y = start ? cur.X : Xsw.y;
+  Isw.y = start ? cur.I : Isw.y;
+  const pf2 I = __builtin_shufflevector(Isw, Isw, 1, 0);
+  pf2 prior;
+  prior.x = prior_code(p.ma, hba, p.e1.x, p.e3.x);
+  prior.y = prior_code(p.mb, hbb, p.e1.y, p.e3.y);
+  const pf2 M = __builtin_shufflevector(L.Xp, L.Xp, 1, 0) * prior;
+  const pf2 D = __builtin_elementwise_fma(L.Mo, p.my, L.Do * p.yy);
+  const pf2 Xn = __builtin_elementwise_fma(M, p.mm, __builtin_elementwise_fma(I, p.gm, D));
+  const pf2 In = __builtin_elementwise_fma(M, p.mx, I * p.xx);
+  if constexpr (WRITE) {
+    if (top)  // row b of lane 15, column t - 31 -> ring slot t - 31
+      asm volatile("ds_write2_b32 %0, %1, %2 offset0:%3 offset1:%4"
+                   :
+                   : "v"(wbase), "v"(Xn.y), "v"(In.y), "i"(2 * S), "i"(2 * S + 1)
+                   : "memory");
+  }
+  else
+    asm volatile("" ::: "memory");  // keep each step's LDS reads in their step (hoisted, they cost registers)
+  if constexpr (COND)  // V lanes: take X at the step dl = lim - t0 (a compare-select in place, not
+                       // sixteen compares hoisted into SGPR pairs)
+    asm volatile("v_cmp_eq_u32 vcc, %2, %3\n\tv_cndmask_b32 %0, %0, %1, vcc"
+                 : "+v"(acc)
+                 : "v"(Xn.y), "i"(S), "v"(dl)
+                 : "vcc");
+  L.Xp = Xsw;
+  L.Xn = Xn;
+  L.In = In;
+  L.Mo = M;
+  L.Do = D;
+}
+
+template <bool COND, bool WRITE>
+__device__ __forceinline__ void pstream_block(Lane2& L, PhRing<float> (&pf)[PFD], int (&hq)[PFD],
+                                              const unsigned char* __restrict__ hp,
+                                              const PhRing<float>* __restrict__ rd, const RowP2& p, const bool start,
+                                              const bool top, const int t0, const int dl, float& acc,
+                                              const uint32_t wbase) {
+  [&]<int... S>(std::integer_sequence<int, S...>) {
+    (pstream_step<COND, WRITE, S>(L, pf, hq, hp, rd, p, start, top, t0, dl, acc, wbase), ...);
+  }(std::make_integer_sequence<int, 16>{});
+}
+
+// Hap bytes -> codes (A,C,G,T,N = 0..4), four per dword: (b >> 1) & 7 is
+// distinct for A, C, T, G, N (0, 1, 2, 3, 7) and v_perm looks the code up; a
+// byte whose code does not map back to itself is outside A/C/G/T/N.
+__device__ __forceinline__ uint32_t hap_codes4(uint32_t x, uint32_t valid, bool& other) {
+  const uint32_t sel = (x >> 1) & 0x07070707u;
+  const uint32_t code = __builtin_amdgcn_perm(0x04050505u, 0x02030100u, sel);
+  const uint32_t back = __builtin_amdgcn_perm(0x0000004Eu, 0x54474341u, code);
+  other |= ((back ^ x) & valid) != 0u;
+  return code;
+}
+
+template <int LB>
+__global__ __launch_bounds__(64, LB) void phmm3_kernel(
+    const PhmmDevBatch b, const int32_t* __restrict__ order, const int64_t* __restrict__ bounds, const int cls,
+    const int K, const int tail_pairs, const int nslot, const int hstride, const PhmmTables<float> tab,
+    double* __restrict__ out, int32_t* __restrict__ rescue_list, unsigned long long* __restrict__ rescue_count,
+    const float thr, const int use_rescue, int32_t* __restrict__ fb_list, unsigned long long* __restrict__ fb_count) {
+  extern __shared__ __align__(16) unsigned char smem_raw[];
+  const int lane = threadIdx.x;
+  const int seg = lane >> 4;
+  const int sl = lane & 15;
+  const int sbase = lane & 48;
+  const int sl2 = 2 * sl;
+  const bool top = sl == 15;
+  PhRing<float>* const Z = reinterpret_cast<PhRing<float>*>(smem_raw);
+  PhRing<float>* const ring = reinterpret_cast<PhRing<float>*>(smem_raw + 512) + seg * nslot;
+  unsigned char* const hbufs = smem_raw + 512 + 32 * nslot + 2 * seg * hstride;  // this segment's two buffers
+  {
+    PhRing<float> z;
+    z.X = lane >= 32 ? 1.f : 0.f;
+    z.I = 0.f;
+    Z[lane] = z;
+    if (sl == 0) {  // column 0 of the boundary is always {0, 0}; lane 15 never writes it
+      PhRing<float> o;
+      o.X = o.I = 0.f;
+      ring[0] = o;
+    }
+  }
+  const int64_t cbeg = bounds[cls];
+  const long long count = bounds[cls + 1] - cbeg;
+  order += cbeg;
+  // Batches: K pairs per segment, except the range's last tail_pairs (its
+  // shortest haplotypes), one pair per segment, so the launch ends on short waves.
+  const long long tailn = count < (long long)tail_pairs ? count : (long long)tail_pairs;
+  const long long headn = count - tailn;
+  const long long per = 4LL * K;
+  const long long nb_head = (headn + per - 1) / per;
+  const long long nbatch = nb_head + (tailn + 3) / 4;
+
+  for (long long w = blockIdx.x; w < nbatch; w += gridDim.x) {
+    const bool head = w < nb_head;
+    const int Kb = head ? K : 1;
+    const long long bstart = head ? w * per : headn + (w - nb_head) * 4;
+    const long long bend = head ? min(headn, bstart + per) : min(count, bstart + 4);
+    // Segment table: lane k of the segment holds pair k of its stream.
+    const long long idx = bstart + 4LL * sl + seg;
+    const int pm = (sl < Kb && idx < bend) ? order[idx] : -1;
+    int Rm = 0, Hm = 0, Um = 0;
+    int64_t rom = 0, hom = 0;
+    if (pm >= 0) {
+      const int ri = b.pair_read[pm], hi = b.pair_hap[pm];
+      Rm = b.read_len[ri];
+      Hm = b.hap_len[hi];
+      rom = b.read_off[ri];
+      hom = b.hap_off[hi];
+      Um = (Rm + 2) >> 1;
+    }
+    int ube = Um;  // inclusive prefix sum of units over the segment
+    ube += __builtin_amdgcn_update_dpp(0, ube, kDppRowShr1, 0xF, 0xF, false);
+    ube += __builtin_amdgcn_update_dpp(0, ube, kDppRowShr2, 0xF, 0xF, false);
+    ube += __builtin_amdgcn_update_dpp(0, ube, kDppRowShr4, 0xF, 0xF, false);
+    ube += __builtin_amdgcn_update_dpp(0, ube, kDppRowShr8, 0xF, 0xF, false);
+    const int ubb = ube - Um;
+    const int total = __shfl(ube, sbase + 15);
+    const int nstr = (wave_max(total) + 15) >> 4;
+    unsigned other = 0;  // bit k: pair k's haplotype needs the byte-compare fallback (segment-uniform)
+
+    // Lane position in stripe st from the pair cursor kc of stripe st - 1
+    // (advanced by at most one pair: every pair spans more than 16 units).
+    int kc = 0;
+    auto locate = [&](int st) {
+      SLane s;
+      const int g = 16 * st + sl;
+      {
+        const int e = __shfl(ube, sbase + min(kc, 15));
+        if (kc < Kb && g >= e) ++kc;
+      }
+      const int kk = min(kc, 15);
+      s.k = kc;
+      s.act = g < total;
+      s.p = __shfl(pm, sbase + kk);
+      s.R = __shfl(Rm, sbase + kk);
+      s.H = __shfl(Hm, sbase + kk);
+      const int lo = __shfl((int)rom, sbase + kk), hi = __shfl((int)(rom >> 32), sbase + kk);
+      s.ro = (int64_t)(((uint64_t)(uint32_t)hi << 32) | (uint32_t)lo);
+      s.u = g - __shfl(ubb, sbase + kk);
+      const int pad = (s.R & 1) ^ 1;
+      s.ra = 2 * s.u + 1 - pad;
+      s.rb = s.ra + 1;
+      s.role_a = s.act ? srole(s.ra, s.R) : 0;
+      s.role_b = s.act ? srole(s.rb, s.R) : 0;
+      return s;
+    };
+    auto raw_of = [&](const SLane& s, int r, int role) {
+      return (role == 2 || role == 3) ? load_raw(b, s.R, s.ro, r - 1) : RawRow{-1, 0, 0, 0, 0, 0, 0};
+    };
+    // The stripe-to-stripe lane state in three registers: p, R | H << 16 and
+    // act | k << 1 | hap alignment << 5 | u << 7.
+    struct SPack {
+      int p, rh, w;
+    };
+    auto pack = [&](const SLane& s) {
+      SPack q;
+      q.p = s.p;
+      q.rh = s.R | (s.H << 16);
+      const uint8_t* const ha = b.hb + (int64_t)(uint32_t)__shfl((int)hom, sbase + min(s.k, 15));
+      const int al = (int)((uintptr_t)ha & 3);  // only its address: a lane past the stream may point anywhere
+      q.w = (s.act ? 1 : 0) | (s.k << 1) | (al << 5) | (s.u << 7);
+      return q;
+    };
+    auto unpack = [&](const SPack& q) {
+      SLane s;
+      s.p = q.p;
+      s.R = q.rh & 0xFFFF;
+      s.H = q.rh >> 16;
+      s.act = q.w & 1;
+      s.k = (q.w >> 1) & 15;
+      s.u = q.w >> 7;
+      s.ro = 0;
+      const int pad = (s.R & 1) ^ 1;
+      s.ra = 2 * s.u + 1 - pad;
+      s.rb = s.ra + 1;
+      s.role_a = s.act ? srole(s.ra, s.R) : 0;
+      s.role_b = s.act ? srole(s.rb, s.R) : 0;
+      return s;
+    };
+    auto params_of = [&](const SLane& s, const RawRow& a, const RawRow& bb) {
+      return srow_pack(srow_params(tab, a, s.role_a, s.ra == 1, s.H), srow_params(tab, bb, s.role_b, s.rb == 1, s.H));
+    };
+
+    // Haplotype codes of the pair that starts in the coming stripe (at most one
+    // per segment): aligned dwords covering its bytes, issued a stripe ahead
+    // (kHapPre per lane; longer haplotypes load the rest when committed).  Its
+    // buffer (pair parity) was last used by the pair two back, which ended in
+    // an earlier stripe.  Column c of pair k sits at hbuf(k) + 3 + al + c.
+    constexpr int kHapPre = 5;
+    uint32_t hv[kHapPre];
+    int hk = -1, hH = 0;
+    const uint8_t* ha = nullptr;
+    auto hap_issue = [&](int st_next, const SLane& first_lane15) {
+      // first_lane15: lane 15's position in stripe st_next (shuffled below)
+      const int k15 = __shfl(first_lane15.k, sbase + 15);
+      const int u15 = __shfl(first_lane15.u, sbase + 15);
+      const bool a15 = __shfl((int)first_lane15.act, sbase + 15) != 0;
+      const int kk = min(k15, 15);
+      hk = (a15 && u15 < 16 && k15 < Kb) ? k15 : -1;  // started within stripe st_next
+      hH = __shfl(Hm, sbase + kk);
+      const int lo = __shfl((int)hom, sbase + kk), hi = __shfl((int)(hom >> 32), sbase + kk);
+      ha = b.hb + (int64_t)(((uint64_t)(uint32_t)hi << 32) | (uint32_t)lo);
+      const int al = (int)((uintptr_t)ha & 3);
+      const uint32_t* const src = reinterpret_cast<const uint32_t*>(ha - al);
+#pragma unroll
+      for (int i = 0; i < kHapPre; ++i) {
+        const int j = sl + 16 * i;
+        hv[i] = (hk >= 0 && 4 * j < al + hH) ? src[j] : 0u;
+      }
+    };
+    auto hap_commit = [&] {
+      bool oth = false;
+      if (hk >= 0) {
+        const int al = (int)((uintptr_t)ha & 3);
+        uint32_t* const dst = reinterpret_cast<uint32_t*>(hbufs + (hk & 1) * hstride + 4);
+        const uint32_t* const src = reinterpret_cast<const uint32_t*>(ha - al);
+        const int nb = al + hH;  // bytes from the aligned start; valid ones are [al, nb)
+        auto put = [&](int j, uint32_t x) {
+          const int lo = 4 * j, hi = lo + 4;
+          uint32_t valid = 0xFFFFFFFFu;
+          if (lo < al) valid &= 0xFFFFFFFFu << (8 * (al - lo));
+          if (hi > nb) valid &= 0xFFFFFFFFu >> (8 * (hi - nb));
+          dst[j] = hap_codes4(x, valid, oth);
+        };
+#pragma unroll
+        for (int i = 0; i < kHapPre; ++i) {
+          const int j = sl + 16 * i;
+          if (4 * j < nb) put(j, hv[i]);
+        }
+        for (int j = sl + 16 * kHapPre; 4 * j < nb; j += 16) put(j, src[j]);
+      }
+      const unsigned long long bal = __ballot(oth);
+      if (hk >= 0 && ((bal >> sbase) & 0xFFFFull)) other |= 1u << hk;
+    };
+
+    SPack cur_pk;
+    RowP2 prm;
+    {
+      const SLane s0 = locate(0);
+      cur_pk = pack(s0);
+      prm = params_of(s0, raw_of(s0, s0.ra, s0.role_a), raw_of(s0, s0.rb, s0.role_b));
+      hap_issue(0, s0);
+    }
+    for (int st = 0; st < nstr; ++st) {
+      const SLane cur = unpack(cur_pk);
+      hap_commit();
+      __syncthreads();
+
+      // This lane's role in the stripe.
+      const bool start = cur.act && (sl == 0 || cur.u == 0);
+      const bool is_z = cur.act && cur.u == 0;
+      const int zsh = (cur.role_a == 1) ? 1 : 0;  // the pad row reads Z one column on
+      const int lim = (cur.role_b == 4) ? cur.H + sl2 + 2 : -1;  // V at its column H + 1
+      const int need = cur.act ? cur.H + sl2 + 3 : 0;
+      const int nblk = (wave_max(need) + 15) >> 4;
+      const int hoff = 3 + ((cur_pk.w >> 5) & 3);
+      const unsigned char* const hp =
+          (cur.act ? hbufs + (cur.k & 1) * hstride + hoff : hbufs) + PFD - sl2;  // hp[t]: column t + PFD - 2l
+
+      // Next stripe: its lane state, raw rows and new haplotype, all in flight
+      // during this stripe.
+      RawRow na, nb;
+      SPack nxt_pk;
+      {
+        const SLane nxt = locate(st + 1);
+        na = raw_of(nxt, nxt.ra, nxt.role_a);
+        nb = raw_of(nxt, nxt.rb, nxt.role_b);
+        nxt_pk = pack(nxt);
+        hap_issue(st + 1, nxt);
+      }
+
+      Lane2 L;
+      L.Mo = L.Do = L.Xp = L.Xn = L.In = pf2{0.f, 0.f};
+      // the boundary value "received at step -1": Z one column on at column
+      // -2l for a pad row, 0 for every other source (columns < 0)
+      L.Xp.y = (is_z && zsh && sl == 0) ? 1.f : 0.f;
+      L.hbp = 6;
+      PhRing<float> pf[PFD];
+      int hq[PFD];
+#pragma unroll
+      for (int q = 0; q < PFD; ++q) {
+        pf[q] = is_z ? Z[32 + q - sl2 + zsh] : ring[q];
+        hq[q] = hp[q - PFD];
+      }
+      float acc = 0.f;
+      for (int blk = 0; blk < nblk; ++blk) {
+        const int t0 = 16 * blk;
+        const PhRing<float>* const rd = is_z ? Z + 32 + min(t0 + PFD - sl2 + zsh, 16) : ring + t0 + PFD;
+        const bool cond = __ballot(lim >= t0 && lim < t0 + 16) != 0ull;
+        const uint32_t wbase = lds_addr(ring + (t0 - 31));
+        const int dl = lim - t0;
+        if (blk >= 2) {
+          if (cond)
+            pstream_block<true, true>(L, pf, hq, hp, rd, prm, start, top, t0, dl, acc, wbase);
+          else
+            pstream_block<false, true>(L, pf, hq, hp, rd, prm, start, top, t0, dl, acc, wbase);
+        } else {
+          if (cond)
+            pstream_block<true, false>(L, pf, hq, hp, rd, prm, start, top, t0, dl, acc, wbase);
+          else
+            pstream_block<false, false>(L, pf, hq, hp, rd, prm, start, top, t0, dl, acc, wbase);
+        }
+      }
+      if (lim >= 0) {
+        const int p = cur.p;
+        if ((other >> cur.k) & 1u) {
+          const unsigned long long k = atomicAdd(fb_count, 1ull);
+          fb_list[k] = p;
+          out[p] = __builtin_nan("");
+        } else if (use_rescue && acc < thr) {
+          const unsigned long long k = atomicAdd(rescue_count, 1ull);
+          rescue_list[k] = p;
+          out[p] = __builtin_nan("");
+        } else {
+          out[p] = (double)(log10f(acc) - tab.log10_init);
+        }
+      }
+      // the next stripe's constants, at the stripe end: computed after block
+      // 0 (as phmm2 does) their values add ~60 VGPRs of pressure
+      prm = params_of(unpack(nxt_pk), na, nb);
+      cur_pk = nxt_pk;
+    }
+    __syncthreads();  // the next batch rewrites the hap buffers
+  }
+}
+
+}  // namespace fcs

@@ -323,3 +323,40 @@ def test_unwritten_results_are_an_error(gpu, tmp_path):
     # and without the fault the same batch is fine
     p = fcship.synth_phmm(7, 256)
     assert np.isfinite(fcship.phmm_compute_pairs(p)).all()
+
+
+@pytest.mark.parametrize("k", [3, 8])
+def test_streamed_segments_forced_k(gpu, tmp_path, k):
+    """The row-streamed kernel (phmm_stream.h) runs K pairs back to back per
+    16-lane segment; small batches use K = 1, so FCSHIP_STREAM_K forces longer
+    streams on test-sized batches: pairs end and start mid-stripe at every
+    lane, odd and even R (pad row), R below the streaming minimum (grouped
+    kernel), both stream hap classes, and haplotypes with bytes outside ACGTN
+    (handed back to the byte-compare kernel)."""
+    import subprocess
+    import sys
+    reads, haps = random_batch(900 + k, 240, 23, 1, 200, 1, 420)
+    h = haps[5].copy()
+    h[::9] = ord("R")
+    haps[5] = h
+    mixed = fcship.make_pairs(reads, haps)
+    c2 = fcship.synth_phmm(4242 + k, 4000)
+    paths = {}
+    for name, p in (("mixed", mixed), ("c2", c2)):
+        paths[name] = tmp_path / f"{name}.npz"
+        np.savez(paths[name], **{f: getattr(p, f) for f in p.__dataclass_fields__})
+    code = (
+        "import sys; sys.path.insert(0, %r)\n"
+        "import numpy as np, fcship\n"
+        "for name in ('mixed', 'c2'):\n"
+        "    d = np.load(sys.argv[1] + '/' + name + '.npz')\n"
+        "    p = fcship.PhmmPairs(**{f: d[f] for f in d.files})\n"
+        "    np.save(sys.argv[1] + '/' + name + '_out.npy', fcship.phmm_compute_pairs(p))\n"
+        "print('DONE')\n"
+    ) % fcship.__file__.rsplit("/", 1)[0]
+    env = dict(__import__("os").environ, FCSHIP_STREAM_K=str(k))
+    r = subprocess.run([sys.executable, "-c", code, str(tmp_path)], env=env, capture_output=True, text=True,
+                       timeout=120)
+    assert "DONE" in r.stdout, r.stderr[-3000:]
+    check_parity(mixed, np.load(tmp_path / "mixed_out.npy"), False)
+    check_parity(c2, np.load(tmp_path / "c2_out.npy"), False)

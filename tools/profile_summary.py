@@ -12,7 +12,7 @@ import os
 import shutil
 import sys
 
-KERNELS = ("phmm2_kernel", "phmm_kernel<float, false, false>")  # fp32 forward: two-row, one-row (long haps)
+KERNELS = ("phmm3_kernel", "phmm2_kernel", "phmm_kernel<float, false, false>")  # fp32 forward: streamed, two-row, one-row
 C2_CELLS = 22721383941  # sum R*H of the default C2 workload (bench.py config.cells_per_gpu)
 LAUNCHES_PER_PASS = 5   # C2's non-empty hap-length classes
 
