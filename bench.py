@@ -328,8 +328,8 @@ def main():
         "roofline": {"bound": "valu", "achieved": round(achieved_tf, 3), "peak": FP32_VECTOR_PEAK_TF,
                      "unit": "TFLOP/s", "frac": round(achieved_tf / FP32_VECTOR_PEAK_TF, 4),
                      "traffic": traffic,
-                     "kernel": "phmm2_kernel (two read rows per lane, packed FP32): fp32 forward pass = one launch "
-                               "per hap-length class, overlapped on 4 streams; achieved = algorithmic FLOPs / pass "
+                     "kernel": "phmm3_kernel (row-streamed segments, two read rows per lane, packed FP32): fp32 forward pass = one launch "
+                               "per launch class, overlapped on 4 streams; achieved = algorithmic FLOPs / pass "
                                "time (HIP events on the launch stream; rocprof pass span in "
                                "profiles/r2/r2b_phmm_summary.json)",
                      "valu_instr_per_cell": vipc,

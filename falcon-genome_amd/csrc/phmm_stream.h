@@ -354,12 +354,11 @@ __global__ __launch_bounds__(64, LB) void phmm3_kernel(
     };
 
     // Haplotype codes of the pair that starts in the coming stripe (at most one
-    // per segment): aligned dwords covering its bytes, issued a stripe ahead
-    // (kHapPre per lane; longer haplotypes load the rest when committed).  Its
-    // buffer (pair parity) was last used by the pair two back, which ended in
-    // an earlier stripe.  Column c of pair k sits at hbuf(k) + 3 + al + c.
-    constexpr int kHapPre = 5;
-    uint32_t hv[kHapPre];
+    // per segment): located a stripe ahead, loaded as the aligned dwords that
+    // cover its bytes when the stripe starts (holding five prefetched dwords
+    // per lane through a stripe measured 2% slower: VGPR pressure).  Its buffer
+    // (pair parity) was last used by the pair two back, which ended in an
+    // earlier stripe.  Column c of pair k sits at hbuf(k) + 3 + al + c.
     int hk = -1, hH = 0;
     const uint8_t* ha = nullptr;
     auto hap_issue = [&](int st_next, const SLane& first_lane15) {
@@ -372,13 +371,6 @@ __global__ __launch_bounds__(64, LB) void phmm3_kernel(
       hH = __shfl(Hm, sbase + kk);
       const int lo = __shfl((int)hom, sbase + kk), hi = __shfl((int)(hom >> 32), sbase + kk);
       ha = b.hb + (int64_t)(((uint64_t)(uint32_t)hi << 32) | (uint32_t)lo);
-      const int al = (int)((uintptr_t)ha & 3);
-      const uint32_t* const src = reinterpret_cast<const uint32_t*>(ha - al);
-#pragma unroll
-      for (int i = 0; i < kHapPre; ++i) {
-        const int j = sl + 16 * i;
-        hv[i] = (hk >= 0 && 4 * j < al + hH) ? src[j] : 0u;
-      }
     };
     auto hap_commit = [&] {
       bool oth = false;
@@ -394,12 +386,15 @@ __global__ __launch_bounds__(64, LB) void phmm3_kernel(
           if (hi > nb) valid &= 0xFFFFFFFFu >> (8 * (hi - nb));
           dst[j] = hap_codes4(x, valid, oth);
         };
+        constexpr int kB = 5;  // dwords per lane per round trip (320 bytes per segment)
+        for (int j0 = sl; 4 * j0 < nb; j0 += 16 * kB) {
+          uint32_t x[kB];
 #pragma unroll
-        for (int i = 0; i < kHapPre; ++i) {
-          const int j = sl + 16 * i;
-          if (4 * j < nb) put(j, hv[i]);
+          for (int i = 0; i < kB; ++i) x[i] = 4 * (j0 + 16 * i) < nb ? src[j0 + 16 * i] : 0u;
+#pragma unroll
+          for (int i = 0; i < kB; ++i)
+            if (4 * (j0 + 16 * i) < nb) put(j0 + 16 * i, x[i]);
         }
-        for (int j = sl + 16 * kHapPre; 4 * j < nb; j += 16) put(j, src[j]);
       }
       const unsigned long long bal = __ballot(oth);
       if (hk >= 0 && ((bal >> sbase) & 0xFFFFull)) other |= 1u << hk;
