@@ -8,6 +8,7 @@
 #include <tuple>
 
 #include "bam.h"
+#include "bam_input.h"
 #include "common.h"
 #include "fcship.h"
 #include "gatk_prep.h"
@@ -38,13 +39,14 @@ struct Read {
   std::string bi, bd;
 };
 
-void load_reads(const std::string& bam, const std::string& chrom, int64_t beg, int64_t end, const CallerOptions& opt,
-                std::vector<Read>& out) {
+void load_reads_one(const std::string& bam, const std::string& chrom, int64_t beg, int64_t end,
+                    const CallerOptions& opt, std::vector<Read>& out) {
   BamReader rd(bam);
   const int tid = rd.header().ref_index(chrom);
   if (tid < 0) return;
-  if (is_regular_file(bam + ".bai")) {
-    const uint64_t off = BamIndex(bam + ".bai").seek_offset(tid, beg);
+  const std::string bai = bam_index_path(bam);
+  if (!bai.empty()) {
+    const uint64_t off = BamIndex(bai).seek_offset(tid, beg);
     if (off) rd.seek(off);
   }
   BamRecord r;
@@ -68,6 +70,15 @@ void load_reads(const std::string& bam, const std::string& chrom, int64_t beg, i
   }
 }
 
+// Reads of the window from every part of the sample, in coordinate order
+// (parts of a `--disable-merge` alignment are each sorted).
+void load_reads(const std::vector<std::string>& bams, const std::string& chrom, int64_t beg, int64_t end,
+                const CallerOptions& opt, std::vector<Read>& out) {
+  for (const std::string& b : bams) load_reads_one(b, chrom, beg, end, opt, out);
+  if (bams.size() > 1)
+    std::stable_sort(out.begin(), out.end(), [](const Read& a, const Read& b) { return a.pos < b.pos; });
+}
+
 struct Allele {
   int64_t pos;  // 0-based anchor
   std::string ref, alt;
@@ -79,7 +90,29 @@ struct Pileup {
   int64_t wb = 0;
   std::vector<int> depth, events;
   std::map<Allele, int> support;
+  // GVCF reference model: per position, sum over bases of log10 P(base | 0/0,
+  // 0/1, 1/1) with 1 = <NON_REF> (any other base)
+  std::vector<double> gl;  // 3 per position; empty unless GVCF
 };
+
+// log10 P(base | genotype) per base quality: [q][0] ref base under 0/0 (1 - e),
+// [q][1] any base under 0/1 (0.5 (1 - e) + 0.5 e / 3), [q][2] non-ref base
+// under 0/0 (e / 3); a ref base under 1/1 is e / 3, a non-ref base 1 - e.
+struct RefModel {
+  double t[94][3];
+  RefModel() {
+    for (int q = 0; q < 94; ++q) {
+      const double e = std::min(0.75, std::pow(10.0, -q / 10.0));
+      t[q][0] = std::log10(1.0 - e);
+      t[q][1] = std::log10(0.5 * (1.0 - e) + 0.5 * e / 3.0);
+      t[q][2] = std::log10(e / 3.0);
+    }
+  }
+};
+const RefModel& ref_model() {
+  static const RefModel m;
+  return m;
+}
 
 // Walks every read's CIGAR once: depth, mismatch/indel events and allele support.
 void build_pileup(const std::string& ref, const std::vector<Read>& reads, int min_bq, Pileup& pu) {
@@ -96,9 +129,17 @@ void build_pileup(const std::string& ref, const std::vector<Read>& reads, int mi
             if (!in(rp) || rd.qual[q] < min_bq) continue;
             ++pu.depth[rp - pu.wb];
             const char b = rd.seq[q];
-            if (b != ref[rp] && ref[rp] != 'N' && b != 'N') {
+            const bool nonref = b != ref[rp] && ref[rp] != 'N' && b != 'N';
+            if (nonref) {
               ++pu.events[rp - pu.wb];
               ++pu.support[{rp, std::string(1, ref[rp]), std::string(1, b)}];
+            }
+            if (!pu.gl.empty()) {
+              const double* t = ref_model().t[std::min<int>(rd.qual[q], 93)];
+              double* g = &pu.gl[3 * (rp - pu.wb)];
+              g[0] += nonref ? t[2] : t[0];
+              g[1] += t[1];
+              g[2] += nonref ? t[0] : t[2];
             }
           }
           break;
@@ -310,9 +351,29 @@ void genotype_germline(const Region& g, const CallerOptions& opt, int64_t own_be
     rec.qual = qual;
     rec.info = "DP=" + std::to_string(la.size());
     rec.format = "GT:AD:DP:GQ:PL";
-    rec.samples = {std::string(gt == 1 ? "0/1" : "1/1") + ":" + std::to_string(ad_ref) + "," + std::to_string(ad_alt) +
-                   ":" + std::to_string(la.size()) + ":" + std::to_string(gq) + ":" + std::to_string(pl[0]) + "," +
-                   std::to_string(pl[1]) + "," + std::to_string(pl[2])};
+    std::string pls = std::to_string(pl[0]) + "," + std::to_string(pl[1]) + "," + std::to_string(pl[2]);
+    std::string ad = std::to_string(ad_ref) + "," + std::to_string(ad_alt);
+    if (opt.gvcf) {
+      // <NON_REF> as a third allele [EXT stand-in for GATK's non-ref likelihoods]:
+      // each read's likelihood under it is its worst haplotype's; PLs of the six
+      // genotypes (0/0 0/1 1/1 0/2 1/2 2/2) from the same diploid model
+      const size_t nh = g.haps.size();
+      double g6[6] = {gl[0], gl[1], gl[2], 0, 0, 0};
+      for (size_t r = 0; r < la.size(); ++r) {
+        double ln = INFINITY;
+        for (size_t h = 0; h < nh; ++h) ln = std::min(ln, g.lik[0][r * nh + h]);
+        g6[3] += log10_add(lr[r], ln) - std::log10(2.0);
+        g6[4] += log10_add(la[r], ln) - std::log10(2.0);
+        g6[5] += ln;
+      }
+      const double m6 = *std::max_element(g6, g6 + 6);
+      pls.clear();
+      for (int k = 0; k < 6; ++k) pls += (k ? "," : "") + std::to_string((int)std::lround(-10.0 * (g6[k] - m6)));
+      rec.alts.push_back("<NON_REF>");
+      ad += ",0";
+    }
+    rec.samples = {std::string(gt == 1 ? "0/1" : "1/1") + ":" + ad + ":" + std::to_string(la.size()) + ":" +
+                   std::to_string(gq) + ":" + pls};
     calls.push_back(rec);
   }
 }
@@ -359,18 +420,95 @@ void genotype_somatic(const Region& g, const CallerOptions& opt, int64_t own_beg
   }
 }
 
+// Reference-confidence blocks of [beg, end) around this interval's calls
+// (GATK --emitRefConfidence GVCF): every position not inside a call's REF span
+// gets the hom-ref genotype likelihoods of its pileup (RefModel); runs of
+// positions whose GQ falls in one band become one record
+// "<NON_REF> END=..  GT:DP:GQ:MIN_DP:PL" with the block's median DP, minimum
+// GQ / DP and element-wise minimum PLs.
+void emit_gvcf(const std::string& seq, const Pileup& pu, int64_t beg, int64_t end, const std::string& chrom,
+               std::vector<const VcfRecord*>& ic, std::vector<VcfRecord>& out) {
+  std::stable_sort(ic.begin(), ic.end(), [](const VcfRecord* a, const VcfRecord* b) { return a->pos < b->pos; });
+  struct Block {
+    int64_t b = -1, e = -1;
+    int band = -1, gq = 99, mindp = 0;
+    int pl[3] = {0, 0, 0};
+    std::vector<int> dps;
+  } blk;
+  auto flush = [&] {
+    if (blk.b < 0) return;
+    VcfRecord r;
+    r.chrom = chrom;
+    r.pos = blk.b + 1;
+    r.ref = std::string(1, seq[blk.b]);
+    r.alts = {"<NON_REF>"};
+    r.filter = ".";
+    r.info = "END=" + std::to_string(blk.e + 1);
+    r.format = "GT:DP:GQ:MIN_DP:PL";
+    std::nth_element(blk.dps.begin(), blk.dps.begin() + blk.dps.size() / 2, blk.dps.end());
+    r.samples = {"0/0:" + std::to_string(blk.dps[blk.dps.size() / 2]) + ":" + std::to_string(blk.gq) + ":" +
+                 std::to_string(blk.mindp) + ":" + std::to_string(blk.pl[0]) + "," + std::to_string(blk.pl[1]) + "," +
+                 std::to_string(blk.pl[2])};
+    out.push_back(std::move(r));
+    blk = Block();
+  };
+  size_t ci = 0;
+  int64_t covered = beg;  // positions below are inside an emitted call's REF span
+  for (int64_t p = beg; p < end; ++p) {
+    while (ci < ic.size() && ic[ci]->pos - 1 <= p) {
+      flush();
+      out.push_back(*ic[ci]);
+      covered = std::max<int64_t>(covered, ic[ci]->pos - 1 + (int64_t)ic[ci]->ref.size());
+      ++ci;
+    }
+    if (p < covered) continue;
+    const int dp = pu.depth[p - pu.wb];
+    const double* g = &pu.gl[3 * (p - pu.wb)];
+    const double mx = std::max({g[0], g[1], g[2]});
+    int pl[3];
+    for (int k = 0; k < 3; ++k) pl[k] = (int)std::lround(-10.0 * (g[k] - mx));
+    const int gq = (pl[0] == 0) ? std::min(99, std::min(pl[1], pl[2])) : 0;
+    const int band = gvcf_band(gq);
+    if (blk.b < 0 || band != blk.band || p != blk.e + 1) {
+      flush();
+      blk.b = p;
+      blk.band = band;
+      blk.gq = gq;
+      blk.mindp = dp;
+      for (int k = 0; k < 3; ++k) blk.pl[k] = pl[k];
+    }
+    blk.e = p;
+    blk.gq = std::min(blk.gq, gq);
+    blk.mindp = std::min(blk.mindp, dp);
+    for (int k = 0; k < 3; ++k) blk.pl[k] = std::min(blk.pl[k], pl[k]);
+    blk.dps.push_back(dp);
+  }
+  flush();
+  for (; ci < ic.size(); ++ci) out.push_back(*ic[ci]);
+}
+
 }  // namespace
 
-CallerStats call_intervals(const Reference& ref, const std::string& bam, const std::string& normal_bam,
-                           const std::vector<Interval>& intervals, const CallerOptions& opt, VcfWriter& out) {
+int gvcf_band(int gq) {
+  static const int bounds[] = {1,  2,  3,  4,  5,  6,  7,  8,  9,  10, 11, 12, 13, 14, 15, 16, 17, 18, 19, 20, 21, 22,
+                               23, 24, 25, 26, 27, 28, 29, 30, 31, 32, 33, 34, 35, 36, 37, 38, 39, 40, 41, 42, 43, 44,
+                               45, 46, 47, 48, 49, 50, 51, 52, 53, 54, 55, 56, 57, 58, 59, 60, 70, 80, 90, 99};
+  return (int)(std::upper_bound(std::begin(bounds), std::end(bounds), gq) - std::begin(bounds));
+}
+
+CallerStats call_intervals(const Reference& ref, const std::vector<std::string>& bams,
+                           const std::vector<std::string>& normal_bams, const std::vector<Interval>& intervals_in,
+                           const CallerOptions& opt, VcfWriter& out) {
   CallerStats st;
   const uint64_t t0 = now_us();
   std::FILE* dump = opt.dump_path.empty() ? nullptr : std::fopen(opt.dump_path.c_str(), "ab");
-  std::vector<VcfRecord> calls;
+  std::vector<VcfRecord> calls, gout;
+  const std::vector<Interval>& intervals = intervals_in;
   std::vector<std::unique_ptr<Region>> pending;
   std::vector<std::tuple<int64_t, int64_t, std::string>> own;  // per pending region: owned range + chrom
   auto flush = [&] {
     if (pending.empty()) return;
+    if (interrupted()) throw interruptedError();
     run_phmm(pending, opt, st, dump);
     for (size_t i = 0; i < pending.size(); ++i) {
       const auto& [ob, oe, chrom] = own[i];
@@ -381,6 +519,8 @@ CallerStats call_intervals(const Reference& ref, const std::string& bam, const s
     own.clear();
   };
   for (const Interval& iv : intervals) {
+    if (interrupted()) throw interruptedError();
+    const size_t c0 = calls.size();
     const int ci = ref.index(iv.chrom);
     if (ci < 0) throw invalidParam("interval contig " + iv.chrom + " is not in the reference");
     const std::string& seq = ref.contigs[ci].seq;
@@ -404,12 +544,13 @@ CallerStats call_intervals(const Reference& ref, const std::string& bam, const s
       we = std::min<int64_t>(L, own_end + ext_r);
       reads[0].clear();
       reads[1].clear();
-      load_reads(bam, iv.chrom, wb, we, opt, reads[0]);
-      if (opt.somatic) load_reads(normal_bam, iv.chrom, wb, we, opt, reads[1]);
+      load_reads(bams, iv.chrom, wb, we, opt, reads[0]);
+      if (opt.somatic) load_reads(normal_bams, iv.chrom, wb, we, opt, reads[1]);
       pu = Pileup();
       pu.wb = wb;
       pu.depth.assign(we - wb, 0);
       pu.events.assign(we - wb, 0);
+      if (opt.gvcf && !opt.somatic) pu.gl.assign(3 * (we - wb), 0.0);
       build_pileup(seq, reads[0], opt.min_base_quality, pu);
       if (opt.somatic) build_pileup(seq, reads[1], opt.min_base_quality, pu);
       std::vector<int64_t> sites;
@@ -485,21 +626,27 @@ CallerStats call_intervals(const Reference& ref, const std::string& bam, const s
       }
     }
     flush();
+    if (opt.gvcf && !opt.somatic) {
+      std::vector<const VcfRecord*> ic;
+      for (size_t i = c0; i < calls.size(); ++i) ic.push_back(&calls[i]);
+      emit_gvcf(seq, pu, own_beg, own_end, iv.chrom, ic, gout);
+    }
   }
   flush();
   if (dump) std::fclose(dump);
-  std::stable_sort(calls.begin(), calls.end(), [&](const VcfRecord& a, const VcfRecord& b) {
+  st.calls = (int64_t)calls.size();
+  std::vector<VcfRecord>& recs = (opt.gvcf && !opt.somatic) ? gout : calls;
+  std::stable_sort(recs.begin(), recs.end(), [&](const VcfRecord& a, const VcfRecord& b) {
     const int ia = ref.index(a.chrom), ib = ref.index(b.chrom);
     return ia != ib ? ia < ib : a.pos < b.pos;
   });
-  for (const VcfRecord& r : calls) out.write(r);
-  st.calls = (int64_t)calls.size();
+  for (const VcfRecord& r : recs) out.write(r);
   st.seconds = (now_us() - t0) / 1e6;
   return st;
 }
 
 VcfHeader caller_vcf_header(const Reference& ref, const std::vector<std::string>& samples, bool somatic,
-                            const std::string& ref_path) {
+                            const std::string& ref_path, bool gvcf) {
   VcfHeader h;
   for (const Contig& c : ref.contigs) h.contigs.emplace_back(c.name, (int64_t)c.seq.size());
   h.samples = samples;
@@ -520,6 +667,20 @@ VcfHeader caller_vcf_header(const Reference& ref, const std::vector<std::string>
               "##FORMAT=<ID=GQ,Number=1,Type=Integer,Description=\"Genotype quality\">",
               "##FORMAT=<ID=PL,Number=G,Type=Integer,Description=\"Phred-scaled genotype likelihoods\">",
               "##FILTER=<ID=PASS,Description=\"All filters passed\">"};
+    if (gvcf) {
+      h.meta.push_back("##ALT=<ID=NON_REF,Description=\"Represents any possible alternative allele at this location\">");
+      h.meta.push_back("##INFO=<ID=END,Number=1,Type=Integer,Description=\"Stop position of the interval\">");
+      h.meta.push_back(
+          "##FORMAT=<ID=MIN_DP,Number=1,Type=Integer,Description=\"Minimum DP observed within the GVCF block\">");
+      int lo = 0;
+      for (int hi : {1,  2,  3,  4,  5,  6,  7,  8,  9,  10, 11, 12, 13, 14, 15, 16, 17, 18, 19, 20, 21, 22,
+                     23, 24, 25, 26, 27, 28, 29, 30, 31, 32, 33, 34, 35, 36, 37, 38, 39, 40, 41, 42, 43, 44,
+                     45, 46, 47, 48, 49, 50, 51, 52, 53, 54, 55, 56, 57, 58, 59, 60, 70, 80, 90, 99, 100}) {
+        h.meta.push_back("##GVCFBlock" + std::to_string(lo) + "-" + std::to_string(hi) + "=minGQ=" + std::to_string(lo) +
+                         "(inclusive),maxGQ=" + std::to_string(hi) + "(exclusive)");
+        lo = hi;
+      }
+    }
   }
   return h;
 }

@@ -41,6 +41,7 @@ struct CallerOptions {
   double min_qual = 30.0;  // stand_call_conf
   double tlod = 6.3, nlod = 2.2;
   std::string dump_path;  // if set: append every region's PairHMM inputs/outputs here (tests)
+  bool gvcf = false;      // htc without -v: reference-confidence blocks + <NON_REF> (GATK --emitRefConfidence GVCF)
 };
 
 struct CallerStats {
@@ -50,14 +51,20 @@ struct CallerStats {
   void add(const CallerStats& o);
 };
 
-// Calls variants of `bam` (tumor BAM in Mutect2 mode, with `normal_bam`) on
-// the intervals; records with POS inside an interval are written to `out` in
-// coordinate order.
-CallerStats call_intervals(const Reference& ref, const std::string& bam, const std::string& normal_bam,
-                           const std::vector<Interval>& intervals, const CallerOptions& opt, VcfWriter& out);
+// Calls variants of `bams` (the parts of one sample, read as one; the tumor in
+// Mutect2 mode, with `normal_bams`) on the intervals; records with POS inside an
+// interval are written to `out` in coordinate order.  In GVCF mode every
+// position of the intervals is covered once: by a call or by a hom-ref block.
+CallerStats call_intervals(const Reference& ref, const std::vector<std::string>& bams,
+                           const std::vector<std::string>& normal_bams, const std::vector<Interval>& intervals,
+                           const CallerOptions& opt, VcfWriter& out);
 
 // Header of the caller's VCF (FORMAT/INFO definitions, contigs, samples).
 VcfHeader caller_vcf_header(const Reference& ref, const std::vector<std::string>& samples, bool somatic,
-                            const std::string& ref_path);
+                            const std::string& ref_path, bool gvcf = false);
+
+// GATK's default GVCF GQ bands (--GVCFGQBands 1..60, 70, 80, 90, 99): the
+// band index of a GQ value; a block holds consecutive positions of one band.
+int gvcf_band(int gq);
 
 }  // namespace fcsg

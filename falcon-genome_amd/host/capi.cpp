@@ -7,6 +7,8 @@
 #include <string>
 
 #include "bam.h"
+#include "bam_input.h"
+#include "caller.h"
 #include "bgzf.h"
 #include "common.h"
 #include "config.h"
@@ -66,6 +68,35 @@ int fcsg_partition_dict(const char* dict_path, int ncontigs, int skip_pseudo, ch
   });
   return g ? g : rc;
 }
+
+// BamInput::merge_region: "bam1,bam2,...\n<region file>\n" of shard `contig`.
+int fcsg_bam_input_shard(const char* path, int contig, int ncontigs, const char* temp_dir, char* buf, int cap) {
+  int rc = 0;
+  const int g = guard([&] {
+    const BamShard sh = BamInput(path).merge_region(contig, ncontigs, temp_dir);
+    std::string s;
+    for (size_t i = 0; i < sh.bams.size(); ++i) s += (i ? "," : "") + sh.bams[i];
+    s += "\n" + sh.region + "\n";
+    rc = copy_out(s, buf, cap);
+  });
+  return g ? g : rc;
+}
+
+// read_regions of each path, intersected when several: "chrom\tlb\tub\n" lines.
+int fcsg_intersect_regions(const char* const* paths, int n, char* buf, int cap) {
+  int rc = 0;
+  const int g = guard([&] {
+    std::vector<std::vector<Interval>> sets;
+    for (int i = 0; i < n; ++i) sets.push_back(read_regions(paths[i]));
+    const auto out = sets.size() == 1 ? sets[0] : intersect_interval_sets(sets);
+    std::string s;
+    for (const Interval& iv : out) s += iv.chrom + "\t" + std::to_string(iv.lb) + "\t" + std::to_string(iv.ub) + "\n";
+    rc = copy_out(s, buf, cap);
+  });
+  return g ? g : rc;
+}
+
+int fcsg_gvcf_band(int gq) { return gvcf_band(gq); }
 
 int fcsg_bgzf_compress_file(const char* in, const char* out) {
   return guard([&] { bgzip_file(in, out); });

@@ -5,6 +5,7 @@
 #include <unistd.h>
 
 #include <algorithm>
+#include <atomic>
 #include <cerrno>
 #include <cstdio>
 #include <cstring>
@@ -12,6 +13,13 @@
 #include <sstream>
 
 namespace fcsg {
+
+namespace {
+std::atomic<int> g_interrupt{0};
+}
+bool interrupted() { return g_interrupt.load(std::memory_order_relaxed) != 0; }
+int interrupt_signal() { return g_interrupt.load(); }
+void set_interrupted(int sig) { g_interrupt.store(sig); }
 
 bool path_exists(const std::string& p) {
   struct stat st;

@@ -44,6 +44,12 @@ class pathEmpty : public std::runtime_error {
  public:
   explicit pathEmpty(const std::string& what) : std::runtime_error("Path of " + what + " is empty") {}
 };
+// Raised where work notices that SIGINT/SIGTERM/SIGHUP arrived (interrupted());
+// fcs-genome then removes its temp dir and exits 130.
+class interruptedError : public failedCommand {
+ public:
+  interruptedError() : failedCommand("[E::fcs-genome] interrupted") {}
+};
 class formatError : public std::runtime_error {
  public:
   explicit formatError(const std::string& what) : std::runtime_error("[E::fcsg] " + what) {}
@@ -67,6 +73,13 @@ inline std::string basename_of(const std::string& path) {
   const size_t k = path.find_last_of('/');
   return k == std::string::npos ? path : path.substr(k + 1);
 }
+
+// Interrupt state (the reference's sigint_handler, src/main.cpp:43-54): set by
+// the signal thread of main(), polled by the Executor before it starts a task
+// and by the in-process workers between device passes.
+bool interrupted();
+int interrupt_signal();
+void set_interrupted(int sig);
 
 bool path_exists(const std::string& p);
 bool is_regular_file(const std::string& p);

@@ -56,6 +56,7 @@ void Stage::run() {
   std::cerr << "[fcs-genome] Start doing " << label_ << std::endl;
   std::vector<std::future<void>> pending;
   for (size_t i = 0; i < tasks_.size(); ++i) {
+    if (interrupted()) break;
     tasks_[i]->check();  // caller thread, like the reference: a bad argument aborts before anything runs
     auto done = std::make_shared<std::promise<void>>();
     pending.push_back(done->get_future());
@@ -69,6 +70,7 @@ void Stage::run() {
     });
   }
   for (auto& f : pending) f.wait();
+  if (interrupted()) throw interruptedError();
   const std::string stage_log = ex_->get_log_name(label_);
   {
     std::ofstream out(stage_log, std::ios::app);
@@ -147,6 +149,7 @@ void Executor::run() {
 }
 
 int Executor::execute(Worker_ptr w, const std::string& log) {
+  if (interrupted()) return 128 + interrupt_signal();  // queued but not started
   TaskContext ctx;
   ctx.job_id = job_id_.fetch_add(1);
   ctx.gpu = gpus_.empty() ? -1 : gpus_[ctx.job_id % gpus_.size()];

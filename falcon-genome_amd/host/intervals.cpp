@@ -1,6 +1,9 @@
 #include "intervals.h"
 
+#include <algorithm>
 #include <fstream>
+#include <map>
+#include <sstream>
 
 #include "common.h"
 #include "fasta.h"
@@ -86,6 +89,81 @@ void write_interval_list(const std::string& path, const std::vector<Interval>& i
   std::ofstream out(path);
   if (!out) throw fileNotFound(path + " (cannot write)");
   for (const Interval& i : iv) out << i.chrom << ':' << i.lb << '-' << i.ub << '\n';
+}
+
+std::vector<Interval> read_bed(const std::string& path) {
+  std::ifstream in(path);
+  if (!in) throw fileNotFound(path);
+  std::vector<Interval> out;
+  std::string line;
+  while (std::getline(in, line)) {
+    if (line.empty() || line[0] == '#' || line.rfind("track", 0) == 0 || line.rfind("browser", 0) == 0) continue;
+    std::istringstream ss(line);
+    Interval iv;
+    int64_t b0 = 0, e0 = 0;
+    if (!(ss >> iv.chrom >> b0 >> e0) || b0 < 0 || e0 < b0) throw invalidParam("BED line '" + line + "' in " + path);
+    if (e0 == b0) continue;  // empty
+    iv.lb = b0 + 1;
+    iv.ub = e0;
+    out.push_back(iv);
+  }
+  return out;
+}
+
+std::vector<Interval> read_regions(const std::string& path) {
+  const size_t n = path.size();
+  if (n >= 4 && path.compare(n - 4, 4, ".bed") == 0) return read_bed(path);
+  return read_interval_list(path);
+}
+
+namespace {
+
+// sorted, merged (overlapping or adjacent) intervals per contig
+std::map<std::string, std::vector<std::pair<int64_t, int64_t>>> normalise(const std::vector<Interval>& iv) {
+  std::map<std::string, std::vector<std::pair<int64_t, int64_t>>> m;
+  for (const Interval& i : iv) m[i.chrom].emplace_back(i.lb, i.ub);
+  for (auto& [c, v] : m) {
+    std::sort(v.begin(), v.end());
+    std::vector<std::pair<int64_t, int64_t>> o;
+    for (const auto& x : v) {
+      if (!o.empty() && x.first <= o.back().second + 1) o.back().second = std::max(o.back().second, x.second);
+      else o.push_back(x);
+    }
+    v = std::move(o);
+  }
+  return m;
+}
+
+}  // namespace
+
+std::vector<Interval> intersect_interval_sets(const std::vector<std::vector<Interval>>& sets) {
+  if (sets.empty()) return {};
+  std::vector<std::string> order;
+  for (const Interval& i : sets[0])
+    if (std::find(order.begin(), order.end(), i.chrom) == order.end()) order.push_back(i.chrom);
+  auto acc = normalise(sets[0]);
+  for (size_t k = 1; k < sets.size(); ++k) {
+    auto other = normalise(sets[k]);
+    for (auto& [c, v] : acc) {
+      const auto it = other.find(c);
+      std::vector<std::pair<int64_t, int64_t>> o;
+      if (it != other.end()) {
+        const auto& w = it->second;
+        size_t a = 0, b = 0;
+        while (a < v.size() && b < w.size()) {
+          const int64_t lo = std::max(v[a].first, w[b].first), hi = std::min(v[a].second, w[b].second);
+          if (lo <= hi) o.emplace_back(lo, hi);
+          if (v[a].second < w[b].second) ++a;
+          else ++b;
+        }
+      }
+      v = std::move(o);
+    }
+  }
+  std::vector<Interval> out;
+  for (const std::string& c : order)
+    for (const auto& x : acc[c]) out.push_back({c, x.first, x.second});
+  return out;
 }
 
 }  // namespace fcsg

@@ -25,5 +25,13 @@ std::vector<std::string> init_contig_intv(const std::string& ref_path, int ncont
                                           bool skip_pseudo_chr = true);
 std::vector<Interval> read_interval_list(const std::string& path);
 void write_interval_list(const std::string& path, const std::vector<Interval>& iv);
+// BED (chrom, 0-based start, end; half-open) as 1-based inclusive intervals;
+// "track"/"browser"/"#" lines skipped.
+std::vector<Interval> read_bed(const std::string& path);
+// A region file by extension: .bed as BED, anything else as a GATK interval list.
+std::vector<Interval> read_regions(const std::string& path);
+// GATK's -isr INTERSECTION of several -L sets: the positions every set holds,
+// as sorted, merged intervals (contig order = first appearance in sets[0]).
+std::vector<Interval> intersect_interval_sets(const std::vector<std::vector<Interval>>& sets);
 
 }  // namespace fcsg

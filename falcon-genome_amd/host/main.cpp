@@ -4,8 +4,13 @@
 // src/worker-align.cpp:29-42), config keys (`conf`) and exit codes
 // (src/main.cpp:165-240: help 0, bad option 1/2, missing file 3, failed
 // stage 4, other error -1), plus `synth` for the synthetic C1/C4/C5 inputs.
+#include <pthread.h>
+#include <unistd.h>
+
+#include <csignal>
 #include <cstring>
 #include <iostream>
+#include <thread>
 #include <map>
 #include <memory>
 #include <string>
@@ -133,13 +138,23 @@ std::vector<std::vector<std::string>> shard_intervals(const std::string& ref, co
   return out;
 }
 
+// Shards of a directory input (BamInput): the parts' region files give the
+// intervals, so only the user's -L (if any) goes to every shard
+// (src/worker-htc.cpp:88-97: init_contig_intv only for a regular-file input).
+std::vector<std::vector<std::string>> dir_shards(const std::string& intv_list) {
+  std::vector<std::vector<std::string>> out(conf().get_int("gatk.ncontigs"));
+  if (!intv_list.empty())
+    for (auto& v : out) v.push_back(intv_list);
+  return out;
+}
+
 int htc_main(int argc, char** argv) {
   Args a;
   common_opts(a);
   a.add("ref", "r", false, true, "reference genome path");
-  a.add("input", "i", false, true, "input BAM file");
-  a.add("output", "o", false, true, "output VCF file (<output>.gz + .tbi are written too)");
-  a.add("produce-vcf", "v", true, false, "produce VCF (the only mode: GVCF blocks are not emitted)");
+  a.add("input", "i", false, true, "input BAM file or directory of part-XXXXXX.bam + .bed/.list");
+  a.add("output", "o", false, true, "output GVCF/VCF file (<output>.gz + .tbi are written too)");
+  a.add("produce-vcf", "v", true, false, "produce VCF instead of GVCF (reference-confidence blocks)");
   a.add("intervalList", "L", false, false, "interval list file");
   a.add("sample-id", "", false, false, "sample id for log files");
   a.add("skip-concat", "s", true, false, "(deprecated) produce a set of VCF files instead of one");
@@ -159,16 +174,17 @@ int htc_main(int argc, char** argv) {
   const std::vector<int> gpus = slots();
   const std::string out_dir = conf().temp_dir() + "/htc";
   create_dir(out_dir);
-  const auto shards = shard_intervals(ref, a.get("intervalList"));
+  const bool flag_vcf = a.has("produce-vcf");
+  const auto shards = is_directory(input) ? dir_shards(a.get("intervalList")) : shard_intervals(ref, a.get("intervalList"));
   BackgroundExecutor warm("gpu-warmup", std::make_shared<DeviceWarmupWorker>(gpus));
   Executor ex("Haplotype Caller", conf().get_int("gatk.htc.nprocs", "gatk.nprocs"), gpus);
   std::vector<std::string> parts;
   warm.wait();
   if (warm.status() != 0) throw failedCommand(std::string("[E::fcs-genome] GPU warm-up failed: ") + fcs_last_error());
   for (size_t k = 0; k < shards.size(); ++k) {
-    const std::string part = get_contig_fname(out_dir, (int)k, "vcf");
+    const std::string part = get_contig_fname(out_dir, (int)k, flag_vcf ? "vcf" : "g.vcf");
     parts.push_back(part);
-    ex.addTask(std::make_shared<HTCWorker>(ref, shards[k], input, part, extra, (int)k, true, true), sample_id);
+    ex.addTask(std::make_shared<HTCWorker>(ref, shards[k], input, part, extra, (int)k, flag_vcf, true), sample_id);
   }
   const std::string plain = output;
   ex.addTask(std::make_shared<VCFConcatWorker>(parts, plain), sample_id, true);
@@ -185,8 +201,8 @@ int mutect2_main(int argc, char** argv) {
   Args a;
   common_opts(a);
   a.add("ref", "r", false, true, "reference genome path");
-  a.add("normal", "n", false, true, "input normal BAM file");
-  a.add("tumor", "t", false, true, "input tumor BAM file");
+  a.add("normal", "n", false, true, "input normal BAM file or directory");
+  a.add("tumor", "t", false, true, "input tumor BAM file or directory");
   a.add("output", "o", false, true, "output VCF file");
   a.add("intervalList", "L", false, false, "interval list file");
   a.add("normal_name", "a", false, false, "normal sample name");
@@ -205,7 +221,10 @@ int mutect2_main(int argc, char** argv) {
   const std::vector<int> gpus = slots();
   const std::string out_dir = conf().temp_dir() + "/mutect2";
   create_dir(out_dir);
-  const auto shards = shard_intervals(ref, a.get("intervalList"));
+  // reference intervals only when both inputs are plain BAM files (src/worker-mutect2.cpp:146-150)
+  const auto shards = (is_regular_file(a.get("normal")) && is_regular_file(a.get("tumor")))
+                          ? shard_intervals(ref, a.get("intervalList"))
+                          : dir_shards(a.get("intervalList"));
   Executor ex("Mutect2", conf().get_int("gatk.mutect2.nprocs", "gatk.nprocs"), gpus);
   std::vector<std::string> parts;
   const std::string sample_id = a.get("sample-id");
@@ -237,6 +256,7 @@ int synth_main(int argc, char** argv) {
   a.add("somatic-af", "", false, false, "somatic allele fraction (default 0.3)");
   a.add("noisy-frac", "", false, false, "fraction of reads drawn with 20% high-quality mismatches (mis-mapped-like)");
   a.add("spike", "", false, false, "chr:pos[,chr:pos...] plant three het SNVs at pos-30, pos, pos+30 (1-based)");
+  a.add("parts", "", false, false, "also split the sample into parts/part-XXXXXX.bam + .bed (N buckets)");
   a.parse(argc, argv);
   SynthSpec sp;
   if (a.has("contigs")) {
@@ -264,6 +284,7 @@ int synth_main(int argc, char** argv) {
     }
   }
   if (a.has("noisy-frac")) sp.noisy_frac = std::stod(a.get("noisy-frac"));
+  if (a.has("parts")) sp.parts = std::stoi(a.get("parts"));
   if (a.has("coverage")) sp.coverage = std::stod(a.get("coverage"));
   if (a.has("seed")) sp.seed = std::stoull(a.get("seed"));
   if (a.has("max-reads")) sp.max_reads = std::stoll(a.get("max-reads"));
@@ -273,9 +294,31 @@ int synth_main(int argc, char** argv) {
   const SynthOutputs o = synth_dataset(sp, a.get("output"));
   std::cout << "{\"ref\": \"" << o.ref_fasta << "\", \"bam\": \"" << o.bam << "\", \"fastq\": \"" << o.fastq
             << "\", \"truth\": \"" << o.truth_vcf << "\", \"tumor_bam\": \"" << o.tumor_bam
+            << "\", \"parts\": \"" << o.parts_dir
             << "\", \"reads\": " << o.n_reads << ", \"tumor_reads\": " << o.n_tumor_reads
             << ", \"variants\": " << o.variants.size() << "}" << std::endl;
   return 0;
+}
+
+// SIGINT / SIGTERM / SIGHUP (the reference's sigint_handler, src/main.cpp:43-54):
+// blocked in every thread and taken by one sigwait thread, which announces the
+// interrupt and sets the flag the Executor and the workers poll; the run then
+// unwinds, removes its temp dir and exits 128 + signal.  A second signal exits
+// at once.
+void start_signal_thread() {
+  sigset_t set;
+  sigemptyset(&set);
+  sigaddset(&set, SIGINT);
+  sigaddset(&set, SIGTERM);
+  sigaddset(&set, SIGHUP);
+  pthread_sigmask(SIG_BLOCK, &set, nullptr);
+  std::thread([set] {
+    int sig = 0;
+    if (sigwait(&set, &sig) != 0) return;
+    std::cerr << "[fcs-genome] Caught interrupt, cleaning up..." << std::endl;
+    set_interrupted(sig);
+    if (sigwait(&set, &sig) == 0) _exit(128 + sig);
+  }).detach();
 }
 
 int print_help() {
@@ -307,6 +350,7 @@ int main(int argc, char** argv) {
     const size_t k = self.find_last_of('/');
     root = k == std::string::npos ? "." : self.substr(0, k) + "/..";
   }
+  start_signal_thread();  // before any other thread exists, so all inherit the mask
   try {
     conf().init(root);
     if (cmd == "htc") ret = htc_main(argc - 1, argv + 1);
@@ -336,6 +380,9 @@ int main(int argc, char** argv) {
     ret = 3;
   } catch (silentExit&) {
     ret = 1;
+  } catch (interruptedError&) {
+    remove_path(conf().temp_dir());
+    ret = 128 + interrupt_signal();
   } catch (failedCommand& e) {
     if (*e.what()) std::cerr << e.what() << std::endl;
     ret = 4;

@@ -1,5 +1,7 @@
 #include "synth.h"
 
+#include "intervals.h"
+
 #include <algorithm>
 #include <cmath>
 #include <fstream>
@@ -258,6 +260,7 @@ SynthOutputs synth_dataset(const SynthSpec& spec, const std::string& dir) {
       const int L = spec.read_len;
       const int64_t n = (int64_t)(coverage * (double)ref.contigs[c].seq.size() / L);
       for (int64_t k = 0; k < n; ++k) {
+        if ((k & 0xFFFF) == 0 && interrupted()) throw interruptedError();
         const int copy = (int)hr.below(2);
         const int som = tumor && hr.uniform() < 2 * spec.somatic_af ? 1 : 0;  // somatic on one copy → AF = somatic_af
         const Hap& hp = haps[copy][som];
@@ -299,6 +302,27 @@ SynthOutputs synth_dataset(const SynthSpec& spec, const std::string& dir) {
     out.fastq = dir + "/sample.fastq";
     out.n_reads = (int64_t)rs.first.size();
     write_reads(rs.first, rs.second, out.bam, out.fastq);
+    if (spec.parts > 0) {
+      std::vector<std::pair<std::string, int64_t>> dict;
+      for (const Contig& c : ref.contigs) dict.emplace_back(c.name, (int64_t)c.seq.size());
+      const auto buckets = partition_contigs(dict, spec.parts, false);
+      out.parts_dir = dir + "/parts";
+      create_dir(out.parts_dir);
+      for (int k = 0; k < spec.parts; ++k) {
+        std::vector<SimRead> part;
+        for (const SimRead& sr : rs.first) {
+          const std::string& chrom = ref.contigs[sr.rec.ref_id].name;
+          for (const Interval& iv : buckets[k])
+            if (iv.chrom == chrom && sr.pos + 1 >= iv.lb && sr.pos + 1 <= iv.ub) {
+              part.push_back(sr);
+              break;
+            }
+        }
+        write_reads(part, rs.second, get_contig_fname(out.parts_dir, k, "bam"), "");
+        std::ofstream bed(get_contig_fname(out.parts_dir, k, "bed"));
+        for (const Interval& iv : buckets[k]) bed << iv.chrom << '\t' << iv.lb - 1 << '\t' << iv.ub << '\n';
+      }
+    }
   }
   if (spec.somatic_rate > 0) {
     auto rs = sample_reads("tumor", true, spec.tumor_coverage, 0x4000);

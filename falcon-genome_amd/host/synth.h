@@ -41,10 +41,14 @@ struct SynthSpec {
   // planted clusters: three het SNVs at centre - 30, centre, centre + 30
   // (0-based), replacing random variants within 100 bp (shard-boundary tests)
   std::vector<std::pair<std::string, int64_t>> spikes;
+  // > 0: also write <dir>/parts/part-XXXXXX.bam (+ .bai, .bed) — the sample's
+  // reads split by alignment start into `parts` genome buckets (init_contig_intv
+  // arithmetic), the layout `fcs-genome align --disable-merge` leaves for htc
+  int parts = 0;
 };
 
 struct SynthOutputs {
-  std::string ref_fasta, bam, tumor_bam, fastq, truth_vcf;
+  std::string ref_fasta, bam, tumor_bam, fastq, truth_vcf, parts_dir;
   int64_t n_reads = 0, n_tumor_reads = 0;
   std::vector<SynthVariant> variants;
 };

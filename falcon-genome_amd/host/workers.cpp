@@ -42,14 +42,24 @@ CallerOptions caller_options_from_config(int gpu) {
   return o;
 }
 
-static std::vector<Interval> read_all(const std::vector<std::string>& paths) {
-  std::vector<Interval> out;
-  for (const std::string& p : paths) {
-    const auto iv = read_interval_list(p);
-    out.insert(out.end(), iv.begin(), iv.end());
+// The shard's intervals: the intersection of every -L set (GATK -isr
+// INTERSECTION); no set at all means the whole reference (GATK without -L).
+static std::vector<Interval> read_all(const Reference& ref, const std::vector<std::string>& paths,
+                                      const std::string& region = "", const std::string& region2 = "") {
+  std::vector<std::vector<Interval>> sets;
+  for (const std::string& p : paths) sets.push_back(read_regions(p));
+  for (const std::string* r : {&region, &region2})
+    if (!r->empty()) sets.push_back(read_regions(*r));
+  if (sets.empty()) {
+    std::vector<Interval> all;
+    for (const Contig& c : ref.contigs) all.push_back({c.name, 1, (int64_t)c.seq.size()});
+    return all;
   }
-  return out;
+  if (sets.size() == 1) return sets[0];
+  return intersect_interval_sets(sets);
 }
+
+static std::string shard_temp_dir(const char* tool) { return conf().temp_dir() + "/" + tool + "_regions"; }
 
 // ------------------------------------------------------------------ HTC
 HTCWorker::HTCWorker(std::string ref_path, std::vector<std::string> intv_paths, std::string input_path,
@@ -66,9 +76,11 @@ HTCWorker::HTCWorker(std::string ref_path, std::vector<std::string> intv_paths, 
 
 void HTCWorker::check() {
   if (!is_regular_file(ref_path_)) throw fileNotFound(ref_path_);
-  if (!is_regular_file(input_path_)) throw fileNotFound(input_path_);
   for (const std::string& p : intv_paths_)
     if (!is_regular_file(p)) throw fileNotFound(p);
+  shard_ = BamInput(input_path_).merge_region(contig_, conf().get_int("gatk.ncontigs"), shard_temp_dir("htc"));
+  for (const std::string& b : shard_.bams)
+    if (!is_regular_file(b)) throw fileNotFound(b);
   if (!flag_f_ && path_exists(output_path_)) throw invalidParam("output " + output_path_ + " exists (use -f)");
 }
 
@@ -77,9 +89,10 @@ int HTCWorker::run(TaskContext& ctx) {
   CallerOptions opt = caller_options_from_config(ctx.gpu);
   auto it = extra_opts_.find("--dump-regions");
   if (it != extra_opts_.end() && !it->second.empty()) opt.dump_path = it->second[0] + "." + std::to_string(contig_);
-  const VcfHeader h = caller_vcf_header(*ref, {"sample"}, false, ref_path_);
+  opt.gvcf = !flag_vcf_;  // the reference's default: --emitRefConfidence GVCF unless -v (HTCWorker.cpp:83-97)
+  const VcfHeader h = caller_vcf_header(*ref, {"sample"}, false, ref_path_, opt.gvcf);
   VcfWriter out(output_path_, h);
-  stats_ = call_intervals(*ref, input_path_, "", read_all(intv_paths_), opt, out);
+  stats_ = call_intervals(*ref, shard_.bams, {}, read_all(*ref, intv_paths_, shard_.region), opt, out);
   out.close();
   if (ctx.log)
     std::fprintf(ctx.log,
@@ -105,10 +118,15 @@ Mutect2Worker::Mutect2Worker(std::string ref_path, std::vector<std::string> intv
       flag_f_(flag_f) {}
 
 void Mutect2Worker::check() {
-  for (const std::string* p : {&ref_path_, &normal_path_, &tumor_path_})
-    if (!is_regular_file(*p)) throw fileNotFound(*p);
+  if (!is_regular_file(ref_path_)) throw fileNotFound(ref_path_);
   for (const std::string& p : intv_paths_)
     if (!is_regular_file(p)) throw fileNotFound(p);
+  const int n = conf().get_int("gatk.ncontigs");
+  normal_ = BamInput(normal_path_).merge_region(contig_, n, shard_temp_dir("mutect2_normal"));
+  tumor_ = BamInput(tumor_path_).merge_region(contig_, n, shard_temp_dir("mutect2_tumor"));
+  for (const BamShard* sh : {&normal_, &tumor_})
+    for (const std::string& b : sh->bams)
+      if (!is_regular_file(b)) throw fileNotFound(b);
   if (!flag_f_ && path_exists(output_path_)) throw invalidParam("output " + output_path_ + " exists (use -f)");
 }
 
@@ -120,7 +138,8 @@ int Mutect2Worker::run(TaskContext& ctx) {
   if (it != extra_opts_.end() && !it->second.empty()) opt.dump_path = it->second[0] + "." + std::to_string(contig_);
   const VcfHeader h = caller_vcf_header(*ref, {"TUMOR", "NORMAL"}, true, ref_path_);
   VcfWriter out(output_path_, h);
-  stats_ = call_intervals(*ref, tumor_path_, normal_path_, read_all(intv_paths_), opt, out);
+  stats_ = call_intervals(*ref, tumor_.bams, normal_.bams, read_all(*ref, intv_paths_, normal_.region, tumor_.region), opt,
+                          out);
   out.close();
   if (ctx.log)
     std::fprintf(ctx.log,

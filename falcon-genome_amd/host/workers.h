@@ -1,7 +1,12 @@
 // Workers of the GPU-backed commands (reference: include/fcs-genome/workers/*.h).
 // HTCWorker / Mutect2Worker keep the reference's constructor arguments
 // (src/workers/HTCWorker.cpp:17-47, Mutect2Worker.cpp:17-107) but run the
-// caller in-process on the task's GPU slot instead of launching GATK;
+// caller in-process on the task's GPU slot instead of launching GATK.  Their
+// input is a BamInput (one indexed BAM, or a directory of part BAMs whose
+// shard `contig` check() resolves with merge_region, as HTCWorker::check does
+// at src/workers/HTCWorker.cpp:36-46); the shard's intervals are the
+// intersection of every -L set (GATK -isr INTERSECTION, HTCWorker.cpp:68):
+// user list, init_contig_intv part, part-BAM region file;
 // VCFConcatWorker / ZIPWorker / TabixWorker are the same tail as
 // src/worker-htc.cpp:153-176, done natively instead of via bcftools/bgzip/tabix.
 #pragma once
@@ -10,6 +15,7 @@
 #include <string>
 #include <vector>
 
+#include "bam_input.h"
 #include "caller.h"
 #include "executor.h"
 #include "fasta.h"
@@ -33,6 +39,7 @@ class HTCWorker : public Worker {
   std::vector<std::string> intv_paths_;
   int contig_;
   bool flag_vcf_, flag_f_;
+  BamShard shard_;
   CallerStats stats_;
 };
 
@@ -50,6 +57,7 @@ class Mutect2Worker : public Worker {
   std::vector<std::string> intv_paths_;
   int contig_;
   bool flag_f_;
+  BamShard normal_, tumor_;
   CallerStats stats_;
 };
 

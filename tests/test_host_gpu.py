@@ -26,7 +26,7 @@ def data(tmp_path_factory):
     # the spiked cluster straddles the 10th/11th shard boundary of gatk.ncontigs = 32
     # (ceil(350000 / 32) = 10938 positions per shard: chr20:109380 | 109381)
     p = H.run_cli("synth", "-o", d, "-c", "chr20:250000,chr21:100000", "-x", "30", "--tumor", "--seed", "11",
-                  "--spike", SPIKE)
+                  "--spike", SPIKE, "--parts", "6")
     assert p.returncode == 0, p.stderr
     return d
 
@@ -83,7 +83,7 @@ ENV = {"FCS_GATK_NCONTIGS": "6", "FCS_GATK_NPROCS": "3", "FCS_GPU_DEVICES": "0"}
 def test_htc_end_to_end(gpu, data, tmp_path):
     out = tmp_path / "htc.vcf"
     dump = tmp_path / "dump"
-    p = H.run_cli("htc", "-r", data / "ref.fasta", "-i", data / "sample.bam", "-o", out, "--dump-regions", dump,
+    p = H.run_cli("htc", "-r", data / "ref.fasta", "-i", data / "sample.bam", "-o", out, "-v", "--dump-regions", dump,
                   env=ENV, cwd=tmp_path)
     assert p.returncode == 0, p.stderr[-3000:]
     assert (tmp_path / "htc.vcf.gz").exists() and (tmp_path / "htc.vcf.gz.tbi").exists()
@@ -152,7 +152,8 @@ def test_htc_gpu_slots_do_not_change_calls(gpu, data, tmp_path):
     for devs, nprocs in (("0", "1"), ("0,0", "4")):
         out = tmp_path / f"htc_{nprocs}.vcf"
         env = dict(ENV, FCS_GPU_DEVICES=devs, FCS_GATK_NPROCS=nprocs)
-        p = H.run_cli("htc", "-r", data / "ref.fasta", "-i", data / "sample.bam", "-o", out, env=env, cwd=tmp_path)
+        p = H.run_cli("htc", "-r", data / "ref.fasta", "-i", data / "sample.bam", "-o", out, "-v", env=env,
+                      cwd=tmp_path)
         assert p.returncode == 0, p.stderr[-3000:]
         outs.append([ln for ln in out.read_text().splitlines() if not ln.startswith("##source")])
     assert outs[0] == outs[1]
@@ -166,7 +167,7 @@ def test_htc_shard_boundaries_do_not_change_calls(gpu, data, tmp_path):
     outs = {}
     for n in ("1", "6", "32"):
         out = tmp_path / f"htc_n{n}.vcf"
-        p = H.run_cli("htc", "-r", data / "ref.fasta", "-i", data / "sample.bam", "-o", out,
+        p = H.run_cli("htc", "-r", data / "ref.fasta", "-i", data / "sample.bam", "-o", out, "-v",
                       env=dict(ENV, FCS_GATK_NCONTIGS=n), cwd=tmp_path)
         assert p.returncode == 0, p.stderr[-3000:]
         outs[n] = [ln for ln in out.read_text().splitlines() if not ln.startswith("##")]
@@ -238,7 +239,7 @@ def test_htc_c4_proxy_all_devices(gpu, tmp_path):
     devs = ",".join(str(i) for i in range(fcship.device_count()))
     out, dump, logs = tmp_path / "htc.vcf", tmp_path / "dump", tmp_path / "log"
     env = dict(ENV, FCS_GATK_NCONTIGS="32", FCS_GATK_NPROCS="8", FCS_GPU_DEVICES=devs, FCS_LOG_DIR=str(logs))
-    p = H.run_cli("htc", "-r", d / "ref.fasta", "-i", d / "sample.bam", "-o", out, "--dump-regions", dump,
+    p = H.run_cli("htc", "-r", d / "ref.fasta", "-i", d / "sample.bam", "-o", out, "-v", "--dump-regions", dump,
                   env=env, cwd=tmp_path)
     assert p.returncode == 0, p.stderr[-3000:]
     t, c = truth(d, False), calls(out)
@@ -253,3 +254,80 @@ def test_htc_c4_proxy_all_devices(gpu, tmp_path):
             ref, _ = oracle_lib.phmm_log10(reads[r], haps[h])
             assert abs(lik[r, h] - ref) <= 1e-5 * abs(ref)
     assert log_totals(logs, "regions") > 1000
+
+
+def records(path):
+    return [ln.split("\t") for ln in open(path).read().splitlines() if not ln.startswith("#")]
+
+
+def test_htc_gvcf_is_the_default(gpu, data, tmp_path):
+    """Without -v htc writes a GVCF, the reference's default
+    (src/workers/HTCWorker.cpp:83-97 --emitRefConfidence GVCF): every position
+    of the genome lies in exactly one hom-ref <NON_REF> block or inside a call,
+    the calls are the -v run's calls with <NON_REF> appended, and 30x coverage
+    gives confident reference blocks over most of the genome (hom-ref GQ ~ 3 per
+    informative base: GQ >= 60 from depth 20 on)."""
+    outs = {}
+    for mode in ("vcf", "gvcf"):
+        out = tmp_path / f"htc.{mode}"
+        args = ["-v"] if mode == "vcf" else []
+        p = H.run_cli("htc", "-r", data / "ref.fasta", "-i", data / "sample.bam", "-o", out, *args, env=ENV,
+                      cwd=tmp_path)
+        assert p.returncode == 0, p.stderr[-3000:]
+        outs[mode] = out
+    hdr = open(outs["gvcf"]).read()
+    assert "##ALT=<ID=NON_REF" in hdr and "##INFO=<ID=END" in hdr and "##GVCFBlock99-100" in hdr
+    lengths = {"chr20": 250000, "chr21": 100000}
+    covered = {c: np.zeros(n + 1, np.int32) for c, n in lengths.items()}
+    blocks = var = 0
+    gq99 = 0
+    gcalls = set()
+    for f in records(outs["gvcf"]):
+        chrom, pos, ref, alts = f[0], int(f[1]), f[3], f[4].split(",")
+        assert alts[-1] == "<NON_REF>"
+        if alts == ["<NON_REF>"]:
+            end = int(f[7].split("END=")[1])
+            assert end >= pos and f[8] == "GT:DP:GQ:MIN_DP:PL" and f[9].startswith("0/0:")
+            assert (covered[chrom][pos:end + 1] == 0).all(), "blocks overlap"
+            covered[chrom][pos:end + 1] += 1
+            blocks += 1
+            if int(f[9].split(":")[2]) >= 60:
+                gq99 += end - pos + 1
+        else:
+            var += 1
+            assert len(f[9].split(":")[4].split(",")) == 6  # PLs of 0/0 0/1 1/1 0/2 1/2 2/2
+            covered[chrom][pos:pos + len(ref)] += 1
+            gcalls.add((chrom, pos, ref, alts[0]))
+    for c, n in lengths.items():
+        assert (covered[c][1:] >= 1).all(), (c, np.flatnonzero(covered[c][1:] == 0)[:10])
+    assert gcalls == calls(outs["vcf"]), "GVCF calls differ from the -v run's"
+    assert var > 100 and blocks > var
+    assert gq99 / sum(lengths.values()) > 0.8, gq99
+
+
+def test_htc_part_bam_directory(gpu, data, tmp_path):
+    """BamInput directory mode (reference src/BamInput.cpp): htc -i on the
+    part-XXXXXX.bam + .bed layout of `align --disable-merge` (here written by
+    synth --parts 6, reads split by alignment start); with gatk.ncontigs = 6
+    each shard reads one part over its .bed region.  Calls equal the one-BAM
+    run's away from the part boundaries (a part holds only the reads that start
+    in it), and recall stays at the one-BAM level."""
+    parts = data / "parts"
+    assert len(list(parts.glob("part-*.bam"))) == 6 and len(list(parts.glob("part-*.bed"))) == 6
+    outs = {}
+    for name, inp in (("one", data / "sample.bam"), ("parts", parts)):
+        out = tmp_path / f"{name}.vcf"
+        p = H.run_cli("htc", "-r", data / "ref.fasta", "-i", inp, "-o", out, "-v", env=ENV, cwd=tmp_path)
+        assert p.returncode == 0, p.stderr[-3000:]
+        outs[name] = calls(out)
+    bounds = []
+    for k in range(6):
+        for ln in (parts / f"part-{k:06d}.bed").read_text().splitlines():
+            c, b, e = ln.split("\t")
+            bounds += [(c, int(b)), (c, int(e))]
+    far = lambda v: all(v[0] != c or abs(v[1] - x) > 1000 for c, x in bounds)  # noqa: E731
+    a = {v for v in outs["one"] if far(v)}
+    b = {v for v in outs["parts"] if far(v)}
+    assert a == b, (sorted(a - b)[:5], sorted(b - a)[:5])
+    t = truth(data, False)
+    assert len(t & outs["parts"]) / len(t) >= 0.88
