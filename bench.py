@@ -163,6 +163,56 @@ def bench_bsw(args, dev, tasks, reps=3):
                 bytes=int(tasks.qbuf.size + tasks.tbuf.size + 24 * tasks.n))
 
 
+def bench_bsw_global(args, dev, tasks, reps=3):
+    """ksw_global2 (the CIGAR pass of bwa_gen_cigar2) on device-resident tasks:
+    scores only, then scores + direction matrix + traceback.  Cells = the band
+    cells bwa's ksw_global2 evaluates: per target row i, columns
+    [max(0, i - w), min(qlen, i + w + 1))."""
+    b, keep = bsw_dev_batch(tasks, dev)
+    n = tasks.n
+    params = fcship.bsw_params()
+    stream = torch.cuda.current_stream(dev)
+    scores = torch.empty(n, dtype=torch.int32, device=dev)
+    ncol = np.minimum(tasks.qlen.astype(np.int64), 2 * tasks.w.astype(np.int64) + 1)
+    zsz = ncol * tasks.tlen
+    zoff = torch.from_numpy(np.concatenate([[0], np.cumsum(zsz)[:-1]]).astype(np.int64)).to(dev)
+    zbuf = torch.empty(int(zsz.sum()), dtype=torch.uint8, device=dev)
+    cap = (tasks.qlen + tasks.tlen + 2).astype(np.int32)
+    coff = torch.from_numpy(np.concatenate([[0], np.cumsum(cap.astype(np.int64))[:-1]]).astype(np.int64)).to(dev)
+    ccap = torch.from_numpy(cap).to(dev)
+    cig = torch.empty(int(cap.astype(np.int64).sum()), dtype=torch.int32, device=dev)
+    ncig = torch.empty(n, dtype=torch.int32, device=dev)
+    B, P = fcship.C.byref(b), fcship.C.byref(params)
+    cells = 0
+    shapes, counts = np.unique(np.stack([tasks.qlen, tasks.tlen, tasks.w], 1), axis=0, return_counts=True)
+    for (q, t, w), c in zip(shapes.tolist(), counts.tolist()):
+        i = np.arange(t)
+        cells += c * int(np.maximum(0, np.minimum(q, i + w + 1) - np.maximum(0, i - w)).sum())
+    out = {}
+    for name, with_cigar in (("scores", False), ("cigar", True)):
+        def run():
+            if with_cigar:
+                fcship.check(fcship.lib.fcs_bsw_global_dev(B, P, scores.data_ptr(), zbuf.data_ptr(), zbuf.numel(),
+                                                           zoff.data_ptr(), cig.data_ptr(), coff.data_ptr(),
+                                                           ccap.data_ptr(), ncig.data_ptr(), dev.index,
+                                                           stream.cuda_stream))
+            else:
+                fcship.check(fcship.lib.fcs_bsw_global_dev(B, P, scores.data_ptr(), None, 0, None, None, None, None,
+                                                           None, dev.index, stream.cuda_stream))
+        run()
+        torch.cuda.synchronize(dev)
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(stream)
+        for _ in range(reps):
+            run()
+        e1.record(stream)
+        torch.cuda.synchronize(dev)
+        ms = e0.elapsed_time(e1) / reps
+        out[name] = dict(ms=round(ms, 3), gcups=round(cells / (ms * 1e-3) / 1e9, 3))
+    del keep
+    return dict(tasks=n, w=int(tasks.w[0]) if n else 0, cells=cells, **out)
+
+
 def bench_e2e(args, rank, local):
     """End-to-end fcs-genome commands on this rank's own synthetic genome
     (C4/C5-shaped: chr1-like random reference, 30x sample, 40x tumor with
@@ -352,6 +402,16 @@ def main():
                        "c3_gcups": round(r3["gcups"], 3), "c3_tasks": r3["tasks"], "c3_ms": round(r3["ms"], 3),
                        "fixed_151x251_gcups": round(rf["gcups"], 3), "fixed_tasks": rf["tasks"],
                        "roofline": bsw_roofline(r3, rf)}
+        gl = fcship.synth_bsw(args.seed + 2, args.bsw_reads // 2, read_len=151, ref_len=10_000_000, w=16,
+                              mode=1, fixed_q=151, fixed_t=151)
+        g = bench_bsw_global(args, dev, gl)
+        line["bsw"]["global"] = {
+            "workload": "ksw_global2 of 151 bp reads against their 151 bp reference span (0.5% subs, 0.05% indels), "
+                        "band w = 16 (bwa_gen_cigar2's inferred band for such reads)",
+            "tasks": g["tasks"], "w": g["w"], "band_cells": g["cells"],
+            "scores_gcups": g["scores"]["gcups"], "scores_ms": g["scores"]["ms"],
+            "cigar_gcups": g["cigar"]["gcups"], "cigar_ms": g["cigar"]["ms"],
+            "kernel": "bsw_global_kernel (one wave per task, F as a DPP max-plus scan) + bsw_traceback_kernel"}
         if world == 1 and not args.no_cpu_baseline:
             line["bsw"]["cpu_baseline"] = cpu_baseline_bsw(
                 fcship.synth_bsw(args.seed + 1, 20000, read_len=151, ref_len=10_000_000), 0,

@@ -74,11 +74,9 @@ __device__ void extend_task(const BswDevBatch& b, const BswParams& p, long long 
     E[k] = 0;
   }
   {
-    int max_ins = (int)((double)(qlen * p.max_mat + p.end_bonus - p.o_ins) / e_ins + 1.);
-    max_ins = max_ins > 1 ? max_ins : 1;
+    const int max_ins = bwa_max_gap(qlen, p.max_mat, p.end_bonus, p.o_ins, e_ins);
     w = w < max_ins ? w : max_ins;
-    int max_del = (int)((double)(qlen * p.max_mat + p.end_bonus - p.o_del) / e_del + 1.);
-    max_del = max_del > 1 ? max_del : 1;
+    const int max_del = bwa_max_gap(qlen, p.max_mat, p.end_bonus, p.o_del, e_del);
     w = w < max_del ? w : max_del;
   }
   __syncthreads();
@@ -250,6 +248,172 @@ int launch_bsw_extend_wide(const BswDevBatch& b, const BswParams& p, int max_qle
 }
 
 // ---------------------------------------------------------------- ksw_global2
+// Lane-per-task ksw_global2 for the narrow bands bwa_gen_cigar2 asks for
+// (w from the score, typically < 32): the band lives in registers in diagonal
+// coordinates, k = j - i + w, so H(i-1, j-1) and H(i, j) share slot k, E(i, j)
+// sits at k + 1 of the previous row and F runs up k: every cell of a row uses
+// compile-time register indices and bwa's sequential row order, exactly.  A
+// row is 2w + 1 cells; rows whose band is cut (by column 0 in the first w rows,
+// by qlen at the end, or by a lane's narrower band) run a masked variant that
+// keeps bwa's boundary values (H(i, -1) = -(o_del + e_del (i + 1)), E = -inf
+// past the band end, F = -inf entering it).  Query codes ride through the band
+// as bytes (5 * code, the bit offset of the score in the target's packed
+// matrix row) shifted one byte per row.  Directions are stored as nibbles
+// (h source | E-continue << 2 | F-continue << 3), one row of the task's band
+// in ceil((2w + 1) / 8) dwords, inside the task's own min(qlen, 2w + 1) * tlen
+// bytes of the direction matrix; the traceback maps bwa's byte index onto
+// them.  Tasks outside these bounds take the wave-per-task kernel below.
+constexpr int kGLaneMaxNB = 65;
+__host__ __device__ __forceinline__ bool glane_ok(int qlen, int tlen, int w, bool mat_ok) {
+  const int nb = 2 * w + 1;
+  return mat_ok && w >= 2 && nb <= kGLaneMaxNB && qlen >= nb && tlen >= 3 &&
+         4LL * ((nb + 7) >> 3) * tlen + 3 <= (long long)nb * tlen;
+}
+__device__ __forceinline__ uint32_t* glane_zrow0(uint8_t* zbuf, const int64_t* zoff, long long task) {
+  return reinterpret_cast<uint32_t*>(((uintptr_t)(zbuf + zoff[task]) + 3) & ~(uintptr_t)3);
+}
+
+template <int NB, bool CIG, bool MASKED>
+__device__ __forceinline__ void glane_row(int (&Hd)[NB], int (&Ed)[NB + 1], const uint32_t (&Qb)[(NB + 4) / 4],
+                                          uint32_t (&nib)[(NB + 7) / 8], const int rowpack, const int lo,
+                                          const int hi, const int hb, const int oe_del, const int oe_ins,
+                                          const int e_del, const int e_ins, int& h1) {
+  int f = kMinusInf;
+#pragma unroll
+  for (int k = 0; k < NB; ++k) {
+    const int qoff = (int)((Qb[k >> 2] >> (8 * (k & 3))) & 0xFFu);
+    const int s = __builtin_amdgcn_sbfe(rowpack, qoff, 5);
+    const int m = Hd[k] + s;
+    int e = Ed[k + 1];
+    int h = m >= e ? m : e;
+    int d = 0;
+    if constexpr (CIG) d = m >= e ? 0 : 1;
+    if constexpr (CIG) d = h >= f ? d : 2;
+    h = h >= f ? h : f;
+    int t = m - oe_del;
+    e -= e_del;
+    if constexpr (CIG) d |= e > t ? 4 : 0;
+    e = e > t ? e : t;
+    t = m - oe_ins;
+    int fn = f - e_ins;
+    if constexpr (CIG) d |= fn > t ? 8 : 0;
+    fn = fn > t ? fn : t;
+    if constexpr (MASKED) {
+      const bool v = k >= lo && k < hi;
+      Hd[k] = v ? h : (k < lo ? hb : Hd[k]);
+      Ed[k] = v ? e : kMinusInf;
+      f = v ? fn : kMinusInf;
+      h1 = v ? h : h1;
+    } else {
+      Hd[k] = h;
+      Ed[k] = e;
+      f = fn;
+      if (k == NB - 1) h1 = h;
+    }
+    if constexpr (CIG) {
+      if ((k & 7) == 0) nib[k >> 3] = (uint32_t)d;
+      else nib[k >> 3] |= (uint32_t)d << (4 * (k & 7));
+    }
+  }
+}
+
+template <int NB, bool CIG>
+__device__ void glane_run(const BswDevBatch& b, const BswParams& p, long long task, bool ok,
+                          int32_t* __restrict__ scores, uint8_t* __restrict__ zbuf, const int64_t* __restrict__ zoff) {
+  constexpr int NQ = (NB + 4) / 4, NW = (NB + 7) / 8;
+  int qlen = 0, tlen = 0, w = 0;
+  const uint8_t* __restrict__ q = nullptr;
+  const uint8_t* __restrict__ tg = nullptr;
+  if (ok) {
+    qlen = b.qlen[task];
+    tlen = b.tlen[task];
+    w = b.w[task];
+    q = b.qbuf + b.qoff[task];
+    tg = b.tbuf + b.toff[task];
+  }
+  const int tmax = wave_max(tlen);
+  const int oe_del = p.o_del + p.e_del, oe_ins = p.o_ins + p.e_ins, e_del = p.e_del, e_ins = p.e_ins;
+  const int nb = 2 * w + 1, nd = (nb + 7) >> 3;
+  uint32_t* __restrict__ z = (CIG && ok) ? glane_zrow0(zbuf, zoff, task) : nullptr;
+  int Hd[NB], Ed[NB + 1];
+  uint32_t Qb[NQ], nib[NW];
+  auto qbyte = [&](int j) -> uint32_t { return (ok && j >= 0 && j < qlen) ? 5u * (uint32_t)q[j] : 0u; };
+#pragma unroll
+  for (int k = 0; k < NB; ++k) {
+    const int j = k - w;  // column of slot k in row 0; Hd holds "H(-1, j - 1)" = bwa's first-row eh[j].h
+    Hd[k] = j == 0 ? 0 : (j >= 1 && j <= w) ? -(p.o_ins + e_ins * j) : kMinusInf;
+    Ed[k] = kMinusInf;
+  }
+  Ed[NB] = kMinusInf;
+#pragma unroll
+  for (int d = 0; d < NQ; ++d) {
+    uint32_t v = 0;
+#pragma unroll
+    for (int c = 0; c < 4; ++c)
+      if (4 * d + c <= NB) v |= qbyte(4 * d + c - w) << (8 * c);
+    Qb[d] = v;
+  }
+#pragma unroll
+  for (int d = 0; d < NW; ++d) nib[d] = 0;
+  int h1 = kMinusInf;
+  int tb_next = (ok && tlen > 0) ? (int)tg[0] : 4;
+  uint32_t qn_next = qbyte(NB + 1 - w);  // byte NB of row 1
+  for (int i = 0; i < tmax; ++i) {
+    const int tb = tb_next;
+    const uint32_t qn = qn_next;
+    tb_next = (ok && i + 1 < tlen) ? (int)tg[i + 1] : 4;  // next row's inputs in flight during this row
+    qn_next = qbyte(i + NB + 2 - w);
+    const int rowpack = tb == 0 ? p.matpack[0] : tb == 1 ? p.matpack[1] : tb == 2 ? p.matpack[2]
+                      : tb == 3 ? p.matpack[3] : p.matpack[4];
+    const bool live = ok && i < tlen;
+    const int lo = live ? w - i : NB;
+    const int hi = live ? min(nb, qlen - i + w) : 0;
+    const int hb = -(p.o_del + e_del * (i + 1));
+    // bwa's h1 at the row start: H(i, -1) when the band starts at column 0,
+    // else -inf; an empty band leaves it in eh[end].h (lanes past their last
+    // row keep their final value)
+    if (live) h1 = lo >= 0 ? hb : kMinusInf;
+    const bool full = __ballot(!(lo <= 0 && hi >= NB)) == 0ull;
+    if (full)
+      glane_row<NB, CIG, false>(Hd, Ed, Qb, nib, rowpack, lo, hi, hb, oe_del, oe_ins, e_del, e_ins, h1);
+    else
+      glane_row<NB, CIG, true>(Hd, Ed, Qb, nib, rowpack, lo, hi, hb, oe_del, oe_ins, e_del, e_ins, h1);
+    if constexpr (CIG) {
+      if (live) {
+        uint32_t* const zr = z + (long long)i * nd;
+#pragma unroll
+        for (int d = 0; d < NW; ++d)
+          if (d < nd) zr[d] = nib[d];
+      }
+    }
+    // next row's query bytes: the band moves one column right
+#pragma unroll
+    for (int d = 0; d < NQ; ++d) Qb[d] = (Qb[d] >> 8) | (d + 1 < NQ ? Qb[d + 1] << 24 : 0u);
+    Qb[NB >> 2] = (Qb[NB >> 2] & ~(0xFFu << (8 * (NB & 3)))) | (qn << (8 * (NB & 3)));
+  }
+  // bwa: score = eh[qlen].h, written by the last row when its band reaches qlen
+  if (ok) scores[task] = qlen <= tlen + w ? h1 : kMinusInf;
+}
+
+// One launch per band class (each with its own register budget): a wave runs
+// in the launch whose NB is the smallest of 17 / 33 / 65 holding its widest band.
+template <int NB, bool CIG>
+__global__ __launch_bounds__(64) void bsw_global_lane_kernel(const BswDevBatch b, const BswParams p,
+                                                             int32_t* __restrict__ scores, uint8_t* __restrict__ zbuf,
+                                                             const int64_t* __restrict__ zoff) {
+  const long long task = (long long)blockIdx.x * 64 + threadIdx.x;
+  bool ok = false;
+  int w = -1;
+  if (task < b.n) {
+    w = b.w[task];
+    ok = glane_ok(b.qlen[task], b.tlen[task], w, p.lane_ok != 0);
+  }
+  const int nbw = 2 * wave_max(ok ? w : -1) + 1;
+  constexpr int lo = NB == 17 ? 0 : NB == 33 ? 17 : 33;
+  if (nbw <= lo || nbw > NB) return;
+  glane_run<NB, CIG>(b, p, task, ok, scores, zbuf, zoff);
+}
+
 template <int NS>
 __device__ void global_task(const BswDevBatch& b, const BswParams& p, long long task, uint8_t* __restrict__ tl,
                             int32_t* __restrict__ scores, uint8_t* __restrict__ zbuf, const int64_t* __restrict__ zoff) {
@@ -336,6 +500,7 @@ __global__ __launch_bounds__(64) void bsw_global_kernel(const BswDevBatch b, con
   extern __shared__ __align__(16) unsigned char tl[];
   for (long long task = blockIdx.x; task < b.n; task += gridDim.x) {
     const int qlen = b.qlen[task];
+    if (glane_ok(qlen, b.tlen[task], b.w[task], p.lane_ok != 0)) continue;  // bsw_global_lane_kernel's
     const int ns = (qlen + 1 + 63) >> 6;
     if (MAXNS <= 4) {
       switch (ns) {
@@ -354,7 +519,7 @@ __global__ __launch_bounds__(64) void bsw_global_kernel(const BswDevBatch b, con
 }
 
 // One lane per task walks the direction bytes back from (tlen-1, last column).
-__global__ void bsw_traceback_kernel(const BswDevBatch b, const uint8_t* __restrict__ zbuf,
+__global__ void bsw_traceback_kernel(const BswDevBatch b, const BswParams p, uint8_t* __restrict__ zbuf,
                                      const int64_t* __restrict__ zoff, uint32_t* __restrict__ cigar,
                                      const int64_t* __restrict__ cigar_off, const int32_t* __restrict__ cigar_cap,
                                      int32_t* __restrict__ n_cigar) {
@@ -364,6 +529,21 @@ __global__ void bsw_traceback_kernel(const BswDevBatch b, const uint8_t* __restr
   const int n_col = qlen < 2 * w + 1 ? qlen : 2 * w + 1;
   const uint8_t* z = zbuf + zoff[task];
   const long long zsize = (long long)n_col * (tlen > 0 ? tlen : 0);
+  // the lane kernel's nibble rows: bwa's byte (row i, band offset c) is cell
+  // k = beg_i + c - i + w of nibble row i; c past the row's band end reads 0,
+  // as bwa's zeroed bytes there do
+  const bool lane = glane_ok(qlen, tlen, w, p.lane_ok != 0);
+  const uint32_t* const zl = lane ? glane_zrow0(zbuf, zoff, task) : nullptr;
+  const int nd = (2 * w + 1 + 7) >> 3;
+  auto zbyte = [&](long long zi) -> int {
+    if (!lane) return z[zi];
+    const int r = (int)(zi / n_col), c = (int)(zi - (long long)r * n_col);
+    const int beg = r > w ? r - w : 0, end = r + w + 1 < qlen ? r + w + 1 : qlen;
+    if (beg + c >= end) return 0;
+    const int k = beg + c - r + w;
+    const int nbl = (int)((zl[(long long)r * nd + (k >> 3)] >> (4 * (k & 7))) & 15u);
+    return (nbl & 3) | ((nbl >> 2) & 1) << 2 | ((nbl >> 3) & 1) << 5;
+  };
   uint32_t* cg = cigar + cigar_off[task];
   const int cap = cigar_cap[task];
   int n = 0, which = 0, curop = -1;
@@ -388,7 +568,7 @@ __global__ void bsw_traceback_kernel(const BswDevBatch b, const uint8_t* __restr
     // cells outside the written band read as 0 (zeroed matrix, bounded index;
     // see oracle/ksw_oracle.c header) instead of bwa's undefined read
     const long long zi = (long long)i * n_col + (k - (i > w ? i - w : 0));
-    which = (zi >= 0 && zi < zsize) ? (z[zi] >> (which << 1) & 3) : 0;
+    which = (zi >= 0 && zi < zsize) ? (zbyte(zi) >> (which << 1) & 3) : 0;
     if (which == 0) push(0, 1), --i, --k;
     else if (which == 1) push(2, 1), --i;
     else push(1, 1), --k;
@@ -421,6 +601,24 @@ int launch_bsw_global(const BswDevBatch& b, const BswParams& p, int max_qlen, in
   long long grid = b.n;
   const long long cap = 2048;
   if (grid > cap) grid = cap;
+  // narrow bands: one lane per task (64 consecutive tasks per wave)
+  const long long lane_waves = (b.n + 63) / 64;
+  if (lane_waves > 0x7FFFFFFFLL) return fail(FCS_ERR_UNSUPPORTED, "[E::fcship] ksw_global2: batch too large");
+  auto lane_launch = [&](auto kern) -> int {
+    hipLaunchKernelGGL(kern, dim3((unsigned)lane_waves), dim3(64), 0, s, b, p, scores, zbuf, zoff);
+    FCS_HIP_CHECK(hipGetLastError());
+    return FCS_OK;
+  };
+  int rc;
+  if (zbuf) {
+    if ((rc = lane_launch(bsw_global_lane_kernel<17, true>)) || (rc = lane_launch(bsw_global_lane_kernel<33, true>)) ||
+        (rc = lane_launch(bsw_global_lane_kernel<65, true>)))
+      return rc;
+  } else {
+    if ((rc = lane_launch(bsw_global_lane_kernel<17, false>)) || (rc = lane_launch(bsw_global_lane_kernel<33, false>)) ||
+        (rc = lane_launch(bsw_global_lane_kernel<65, false>)))
+      return rc;
+  }
   if (max_qlen <= 255)
     hipLaunchKernelGGL(bsw_global_kernel<4>, dim3((unsigned)grid), dim3(64), lds, s, b, p, scores, zbuf, zoff);
   else
@@ -428,7 +626,7 @@ int launch_bsw_global(const BswDevBatch& b, const BswParams& p, int max_qlen, in
   FCS_HIP_CHECK(hipGetLastError());
   if (cigar) {
     const long long nb = (b.n + 63) / 64;
-    hipLaunchKernelGGL(bsw_traceback_kernel, dim3((unsigned)nb), dim3(64), 0, s, b, zbuf, zoff, cigar, cigar_off,
+    hipLaunchKernelGGL(bsw_traceback_kernel, dim3((unsigned)nb), dim3(64), 0, s, b, p, zbuf, zoff, cigar, cigar_off,
                        cigar_cap, n_cigar);
     FCS_HIP_CHECK(hipGetLastError());
   }

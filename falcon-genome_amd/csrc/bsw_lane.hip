@@ -290,11 +290,9 @@ __device__ __forceinline__ void lane_wave(const BswDevBatch& b, const BswParams&
     }
   }
   {
-    int max_ins = (int)((double)(qlen * p.max_mat + p.end_bonus - p.o_ins) / e_ins + 1.);
-    max_ins = max_ins > 1 ? max_ins : 1;
+    const int max_ins = bwa_max_gap(qlen, p.max_mat, p.end_bonus, p.o_ins, e_ins);
     w = w < max_ins ? w : max_ins;
-    int max_del = (int)((double)(qlen * p.max_mat + p.end_bonus - p.o_del) / e_del + 1.);
-    max_del = max_del > 1 ? max_del : 1;
+    const int max_del = bwa_max_gap(qlen, p.max_mat, p.end_bonus, p.o_del, e_del);
     w = w < max_del ? w : max_del;
   }
 

@@ -280,11 +280,9 @@ __device__ __forceinline__ void task_load(PairTask& T, const BswDevBatch& b, con
     T.w = b.w[T.id];
     T.tg = b.tbuf + b.toff[T.id];
   }
-  int max_ins = (int)((double)(T.qlen * p.max_mat + p.end_bonus - p.o_ins) / p.e_ins + 1.);
-  max_ins = max_ins > 1 ? max_ins : 1;
+  const int max_ins = bwa_max_gap(T.qlen, p.max_mat, p.end_bonus, p.o_ins, p.e_ins);
   T.w = T.w < max_ins ? T.w : max_ins;
-  int max_del = (int)((double)(T.qlen * p.max_mat + p.end_bonus - p.o_del) / p.e_del + 1.);
-  max_del = max_del > 1 ? max_del : 1;
+  const int max_del = bwa_max_gap(T.qlen, p.max_mat, p.end_bonus, p.o_del, p.e_del);
   T.w = T.w < max_del ? T.w : max_del;
   T.beg = 0;
   T.end = T.qlen;

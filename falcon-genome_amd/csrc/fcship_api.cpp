@@ -1079,6 +1079,35 @@ int fcs_bsw_global(const fcs_bsw_task* tasks, int32_t n, const fcs_bsw_params* p
   return FCS_OK;
 }
 
+int fcs_bsw_global_dev(const fcs_bsw_batch* b, const fcs_bsw_params* params, int32_t* dev_scores, uint8_t* dev_zbuf,
+                       int64_t zbytes, const int64_t* dev_zoff, uint32_t* dev_cigar, const int64_t* dev_cigar_off,
+                       const int32_t* dev_cigar_cap, int32_t* dev_n_cigar, int32_t device, void* stream) {
+  if (!b || b->n < 0 || (b->n > 0 && !dev_scores)) return fail(FCS_ERR_INVALID, "[E::fcs_bsw_global_dev] bad arguments");
+  const bool want_cigar = dev_cigar != nullptr;
+  if (want_cigar && (!dev_zbuf || !dev_zoff || !dev_cigar_off || !dev_cigar_cap || !dev_n_cigar))
+    return fail(FCS_ERR_INVALID, "[E::fcs_bsw_global_dev] CIGARs need the direction matrix, offsets, caps and counts");
+  int rc = check_params(params);
+  if (rc) return rc;
+  if (b->n == 0) return FCS_OK;
+  if (b->n > 0x7FFFFFFF) return fail(FCS_ERR_UNSUPPORTED, "[E::fcs_bsw_global_dev] more than 2^31-1 tasks");
+  if ((rc = check_device(device))) return rc;
+  FCS_HIP_CHECK(hipSetDevice(device));
+  BswDevBatch d;
+  d.qbuf = b->qbuf;
+  d.qoff = b->qoff;
+  d.qlen = b->qlen;
+  d.tbuf = b->tbuf;
+  d.toff = b->toff;
+  d.tlen = b->tlen;
+  d.h0 = b->h0;
+  d.w = b->w;
+  d.n = b->n;
+  return launch_bsw_global(d, to_params(params), std::max(b->max_qlen, 1), std::max(b->max_tlen, 1), dev_scores,
+                           want_cigar ? dev_zbuf : nullptr, want_cigar ? zbytes : 0, want_cigar ? dev_zoff : nullptr,
+                           dev_cigar, want_cigar ? dev_cigar_off : nullptr, want_cigar ? dev_cigar_cap : nullptr,
+                           want_cigar ? dev_n_cigar : nullptr, (hipStream_t)stream);
+}
+
 int fcs_ksw_extend2(int qlen, const uint8_t* query, int tlen, const uint8_t* target, int m, const int8_t* mat,
                     int o_del, int e_del, int o_ins, int e_ins, int w, int end_bonus, int zdrop, int h0, int* qle,
                     int* tle, int* gtle, int* gscore, int* max_off) {
@@ -1135,6 +1164,6 @@ int fcs_ksw_global2(int qlen, const uint8_t* query, int tlen, const uint8_t* tar
   return score;
 }
 
-int fcs_abi_symbol_count(void) { return 31; }
+int fcs_abi_symbol_count(void) { return 32; }
 
 }  // extern "C"

@@ -77,6 +77,19 @@ __device__ __forceinline__ int wave_max(int v) {
   return read_lane(wave_incl_max(v, INT32_MIN), 63);
 }
 
+// ------------------------------------------------------------ ksw band limit
+// bwa ksw_extend2's max_ins / max_del: (int)((double)(qlen * max_mat +
+// end_bonus - o) / e + 1.), at least 1.  In integers: for e > 0 the truncation
+// of n / e + 1 is (n + e) / e with C's truncating division (for |n| < 2^31 and
+// e < 2^20 the double quotient never rounds across an integer), which keeps
+// the f64 divide (and its register pairs) out of the SW kernels' wave setup.
+__host__ __device__ __forceinline__ int bwa_max_gap(int qlen, int max_mat, int end_bonus, int o, int e) {
+  if (e <= 0) return 0x7FFFFFFF;  // bwa divides by zero here; the cast of +inf saturates on gfx950: no limit
+  const int n = qlen * max_mat + end_bonus - o;
+  const int m = (n + e) / e;
+  return m > 1 ? m : 1;
+}
+
 // ------------------------------------------------------------ PairHMM tables
 // Host-computed (fcship_tables.cpp) GKL Context<T> tables, uploaded once per device.
 template <typename T>

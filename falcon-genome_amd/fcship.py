@@ -142,6 +142,9 @@ _sig("fcs_bsw_extend_plan", C.c_int, [C.c_void_p, C.POINTER(BswBatch), C.POINTER
                                       C.c_void_p])
 _sig("fcs_bsw_global", C.c_int, [C.POINTER(BswTask), C.c_int32, C.POINTER(BswParams), i32p, u32p, i64p, i32p,
                                  i32p, C.c_int32])
+_sig("fcs_bsw_global_dev", C.c_int, [C.POINTER(BswBatch), C.POINTER(BswParams), C.c_void_p, C.c_void_p, C.c_int64,
+                                     C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_int32,
+                                     C.c_void_p])
 _sig("fcs_ksw_extend2", C.c_int, [C.c_int, u8p, C.c_int, u8p, C.c_int, i8p, C.c_int, C.c_int, C.c_int, C.c_int,
                                   C.c_int, C.c_int, C.c_int, C.c_int, C.POINTER(C.c_int), C.POINTER(C.c_int),
                                   C.POINTER(C.c_int), C.POINTER(C.c_int), C.POINTER(C.c_int)])

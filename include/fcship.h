@@ -236,6 +236,18 @@ int fcs_bsw_global(const fcs_bsw_task* tasks, int32_t n, const fcs_bsw_params* p
                    uint32_t* cigar_arena, const int64_t* cigar_off, const int32_t* cigar_cap,
                    int32_t* n_cigar, int32_t device);
 
+/* Device path of ksw_global2 (stream-ordered, no host sync): task k of
+ * dev_batch aligned with band dev_batch->w[k]; dev_scores[k] = global score.
+ * Scores only when dev_cigar is null.  Otherwise dev_zbuf holds task k's
+ * direction matrix at dev_zoff[k] (min(qlen, 2w+1) * tlen bytes, caller-sized;
+ * zbytes = its total), the CIGAR ops go to dev_cigar[dev_cigar_off[k] ..
+ * + dev_cigar_cap[k]) and their count to dev_n_cigar[k] (a count above the cap
+ * means the ops were truncated). */
+int fcs_bsw_global_dev(const fcs_bsw_batch* dev_batch, const fcs_bsw_params* params, int32_t* dev_scores,
+                       uint8_t* dev_zbuf, int64_t zbytes, const int64_t* dev_zoff, uint32_t* dev_cigar,
+                       const int64_t* dev_cigar_off, const int32_t* dev_cigar_cap, int32_t* dev_n_cigar,
+                       int32_t device, void* stream);
+
 /* Signature twins of bwa's ksw.c entry points, running on GPU `device` 0 (or
  * the device set by fcs_set_default_device).  m must be 5.  They return the
  * score exactly as bwa does; because a global score can be negative, failure

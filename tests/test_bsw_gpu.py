@@ -244,3 +244,23 @@ def test_pair_kernel_mixed_lengths_in_a_wave(gpu):
 
 def test_pair_kernel_c3_batch(gpu):
     assert_extend_equal(fcship.synth_bsw(20261016, 20000, ref_len=4_000_000))
+
+
+@pytest.mark.parametrize("w", [4, 16, 30])
+def test_global_lane_kernel_narrow_bands(gpu, w):
+    """bwa_gen_cigar2-shaped batches (151 bp reads vs their reference span,
+    one narrow band for the whole batch) run in the lane-per-task kernel's
+    unmasked rows; scores and CIGARs bit-exact against the oracle.  Mixed bands
+    and shapes (masked rows, the wave kernel's share, out-of-band tracebacks)
+    are covered by test_global_scores_and_cigars."""
+    t = fcship.synth_bsw(100 + w, 1500, read_len=151, ref_len=1_000_000, w=w, mode=1, fixed_q=151, fixed_t=151)
+    t.tlen[::7] -= 3  # some tasks a few target bases short of their query
+    scores, cigars = fcship.bsw_global(t)
+    m = fcship.default_mat()
+    for k in range(t.n):
+        q, tg, _, ww = t.task(k)
+        rs, rc = oracle_lib.ksw_global2(q, tg, ww, m)
+        assert scores[k] == rs, f"task {k}: score {scores[k]} != {rs}"
+        assert np.array_equal(cigars[k], rc), f"task {k}: {fcship.cigar_str(cigars[k])} != {fcship.cigar_str(rc)}"
+    s2, _ = fcship.bsw_global(t, with_cigar=False)
+    assert np.array_equal(s2, scores)
