@@ -614,7 +614,7 @@ CallerStats call_intervals(const Reference& ref, const std::vector<std::string>&
             PreparedRead pr;
             gatk_prepare_read(rd.seq.substr(qs, qe - qs), q, rd.bi.empty() ? "" : rd.bi.substr(qs, qe - qs),
                               rd.bd.empty() ? "" : rd.bd.substr(qs, qe - qs), rd.mapq, pr,
-                              opt.base_quality_threshold);
+                              opt.base_quality_threshold, (PcrIndelModel)opt.pcr_indel_model);
             g->reads[s].push_back(std::move(pr));
           }
         }

@@ -31,6 +31,7 @@ struct CallerOptions {
   bool somatic = false;  // Mutect2 mode (tumor BAM + normal BAM)
   int min_base_quality = 10;
   int base_quality_threshold = 18;
+  int pcr_indel_model = 3;  // PcrIndelModel (gatk_prep.h): GATK's default CONSERVATIVE
   int min_mapq = 20;
   double active_fraction = 0.15;
   int padding = 50;

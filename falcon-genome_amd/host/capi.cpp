@@ -43,11 +43,11 @@ extern "C" {
 const char* fcsg_last_error() { return g_err.c_str(); }
 
 int fcsg_prepare_read(const char* bases, const uint8_t* quals, int len, const char* bi, const char* bd, int mapq,
-                      int threshold, uint8_t* bq, uint8_t* iq, uint8_t* dq, uint8_t* gcp) {
+                      int threshold, int pcr_model, uint8_t* bq, uint8_t* iq, uint8_t* dq, uint8_t* gcp) {
   return guard([&] {
     PreparedRead pr;
     gatk_prepare_read(std::string(bases, len), std::vector<uint8_t>(quals, quals + len), bi ? std::string(bi) : "",
-                      bd ? std::string(bd) : "", mapq, pr, threshold);
+                      bd ? std::string(bd) : "", mapq, pr, threshold, (PcrIndelModel)pcr_model);
     std::memcpy(bq, pr.base_q.data(), len);
     std::memcpy(iq, pr.ins_q.data(), len);
     std::memcpy(dq, pr.del_q.data(), len);
@@ -97,6 +97,8 @@ int fcsg_intersect_regions(const char* const* paths, int n, char* buf, int cap) 
 }
 
 int fcsg_gvcf_band(int gq) { return gvcf_band(gq); }
+int fcsg_tandem_repeat_units(const char* bases, int offset) { return tandem_repeat_units(bases, offset); }
+int fcsg_pcr_indel_cap(int repeat_len, int model) { return pcr_indel_cap(repeat_len, (PcrIndelModel)model); }
 
 int fcsg_bgzf_compress_file(const char* in, const char* out) {
   return guard([&] { bgzip_file(in, out); });

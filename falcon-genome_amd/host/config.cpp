@@ -49,6 +49,8 @@ void Config::init(const std::string& root_dir) {
   // caller knobs (GATK HaplotypeCaller / Mutect2 argument defaults)
   declare("htc.min_base_quality", "10", "min base quality counted as evidence of activity");
   declare("htc.base_quality_threshold", "18", "PairHMM: base quals below this become 6");
+  declare("htc.pcr_indel_model", "CONSERVATIVE",
+          "GATK --pcr-indel-model: NONE, HOSTILE, AGGRESSIVE, CONSERVATIVE (gap-open caps in tandem repeats)");
   declare("htc.min_mapq", "20", "reads below this mapping quality are ignored");
   declare("htc.active_fraction", "0.15", "mismatch/indel fraction that makes a site active");
   declare("htc.padding", "50", "bases added either side of an active site");

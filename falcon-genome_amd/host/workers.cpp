@@ -6,6 +6,7 @@
 #include "common.h"
 #include "config.h"
 #include "fcship.h"
+#include "gatk_prep.h"
 #include "intervals.h"
 #include "vcf.h"
 
@@ -28,6 +29,7 @@ CallerOptions caller_options_from_config(int gpu) {
   o.gpu = gpu < 0 ? 0 : gpu;
   o.min_base_quality = c.get_int("htc.min_base_quality");
   o.base_quality_threshold = c.get_int("htc.base_quality_threshold");
+  o.pcr_indel_model = (int)parse_pcr_indel_model(c.get_string("htc.pcr_indel_model"));
   o.min_mapq = c.get_int("htc.min_mapq");
   o.active_fraction = std::stod(c.get_string("htc.active_fraction"));
   o.padding = c.get_int("htc.padding");

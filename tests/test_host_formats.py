@@ -251,15 +251,45 @@ def test_gatk_prepare_read_rules():
     bi = bytes([33 + x for x in [45, 3, 6, 7, 40, 45, 45, 45, 0, 10]])
     out = [np.zeros(10, np.uint8) for _ in range(4)]
     ptr = lambda a: a.ctypes.data_as(C.POINTER(C.c_uint8))  # noqa: E731
-    H.check(H.lib.fcsg_prepare_read(bases, ptr(q), 10, bi, None, 30, 18, *[ptr(o) for o in out]))
+    H.check(H.lib.fcsg_prepare_read(bases, ptr(q), 10, bi, None, 30, 18, 0, *[ptr(o) for o in out]))
     bq, iq, dq, gcp = out
     # cap at MQ 30 first, then < 18 → 6
     assert bq.tolist() == [6, 6, 18, 19, 30, 30, 30, 30, 6, 25]
     assert iq.tolist() == [45, 6, 6, 7, 40, 45, 45, 45, 6, 10]  # BI tag, floored at 6
     assert dq.tolist() == [45] * 10  # no BD tag → 45
     assert gcp.tolist() == [10] * 10
-    H.check(H.lib.fcsg_prepare_read(bases, ptr(q), 10, None, None, 10, 18, *[ptr(o) for o in out]))
+    H.check(H.lib.fcsg_prepare_read(bases, ptr(q), 10, None, None, 10, 18, 0, *[ptr(o) for o in out]))
     assert out[0].tolist() == [6] * 10  # MQ 10 < 18 caps everything to 6
+
+
+def test_pcr_indel_error_model():
+    """GATK's --pcr-indel-model (PairHMMLikelihoodCalculationEngine, [EXT],
+    restated; parity unpinned): the gap-open cap per tandem-repeat run length and
+    its application to positions 0 .. n-2 before the floor at 6."""
+    import math
+    for model, rate in ((1, 1.0), (2, 2.0), (3, 3.0)):
+        for rl in range(21):
+            v = 40.0 - math.exp(rl / (rate * math.pi)) + 1.0
+            assert H.lib.fcsg_pcr_indel_cap(rl, model) == max(10, int(v + 0.5)), (model, rl)
+    assert H.lib.fcsg_pcr_indel_cap(20, 3) == 33 and H.lib.fcsg_pcr_indel_cap(20, 1) == 10
+    rep = H.lib.fcsg_tandem_repeat_units
+    assert rep(b"AAAAAAAAAA", 4) == 10          # (A)5 back + (A)5 forward
+    assert rep(b"ACACACGT", 3) == 1             # back unit AC x2, forward unit A x1: A's back run is 0
+    assert rep(b"ACACACAC", 3) == 4             # (AC)2 back + (AC)2 forward
+    assert rep(b"A" * 30, 10) == 20             # capped at MAX_REPEAT_LENGTH
+    assert rep(b"TTCTTCCCC", 5) == 4            # GATK's comment: TTCTT(C)CCC is (C)4, not (TTC)2
+    bases = b"GATTTTTTTTCAG"
+    n = len(bases)
+    q = np.full(n, 30, np.uint8)
+    out = [np.zeros(n, np.uint8) for _ in range(4)]
+    ptr = lambda a: a.ctypes.data_as(C.POINTER(C.c_uint8))  # noqa: E731
+    H.check(H.lib.fcsg_prepare_read(bases, ptr(q), n, None, None, 60, 18, 3, *[ptr(o) for o in out]))
+    caps = [H.lib.fcsg_pcr_indel_cap(rep(bases, i), 3) for i in range(n - 1)]
+    assert out[1].tolist() == [min(45, c) for c in caps] + [45]  # the last base keeps its GOP
+    assert out[2].tolist() == out[1].tolist()
+    assert min(caps) < 40  # the T run lowers the caps inside it
+    H.check(H.lib.fcsg_prepare_read(bases, ptr(q), n, None, None, 60, 18, 0, *[ptr(o) for o in out]))
+    assert out[1].tolist() == [45] * n  # NONE
 
 
 # ------------------------------------------------------------------ executor
