@@ -12,8 +12,11 @@ import fcship  # noqa: F401  (loads torch + libfcship first: one HIP runtime per
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 PKG = os.path.join(ROOT, "falcon-genome_amd")
-BIN = os.path.join(PKG, "bin", "fcs-genome")
-LIB_PATH = os.path.join(PKG, "libfcsgenome.so")
+# FCS_SAN=address|thread|undefined selects the sanitizer build (tools/sanitize.sh)
+SAN = os.environ.get("FCS_SAN", "")
+_DIR = os.path.join(PKG, "_san", SAN) if SAN else PKG
+BIN = os.path.join(_DIR, "bin", "fcs-genome")
+LIB_PATH = os.path.join(_DIR, "libfcsgenome.so")
 
 lib = C.CDLL(LIB_PATH)
 lib.fcsg_last_error.restype = C.c_char_p

@@ -14,7 +14,8 @@ import numpy as np
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 ORACLE_DIR = os.path.join(ROOT, "oracle")
-ORACLE_LIB = os.path.join(ORACLE_DIR, "liboracle.so")
+ORACLE_LIB = (os.path.join(ORACLE_DIR, "_san", os.environ["FCS_SAN"], "liboracle.so") if os.environ.get("FCS_SAN")
+              else os.path.join(ORACLE_DIR, "liboracle.so"))
 
 
 def _load():
@@ -46,6 +47,9 @@ lib.oracle_phmm_java_log10.argtypes = [vp, vp, vp, vp, vp, C.c_int, vp, C.c_int]
 lib.oracle_phmm_batch.restype = None
 lib.oracle_phmm_batch.argtypes = [vp] * 5 + [vp, vp, vp, vp, vp, vp, vp, C.c_int64, vp, vp, vp, C.c_int]
 lib.oracle_omp_max_threads.restype = C.c_int
+lib.oracle_phmm_simd_available.restype = C.c_int
+lib.oracle_phmm_simd_batch.restype = C.c_int
+lib.oracle_phmm_simd_batch.argtypes = lib.oracle_phmm_batch.argtypes
 lib.oracle_ksw_extend2.restype = C.c_int
 lib.oracle_ksw_extend2.argtypes = [C.c_int, vp, C.c_int, vp, C.c_int, vp] + [C.c_int] * 8 + [vp] * 6
 lib.oracle_ksw_global2.restype = C.c_int
@@ -102,6 +106,22 @@ def phmm_java_log10(read, hap):
     r = _rd(read)
     h = _a(hap.encode() if isinstance(hap, str) else hap)
     return float(lib.oracle_phmm_java_log10(*[_p(x) for x in r], len(r[0]), _p(h), len(h)))
+
+
+def phmm_simd_batch(p, threads=1, raw=False):
+    """GKL-style AVX-512 PairHMM (oracle/pairhmm_simd.c), same outputs as
+    phmm_batch; None when the CPU has no AVX-512."""
+    n = int(p.pair_read.size)
+    out = np.zeros(n, np.float64)
+    ud = np.zeros(n, np.int32)
+    rawf = np.zeros(n, np.float32) if raw else None
+    rc = lib.oracle_phmm_simd_batch(_p(p.read_bases), _p(p.read_bq), _p(p.read_iq), _p(p.read_dq), _p(p.read_gcp),
+                                    _p(p.read_off), _p(p.read_len), _p(p.hap_bases), _p(p.hap_off), _p(p.hap_len),
+                                    _p(p.pair_read), _p(p.pair_hap), n, _p(rawf) if raw else None, _p(out), _p(ud),
+                                    threads)
+    if rc < 0:
+        return None
+    return (out, ud.astype(bool), rawf) if raw else (out, ud.astype(bool))
 
 
 def phmm_batch(p, threads=1, raw=False):
