@@ -74,53 +74,34 @@ struct SRowC {
   int mask;
 };
 
+// Branch-free (selects only): an SRowC assembled in role branches was merged
+// through a 36-byte stack copy, i.e. a scratch store + reload per stripe
+// (0.5-0.8 GB of scratch traffic per C2 pass, profiles/r2/r2d_*).
 __device__ __forceinline__ SRowC srow_params(const PhmmTables<float>& tab, const RawRow& raw, int role, bool first,
                                              int H) {
+  const RowP<float> q = row_params<float, false>(tab, raw);
+  const bool real = role == 2 || role == 3;  // rows 1..R
+  const bool mid = role == 2;                // rows 1..R-1
+  const bool last = role == 3;               // row R hands X = M + I, I = 0; D is never needed by anyone
+  const bool v = role == 4;                  // V: D = running sum of M; X = M + D
+  const bool pad = role == 1;                // pad: X = prior * Xp = Z one column on, I = 0, D = 0
+  // row 1: M(1, c) = prior * x0 (x0 = X(0, c - 1) for c - 1 >= 0); x * 1.f is exact elsewhere
+  const float x0 = first ? (tab.init_const / (float)H) * tab.dmatch[raw.gq & 127] : 1.f;
+  const float one_vp = (v || pad) ? 1.f : 0.f;
   SRowC c;
-  if (role == 2 || role == 3) {
-    const RowP<float> q = row_params<float, false>(tab, raw);
-    c.e1 = q.e1;
-    c.e3 = q.e3;
-    c.my = q.my;
-    c.yy = q.yy;
-    c.mm = q.mm;
-    c.gm = q.gm;
-    c.mx = q.mx;
-    c.xx = q.xx;
-    c.mask = q.rmask;
-    if (role == 3) {  // hand X = M + I, I = 0; D is never needed by anyone
-      c.my = 0.f;
-      c.mm = 1.f;
-      c.gm = 1.f;
-      c.mx = 0.f;
-      c.xx = 0.f;
-    }
-    if (first) {  // M(1, c) = prior * x0 (x0 = X(0, c - 1) for c - 1 >= 0)
-      const float x0 = (tab.init_const / (float)H) * tab.dmatch[raw.gq & 127];
-      c.e1 *= x0;
-      c.e3 *= x0;
-    }
-  } else if (role == 4) {  // V: D = running sum of M; X = M + D
-    c.e1 = c.e3 = 1.f;
-    c.my = c.yy = 1.f;
-    c.mm = c.gm = 1.f;
-    c.mx = c.xx = 0.f;
-    c.mask = 0;
-  } else if (role == 1) {  // pad: X = prior * Xp = Z one column on, I = 0, D = 0
-    c.e1 = c.e3 = 1.f;
-    c.my = c.yy = 0.f;
-    c.mm = 1.f;
-    c.gm = 0.f;
-    c.mx = c.xx = 0.f;
-    c.mask = 0;
-  } else {
-    c.e1 = c.e3 = c.my = c.yy = c.mm = c.gm = c.mx = c.xx = 0.f;
-    c.mask = 0;
-  }
+  c.e1 = real ? q.e1 * x0 : one_vp;
+  c.e3 = real ? q.e3 * x0 : one_vp;
+  c.my = mid ? q.my : v ? 1.f : 0.f;
+  c.yy = real ? q.yy : v ? 1.f : 0.f;
+  c.mm = mid ? q.mm : (last || v || pad) ? 1.f : 0.f;
+  c.gm = mid ? q.gm : (last || v) ? 1.f : 0.f;
+  c.mx = mid ? q.mx : 0.f;
+  c.xx = mid ? q.xx : 0.f;
+  c.mask = real ? q.rmask : 0;
   return c;
 }
 
-__device__ __forceinline__ RowP2 srow_pack(const SRowC& a, const SRowC& b) {
+__device__ __forceinline__ RowP2 srow_pack(const SRowC a, const SRowC b) {
   RowP2 p;
   p.e1 = pf2{a.e1, b.e1};
   p.e3 = pf2{a.e3, b.e3};

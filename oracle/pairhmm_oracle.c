@@ -44,6 +44,30 @@
  *   rescue : if float result < 1e-28f, redo in double
  *   log10  : float  -> (double)(log10f(res) - log10f(2^120))
  *            double -> log10(res) - log10(2^1020)
+ *
+ * [EXT] decisions where GKL itself cannot be consulted here (each one PARITY
+ * UNPINNED; DESIGN.md §2 carries the same list):
+ *   - Bytes outside A/C/G/T/N.  GKL's AVX kernels first map bases through a
+ *     ConvertChar table (A,C,T,G,N -> small codes); from memory its other
+ *     entries are zero, which would make an unknown byte compare like 'A' (and
+ *     lowercase bases likewise).  That recollection cannot be verified (GKL is
+ *     not vendored, no network), so this oracle and the product keep GATK's
+ *     Java semantics (LoglessPairHMM: plain byte equality, 'N' a wildcard on
+ *     either side), which GKL is contractually tested against.  Reads and
+ *     haplotypes reaching the PairHMM from HaplotypeCaller are A/C/G/T/N in
+ *     practice; tests/test_pairhmm_gpu.py::test_bytes_outside_acgtn pins the
+ *     chosen rule on the GPU.
+ *   - FTZ/DAZ.  Whether GKL runs its float pass with flush-to-zero is unknown
+ *     here.  It stays inside the 1e-5 bar: a float sum below 1e-28 (scaled
+ *     by 2^120) is recomputed in double anyway, and flushing denormal cells
+ *     (< 1.2e-38 each, path gains <= 1) moves an accepted sum by at most
+ *     R*H*1.2e-38, about 4e-34 for a 101 x 300 pair, i.e. < 4e-6 of any sum
+ *     >= 1e-28.  This oracle keeps denormals (IEEE default); so does the GPU
+ *     kernel.
+ *   - GATK's PCR indel error model (--pcr-indel-model, CONSERVATIVE default)
+ *     rewrites the ins/del GOPs before they reach the PairHMM; it is applied by
+ *     the caller's read preparation (falcon-genome_amd/host/gatk_prep.cpp), not
+ *     here: this oracle consumes prepared qualities, as GKL does.
  */
 #include <math.h>
 #include <stdint.h>

@@ -1,42 +1,61 @@
-"""VALU lane-instructions per cell of the SW kernels, from rocprofv3 --pmc
-SQ_INSTS_VALU runs of tools/bsw_bench.py (one per workload), written to
-profiles/pmc_bsw.json for bench.py's SW roofline.
+"""SW counters per ksw_extend2 batch from the rocprofv3 --pmc passes of
+tools/gpu_session.sh's `bswpmc` step (tools/bsw_bench.py, --reps 1 = one
+warm-up + one timed batch, so totals are halved), written to
+profiles/pmc_bsw.json for bench.py's SW roofline:
+  * SQ issue counters of every bsw_* kernel for C3 and the fixed 151x251
+    workload -> VALU lane-instructions per evaluated cell, stall fractions;
+  * FETCH_SIZE / WRITE_SIZE of C3 -> HBM bytes per batch (against the
+    algorithmic qlen + tlen + 24 bytes per task).
 
-usage: python tools/pmc_bsw.py <c3_pmc_dir> <c3_bench.log> <fixed_pmc_dir> <fixed_bench.log> <tag>"""
+usage: python tools/pmc_bsw.py gpurun_out/<tag> <tag>"""
 import csv
 import glob
 import json
 import os
 import sys
 
+BATCHES = 2.0  # bsw_bench.py --reps 1: warm-up + timed
 
-def valu(d):
-    tot, n = 0.0, set()
+
+def totals(d):
+    tot = {}
     for f in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
         for r in csv.DictReader(open(f)):
-            if "bsw_" in r["Kernel_Name"] and r["Counter_Name"] == "SQ_INSTS_VALU":
-                tot += float(r["Counter_Value"])
-                n.add(r.get("Dispatch_Id", ""))
-    return tot
+            if "bsw_" in r["Kernel_Name"]:
+                tot[r["Counter_Name"]] = tot.get(r["Counter_Name"], 0.0) + float(r["Counter_Value"])
+    return {k: v / BATCHES for k, v in tot.items()}
 
 
-def cells(log, key):
+def bench_line(log):
     for line in open(log):
         if line.startswith("{"):
-            return json.loads(line)[key]["cells"]
+            return json.loads(line)
     raise SystemExit(f"no bench line in {log}")
 
 
 def main():
-    c3d, c3l, fxd, fxl, tag = sys.argv[1:6]
+    src, tag = sys.argv[1:3]
     out = {}
-    for name, d, log in (("c3", c3d, c3l), ("fixed", fxd, fxl)):
-        # bsw_bench.py --reps 1 runs the workload twice (warm-up + timed)
-        v = valu(d) / 2
-        c = cells(log, name)
-        out[name] = {"valu_wave_instr": v, "cells": c, "valu_lane_instr_per_cell": round(64 * v / c, 3)}
-    out["_note"] = ("SQ_INSTS_VALU (wave64 instructions) of every bsw_* kernel of one ksw_extend2 batch (keys, "
-                    "bounds, pair / lane kernels), x64 lanes / evaluated cells; separate rocprofv3 --pmc runs")
+    for name in ("c3", "fixed"):
+        sq = totals(os.path.join(src, f"bswpmc_{name}"))
+        b = bench_line(os.path.join(src, f"bswpmc_{name}.log"))[name]
+        d = {"cells": b["cells"], "tasks": b["tasks"], "counters_per_batch": sq,
+             "valu_lane_instr_per_cell": round(64 * sq["SQ_INSTS_VALU"] / b["cells"], 3)}
+        wc = sq.get("SQ_WAVE_CYCLES")
+        for k in ("SQ_ACTIVE_INST_ANY", "SQ_WAIT_INST_ANY", "SQ_WAIT_ANY"):
+            if wc and k in sq:
+                d[k.lower() + "_frac_of_wave_cycles"] = round(sq[k] / wc, 4)
+        out[name] = d
+    fe = totals(os.path.join(src, "bswpmc_c3_fetch")).get("FETCH_SIZE")
+    wr = totals(os.path.join(src, "bswpmc_c3_write")).get("WRITE_SIZE")
+    if fe is not None and wr is not None:
+        out["c3"]["hbm_bytes_per_batch"] = int(round((fe + wr) * 1024))
+        out["c3"]["fetch_kib"], out["c3"]["write_kib"] = fe, wr
+    out["_note"] = ("rocprofv3 --pmc of tools/bsw_bench.py --which <w> --reps 1 (separate passes: SQ issue/stall "
+                    "counters, FETCH_SIZE, WRITE_SIZE), every bsw_* kernel of one ksw_extend2 batch (keys, bounds, "
+                    "extension launch), halved for the warm-up batch; VALU per cell = SQ_INSTS_VALU x 64 / evaluated "
+                    "cells; SQ_*_CYCLES / WAIT / ACTIVE in quad-cycles; FETCH_SIZE uncorrected (1-4 B per-lane loads, "
+                    "the gfx950 1/2 calibration of MI355X_MICROARCH.md is for 16 B/lane streams)")
     out["source"] = tag
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     json.dump(out, open(os.path.join(root, "profiles", "pmc_bsw.json"), "w"), indent=1)

@@ -13,8 +13,8 @@ import shutil
 import sys
 
 KERNELS = ("phmm3_kernel", "phmm2_kernel", "phmm_kernel<float, false, false>")  # fp32 forward: streamed, two-row, one-row
+PASS_MARK = "phmm_keys_kernel"  # one schedule (keys kernel) per forward pass
 C2_CELLS = 22721383941  # sum R*H of the default C2 workload (bench.py config.cells_per_gpu)
-LAUNCHES_PER_PASS = 5   # C2's non-empty hap-length classes
 
 
 def is_fwd(name):
@@ -22,32 +22,43 @@ def is_fwd(name):
 
 
 def counters(path):
-    """Counter totals of the forward-pass kernels, and the number of forward passes they span."""
-    tot, launches = {}, set()
+    """Counter totals of the forward-pass kernels, and the number of forward
+    passes they span (= schedules run: one keys-kernel dispatch per pass)."""
+    tot, marks = {}, set()
     for x in csv.DictReader(open(path)):
         if is_fwd(x["Kernel_Name"]):
             tot[x["Counter_Name"]] = tot.get(x["Counter_Name"], 0.0) + float(x["Counter_Value"])
-            launches.add(x["Dispatch_Id"])
-    return tot, len(launches) / LAUNCHES_PER_PASS
+        elif PASS_MARK in x["Kernel_Name"]:
+            marks.add(x["Dispatch_Id"])
+    return tot, max(1, len(marks))
 
 
 def main():
     src, dst, tag = sys.argv[1:4]
     cells = int(sys.argv[4]) if len(sys.argv) > 4 else C2_CELLS
     os.makedirs(dst, exist_ok=True)
-    shutil.copy(os.path.join(src, "prof", "run_kernel_stats.csv"), os.path.join(dst, f"{tag}_kernel_stats.csv"))
+    summary = {"kernels": KERNELS}
     for f in ("bench.log", "benchq.log", "pytest_gpu.log"):
         if os.path.exists(os.path.join(src, f)):
             shutil.copy(os.path.join(src, f), os.path.join(dst, f"{tag}_{f}"))
-    rows = list(csv.DictReader(open(os.path.join(src, "prof", "run_kernel_trace.csv"))))
-    ph = sorted((r for r in rows if is_fwd(r["Kernel_Name"])), key=lambda r: int(r["Start_Timestamp"]))
-    # a pass = LAUNCHES_PER_PASS consecutive class launches (in start order)
-    passes = [[(int(r["Start_Timestamp"]), int(r["End_Timestamp"])) for r in ph[i:i + LAUNCHES_PER_PASS]]
-              for i in range(0, len(ph) - LAUNCHES_PER_PASS + 1, LAUNCHES_PER_PASS)]
-    spans = [(max(e for _, e in p) - min(s for s, _ in p)) / 1e6 for p in passes]
-    summary = {"kernels": KERNELS, "launches_per_pass": [len(p) for p in passes], "pass_span_ms": spans,
-               "note": "span = last end - first start over the class launches of one forward pass; "
-                       "compare with bench.py stages_ms.forward_fp32 (HIP events on the launch stream)"}
+    if os.path.exists(os.path.join(src, "prof", "run_kernel_trace.csv")):
+        shutil.copy(os.path.join(src, "prof", "run_kernel_stats.csv"), os.path.join(dst, f"{tag}_kernel_stats.csv"))
+        rows = list(csv.DictReader(open(os.path.join(src, "prof", "run_kernel_trace.csv"))))
+        rows.sort(key=lambda r: int(r["Start_Timestamp"]))
+        # a pass = the forward launches between one schedule (keys kernel) and the next
+        passes, cur = [], None
+        for r in rows:
+            if PASS_MARK in r["Kernel_Name"]:
+                cur = []
+                passes.append(cur)
+            elif is_fwd(r["Kernel_Name"]) and cur is not None:
+                cur.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"])))
+        passes = [p for p in passes if p]
+        spans = [(max(e for _, e in p) - min(s for s, _ in p)) / 1e6 for p in passes]
+        summary.update({"launches_per_pass": [len(p) for p in passes], "pass_span_ms": spans,
+                        "pass_span_ms_warm_min": min(spans[1:] or spans or [0]),
+                        "note": "span = last end - first start over the class launches of one forward pass; "
+                                "compare with bench.py stages_ms.forward_fp32 (HIP events on the launch stream)"})
     pmc = {}
     for d in sorted(os.listdir(src)):
         p = os.path.join(src, d, "run_counter_collection.csv")
