@@ -230,8 +230,10 @@ def bench_e2e(args, rank, local):
     try:
         L = int(args.e2e_mbp * 1e6)
         subprocess.run([exe, "synth", "-o", work + "/d", "-c", f"chr1:{L}", "-x", "30", "--tumor",
-                        "--seed", str(args.seed + rank)], env=env, check=True, capture_output=True)
-        out = {"data": f"synthetic chr1-like {args.e2e_mbp:g} Mbp per GPU, sample 30x, tumor 40x (+1e-4 somatic)"}
+                        "--noisy-frac", "0.01", "--seed", str(args.seed + rank)], env=env, check=True,
+                       capture_output=True)
+        out = {"data": f"synthetic chr1-like {args.e2e_mbp:g} Mbp per GPU, sample 30x, tumor 40x (+1e-4 somatic), "
+                       "1% of reads mis-mapped-like (20% high-quality mismatches: their pairs reach the fp64 rescue)"}
 
         def timed(name, cmd):
             shutil.rmtree(env["FCS_LOG_DIR"], ignore_errors=True)
@@ -246,16 +248,32 @@ def bench_e2e(args, rank, local):
                     logs += open(os.path.join(env["FCS_LOG_DIR"], f)).read()
             return dt, logs, r.stderr
         d = work + "/d"
-        dt, logs, _ = timed("htc", ["htc", "-r", d + "/ref.fasta", "-i", d + "/sample.bam", "-o", work + "/htc.vcf"])
-        reg = sum(int(x) for x in re.findall(r"(\d+) regions", logs))
-        pairs = sum(int(x) for x in re.findall(r"(\d+) pairs", logs))
-        cells = sum(int(x) for x in re.findall(r"(\d+) cells", logs))
-        out["htc"] = {"regions": reg, "pairs": pairs, "cells": cells, "seconds": round(dt, 3),
-                      "regions_per_s": round(reg / dt, 1)}
+
+        def shard_stats(logs, dt):
+            """Per-shard caller lines summed over the shards (workers/*.cpp): counts,
+            and the stage times as thread-seconds (shards run concurrently)."""
+            tot = lambda pat, f=float: sum(f(x) for x in re.findall(pat, logs))  # noqa: E731
+            st = {"regions": tot(r"(\d+) regions", int), "pairs": tot(r"(\d+) pairs", int),
+                  "cells": tot(r"(\d+) cells", int), "rescued_pairs": tot(r"(\d+) rescued", int),
+                  "seconds": round(dt, 3)}
+            st["regions_per_s"] = round(st["regions"] / dt, 1)
+            brk = {k: round(tot(pat), 3) for k, pat in (
+                ("decode", r"decode ([\d.]+) s"), ("pileup", r"pileup ([\d.]+) s"),
+                ("regions", r"regions ([\d.]+) s\b"), ("phmm_call", r"PairHMM ([\d.]+) s"),
+                ("genotype", r"genotype ([\d.]+) s"), ("output", r"output ([\d.]+) s"))}
+            st["stage_thread_seconds"] = brk
+            dev, res = tot(r"device ([\d.]+) s"), tot(r"rescue ([\d.]+) s")
+            st["phmm_device_seconds"] = round(dev, 4)
+            st["rescue_fp64_device_seconds"] = round(res, 4)
+            st["gpu_busy_frac"] = round(dev / dt, 4)  # PairHMM device time (HIP events) / wall time, one GPU
+            st["effective_gcups"] = round(st["cells"] / dt / 1e9, 2)
+            return st
+        dt, logs, _ = timed("htc", ["htc", "-r", d + "/ref.fasta", "-i", d + "/sample.bam", "-o", work + "/htc.g.vcf"])
+        out["htc"] = shard_stats(logs, dt)
+        out["htc"]["output"] = "GVCF (the reference's default)"
         dt, logs, _ = timed("mutect2", ["mutect2", "-r", d + "/ref.fasta", "-t", d + "/tumor.bam", "-n",
                                         d + "/sample.bam", "-o", work + "/m2.vcf"])
-        reg = sum(int(x) for x in re.findall(r"(\d+) regions", logs))
-        out["mutect2"] = {"regions": reg, "seconds": round(dt, 3), "regions_per_s": round(reg / dt, 1)}
+        out["mutect2"] = shard_stats(logs, dt)
         dt, _, err = timed("align", ["align", "-r", d + "/ref.fasta", "-1", d + "/sample.fastq", "-o",
                                      work + "/aln.bam"])
         m = re.search(r"(\d+) reads, (\d+) mapped, (\d+) extension tasks", err)
@@ -323,6 +341,10 @@ def bsw_roofline(r3, rf):
            "body_instr_per_cell": 9.75,
            "hbm_GBs": round(r3["bytes"] / (r3["ms"] * 1e-3) / 1e9, 2),
            "hbm_frac": round(r3["bytes"] / (r3["ms"] * 1e-3) / 1e9 / HBM_PEAK_GBS, 5)}
+    c3m = meas.get("c3", {})
+    if c3m.get("hbm_bytes_per_batch"):
+        out["traffic"] = c3m["hbm_bytes_per_batch"]
+        out["traffic_note"] = "FETCH_SIZE + WRITE_SIZE of one C3 batch (profiles/pmc_bsw.json)"
     if per3:
         ach = r3["gcups"] * 1e9 * per3
         out.update(achieved=round(ach / 1e12, 3), frac=round(ach / VALU_LANE_INSTR_PEAK, 4),
@@ -410,7 +432,7 @@ def main():
                      "kernel": "phmm3_kernel (row-streamed segments, two read rows per lane, packed FP32): fp32 forward pass = one launch "
                                "per launch class, overlapped on 4 streams; achieved = algorithmic FLOPs / pass "
                                "time (HIP events on the launch stream; rocprof pass span in "
-                               "profiles/r2/r2b_phmm_summary.json)",
+                               "profiles/r2/r2d_phmm_summary.json)",
                      "valu_instr_per_cell": vipc,
                      "valu_issue_frac": (round(ph["cells"] / fwd_s * vipc / VALU_LANE_INSTR_PEAK, 4) if vipc
                                          else None),

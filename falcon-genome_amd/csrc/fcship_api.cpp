@@ -23,6 +23,7 @@ namespace fcs {
 
 static thread_local std::string g_last_error;
 static thread_local int64_t g_last_rescued = 0;
+static thread_local double g_last_device_ms = 0, g_last_rescue_ms = 0;
 void set_error(const std::string& msg) { g_last_error = msg; }
 int fail(int code, const std::string& msg) {
   set_error(msg);
@@ -130,6 +131,7 @@ struct Session {
   size_t dev_cap = 0;
   void* host = nullptr;
   size_t host_cap = 0;
+  hipEvent_t ev[3] = {nullptr, nullptr, nullptr};  // PairHMM call: start, after forward, after rescue
   ~Session();
   int ensure_dev(size_t bytes);
   int ensure_host(size_t bytes);
@@ -296,6 +298,8 @@ Session::~Session() {
   if (s) (void)hipStreamSynchronize(s);
   fcs_phmm_plan_destroy(phmm);
   fcs_bsw_plan_destroy(bsw);
+  for (hipEvent_t e : ev)
+    if (e) (void)hipEventDestroy(e);
   if (dev) (void)hipFree(dev);
   if (host) (void)hipHostFree(host);
 }
@@ -545,6 +549,13 @@ int fcs_phmm_dev_run(fcs_phmm_plan* plan, const fcs_phmm_batch* b, double* out, 
   return fcs_phmm_dev_rescue(plan, b, out, opts, stream);
 }
 
+int fcs_phmm_last_device_ms(double* device_ms, double* rescue_ms) {
+  if (!device_ms || !rescue_ms) return fail(FCS_ERR_INVALID, "[E::fcs_phmm_last_device_ms] null output");
+  *device_ms = g_last_device_ms;
+  *rescue_ms = g_last_rescue_ms;
+  return FCS_OK;
+}
+
 int fcs_phmm_last_rescued(int64_t* count) {
   if (!count) return fail(FCS_ERR_INVALID, "[E::fcs_phmm_last_rescued] null count");
   *count = g_last_rescued;
@@ -624,7 +635,14 @@ int phmm_staged(const PhmmStage& g, const fcs_phmm_opts& opts, Fill&& fill, cons
   d.max_hap_len = g.max_hap_len;
   double* dout = S->d<double>(out_off);
   FCS_HIP_CHECK(hipMemsetAsync(dout, 0xFF, 8 * np, s));  // all-ones = NaN: "not written"
-  if ((rc = fcs_phmm_dev_run(S->phmm, &d, dout, &opts, s))) return rc;
+  for (hipEvent_t& e : S->ev)
+    if (!e) FCS_HIP_CHECK(hipEventCreate(&e));
+  FCS_HIP_CHECK(hipEventRecord(S->ev[0], s));
+  if ((rc = fcs_phmm_dev_schedule(S->phmm, &d, s)) || (rc = fcs_phmm_dev_forward(S->phmm, &d, dout, &opts, s)))
+    return rc;
+  FCS_HIP_CHECK(hipEventRecord(S->ev[1], s));
+  if ((rc = fcs_phmm_dev_rescue(S->phmm, &d, dout, &opts, s))) return rc;
+  FCS_HIP_CHECK(hipEventRecord(S->ev[2], s));
   double* hout = S->h<double>(out_off);
   FCS_HIP_CHECK(hipMemcpyAsync(hout, dout, 8 * np, hipMemcpyDeviceToHost, s));
   // into the input staging: its H2D copy is stream-ordered before this copy
@@ -634,6 +652,11 @@ int phmm_staged(const PhmmStage& g, const fcs_phmm_opts& opts, Fill&& fill, cons
     FCS_HIP_CHECK(hipMemcpyAsync(hres, S->phmm->rescue_count, sizeof(*hres), hipMemcpyDeviceToHost, s));
   FCS_HIP_CHECK(hipStreamSynchronize(s));
   if (opts.use_fp64_rescue) g_last_rescued = (int64_t)*hres;
+  float ms_all = 0.f, ms_res = 0.f;
+  FCS_HIP_CHECK(hipEventElapsedTime(&ms_all, S->ev[0], S->ev[2]));
+  FCS_HIP_CHECK(hipEventElapsedTime(&ms_res, S->ev[1], S->ev[2]));
+  g_last_device_ms = ms_all;
+  g_last_rescue_ms = ms_res;
   int64_t missing = 0;
   for (size_t k = 0; k < np; ++k) missing += std::isnan(hout[k]);
   if (missing)
@@ -1164,6 +1187,6 @@ int fcs_ksw_global2(int qlen, const uint8_t* query, int tlen, const uint8_t* tar
   return score;
 }
 
-int fcs_abi_symbol_count(void) { return 32; }
+int fcs_abi_symbol_count(void) { return 33; }
 
 }  // extern "C"

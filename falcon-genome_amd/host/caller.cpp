@@ -25,6 +25,13 @@ void CallerStats::add(const CallerStats& o) {
   rescued += o.rescued;
   seconds += o.seconds;
   phmm_seconds += o.phmm_seconds;
+  phmm_device_seconds += o.phmm_device_seconds;
+  rescue_device_seconds += o.rescue_device_seconds;
+  decode_seconds += o.decode_seconds;
+  pileup_seconds += o.pileup_seconds;
+  region_seconds += o.region_seconds;
+  genotype_seconds += o.genotype_seconds;
+  output_seconds += o.output_seconds;
 }
 
 namespace {
@@ -306,6 +313,11 @@ void run_phmm(std::vector<std::unique_ptr<Region>>& batch, const CallerOptions& 
   if (rc != FCS_OK) throw failedCommand(std::string(fcs_last_error()));
   int64_t nres = 0;
   if (fcs_phmm_last_rescued(&nres) == FCS_OK) st.rescued += nres;
+  double dev_ms = 0, res_ms = 0;
+  if (fcs_phmm_last_device_ms(&dev_ms, &res_ms) == FCS_OK) {
+    st.phmm_device_seconds += dev_ms / 1e3;
+    st.rescue_device_seconds += res_ms / 1e3;
+  }
   if (dump)
     for (const auto& g : batch)
       for (int s = 0; s < 2; ++s)
@@ -510,11 +522,13 @@ CallerStats call_intervals(const Reference& ref, const std::vector<std::string>&
     if (pending.empty()) return;
     if (interrupted()) throw interruptedError();
     run_phmm(pending, opt, st, dump);
+    const uint64_t tg = now_us();
     for (size_t i = 0; i < pending.size(); ++i) {
       const auto& [ob, oe, chrom] = own[i];
       if (opt.somatic) genotype_somatic(*pending[i], opt, ob, oe, chrom, calls);
       else genotype_germline(*pending[i], opt, ob, oe, chrom, calls);
     }
+    st.genotype_seconds += (now_us() - tg) / 1e6;
     pending.clear();
     own.clear();
   };
@@ -544,8 +558,11 @@ CallerStats call_intervals(const Reference& ref, const std::vector<std::string>&
       we = std::min<int64_t>(L, own_end + ext_r);
       reads[0].clear();
       reads[1].clear();
+      const uint64_t td = now_us();
       load_reads(bams, iv.chrom, wb, we, opt, reads[0]);
       if (opt.somatic) load_reads(normal_bams, iv.chrom, wb, we, opt, reads[1]);
+      const uint64_t tp = now_us();
+      st.decode_seconds += (tp - td) / 1e6;
       pu = Pileup();
       pu.wb = wb;
       pu.depth.assign(we - wb, 0);
@@ -570,11 +587,14 @@ CallerStats call_intervals(const Reference& ref, const std::vector<std::string>&
         if (we < L && last + 2 * opt.padding >= we) grow_r = true;
         clusters.emplace_back(first, last);
       }
+      st.pileup_seconds += (now_us() - tp) / 1e6;
       if (!grow_l && !grow_r) break;
       if (grow_l) ext_l *= 2;
       if (grow_r) ext_r *= 2;
     }
     st.reads += (int64_t)(reads[0].size() + reads[1].size());
+    const uint64_t tr = now_us();
+    const double in_flush0 = st.phmm_seconds + st.genotype_seconds;
     for (const auto& [first, last] : clusters) {
       for (int64_t rb = std::max<int64_t>(0, first - opt.padding); rb < std::min<int64_t>(L, last + opt.padding + 1);
            rb += opt.max_region) {
@@ -625,15 +645,19 @@ CallerStats call_intervals(const Reference& ref, const std::vector<std::string>&
         if ((int)pending.size() >= opt.batch_regions) flush();
       }
     }
+    st.region_seconds += (now_us() - tr) / 1e6 - (st.phmm_seconds + st.genotype_seconds - in_flush0);
     flush();
     if (opt.gvcf && !opt.somatic) {
+      const uint64_t tv = now_us();
       std::vector<const VcfRecord*> ic;
       for (size_t i = c0; i < calls.size(); ++i) ic.push_back(&calls[i]);
       emit_gvcf(seq, pu, own_beg, own_end, iv.chrom, ic, gout);
+      st.output_seconds += (now_us() - tv) / 1e6;
     }
   }
   flush();
   if (dump) std::fclose(dump);
+  const uint64_t tw = now_us();
   st.calls = (int64_t)calls.size();
   std::vector<VcfRecord>& recs = (opt.gvcf && !opt.somatic) ? gout : calls;
   std::stable_sort(recs.begin(), recs.end(), [&](const VcfRecord& a, const VcfRecord& b) {
@@ -641,6 +665,7 @@ CallerStats call_intervals(const Reference& ref, const std::vector<std::string>&
     return ia != ib ? ia < ib : a.pos < b.pos;
   });
   for (const VcfRecord& r : recs) out.write(r);
+  st.output_seconds += (now_us() - tw) / 1e6;
   st.seconds = (now_us() - t0) / 1e6;
   return st;
 }

@@ -166,6 +166,10 @@ int fcs_phmm_plan_rescue_count(fcs_phmm_plan* plan, void* stream, int64_t* count
 /* Pairs the fp64 rescue recomputed in the calling thread's last synchronous
  * fcs_phmm_compute / _regions / _pairs call (0 when rescue is off). */
 int fcs_phmm_last_rescued(int64_t* count);
+/* Device time of the calling thread's last synchronous PairHMM call, from HIP
+ * events on its stream: schedule + fp32 forward + fp64 rescue, and the rescue
+ * stage alone (ms).  Host staging and PCIe copies are not included. */
+int fcs_phmm_last_device_ms(double* device_ms, double* rescue_ms);
 
 /* -------------------------------------------------------------- banded SW */
 typedef struct {
