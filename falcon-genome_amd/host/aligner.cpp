@@ -12,6 +12,7 @@
 #include "config.h"
 #include "executor.h"
 #include "fcship.h"
+#include "seedext.h"
 
 namespace fcsg {
 
@@ -37,13 +38,6 @@ std::string revcomp(const std::string& s) {
   std::string o(s.rbegin(), s.rend());
   for (char& c : o) c = c == 'A' ? 'T' : c == 'C' ? 'G' : c == 'G' ? 'C' : c == 'T' ? 'A' : 'N';
   return o;
-}
-
-// bwa's infer_bw (bwamem.c): band implied by a score over lengths l1, l2.
-int infer_bw(int l1, int l2, int score, int a, int q, int r) {
-  int w = (int)((double)(std::min(l1, l2) * a - score - q) / r + 2.);
-  if (w < std::abs(l1 - l2)) w = std::abs(l1 - l2);
-  return w;
 }
 
 // Static split of [0, n) over up to `threads` std::threads.
@@ -76,7 +70,6 @@ struct Aln {
   int score = 0, truesc = 0;
   int qb = 0, qe = 0;
   int64_t rb = 0, re = 0;
-  int w_left = 0, w_right = 0;
   std::vector<uint32_t> cigar;
   int nm = 0;
   std::string md;
@@ -91,6 +84,8 @@ KmerIndex::KmerIndex(const Reference& ref, int k) : k_(k) {
   for (const Contig& c : ref.contigs) {
     starts_.push_back(g);
     const int64_t L = (int64_t)c.seq.size();
+    codes_.emplace_back(L);
+    for (int64_t p = 0; p < L; ++p) codes_.back()[p] = code_of(c.seq[p]);
     uint64_t key = 0;
     int valid = 0;
     const uint64_t mask = (k == 32) ? ~0ull : ((1ull << (2 * k)) - 1);
@@ -136,7 +131,6 @@ AlignStats align_reads(const Reference& ref, const KmerIndex& idx, const std::ve
   const uint64_t t0 = now_us();
   fcs_bsw_params P;
   fcs_bsw_params_default(&P);
-  const int a = 1;  // match score of the default matrix
   const int k = idx.k();
   const uint64_t kmask = (1ull << (2 * k)) - 1;
   std::vector<Aln> alns(seqs.size());
@@ -228,183 +222,46 @@ AlignStats align_reads(const Reference& ref, const KmerIndex& idx, const std::ve
   };
   parallel_for(seqs.size(), opt.threads, seed_read);
 
-  auto run_ext = [&](std::vector<fcs_bsw_task>& tasks, std::vector<fcs_bsw_result>& res) {
-    res.resize(tasks.size());
-    if (tasks.empty()) return;
-    const uint64_t g0 = now_us();
-    if (fcs_bsw_extend(tasks.data(), (int32_t)tasks.size(), &P, res.data(), opt.gpu) != FCS_OK)
-      throw failedCommand(std::string(fcs_last_error()));
-    st.gpu_seconds += (now_us() - g0) / 1e6;
-    st.ext_tasks += (int64_t)tasks.size();
-  };
-
-  // ---- left extensions (reversed prefix vs reversed reference), band retry
-  std::vector<std::vector<uint8_t>> lq(alns.size()), lt(alns.size());
+  // ---- bwa's extension protocol on the GPU (host/seedext.cpp): left and right
+  // extensions with band retry, local vs to-end, CIGARs by banded global alignment
   {
+    std::vector<SeedJob> jobs;
     std::vector<int> who;
-    std::vector<fcs_bsw_task> tasks;
-    std::vector<fcs_bsw_result> res;
     for (Aln& A : alns) {
       if (!A.mapped) continue;
-      A.score = A.truesc = A.seed_len * a;
-      A.qb = A.seed_q;
-      A.rb = A.seed_r;
-      if (A.seed_q == 0) continue;
-      const std::string& R = ref.contigs[A.contig].seq;
-      const int64_t tl = std::min<int64_t>(A.seed_r, A.seed_q + opt.w);
-      auto& q = lq[A.read];
-      auto& t = lt[A.read];
-      q.assign(A.q.rend() - A.seed_q, A.q.rend());
-      t.resize(tl);
-      for (int64_t i = 0; i < tl; ++i) t[i] = code_of(R[A.seed_r - 1 - i]);
+      const std::vector<uint8_t>& R = idx.codes(A.contig);
+      SeedJob J;
+      J.q = A.q.data();
+      J.qlen = (int)A.q.size();
+      J.ref = R.data();
+      J.rlen = (int64_t)R.size();
+      J.seed_q = A.seed_q;
+      J.seed_r = A.seed_r;
+      J.seed_len = A.seed_len;
+      jobs.push_back(J);
       who.push_back(A.read);
     }
-    std::vector<int> w_of(alns.size(), opt.w);
-    std::vector<int> todo = who;
-    for (int pass = 0; pass < 2 && !todo.empty(); ++pass) {
-      tasks.clear();
-      for (int r : todo)
-        tasks.push_back({(int32_t)lq[r].size(), (int32_t)lt[r].size(), alns[r].seed_len * a, w_of[r], lq[r].data(),
-                         lt[r].data()});
-      run_ext(tasks, res);
-      std::vector<int> again;
-      for (size_t i = 0; i < todo.size(); ++i) {
-        Aln& A = alns[todo[i]];
-        const fcs_bsw_result& x = res[i];
-        const int prev = A.score;
-        A.score = x.score;
-        A.w_left = w_of[A.read];
-        if (x.gscore <= 0 || x.gscore <= A.score - P.end_bonus) {  // local
-          A.qb = A.seed_q - x.qle;
-          A.rb = A.seed_r - x.tle;
-          A.truesc = A.score;
-        } else {  // to-end
-          A.qb = 0;
-          A.rb = A.seed_r - x.gtle;
-          A.truesc = x.gscore;
-        }
-        const int w = w_of[A.read];
-        if (pass == 0 && A.score != prev && x.max_off >= (w >> 1) + (w >> 2)) {
-          w_of[A.read] = w << 1;
-          again.push_back(A.read);
-        }
-      }
-      todo = again;
-    }
-  }
-  // ---- right extensions (h0 = score after the left extension)
-  {
-    std::vector<int> who;
-    std::vector<fcs_bsw_task> tasks;
-    std::vector<fcs_bsw_result> res;
-    std::vector<int> sc0(alns.size(), 0), w_of(alns.size(), opt.w), left_true(alns.size(), 0);
-    for (Aln& A : alns) {
-      if (!A.mapped) continue;
-      const int qe = A.seed_q + A.seed_len;
-      A.qe = qe;
-      A.re = A.seed_r + A.seed_len;
-      if (qe == (int)A.q.size()) continue;
-      const std::string& R = ref.contigs[A.contig].seq;
-      auto& q = lq[A.read];
-      auto& t = lt[A.read];
-      q.assign(A.q.begin() + qe, A.q.end());
-      const int64_t tl = std::min<int64_t>((int64_t)R.size() - A.re, (int64_t)q.size() + opt.w);
-      t.resize(std::max<int64_t>(tl, 0));
-      for (int64_t i = 0; i < tl; ++i) t[i] = code_of(R[A.re + i]);
-      sc0[A.read] = A.score;
-      left_true[A.read] = A.truesc;
-      who.push_back(A.read);
-    }
-    std::vector<int> todo = who;
-    for (int pass = 0; pass < 2 && !todo.empty(); ++pass) {
-      tasks.clear();
-      for (int r : todo)
-        tasks.push_back({(int32_t)lq[r].size(), (int32_t)lt[r].size(), sc0[r], w_of[r], lq[r].data(), lt[r].data()});
-      run_ext(tasks, res);
-      std::vector<int> again;
-      for (size_t i = 0; i < todo.size(); ++i) {
-        Aln& A = alns[todo[i]];
-        const fcs_bsw_result& x = res[i];
-        const int prev = A.score;
-        const int qe0 = A.seed_q + A.seed_len;
-        const int64_t re0 = A.seed_r + A.seed_len;
-        A.score = x.score;
-        A.w_right = w_of[A.read];
-        // each try recomputes the right part from the left result (sc0)
-        if (x.gscore <= 0 || x.gscore <= A.score - P.end_bonus) {  // local
-          A.qe = qe0 + x.qle;
-          A.re = re0 + x.tle;
-          A.truesc = left_true[A.read] + A.score - sc0[A.read];
-        } else {  // to-end
-          A.qe = (int)A.q.size();
-          A.re = re0 + x.gtle;
-          A.truesc = left_true[A.read] + x.gscore - sc0[A.read];
-        }
-        const int w = w_of[A.read];
-        if (pass == 0 && A.score != prev && x.max_off >= (w >> 1) + (w >> 2)) {
-          w_of[A.read] = w << 1;
-          again.push_back(A.read);
-        }
-      }
-      todo = again;
-    }
-  }
-
-  // ---- global alignment for the CIGAR (bwa_gen_cigar2 with band inference / widening)
-  {
-    std::vector<int> todo;
-    std::vector<int> w2(alns.size(), 0), last_sc(alns.size(), INT32_MIN), tries(alns.size(), 0);
-    std::vector<std::vector<uint8_t>> gq(alns.size()), gt(alns.size());
-    for (Aln& A : alns) {
-      if (!A.mapped) continue;
-      if (A.qe <= A.qb || A.re <= A.rb) {
-        A.mapped = false;
-        continue;
-      }
-      const std::string& R = ref.contigs[A.contig].seq;
-      gq[A.read].assign(A.q.begin() + A.qb, A.q.begin() + A.qe);
-      gt[A.read].resize(A.re - A.rb);
-      for (int64_t i = A.rb; i < A.re; ++i) gt[A.read][i - A.rb] = code_of(R[i]);
-      const int l1 = A.qe - A.qb, l2 = (int)(A.re - A.rb);
-      int w = std::max(infer_bw(l1, l2, A.truesc, a, P.o_del, P.e_del), infer_bw(l1, l2, A.truesc, a, P.o_ins, P.e_ins));
-      const int wmax = std::max(A.w_left, A.w_right) ? std::max(A.w_left, A.w_right) : opt.w;
-      if (w > opt.w) w = std::min(w, wmax);
-      w2[A.read] = w;
-      todo.push_back(A.read);
-    }
-    while (!todo.empty()) {
-      std::vector<fcs_bsw_task> tasks;
-      std::vector<int64_t> off;
-      std::vector<int32_t> cap;
-      int64_t tot = 0;
-      for (int r : todo) {
-        w2[r] = std::min(w2[r], opt.w << 2);
-        tasks.push_back({(int32_t)gq[r].size(), (int32_t)gt[r].size(), 0, w2[r], gq[r].data(), gt[r].data()});
-        off.push_back(tot);
-        cap.push_back((int32_t)(gq[r].size() + gt[r].size() + 1));
-        tot += cap.back();
-      }
-      std::vector<int32_t> scores(tasks.size()), ncig(tasks.size());
-      std::vector<uint32_t> arena((size_t)std::max<int64_t>(tot, 1));
-      const uint64_t g0 = now_us();
-      if (fcs_bsw_global(tasks.data(), (int32_t)tasks.size(), &P, scores.data(), arena.data(), off.data(), cap.data(),
-                         ncig.data(), opt.gpu) != FCS_OK)
-        throw failedCommand(std::string(fcs_last_error()));
-      st.gpu_seconds += (now_us() - g0) / 1e6;
-      st.global_tasks += (int64_t)tasks.size();
-      std::vector<int> again;
-      for (size_t i = 0; i < todo.size(); ++i) {
-        Aln& A = alns[todo[i]];
-        A.cigar.assign(arena.begin() + off[i], arena.begin() + off[i] + ncig[i]);
-        const int sc = scores[i];
-        const bool stop = sc == last_sc[A.read] || w2[A.read] == opt.w << 2;
-        last_sc[A.read] = sc;
-        if (!stop && ++tries[A.read] < 3 && sc < A.truesc - a) {
-          w2[A.read] <<= 1;
-          again.push_back(A.read);
-        }
-      }
-      todo = again;
+    SeedExtOptions so;
+    so.w = opt.w;
+    so.pen_clip5 = so.pen_clip3 = P.end_bonus;
+    so.gpu = opt.gpu;
+    std::vector<SeedAln> res;
+    SeedExtStats xs;
+    extend_seeds(jobs, P, so, res, xs);
+    st.ext_tasks += xs.ext_tasks;
+    st.global_tasks += xs.global_tasks;
+    st.gpu_seconds += xs.gpu_seconds;
+    for (size_t i = 0; i < who.size(); ++i) {
+      Aln& A = alns[who[i]];
+      SeedAln& x = res[i];
+      A.qb = x.qb;
+      A.qe = x.qe;
+      A.rb = x.rb;
+      A.re = x.re;
+      A.score = x.score;
+      A.truesc = x.truesc;
+      A.cigar.swap(x.cigar);
+      if (A.qe <= A.qb || A.re <= A.rb) A.mapped = false;
     }
   }
 

@@ -4,12 +4,9 @@
 //
 // Per chunk of reads (bwa.chunk_size): exact-match seeds from a k-mer index of
 // the reference, the best chain per read, then bwa's extension protocol on the
-// GPU — one batch of left extensions (reversed query/target, h0 = seed score),
-// one batch of right extensions (h0 = the left score), each retried with a
-// doubled band where max_off >= 3/4 w (MAX_BAND_TRY = 2) — bwa's local vs
-// to-end clipping decision (pen_clip 5), and one batch of banded global
-// alignments (ksw_global2) for the CIGARs with bwa's band inference and
-// widening.  NM / MD / AS tags, soft clips, sorted BAM + BAI output.
+// GPU (host/seedext.h: mem_chain2aln's windows, left / right extensions with
+// band retry, local vs to-end, mem_reg2aln / bwa_gen_cigar2's global
+// alignment for the CIGAR).  NM / MD / AS tags, soft clips, sorted BAM + BAI.
 // What stands in for bwa [EXT]: seeds are k-mer hits grown to maximal exact
 // matches instead of SMEMs from an FM-index, and chaining keeps the diagonal
 // with the most hits.
@@ -49,9 +46,12 @@ class KmerIndex {
   // global coordinate ↔ (contig, offset)
   int contig_of(uint64_t g, int64_t& off) const;
   uint64_t global(int contig) const { return starts_[contig]; }
+  // the contig's bases as codes 0..4 (A, C, G, T, other)
+  const std::vector<uint8_t>& codes(int contig) const { return codes_[contig]; }
 
  private:
   int k_;
+  std::vector<std::vector<uint8_t>> codes_;
   std::vector<uint64_t> keys_, pos_;  // sorted by key
   std::vector<uint64_t> starts_;
 };

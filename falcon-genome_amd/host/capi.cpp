@@ -15,6 +15,7 @@
 #include "executor.h"
 #include "fasta.h"
 #include "gatk_prep.h"
+#include "seedext.h"
 #include "intervals.h"
 #include "vcf.h"
 
@@ -97,6 +98,47 @@ int fcsg_intersect_regions(const char* const* paths, int n, char* buf, int cap) 
 }
 
 int fcsg_gvcf_band(int gq) { return gvcf_band(gq); }
+
+// bwa's seed-extension protocol (host/seedext.h) over n seeds on one reference
+// sequence (codes 0..4); per job out_i = {qb, qe, score, truesc, w, gscore, gw},
+// out_r = {rb, re}, the CIGAR (ksw ops) in cig[cig_off[i] ...] (ncig[i] ops).
+int fcsg_extend_seeds(int n, const uint8_t* qbuf, const int64_t* qoff, const int32_t* qlen, const uint8_t* ref,
+                      int64_t rlen, const int32_t* seed_q, const int64_t* seed_r, const int32_t* seed_len, int w,
+                      int pen_clip5, int pen_clip3, int gpu, int32_t* out_i, int64_t* out_r, uint32_t* cig,
+                      const int64_t* cig_off, const int32_t* cig_cap, int32_t* ncig) {
+  return guard([&] {
+    std::vector<SeedJob> jobs(n);
+    for (int i = 0; i < n; ++i) {
+      jobs[i].q = qbuf + qoff[i];
+      jobs[i].qlen = qlen[i];
+      jobs[i].ref = ref;
+      jobs[i].rlen = rlen;
+      jobs[i].seed_q = seed_q[i];
+      jobs[i].seed_r = seed_r[i];
+      jobs[i].seed_len = seed_len[i];
+    }
+    fcs_bsw_params P;
+    fcs_bsw_params_default(&P);
+    SeedExtOptions so;
+    so.w = w;
+    so.pen_clip5 = pen_clip5;
+    so.pen_clip3 = pen_clip3;
+    so.gpu = gpu;
+    std::vector<SeedAln> res;
+    SeedExtStats st;
+    extend_seeds(jobs, P, so, res, st);
+    for (int i = 0; i < n; ++i) {
+      const SeedAln& x = res[i];
+      int32_t* o = out_i + 7 * (int64_t)i;
+      o[0] = x.qb, o[1] = x.qe, o[2] = x.score, o[3] = x.truesc, o[4] = x.w, o[5] = x.gscore, o[6] = x.gw;
+      out_r[2 * i] = x.rb;
+      out_r[2 * i + 1] = x.re;
+      if ((int64_t)x.cigar.size() > cig_cap[i]) throw invalidParam("fcsg_extend_seeds: CIGAR capacity");
+      std::copy(x.cigar.begin(), x.cigar.end(), cig + cig_off[i]);
+      ncig[i] = (int32_t)x.cigar.size();
+    }
+  });
+}
 int fcsg_tandem_repeat_units(const char* bases, int offset) { return tandem_repeat_units(bases, offset); }
 int fcsg_pcr_indel_cap(int repeat_len, int model) { return pcr_indel_cap(repeat_len, (PcrIndelModel)model); }
 

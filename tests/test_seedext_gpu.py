@@ -1,0 +1,143 @@
+"""Seed-extension protocol: bwa's mem_chain2aln /
+mem_reg2aln / bwa_gen_cigar2 as `fcs-genome align` runs it on the GPU
+(falcon-genome_amd/host/seedext.cpp, through fcsg_extend_seeds) against the
+CPU restatement oracle/bwa_ext_oracle.c: window, left/right extensions with
+band retry, local vs to-end, truesc, band, global score, band of the final
+ksw_global2 and the CIGAR must all be identical.  bwa itself is [EXT]
+(parity unpinned); the restatement is pinned by hand-checked cases below."""
+import ctypes as C
+
+import numpy as np
+import pytest
+
+import oracle_lib
+
+vp = C.c_void_p
+oracle_lib.lib.oracle_extend_seed.restype = C.c_int
+oracle_lib.lib.oracle_extend_seed.argtypes = ([C.c_int, vp, C.c_int64, vp, C.c_int, C.c_int64, C.c_int, vp] +
+                                              [C.c_int] * 8 + [vp, vp, vp, C.c_int, vp])
+MAT = np.array([1 if i == j else -4 for i in range(4) for j in range(4)], np.int8)
+MAT5 = np.zeros(25, np.int8)
+for i in range(5):
+    for j in range(5):
+        MAT5[i * 5 + j] = -1 if (i == 4 or j == 4) else (1 if i == j else -4)
+
+
+def oracle(q, ref, sq, sr, sl, w=100, clip5=5, clip3=5):
+    oi = np.zeros(7, np.int32)
+    orr = np.zeros(2, np.int64)
+    cap = len(q) + 4 * w + 64
+    cig = np.zeros(cap, np.uint32)
+    nc = C.c_int()
+    rc = oracle_lib.lib.oracle_extend_seed(len(q), q.ctypes.data, len(ref), ref.ctypes.data, sq, sr, sl,
+                                           MAT5.ctypes.data, 6, 1, 6, 1, 100, w, clip5, clip3, oi.ctypes.data,
+                                           orr.ctypes.data, cig.ctypes.data, cap, C.byref(nc))
+    assert rc == 0
+    return oi, orr, cig[:nc.value]
+
+
+def test_oracle_hand_cases():
+    rng = np.random.default_rng(3)
+    ref = rng.integers(0, 4, 5000).astype(np.uint8)
+    q = ref[1000:1151].copy()
+    oi, orr, cig = oracle(q, ref, 60, 1060, 25)
+    assert list(oi[:4]) == [0, 151, 151, 151] and list(orr) == [1000, 1151]
+    assert list(cig) == [151 << 4] and oi[5] == 151 and oi[6] == 0  # equal lengths, w_ = 0: no DP
+    q2 = q.copy()
+    q2[:30] = (q2[:30] + 1) % 4  # junk head: local clip on the left
+    oi, orr, cig = oracle(q2, ref, 60, 1060, 25)
+    assert oi[0] > 0 and orr[0] == 1000 + oi[0]
+    q3 = np.concatenate([q[:80], q[81:]])  # one deletion from the reference
+    oi, orr, cig = oracle(q3, ref, 90, 1091, 25)
+    assert list(orr) == [1000, 1151] and oi[3] == 150 - 7  # 150 matches, gap open 6 + extend 1
+    assert [c & 15 for c in cig] == [0, 2, 0]
+
+
+def synth_jobs(seed, n, rlen=300_000):
+    rng = np.random.default_rng(seed)
+    ref = rng.integers(0, 4, rlen).astype(np.uint8)
+    ref[rng.random(rlen) < 0.002] = 4
+    qs, jobs = [], []
+    for k in range(n):
+        L = int(rng.integers(60, 152))
+        kind = k % 6
+        if kind == 5:  # near the sequence ends: windows clipped
+            p = int(rng.integers(0, 40)) if k % 2 else rlen - L - int(rng.integers(0, 40))
+        else:
+            p = int(rng.integers(200, rlen - 400))
+        src = list(ref[p:p + L + 40])
+        q, tr = [], []  # tr[i] = reference offset of query base i (-1: inserted)
+        i = 0
+        sub, ind = (0.01, 0.004) if kind < 3 else (0.05, 0.02)
+        while len(q) < L and i < len(src):
+            u = rng.random()
+            if u < ind / 2:
+                q.append(int(rng.integers(0, 4)))
+                tr.append(-1)
+                continue
+            if u < ind:
+                i += int(rng.integers(1, 4))
+                continue
+            b = int(src[i])
+            if rng.random() < sub:
+                b = (b + 1 + int(rng.integers(0, 3))) % 4
+            q.append(b)
+            tr.append(p + i)
+            i += 1
+        q = np.array(q, np.uint8)
+        if kind == 3:  # unrelated tail: z-drop / local clip
+            cut = int(rng.integers(len(q) // 2, len(q)))
+            q[cut:] = rng.integers(0, 4, len(q) - cut)
+        if kind == 4 and len(q) > 10:
+            q[rng.random(len(q)) < 0.02] = 4
+        # seed: the longest exact-match run of at least 19 bases, by the true mapping
+        best = None
+        j = 0
+        while j < len(q):
+            e = j
+            while (e < len(q) and tr[e] >= 0 and q[e] < 4 and q[e] == ref[tr[e]]
+                   and (e == j or tr[e] == tr[e - 1] + 1)):
+                e += 1
+            if e - j >= 19 and (best is None or e - j > best[1] - best[0]):
+                best = (j, e)
+            j = max(e, j + 1)
+        if best is None:
+            continue
+        sq, se = best
+        if k % 4 == 1:  # part of the run only: seeds not maximal
+            se = sq + max(19, (se - sq) // 2)
+        qs.append(q)
+        jobs.append((sq, tr[sq], se - sq))
+    return ref, qs, jobs
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("w", [100, 20])
+def test_extend_seeds_match_oracle(gpu, w):
+    import host_lib as H
+    ref, qs, jobs = synth_jobs(41 + w, 1200)
+    n = len(jobs)
+    qlen = np.array([len(q) for q in qs], np.int32)
+    qoff = np.concatenate([[0], np.cumsum(qlen[:-1])]).astype(np.int64)
+    qbuf = np.concatenate(qs).astype(np.uint8)
+    sq = np.array([j[0] for j in jobs], np.int32)
+    sr = np.array([j[1] for j in jobs], np.int64)
+    sl = np.array([j[2] for j in jobs], np.int32)
+    cap = (qlen + 4 * w + 64).astype(np.int32)
+    coff = np.concatenate([[0], np.cumsum(cap[:-1])]).astype(np.int64)
+    cig = np.zeros(int(cap.sum()), np.uint32)
+    oi = np.zeros((n, 7), np.int32)
+    orr = np.zeros((n, 2), np.int64)
+    nc = np.zeros(n, np.int32)
+    P = lambda a: a.ctypes.data  # noqa: E731
+    H.check(H.lib.fcsg_extend_seeds(n, vp(P(qbuf)), vp(P(qoff)), vp(P(qlen)), vp(P(ref)), C.c_int64(len(ref)),
+                                    vp(P(sq)), vp(P(sr)), vp(P(sl)), w, 5, 5, 0, vp(P(oi)), vp(P(orr)), vp(P(cig)),
+                                    vp(P(coff)), vp(P(cap)), vp(P(nc))))
+    kinds = set()
+    for i in range(n):
+        e_i, e_r, e_c = oracle(qs[i], ref, int(sq[i]), int(sr[i]), int(sl[i]), w=w)
+        got_c = cig[coff[i]:coff[i] + nc[i]]
+        assert list(oi[i]) == list(e_i) and list(orr[i]) == list(e_r), (i, oi[i], e_i, orr[i], e_r)
+        assert np.array_equal(got_c, e_c), i
+        kinds.add((e_i[0] == 0, e_i[1] == len(qs[i]), e_i[4] > w, e_i[6] == 0))
+    assert len(kinds) >= 5  # local and to-end on both sides, band retries, the no-DP path
