@@ -230,7 +230,7 @@ def bench_e2e(args, rank, local):
     try:
         L = int(args.e2e_mbp * 1e6)
         subprocess.run([exe, "synth", "-o", work + "/d", "-c", f"chr1:{L}", "-x", "30", "--tumor",
-                        "--noisy-frac", "0.01", "--seed", str(args.seed + rank)], env=env, check=True,
+                        "--noisy-frac", "0.01", "--paired", "350", "--seed", str(args.seed + rank)], env=env, check=True,
                        capture_output=True)
         out = {"data": f"synthetic chr1-like {args.e2e_mbp:g} Mbp per GPU, sample 30x, tumor 40x (+1e-4 somatic), "
                        "1% of reads mis-mapped-like (20% high-quality mismatches: their pairs reach the fp64 rescue)"}
@@ -274,12 +274,19 @@ def bench_e2e(args, rank, local):
         dt, logs, _ = timed("mutect2", ["mutect2", "-r", d + "/ref.fasta", "-t", d + "/tumor.bam", "-n",
                                         d + "/sample.bam", "-o", work + "/m2.vcf"])
         out["mutect2"] = shard_stats(logs, dt)
-        dt, _, err = timed("align", ["align", "-r", d + "/ref.fasta", "-1", d + "/sample.fastq", "-o",
-                                     work + "/aln.bam"])
-        m = re.search(r"(\d+) reads, (\d+) mapped, (\d+) extension tasks", err)
+        dt, _, err = timed("align", ["align", "-r", d + "/ref.fasta", "-1", d + "/sample_1.fastq", "-2",
+                                     d + "/sample_2.fastq", "-o", work + "/aln.bam"])
+        m = re.search(r"(\d+) reads, (\d+) mapped, (\d+) extension tasks, (\d+) global alignments, ([\d.]+) s "
+                      r"\(GPU calls ([\d.]+) s\)", err)
+        pm = re.search(r"(\d+) reads properly paired, (\d+) mates rescued, insert ([\d.]+) \+- ([\d.]+)", err)
         n = int(m.group(1)) if m else 0
-        out["align"] = {"reads": n, "ext_tasks": int(m.group(3)) if m else 0, "seconds": round(dt, 3),
-                        "reads_per_s": round(n / dt, 1)}
+        out["align"] = {"mode": "paired-end 2x151, fragments N(350, 50)", "reads": n,
+                        "mapped": int(m.group(2)) if m else 0, "ext_tasks": int(m.group(3)) if m else 0,
+                        "global_tasks": int(m.group(4)) if m else 0,
+                        "gpu_call_seconds": float(m.group(6)) if m else None,
+                        "proper_pair_reads": int(pm.group(1)) if pm else None,
+                        "mates_rescued": int(pm.group(2)) if pm else None,
+                        "seconds": round(dt, 3), "reads_per_s": round(n / dt, 1)}
         return out
     finally:
         shutil.rmtree(work, ignore_errors=True)

@@ -7,6 +7,7 @@
 #include <iostream>
 #include <map>
 #include <thread>
+#include <unordered_map>
 
 #include "common.h"
 #include "config.h"
@@ -56,24 +57,413 @@ void parallel_for(size_t n, int threads, F&& fn) {
   for (auto& x : th) x.join();
 }
 
-// One read's alignment in progress.
-struct Aln {
-  int read = -1;
-  bool rev = false, mapped = false;
+// One candidate placement of a read: a chain's seed (a maximal exact match)
+// and, after the GPU extension round, its alignment.
+struct Cand {
+  bool rev = false;
   int contig = -1;
-  int mapq = 0;
-  std::string seq;            // oriented query bases (revcomp for reverse)
-  std::vector<uint8_t> q;     // codes of seq
-  std::vector<uint8_t> qual;  // oriented quals
-  int64_t seed_r = 0;         // contig offset of the seed start
+  int hits = 0;  // k-mer hits of the chain
   int seed_q = 0, seed_len = 0;
-  int score = 0, truesc = 0;
-  int qb = 0, qe = 0;
-  int64_t rb = 0, re = 0;
-  std::vector<uint32_t> cigar;
-  int nm = 0;
-  std::string md;
+  int64_t seed_r = 0;
+  SeedAln aln;
+  bool done = false;  // extended
+  bool ok = false;    // extension produced an alignment with a CIGAR
 };
+
+// One read: both orientations and its candidates.
+struct ReadAln {
+  std::string seq[2];            // forward, reverse complement
+  std::vector<uint8_t> code[2];  // codes of seq[]
+  std::vector<Cand> cands;
+  int best = -1;      // index into cands of the primary alignment
+  int sub = 0;        // best score of another locus (bwa's a->sub), 0 if none
+  int sub_n = 0;      // other loci scoring close to the best
+  int mapq = 0;
+};
+
+// bwa mem_approx_mapq_se (MEM_MAPQ_COEF 30, mapQ_coef_len 0): the primary's
+// score against the best other locus, scaled by the seed coverage and identity.
+int approx_mapq_se(const SeedAln& a, int sub, int sub_n, int seedcov, int min_seed_len, int match, int mismatch) {
+  sub = sub ? sub : min_seed_len * match;
+  if (sub >= a.truesc || a.truesc <= 0) return 0;
+  const int l = std::max(a.qe - a.qb, (int)(a.re - a.rb));
+  const double identity = 1. - (double)(l * match - a.truesc) / (match + mismatch) / l;
+  int mapq = (int)(30.0 * (1. - (double)sub / a.truesc) * std::log((double)std::max(seedcov, 1)) + .499);
+  if (identity < 0.95) mapq = (int)(mapq * identity * identity + .499);
+  if (sub_n > 0) mapq -= (int)(4.343 * std::log((double)sub_n + 1) + .499);
+  return std::max(0, std::min(60, mapq));
+}
+
+int64_t aln_pos(const Cand& c) { return c.aln.rb; }
+int64_t aln_end(const Cand& c) { return c.aln.re; }
+
+// Seeds and chains of one read (both strands): k-mer hits every seed_step
+// bases, chains = runs of diagonals within 8 of each other; up to
+// max_chains chains with at least drop_ratio x the best chain's hits, each
+// represented by the earliest hit on its most supported diagonal, grown to a
+// maximal exact match.
+void seed_read(const Reference& ref, const KmerIndex& idx, const AlignOptions& opt, ReadAln& R) {
+  const int k = idx.k();
+  const uint64_t kmask = (1ull << (2 * k)) - 1;
+  struct Hit {
+    int64_t d;
+    int qp;
+    uint64_t g;
+  };
+  struct Chain {
+    int n;
+    bool rev;
+    int qp;
+    uint64_t g;
+  };
+  std::vector<Chain> chains;
+  std::vector<Hit> hits;
+  for (int strand = 0; strand < 2; ++strand) {
+    const std::vector<uint8_t>& c = R.code[strand];
+    hits.clear();
+    for (int qp = 0; qp + k <= (int)c.size(); qp += opt.seed_step) {
+      uint64_t key = 0;
+      bool ok = true;
+      for (int i = 0; i < k && ok; ++i) {
+        if (c[qp + i] > 3) ok = false;
+        key = ((key << 2) | c[qp + i]) & kmask;
+      }
+      if (!ok) continue;
+      const auto [b, e] = idx.lookup(key);
+      if (e - b == 0 || e - b > opt.max_occ) continue;
+      for (const uint64_t* p = b; p != e; ++p) hits.push_back({(int64_t)*p - qp, qp, *p});
+    }
+    std::sort(hits.begin(), hits.end(), [](const Hit& x, const Hit& y) { return x.d != y.d ? x.d < y.d : x.qp < y.qp; });
+    size_t i = 0;
+    while (i < hits.size()) {
+      size_t j = i;
+      int n = 0, dn_best = 0;
+      const Hit* seed = &hits[i];
+      while (j < hits.size() && (j == i || hits[j].d - hits[j - 1].d <= 8)) {
+        size_t e = j;
+        while (e < hits.size() && hits[e].d == hits[j].d) ++e;  // one diagonal
+        if ((int)(e - j) > dn_best) {
+          dn_best = (int)(e - j);
+          seed = &hits[j];
+        }
+        n += (int)(e - j);
+        j = e;
+      }
+      chains.push_back({n, strand != 0, seed->qp, seed->g});
+      i = j;
+    }
+  }
+  if (chains.empty()) return;
+  std::stable_sort(chains.begin(), chains.end(), [](const Chain& a, const Chain& b) { return a.n > b.n; });
+  const int best_n = chains[0].n;
+  for (const Chain& ch : chains) {
+    if ((int)R.cands.size() >= opt.max_chains || ch.n < opt.drop_ratio * best_n) break;
+    Cand C;
+    C.rev = ch.rev;
+    C.hits = ch.n;
+    int64_t off = 0;
+    C.contig = idx.contig_of(ch.g, off);
+    const std::vector<uint8_t>& rc = idx.codes(C.contig);
+    const std::vector<uint8_t>& q = R.code[ch.rev];
+    int qs = ch.qp, qe = ch.qp + k;
+    int64_t rs = off;
+    while (qs > 0 && rs > 0 && q[qs - 1] < 4 && q[qs - 1] == rc[rs - 1]) --qs, --rs;
+    while (qe < (int)q.size() && rs + (qe - qs) < (int64_t)rc.size() && q[qe] < 4 && q[qe] == rc[rs + (qe - qs)]) ++qe;
+    C.seed_q = qs;
+    C.seed_len = qe - qs;
+    C.seed_r = rs;
+    R.cands.push_back(std::move(C));
+  }
+}
+
+// One GPU extension round over every pending candidate of `reads`.
+void extend_cands(const KmerIndex& idx, const fcs_bsw_params& P, const AlignOptions& opt, std::vector<ReadAln*>& reads,
+                  bool only_new, AlignStats& st) {
+  std::vector<SeedJob> jobs;
+  std::vector<Cand*> who;
+  for (ReadAln* R : reads)
+    for (Cand& C : R->cands) {
+      if (only_new && C.done) continue;
+      const std::vector<uint8_t>& rc = idx.codes(C.contig);
+      SeedJob J;
+      J.q = R->code[C.rev].data();
+      J.qlen = (int)R->code[C.rev].size();
+      J.ref = rc.data();
+      J.rlen = (int64_t)rc.size();
+      J.seed_q = C.seed_q;
+      J.seed_r = C.seed_r;
+      J.seed_len = C.seed_len;
+      jobs.push_back(J);
+      who.push_back(&C);
+    }
+  if (jobs.empty()) return;
+  SeedExtOptions so;
+  so.w = opt.w;
+  so.pen_clip5 = so.pen_clip3 = P.end_bonus;
+  so.gpu = opt.gpu;
+  std::vector<SeedAln> res;
+  SeedExtStats xs;
+  extend_seeds(jobs, P, so, res, xs);
+  st.ext_tasks += xs.ext_tasks;
+  st.global_tasks += xs.global_tasks;
+  st.gpu_seconds += xs.gpu_seconds;
+  for (size_t i = 0; i < who.size(); ++i) {
+    Cand& C = *who[i];
+    C.aln = std::move(res[i]);
+    C.done = true;
+    C.ok = C.aln.qe > C.aln.qb && C.aln.re > C.aln.rb && !C.aln.cigar.empty();
+  }
+}
+
+// Primary alignment, the best other locus (bwa's sub) and the single-end MAPQ.
+void pick_primary(ReadAln& R, const AlignOptions& opt) {
+  R.best = -1;
+  for (int i = 0; i < (int)R.cands.size(); ++i) {
+    const Cand& C = R.cands[i];
+    if (!C.ok) continue;
+    if (R.best < 0 || C.aln.truesc > R.cands[R.best].aln.truesc ||
+        (C.aln.truesc == R.cands[R.best].aln.truesc && C.hits > R.cands[R.best].hits))
+      R.best = i;
+  }
+  R.sub = 0;
+  R.sub_n = 0;
+  R.mapq = 0;
+  if (R.best < 0) return;
+  const Cand& B = R.cands[R.best];
+  const int L = (int)R.code[0].size();
+  for (int i = 0; i < (int)R.cands.size(); ++i) {
+    const Cand& C = R.cands[i];
+    if (i == R.best || !C.ok) continue;
+    const bool same_locus = C.contig == B.contig && C.rev == B.rev && std::llabs(C.aln.rb - B.aln.rb) < L / 2;
+    if (same_locus) continue;
+    R.sub = std::max(R.sub, C.aln.truesc);
+    if (C.aln.truesc >= B.aln.truesc - 5) ++R.sub_n;  // bwa: other hits within the mapQ_coef window
+  }
+  R.mapq = approx_mapq_se(B.aln, R.sub, R.sub_n, B.seed_len, opt.k, 1, 4);
+}
+
+// Insert-size distribution of one batch (bwa mem_pestat, FR orientation):
+// quartiles of the fragment lengths of confidently placed pairs; proper pairs
+// lie in [p25 - 3 IQR, p75 + 3 IQR] (at least mean +- 4 sd), mean / sd over the
+// values within [p25 - 2 IQR, p75 + 2 IQR].
+struct PeStat {
+  bool ok = false;
+  int low = 0, high = 0;
+  double avg = 0, std = 1;
+  int n = 0;
+};
+
+int64_t frag_len(const Cand& a, const Cand& b) {
+  return std::max(aln_end(a), aln_end(b)) - std::min(aln_pos(a), aln_pos(b));
+}
+
+bool fr_pair(const Cand& a, const Cand& b) {
+  if (a.contig != b.contig || a.rev == b.rev) return false;
+  const Cand& f = a.rev ? b : a;  // forward mate starts at the left
+  const Cand& r = a.rev ? a : b;
+  return aln_pos(f) <= aln_pos(r) && aln_end(f) <= aln_end(r) + 16;
+}
+
+PeStat pestat(const std::vector<ReadAln>& m1, const std::vector<ReadAln>& m2) {
+  PeStat ps;
+  std::vector<int64_t> v;
+  for (size_t i = 0; i < m1.size(); ++i) {
+    const ReadAln &a = m1[i], &b = m2[i];
+    if (a.best < 0 || b.best < 0 || a.mapq < 20 || b.mapq < 20) continue;
+    const Cand &x = a.cands[a.best], &y = b.cands[b.best];
+    if (!fr_pair(x, y)) continue;
+    const int64_t f = frag_len(x, y);
+    if (f > 0 && f < 10000) v.push_back(f);
+  }
+  ps.n = (int)v.size();
+  if (v.size() < 25) return ps;  // bwa: too few pairs to estimate
+  std::sort(v.begin(), v.end());
+  const double p25 = (double)v[(size_t)(.25 * v.size() + .499)], p75 = (double)v[(size_t)(.75 * v.size() + .499)];
+  const double iqr = p75 - p25;
+  const double lo2 = p25 - 2. * iqr, hi2 = p75 + 2. * iqr;
+  double s = 0, s2 = 0;
+  int n = 0;
+  for (int64_t x : v)
+    if (x >= lo2 && x <= hi2) s += (double)x, s2 += (double)x * (double)x, ++n;
+  ps.avg = s / n;
+  ps.std = std::sqrt(std::max(1e-9, s2 / n - ps.avg * ps.avg));
+  ps.low = (int)(p25 - 3. * iqr + .499);
+  ps.high = (int)(p75 + 3. * iqr + .499);
+  if (ps.low > ps.avg - 4. * ps.std) ps.low = (int)(ps.avg - 4. * ps.std + .499);
+  if (ps.high < ps.avg + 4. * ps.std) ps.high = (int)(ps.avg + 4. * ps.std + .499);
+  ps.low = std::max(ps.low, 1);
+  ps.ok = true;
+  return ps;
+}
+
+// bwa mem_pair's insert-size log-likelihood term in score units.
+int pair_penalty(const PeStat& ps, int64_t dist, int match) {
+  const double ns = ((double)dist - ps.avg) / ps.std;
+  return (int)(.721 * std::log(2. * std::erfc(std::fabs(ns) * M_SQRT1_2)) * match + .499);
+}
+
+// Mate rescue (bwa mem_matesw's role): the mate is searched in the window the
+// insert-size distribution allows opposite `anchor`, on the other strand, by
+// 12-mer exact hits of the window; the best-supported diagonal becomes a seed
+// for the regular extension round.  Returns false when nothing seeds.
+bool rescue_seed(const KmerIndex& idx, const PeStat& ps, const Cand& anchor, ReadAln& mate) {
+  const int kk = 12;
+  const std::vector<uint8_t>& rc = idx.codes(anchor.contig);
+  const int64_t L = (int64_t)mate.code[0].size();
+  const bool rev = !anchor.rev;
+  int64_t wb, we;
+  if (!anchor.rev) {  // anchor forward at the left: the mate ends within [pos + low, pos + high]
+    wb = aln_pos(anchor) + ps.low - L;
+    we = aln_pos(anchor) + ps.high;
+  } else {  // anchor reverse at the right: the mate starts within [end - high, end - low]
+    wb = aln_end(anchor) - ps.high;
+    we = aln_end(anchor) - ps.low + L;
+  }
+  wb = std::max<int64_t>(0, wb);
+  we = std::min<int64_t>((int64_t)rc.size(), we);
+  if (we - wb < kk || we - wb > 100000) return false;
+  std::unordered_multimap<uint32_t, int64_t> win;
+  win.reserve((size_t)(we - wb));
+  uint32_t key = 0;
+  int valid = 0;
+  const uint32_t mask = (1u << (2 * kk)) - 1;
+  for (int64_t p = wb; p < we; ++p) {
+    if (rc[p] > 3) {
+      valid = 0;
+      continue;
+    }
+    key = ((key << 2) | rc[p]) & mask;
+    if (++valid >= kk) win.emplace(key, p - kk + 1);
+  }
+  const std::vector<uint8_t>& q = mate.code[rev];
+  std::map<int64_t, std::pair<int, int>> diag;  // diagonal -> (hits, first query pos)
+  key = 0;
+  valid = 0;
+  for (int i = 0; i < (int)q.size(); ++i) {
+    if (q[i] > 3) {
+      valid = 0;
+      continue;
+    }
+    key = ((key << 2) | q[i]) & mask;
+    if (++valid < kk) continue;
+    const int qp = i - kk + 1;
+    auto range = win.equal_range(key);
+    for (auto it = range.first; it != range.second; ++it) {
+      auto& d = diag[it->second - qp];
+      if (d.first++ == 0) d.second = qp;
+    }
+  }
+  int best = 0;
+  int64_t bd = 0;
+  int bq = 0;
+  for (const auto& [d, h] : diag)
+    if (h.first > best) best = h.first, bd = d, bq = h.second;
+  if (best < 2) return false;
+  Cand C;
+  C.rev = rev;
+  C.contig = anchor.contig;
+  C.hits = best;
+  int qs = bq, qe = bq + kk;
+  int64_t rs = bd + bq;
+  while (qs > 0 && rs > 0 && q[qs - 1] < 4 && q[qs - 1] == rc[rs - 1]) --qs, --rs;
+  while (qe < (int)q.size() && rs + (qe - qs) < (int64_t)rc.size() && q[qe] < 4 && q[qe] == rc[rs + (qe - qs)]) ++qe;
+  C.seed_q = qs;
+  C.seed_len = qe - qs;
+  C.seed_r = rs;
+  mate.cands.push_back(std::move(C));
+  return true;
+}
+
+// The BAM record of one read: its primary alignment (soft clips, NM / MD /
+// AS) or an unmapped record.
+BamRecord make_record(const Reference& ref, const ReadAln& R, const std::string& name, const std::string& fq_seq,
+                      const std::string& fq_qual, const AlignOptions& opt) {
+  BamRecord rec;
+  rec.name = name;
+  rec.set_aux_string("RG", opt.rg);
+  auto quals = [&](bool rev) {
+    std::vector<uint8_t> q(fq_seq.size());
+    for (size_t i = 0; i < q.size(); ++i) {
+      const size_t j = rev ? q.size() - 1 - i : i;
+      q[i] = (uint8_t)(j < fq_qual.size() ? std::max(0, fq_qual[j] - 33) : 30);
+    }
+    return q;
+  };
+  if (R.best < 0) {
+    rec.flag = kUnmapped;
+    rec.seq = fq_seq;
+    rec.qual = quals(false);
+    return rec;
+  }
+  const Cand& C = R.cands[R.best];
+  const SeedAln& A = C.aln;
+  const std::vector<uint8_t>& q = R.code[C.rev];
+  std::vector<uint32_t> cig;
+  if (A.qb > 0) cig.push_back(cigar_pack((uint32_t)A.qb, kS));
+  for (uint32_t c : A.cigar) {
+    const uint32_t op = c & 0xf;  // ksw ops: 0 = M, 1 = I, 2 = D
+    cig.push_back(cigar_pack(c >> 4, op == 0 ? kM : op == 1 ? kI : kD));
+  }
+  if (A.qe < (int)q.size()) cig.push_back(cigar_pack((uint32_t)(q.size() - A.qe), kS));
+  const std::string& Rs = ref.contigs[C.contig].seq;
+  int nm = 0, run = 0;
+  std::string md;
+  int qi = A.qb;
+  int64_t ri = A.rb;
+  for (uint32_t c : A.cigar) {
+    const uint32_t len = c >> 4, op = c & 0xf;
+    if (op == 0) {
+      for (uint32_t j = 0; j < len; ++j, ++qi, ++ri) {
+        if (q[qi] != code_of(Rs[ri]) || q[qi] > 3) {
+          ++nm;
+          md += std::to_string(run);
+          md += Rs[ri];
+          run = 0;
+        } else {
+          ++run;
+        }
+      }
+    } else if (op == 1) {
+      nm += (int)len;
+      qi += (int)len;
+    } else {
+      nm += (int)len;
+      md += std::to_string(run) + "^" + Rs.substr(ri, len);
+      run = 0;
+      ri += len;
+    }
+  }
+  md += std::to_string(run);
+  rec.ref_id = C.contig;
+  rec.pos = (int32_t)A.rb;
+  rec.mapq = (uint8_t)R.mapq;
+  rec.flag = C.rev ? kReverse : 0;
+  rec.cigar = cig;
+  rec.seq = R.seq[C.rev];
+  rec.qual = quals(C.rev);
+  rec.set_aux_int("NM", nm);
+  rec.set_aux_string("MD", md);
+  rec.set_aux_int("AS", A.truesc);
+  return rec;
+}
+
+// Seeds, chains and the GPU extension round for a batch of reads.
+void align_batch(const Reference& ref, const KmerIndex& idx, const std::vector<std::string>& seqs,
+                 const AlignOptions& opt, std::vector<ReadAln>& reads, AlignStats& st) {
+  reads.assign(seqs.size(), ReadAln{});
+  parallel_for(seqs.size(), opt.threads, [&](size_t r) {
+    ReadAln& R = reads[r];
+    R.seq[0] = seqs[r];
+    R.seq[1] = revcomp(seqs[r]);
+    R.code[0] = encode(R.seq[0]);
+    R.code[1] = encode(R.seq[1]);
+    seed_read(ref, idx, opt, R);
+  });
+  std::vector<ReadAln*> ptr;
+  for (ReadAln& R : reads) ptr.push_back(&R);
+  extend_cands(idx, st.params, opt, ptr, false, st);
+  parallel_for(reads.size(), opt.threads, [&](size_t r) { pick_primary(reads[r], opt); });
+}
 
 }  // namespace
 
@@ -128,211 +518,133 @@ AlignStats align_reads(const Reference& ref, const KmerIndex& idx, const std::ve
                        const std::vector<std::string>& seqs, const std::vector<std::string>& quals,
                        const AlignOptions& opt, std::vector<BamRecord>& out) {
   AlignStats st;
+  fcs_bsw_params_default(&st.params);
   const uint64_t t0 = now_us();
-  fcs_bsw_params P;
-  fcs_bsw_params_default(&P);
-  const int k = idx.k();
-  const uint64_t kmask = (1ull << (2 * k)) - 1;
-  std::vector<Aln> alns(seqs.size());
-
-  // ---- seeds and the best chain per read (host threads over reads)
+  std::vector<ReadAln> reads;
+  align_batch(ref, idx, seqs, opt, reads, st);
   st.reads = (int64_t)seqs.size();
-  auto seed_read = [&](size_t r) {
-    Aln& A = alns[r];
-    A.read = (int)r;
-    struct Hit {
-      int64_t d;
-      int qp;
-      uint64_t g;
-    };
-    std::vector<Hit> hits;
-    int best_hits = 0, second_hits = 0, best_qp = 0;
-    uint64_t best_g = 0;
-    bool best_rev = false;
-    for (int strand = 0; strand < 2; ++strand) {
-      const std::string s = strand ? revcomp(seqs[r]) : seqs[r];
-      const std::vector<uint8_t> c = encode(s);
-      hits.clear();
-      for (int qp = 0; qp + k <= (int)c.size(); qp += opt.seed_step) {
-        uint64_t key = 0;
-        bool ok = true;
-        for (int i = 0; i < k && ok; ++i) {
-          if (c[qp + i] > 3) ok = false;
-          key = ((key << 2) | c[qp + i]) & kmask;
-        }
-        if (!ok) continue;
-        const auto [b, e] = idx.lookup(key);
-        if (e - b == 0 || e - b > opt.max_occ) continue;
-        for (const uint64_t* p = b; p != e; ++p) hits.push_back({(int64_t)*p - qp, qp, *p});
-      }
-      // chains: diagonals within 8 of the previous one (indels shift them);
-      // a chain's seed is its earliest hit on its most supported diagonal
-      std::sort(hits.begin(), hits.end(), [](const Hit& x, const Hit& y) { return x.d != y.d ? x.d < y.d : x.qp < y.qp; });
-      size_t i = 0;
-      while (i < hits.size()) {
-        size_t j = i;
-        int n = 0, dn_best = 0;
-        const Hit* seed = &hits[i];
-        while (j < hits.size() && (j == i || hits[j].d - hits[j - 1].d <= 8)) {
-          size_t e = j;
-          while (e < hits.size() && hits[e].d == hits[j].d) ++e;  // one diagonal
-          if ((int)(e - j) > dn_best) {
-            dn_best = (int)(e - j);
-            seed = &hits[j];
-          }
-          n += (int)(e - j);
-          j = e;
-        }
-        if (n > best_hits) {
-          second_hits = best_hits;
-          best_hits = n;
-          best_rev = strand;
-          best_qp = seed->qp;
-          best_g = seed->g;
-        } else if (n > second_hits) {
-          second_hits = n;
-        }
-        i = j;
-      }
-    }
-    if (best_hits == 0) return;
-    A.rev = best_rev;
-    A.seq = best_rev ? revcomp(seqs[r]) : seqs[r];
-    A.q = encode(A.seq);
-    A.qual.resize(A.seq.size());
-    for (size_t i = 0; i < A.seq.size(); ++i) {
-      const size_t j = best_rev ? A.seq.size() - 1 - i : i;
-      A.qual[i] = (uint8_t)(j < quals[r].size() ? std::max(0, quals[r][j] - 33) : 30);
-    }
-    int64_t off = 0;
-    A.contig = idx.contig_of(best_g, off);
-    const std::string& R = ref.contigs[A.contig].seq;
-    // grow the k-mer hit to a maximal exact match
-    int qs = best_qp, qe = best_qp + k;
-    int64_t rs = off;
-    while (qs > 0 && rs > 0 && A.q[qs - 1] < 4 && A.q[qs - 1] == code_of(R[rs - 1])) --qs, --rs;
-    while (qe < (int)A.q.size() && rs + (qe - qs) < (int64_t)R.size() && A.q[qe] < 4 &&
-           A.q[qe] == code_of(R[rs + (qe - qs)]))
-      ++qe;
-    A.seed_q = qs;
-    A.seed_len = qe - qs;
-    A.seed_r = rs;
-    A.mapped = true;
-    A.mapq = second_hits >= best_hits ? 0 : std::min(60, (int)std::lround(60.0 * (best_hits - second_hits) / best_hits));
-  };
-  parallel_for(seqs.size(), opt.threads, seed_read);
+  const size_t base = out.size();
+  out.resize(base + reads.size());
+  parallel_for(reads.size(), opt.threads,
+               [&](size_t i) { out[base + i] = make_record(ref, reads[i], names[i], seqs[i], quals[i], opt); });
+  for (const ReadAln& R : reads) st.mapped += R.best >= 0;
+  st.seconds = (now_us() - t0) / 1e6;
+  return st;
+}
 
-  // ---- bwa's extension protocol on the GPU (host/seedext.cpp): left and right
-  // extensions with band retry, local vs to-end, CIGARs by banded global alignment
-  {
-    std::vector<SeedJob> jobs;
-    std::vector<int> who;
-    for (Aln& A : alns) {
-      if (!A.mapped) continue;
-      const std::vector<uint8_t>& R = idx.codes(A.contig);
-      SeedJob J;
-      J.q = A.q.data();
-      J.qlen = (int)A.q.size();
-      J.ref = R.data();
-      J.rlen = (int64_t)R.size();
-      J.seed_q = A.seed_q;
-      J.seed_r = A.seed_r;
-      J.seed_len = A.seed_len;
-      jobs.push_back(J);
-      who.push_back(A.read);
-    }
-    SeedExtOptions so;
-    so.w = opt.w;
-    so.pen_clip5 = so.pen_clip3 = P.end_bonus;
-    so.gpu = opt.gpu;
-    std::vector<SeedAln> res;
-    SeedExtStats xs;
-    extend_seeds(jobs, P, so, res, xs);
-    st.ext_tasks += xs.ext_tasks;
-    st.global_tasks += xs.global_tasks;
-    st.gpu_seconds += xs.gpu_seconds;
-    for (size_t i = 0; i < who.size(); ++i) {
-      Aln& A = alns[who[i]];
-      SeedAln& x = res[i];
-      A.qb = x.qb;
-      A.qe = x.qe;
-      A.rb = x.rb;
-      A.re = x.re;
-      A.score = x.score;
-      A.truesc = x.truesc;
-      A.cigar.swap(x.cigar);
-      if (A.qe <= A.qb || A.re <= A.rb) A.mapped = false;
+AlignStats align_pairs(const Reference& ref, const KmerIndex& idx, const std::vector<std::string>& names,
+                       const std::vector<std::string>& seqs1, const std::vector<std::string>& quals1,
+                       const std::vector<std::string>& seqs2, const std::vector<std::string>& quals2,
+                       const AlignOptions& opt, std::vector<BamRecord>& out) {
+  AlignStats st;
+  fcs_bsw_params_default(&st.params);
+  const uint64_t t0 = now_us();
+  const size_t n = names.size();
+  if (seqs1.size() != n || seqs2.size() != n) throw invalidParam("align_pairs: mate lists differ in length");
+  // both mates in one batch: one GPU extension round for all
+  std::vector<std::string> both(seqs1);
+  both.insert(both.end(), seqs2.begin(), seqs2.end());
+  std::vector<ReadAln> all;
+  align_batch(ref, idx, both, opt, all, st);
+  std::vector<ReadAln> m1(std::make_move_iterator(all.begin()), std::make_move_iterator(all.begin() + n));
+  std::vector<ReadAln> m2(std::make_move_iterator(all.begin() + n), std::make_move_iterator(all.end()));
+  all.clear();
+  const PeStat ps = pestat(m1, m2);
+  st.pe_pairs = ps.n;
+  st.pe_low = ps.low;
+  st.pe_high = ps.high;
+  st.pe_avg = ps.avg;
+  st.pe_std = ps.std;
+  // mate rescue: a confidently placed mate whose partner has no alignment in the
+  // allowed window gets the window searched for the partner
+  if (ps.ok) {
+    std::vector<ReadAln*> resc;
+    for (size_t i = 0; i < n; ++i)
+      for (int side = 0; side < 2; ++side) {
+        ReadAln& a = side ? m2[i] : m1[i];
+        ReadAln& b = side ? m1[i] : m2[i];
+        if (a.best < 0 || a.mapq < 20) continue;
+        const Cand& A = a.cands[a.best];
+        bool have = false;
+        for (const Cand& C : b.cands)
+          if (C.ok && fr_pair(A, C) && frag_len(A, C) >= ps.low && frag_len(A, C) <= ps.high) have = true;
+        if (have) continue;
+        if (rescue_seed(idx, ps, A, b)) resc.push_back(&b);
+      }
+    std::sort(resc.begin(), resc.end());
+    resc.erase(std::unique(resc.begin(), resc.end()), resc.end());
+    st.rescued = (int64_t)resc.size();
+    extend_cands(idx, st.params, opt, resc, true, st);
+  }
+  // pairing (bwa mem_pair): the best FR combination within [low, high] by
+  // score + insert-size log-likelihood, against the unpaired best - pen_unpaired
+  const int pen_unpaired = 17;
+  std::vector<char> proper(n, 0);
+  for (size_t i = 0; i < n; ++i) {
+    ReadAln &a = m1[i], &b = m2[i];
+    pick_primary(a, opt);
+    pick_primary(b, opt);
+    if (!ps.ok) continue;
+    int bi = -1, bj = -1, best = INT32_MIN, second = INT32_MIN;
+    for (int x = 0; x < (int)a.cands.size(); ++x)
+      for (int y = 0; y < (int)b.cands.size(); ++y) {
+        const Cand &A = a.cands[x], &B = b.cands[y];
+        if (!A.ok || !B.ok || !fr_pair(A, B)) continue;
+        const int64_t f = frag_len(A, B);
+        if (f < ps.low || f > ps.high) continue;
+        const int s = A.aln.truesc + B.aln.truesc + pair_penalty(ps, f, 1);
+        if (s > best) second = best, best = s, bi = x, bj = y;
+        else if (s > second) second = s;
+      }
+    if (bi < 0) continue;
+    const int unpaired = (a.best >= 0 ? a.cands[a.best].aln.truesc : 0) +
+                         (b.best >= 0 ? b.cands[b.best].aln.truesc : 0) - pen_unpaired;
+    if (best < unpaired) continue;
+    proper[i] = 1;
+    const int q_pe = second == INT32_MIN ? 60 : std::min(60, (int)(6.02 * (best - second) + .499));
+    for (int side = 0; side < 2; ++side) {
+      ReadAln& r = side ? b : a;
+      const int pick = side ? bj : bi;
+      const int q_se = pick == r.best ? r.mapq : 0;
+      r.best = pick;
+      r.mapq = std::max(q_se, std::min(q_pe, q_se + 40));
     }
   }
-
-  // ---- records (host threads; one slot per read keeps the input order)
   const size_t base = out.size();
-  out.resize(base + alns.size());
-  std::vector<char> mapped_flag(alns.size(), 0);
-  parallel_for(alns.size(), opt.threads, [&](size_t ai) {
-    Aln& A = alns[ai];
-    BamRecord& rec = out[base + ai];
-    rec.name = names[A.read];
-    rec.set_aux_string("RG", opt.rg);
-    if (!A.mapped || A.cigar.empty()) {
-      rec.flag = kUnmapped;
-      rec.seq = seqs[A.read];
-      rec.qual.resize(rec.seq.size());
-      for (size_t i = 0; i < rec.seq.size(); ++i)
-        rec.qual[i] = (uint8_t)(i < quals[A.read].size() ? std::max(0, quals[A.read][i] - 33) : 30);
-      return;
+  out.resize(base + 2 * n);
+  parallel_for(n, opt.threads, [&](size_t i) {
+    BamRecord r1 = make_record(ref, m1[i], names[i], seqs1[i], quals1[i], opt);
+    BamRecord r2 = make_record(ref, m2[i], names[i], seqs2[i], quals2[i], opt);
+    r1.flag |= kPaired | kRead1;
+    r2.flag |= kPaired | kRead2;
+    const bool u1 = r1.flag & kUnmapped, u2 = r2.flag & kUnmapped;
+    if (!u1 && u2) r2.ref_id = r1.ref_id, r2.pos = r1.pos;  // SAM: an unmapped mate takes its partner's place
+    if (u1 && !u2) r1.ref_id = r2.ref_id, r1.pos = r2.pos;
+    auto link = [](BamRecord& x, const BamRecord& y) {
+      x.next_ref_id = y.ref_id;
+      x.next_pos = y.pos;
+      if (y.flag & kUnmapped) x.flag |= kMateUnmapped;
+      if (y.flag & kReverse) x.flag |= kMateReverse;
+    };
+    link(r1, r2);
+    link(r2, r1);
+    if (proper[i]) {
+      r1.flag |= kProperPair;
+      r2.flag |= kProperPair;
     }
-    mapped_flag[ai] = 1;
-    std::vector<uint32_t> cig;
-    if (A.qb > 0) cig.push_back(cigar_pack((uint32_t)A.qb, kS));
-    for (uint32_t c : A.cigar) {
-      // ksw ops: 0 = M, 1 = I, 2 = D
-      const uint32_t op = c & 0xf;
-      cig.push_back(cigar_pack(c >> 4, op == 0 ? kM : op == 1 ? kI : kD));
+    if (!u1 && !u2 && r1.ref_id == r2.ref_id) {  // TLEN: leftmost to rightmost mapped base, signed
+      const int64_t b = std::min<int64_t>(r1.pos, r2.pos), e = std::max(r1.end(), r2.end());
+      const int32_t t = (int32_t)(e - b);
+      const bool first = r1.pos < r2.pos || (r1.pos == r2.pos && !(r1.flag & kReverse));
+      r1.tlen = first ? t : -t;
+      r2.tlen = first ? -t : t;
     }
-    if (A.qe < (int)A.q.size()) cig.push_back(cigar_pack((uint32_t)(A.q.size() - A.qe), kS));
-    // NM / MD over the aligned part
-    const std::string& R = ref.contigs[A.contig].seq;
-    int nm = 0, run = 0;
-    std::string md;
-    int qi = A.qb;
-    int64_t ri = A.rb;
-    for (uint32_t c : A.cigar) {
-      const uint32_t len = c >> 4, op = c & 0xf;
-      if (op == 0) {
-        for (uint32_t j = 0; j < len; ++j, ++qi, ++ri) {
-          if (A.q[qi] != code_of(R[ri]) || A.q[qi] > 3) {
-            ++nm;
-            md += std::to_string(run);
-            md += R[ri];
-            run = 0;
-          } else {
-            ++run;
-          }
-        }
-      } else if (op == 1) {
-        nm += (int)len;
-        qi += (int)len;
-      } else {
-        nm += (int)len;
-        md += std::to_string(run) + "^" + R.substr(ri, len);
-        run = 0;
-        ri += len;
-      }
-    }
-    md += std::to_string(run);
-    rec.ref_id = A.contig;
-    rec.pos = (int32_t)A.rb;
-    rec.mapq = (uint8_t)A.mapq;
-    rec.flag = A.rev ? kReverse : 0;
-    rec.cigar = cig;
-    rec.seq = A.seq;
-    rec.qual = A.qual;
-    rec.set_aux_int("NM", nm);
-    rec.set_aux_string("MD", md);
-    rec.set_aux_int("AS", A.truesc);
+    out[base + 2 * i] = std::move(r1);
+    out[base + 2 * i + 1] = std::move(r2);
   });
-  for (char m : mapped_flag) st.mapped += m;
+  for (size_t i = 0; i < n; ++i) st.mapped += (m1[i].best >= 0) + (m2[i].best >= 0);
+  for (size_t i = 0; i < n; ++i) st.proper += 2 * proper[i];
+  st.reads = 2 * (int64_t)n;
   st.seconds = (now_us() - t0) / 1e6;
   return st;
 }
@@ -404,22 +716,25 @@ int align_main(int argc, char** argv) {
   const KmerIndex idx(ref, opt.k);
   std::vector<BamRecord> recs;
   AlignStats tot;
-  for (int mate = 0; mate < (fq2.empty() ? 1 : 2); ++mate) {
-    std::ifstream in(mate ? fq2 : fq1);
+  auto add = [&](const AlignStats& st) {
+    tot.reads += st.reads;
+    tot.mapped += st.mapped;
+    tot.proper += st.proper;
+    tot.rescued += st.rescued;
+    tot.seconds += st.seconds;
+    tot.gpu_seconds += st.gpu_seconds;
+    tot.ext_tasks += st.ext_tasks;
+    tot.global_tasks += st.global_tasks;
+    if (st.pe_pairs) tot.pe_pairs = st.pe_pairs, tot.pe_low = st.pe_low, tot.pe_high = st.pe_high,
+                     tot.pe_avg = st.pe_avg, tot.pe_std = st.pe_std;
+  };
+  if (fq2.empty()) {
+    std::ifstream in(fq1);
     std::vector<std::string> names, seqs, quals;
     std::string n, s, q;
     auto flush = [&] {
       if (names.empty()) return;
-      const size_t first = recs.size();
-      const AlignStats st = align_reads(ref, idx, names, seqs, quals, opt, recs);
-      if (!fq2.empty())
-        for (size_t i = first; i < recs.size(); ++i) recs[i].flag |= kPaired | (mate ? kRead2 : kRead1);
-      tot.reads += st.reads;
-      tot.mapped += st.mapped;
-      tot.seconds += st.seconds;
-      tot.gpu_seconds += st.gpu_seconds;
-      tot.ext_tasks += st.ext_tasks;
-      tot.global_tasks += st.global_tasks;
+      add(align_reads(ref, idx, names, seqs, quals, opt, recs));
       names.clear();
       seqs.clear();
       quals.clear();
@@ -429,6 +744,28 @@ int align_main(int argc, char** argv) {
       seqs.push_back(s);
       quals.push_back(q);
       if ((int)names.size() >= opt.chunk_size) flush();
+    }
+    flush();
+  } else {  // paired: both files in lockstep, bwa's per-batch insert-size estimate
+    std::ifstream in1(fq1), in2(fq2);
+    std::vector<std::string> names, s1, q1, s2, q2;
+    std::string n1, a1, b1, n2, a2, b2;
+    auto flush = [&] {
+      if (names.empty()) return;
+      add(align_pairs(ref, idx, names, s1, q1, s2, q2, opt, recs));
+      for (auto* v : {&names, &s1, &q1, &s2, &q2}) v->clear();
+    };
+    for (;;) {
+      const bool g1 = read_fastq(in1, n1, a1, b1), g2 = read_fastq(in2, n2, a2, b2);
+      if (g1 != g2) throw formatError("paired FASTQ files differ in read count");
+      if (!g1) break;
+      if (n1 != n2) throw formatError("paired FASTQ names differ: " + n1 + " vs " + n2);
+      names.push_back(n1);
+      s1.push_back(a1);
+      q1.push_back(b1);
+      s2.push_back(a2);
+      q2.push_back(b2);
+      if ((int)names.size() >= opt.chunk_size / 2) flush();
     }
     flush();
   }
@@ -453,7 +790,12 @@ int align_main(int argc, char** argv) {
   bam_index_build(output);
   std::cerr << "[fcs-genome align] " << tot.reads << " reads, " << tot.mapped << " mapped, " << tot.ext_tasks
             << " extension tasks, " << tot.global_tasks << " global alignments, " << tot.seconds << " s (GPU calls "
-            << tot.gpu_seconds << " s)" << std::endl;
+            << tot.gpu_seconds << " s)";
+  if (!fq2.empty())
+    std::cerr << "; pairs: " << tot.proper << " reads properly paired, " << tot.rescued << " mates rescued, insert "
+              << tot.pe_avg << " +- " << tot.pe_std << " [" << tot.pe_low << ", " << tot.pe_high << "] from "
+              << tot.pe_pairs << " pairs";
+  std::cerr << std::endl;
   return 0;
 }
 

@@ -18,6 +18,7 @@
 
 #include "bam.h"
 #include "fasta.h"
+#include "fcship.h"
 
 namespace fcsg {
 
@@ -29,12 +30,19 @@ struct AlignOptions {
   int w = 100;           // band width
   int chunk_size = 100000;
   int threads = 16;        // host threads for seeding / task building (bwa.nt)
+  int max_chains = 3;      // candidate chains extended per read
+  double drop_ratio = 0.5; // ... with at least this fraction of the best chain's hits (bwa -D)
   std::string rg = "sample", sample = "sample", platform = "illumina", library = "sample";
 };
 
 struct AlignStats {
   int64_t reads = 0, mapped = 0, ext_tasks = 0, ext_cells = 0, global_tasks = 0;
+  int64_t proper = 0, rescued = 0;  // paired: reads flagged proper pair, mates rescued
   double seconds = 0, gpu_seconds = 0;
+  // paired: the insert-size estimate of the (last) batch
+  int pe_pairs = 0, pe_low = 0, pe_high = 0;
+  double pe_avg = 0, pe_std = 0;
+  fcs_bsw_params params{};  // scoring of the batch (bwa defaults)
 };
 
 class KmerIndex {
@@ -56,9 +64,22 @@ class KmerIndex {
   std::vector<uint64_t> starts_;
 };
 
-// Aligns FASTQ reads; records appended to `out` (unsorted).
+// Aligns FASTQ reads; records appended to `out` (unsorted).  Up to
+// max_chains candidate chains per read are extended; the best by truesc is
+// primary, the best other locus sets bwa's single-end MAPQ.
 AlignStats align_reads(const Reference& ref, const KmerIndex& idx, const std::vector<std::string>& names,
                        const std::vector<std::string>& seqs, const std::vector<std::string>& quals,
+                       const AlignOptions& opt, std::vector<BamRecord>& out);
+
+// Paired-end batch (bwa mem_sam_pe's role): both mates seeded and extended in
+// one GPU round, the insert-size distribution estimated from the batch (FR
+// pairs, bwa mem_pestat's quartile bounds), mates rescued in the window the
+// distribution allows, the best pair chosen by score + insert-size likelihood
+// against the unpaired best - 17, then proper-pair / mate flags, RNEXT / PNEXT
+// / TLEN and paired MAPQ.  Records (read 1, read 2 per pair) appended to `out`.
+AlignStats align_pairs(const Reference& ref, const KmerIndex& idx, const std::vector<std::string>& names,
+                       const std::vector<std::string>& seqs1, const std::vector<std::string>& quals1,
+                       const std::vector<std::string>& seqs2, const std::vector<std::string>& quals2,
                        const AlignOptions& opt, std::vector<BamRecord>& out);
 
 }  // namespace fcsg

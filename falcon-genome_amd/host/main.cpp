@@ -257,6 +257,7 @@ int synth_main(int argc, char** argv) {
   a.add("noisy-frac", "", false, false, "fraction of reads drawn with 20% high-quality mismatches (mis-mapped-like)");
   a.add("spike", "", false, false, "chr:pos[,chr:pos...] plant three het SNVs at pos-30, pos, pos+30 (1-based)");
   a.add("parts", "", false, false, "also split the sample into parts/part-XXXXXX.bam + .bed (N buckets)");
+  a.add("paired", "", false, false, "also write sample_1/2.fastq: FR pairs with fragment length ~ N(ARG, 50)");
   a.parse(argc, argv);
   SynthSpec sp;
   if (a.has("contigs")) {
@@ -285,6 +286,7 @@ int synth_main(int argc, char** argv) {
   }
   if (a.has("noisy-frac")) sp.noisy_frac = std::stod(a.get("noisy-frac"));
   if (a.has("parts")) sp.parts = std::stoi(a.get("parts"));
+  if (a.has("paired")) sp.paired_insert = std::stoi(a.get("paired"));
   if (a.has("coverage")) sp.coverage = std::stod(a.get("coverage"));
   if (a.has("seed")) sp.seed = std::stoull(a.get("seed"));
   if (a.has("max-reads")) sp.max_reads = std::stoll(a.get("max-reads"));
@@ -294,7 +296,8 @@ int synth_main(int argc, char** argv) {
   const SynthOutputs o = synth_dataset(sp, a.get("output"));
   std::cout << "{\"ref\": \"" << o.ref_fasta << "\", \"bam\": \"" << o.bam << "\", \"fastq\": \"" << o.fastq
             << "\", \"truth\": \"" << o.truth_vcf << "\", \"tumor_bam\": \"" << o.tumor_bam
-            << "\", \"parts\": \"" << o.parts_dir
+            << "\", \"parts\": \"" << o.parts_dir << "\", \"fastq1\": \"" << o.fastq1 << "\", \"fastq2\": \""
+            << o.fastq2 << "\", \"pairs_truth\": \"" << o.pairs_truth
             << "\", \"reads\": " << o.n_reads << ", \"tumor_reads\": " << o.n_tumor_reads
             << ", \"variants\": " << o.variants.size() << "}" << std::endl;
   return 0;

@@ -324,6 +324,52 @@ SynthOutputs synth_dataset(const SynthSpec& spec, const std::string& dir) {
       }
     }
   }
+  if (spec.paired_insert > 0) {  // FR pairs of germline fragments
+    out.fastq1 = dir + "/sample_1.fastq";
+    out.fastq2 = dir + "/sample_2.fastq";
+    out.pairs_truth = dir + "/pairs_truth.tsv";
+    std::ofstream f1(out.fastq1), f2(out.fastq2), tt(out.pairs_truth);
+    int64_t idx = 0;
+    const int L = spec.read_len;
+    for (size_t c = 0; c < ref.contigs.size(); ++c) {
+      Rng hr(spec.seed, 0x5000 + 0x10 * c);
+      Hap haps[2];
+      for (int copy = 0; copy < 2; ++copy) {
+        std::vector<const SynthVariant*> vs;
+        for (const SynthVariant& v : per[c])
+          if (!v.somatic && (v.gt == 2 || ((v.pos * 2654435761u) >> 7 & 1) == (uint64_t)copy)) vs.push_back(&v);
+        haps[copy] = build_hap(ref.contigs[c].seq, vs);
+      }
+      const int64_t n = (int64_t)(spec.coverage / 2 * (double)ref.contigs[c].seq.size() / L);
+      for (int64_t k = 0; k < n; ++k) {
+        if ((k & 0xFFFF) == 0 && interrupted()) throw interruptedError();
+        const Hap& hp = haps[hr.below(2)];
+        const double u1 = std::max(hr.uniform(), 1e-12), u2 = hr.uniform();
+        const double z = std::sqrt(-2. * std::log(u1)) * std::cos(6.283185307179586 * u2);
+        const int64_t ins = std::max<int64_t>(L, (int64_t)std::llround(spec.paired_insert + spec.paired_sd * z));
+        if ((int64_t)hp.seq.size() <= ins) continue;
+        const int64_t s0 = (int64_t)hr.below(hp.seq.size() - ins);
+        SimRead fw, rv;
+        if (!make_read(hp, s0, L, hr, spec.err_rate, fw) || !make_read(hp, s0 + ins - L, L, hr, spec.err_rate, rv))
+          continue;
+        const bool flip = hr.uniform() < 0.5;  // read 1 from the reverse strand
+        const std::string name = "pair:" + std::to_string(idx++);
+        auto fq = [](const SimRead& r, bool rev) {
+          std::string qs(r.rec.qual.size(), '!');
+          for (size_t i = 0; i < qs.size(); ++i) qs[i] = (char)(33 + r.rec.qual[i]);
+          return rev ? std::make_pair(revcomp(r.rec.seq), std::string(qs.rbegin(), qs.rend()))
+                     : std::make_pair(r.rec.seq, qs);
+        };
+        const SimRead& m1 = flip ? rv : fw;
+        const SimRead& m2 = flip ? fw : rv;
+        const auto a = fq(m1, flip), b = fq(m2, !flip);
+        f1 << '@' << name << "/1\n" << a.first << "\n+\n" << a.second << '\n';
+        f2 << '@' << name << "/2\n" << b.first << "\n+\n" << b.second << '\n';
+        tt << name << "\t1\t" << c << '\t' << m1.pos << '\t' << (flip ? 1 : 0) << '\n';
+        tt << name << "\t2\t" << c << '\t' << m2.pos << '\t' << (flip ? 0 : 1) << '\n';
+      }
+    }
+  }
   if (spec.somatic_rate > 0) {
     auto rs = sample_reads("tumor", true, spec.tumor_coverage, 0x4000);
     out.tumor_bam = dir + "/tumor.bam";

@@ -45,10 +45,15 @@ struct SynthSpec {
   // reads split by alignment start into `parts` genome buckets (init_contig_intv
   // arithmetic), the layout `fcs-genome align --disable-merge` leaves for htc
   int parts = 0;
+  // > 0: also write <dir>/sample_1.fastq + sample_2.fastq, FR read pairs of
+  // fragments with length ~ N(paired_insert, paired_sd) (coverage / 2 of
+  // fragments), and <dir>/pairs_truth.tsv (name, mate, contig, pos, reverse)
+  int paired_insert = 0;
+  int paired_sd = 50;
 };
 
 struct SynthOutputs {
-  std::string ref_fasta, bam, tumor_bam, fastq, truth_vcf, parts_dir;
+  std::string ref_fasta, bam, tumor_bam, fastq, truth_vcf, parts_dir, fastq1, fastq2, pairs_truth;
   int64_t n_reads = 0, n_tumor_reads = 0;
   std::vector<SynthVariant> variants;
 };

@@ -89,7 +89,8 @@ def read_bam(path):
         k += (l_seq + 1) // 2
         qual = b[k:k + l_seq]
         k += l_seq
-        recs.append(dict(ref_id=ref_id, pos=pos, mapq=mapq, bin=bin_, flag=flag, name=name,
+        recs.append(dict(ref_id=ref_id, pos=pos, mapq=mapq, bin=bin_, flag=flag, name=name, next_ref_id=nref,
+                         next_pos=npos, tlen=tlen,
                          cigar=["%d%s" % (c >> 4, "MIDNSHP=X"[c & 15]) for c in cig], seq=seq,
                          qual=bytes(qual), aux=bytes(b[k:]), voff=None))
         p += 4 + bs

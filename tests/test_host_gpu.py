@@ -144,6 +144,71 @@ def test_align_end_to_end(gpu, data, tmp_path):
     assert same_cig / mapped >= 0.9, (same_cig, mapped)
 
 
+def test_align_paired_end(gpu, tmp_path):
+    """Paired-end align (row f4): FR pairs of N(350, 50) fragments; 4% of the
+    read-2 mates carry a mismatch every 16 bases, so no 19-mer seeds them and
+    only the mate rescue (12-mer window search opposite the read-1 alignment)
+    places them.  Checks placement against the generator's truth, proper-pair
+    flags, mate fields, signed TLEN and the insert-size estimate."""
+    import re
+    d = tmp_path / "pe"
+    p = H.run_cli("synth", "-o", d, "-c", "chr1:400000", "-x", "16", "--paired", "350", "--seed", "77",
+                  env=ENV, cwd=tmp_path, timeout=600)
+    assert p.returncode == 0, p.stderr[-2000:]
+    truth = {}
+    for line in open(d / "pairs_truth.tsv"):
+        name, mate, contig, pos, rev = line.split()
+        truth[(name, int(mate))] = (int(contig), int(pos), int(rev))
+    # damage some read-2 mates: a mismatch every 16 bases defeats 19-mer seeding
+    lines = open(d / "sample_2.fastq").read().split("\n")
+    damaged = set()
+    flip = {"A": "C", "C": "G", "G": "T", "T": "A", "N": "A"}
+    for i in range(0, len(lines) - 3, 4):
+        if (i // 4) % 25 == 7:
+            seq = list(lines[i + 1])
+            for j in range(5, len(seq), 16):
+                seq[j] = flip[seq[j]]
+            lines[i + 1] = "".join(seq)
+            damaged.add(lines[i][1:].split("/")[0])
+    open(d / "sample_2.fastq", "w").write("\n".join(lines))
+    out = tmp_path / "pe.bam"
+    p = H.run_cli("align", "-r", d / "ref.fasta", "-1", d / "sample_1.fastq", "-2", d / "sample_2.fastq", "-o", out,
+                  env=ENV, cwd=tmp_path)
+    assert p.returncode == 0, p.stderr[-3000:]
+    m = re.search(r"insert ([\d.]+) \+- ([\d.]+) \[(\d+), (\d+)\] from (\d+) pairs", p.stderr)
+    assert m, p.stderr[-1000:]
+    avg, sd = float(m.group(1)), float(m.group(2))
+    assert abs(avg - 350) < 15 and 35 < sd < 65, (avg, sd)
+    _, _, recs = H.read_bam(out)
+    by = {}
+    for r in recs:
+        by[(r["name"], 1 if r["flag"] & 0x40 else 2)] = r
+    assert len(by) == len(truth) and len(recs) == len(truth)
+    ok = mapped = proper = resc_ok = 0
+    for (name, mate), r in by.items():
+        assert r["flag"] & 0x1 and (r["flag"] & 0xC0) in (0x40, 0x80)
+        o = by[(name, 3 - mate)]
+        assert r["next_pos"] == o["pos"] and r["next_ref_id"] == o["ref_id"]
+        assert bool(r["flag"] & 0x8) == bool(o["flag"] & 0x4)
+        if r["flag"] & 0x4:
+            continue
+        mapped += 1
+        assert bool(r["flag"] & 0x20) == bool(o["flag"] & 0x10)
+        c, pos, rev = truth[(name, mate)]
+        hit = (r["ref_id"], r["pos"], bool(r["flag"] & 0x10)) == (c, pos, bool(rev))
+        ok += hit
+        if r["flag"] & 0x2:
+            proper += 1
+            assert r["tlen"] == -o["tlen"] and abs(r["tlen"]) > 0
+        if mate == 2 and name in damaged:
+            resc_ok += hit
+    n = len(truth)
+    assert mapped / n >= 0.99, (mapped, n)
+    assert ok / mapped >= 0.97, (ok, mapped)
+    assert proper / n >= 0.95, (proper, n)
+    assert resc_ok >= 0.8 * len(damaged), (resc_ok, len(damaged))
+
+
 def test_htc_gpu_slots_do_not_change_calls(gpu, data, tmp_path):
     """Shards dealt over two GPU slots (both on device 0 here — the dealing
     rule is the same as over two devices) and more concurrent tasks give the
