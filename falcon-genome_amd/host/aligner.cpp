@@ -13,6 +13,7 @@
 #include "config.h"
 #include "executor.h"
 #include "fcship.h"
+#include "intervals.h"
 #include "seedext.h"
 
 namespace fcsg {
@@ -670,7 +671,7 @@ bool read_fastq(std::ifstream& in, std::string& name, std::string& seq, std::str
 
 int align_main(int argc, char** argv) {
   std::string ref_path, fq1, fq2, output, rg = "sample", sp = "sample", pl = "illumina", lb = "sample";
-  bool force = false;
+  bool force = false, disable_merge = false;
   for (int i = 1; i < argc; ++i) {
     const std::string a = argv[i];
     auto val = [&]() -> std::string {
@@ -680,7 +681,8 @@ int align_main(int argc, char** argv) {
     if (a == "-h" || a == "--help") {
       std::cerr << "'fcs-genome align' options:\n  -r, --ref arg\n  -1, --fastq1 arg\n  -2, --fastq2 arg\n"
                    "  -o, --output arg\n  -R, --rg arg\n  -S, --sp arg\n  -P, --pl arg\n  -L, --lb arg\n"
-                   "  -l, --align-only\n  -f, --force\n";
+                   "  -l, --align-only\n  --disable-merge   write bwa.num_buckets sorted bucket BAMs "
+                   "(part-XXXXXX.bam + .bai + .bed) into the output directory\n  -f, --force\n";
       throw helpRequest();
     } else if (a == "-r" || a == "--ref") ref_path = val();
     else if (a == "-1" || a == "--fastq1") fq1 = val();
@@ -691,7 +693,8 @@ int align_main(int argc, char** argv) {
     else if (a == "-P" || a == "--pl") pl = val();
     else if (a == "-L" || a == "--lb") lb = val();
     else if (a == "-f" || a == "--force") force = true;
-    else if (a == "-l" || a == "--align-only" || a == "--disable-merge") continue;
+    else if (a == "--disable-merge") disable_merge = true;
+    else if (a == "-l" || a == "--align-only") continue;
     else throw invalidParam(a);
   }
   if (ref_path.empty()) throw invalidParam("--ref is required");
@@ -782,12 +785,54 @@ int align_main(int argc, char** argv) {
   }
   h.text += "@RG\tID:" + rg + "\tSM:" + sp + "\tPL:" + pl + "\tLB:" + lb + "\n";
   h.text += "@PG\tID:fcs-genome\tPN:fcs-genome align\n";
-  {
+  if (!disable_merge) {
     BamWriter w(output, h);
     for (const BamRecord& r : recs) w.write(r);
     w.close();
+    bam_index_build(output);
+  } else {
+    // bwa-flow --merge_bams=0 (reference BWAWorker.cpp:140-147, worker-align.cpp:186-195):
+    // num_buckets coordinate-sorted bucket BAMs; here the buckets are the
+    // init_contig_intv parts of the genome (the region files htc's BamInput
+    // pairs them with), a read goes to the bucket of its alignment start,
+    // unmapped reads without a placed mate to the last bucket
+    const int nb = std::max(1, conf().get_int("bwa.num_buckets"));
+    std::vector<std::pair<std::string, int64_t>> dict;
+    for (const Contig& c : ref.contigs) dict.emplace_back(c.name, (int64_t)c.seq.size());
+    const auto buckets = partition_contigs(dict, nb, false);
+    create_dir(output);
+    std::vector<std::vector<const BamRecord*>> per(nb);
+    std::vector<std::vector<std::pair<int64_t, int64_t>>> span(ref.contigs.size());  // per contig: [lb, ub] -> bucket
+    std::vector<std::vector<int>> span_b(ref.contigs.size());
+    for (int k = 0; k < nb; ++k)
+      for (const Interval& iv : buckets[k]) {
+        const int c = ref.index(iv.chrom);
+        span[c].emplace_back(iv.lb, iv.ub);
+        span_b[c].push_back(k);
+      }
+    for (const BamRecord& r : recs) {
+      int k = nb - 1;
+      if (r.ref_id >= 0) {
+        const auto& sp = span[r.ref_id];
+        const int64_t p1 = (int64_t)r.pos + 1;
+        for (size_t j = 0; j < sp.size(); ++j)
+          if (p1 >= sp[j].first && p1 <= sp[j].second) {
+            k = span_b[r.ref_id][j];
+            break;
+          }
+      }
+      per[k].push_back(&r);
+    }
+    for (int k = 0; k < nb; ++k) {
+      const std::string bam = get_contig_fname(output, k, "bam");
+      BamWriter w(bam, h);
+      for (const BamRecord* r : per[k]) w.write(*r);
+      w.close();
+      bam_index_build(bam);
+      std::ofstream bed(get_contig_fname(output, k, "bed"));
+      for (const Interval& iv : buckets[k]) bed << iv.chrom << '\t' << iv.lb - 1 << '\t' << iv.ub << '\n';
+    }
   }
-  bam_index_build(output);
   std::cerr << "[fcs-genome align] " << tot.reads << " reads, " << tot.mapped << " mapped, " << tot.ext_tasks
             << " extension tasks, " << tot.global_tasks << " global alignments, " << tot.seconds << " s (GPU calls "
             << tot.gpu_seconds << " s)";

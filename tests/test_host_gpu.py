@@ -396,3 +396,37 @@ def test_htc_part_bam_directory(gpu, data, tmp_path):
     assert a == b, (sorted(a - b)[:5], sorted(b - a)[:5])
     t = truth(data, False)
     assert len(t & outs["parts"]) / len(t) >= 0.88
+
+
+def test_align_disable_merge_buckets_feed_htc(gpu, data, tmp_path):
+    """align --disable-merge (reference worker-align.cpp:186-195, bwa-flow
+    --merge_bams=0): bwa.num_buckets coordinate-sorted part-XXXXXX.bam + .bai
+    + .bed in the output directory, every read in the bucket of its alignment
+    start; htc then runs on that directory (BamInput) as the reference's
+    pipeline does, with recall at the one-BAM level."""
+    env = dict(ENV, FCS_BWA_NUM_BUCKETS="6")
+    out = tmp_path / "buckets"
+    p = H.run_cli("align", "-r", data / "ref.fasta", "-1", data / "sample.fastq", "-o", out, "--disable-merge",
+                  env=env, cwd=tmp_path)
+    assert p.returncode == 0, p.stderr[-3000:]
+    bams = sorted(out.glob("part-*.bam"))
+    assert len(bams) == 6 and len(list(out.glob("part-*.bam.bai"))) == 6 and len(list(out.glob("part-*.bed"))) == 6
+    _, _, truth_recs = H.read_bam(data / "sample.bam")
+    total = 0
+    for k, b in enumerate(bams):
+        names, _, recs = H.read_bam(b)
+        total += len(recs)
+        ranges = []
+        for ln in (out / f"part-{k:06d}.bed").read_text().splitlines():
+            c, lo, hi = ln.split("\t")
+            ranges.append((names.index(c), int(lo), int(hi)))
+        placed = [r for r in recs if not r["flag"] & 4]
+        assert [(r["ref_id"], r["pos"]) for r in placed] == sorted((r["ref_id"], r["pos"]) for r in placed)
+        for r in placed:
+            assert any(r["ref_id"] == c and lo <= r["pos"] < hi for c, lo, hi in ranges)
+    assert total == len(truth_recs)
+    vcf = tmp_path / "b.vcf"
+    p = H.run_cli("htc", "-r", data / "ref.fasta", "-i", out, "-o", vcf, "-v", env=ENV, cwd=tmp_path)
+    assert p.returncode == 0, p.stderr[-3000:]
+    t = truth(data, False)
+    assert len(t & calls(vcf)) / len(t) >= 0.88
