@@ -249,6 +249,10 @@ def bench_e2e(args, rank, local):
             return dt, logs, r.stderr
         d = work + "/d"
 
+        def stage_s(err, name):
+            m = re.search(name + r" finishes in ([\d.]+) seconds", err)
+            return float(m.group(1)) if m else None
+
         def shard_stats(logs, dt):
             """Per-shard caller lines summed over the shards (workers/*.cpp): counts,
             and the stage times as thread-seconds (shards run concurrently)."""
@@ -268,12 +272,19 @@ def bench_e2e(args, rank, local):
             st["gpu_busy_frac"] = round(dev / dt, 4)  # PairHMM device time (HIP events) / wall time, one GPU
             st["effective_gcups"] = round(st["cells"] / dt / 1e9, 2)
             return st
-        dt, logs, _ = timed("htc", ["htc", "-r", d + "/ref.fasta", "-i", d + "/sample.bam", "-o", work + "/htc.g.vcf"])
+        dt, logs, err = timed("htc", ["htc", "-r", d + "/ref.fasta", "-i", d + "/sample.bam", "-o",
+                                      work + "/htc.g.vcf"])
         out["htc"] = shard_stats(logs, dt)
         out["htc"]["output"] = "GVCF (the reference's default)"
-        dt, logs, _ = timed("mutect2", ["mutect2", "-r", d + "/ref.fasta", "-t", d + "/tumor.bam", "-n",
-                                        d + "/sample.bam", "-o", work + "/m2.vcf"])
+        hs = stage_s(err, "Haplotype Caller")
+        out["htc"]["caller_stage_seconds"] = hs  # the 32-shard stage alone: no process start, GPU init, concat
+        out["htc"]["caller_stage_regions_per_s"] = round(out["htc"]["regions"] / hs, 1) if hs else None
+        dt, logs, err = timed("mutect2", ["mutect2", "-r", d + "/ref.fasta", "-t", d + "/tumor.bam", "-n",
+                                          d + "/sample.bam", "-o", work + "/m2.vcf"])
         out["mutect2"] = shard_stats(logs, dt)
+        ms = stage_s(err, "Mutect2")
+        out["mutect2"]["caller_stage_seconds"] = ms
+        out["mutect2"]["caller_stage_regions_per_s"] = round(out["mutect2"]["regions"] / ms, 1) if ms else None
         dt, _, err = timed("align", ["align", "-r", d + "/ref.fasta", "-1", d + "/sample_1.fastq", "-2",
                                      d + "/sample_2.fastq", "-o", work + "/aln.bam"])
         m = re.search(r"(\d+) reads, (\d+) mapped, (\d+) extension tasks, (\d+) global alignments, ([\d.]+) s "

@@ -62,7 +62,7 @@ class BamWriter {
   BamWriter(const std::string& path, const BamHeader& h, int level = 6);
   void write(const BamRecord& r);
   void close() { bgzf_.close(); }
-  uint64_t tell() const { return bgzf_.tell(); }
+  uint64_t tell() { return bgzf_.tell(); }
 
  private:
   BgzfWriter bgzf_;

@@ -2,7 +2,9 @@
 
 #include <zlib.h>
 
+#include <algorithm>
 #include <cstring>
+#include <thread>
 
 #include "common.h"
 
@@ -62,6 +64,8 @@ BgzfWriter::BgzfWriter(const std::string& path, int level) : level_(level) {
   f_ = std::fopen(path.c_str(), "wb");
   if (!f_) throw fileNotFound(path + " (cannot open for writing)");
   buf_.reserve(kBgzfMaxBlock);
+  const unsigned hc = std::max(1u, std::thread::hardware_concurrency());
+  max_pending_ = 2 * (size_t)std::min(8u, hc);
 }
 
 BgzfWriter::~BgzfWriter() {
@@ -72,9 +76,21 @@ BgzfWriter::~BgzfWriter() {
 }
 
 void BgzfWriter::emit_block(const uint8_t* data, size_t n) {
-  const std::vector<uint8_t> blk = make_block(data, n, level_);
-  if (std::fwrite(blk.data(), 1, blk.size(), f_) != blk.size()) throw internalError("[E::bgzf] write failed");
-  coff_ += blk.size();
+  std::vector<uint8_t> in(data, data + n);
+  const int level = level_;
+  pending_.push_back(std::async(std::launch::async, [in = std::move(in), level] {
+    return make_block(in.data(), in.size(), level);
+  }));
+  drain(max_pending_);
+}
+
+void BgzfWriter::drain(size_t keep) {
+  while (pending_.size() > keep) {
+    const std::vector<uint8_t> blk = pending_.front().get();
+    pending_.pop_front();
+    if (std::fwrite(blk.data(), 1, blk.size(), f_) != blk.size()) throw internalError("[E::bgzf] write failed");
+    coff_ += blk.size();
+  }
 }
 
 void BgzfWriter::write(const void* data, size_t n) {
@@ -97,6 +113,7 @@ void BgzfWriter::flush() {
 void BgzfWriter::close() {
   if (closed_ || !f_) return;
   flush();
+  drain(0);
   std::fwrite(kBgzfEof, 1, sizeof kBgzfEof, f_);
   std::fclose(f_);
   f_ = nullptr;

@@ -10,6 +10,8 @@
 
 #include <cstdint>
 #include <cstdio>
+#include <deque>
+#include <future>
 #include <string>
 #include <vector>
 
@@ -31,16 +33,24 @@ class BgzfWriter {
   // Ends the current block so the next write starts a new one (BAM header, index points).
   void flush();
   // Virtual offset of the next byte written.
-  uint64_t tell() const { return (coff_ << 16) | (uint64_t)buf_.size(); }
+  uint64_t tell() {
+    drain(0);
+    return (coff_ << 16) | (uint64_t)buf_.size();
+  }
   void close();  // flush + EOF block
 
  private:
   void emit_block(const uint8_t* data, size_t n);
+  void drain(size_t keep);  // write finished blocks in order until <= keep are pending
   FILE* f_ = nullptr;
   int level_;
   std::vector<uint8_t> buf_;
-  uint64_t coff_ = 0;  // compressed offset of the block being filled
+  uint64_t coff_ = 0;  // compressed offset of the block being filled (all pending blocks written)
   bool closed_ = false;
+  // blocks compress on worker threads (htslib's thread pool role) and are
+  // written in order; tell() first writes every pending block
+  std::deque<std::future<std::vector<uint8_t>>> pending_;
+  size_t max_pending_ = 0;
 };
 
 class BgzfReader {
