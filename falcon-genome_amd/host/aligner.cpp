@@ -98,81 +98,101 @@ int approx_mapq_se(const SeedAln& a, int sub, int sub_n, int seedcov, int min_se
 int64_t aln_pos(const Cand& c) { return c.aln.rb; }
 int64_t aln_end(const Cand& c) { return c.aln.re; }
 
-// Seeds and chains of one read (both strands): k-mer hits every seed_step
-// bases, chains = runs of diagonals within 8 of each other; up to
-// max_chains chains with at least drop_ratio x the best chain's hits, each
-// represented by the earliest hit on its most supported diagonal, grown to a
-// maximal exact match.
+// Seeds and chains of one read (bwa mem_collect_intv + mem_chain): SMEMs of
+// length >= min_seed_len on the FMD-index (both strands at once) and re-seeds
+// inside long, rare SMEMs; every occurrence (sampled down to max_occ per
+// SMEM) is a seed; seeds join a chain of the same contig and strand when they
+// continue it (bwa test_and_merge: colinear, diagonal within w, gaps below
+// max_chain_gap); chains weighed by the query bases their seeds cover; up to
+// max_chains chains with at least drop_ratio x the best weight become
+// candidates, each extended from its longest seed.
 void seed_read(const Reference& ref, const KmerIndex& idx, const AlignOptions& opt, ReadAln& R) {
-  const int k = idx.k();
-  const uint64_t kmask = (1ull << (2 * k)) - 1;
-  struct Hit {
-    int64_t d;
-    int qp;
-    uint64_t g;
-  };
-  struct Chain {
-    int n;
+  const std::vector<uint8_t>& q = R.code[0];
+  const int L = (int)q.size();
+  std::vector<BiInterval> mems;
+  idx.fmd().collect(q.data(), L, opt.k, (int)(opt.k * 1.5 + .499), 10, mems);
+  struct Seed {
+    int contig;
     bool rev;
-    int qp;
-    uint64_t g;
+    int qbeg, len;
+    int64_t rbeg;
   };
-  std::vector<Chain> chains;
-  std::vector<Hit> hits;
-  for (int strand = 0; strand < 2; ++strand) {
-    const std::vector<uint8_t>& c = R.code[strand];
-    hits.clear();
-    for (int qp = 0; qp + k <= (int)c.size(); qp += opt.seed_step) {
-      uint64_t key = 0;
-      bool ok = true;
-      for (int i = 0; i < k && ok; ++i) {
-        if (c[qp + i] > 3) ok = false;
-        key = ((key << 2) | c[qp + i]) & kmask;
-      }
-      if (!ok) continue;
-      const auto [b, e] = idx.lookup(key);
-      if (e - b == 0 || e - b > opt.max_occ) continue;
-      for (const uint64_t* p = b; p != e; ++p) hits.push_back({(int64_t)*p - qp, qp, *p});
-    }
-    std::sort(hits.begin(), hits.end(), [](const Hit& x, const Hit& y) { return x.d != y.d ? x.d < y.d : x.qp < y.qp; });
-    size_t i = 0;
-    while (i < hits.size()) {
-      size_t j = i;
-      int n = 0, dn_best = 0;
-      const Hit* seed = &hits[i];
-      while (j < hits.size() && (j == i || hits[j].d - hits[j - 1].d <= 8)) {
-        size_t e = j;
-        while (e < hits.size() && hits[e].d == hits[j].d) ++e;  // one diagonal
-        if ((int)(e - j) > dn_best) {
-          dn_best = (int)(e - j);
-          seed = &hits[j];
-        }
-        n += (int)(e - j);
-        j = e;
-      }
-      chains.push_back({n, strand != 0, seed->qp, seed->g});
-      i = j;
+  std::vector<Seed> seeds;
+  for (const BiInterval& m : mems) {
+    const int64_t step = m.s > opt.max_occ ? m.s / opt.max_occ : 1;
+    for (int64_t j = 0, kept = 0; j < m.s && kept < opt.max_occ; j += step, ++kept) {
+      Seed sd;
+      idx.fmd().locate(m, j, sd.contig, sd.rbeg, sd.rev);
+      sd.len = m.qe - m.qb;
+      sd.qbeg = sd.rev ? L - m.qe : m.qb;  // query offset in the oriented read
+      seeds.push_back(sd);
     }
   }
-  if (chains.empty()) return;
-  std::stable_sort(chains.begin(), chains.end(), [](const Chain& a, const Chain& b) { return a.n > b.n; });
-  const int best_n = chains[0].n;
+  if (seeds.empty()) return;
+  std::stable_sort(seeds.begin(), seeds.end(), [](const Seed& a, const Seed& b) {
+    return a.contig != b.contig ? a.contig < b.contig : a.rev != b.rev ? a.rev < b.rev
+         : a.qbeg != b.qbeg ? a.qbeg < b.qbeg : a.rbeg < b.rbeg;
+  });
+  struct Chain {
+    int contig;
+    bool rev;
+    std::vector<Seed> s;
+    int weight = 0;
+  };
+  std::vector<Chain> chains;
+  const int max_chain_gap = 10000;
+  size_t group0 = 0;
+  for (size_t i = 0; i < seeds.size(); ++i) {
+    const Seed& sd = seeds[i];
+    if (i > 0 && (sd.contig != seeds[i - 1].contig || sd.rev != seeds[i - 1].rev)) group0 = chains.size();
+    bool merged = false;
+    for (size_t c = group0; c < chains.size() && !merged; ++c) {
+      const Seed& last = chains[c].s.back();
+      if (sd.qbeg >= last.qbeg && sd.qbeg + sd.len <= last.qbeg + last.len && sd.rbeg >= last.rbeg &&
+          sd.rbeg + sd.len <= last.rbeg + last.len) {
+        merged = true;  // contained in the last seed
+        break;
+      }
+      const int64_t x = sd.qbeg - last.qbeg, y = sd.rbeg - last.rbeg;
+      if (y >= 0 && x - y <= opt.w && y - x <= opt.w && x - last.len < max_chain_gap && y - last.len < max_chain_gap) {
+        chains[c].s.push_back(sd);
+        merged = true;
+      }
+    }
+    if (!merged) chains.push_back({sd.contig, sd.rev, {sd}, 0});
+  }
+  for (Chain& ch : chains) {  // bwa mem_chain_weight: query bases covered by the seeds (min with the reference's)
+    int64_t wq = 0, wr = 0, endq = 0, endr = 0;
+    for (const Seed& sd : ch.s) {
+      if (sd.qbeg >= endq) wq += sd.len;
+      else if (sd.qbeg + sd.len > endq) wq += sd.qbeg + sd.len - endq;
+      endq = std::max<int64_t>(endq, sd.qbeg + sd.len);
+    }
+    std::vector<const Seed*> byr;
+    for (const Seed& sd : ch.s) byr.push_back(&sd);
+    std::sort(byr.begin(), byr.end(), [](const Seed* a, const Seed* b) { return a->rbeg < b->rbeg; });
+    endr = 0;
+    for (const Seed* sd : byr) {
+      if (sd->rbeg >= endr) wr += sd->len;
+      else if (sd->rbeg + sd->len > endr) wr += sd->rbeg + sd->len - endr;
+      endr = std::max<int64_t>(endr, sd->rbeg + sd->len);
+    }
+    ch.weight = (int)std::min(wq, wr);
+  }
+  std::stable_sort(chains.begin(), chains.end(), [](const Chain& a, const Chain& b) { return a.weight > b.weight; });
+  const int best_w = chains[0].weight;
   for (const Chain& ch : chains) {
-    if ((int)R.cands.size() >= opt.max_chains || ch.n < opt.drop_ratio * best_n) break;
+    if ((int)R.cands.size() >= opt.max_chains || ch.weight < opt.drop_ratio * best_w) break;
+    const Seed* top = &ch.s[0];
+    for (const Seed& sd : ch.s)
+      if (sd.len > top->len) top = &sd;
     Cand C;
     C.rev = ch.rev;
-    C.hits = ch.n;
-    int64_t off = 0;
-    C.contig = idx.contig_of(ch.g, off);
-    const std::vector<uint8_t>& rc = idx.codes(C.contig);
-    const std::vector<uint8_t>& q = R.code[ch.rev];
-    int qs = ch.qp, qe = ch.qp + k;
-    int64_t rs = off;
-    while (qs > 0 && rs > 0 && q[qs - 1] < 4 && q[qs - 1] == rc[rs - 1]) --qs, --rs;
-    while (qe < (int)q.size() && rs + (qe - qs) < (int64_t)rc.size() && q[qe] < 4 && q[qe] == rc[rs + (qe - qs)]) ++qe;
-    C.seed_q = qs;
-    C.seed_len = qe - qs;
-    C.seed_r = rs;
+    C.contig = ch.contig;
+    C.hits = ch.weight;
+    C.seed_q = top->qbeg;
+    C.seed_len = top->len;
+    C.seed_r = top->rbeg;
     R.cands.push_back(std::move(C));
   }
 }
@@ -240,7 +260,7 @@ void pick_primary(ReadAln& R, const AlignOptions& opt) {
     R.sub = std::max(R.sub, C.aln.truesc);
     if (C.aln.truesc >= B.aln.truesc - 5) ++R.sub_n;  // bwa: other hits within the mapQ_coef window
   }
-  R.mapq = approx_mapq_se(B.aln, R.sub, R.sub_n, B.seed_len, opt.k, 1, 4);
+  R.mapq = approx_mapq_se(B.aln, R.sub, R.sub_n, std::max(B.hits, B.seed_len), opt.k, 1, 4);
 }
 
 // Insert-size distribution of one batch (bwa mem_pestat, FR orientation):
@@ -469,50 +489,12 @@ void align_batch(const Reference& ref, const KmerIndex& idx, const std::vector<s
 }  // namespace
 
 KmerIndex::KmerIndex(const Reference& ref, int k) : k_(k) {
-  if (k < 8 || k > 31) throw invalidParam("seed length must be in [8, 31]");
-  uint64_t g = 0;
-  std::vector<std::pair<uint64_t, uint64_t>> kv;
+  if (k < 8 || k > 63) throw invalidParam("minimum seed length must be in [8, 63]");
   for (const Contig& c : ref.contigs) {
-    starts_.push_back(g);
-    const int64_t L = (int64_t)c.seq.size();
-    codes_.emplace_back(L);
-    for (int64_t p = 0; p < L; ++p) codes_.back()[p] = code_of(c.seq[p]);
-    uint64_t key = 0;
-    int valid = 0;
-    const uint64_t mask = (k == 32) ? ~0ull : ((1ull << (2 * k)) - 1);
-    for (int64_t p = 0; p < L; ++p) {
-      const uint8_t b = code_of(c.seq[p]);
-      if (b > 3) {
-        valid = 0;
-        key = 0;
-        continue;
-      }
-      key = ((key << 2) | b) & mask;
-      if (++valid >= k) kv.emplace_back(key, g + (uint64_t)(p - k + 1));
-    }
-    g += (uint64_t)L;
+    codes_.emplace_back(c.seq.size());
+    for (size_t p = 0; p < c.seq.size(); ++p) codes_.back()[p] = code_of(c.seq[p]);
   }
-  starts_.push_back(g);
-  std::sort(kv.begin(), kv.end());
-  keys_.resize(kv.size());
-  pos_.resize(kv.size());
-  for (size_t i = 0; i < kv.size(); ++i) {
-    keys_[i] = kv[i].first;
-    pos_[i] = kv[i].second;
-  }
-}
-
-std::pair<const uint64_t*, const uint64_t*> KmerIndex::lookup(uint64_t key) const {
-  auto lo = std::lower_bound(keys_.begin(), keys_.end(), key);
-  auto hi = std::upper_bound(lo, keys_.end(), key);
-  return {pos_.data() + (lo - keys_.begin()), pos_.data() + (hi - keys_.begin())};
-}
-
-int KmerIndex::contig_of(uint64_t g, int64_t& off) const {
-  const auto it = std::upper_bound(starts_.begin(), starts_.end(), g);
-  const int c = (int)(it - starts_.begin()) - 1;
-  off = (int64_t)(g - starts_[c]);
-  return c;
+  fmd_ = std::make_unique<FmdIndex>(codes_);
 }
 
 AlignStats align_reads(const Reference& ref, const KmerIndex& idx, const std::vector<std::string>& names,

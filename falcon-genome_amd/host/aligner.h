@@ -2,31 +2,31 @@
 // bwa bwamem.c mem_chain2aln / mem_reg2aln and bwa.c bwa_gen_cigar2, reached
 // in the reference through BWAWorker: /root/reference/src/workers/BWAWorker.cpp:94-186).
 //
-// Per chunk of reads (bwa.chunk_size): exact-match seeds from a k-mer index of
-// the reference, the best chain per read, then bwa's extension protocol on the
-// GPU (host/seedext.h: mem_chain2aln's windows, left / right extensions with
+// Per chunk of reads (bwa.chunk_size): SMEM seeds, up to max_chains chains
+// per read, then bwa's extension protocol on the GPU (host/seedext.h: mem_chain2aln's windows, left / right extensions with
 // band retry, local vs to-end, mem_reg2aln / bwa_gen_cigar2's global
 // alignment for the CIGAR).  NM / MD / AS tags, soft clips, sorted BAM + BAI.
-// What stands in for bwa [EXT]: seeds are k-mer hits grown to maximal exact
-// matches instead of SMEMs from an FM-index, and chaining keeps the diagonal
-// with the most hits.
+// Seeds are bwa's SMEMs on an FMD-index of the reference (host/fmindex.h),
+// chained as bwa's mem_chain does; [EXT] bwa is not vendored, so this is a
+// restatement (parity unpinned against bwa itself).
 #pragma once
 
 #include <cstdint>
+#include <memory>
 #include <string>
 #include <vector>
 
 #include "bam.h"
 #include "fasta.h"
+#include "fmindex.h"
 #include "fcship.h"
 
 namespace fcsg {
 
 struct AlignOptions {
   int gpu = 0;
-  int k = 19;            // seed k-mer length (bwa min_seed_len)
-  int seed_step = 4;     // query positions sampled for seeds
-  int max_occ = 64;      // ignore k-mers with more hits
+  int k = 19;            // minimum SMEM length (bwa -k min_seed_len)
+  int max_occ = 500;     // occurrences kept per SMEM (bwa -c max_occ; sampled beyond)
   int w = 100;           // band width
   int chunk_size = 100000;
   int threads = 16;        // host threads for seeding / task building (bwa.nt)
@@ -45,23 +45,20 @@ struct AlignStats {
   fcs_bsw_params params{};  // scoring of the batch (bwa defaults)
 };
 
+// The aligner's reference index: contigs as codes and their FMD-index
+// (host/fmindex.h) for SMEM seeding.
 class KmerIndex {
  public:
   KmerIndex(const Reference& ref, int k);
-  // hits of the k-mer starting at codes[0] (2-bit codes, no N): global positions
-  std::pair<const uint64_t*, const uint64_t*> lookup(uint64_t key) const;
-  int k() const { return k_; }
-  // global coordinate ↔ (contig, offset)
-  int contig_of(uint64_t g, int64_t& off) const;
-  uint64_t global(int contig) const { return starts_[contig]; }
+  int k() const { return k_; }  // minimum seed length (bwa -k)
   // the contig's bases as codes 0..4 (A, C, G, T, other)
   const std::vector<uint8_t>& codes(int contig) const { return codes_[contig]; }
+  const FmdIndex& fmd() const { return *fmd_; }
 
  private:
   int k_;
   std::vector<std::vector<uint8_t>> codes_;
-  std::vector<uint64_t> keys_, pos_;  // sorted by key
-  std::vector<uint64_t> starts_;
+  std::unique_ptr<FmdIndex> fmd_;
 };
 
 // Aligns FASTQ reads; records appended to `out` (unsorted).  Up to

@@ -14,6 +14,7 @@
 #include "config.h"
 #include "executor.h"
 #include "fasta.h"
+#include "fmindex.h"
 #include "gatk_prep.h"
 #include "seedext.h"
 #include "intervals.h"
@@ -98,6 +99,41 @@ int fcsg_intersect_regions(const char* const* paths, int n, char* buf, int cap) 
 }
 
 int fcsg_gvcf_band(int gq) { return gvcf_band(gq); }
+
+// SMEM seeding on an FMD-index of the given contigs (codes 0..4): SMEMs of q
+// (bwa mem_collect_intv rounds 1-2), out = {qb, qe, occurrences} per SMEM and
+// loc = {contig, offset, reverse} of every occurrence (at most loc_cap rows,
+// SMEM by SMEM, each SMEM's occurrences in suffix-array order).  Returns the
+// SMEM count, or < 0 on error.
+int fcsg_fmd_smems(const uint8_t* ref, const int64_t* clen, int ncontig, const uint8_t* q, int qlen, int min_len,
+                   int split_len, int split_width, int32_t* out, int cap, int64_t* loc, int loc_cap) {
+  int n = -1;
+  const int rc = guard([&] {
+    std::vector<std::vector<uint8_t>> cs;
+    int64_t o = 0;
+    for (int i = 0; i < ncontig; ++i) {
+      cs.emplace_back(ref + o, ref + o + clen[i]);
+      o += clen[i];
+    }
+    const FmdIndex fmd(cs);
+    std::vector<BiInterval> v;
+    fmd.collect(q, qlen, min_len, split_len, split_width, v);
+    if ((int)v.size() > cap) throw invalidParam("fcsg_fmd_smems: capacity");
+    int64_t nl = 0;
+    for (size_t i = 0; i < v.size(); ++i) {
+      out[3 * i] = v[i].qb, out[3 * i + 1] = v[i].qe, out[3 * i + 2] = (int32_t)v[i].s;
+      for (int64_t j = 0; j < v[i].s && nl < loc_cap; ++j, ++nl) {
+        int c;
+        int64_t off;
+        bool rev;
+        fmd.locate(v[i], j, c, off, rev);
+        loc[3 * nl] = c, loc[3 * nl + 1] = off, loc[3 * nl + 2] = rev;
+      }
+    }
+    n = (int)v.size();
+  });
+  return rc < 0 ? rc : n;
+}
 
 // bwa's seed-extension protocol (host/seedext.h) over n seeds on one reference
 // sequence (codes 0..4); per job out_i = {qb, qe, score, truesc, w, gscore, gw},

@@ -1,0 +1,267 @@
+#include "fmindex.h"
+
+#include <algorithm>
+#include <stdexcept>
+
+#include "common.h"
+
+namespace fcsg {
+
+namespace {
+
+constexpr uint32_t kEmpty = 0xFFFFFFFFu;
+
+void buckets(const uint32_t* s, int64_t n, int K, std::vector<int64_t>& bkt, bool end) {
+  std::fill(bkt.begin(), bkt.end(), 0);
+  for (int64_t i = 0; i < n; ++i) ++bkt[s[i]];
+  int64_t sum = 0;
+  for (int c = 0; c < K; ++c) {
+    sum += bkt[c];
+    bkt[c] = end ? sum : sum - bkt[c];
+  }
+}
+
+void induce(const uint32_t* s, uint32_t* sa, int64_t n, int K, const std::vector<uint8_t>& t,
+            std::vector<int64_t>& bkt) {
+  buckets(s, n, K, bkt, false);  // L-type suffixes, left to right from bucket starts
+  for (int64_t i = 0; i < n; ++i) {
+    if (sa[i] == kEmpty || sa[i] == 0) continue;
+    const int64_t j = (int64_t)sa[i] - 1;
+    if (!t[j]) sa[bkt[s[j]]++] = (uint32_t)j;
+  }
+  buckets(s, n, K, bkt, true);  // S-type suffixes, right to left from bucket ends
+  for (int64_t i = n - 1; i >= 0; --i) {
+    if (sa[i] == kEmpty || sa[i] == 0) continue;
+    const int64_t j = (int64_t)sa[i] - 1;
+    if (t[j]) sa[--bkt[s[j]]] = (uint32_t)j;
+  }
+}
+
+}  // namespace
+
+// SA-IS (Nong, Zhang and Chan 2009): sort the LMS substrings by induction,
+// name them, recurse on the reduced string when names repeat, then induce
+// the full order from the sorted LMS suffixes.
+void sais(const uint32_t* s, uint32_t* sa, int64_t n, int K) {
+  std::vector<uint8_t> t(n);  // 1 = S-type
+  t[n - 1] = 1;
+  for (int64_t i = n - 2; i >= 0; --i) t[i] = s[i] < s[i + 1] || (s[i] == s[i + 1] && t[i + 1]);
+  auto lms = [&](int64_t i) { return i > 0 && t[i] && !t[i - 1]; };
+  std::vector<int64_t> bkt(K);
+  std::fill(sa, sa + n, kEmpty);
+  buckets(s, n, K, bkt, true);
+  for (int64_t i = 1; i < n; ++i)
+    if (lms(i)) sa[--bkt[s[i]]] = (uint32_t)i;
+  induce(s, sa, n, K, t, bkt);
+  int64_t n1 = 0;
+  for (int64_t i = 0; i < n; ++i)
+    if (sa[i] != kEmpty && lms(sa[i])) sa[n1++] = sa[i];
+  std::fill(sa + n1, sa + n, kEmpty);
+  int64_t name = 0, prev = -1;
+  for (int64_t i = 0; i < n1; ++i) {
+    const int64_t pos = sa[i];
+    bool diff = false;
+    for (int64_t d = 0; d < n; ++d) {
+      if (prev == -1 || s[pos + d] != s[prev + d] || t[pos + d] != t[prev + d]) {
+        diff = true;
+        break;
+      }
+      if (d > 0 && (lms(pos + d) || lms(prev + d))) break;
+    }
+    if (diff) {
+      ++name;
+      prev = pos;
+    }
+    sa[n1 + pos / 2] = (uint32_t)(name - 1);
+  }
+  for (int64_t i = n - 1, j = n - 1; i >= n1; --i)
+    if (sa[i] != kEmpty) sa[j--] = sa[i];
+  uint32_t* s1 = sa + n - n1;
+  if (name < n1) {
+    sais(s1, sa, n1, (int)name);
+  } else {
+    for (int64_t i = 0; i < n1; ++i) sa[s1[i]] = (uint32_t)i;
+  }
+  for (int64_t i = 1, j = 0; i < n; ++i)
+    if (lms(i)) s1[j++] = (uint32_t)i;
+  for (int64_t i = 0; i < n1; ++i) sa[i] = s1[sa[i]];
+  std::fill(sa + n1, sa + n, kEmpty);
+  buckets(s, n, K, bkt, true);
+  for (int64_t i = n1 - 1; i >= 0; --i) {
+    const uint32_t j = sa[i];
+    sa[i] = kEmpty;
+    sa[--bkt[s[j]]] = j;
+  }
+  induce(s, sa, n, K, t, bkt);
+}
+
+FmdIndex::FmdIndex(const std::vector<std::vector<uint8_t>>& contigs) {
+  // F = 5 C_1 5 C_2 ... 5 C_n 5;  T = F revcomp(F) $
+  std::vector<uint32_t> T;
+  int64_t total = 1;
+  for (const auto& c : contigs) total += (int64_t)c.size() + 1;
+  if (2 * total + 1 >= (int64_t)kEmpty) throw invalidParam("FMD-index: reference too long for 32-bit positions");
+  T.reserve(2 * total + 1);
+  for (const auto& c : contigs) {
+    T.push_back(5);
+    cstart_.push_back((int64_t)T.size());
+    clen_.push_back((int64_t)c.size());
+    for (uint8_t b : c) T.push_back(b < 4 ? b + 1u : 5u);
+  }
+  T.push_back(5);
+  flen_ = (int64_t)T.size();
+  for (int64_t i = flen_ - 1; i >= 0; --i) T.push_back(T[i] == 5 ? 5u : 5u - T[i]);
+  T.push_back(0);
+  n_ = (int64_t)T.size();
+  sa_.resize(n_);
+  sais(T.data(), sa_.data(), n_, 6);
+  C_.assign(7, 0);
+  for (uint32_t c : T) ++C_[c + 1];
+  for (int c = 1; c < 7; ++c) C_[c] += C_[c - 1];
+  const int64_t nb = (n_ + 63) / 64;
+  bits_.assign(4 * nb, 0);
+  cnt_.assign(4 * nb, 0);
+  uint32_t run[4] = {0, 0, 0, 0};
+  for (int64_t b = 0; b < nb; ++b) {
+    for (int c = 0; c < 4; ++c) cnt_[4 * b + c] = run[c];
+    for (int64_t i = 64 * b; i < std::min(n_, 64 * b + 64); ++i) {
+      const uint32_t p = sa_[i];
+      const uint32_t ch = p ? T[p - 1] : 0;  // BWT symbol
+      if (ch >= 1 && ch <= 4) {
+        bits_[4 * b + ch - 1] |= 1ull << (i & 63);
+        ++run[ch - 1];
+      }
+    }
+  }
+}
+
+int64_t FmdIndex::occ(int c, int64_t i) const {
+  if (i <= 0) return 0;
+  const int64_t b = i >> 6;
+  const int r = (int)(i & 63);
+  int64_t v = b < (int64_t)(cnt_.size() / 4) ? cnt_[4 * b + c - 1] : cnt_[cnt_.size() - 4 + c - 1];
+  if (b < (int64_t)(bits_.size() / 4)) {
+    if (r) v += __builtin_popcountll(bits_[4 * b + c - 1] & ((1ull << r) - 1));
+  } else {  // i == n: the whole last block
+    v += __builtin_popcountll(bits_[bits_.size() - 4 + c - 1]);
+  }
+  return v;
+}
+
+void FmdIndex::set_intv(int c, BiInterval& iv) const {
+  iv.k = C_[c];
+  iv.s = C_[c + 1] - C_[c];
+  iv.l = C_[5 - c];
+}
+
+// bwa bwt_extend: the four one-base extensions of ik, backward (cP, is_back)
+// or forward (P comp(c), reported at index c: the backward extension of
+// revcomp(P) by c).  The other coordinate follows from the counts: the
+// revcomp(P) x (resp. P x) suffixes are ordered by x, and x = $ never occurs
+// (the base before $ is a separator).
+void FmdIndex::extend(const BiInterval& ik, BiInterval ok[5], bool is_back) const {
+  const int64_t base = is_back ? ik.k : ik.l;
+  for (int c = 1; c <= 4; ++c) {
+    const int64_t tk = occ(c, base), tl = occ(c, base + ik.s);
+    (is_back ? ok[c].k : ok[c].l) = C_[c] + tk;
+    ok[c].s = tl - tk;
+  }
+  int64_t o = is_back ? ik.l : ik.k;
+  for (int c = 4; c >= 1; --c) {
+    (is_back ? ok[c].l : ok[c].k) = o;
+    o += ok[c].s;
+  }
+}
+
+int FmdIndex::smem1(const uint8_t* q, int len, int x, int64_t min_intv, std::vector<BiInterval>& mem) const {
+  mem.clear();
+  if (q[x] > 3) return x + 1;
+  if (min_intv < 1) min_intv = 1;
+  std::vector<BiInterval> a0, a1;
+  std::vector<BiInterval>*prev = &a0, *curr = &a1;
+  BiInterval ik, ok[5];
+  set_intv(q[x] + 1, ik);
+  ik.qe = x + 1;
+  int i;
+  for (i = x + 1; i < len; ++i) {  // forward search
+    if (ik.s < min_intv) break;
+    if (q[i] < 4) {
+      const int c = 4 - q[i];  // index of the forward extension by q[i]
+      extend(ik, ok, false);
+      if (ok[c].s != ik.s) {
+        curr->push_back(ik);
+        if (ok[c].s < min_intv) break;
+      }
+      ik = ok[c];
+      ik.qe = i + 1;
+    } else {
+      curr->push_back(ik);
+      break;
+    }
+  }
+  if (i == len) curr->push_back(ik);
+  std::reverse(curr->begin(), curr->end());  // longest forward match first
+  const int ret = curr->front().qe;
+  std::swap(curr, prev);
+  for (i = x - 1; i >= -1; --i) {  // backward search for MEMs
+    const int c = i < 0 ? -1 : q[i] < 4 ? q[i] + 1 : -1;
+    curr->clear();
+    for (const BiInterval& p : *prev) {
+      if (c >= 0 && ik.s >= min_intv) extend(p, ok, true);  // bwa tests ik, not p
+      if (c < 0 || ok[c].s < min_intv) {
+        if (curr->empty()) {  // no longer match in this round: p is maximal
+          if (mem.empty() || i + 1 < mem.back().qb) {
+            ik = p;
+            ik.qb = i + 1;
+            mem.push_back(ik);
+          }
+        }
+      } else if (curr->empty() || ok[c].s != curr->back().s) {
+        ok[c].qe = p.qe;
+        curr->push_back(ok[c]);
+      }
+    }
+    if (curr->empty()) break;
+    std::swap(curr, prev);
+  }
+  std::reverse(mem.begin(), mem.end());  // by start coordinate
+  return ret;
+}
+
+void FmdIndex::collect(const uint8_t* q, int len, int min_len, int split_len, int split_width,
+                       std::vector<BiInterval>& out) const {
+  out.clear();
+  std::vector<BiInterval> m;
+  for (int x = 0; x < len;) {
+    if (q[x] < 4) {
+      x = smem1(q, len, x, 1, m);
+      for (const BiInterval& p : m)
+        if (p.qe - p.qb >= min_len) out.push_back(p);
+    } else {
+      ++x;
+    }
+  }
+  const size_t n0 = out.size();
+  for (size_t k = 0; k < n0; ++k) {  // re-seeding inside long SMEMs with few hits
+    const BiInterval p = out[k];
+    if (p.qe - p.qb < split_len || p.s > split_width) continue;
+    smem1(q, len, (p.qb + p.qe) >> 1, p.s + 1, m);
+    for (const BiInterval& r : m)
+      if (r.qe - r.qb >= min_len) out.push_back(r);
+  }
+  std::stable_sort(out.begin(), out.end(), [](const BiInterval& a, const BiInterval& b) {
+    return a.qb != b.qb ? a.qb < b.qb : a.qe < b.qe;
+  });
+}
+
+void FmdIndex::locate(const BiInterval& iv, int64_t j, int& contig, int64_t& off, bool& rev) const {
+  int64_t p = sa_[iv.k + j];
+  const int64_t len = iv.qe - iv.qb;
+  rev = p >= flen_;
+  if (rev) p = 2 * flen_ - p - len;  // start of the reverse-strand match on F
+  const auto it = std::upper_bound(cstart_.begin(), cstart_.end(), p);
+  contig = (int)(it - cstart_.begin()) - 1;
+  off = p - cstart_[contig];
+}
+
+}  // namespace fcsg
