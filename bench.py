@@ -482,6 +482,19 @@ def main():
             "cigar_gcups": g["cigar"]["gcups"], "cigar_ms": g["cigar"]["ms"],
             "kernel": "bsw_global_lane_kernel<33> (one task per lane, band in registers, nibble direction rows) + "
                       "bsw_traceback_kernel; wider bands go to bsw_global_kernel (one wave per task)"}
+        gm = {}
+        try:
+            gm = json.load(open(os.path.join(ROOT, "profiles", "pmc_bsw.json"))).get("global", {})
+        except (OSError, ValueError):
+            pass
+        if gm.get("dp_valu_lane_instr_per_cell"):
+            vpc = gm["dp_valu_lane_instr_per_cell"]
+            ach = g["scores"]["gcups"] * 1e9 * vpc
+            line["bsw"]["global"]["roofline"] = {
+                "bound": "valu", "unit": "T lane-instr/s", "peak": round(VALU_LANE_INSTR_PEAK / 1e12, 3),
+                "achieved": round(ach / 1e12, 3), "frac": round(ach / VALU_LANE_INSTR_PEAK, 4),
+                "valu_instr_per_cell": vpc, "of": "scores-only pass (DP kernels)",
+                "valu_source": "profiles/pmc_bsw.json global (SQ_INSTS_VALU x 64 / band cells)"}
         if world == 1 and not args.no_cpu_baseline:
             line["bsw"]["cpu_baseline"] = cpu_baseline_bsw(
                 fcship.synth_bsw(args.seed + 1, 20000, read_len=151, ref_len=10_000_000), 0, cpu_threads())

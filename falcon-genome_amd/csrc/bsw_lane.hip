@@ -491,7 +491,6 @@ __global__ __launch_bounds__(64, 2) void bsw_ext_kernel(const BswDevBatch b, con
     case 9: lane_wave<152, SYM, true>(b, p, order, lo, hi, res, cells_out, qsel, tab); break;
     case 8: lane_wave<128, SYM, true>(b, p, order, lo, hi, res, cells_out, qsel, tab); break;
     case 7: lane_wave<96, SYM, true>(b, p, order, lo, hi, res, cells_out, qsel, tab); break;
-    case 6: lane_wave<152, SYM, false>(b, p, order, lo, hi, res, cells_out, qsel, tab); break;
     case 5: lane_wave<128, SYM, false>(b, p, order, lo, hi, res, cells_out, qsel, tab); break;
     case 4: lane_wave<96, SYM, false>(b, p, order, lo, hi, res, cells_out, qsel, tab); break;
     case 3: lane_wave<64, SYM, false>(b, p, order, lo, hi, res, cells_out, qsel, tab); break;
@@ -542,7 +541,12 @@ __device__ __forceinline__ int bsw_bucket(int qlen, int tlen, int h0, bool acgt,
   if (need <= 64) return 3;
   const int c = need <= 96 ? 4 : need <= 128 ? 5 : need <= 152 ? 6 : -1;
   if (c < 0) return kBswWideBucket;
-  return bound < 256 ? c + 3 : c;
+  if (bound < 256) return c + 3;
+  // 16-bit entries for 152 columns do not fit the extension kernel's 256
+  // VGPRs (the lane wave spilled 16 of them, in the row loop): such tasks
+  // (qlen > 127 with a query N or scores >= 256 — rare under bwa) take the
+  // wave-per-task kernel instead
+  return c == 6 ? kBswWideBucket : c;
 }
 
 // No base outside A/C/G/T (code >= 4) among the n query bytes at s: aligned

@@ -22,7 +22,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--reads", type=int, default=500_000)
     ap.add_argument("--seed", type=int, default=20261015)
-    ap.add_argument("--which", default="both", choices=["c3", "fixed", "both"])
+    ap.add_argument("--which", default="both", choices=["c3", "fixed", "both", "global"])
     ap.add_argument("--reps", type=int, default=3)
     args = ap.parse_args()
     dev = torch.device("cuda", 0)
@@ -37,6 +37,10 @@ def main():
                              fixed_q=151, fixed_t=251)
         r = bench.bench_bsw(args, dev, t, reps=args.reps)
         out["fixed"] = {k: (round(v, 3) if isinstance(v, float) else v) for k, v in r.items()}
+    if args.which == "global":  # bench.py's ksw_global2 workload, scores + CIGARs (reps + 1 runs each)
+        t = fcship.synth_bsw(args.seed + 2, args.reads // 2, read_len=151, ref_len=10_000_000, w=16, mode=1,
+                             fixed_q=151, fixed_t=151)
+        out["global"] = bench.bench_bsw_global(args, dev, t, reps=args.reps)
     print(json.dumps(out))
 
 

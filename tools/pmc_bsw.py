@@ -51,6 +51,23 @@ def main():
     if fe is not None and wr is not None:
         out["c3"]["hbm_bytes_per_batch"] = int(round((fe + wr) * 1024))
         out["c3"]["fetch_kib"], out["c3"]["write_kib"] = fe, wr
+    gdir = os.path.join(src, "bswpmc_global")
+    if os.path.isdir(gdir):  # ksw_global2: scores-only and scores + CIGAR runs, 2 each (warm-up + timed)
+        tot = {}
+        for f in glob.glob(os.path.join(gdir, "**", "*counter_collection.csv"), recursive=True):
+            for r in csv.DictReader(open(f)):
+                n = r["Kernel_Name"]
+                if "bsw_global" in n and r["Counter_Name"] == "SQ_INSTS_VALU":
+                    k = "cigar" if ", true>" in n else "scores"  # bsw_global_lane_kernel<NB, CIG>
+                    tot[k] = tot.get(k, 0.0) + float(r["Counter_Value"])
+                elif "traceback" in n and r["Counter_Name"] == "SQ_INSTS_VALU":
+                    tot["traceback"] = tot.get("traceback", 0.0) + float(r["Counter_Value"])
+        g = bench_line(os.path.join(src, "bswpmc_global.log"))["global"]
+        # each mode runs twice (warm-up + timed): scores-only DP, DP with direction rows + traceback
+        out["global"] = {"band_cells": g["cells"], "tasks": g["tasks"],
+                         "dp_valu_lane_instr_per_cell": round(64 * tot.get("scores", 0) / 2 / g["cells"], 3),
+                         "dp_cigar_valu_lane_instr_per_cell": round(64 * tot.get("cigar", 0) / 2 / g["cells"], 3),
+                         "traceback_valu_wave_instr": tot.get("traceback", 0) / 2}
     out["_note"] = ("rocprofv3 --pmc of tools/bsw_bench.py --which <w> --reps 1 (separate passes: SQ issue/stall "
                     "counters, FETCH_SIZE, WRITE_SIZE), every bsw_* kernel of one ksw_extend2 batch (keys, bounds, "
                     "extension launch), halved for the warm-up batch; VALU per cell = SQ_INSTS_VALU x 64 / evaluated "
