@@ -176,11 +176,12 @@ int htc_main(int argc, char** argv) {
   create_dir(out_dir);
   const bool flag_vcf = a.has("produce-vcf");
   const auto shards = is_directory(input) ? dir_shards(a.get("intervalList")) : shard_intervals(ref, a.get("intervalList"));
+  // the GPU runtime and tables come up in the background while the first
+  // shards decode and pile up their reads (the reference's BackgroundExecutor
+  // NAM daemon runs beside its Executor the same way)
   BackgroundExecutor warm("gpu-warmup", std::make_shared<DeviceWarmupWorker>(gpus));
   Executor ex("Haplotype Caller", conf().get_int("gatk.htc.nprocs", "gatk.nprocs"), gpus);
   std::vector<std::string> parts;
-  warm.wait();
-  if (warm.status() != 0) throw failedCommand(std::string("[E::fcs-genome] GPU warm-up failed: ") + fcs_last_error());
   for (size_t k = 0; k < shards.size(); ++k) {
     const std::string part = get_contig_fname(out_dir, (int)k, flag_vcf ? "vcf" : "g.vcf");
     parts.push_back(part);
@@ -194,6 +195,8 @@ int htc_main(int argc, char** argv) {
     ex.addTask(std::make_shared<TabixWorker>(plain + ".gz"), sample_id, true);
   }
   ex.run();
+  warm.wait();
+  if (warm.status() != 0) throw failedCommand(std::string("[E::fcs-genome] GPU warm-up failed: ") + fcs_last_error());
   return 0;
 }
 
@@ -225,6 +228,7 @@ int mutect2_main(int argc, char** argv) {
   const auto shards = (is_regular_file(a.get("normal")) && is_regular_file(a.get("tumor")))
                           ? shard_intervals(ref, a.get("intervalList"))
                           : dir_shards(a.get("intervalList"));
+  BackgroundExecutor warm("gpu-warmup", std::make_shared<DeviceWarmupWorker>(gpus));
   Executor ex("Mutect2", conf().get_int("gatk.mutect2.nprocs", "gatk.nprocs"), gpus);
   std::vector<std::string> parts;
   const std::string sample_id = a.get("sample-id");
@@ -241,6 +245,8 @@ int mutect2_main(int argc, char** argv) {
   ex.addTask(std::make_shared<ZIPWorker>(output, output + ".gz", true), sample_id, true);
   ex.addTask(std::make_shared<TabixWorker>(output + ".gz"), sample_id, true);
   ex.run();
+  warm.wait();
+  if (warm.status() != 0) throw failedCommand(std::string("[E::fcs-genome] GPU warm-up failed: ") + fcs_last_error());
   return 0;
 }
 
