@@ -42,6 +42,10 @@
 
 namespace fcs {
 
+#ifndef FCS_STREAM_PFD
+#define FCS_STREAM_PFD 2
+#endif
+constexpr int kStreamPfd = FCS_STREAM_PFD;  // LDS read-ahead of the 3/2/1-wave stream classes
 constexpr int kStreamMinR = 33;  // a pair spans >= 17 units: at most two pairs per stripe and segment
 constexpr int kStreamMaxK = 8;   // pairs per segment stream
 // Hap-length bounds of the stream classes: LDS <= 10,240 B per wave (4 waves per
@@ -131,8 +135,8 @@ __device__ __forceinline__ int srole(int r, int R) { return r == 0 ? 1 : r < R ?
 // One step: phmm2_step without the byte-compare and summing variants; the
 // boundary source is this block's per-lane pointer `rd` (ring or Z) and COND
 // captures the V lanes' X at their column H + 1.
-template <bool COND, bool WRITE, int S>
-__device__ __forceinline__ void pstream_step(Lane2& L, PhRing<float> (&pf)[PFD], int (&hq)[PFD],
+template <bool COND, bool WRITE, int S, int PF>
+__device__ __forceinline__ void pstream_step(Lane2& L, PhRing<float> (&pf)[PF], int (&hq)[PF],
                                              const unsigned char* __restrict__ hp, const PhRing<float>* __restrict__ rd,
                                              const RowP2& p, const bool start, const bool top, const int t0,
                                              const int dl, float& acc, const uint32_t wbase) {
@@ -140,12 +144,12 @@ __device__ __forceinline__ void pstream_step(Lane2& L, PhRing<float> (&pf)[PFD],
   const PhRing<float> cur = pf[0];
   const int hba = hq[0];
 #pragma unroll
-  for (int k = 0; k + 1 < PFD; ++k) {
+  for (int k = 0; k + 1 < PF; ++k) {
     pf[k] = pf[k + 1];
     hq[k] = hq[k + 1];
   }
-  pf[PFD - 1] = rd[S];     // boundary input for step t + PFD
-  hq[PFD - 1] = hp[t];     // row a's hap code for column t + PFD - 2l
+  pf[PF - 1] = rd[S];     // boundary input for step t + PF
+  hq[PF - 1] = hp[t];     // row a's hap code for column t + PF - 2l
   const int hbb = L.hbp;
   L.hbp = hba;
   pf2 Xsw = L.Xn, Isw = L.In;
@@ -183,14 +187,14 @@ __device__ __forceinline__ void pstream_step(Lane2& L, PhRing<float> (&pf)[PFD],
   L.Do = D;
 }
 
-template <bool COND, bool WRITE>
-__device__ __forceinline__ void pstream_block(Lane2& L, PhRing<float> (&pf)[PFD], int (&hq)[PFD],
+template <bool COND, bool WRITE, int PF>
+__device__ __forceinline__ void pstream_block(Lane2& L, PhRing<float> (&pf)[PF], int (&hq)[PF],
                                               const unsigned char* __restrict__ hp,
                                               const PhRing<float>* __restrict__ rd, const RowP2& p, const bool start,
                                               const bool top, const int t0, const int dl, float& acc,
                                               const uint32_t wbase) {
   [&]<int... S>(std::integer_sequence<int, S...>) {
-    (pstream_step<COND, WRITE, S>(L, pf, hq, hp, rd, p, start, top, t0, dl, acc, wbase), ...);
+    (pstream_step<COND, WRITE, S, PF>(L, pf, hq, hp, rd, p, start, top, t0, dl, acc, wbase), ...);
   }(std::make_integer_sequence<int, 16>{});
 }
 
@@ -218,6 +222,8 @@ __global__ __launch_bounds__(64, LB) void phmm3_kernel(
   const int sbase = lane & 48;
   const int sl2 = 2 * sl;
   const bool top = sl == 15;
+  // LDS read-ahead (steps): the 4-wave class has no VGPRs to spare beyond 2
+  constexpr int PF = LB >= 4 ? 2 : kStreamPfd;
   PhRing<float>* const Z = reinterpret_cast<PhRing<float>*>(smem_raw);
   PhRing<float>* const ring = reinterpret_cast<PhRing<float>*>(smem_raw + 512) + seg * nslot;
   unsigned char* const hbufs = smem_raw + 512 + 32 * nslot + 2 * seg * hstride;  // this segment's two buffers
@@ -403,7 +409,7 @@ __global__ __launch_bounds__(64, LB) void phmm3_kernel(
       const int nblk = (wave_max(need) + 15) >> 4;
       const int hoff = 3 + ((cur_pk.w >> 5) & 3);
       const unsigned char* const hp =
-          (cur.act ? hbufs + (cur.k & 1) * hstride + hoff : hbufs) + PFD - sl2;  // hp[t]: column t + PFD - 2l
+          (cur.act ? hbufs + (cur.k & 1) * hstride + hoff : hbufs) + PF - sl2;  // hp[t]: column t + PF - 2l
 
       // Next stripe: its lane state, raw rows and new haplotype, all in flight
       // during this stripe.
@@ -423,30 +429,30 @@ __global__ __launch_bounds__(64, LB) void phmm3_kernel(
       // -2l for a pad row, 0 for every other source (columns < 0)
       L.Xp.y = (is_z && zsh && sl == 0) ? 1.f : 0.f;
       L.hbp = 6;
-      PhRing<float> pf[PFD];
-      int hq[PFD];
+      PhRing<float> pf[PF];
+      int hq[PF];
 #pragma unroll
-      for (int q = 0; q < PFD; ++q) {
+      for (int q = 0; q < PF; ++q) {
         pf[q] = is_z ? Z[32 + q - sl2 + zsh] : ring[q];
-        hq[q] = hp[q - PFD];
+        hq[q] = hp[q - PF];
       }
       float acc = 0.f;
       for (int blk = 0; blk < nblk; ++blk) {
         const int t0 = 16 * blk;
-        const PhRing<float>* const rd = is_z ? Z + 32 + min(t0 + PFD - sl2 + zsh, 16) : ring + t0 + PFD;
+        const PhRing<float>* const rd = is_z ? Z + 32 + min(t0 + PF - sl2 + zsh, 16) : ring + t0 + PF;
         const bool cond = __ballot(lim >= t0 && lim < t0 + 16) != 0ull;
         const uint32_t wbase = lds_addr(ring + (t0 - 31));
         const int dl = lim - t0;
         if (blk >= 2) {
           if (cond)
-            pstream_block<true, true>(L, pf, hq, hp, rd, prm, start, top, t0, dl, acc, wbase);
+            pstream_block<true, true, PF>(L, pf, hq, hp, rd, prm, start, top, t0, dl, acc, wbase);
           else
-            pstream_block<false, true>(L, pf, hq, hp, rd, prm, start, top, t0, dl, acc, wbase);
+            pstream_block<false, true, PF>(L, pf, hq, hp, rd, prm, start, top, t0, dl, acc, wbase);
         } else {
           if (cond)
-            pstream_block<true, false>(L, pf, hq, hp, rd, prm, start, top, t0, dl, acc, wbase);
+            pstream_block<true, false, PF>(L, pf, hq, hp, rd, prm, start, top, t0, dl, acc, wbase);
           else
-            pstream_block<false, false>(L, pf, hq, hp, rd, prm, start, top, t0, dl, acc, wbase);
+            pstream_block<false, false, PF>(L, pf, hq, hp, rd, prm, start, top, t0, dl, acc, wbase);
         }
       }
       if (lim >= 0) {
