@@ -1,0 +1,13 @@
+#!/bin/bash
+# rocprofv3 kernel trace of `fcs-genome htc` with 4 concurrent shard threads on
+# one GPU, and the overlap of their PairHMM passes (tools/htc_overlap.py).
+set -u
+O=$GRAFT_REPO_ROOT/gpurun_out/${1:-ovl}; mkdir -p $O
+W=$(mktemp -d /tmp/ovl.XXXX)
+export FCS_GPU_DEVICES=0 FCS_LOG_DIR=$W/log FCS_TEMP_DIR=$W FCS_GATK_NPROCS=4 TMPDIR=/tmp
+B=$GRAFT_REPO_ROOT/falcon-genome_amd/bin/fcs-genome
+timeout -k 10 300 $B synth -o $W/d -c chr1:4000000 -x 30 > /dev/null || exit 1
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/prof -o run --output-format csv -- \
+  $B htc -r $W/d/ref.fasta -i $W/d/sample.bam -o $W/h.g.vcf > $O/htc.log 2>&1 || { tail $O/htc.log; exit 1; }
+python3 $GRAFT_REPO_ROOT/tools/htc_overlap.py $O/prof/run_kernel_trace.csv | tee $O/overlap.json
+rm -rf $W
