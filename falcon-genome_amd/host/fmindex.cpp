@@ -9,57 +9,58 @@ namespace fcsg {
 
 namespace {
 
-constexpr uint32_t kEmpty = 0xFFFFFFFFu;
+template <typename I>
+constexpr I kEmpty = ~I(0);
 
-void buckets(const uint32_t* s, int64_t n, int K, std::vector<int64_t>& bkt, bool end) {
+template <typename C>
+void buckets(const C* s, int64_t n, int64_t K, std::vector<int64_t>& bkt, bool end) {
   std::fill(bkt.begin(), bkt.end(), 0);
   for (int64_t i = 0; i < n; ++i) ++bkt[s[i]];
   int64_t sum = 0;
-  for (int c = 0; c < K; ++c) {
+  for (int64_t c = 0; c < K; ++c) {
     sum += bkt[c];
     bkt[c] = end ? sum : sum - bkt[c];
   }
 }
 
-void induce(const uint32_t* s, uint32_t* sa, int64_t n, int K, const std::vector<uint8_t>& t,
-            std::vector<int64_t>& bkt) {
+template <typename C, typename I>
+void induce(const C* s, I* sa, int64_t n, int64_t K, const std::vector<uint8_t>& t, std::vector<int64_t>& bkt) {
   buckets(s, n, K, bkt, false);  // L-type suffixes, left to right from bucket starts
   for (int64_t i = 0; i < n; ++i) {
-    if (sa[i] == kEmpty || sa[i] == 0) continue;
+    if (sa[i] == kEmpty<I> || sa[i] == 0) continue;
     const int64_t j = (int64_t)sa[i] - 1;
-    if (!t[j]) sa[bkt[s[j]]++] = (uint32_t)j;
+    if (!t[j]) sa[bkt[s[j]]++] = (I)j;
   }
   buckets(s, n, K, bkt, true);  // S-type suffixes, right to left from bucket ends
   for (int64_t i = n - 1; i >= 0; --i) {
-    if (sa[i] == kEmpty || sa[i] == 0) continue;
+    if (sa[i] == kEmpty<I> || sa[i] == 0) continue;
     const int64_t j = (int64_t)sa[i] - 1;
-    if (t[j]) sa[--bkt[s[j]]] = (uint32_t)j;
+    if (t[j]) sa[--bkt[s[j]]] = (I)j;
   }
 }
 
-}  // namespace
-
 // SA-IS (Nong, Zhang and Chan 2009): sort the LMS substrings by induction,
-// name them, recurse on the reduced string when names repeat, then induce
-// the full order from the sorted LMS suffixes.
-void sais(const uint32_t* s, uint32_t* sa, int64_t n, int K) {
+// name them, recurse on the reduced string (stored in the SA's upper half)
+// when names repeat, then induce the full order from the sorted LMS suffixes.
+template <typename C, typename I>
+void sais_t(const C* s, I* sa, int64_t n, int64_t K) {
   std::vector<uint8_t> t(n);  // 1 = S-type
   t[n - 1] = 1;
   for (int64_t i = n - 2; i >= 0; --i) t[i] = s[i] < s[i + 1] || (s[i] == s[i + 1] && t[i + 1]);
   auto lms = [&](int64_t i) { return i > 0 && t[i] && !t[i - 1]; };
   std::vector<int64_t> bkt(K);
-  std::fill(sa, sa + n, kEmpty);
+  std::fill(sa, sa + n, kEmpty<I>);
   buckets(s, n, K, bkt, true);
   for (int64_t i = 1; i < n; ++i)
-    if (lms(i)) sa[--bkt[s[i]]] = (uint32_t)i;
+    if (lms(i)) sa[--bkt[s[i]]] = (I)i;
   induce(s, sa, n, K, t, bkt);
   int64_t n1 = 0;
   for (int64_t i = 0; i < n; ++i)
-    if (sa[i] != kEmpty && lms(sa[i])) sa[n1++] = sa[i];
-  std::fill(sa + n1, sa + n, kEmpty);
+    if (sa[i] != kEmpty<I> && lms((int64_t)sa[i])) sa[n1++] = sa[i];
+  std::fill(sa + n1, sa + n, kEmpty<I>);
   int64_t name = 0, prev = -1;
   for (int64_t i = 0; i < n1; ++i) {
-    const int64_t pos = sa[i];
+    const int64_t pos = (int64_t)sa[i];
     bool diff = false;
     for (int64_t d = 0; d < n; ++d) {
       if (prev == -1 || s[pos + d] != s[prev + d] || t[pos + d] != t[prev + d]) {
@@ -72,60 +73,63 @@ void sais(const uint32_t* s, uint32_t* sa, int64_t n, int K) {
       ++name;
       prev = pos;
     }
-    sa[n1 + pos / 2] = (uint32_t)(name - 1);
+    sa[n1 + pos / 2] = (I)(name - 1);
   }
   for (int64_t i = n - 1, j = n - 1; i >= n1; --i)
-    if (sa[i] != kEmpty) sa[j--] = sa[i];
-  uint32_t* s1 = sa + n - n1;
+    if (sa[i] != kEmpty<I>) sa[j--] = sa[i];
+  I* s1 = sa + n - n1;
   if (name < n1) {
-    sais(s1, sa, n1, (int)name);
+    sais_t<I, I>(s1, sa, n1, name);
   } else {
-    for (int64_t i = 0; i < n1; ++i) sa[s1[i]] = (uint32_t)i;
+    for (int64_t i = 0; i < n1; ++i) sa[s1[i]] = (I)i;
   }
   for (int64_t i = 1, j = 0; i < n; ++i)
-    if (lms(i)) s1[j++] = (uint32_t)i;
+    if (lms(i)) s1[j++] = (I)i;
   for (int64_t i = 0; i < n1; ++i) sa[i] = s1[sa[i]];
-  std::fill(sa + n1, sa + n, kEmpty);
+  std::fill(sa + n1, sa + n, kEmpty<I>);
   buckets(s, n, K, bkt, true);
   for (int64_t i = n1 - 1; i >= 0; --i) {
-    const uint32_t j = sa[i];
-    sa[i] = kEmpty;
+    const I j = sa[i];
+    sa[i] = kEmpty<I>;
     sa[--bkt[s[j]]] = j;
   }
   induce(s, sa, n, K, t, bkt);
 }
 
+}  // namespace
+
+void sais(const uint8_t* s, uint64_t* sa, int64_t n, int K) { sais_t<uint8_t, uint64_t>(s, sa, n, K); }
+
 FmdIndex::FmdIndex(const std::vector<std::vector<uint8_t>>& contigs) {
   // F = 5 C_1 5 C_2 ... 5 C_n 5;  T = F revcomp(F) $
-  std::vector<uint32_t> T;
+  std::vector<uint8_t> T;
   int64_t total = 1;
   for (const auto& c : contigs) total += (int64_t)c.size() + 1;
-  if (2 * total + 1 >= (int64_t)kEmpty) throw invalidParam("FMD-index: reference too long for 32-bit positions");
   T.reserve(2 * total + 1);
   for (const auto& c : contigs) {
     T.push_back(5);
     cstart_.push_back((int64_t)T.size());
     clen_.push_back((int64_t)c.size());
-    for (uint8_t b : c) T.push_back(b < 4 ? b + 1u : 5u);
+    for (uint8_t b : c) T.push_back(b < 4 ? (uint8_t)(b + 1) : (uint8_t)5);
   }
   T.push_back(5);
   flen_ = (int64_t)T.size();
-  for (int64_t i = flen_ - 1; i >= 0; --i) T.push_back(T[i] == 5 ? 5u : 5u - T[i]);
+  for (int64_t i = flen_ - 1; i >= 0; --i) T.push_back(T[i] == 5 ? (uint8_t)5 : (uint8_t)(5 - T[i]));
   T.push_back(0);
   n_ = (int64_t)T.size();
   sa_.resize(n_);
   sais(T.data(), sa_.data(), n_, 6);
   C_.assign(7, 0);
-  for (uint32_t c : T) ++C_[c + 1];
+  for (uint8_t c : T) ++C_[c + 1];
   for (int c = 1; c < 7; ++c) C_[c] += C_[c - 1];
   const int64_t nb = (n_ + 63) / 64;
   bits_.assign(4 * nb, 0);
   cnt_.assign(4 * nb, 0);
-  uint32_t run[4] = {0, 0, 0, 0};
+  uint64_t run[4] = {0, 0, 0, 0};
   for (int64_t b = 0; b < nb; ++b) {
     for (int c = 0; c < 4; ++c) cnt_[4 * b + c] = run[c];
     for (int64_t i = 64 * b; i < std::min(n_, 64 * b + 64); ++i) {
-      const uint32_t p = sa_[i];
+      const uint64_t p = sa_[i];
       const uint32_t ch = p ? T[p - 1] : 0;  // BWT symbol
       if (ch >= 1 && ch <= 4) {
         bits_[4 * b + ch - 1] |= 1ull << (i & 63);

@@ -50,15 +50,15 @@ class FmdIndex {
   void set_intv(int c, BiInterval& iv) const;
   int64_t n_ = 0, flen_ = 0;
   std::vector<int64_t> C_;               // C_[c] = symbols < c
-  std::vector<uint32_t> sa_;             // suffix array (n < 2^32)
+  std::vector<uint64_t> sa_;             // suffix array
   std::vector<uint64_t> bits_;           // per 64-block: bit vectors of A, C, G, T
-  std::vector<uint32_t> cnt_;            // per 64-block: counts of A, C, G, T before the block
+  std::vector<uint64_t> cnt_;            // per 64-block: counts of A, C, G, T before the block
   std::vector<int64_t> cstart_;          // forward-text start of each contig
   std::vector<int64_t> clen_;
 };
 
 // SA-IS suffix array of s[0, n) over the alphabet [0, K) with s[n-1] == 0
-// unique and smallest.
-void sais(const uint32_t* s, uint32_t* sa, int64_t n, int K);
+// unique and smallest (64-bit positions: whole human references fit).
+void sais(const uint8_t* s, uint64_t* sa, int64_t n, int K);
 
 }  // namespace fcsg
