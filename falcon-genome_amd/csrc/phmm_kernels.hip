@@ -584,7 +584,10 @@ int launch_phmm_forward(const PhmmDevBatch& b, const int32_t* order, int64_t cou
       FCS_HIP_CHECK(hipGetLastError());
       return FCS_OK;
     };
-    const int rc = w >= 4 ? launch(phmm3_kernel<4>) : w == 3 ? launch(phmm3_kernel<3>)
+#ifndef FCS_STREAM_LB4
+#define FCS_STREAM_LB4 1
+#endif
+    const int rc = (w >= 4 && FCS_STREAM_LB4) ? launch(phmm3_kernel<4>) : w >= 3 ? launch(phmm3_kernel<3>)
                  : w == 2 ? launch(phmm3_kernel<2>) : launch(phmm3_kernel<1>);
     if (rc != FCS_OK) return rc;
   }
