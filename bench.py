@@ -367,6 +367,13 @@ def bsw_roofline(r3, rf):
         ach = r3["gcups"] * 1e9 * per3
         out.update(achieved=round(ach / 1e12, 3), frac=round(ach / VALU_LANE_INSTR_PEAK, 4),
                    valu_instr_per_cell=per3, valu_source=meas.get("source"))
+    try:
+        ck = json.load(open(os.path.join(ROOT, "profiles", "clock.json"))).get("bsw_ext")
+    except (OSError, ValueError):
+        ck = None
+    if per3 and ck:
+        out["effective_clock_ghz"] = ck
+        out["frac_at_effective_clock"] = round(r3["gcups"] * 1e9 * per3 / (VALU_LANE_INSTR_PEAK * ck / 2.4), 4)
     if perf:
         out["fixed_frac"] = round(rf["gcups"] * 1e9 * perf / VALU_LANE_INSTR_PEAK, 4)
         out["fixed_valu_instr_per_cell"] = perf
@@ -421,6 +428,10 @@ def main():
     achieved_tf = FLOPS_PER_CELL * ph["cells"] / fwd_s / 1e12
     traffic = load_traffic("phmm_fwd_fp32")
     pmc, pmc_src = load_pmc_phmm()
+    try:
+        clk = json.load(open(os.path.join(ROOT, "profiles", "clock.json")))
+    except (OSError, ValueError):
+        clk = {}
     vipc = pmc.get("valu_lane_instr_per_cell")
     p = ph["p"]
     alg_bytes = int(5 * p.read_len.sum() + p.hap_len.sum() + 4 * p.n_pairs + 8 * p.n_pairs)
@@ -455,6 +466,10 @@ def main():
                      "valu_issue_frac": (round(ph["cells"] / fwd_s * vipc / VALU_LANE_INSTR_PEAK, 4) if vipc
                                          else None),
                      "valu_source": f"profiles/pmc_phmm.json ({pmc_src}: SQ_INSTS_VALU x 64 / cells)",
+                     "effective_clock_ghz": clk.get("phmm_fwd_fp32"),
+                     "valu_issue_frac_at_effective_clock": (
+                         round(ph["cells"] / fwd_s * vipc / (VALU_LANE_INSTR_PEAK * clk["phmm_fwd_fp32"] / 2.4), 4)
+                         if vipc and clk.get("phmm_fwd_fp32") else None),
                      "kernel_gcups": round(ph["cells"] / fwd_s / 1e9, 3),
                      "algorithmic_bytes_per_launch": alg_bytes,
                      "algorithmic_hbm_GBs": round(alg_bytes / fwd_s / 1e9, 2),
