@@ -99,8 +99,8 @@ int64_t aln_pos(const Cand& c) { return c.aln.rb; }
 int64_t aln_end(const Cand& c) { return c.aln.re; }
 
 // Seeds and chains of one read (bwa mem_collect_intv + mem_chain): SMEMs of
-// length >= min_seed_len on the FMD-index (both strands at once) and re-seeds
-// inside long, rare SMEMs; every occurrence (sampled down to max_occ per
+// length >= min_seed_len on the FMD-index (both strands at once), re-seeds
+// inside long, rare SMEMs and the third-round forward seeds; every occurrence (sampled down to max_occ per
 // SMEM) is a seed; seeds join a chain of the same contig and strand when they
 // continue it (bwa test_and_merge: colinear, diagonal within w, gaps below
 // max_chain_gap); chains weighed by the query bases their seeds cover; up to
@@ -110,7 +110,7 @@ void seed_read(const Reference& ref, const KmerIndex& idx, const AlignOptions& o
   const std::vector<uint8_t>& q = R.code[0];
   const int L = (int)q.size();
   std::vector<BiInterval> mems;
-  idx.fmd().collect(q.data(), L, opt.k, (int)(opt.k * 1.5 + .499), 10, mems);
+  idx.fmd().collect(q.data(), L, opt.k, (int)(opt.k * 1.5 + .499), 10, 20, mems);  // bwa -r 1.5, -y 20
   struct Seed {
     int contig;
     bool rev;

@@ -100,13 +100,14 @@ int fcsg_intersect_regions(const char* const* paths, int n, char* buf, int cap) 
 
 int fcsg_gvcf_band(int gq) { return gvcf_band(gq); }
 
-// SMEM seeding on an FMD-index of the given contigs (codes 0..4): SMEMs of q
-// (bwa mem_collect_intv rounds 1-2), out = {qb, qe, occurrences} per SMEM and
+// SMEM seeding on an FMD-index of the given contigs (codes 0..4): seeds of q
+// (bwa mem_collect_intv; max_mem_intv 0 skips its third round), out = {qb, qe, occurrences} per SMEM and
 // loc = {contig, offset, reverse} of every occurrence (at most loc_cap rows,
 // SMEM by SMEM, each SMEM's occurrences in suffix-array order).  Returns the
 // SMEM count, or < 0 on error.
 int fcsg_fmd_smems(const uint8_t* ref, const int64_t* clen, int ncontig, const uint8_t* q, int qlen, int min_len,
-                   int split_len, int split_width, int32_t* out, int cap, int64_t* loc, int loc_cap) {
+                   int split_len, int split_width, int max_mem_intv, int32_t* out, int cap, int64_t* loc,
+                   int loc_cap) {
   int n = -1;
   const int rc = guard([&] {
     std::vector<std::vector<uint8_t>> cs;
@@ -117,7 +118,7 @@ int fcsg_fmd_smems(const uint8_t* ref, const int64_t* clen, int ncontig, const u
     }
     const FmdIndex fmd(cs);
     std::vector<BiInterval> v;
-    fmd.collect(q, qlen, min_len, split_len, split_width, v);
+    fmd.collect(q, qlen, min_len, split_len, split_width, max_mem_intv, v);
     if ((int)v.size() > cap) throw invalidParam("fcsg_fmd_smems: capacity");
     int64_t nl = 0;
     for (size_t i = 0; i < v.size(); ++i) {

@@ -232,7 +232,7 @@ int FmdIndex::smem1(const uint8_t* q, int len, int x, int64_t min_intv, std::vec
   return ret;
 }
 
-void FmdIndex::collect(const uint8_t* q, int len, int min_len, int split_len, int split_width,
+void FmdIndex::collect(const uint8_t* q, int len, int min_len, int split_len, int split_width, int64_t max_mem_intv,
                        std::vector<BiInterval>& out) const {
   out.clear();
   std::vector<BiInterval> m;
@@ -252,6 +252,38 @@ void FmdIndex::collect(const uint8_t* q, int len, int min_len, int split_len, in
     smem1(q, len, (p.qb + p.qe) >> 1, p.s + 1, m);
     for (const BiInterval& r : m)
       if (r.qe - r.qb >= min_len) out.push_back(r);
+  }
+  if (max_mem_intv > 0) {  // third round (bwt_seed_strategy1): the first forward match of
+    // length >= min_len from each x with fewer than max_mem_intv occurrences
+    for (int x = 0; x < len;) {
+      if (q[x] > 3) {
+        ++x;
+        continue;
+      }
+      BiInterval ik, ok[5];
+      set_intv(q[x] + 1, ik);
+      int next = len;
+      for (int i = x + 1; i < len; ++i) {
+        if (q[i] > 3) {
+          next = i + 1;
+          break;
+        }
+        extend(ik, ok, false);
+        const BiInterval& o = ok[4 - q[i]];
+        if (o.s < max_mem_intv && i - x >= min_len) {
+          if (o.s > 0) {
+            BiInterval m = o;
+            m.qb = x;
+            m.qe = i + 1;
+            out.push_back(m);
+          }
+          next = i + 1;
+          break;
+        }
+        ik = o;
+      }
+      x = next;
+    }
   }
   std::stable_sort(out.begin(), out.end(), [](const BiInterval& a, const BiInterval& b) {
     return a.qb != b.qb ? a.qb < b.qb : a.qe < b.qe;

@@ -10,8 +10,9 @@
 // plus block counts.  A bi-interval (k, l, s) holds the SA interval of P
 // (k, s) and of revcomp(P) (l, s), so P extends in both directions (bwa's
 // bwt_extend); bwt_smem1 finds, for a query position x, the SMEMs overlapping
-// x, and mem_collect_intv's first two rounds (all SMEMs of length >= min_len,
-// then re-seeding inside long SMEMs with few occurrences) give the seeds.
+// x, and mem_collect_intv's three rounds (all SMEMs of length >= min_len,
+// re-seeding inside long SMEMs with few occurrences, and the LAST-like forward
+// seeds of bwt_seed_strategy1) give the seeds.
 #pragma once
 
 #include <cstdint>
@@ -35,9 +36,12 @@ class FmdIndex {
   // bwt_smem1: SMEMs of q (codes 0..4) overlapping position x with at least
   // min_intv occurrences; returns the next start position (bwa's return value).
   int smem1(const uint8_t* q, int len, int x, int64_t min_intv, std::vector<BiInterval>& out) const;
-  // mem_collect_intv rounds 1-2: SMEMs of length >= min_len, plus re-seeds
-  // inside SMEMs longer than split_len with <= split_width occurrences.
-  void collect(const uint8_t* q, int len, int min_len, int split_len, int split_width,
+  // mem_collect_intv: SMEMs of length >= min_len; re-seeds inside SMEMs longer
+  // than split_len with <= split_width occurrences; when max_mem_intv > 0, the
+  // third round (bwt_seed_strategy1: from each x, the first forward match of
+  // length >= min_len with fewer than max_mem_intv occurrences).  Sorted by
+  // query start.
+  void collect(const uint8_t* q, int len, int min_len, int split_len, int split_width, int64_t max_mem_intv,
                std::vector<BiInterval>& out) const;
   // Occurrence j (< s) of interval iv: contig, forward-strand offset of the
   // match start, and whether the match is on the reverse strand (then the

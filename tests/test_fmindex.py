@@ -27,7 +27,7 @@ def make_ref(rng):
     return contigs
 
 
-def smems(contigs, q, min_len=1, split_len=10**9, split_width=10, loc_cap=100000):
+def smems(contigs, q, min_len=1, split_len=10**9, split_width=10, max_mem_intv=0, loc_cap=100000):
     code = {"A": 0, "C": 1, "G": 2, "T": 3}
     ref = np.array([code.get(b, 4) for b in "".join(contigs)], np.uint8)
     cl = np.array([len(c) for c in contigs], np.int64)
@@ -35,7 +35,7 @@ def smems(contigs, q, min_len=1, split_len=10**9, split_width=10, loc_cap=100000
     out = np.zeros((4 * len(q) + 8, 3), np.int32)
     loc = np.zeros((loc_cap, 3), np.int64)
     n = H.lib.fcsg_fmd_smems(ref.ctypes.data_as(C.c_void_p), cl.ctypes.data_as(C.c_void_p), len(contigs),
-                             qa.ctypes.data_as(C.c_void_p), len(q), min_len, split_len, split_width,
+                             qa.ctypes.data_as(C.c_void_p), len(q), min_len, split_len, split_width, max_mem_intv,
                              out.ctypes.data_as(C.c_void_p), len(out), loc.ctypes.data_as(C.c_void_p), loc_cap)
     assert n >= 0, H.lib.fcsg_last_error()
     return [tuple(int(x) for x in r) for r in out[:n]], loc
@@ -108,3 +108,28 @@ def test_reseeding_finds_shorter_repeated_seeds():
     assert got == [(0, 70, 1)]
     got, _ = smems(contigs, q, min_len=19, split_len=28, split_width=10)
     assert (0, 70, 1) in got and any(s >= 2 and e - b >= 19 for b, e, s in got), got
+
+
+def test_third_round_forward_seeds():
+    """bwt_seed_strategy1: from each x, the first forward extension of length
+    >= min_len whose occurrence count drops below max_mem_intv; the next x is
+    one past its end."""
+    rng = np.random.default_rng(8)
+    contigs = make_ref(rng)
+    texts = contigs + [revcomp(c) for c in contigs]
+    q = contigs[1][480:600]
+    got, _ = smems(contigs, q, min_len=19, split_len=10**9, max_mem_intv=20)
+    smem_only, _ = smems(contigs, q, min_len=19, split_len=10**9, max_mem_intv=0)
+    third = [g for g in got if g not in smem_only or got.count(g) > smem_only.count(g)]
+    want, x = [], 0
+    while x < len(q):
+        nxt = len(q)
+        for i in range(x + 1, len(q)):
+            c = count_occ(texts, q[x:i + 1])
+            if c < 20 and i - x >= 19:
+                if c > 0:
+                    want.append((x, i + 1, c))
+                nxt = i + 1
+                break
+        x = nxt
+    assert sorted(third) == sorted(want)
