@@ -42,6 +42,10 @@
 
 namespace fcs {
 
+#ifndef FCS_STREAM_HALF
+#define FCS_STREAM_HALF 8
+#endif
+constexpr int kStreamHalf = FCS_STREAM_HALF;  // a stripe's last block runs 8 steps when that suffices (0: never)
 #ifndef FCS_STREAM_PFD
 #define FCS_STREAM_PFD 2
 #endif
@@ -187,7 +191,7 @@ __device__ __forceinline__ void pstream_step(Lane2& L, PhRing<float> (&pf)[PF], 
   L.Do = D;
 }
 
-template <bool COND, bool WRITE, int PF>
+template <bool COND, bool WRITE, int PF, int NS = 16>
 __device__ __forceinline__ void pstream_block(Lane2& L, PhRing<float> (&pf)[PF], int (&hq)[PF],
                                               const unsigned char* __restrict__ hp,
                                               const PhRing<float>* __restrict__ rd, const RowP2& p, const bool start,
@@ -195,7 +199,7 @@ __device__ __forceinline__ void pstream_block(Lane2& L, PhRing<float> (&pf)[PF],
                                               const uint32_t wbase) {
   [&]<int... S>(std::integer_sequence<int, S...>) {
     (pstream_step<COND, WRITE, S, PF>(L, pf, hq, hp, rd, p, start, top, t0, dl, acc, wbase), ...);
-  }(std::make_integer_sequence<int, 16>{});
+  }(std::make_integer_sequence<int, NS>{});
 }
 
 // Hap bytes -> codes (A,C,G,T,N = 0..4), four per dword: (b >> 1) & 7 is
@@ -406,7 +410,11 @@ __global__ __launch_bounds__(64, LB) void phmm3_kernel(
       const int zsh = (cur.role_a == 1) ? 1 : 0;  // the pad row reads Z one column on
       const int lim = (cur.role_b == 4) ? cur.H + sl2 + 2 : -1;  // V at its column H + 1
       const int need = cur.act ? cur.H + sl2 + 3 : 0;
-      const int nblk = (wave_max(need) + 15) >> 4;
+      // 16-step blocks, and an 8-step block when the stripe's last block would
+      // need no more than 8 steps
+      const int nmax = wave_max(need);
+      const int nblk = (nmax >> 4) + ((nmax & 15) > kStreamHalf ? 1 : 0);
+      const bool half = (nmax & 15) != 0 && (nmax & 15) <= kStreamHalf;
       const int hoff = 3 + ((cur_pk.w >> 5) & 3);
       const unsigned char* const hp =
           (cur.act ? hbufs + (cur.k & 1) * hstride + hoff : hbufs) + PF - sl2;  // hp[t]: column t + PF - 2l
@@ -453,6 +461,24 @@ __global__ __launch_bounds__(64, LB) void phmm3_kernel(
             pstream_block<true, false, PF>(L, pf, hq, hp, rd, prm, start, top, t0, dl, acc, wbase);
           else
             pstream_block<false, false, PF>(L, pf, hq, hp, rd, prm, start, top, t0, dl, acc, wbase);
+        }
+      }
+      if (half) {
+        const int t0 = 16 * nblk;
+        const PhRing<float>* const rd = is_z ? Z + 32 + min(t0 + PF - sl2 + zsh, 16) : ring + t0 + PF;
+        const bool cond = __ballot(lim >= t0 && lim < t0 + 8) != 0ull;
+        const uint32_t wbase = lds_addr(ring + (t0 - 31));
+        const int dl = lim - t0;
+        if (nblk >= 2) {
+          if (cond)
+            pstream_block<true, true, PF, 8>(L, pf, hq, hp, rd, prm, start, top, t0, dl, acc, wbase);
+          else
+            pstream_block<false, true, PF, 8>(L, pf, hq, hp, rd, prm, start, top, t0, dl, acc, wbase);
+        } else {
+          if (cond)
+            pstream_block<true, false, PF, 8>(L, pf, hq, hp, rd, prm, start, top, t0, dl, acc, wbase);
+          else
+            pstream_block<false, false, PF, 8>(L, pf, hq, hp, rd, prm, start, top, t0, dl, acc, wbase);
         }
       }
       if (lim >= 0) {
