@@ -15,6 +15,7 @@
 #include <map>
 #include <memory>
 #include <mutex>
+#include <thread>
 #include <vector>
 
 #include "fcship_internal.h"
@@ -670,6 +671,73 @@ int phmm_staged(const PhmmStage& g, const fcs_phmm_opts& opts, Fill&& fill, cons
 
 extern "C" {
 
+int fcs_phmm_partition(const fcs_phmm_batch* b, int32_t n_slices, int64_t* cuts) {
+  int rc = check_batch_shape(b);
+  if (rc) return rc;
+  if (n_slices <= 0 || !cuts) return fail(FCS_ERR_INVALID, "[E::fcs_phmm_partition] need n_slices > 0 and cuts");
+  const int64_t n = b->n_pairs;
+  std::vector<double> cum((size_t)n);
+  double run = 0;
+  for (int64_t p = 0; p < n; ++p) {
+    const int32_t ri = b->pair_read[p], hi = b->pair_hap[p];
+    if (ri < 0 || ri >= b->n_reads || hi < 0 || hi >= b->n_haps)
+      return fail(FCS_ERR_INVALID, "[E::fcs_phmm_partition] pair index out of range");
+    run += (double)b->read_len[ri] * (double)b->hap_len[hi];
+    cum[p] = run;
+  }
+  // the cut where the running cost first reaches k/n of the total
+  // (falcon-genome_amd/sharding.py balanced_slices, its test oracle)
+  cuts[0] = 0;
+  for (int32_t k = 1; k < n_slices; ++k) {
+    int64_t c;
+    if (n == 0) c = 0;
+    else if (run > 0) c = (int64_t)(std::lower_bound(cum.begin(), cum.end(), run * k / n_slices) - cum.begin()) + 1;
+    else c = n * k / n_slices;
+    cuts[k] = std::max(cuts[k - 1], std::min(c, n));
+  }
+  cuts[n_slices] = n;
+  return FCS_OK;
+}
+
+int fcs_phmm_compute_pairs_multi(const fcs_phmm_batch* b, double* out_log10, const fcs_phmm_opts* opts_in,
+                                 const int32_t* devices, int32_t n_devices) {
+  if (n_devices <= 0 || !devices) return fail(FCS_ERR_INVALID, "[E::fcs_phmm_compute_pairs_multi] no devices");
+  std::vector<int64_t> cuts((size_t)n_devices + 1);
+  int rc = fcs_phmm_partition(b, n_devices, cuts.data());
+  if (rc) return rc;
+  if (b->n_pairs > 0 && !out_log10) return fail(FCS_ERR_INVALID, "[E::fcs_phmm_compute_pairs_multi] null output");
+  fcs_phmm_opts opts;
+  if (opts_in) opts = *opts_in;
+  else fcs_phmm_opts_default(&opts);
+  std::vector<int> rcs((size_t)n_devices, FCS_OK);
+  std::vector<std::string> errs((size_t)n_devices);
+  std::vector<int64_t> resc((size_t)n_devices, 0);
+  std::vector<std::thread> th;
+  for (int32_t k = 0; k < n_devices; ++k) {
+    if (cuts[k + 1] == cuts[k]) continue;
+    th.emplace_back([&, k] {
+      fcs_phmm_batch sub = *b;
+      sub.pair_read = b->pair_read + cuts[k];
+      sub.pair_hap = b->pair_hap + cuts[k];
+      sub.n_pairs = cuts[k + 1] - cuts[k];
+      fcs_phmm_opts o = opts;
+      o.device = devices[k];
+      rcs[k] = fcs_phmm_compute_pairs(&sub, out_log10 + cuts[k], &o);
+      if (rcs[k] != FCS_OK) errs[k] = fcs_last_error();
+      int64_t r = 0;
+      if (fcs_phmm_last_rescued(&r) == FCS_OK) resc[k] = r;
+    });
+  }
+  for (auto& t : th) t.join();
+  int64_t tot = 0;
+  for (int32_t k = 0; k < n_devices; ++k) {
+    if (rcs[k] != FCS_OK) return fail(rcs[k], errs[k]);
+    tot += resc[k];
+  }
+  g_last_rescued = tot;
+  return FCS_OK;
+}
+
 int fcs_phmm_compute_pairs(const fcs_phmm_batch* b, double* out_log10, const fcs_phmm_opts* opts_in) {
   int rc = check_batch_shape(b);
   if (rc) return rc;
@@ -1187,6 +1255,6 @@ int fcs_ksw_global2(int qlen, const uint8_t* query, int tlen, const uint8_t* tar
   return score;
 }
 
-int fcs_abi_symbol_count(void) { return 33; }
+int fcs_abi_symbol_count(void) { return 35; }
 
 }  // extern "C"

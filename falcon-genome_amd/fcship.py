@@ -131,6 +131,9 @@ _sig("fcs_phmm_dev_run", C.c_int, [C.c_void_p, C.POINTER(PhmmBatch), C.c_void_p,
 _sig("fcs_phmm_plan_rescue_count", C.c_int, [C.c_void_p, C.c_void_p, i64p])
 _sig("fcs_phmm_last_rescued", C.c_int, [i64p])
 _sig("fcs_phmm_last_device_ms", C.c_int, [C.POINTER(C.c_double), C.POINTER(C.c_double)])
+_sig("fcs_phmm_partition", C.c_int, [C.POINTER(PhmmBatch), C.c_int32, C.c_void_p])
+_sig("fcs_phmm_compute_pairs_multi", C.c_int, [C.POINTER(PhmmBatch), C.c_void_p, C.POINTER(PhmmOpts), C.c_void_p,
+                                               C.c_int32])
 _sig("fcs_bsw_params_default", None, [C.POINTER(BswParams)])
 _sig("fcs_bsw_extend", C.c_int, [C.POINTER(BswTask), C.c_int32, C.POINTER(BswParams), C.POINTER(BswResult),
                                  C.c_int32])
@@ -256,6 +259,23 @@ def phmm_compute_pairs(p: PhmmPairs, **kw) -> np.ndarray:
     b = p.to_struct()
     o = phmm_opts(**kw)
     check(lib.fcs_phmm_compute_pairs(C.byref(b), out.ctypes.data_as(f64p), C.byref(o)))
+    return out
+
+
+def phmm_partition(p: PhmmPairs, n: int) -> np.ndarray:
+    """Cut points of the multi-GPU static partition (cuts[0..n])."""
+    cuts = np.zeros(n + 1, dtype=np.int64)
+    b = p.to_struct()
+    check(lib.fcs_phmm_partition(C.byref(b), n, cuts.ctypes.data))
+    return cuts
+
+
+def phmm_compute_pairs_multi(p: PhmmPairs, devices, **kw) -> np.ndarray:
+    out = np.zeros(p.n_pairs, dtype=np.float64)
+    b = p.to_struct()
+    o = phmm_opts(**kw)
+    d = np.asarray(devices, dtype=np.int32)
+    check(lib.fcs_phmm_compute_pairs_multi(C.byref(b), out.ctypes.data, C.byref(o), d.ctypes.data, len(d)))
     return out
 
 

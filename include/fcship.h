@@ -147,6 +147,17 @@ int fcs_phmm_compute_pairs(const fcs_phmm_batch* b, double* out_log10, const fcs
 /* Device-resident path.  A plan owns the scratch (schedule, sort temp storage,
  * rescue list) for batches up to max_pairs pairs. */
 typedef struct fcs_phmm_plan fcs_phmm_plan;
+/* Multi-GPU static partition of one pair batch (the
+ * reference's GPU/host placement is src/Executor.cpp:262): the pairs are cut
+ * into n contiguous slices of ~equal total R*H cells (the cut where the
+ * running cost first reaches k/n of the total; cuts[0..n], cuts[n] = n_pairs)
+ * and each slice runs on its device from its own host thread, writing its
+ * disjoint slice of out_log10.  No collective; results equal the one-device
+ * call's.  fcs_phmm_last_rescued reports the sum over the slices. */
+int fcs_phmm_partition(const fcs_phmm_batch* b, int32_t n_slices, int64_t* cuts);
+int fcs_phmm_compute_pairs_multi(const fcs_phmm_batch* b, double* out_log10, const fcs_phmm_opts* opts,
+                                 const int32_t* devices, int32_t n_devices);
+
 int fcs_phmm_plan_create(int32_t device, int64_t max_pairs, fcs_phmm_plan** plan);
 int fcs_phmm_plan_destroy(fcs_phmm_plan* plan);
 /* Stage 1: order pairs into 4-pair wave groups by (read len, hap len). */

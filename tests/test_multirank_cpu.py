@@ -77,3 +77,17 @@ def test_two_rank_gloo_partition():
         assert p.exitcode == 0
     mn, mx, el = q.get(timeout=10)
     assert mn == 1 and mx == 1 and el == 1.5
+
+
+def test_product_partition_matches_sharding_plan():
+    """The C-ABI's multi-GPU split (fcs_phmm_partition, used by
+    fcs_phmm_compute_pairs_multi) cuts exactly where sharding.balanced_slices
+    does over the pairs' R*H costs (host-only: no device call)."""
+    import fcship
+    for seed, n_pairs in ((1, 5000), (2, 777), (3, 1)):
+        p = fcship.synth_phmm(seed, n_pairs, R=101, hmin=150, hmax=300)
+        costs = p.read_len[p.pair_read].astype(np.int64) * p.hap_len[p.pair_hap].astype(np.int64)
+        for n in (1, 2, 3, 8):
+            cuts = fcship.phmm_partition(p, n)
+            want = sharding.balanced_slices(costs, n)
+            assert [(int(cuts[k]), int(cuts[k + 1])) for k in range(n)] == want, (seed, n)

@@ -360,3 +360,28 @@ def test_streamed_segments_forced_k(gpu, tmp_path, k):
     assert "DONE" in r.stdout, r.stderr[-3000:]
     check_parity(mixed, np.load(tmp_path / "mixed_out.npy"), False)
     check_parity(c2, np.load(tmp_path / "c2_out.npy"), False)
+
+
+def test_multi_device_static_partition(gpu):
+    """fcs_phmm_compute_pairs_multi (SURVEY.md §8e static partition): slices of
+    ~equal R*H cells on several device slots (all device 0 on a one-GPU box —
+    the split and the per-slice runs are the same code as over 8 devices),
+    one host thread per slice; the results and the rescued-pair total equal
+    the one-call run's, and stay within 1e-5 of the oracle."""
+    import ctypes as C
+    reads, haps = random_batch(77, 300, 12, 60, 151, 100, 400)
+    ur, uh = random_batch(78, 40, 4, 90, 150, 150, 300, n_frac=0.0, related=False)
+    ur = [(r[0], np.full(r[0].size, 40, np.uint8), np.full(r[0].size, 60, np.uint8),
+           np.full(r[0].size, 60, np.uint8), r[4]) for r in ur]  # these underflow: fp64 rescue
+    p = fcship.make_pairs(reads + ur, haps + uh)
+    one = fcship.phmm_compute_pairs(p)
+    r1 = C.c_int64()
+    fcship.lib.fcs_phmm_last_rescued(C.byref(r1))
+    for devs in ([0, 0], [0, 0, 0, 0, 0]):
+        multi = fcship.phmm_compute_pairs_multi(p, devs)
+        rm = C.c_int64()
+        fcship.lib.fcs_phmm_last_rescued(C.byref(rm))
+        assert np.allclose(multi, one, rtol=1e-12, atol=0), np.abs(multi - one).max()
+        assert rm.value == r1.value
+    assert r1.value > 0
+    check_parity(p, one, False)
