@@ -1067,6 +1067,37 @@ static int pack_tasks(const fcs_bsw_task* tasks, int32_t n, PackedTasks& pk) {
   return FCS_OK;
 }
 
+int fcs_bsw_extend_multi(const fcs_bsw_task* tasks, int32_t n, const fcs_bsw_params* params,
+                         fcs_bsw_result* results, const int32_t* devices, int32_t n_devices) {
+  if (n < 0 || (n > 0 && (!tasks || !results)) || n_devices <= 0 || !devices)
+    return fail(FCS_ERR_INVALID, "[E::fcs_bsw_extend_multi] bad arguments");
+  // §8e: contiguous slices of ~equal qlen * tlen, one device each, one host thread each
+  std::vector<double> cum((size_t)n);
+  double run = 0;
+  for (int32_t i = 0; i < n; ++i) cum[i] = (run += (double)std::max(tasks[i].qlen, 0) * std::max(tasks[i].tlen, 0));
+  std::vector<int32_t> cuts((size_t)n_devices + 1, 0);
+  for (int32_t k = 1; k < n_devices; ++k) {
+    int64_t c = run > 0 ? (int64_t)(std::lower_bound(cum.begin(), cum.end(), run * k / n_devices) - cum.begin()) + 1
+                        : (int64_t)n * k / n_devices;
+    cuts[k] = (int32_t)std::max<int64_t>(cuts[k - 1], std::min<int64_t>(c, n));
+  }
+  cuts[n_devices] = n;
+  std::vector<int> rcs((size_t)n_devices, FCS_OK);
+  std::vector<std::string> errs((size_t)n_devices);
+  std::vector<std::thread> th;
+  for (int32_t k = 0; k < n_devices; ++k) {
+    if (cuts[k + 1] == cuts[k]) continue;
+    th.emplace_back([&, k] {
+      rcs[k] = fcs_bsw_extend(tasks + cuts[k], cuts[k + 1] - cuts[k], params, results + cuts[k], devices[k]);
+      if (rcs[k] != FCS_OK) errs[k] = fcs_last_error();
+    });
+  }
+  for (auto& t : th) t.join();
+  for (int32_t k = 0; k < n_devices; ++k)
+    if (rcs[k] != FCS_OK) return fail(rcs[k], errs[k]);
+  return FCS_OK;
+}
+
 int fcs_bsw_extend(const fcs_bsw_task* tasks, int32_t n, const fcs_bsw_params* params, fcs_bsw_result* results,
                    int32_t device) {
   if (n < 0 || (n > 0 && (!tasks || !results))) return fail(FCS_ERR_INVALID, "[E::fcs_bsw_extend] bad arguments");
@@ -1255,6 +1286,6 @@ int fcs_ksw_global2(int qlen, const uint8_t* query, int tlen, const uint8_t* tar
   return score;
 }
 
-int fcs_abi_symbol_count(void) { return 35; }
+int fcs_abi_symbol_count(void) { return 36; }
 
 }  // extern "C"

@@ -137,6 +137,8 @@ _sig("fcs_phmm_compute_pairs_multi", C.c_int, [C.POINTER(PhmmBatch), C.c_void_p,
 _sig("fcs_bsw_params_default", None, [C.POINTER(BswParams)])
 _sig("fcs_bsw_extend", C.c_int, [C.POINTER(BswTask), C.c_int32, C.POINTER(BswParams), C.POINTER(BswResult),
                                  C.c_int32])
+_sig("fcs_bsw_extend_multi", C.c_int, [C.POINTER(BswTask), C.c_int32, C.POINTER(BswParams), C.POINTER(BswResult),
+                                       C.c_void_p, C.c_int32])
 _sig("fcs_bsw_extend_dev", C.c_int, [C.POINTER(BswBatch), C.POINTER(BswParams), C.c_void_p, C.c_void_p,
                                      C.c_int32, C.c_void_p])
 _sig("fcs_bsw_extend_batch", C.c_int, [C.POINTER(BswBatch), C.POINTER(BswParams), i32p, i64p, C.c_int32])
@@ -412,6 +414,24 @@ def bsw_extend_batch(t: BswTasks, params: BswParams | None = None, device=0):
     check(lib.fcs_bsw_extend_batch(C.byref(b), C.byref(params), res.ctypes.data_as(i32p),
                                    cells.ctypes.data_as(i64p), device))
     return res, cells
+
+
+def bsw_extend_tasks(t: BswTasks, params: BswParams | None = None, device=0, devices=None):
+    """fcs_bsw_extend over an array of fcs_bsw_task (bwa's per-task pointers);
+    devices: a list of device slots -> fcs_bsw_extend_multi (static partition)."""
+    params = params or bsw_params()
+    arr = (BswTask * max(t.n, 1))()
+    base_q, base_t = t.qbuf.ctypes.data, t.tbuf.ctypes.data
+    for i in range(t.n):
+        arr[i] = BswTask(int(t.qlen[i]), int(t.tlen[i]), int(t.h0[i]), int(t.w[i]),
+                         C.cast(base_q + int(t.qoff[i]), u8p), C.cast(base_t + int(t.toff[i]), u8p))
+    res = (BswResult * max(t.n, 1))()
+    if devices is None:
+        check(lib.fcs_bsw_extend(arr, t.n, C.byref(params), res, device))
+    else:
+        d = np.asarray(devices, np.int32)
+        check(lib.fcs_bsw_extend_multi(arr, t.n, C.byref(params), res, d.ctypes.data, len(d)))
+    return np.array([[r.score, r.qle, r.tle, r.gtle, r.gscore, r.max_off] for r in res[:t.n]], np.int32)
 
 
 def bsw_global(t: BswTasks, params: BswParams | None = None, device=0, with_cigar=True):

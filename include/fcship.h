@@ -204,6 +204,10 @@ void fcs_bsw_params_default(fcs_bsw_params* p);
 /* Batched ksw_extend2 (host pointers, synchronous). */
 int fcs_bsw_extend(const fcs_bsw_task* tasks, int32_t n, const fcs_bsw_params* params,
                    fcs_bsw_result* results, int32_t device);
+/* The same over several devices: contiguous slices of ~equal
+ * qlen * tlen, one device and one host thread each, disjoint result slices. */
+int fcs_bsw_extend_multi(const fcs_bsw_task* tasks, int32_t n, const fcs_bsw_params* params,
+                         fcs_bsw_result* results, const int32_t* devices, int32_t n_devices);
 
 /* Packed structure-of-arrays extension batch (device or host pointers
  * depending on the entry point).  Task k: query bytes

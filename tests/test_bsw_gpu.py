@@ -264,3 +264,15 @@ def test_global_lane_kernel_narrow_bands(gpu, w):
         assert np.array_equal(cigars[k], rc), f"task {k}: {fcship.cigar_str(cigars[k])} != {fcship.cigar_str(rc)}"
     s2, _ = fcship.bsw_global(t, with_cigar=False)
     assert np.array_equal(s2, scores)
+
+
+def test_extend_multi_device_static_partition(gpu):
+    """fcs_bsw_extend_multi: contiguous slices of ~equal
+    qlen*tlen over several device slots (device 0 here), one host thread each;
+    every result equals the one-device batch and the oracle."""
+    t = random_tasks(41, 700)
+    one = fcship.bsw_extend_tasks(t)
+    ref, _ = oracle_lib.ksw_extend2_batch(t, fcship.default_mat())
+    assert np.array_equal(one, ref)
+    for devs in ([0, 0], [0, 0, 0, 0]):
+        assert np.array_equal(fcship.bsw_extend_tasks(t, devices=devs), ref)
