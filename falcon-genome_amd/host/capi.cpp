@@ -177,6 +177,7 @@ int fcsg_extend_seeds(int n, const uint8_t* qbuf, const int64_t* qoff, const int
   });
 }
 int fcsg_tandem_repeat_units(const char* bases, int offset) { return tandem_repeat_units(bases, offset); }
+void fcsg_tandem_repeat_runs(const char* bases, int n, uint8_t* out) { tandem_repeat_runs(bases, n, out); }
 int fcsg_pcr_indel_cap(int repeat_len, int model) { return pcr_indel_cap(repeat_len, (PcrIndelModel)model); }
 
 int fcsg_bgzf_compress_file(const char* in, const char* out) {

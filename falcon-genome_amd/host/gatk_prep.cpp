@@ -1,8 +1,11 @@
 #include "gatk_prep.h"
 
 #include <algorithm>
+#include <array>
 #include <cmath>
 #include <cstring>
+
+#include <emmintrin.h>
 
 #include "common.h"
 
@@ -81,6 +84,82 @@ int tandem_repeat_units(const std::string& bases, int offset) {
   return max_rl > kMaxRepeatLen ? kMaxRepeatLen : max_rl;
 }
 
+void tandem_repeat_runs(const char* r, int n, uint8_t* out) {
+  // Every repetitions() call above becomes a lookup into two tables of match
+  // runs, one row of eight unit lengths u = 1 .. 8 per position (16-byte SSE2
+  // lanes, saturating at 255 — far past the cap of 20 copies):
+  //   bk[k][8 - u] = the number of consecutive k' = k, k - 1, ... with
+  //                  r[k' - u] == r[k'];
+  //   fw[j][u - 1] = the number of consecutive j' = j, j + 1, ... with
+  //                  r[j'] == r[j' + u].
+  // A unit of length u ending at o has k further copies behind it exactly when
+  // bk[o][8 - u] >= k u, a unit starting at o + 1 k further copies ahead when
+  // fw[o + 1][u - 1] >= k u; the first u with a second copy is a bit scan of
+  // the lanes >= u.  Positions outside the read hold pairwise distinct
+  // sentinels that match no base.
+  if (n <= 1) return;
+  constexpr int U = kMaxStrUnit;
+  static_assert(U == 8, "one 8-byte row per position");
+  static const auto kDiv = [] {
+    std::array<std::array<uint8_t, 256>, U + 1> t{};
+    for (int u = 1; u <= U; ++u)
+      for (int x = 0; x < 256; ++x) t[u][x] = (uint8_t)std::min(x / u, 255);
+    return t;
+  }();
+  thread_local std::vector<char> tl_seq;
+  thread_local std::vector<uint8_t> tl_bk, tl_fw;
+  std::vector<char>& vs = tl_seq;
+  std::vector<uint8_t>& vb = tl_bk;
+  std::vector<uint8_t>& vf = tl_fw;
+  vs.resize((size_t)n + 2 * U + 8);
+  for (int k = 0; k < U; ++k) vs[k] = (char)(9 + k);  // before the read: 9 .. 16
+  std::memcpy(vs.data() + U, r, (size_t)n);
+  for (int k = 0; k < U + 8; ++k) vs[U + n + k] = (char)(1 + (k & 7));  // after: 1 .. 8 (only 8 are compared)
+  vb.resize((size_t)(n + 1) * U + 8);
+  vf.resize((size_t)(n + 1) * U + 8);
+  const char* q = vs.data() + U;
+  uint8_t* const bk = vb.data();
+  uint8_t* const fw = vf.data();
+  const __m128i zero = _mm_setzero_si128(), one = _mm_set1_epi8(1);
+  __m128i run = zero;
+  for (int k = 0; k < n; ++k) {  // lane c: q[k - 8 + c] == q[k], u = 8 - c
+    const __m128i prev = _mm_loadl_epi64((const __m128i*)(q + k - 8));
+    const __m128i eq = _mm_cmpeq_epi8(prev, _mm_set1_epi8(q[k]));
+    run = _mm_and_si128(_mm_adds_epu8(run, one), eq);
+    _mm_storel_epi64((__m128i*)(bk + (size_t)k * U), run);
+  }
+  run = zero;
+  _mm_storel_epi64((__m128i*)(fw + (size_t)n * U), zero);
+  for (int j = n - 1; j >= 0; --j) {  // lane i: q[j + 1 + i] == q[j], u = i + 1
+    const __m128i next = _mm_loadl_epi64((const __m128i*)(q + j + 1));
+    const __m128i eq = _mm_cmpeq_epi8(next, _mm_set1_epi8(q[j]));
+    run = _mm_and_si128(_mm_adds_epu8(run, one), eq);
+    _mm_storel_epi64((__m128i*)(fw + (size_t)j * U), run);
+  }
+  const __m128i ub = _mm_setr_epi8(8, 7, 6, 5, 4, 3, 2, 1, 0, 0, 0, 0, 0, 0, 0, 0);
+  const __m128i uf = _mm_setr_epi8(1, 2, 3, 4, 5, 6, 7, 8, 0, 0, 0, 0, 0, 0, 0, 0);
+  for (int o = 0; o + 1 < n; ++o) {
+    const __m128i rb = _mm_loadl_epi64((const __m128i*)(bk + (size_t)o * U));
+    const __m128i rf = _mm_loadl_epi64((const __m128i*)(fw + (size_t)(o + 1) * U));
+    // lanes whose run covers one more copy: u - run saturates to 0
+    const unsigned mb = (unsigned)_mm_movemask_epi8(_mm_cmpeq_epi8(_mm_subs_epu8(ub, rb), zero)) & 0xFF;
+    const unsigned mf = (unsigned)_mm_movemask_epi8(_mm_cmpeq_epi8(_mm_subs_epu8(uf, rf), zero)) & 0xFF;
+    // smallest u: the highest back lane, the lowest forward lane; none: the
+    // single base with one copy (its run reads 0)
+    const int bu = mb ? 8 - (31 - __builtin_clz(mb)) : 1;
+    const int fu = mf ? 1 + __builtin_ctz(mf) : 1;
+    const int max_bw = 1 + kDiv[bu][bk[(size_t)o * U + 8 - bu]];
+    const int max_fw = 1 + kDiv[fu][fw[(size_t)(o + 1) * U + fu - 1]];
+    // the forward unit r[o+1, o+fu] equals the backward one r[o-bu+1, o]
+    // exactly when r[o'] == r[o' + fu] for o' = o .. o - fu + 1; otherwise
+    // count the forward unit's copies behind o
+    const int bf = bk[(size_t)(o + fu) * U + 8 - fu];
+    const int same = (bf >= fu) & (fu == bu);
+    const int rl = max_fw + same * max_bw + (1 - same) * kDiv[fu][bf];
+    out[o] = (uint8_t)std::min(rl, kMaxRepeatLen);
+  }
+}
+
 int pcr_indel_cap(int repeat_len, PcrIndelModel m) {
   if (m == PcrIndelModel::NONE) return 255;
   const double rate = m == PcrIndelModel::HOSTILE ? 1.0 : m == PcrIndelModel::AGGRESSIVE ? 2.0 : 3.0;
@@ -110,8 +189,12 @@ void gatk_prepare_read(const std::string& bases, const std::vector<uint8_t>& qua
   if (pcr != PcrIndelModel::NONE) {
     int cache[kMaxRepeatLen + 1];
     for (int r = 0; r <= kMaxRepeatLen; ++r) cache[r] = pcr_indel_cap(r, pcr);
+    thread_local std::vector<uint8_t> tl_runs;
+    std::vector<uint8_t>& runs = tl_runs;
+    runs.resize(n);
+    tandem_repeat_runs(bases.data(), (int)n, runs.data());
     for (size_t i = 1; i < n; ++i) {  // applyPCRErrorModel: positions 0 .. n - 2
-      const int c = cache[tandem_repeat_units(bases, (int)i - 1)];
+      const int c = cache[runs[i - 1]];
       ins[i - 1] = std::min(ins[i - 1] & 0xFF, c);
       del[i - 1] = std::min(del[i - 1] & 0xFF, c);
     }

@@ -35,6 +35,9 @@ PcrIndelModel parse_pcr_indel_model(const std::string& s);  // throws invalidPar
 
 // GATK's tandem repeat run length at `offset` (capped at 20).
 int tandem_repeat_units(const std::string& bases, int offset);
+// The same for every offset 0 .. n - 2 at once (out[0, n - 1)), in O(8 n)
+// from per-unit-length runs of r[j] == r[j + u]; the read-preparation path.
+void tandem_repeat_runs(const char* bases, int n, uint8_t* out);
 // The model's gap-open cap for a repeat run length.
 int pcr_indel_cap(int repeat_len, PcrIndelModel m);
 

@@ -292,6 +292,31 @@ def test_pcr_indel_error_model():
     assert out[1].tolist() == [45] * n  # NONE
 
 
+def test_tandem_repeat_runs_equal_per_offset_scan():
+    """The O(8 n) all-offsets run lengths the read preparation uses equal
+    findTandemRepeatUnits evaluated offset by offset, on random reads and on
+    reads built from short repeated units (the cases with long runs, unit
+    changes at the offset and the 20 cap)."""
+    rng = np.random.default_rng(11)
+    acgt = np.frombuffer(b"ACGT", np.uint8)
+    reads = [b"AC", b"AAAAAAAAAA", b"TTCTTCCCC", b"ACACACGT", b"A" * 40,
+             b"A" * 600, b"ACG" * 200, b"C" * 300 + b"ACGTTGCA" * 40]  # runs past the 255 saturation
+    for _ in range(400):
+        if rng.random() < 0.4:
+            reads.append(rng.choice(acgt, int(rng.integers(2, 160))).tobytes())
+        else:
+            parts = []
+            while sum(map(len, parts)) < 120:
+                unit = rng.choice(acgt, int(rng.integers(1, 10))).tobytes()
+                parts.append(unit * int(rng.integers(1, 8)))
+            reads.append(b"".join(parts)[: int(rng.integers(2, 160))])
+    for r in reads:
+        out = np.zeros(len(r), np.uint8)
+        H.lib.fcsg_tandem_repeat_runs(r, len(r), out.ctypes.data_as(C.POINTER(C.c_uint8)))
+        want = [H.lib.fcsg_tandem_repeat_units(r, i) for i in range(len(r) - 1)]
+        assert out[: len(r) - 1].tolist() == want, r
+
+
 # ------------------------------------------------------------------ executor
 def test_executor_slots_logs_and_failure(tmp_path):
     buf = C.create_string_buffer(1 << 16)
