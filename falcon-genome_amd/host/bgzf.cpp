@@ -1,9 +1,12 @@
 #include "bgzf.h"
 
+#include <dlfcn.h>
 #include <zlib.h>
 
 #include <algorithm>
+#include <cstdlib>
 #include <cstring>
+#include <memory>
 #include <thread>
 
 #include "common.h"
@@ -27,21 +30,108 @@ uint32_t get32(const uint8_t* p) {
   return (uint32_t)p[0] | ((uint32_t)p[1] << 8) | ((uint32_t)p[2] << 16) | ((uint32_t)p[3] << 24);
 }
 
+// The raw-deflate codec.  libdeflate (the image's libdeflate.so.0, the codec
+// htslib prefers when built with it) inflates and deflates whole 64 KiB
+// blocks in one call, about twice zlib's speed; it is opened at run time and
+// zlib stays the codec when it is absent or FCS_BGZF_ZLIB=1.  Either codec's
+// output is a valid raw-deflate stream, so files differ only in the
+// compressed bytes, never in content.
+struct Libdeflate {
+  void* (*alloc_decompressor)() = nullptr;
+  int (*deflate_decompress)(void*, const void*, size_t, void*, size_t, size_t*) = nullptr;
+  void (*free_decompressor)(void*) = nullptr;
+  void* (*alloc_compressor)(int) = nullptr;
+  size_t (*deflate_compress)(void*, const void*, size_t, void*, size_t) = nullptr;
+  void (*free_compressor)(void*) = nullptr;
+  uint32_t (*crc32)(uint32_t, const void*, size_t) = nullptr;
+  bool ok = false;
+};
+
+const Libdeflate& libdeflate() {
+  static const Libdeflate L = [] {
+    Libdeflate l;
+    const char* force = std::getenv("FCS_BGZF_ZLIB");
+    if (force && *force && *force != '0') return l;
+    void* h = dlopen("libdeflate.so.0", RTLD_NOW | RTLD_LOCAL);
+    if (!h) return l;
+    auto sym = [&](auto& f, const char* name) { f = reinterpret_cast<std::remove_reference_t<decltype(f)>>(dlsym(h, name)); };
+    sym(l.alloc_decompressor, "libdeflate_alloc_decompressor");
+    sym(l.deflate_decompress, "libdeflate_deflate_decompress");
+    sym(l.free_decompressor, "libdeflate_free_decompressor");
+    sym(l.alloc_compressor, "libdeflate_alloc_compressor");
+    sym(l.deflate_compress, "libdeflate_deflate_compress");
+    sym(l.free_compressor, "libdeflate_free_compressor");
+    sym(l.crc32, "libdeflate_crc32");
+    l.ok = l.alloc_decompressor && l.deflate_decompress && l.free_decompressor && l.alloc_compressor &&
+           l.deflate_compress && l.free_compressor && l.crc32;
+    return l;
+  }();
+  return L;
+}
+
+uint32_t block_crc(const uint8_t* p, size_t n) {
+  const Libdeflate& L = libdeflate();
+  return L.ok ? L.crc32(0, p, n) : (uint32_t)crc32(crc32(0L, Z_NULL, 0), p, (uInt)n);
+}
+
+// Raw inflate of a whole block into out[0, isize); false when corrupt.
+bool inflate_block(const uint8_t* in, size_t n, uint8_t* out, size_t isize) {
+  const Libdeflate& L = libdeflate();
+  if (L.ok) {
+    struct Free {
+      void operator()(void* d) const { libdeflate().free_decompressor(d); }
+    };
+    thread_local std::unique_ptr<void, Free> dec(L.alloc_decompressor());
+    if (!dec) throw internalError("[E::bgzf] libdeflate_alloc_decompressor failed");
+    size_t got = 0;
+    return L.deflate_decompress(dec.get(), in, n, out, isize, &got) == 0 && got == isize;
+  }
+  z_stream zs{};
+  if (inflateInit2(&zs, -15) != Z_OK) throw internalError("[E::bgzf] inflateInit2 failed");
+  zs.next_in = const_cast<uint8_t*>(in);
+  zs.avail_in = (uInt)n;
+  zs.next_out = out;
+  zs.avail_out = (uInt)isize;
+  const int rc = inflate(&zs, Z_FINISH);
+  inflateEnd(&zs);
+  return rc == Z_STREAM_END && zs.total_out == isize;
+}
+
+// Raw deflate of data[0, n) into out[0, cap) at `level`; 0 when it does not fit.
+size_t deflate_block(const uint8_t* data, size_t n, uint8_t* out, size_t cap, int level) {
+  const Libdeflate& L = libdeflate();
+  if (L.ok && level > 0) {
+    struct Free {
+      void operator()(void* c) const { libdeflate().free_compressor(c); }
+    };
+    thread_local int tl_level = -1;
+    thread_local std::unique_ptr<void, Free> comp;
+    if (tl_level != level) {
+      comp.reset(L.alloc_compressor(std::min(level, 12)));
+      if (!comp) throw internalError("[E::bgzf] libdeflate_alloc_compressor failed");
+      tl_level = level;
+    }
+    return L.deflate_compress(comp.get(), data, n, out, cap);
+  }
+  z_stream zs{};
+  if (deflateInit2(&zs, level, Z_DEFLATED, -15, 8, Z_DEFAULT_STRATEGY) != Z_OK)
+    throw internalError("[E::bgzf] deflateInit2 failed");
+  zs.next_in = const_cast<uint8_t*>(data);
+  zs.avail_in = (uInt)n;
+  zs.next_out = out;
+  zs.avail_out = (uInt)cap;
+  const int rc = deflate(&zs, Z_FINISH);
+  const size_t clen = zs.total_out;
+  deflateEnd(&zs);
+  return rc == Z_STREAM_END ? clen : 0;
+}
+
 // One BGZF member for n <= kBgzfMaxBlock input bytes.
 std::vector<uint8_t> make_block(const uint8_t* data, size_t n, int level) {
   std::vector<uint8_t> out(kBgzfMaxBlock + 64);
   for (int attempt = 0; attempt < 2; ++attempt) {
-    z_stream zs{};
-    if (deflateInit2(&zs, attempt ? 0 : level, Z_DEFLATED, -15, 8, Z_DEFAULT_STRATEGY) != Z_OK)
-      throw internalError("[E::bgzf] deflateInit2 failed");
-    zs.next_in = const_cast<uint8_t*>(data);
-    zs.avail_in = (uInt)n;
-    zs.next_out = out.data() + 18;
-    zs.avail_out = (uInt)(kBgzfMaxBlock - 18 - 8);
-    const int rc = deflate(&zs, Z_FINISH);
-    const size_t clen = zs.total_out;
-    deflateEnd(&zs);
-    if (rc != Z_STREAM_END) {
+    const size_t clen = deflate_block(data, n, out.data() + 18, kBgzfMaxBlock - 18 - 8, attempt ? 0 : level);
+    if (clen == 0) {
       if (attempt == 0) continue;  // incompressible: store (level 0) instead
       throw internalError("[E::bgzf] block does not fit in 64 KiB");
     }
@@ -49,7 +139,7 @@ std::vector<uint8_t> make_block(const uint8_t* data, size_t n, int level) {
     static const uint8_t hdr[16] = {0x1f, 0x8b, 0x08, 0x04, 0, 0, 0, 0, 0, 0xff, 0x06, 0, 0x42, 0x43, 0x02, 0};
     std::memcpy(out.data(), hdr, 16);
     put16(out.data() + 16, (uint32_t)(bsize - 1));
-    put32(out.data() + 18 + clen, (uint32_t)crc32(crc32(0L, Z_NULL, 0), data, (uInt)n));
+    put32(out.data() + 18 + clen, block_crc(data, n));
     put32(out.data() + 18 + clen + 4, (uint32_t)n);
     out.resize(bsize);
     return out;
@@ -157,18 +247,12 @@ bool BgzfReader::load_block() {
     const size_t hdr = 12 + xlen;
     const uint32_t isize = get32(&comp[bsize - 4]);
     const uint32_t crc = get32(&comp[bsize - 8]);
-    block_.assign(isize, 0);
+    if (isize > kBgzfMaxBlock || bsize < hdr + 8) throw formatError("corrupt BGZF block header");
+    block_.resize(isize);
     if (isize > 0) {
-      z_stream zs{};
-      if (inflateInit2(&zs, -15) != Z_OK) throw internalError("[E::bgzf] inflateInit2 failed");
-      zs.next_in = comp.data() + hdr;
-      zs.avail_in = (uInt)(bsize - hdr - 8);
-      zs.next_out = block_.data();
-      zs.avail_out = isize;
-      const int rc = inflate(&zs, Z_FINISH);
-      inflateEnd(&zs);
-      if (rc != Z_STREAM_END || zs.total_out != isize) throw formatError("corrupt BGZF block payload");
-      if ((uint32_t)crc32(crc32(0L, Z_NULL, 0), block_.data(), isize) != crc) throw formatError("BGZF CRC mismatch");
+      if (!inflate_block(comp.data() + hdr, bsize - hdr - 8, block_.data(), isize))
+        throw formatError("corrupt BGZF block payload");
+      if (block_crc(block_.data(), isize) != crc) throw formatError("BGZF CRC mismatch");
     }
     next_coff_ = block_coff_ + bsize;
     pos_ = 0;

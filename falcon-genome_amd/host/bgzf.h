@@ -1,4 +1,4 @@
-// BGZF (blocked gzip) reader and writer on zlib — the container of BAM,
+// BGZF (blocked gzip) reader and writer on libdeflate (zlib when absent) — the container of BAM,
 // bgzipped VCF and tabix indexes (the reference shells
 // out to bgzip/tabix/samtools for these, src/worker-htc.cpp:153-176).
 //
