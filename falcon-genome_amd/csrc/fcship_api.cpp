@@ -14,6 +14,7 @@
 #include <cstring>
 #include <map>
 #include <memory>
+#include <condition_variable>
 #include <mutex>
 #include <thread>
 #include <vector>
@@ -45,43 +46,39 @@ int check_device(int device) {
   return FCS_OK;
 }
 
-// One stream per (thread, device) for the synchronous host-pointer entry points.
-hipStream_t thread_stream(int device) {
-  static thread_local std::map<int, hipStream_t> streams;
-  auto it = streams.find(device);
-  if (it != streams.end()) return it->second;
-  hipStream_t s = nullptr;
-  if (hipStreamCreateWithFlags(&s, hipStreamNonBlocking) != hipSuccess) return nullptr;
-  streams[device] = s;
-  return s;
-}
-
 struct ForkSet {
   hipStream_t side[kForkStreams - 1] = {};
   hipEvent_t fork = nullptr;
   hipEvent_t join[kForkStreams - 1] = {};
 };
 
-// Side streams and events of the calling thread on the current device.
-ForkSet* fork_set() {
+// Side streams and events of a launch stream on the current device, created
+// on the stream's first fork and kept for the process (a stream costs about
+// 3.5 ms to create on gfx950, so they are made once per launch stream, not
+// per call or per thread).  A launch stream is used by one call at a time:
+// a pooled session's stream by its lease holder, a caller's stream by the
+// caller.
+ForkSet* fork_set(hipStream_t s) {
   int device = 0;
   if (hipGetDevice(&device) != hipSuccess) return nullptr;
-  static thread_local std::map<int, ForkSet> sets;
-  auto it = sets.find(device);
-  if (it != sets.end()) return &it->second;
+  static std::mutex mu;
+  static auto* sets = new std::map<std::pair<int, hipStream_t>, ForkSet>();  // outlives static teardown
+  std::lock_guard<std::mutex> lk(mu);
+  auto it = sets->find({device, s});
+  if (it != sets->end()) return &it->second;
   ForkSet f;
   if (hipEventCreateWithFlags(&f.fork, hipEventDisableTiming) != hipSuccess) return nullptr;
   for (int i = 0; i < kForkStreams - 1; ++i)
     if (hipStreamCreateWithFlags(&f.side[i], hipStreamNonBlocking) != hipSuccess ||
         hipEventCreateWithFlags(&f.join[i], hipEventDisableTiming) != hipSuccess)
       return nullptr;
-  return &(sets[device] = f);
+  return &((*sets)[{device, s}] = f);
 }
 
 }  // namespace
 
 int fork_streams(hipStream_t s, hipStream_t (&fs)[kForkStreams]) {
-  ForkSet* f = fork_set();
+  ForkSet* f = fork_set(s);
   if (!f) return fail(FCS_ERR_DEVICE, "[E::fcship] cannot create side streams");
   FCS_HIP_CHECK(hipEventRecord(f->fork, s));
   fs[0] = s;
@@ -93,7 +90,7 @@ int fork_streams(hipStream_t s, hipStream_t (&fs)[kForkStreams]) {
 }
 
 int join_streams(hipStream_t s, const hipStream_t (&fs)[kForkStreams]) {
-  ForkSet* f = fork_set();
+  ForkSet* f = fork_set(s);
   if (!f) return fail(FCS_ERR_DEVICE, "[E::fcship] cannot create side streams");
   for (int i = 0; i < kForkStreams - 1; ++i) {
     FCS_HIP_CHECK(hipEventRecord(f->join[i], fs[i + 1]));
@@ -116,13 +113,21 @@ struct Layout {
 
 }  // namespace
 
-// Per-(thread, device) state of the synchronous host-pointer entry points:
-// the thread's stream, a PairHMM plan and an SW plan grown to the largest
-// batch seen, one device arena for the batch's inputs and outputs and one
-// pinned host arena it is staged through (one H2D and one D2H copy per call).
-// After warm-up a call allocates nothing: no hipMalloc/hipFree (hipFree
-// synchronises the whole device, so per-call frees serialised the Executor's
-// concurrent shard threads on one GPU) and no null-stream operation.
+// State of the synchronous host-pointer entry points on one device: a stream,
+// a PairHMM plan and an SW plan grown to the largest batch seen, one device
+// arena for the batch's inputs and outputs and one pinned host arena it is
+// staged through (one H2D and one D2H copy per call).  After warm-up a call
+// allocates nothing: no hipMalloc/hipFree (hipFree synchronises the whole
+// device, so per-call frees serialised the Executor's concurrent shard
+// threads on one GPU) and no null-stream operation.
+//
+// Sessions live in a per-device pool and a call leases one for its duration.
+// Creating one costs four streams (its own and three fork side streams,
+// about 14 ms together); with one session per calling thread, the htc stage's
+// 16 shard threads spent 0.22 s creating 64 streams, serialised inside the
+// runtime, before their first PairHMM call.  The pool holds at most
+// FCS_SESSIONS_PER_DEVICE (default 4) sessions, which fcs_device_warmup
+// creates ahead of time; a call finding all of them busy waits for one.
 struct Session {
   int device = 0;
   hipStream_t s = nullptr;
@@ -133,7 +138,6 @@ struct Session {
   void* host = nullptr;
   size_t host_cap = 0;
   hipEvent_t ev[3] = {nullptr, nullptr, nullptr};  // PairHMM call: start, after forward, after rescue
-  ~Session();
   int ensure_dev(size_t bytes);
   int ensure_host(size_t bytes);
   int ensure_phmm(int64_t pairs);
@@ -146,19 +150,115 @@ namespace {
 
 size_t grown(size_t need, size_t cap) { return std::max(need + need / 4, std::min<size_t>(2 * cap, need + (1u << 30))); }
 
-// The calling thread's session on `device` (created on first use).
-Session* session(int device) {
-  static thread_local std::map<int, std::unique_ptr<Session>> sessions;
-  auto& slot = sessions[device];
-  if (!slot) {
-    hipStream_t s = thread_stream(device);
-    if (!s) return nullptr;
-    slot.reset(new Session());
-    slot->device = device;
-    slot->s = s;
-  }
-  return slot.get();
+int sessions_per_device() {
+  static const int n = [] {
+    const char* e = std::getenv("FCS_SESSIONS_PER_DEVICE");
+    const int v = e && *e ? std::atoi(e) : 4;
+    return std::max(1, std::min(v, 64));
+  }();
+  return n;
 }
+
+struct SessionPool {
+  std::mutex mu;
+  std::condition_variable cv;
+  std::vector<Session*> all, idle;  // never freed: the pools outlive static teardown and the HIP runtime
+  int creating = 0;
+};
+
+SessionPool& session_pool(int device) {
+  static std::mutex mu;
+  static auto* pools = new std::map<int, SessionPool*>();
+  std::lock_guard<std::mutex> lk(mu);
+  SessionPool*& p = (*pools)[device];
+  if (!p) p = new SessionPool();
+  return *p;
+}
+
+// A new session on `device` (the current device), or null.
+Session* create_session(int device) {
+  auto* S = new Session();
+  S->device = device;
+  if (hipStreamCreateWithFlags(&S->s, hipStreamNonBlocking) != hipSuccess || !fork_set(S->s)) {
+    delete S;  // a failed stream is not reused; nothing else was created
+    return nullptr;
+  }
+  return S;
+}
+
+// Grows the pool of `device` (the current device) to n idle-or-busy sessions.
+int prefill_sessions(int device, int n) {
+  SessionPool& P = session_pool(device);
+  n = std::min(n, sessions_per_device());
+  for (;;) {
+    {
+      std::lock_guard<std::mutex> lk(P.mu);
+      if ((int)P.all.size() + P.creating >= n) return FCS_OK;
+      ++P.creating;
+    }
+    Session* S = create_session(device);
+    {
+      std::lock_guard<std::mutex> lk(P.mu);
+      --P.creating;
+      if (S) P.all.push_back(S), P.idle.push_back(S);
+    }
+    P.cv.notify_one();
+    if (!S) return fail(FCS_ERR_DEVICE, "[E::fcship] stream creation failed");
+  }
+}
+
+// A session of `device` (the current device) held for one call.
+class SessionLease {
+ public:
+  SessionLease() = default;
+  SessionLease(const SessionLease&) = delete;
+  SessionLease& operator=(const SessionLease&) = delete;
+  ~SessionLease() { release(); }
+  int acquire(int device) {
+    release();
+    SessionPool& P = session_pool(device);
+    std::unique_lock<std::mutex> lk(P.mu);
+    for (;;) {
+      if (!P.idle.empty()) {
+        s_ = P.idle.back();
+        P.idle.pop_back();
+        pool_ = &P;
+        return FCS_OK;
+      }
+      if ((int)P.all.size() + P.creating < sessions_per_device()) break;
+      P.cv.wait(lk);
+    }
+    ++P.creating;
+    lk.unlock();
+    Session* S = create_session(device);
+    lk.lock();
+    --P.creating;
+    if (!S) {
+      P.cv.notify_one();
+      return fail(FCS_ERR_DEVICE, "[E::fcship] stream creation failed");
+    }
+    P.all.push_back(S);
+    s_ = S;
+    pool_ = &P;
+    return FCS_OK;
+  }
+  Session* operator->() const { return s_; }
+  Session* get() const { return s_; }
+
+ private:
+  void release() {
+    if (!s_) return;
+    {
+      std::lock_guard<std::mutex> lk(pool_->mu);
+      pool_->idle.push_back(s_);
+    }
+    pool_->cv.notify_one();
+    s_ = nullptr;
+    pool_ = nullptr;
+  }
+  Session* s_ = nullptr;
+  SessionPool* pool_ = nullptr;
+};
 
 BswParams to_params(const fcs_bsw_params* p) {
   BswParams q;
@@ -293,17 +393,6 @@ struct fcs_phmm_plan {
 };
 
 namespace fcs {
-
-Session::~Session() {
-  (void)hipSetDevice(device);
-  if (s) (void)hipStreamSynchronize(s);
-  fcs_phmm_plan_destroy(phmm);
-  fcs_bsw_plan_destroy(bsw);
-  for (hipEvent_t e : ev)
-    if (e) (void)hipEventDestroy(e);
-  if (dev) (void)hipFree(dev);
-  if (host) (void)hipHostFree(host);
-}
 
 int Session::ensure_dev(size_t bytes) {
   if (bytes <= dev_cap) return FCS_OK;
@@ -550,6 +639,22 @@ int fcs_phmm_dev_run(fcs_phmm_plan* plan, const fcs_phmm_batch* b, double* out, 
   return fcs_phmm_dev_rescue(plan, b, out, opts, stream);
 }
 
+int fcs_device_warmup(int32_t device, int32_t sessions) {
+  int rc = check_device(device);
+  if (rc) return rc;
+  // a 1x1 PairHMM call: runtime, code objects, GKL tables and one session
+  static const uint8_t b[1] = {'A'}, q[1] = {30}, g[1] = {10}, iq[1] = {45};
+  const fcs_phmm_read r{b, q, iq, iq, g, 1};
+  const fcs_phmm_hap h{b, 1};
+  double out = 0;
+  fcs_phmm_opts o;
+  fcs_phmm_opts_default(&o);
+  o.device = device;
+  if ((rc = fcs_phmm_compute(&r, 1, &h, 1, &out, &o))) return rc;
+  FCS_HIP_CHECK(hipSetDevice(device));
+  return prefill_sessions(device, sessions <= 0 ? sessions_per_device() : sessions);
+}
+
 int fcs_phmm_last_device_ms(double* device_ms, double* rescue_ms) {
   if (!device_ms || !rescue_ms) return fail(FCS_ERR_INVALID, "[E::fcs_phmm_last_device_ms] null output");
   *device_ms = g_last_device_ms;
@@ -583,7 +688,7 @@ namespace {
 // stream into an output pre-filled with NaN, one D2H copy, and a check that
 // every pair's result was written (a pair the schedule or a class launch
 // skipped would otherwise go downstream as garbage).  Returns the results in
-// pinned memory (valid until the thread's next call).
+// pinned memory (valid while the caller holds the lease).
 struct PhmmStage {
   int64_t n_reads = 0, n_haps = 0, n_pairs = 0, read_bytes = 0, hap_bytes = 0;
   int32_t max_read_len = 0, max_hap_len = 0;
@@ -591,12 +696,13 @@ struct PhmmStage {
 enum { kRb, kBq, kIq, kDq, kGq, kRo, kRl, kHb, kHo, kHl, kPr, kPh, kNArr };
 
 template <typename Fill>
-int phmm_staged(const PhmmStage& g, const fcs_phmm_opts& opts, Fill&& fill, const double** host_out) {
+int phmm_staged(const PhmmStage& g, const fcs_phmm_opts& opts, SessionLease& lease, Fill&& fill,
+                const double** host_out) {
   int rc = check_device(opts.device);
   if (rc) return rc;
   FCS_HIP_CHECK(hipSetDevice(opts.device));
-  Session* S = session(opts.device);
-  if (!S) return fail(FCS_ERR_DEVICE, "[E::fcship] stream creation failed");
+  if ((rc = lease.acquire(opts.device))) return rc;
+  Session* S = lease.get();
   const size_t RB = (size_t)g.read_bytes, HB = (size_t)g.hap_bytes, nr = (size_t)g.n_reads, nh = (size_t)g.n_haps,
                np = (size_t)g.n_pairs;
   Layout L;
@@ -771,7 +877,8 @@ int fcs_phmm_compute_pairs(const fcs_phmm_batch* b, double* out_log10, const fcs
   const size_t RB = (size_t)b->read_bytes, HB = (size_t)b->hap_bytes, nr = (size_t)b->n_reads,
                nh = (size_t)b->n_haps, np = (size_t)b->n_pairs;
   const double* res = nullptr;
-  rc = phmm_staged(g, opts, [&](Session* S, const size_t* off) {
+  SessionLease lease;  // holds the pinned results until they are copied out
+  rc = phmm_staged(g, opts, lease, [&](Session* S, const size_t* off) {
     std::memcpy(S->h<void>(off[kRb]), b->read_bases, RB);
     std::memcpy(S->h<void>(off[kBq]), b->read_bq, RB);
     std::memcpy(S->h<void>(off[kIq]), b->read_iq, RB);
@@ -838,7 +945,8 @@ int fcs_phmm_compute_regions(const fcs_phmm_region* regions, int32_t n_regions, 
   if (opts_in) opts = *opts_in;
   else fcs_phmm_opts_default(&opts);
   const double* res = nullptr;
-  const int rc = phmm_staged(g, opts, [&](Session* S, const size_t* off) {
+  SessionLease lease;  // holds the pinned results until they are copied out
+  const int rc = phmm_staged(g, opts, lease, [&](Session* S, const size_t* off) {
     uint8_t *rb = S->h<uint8_t>(off[kRb]), *bq = S->h<uint8_t>(off[kBq]), *iq = S->h<uint8_t>(off[kIq]),
             *dq = S->h<uint8_t>(off[kDq]), *gq = S->h<uint8_t>(off[kGq]), *hb = S->h<uint8_t>(off[kHb]);
     int64_t *roff = S->h<int64_t>(off[kRo]), *hoff = S->h<int64_t>(off[kHo]);
@@ -987,8 +1095,9 @@ int fcs_bsw_extend_batch(const fcs_bsw_batch* b, const fcs_bsw_params* params, i
     if (b->tbuf[i] > 4) return fail(FCS_ERR_INVALID, "[E::fcs_bsw_extend_batch] target base code > 4");
   if ((rc = check_device(device))) return rc;
   FCS_HIP_CHECK(hipSetDevice(device));
-  Session* S = session(device);
-  if (!S) return fail(FCS_ERR_DEVICE, "[E::fcship] stream creation failed");
+  SessionLease lease;
+  if ((rc = lease.acquire(device))) return rc;
+  Session* S = lease.get();
   const size_t n = (size_t)b->n;
   Layout L;
   const size_t oq = L.add((size_t)b->qbytes), oqo = L.add(8 * n), oql = L.add(4 * n), ot = L.add((size_t)b->tbytes),
@@ -1142,8 +1251,9 @@ int fcs_bsw_global(const fcs_bsw_task* tasks, int32_t n, const fcs_bsw_params* p
     if (pk.t[i] > 4) return fail(FCS_ERR_INVALID, "[E::fcs_bsw_global] target base code > 4");
   if ((rc = check_device(device))) return rc;
   FCS_HIP_CHECK(hipSetDevice(device));
-  Session* S = session(device);
-  if (!S) return fail(FCS_ERR_DEVICE, "[E::fcship] stream creation failed");
+  SessionLease lease;
+  if ((rc = lease.acquire(device))) return rc;
+  Session* S = lease.get();
   const size_t nn = (size_t)n;
   // The direction matrix (and its offsets) only when CIGARs are wanted: a
   // scores-only batch needs none of it.
@@ -1286,6 +1396,6 @@ int fcs_ksw_global2(int qlen, const uint8_t* query, int tlen, const uint8_t* tar
   return score;
 }
 
-int fcs_abi_symbol_count(void) { return 36; }
+int fcs_abi_symbol_count(void) { return 37; }
 
 }  // extern "C"

@@ -689,6 +689,7 @@ int align_main(int argc, char** argv) {
   const std::vector<int> gpus = conf().gpu_devices();
   if (gpus.empty()) throw failedCommand("[E::fcs-genome] no GPU visible (gpu.devices); the GPU path has no CPU fallback");
 
+  const uint64_t t_start = now_us();
   const Reference ref = load_fasta(ref_path);
   AlignOptions opt;
   opt.gpu = gpus[0];
@@ -698,7 +699,9 @@ int align_main(int argc, char** argv) {
     const int nt = conf().get_int("bwa.nt");
     opt.threads = nt > 0 ? nt : (int)std::min(16u, std::max(1u, std::thread::hardware_concurrency()));
   }
+  const uint64_t t_ref = now_us();
   const KmerIndex idx(ref, opt.k);
+  const uint64_t t_idx = now_us();
   std::vector<BamRecord> recs;
   AlignStats tot;
   auto add = [&](const AlignStats& st) {
@@ -754,6 +757,7 @@ int align_main(int argc, char** argv) {
     }
     flush();
   }
+  const uint64_t t_aln = now_us();
   std::stable_sort(recs.begin(), recs.end(), [](const BamRecord& x, const BamRecord& y) {
     const uint32_t a = (uint32_t)x.ref_id, b = (uint32_t)y.ref_id;  // unmapped (-1) last
     return a != b ? a < b : x.pos < y.pos;
@@ -823,6 +827,10 @@ int align_main(int argc, char** argv) {
               << tot.pe_avg << " +- " << tot.pe_std << " [" << tot.pe_low << ", " << tot.pe_high << "] from "
               << tot.pe_pairs << " pairs";
   std::cerr << std::endl;
+  const uint64_t t_end = now_us();
+  std::cerr << "[fcs-genome align] phases: reference " << (t_ref - t_start) / 1e6 << " s, FMD index "
+            << (t_idx - t_ref) / 1e6 << " s, FASTQ + alignment " << (t_aln - t_idx) / 1e6 << " s (alignment "
+            << tot.seconds << " s), sort + BAM + index " << (t_end - t_aln) / 1e6 << " s" << std::endl;
   return 0;
 }
 

@@ -179,6 +179,7 @@ void BgzfWriter::drain(size_t keep) {
     const std::vector<uint8_t> blk = pending_.front().get();
     pending_.pop_front();
     if (std::fwrite(blk.data(), 1, blk.size(), f_) != blk.size()) throw internalError("[E::bgzf] write failed");
+    coffs_.push_back(coff_);
     coff_ += blk.size();
   }
 }

@@ -38,6 +38,10 @@ class BgzfWriter {
     return (coff_ << 16) | (uint64_t)buf_.size();
   }
   void close();  // flush + EOF block
+  // Compressed start of every block written so far, in order (complete after
+  // close()); with no flush() between writes, block k holds the uncompressed
+  // bytes [k kBgzfBlockData, (k + 1) kBgzfBlockData).
+  const std::vector<uint64_t>& block_offsets() const { return coffs_; }
 
  private:
   void emit_block(const uint8_t* data, size_t n);
@@ -46,6 +50,7 @@ class BgzfWriter {
   int level_;
   std::vector<uint8_t> buf_;
   uint64_t coff_ = 0;  // compressed offset of the block being filled (all pending blocks written)
+  std::vector<uint64_t> coffs_;
   bool closed_ = false;
   // blocks compress on worker threads (htslib's thread pool role) and are
   // written in order; tell() first writes every pending block

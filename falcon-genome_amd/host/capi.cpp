@@ -278,6 +278,9 @@ int fcsg_vcf_concat(const char* const* inputs, int n, const char* output) {
   return guard([&] { vcf_concat(std::vector<std::string>(inputs, inputs + n), output); });
 }
 
+int fcsg_bgzip_tabix(const char* in, const char* out) {
+  return guard([&] { bgzip_tabix_file(in, out); });
+}
 int fcsg_tabix(const char* vcf_gz) {
   return guard([&] { tabix_index_vcf(vcf_gz); });
 }

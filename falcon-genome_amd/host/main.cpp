@@ -191,8 +191,7 @@ int htc_main(int argc, char** argv) {
   ex.addTask(std::make_shared<VCFConcatWorker>(parts, plain), sample_id, true);
   if (!a.has("skip-concat")) {
     if (!force && path_exists(plain + ".gz")) throw invalidParam("output " + plain + ".gz exists (use -f)");
-    ex.addTask(std::make_shared<ZIPWorker>(plain, plain + ".gz", force), sample_id, true);
-    ex.addTask(std::make_shared<TabixWorker>(plain + ".gz"), sample_id, true);
+    ex.addTask(std::make_shared<ZIPWorker>(plain, plain + ".gz", force, true), sample_id, true);
   }
   ex.run();
   warm.wait();
@@ -242,8 +241,7 @@ int mutect2_main(int argc, char** argv) {
                sample_id);
   }
   ex.addTask(std::make_shared<VCFConcatWorker>(parts, output), sample_id, true);
-  ex.addTask(std::make_shared<ZIPWorker>(output, output + ".gz", true), sample_id, true);
-  ex.addTask(std::make_shared<TabixWorker>(output + ".gz"), sample_id, true);
+  ex.addTask(std::make_shared<ZIPWorker>(output, output + ".gz", true, true), sample_id, true);
   ex.run();
   warm.wait();
   if (warm.status() != 0) throw failedCommand(std::string("[E::fcs-genome] GPU warm-up failed: ") + fcs_last_error());

@@ -1,6 +1,9 @@
 #include "vcf.h"
 
+#include <algorithm>
+#include <cstdint>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <fstream>
 #include <map>
@@ -71,17 +74,44 @@ void VcfWriter::close() {
 }
 
 void vcf_concat(const std::vector<std::string>& inputs, const std::string& output) {
-  std::ofstream out(output);
+  // whole parts at a time: every line of the first part, the others without
+  // their '#' lines; a last line without '\n' gets one
+  std::FILE* out = std::fopen(output.c_str(), "wb");
   if (!out) throw fileNotFound(output + " (cannot write)");
+  std::vector<char> buf;
+  std::string tail;
   for (size_t i = 0; i < inputs.size(); ++i) {
-    std::ifstream in(inputs[i]);
-    if (!in) throw fileNotFound(inputs[i]);
-    std::string line;
-    while (std::getline(in, line)) {
-      if (!line.empty() && line[0] == '#' && i > 0) continue;
-      out << line << '\n';
+    std::FILE* in = std::fopen(inputs[i].c_str(), "rb");
+    if (!in) {
+      std::fclose(out);
+      throw fileNotFound(inputs[i]);
+    }
+    std::fseek(in, 0, SEEK_END);
+    const long n = std::ftell(in);
+    std::fseek(in, 0, SEEK_SET);
+    buf.resize((size_t)std::max(n, 0L));
+    const size_t got = n > 0 ? std::fread(buf.data(), 1, (size_t)n, in) : 0;
+    std::fclose(in);
+    buf.resize(got);
+    size_t p = 0, run = 0;  // copy [run, p) in one write when a skipped line or the end comes
+    bool ok = true;
+    while (p < buf.size()) {
+      const char* nl = static_cast<const char*>(std::memchr(buf.data() + p, '\n', buf.size() - p));
+      const size_t e = nl ? (size_t)(nl - buf.data()) + 1 : buf.size();
+      if (i > 0 && buf[p] == '#') {
+        ok = ok && std::fwrite(buf.data() + run, 1, p - run, out) == p - run;
+        run = e;
+      }
+      p = e;
+    }
+    ok = ok && std::fwrite(buf.data() + run, 1, buf.size() - run, out) == buf.size() - run;
+    if (ok && run < buf.size() && buf.back() != '\n') ok = std::fputc('\n', out) != EOF;
+    if (!ok) {
+      std::fclose(out);
+      throw internalError("[E::vcf] write to " + output + " failed");
     }
   }
+  if (std::fclose(out) != 0) throw internalError("[E::vcf] write to " + output + " failed");
 }
 
 void bgzip_file(const std::string& input, const std::string& output) {
@@ -104,48 +134,41 @@ void put(std::string& s, T v) {
   s.append(reinterpret_cast<const char*>(&v), sizeof v);
 }
 
-struct RefIndex {
-  std::map<uint32_t, std::vector<std::pair<uint64_t, uint64_t>>> bins;
-  std::vector<uint64_t> linear;  // 16 kb windows
-};
-
-}  // namespace
-
-void tabix_index_vcf(const std::string& vcf_gz) {
-  BgzfReader rd(vcf_gz);
-  std::vector<std::string> names;
-  std::map<std::string, int> name_id;
-  std::vector<RefIndex> idx;
-  std::string line;
-  int last_tid = -1;
-  int64_t last_pos = -1;
-  for (;;) {
-    const uint64_t beg_off = rd.tell();
-    if (!rd.getline(line)) break;
-    const uint64_t end_off = rd.tell();
-    if (line.empty() || line[0] == '#') continue;
-    const size_t t1 = line.find('\t'), t2 = line.find('\t', t1 + 1), t3 = line.find('\t', t2 + 1),
-                 t4 = line.find('\t', t3 + 1);
-    if (t4 == std::string::npos) throw formatError(vcf_gz + ": malformed VCF line");
-    const std::string chrom = line.substr(0, t1);
-    const int64_t pos = std::stoll(line.substr(t1 + 1, t2 - t1 - 1));
-    const int64_t rlen = (int64_t)(t4 - t3 - 1);
-    auto it = name_id.find(chrom);
-    int tid;
-    if (it == name_id.end()) {
-      tid = (int)names.size();
-      name_id[chrom] = tid;
-      names.push_back(chrom);
-      idx.emplace_back();
-    } else {
-      tid = it->second;
-      if (tid != last_tid) throw formatError(vcf_gz + ": chromosome blocks not contiguous (unsorted VCF)");
+// The tabix index (VCF preset) of a coordinate-sorted VCF, fed one record
+// line at a time with the virtual offsets of its start and of the next line.
+class TabixBuilder {
+ public:
+  explicit TabixBuilder(std::string label) : label_(std::move(label)) {}
+  void add(const char* line, size_t len, uint64_t beg_off, uint64_t end_off) {
+    if (len == 0 || line[0] == '#') return;
+    const char* e = line + len;
+    const char* t[4];
+    const char* p = line;
+    for (int k = 0; k < 4; ++k) {
+      t[k] = static_cast<const char*>(std::memchr(p, '\t', (size_t)(e - p)));
+      if (!t[k]) throw formatError(label_ + ": malformed VCF line");
+      p = t[k] + 1;
     }
-    if (tid == last_tid && pos < last_pos) throw formatError(vcf_gz + ": positions not sorted");
-    last_tid = tid;
-    last_pos = pos;
+    const std::string chrom(line, t[0]);
+    char* pe = nullptr;
+    const int64_t pos = std::strtoll(t[0] + 1, &pe, 10);
+    if (pe != t[1]) throw formatError(label_ + ": malformed VCF POS");
+    const int64_t rlen = (int64_t)(t[3] - t[2] - 1);
+    int tid;
+    if (!names_.empty() && chrom == names_.back()) {
+      tid = (int)names_.size() - 1;
+    } else {
+      if (name_id_.count(chrom)) throw formatError(label_ + ": chromosome blocks not contiguous (unsorted VCF)");
+      tid = (int)names_.size();
+      name_id_[chrom] = tid;
+      names_.push_back(chrom);
+      idx_.emplace_back();
+    }
+    if (tid == last_tid_ && pos < last_pos_) throw formatError(label_ + ": positions not sorted");
+    last_tid_ = tid;
+    last_pos_ = pos;
     const int64_t beg = pos - 1, end = beg + std::max<int64_t>(rlen, 1);
-    RefIndex& ri = idx[tid];
+    RefIndex& ri = idx_[tid];
     auto& chunks = ri.bins[reg2bin(beg, end)];
     if (!chunks.empty() && chunks.back().second == beg_off) chunks.back().second = end_off;  // extend the run
     else chunks.emplace_back(beg_off, end_off);
@@ -154,37 +177,150 @@ void tabix_index_vcf(const std::string& vcf_gz) {
     for (int64_t w = w0; w <= w1; ++w)
       if (ri.linear[w] == 0) ri.linear[w] = beg_off;
   }
-  std::string s = "TBI\1";
-  put<int32_t>(s, (int32_t)names.size());
-  put<int32_t>(s, 2);    // format: VCF
-  put<int32_t>(s, 1);    // col_seq
-  put<int32_t>(s, 2);    // col_beg
-  put<int32_t>(s, 0);    // col_end
-  put<int32_t>(s, '#');  // meta char
-  put<int32_t>(s, 0);    // skip
-  std::string nm;
-  for (const std::string& n : names) nm += n + '\0';
-  put<int32_t>(s, (int32_t)nm.size());
-  s += nm;
-  for (RefIndex& ri : idx) {
-    put<int32_t>(s, (int32_t)ri.bins.size());
-    for (const auto& b : ri.bins) {
-      put<uint32_t>(s, b.first);
-      put<int32_t>(s, (int32_t)b.second.size());
-      for (const auto& c : b.second) {
-        put<uint64_t>(s, c.first);
-        put<uint64_t>(s, c.second);
+  void write(const std::string& path) {
+    std::string s = "TBI\1";
+    put<int32_t>(s, (int32_t)names_.size());
+    put<int32_t>(s, 2);    // format: VCF
+    put<int32_t>(s, 1);    // col_seq
+    put<int32_t>(s, 2);    // col_beg
+    put<int32_t>(s, 0);    // col_end
+    put<int32_t>(s, '#');  // meta char
+    put<int32_t>(s, 0);    // skip
+    std::string nm;
+    for (const std::string& n : names_) nm += n + '\0';
+    put<int32_t>(s, (int32_t)nm.size());
+    s += nm;
+    for (RefIndex& ri : idx_) {
+      put<int32_t>(s, (int32_t)ri.bins.size());
+      for (const auto& b : ri.bins) {
+        put<uint32_t>(s, b.first);
+        put<int32_t>(s, (int32_t)b.second.size());
+        for (const auto& c : b.second) {
+          put<uint64_t>(s, c.first);
+          put<uint64_t>(s, c.second);
+        }
       }
+      // empty windows take the next non-empty offset to their left (tabix convention)
+      for (size_t w = 1; w < ri.linear.size(); ++w)
+        if (ri.linear[w] == 0) ri.linear[w] = ri.linear[w - 1];
+      put<int32_t>(s, (int32_t)ri.linear.size());
+      for (uint64_t o : ri.linear) put<uint64_t>(s, o);
     }
-    // empty windows take the next non-empty offset to their left (tabix convention)
-    for (size_t w = 1; w < ri.linear.size(); ++w)
-      if (ri.linear[w] == 0) ri.linear[w] = ri.linear[w - 1];
-    put<int32_t>(s, (int32_t)ri.linear.size());
-    for (uint64_t o : ri.linear) put<uint64_t>(s, o);
+    BgzfWriter w(path);
+    w.write(s);
+    w.close();
   }
-  BgzfWriter w(vcf_gz + ".tbi");
-  w.write(s);
+
+ private:
+  struct RefIndex {
+    std::map<uint32_t, std::vector<std::pair<uint64_t, uint64_t>>> bins;
+    std::vector<uint64_t> linear;  // 16 kb windows
+  };
+  std::string label_;
+  std::vector<std::string> names_;
+  std::map<std::string, int> name_id_;
+  std::vector<RefIndex> idx_;
+  int last_tid_ = -1;
+  int64_t last_pos_ = -1;
+};
+
+}  // namespace
+
+void tabix_index_vcf(const std::string& vcf_gz) {
+  BgzfReader rd(vcf_gz);
+  TabixBuilder tb(vcf_gz);
+  std::string line;
+  for (;;) {
+    const uint64_t beg_off = rd.tell();
+    if (!rd.getline(line)) break;
+    tb.add(line.data(), line.size(), beg_off, rd.tell());
+  }
+  tb.write(vcf_gz + ".tbi");
+}
+
+void bgzip_tabix_file(const std::string& input, const std::string& output) {
+  // One pass over the plain VCF: its bytes go to the (parallel) BGZF writer
+  // and its record lines to the index.  The writer packs exactly
+  // kBgzfBlockData bytes per block, so a line's uncompressed offset U names
+  // its block and in-block offset, and the blocks' compressed starts (known
+  // after close) give the virtual offsets — the same ones a BgzfReader's
+  // tell() reports (a line ending at a block's end is at (block, kBgzfBlockData)).
+  std::FILE* in = std::fopen(input.c_str(), "rb");
+  if (!in) throw fileNotFound(input);
+  BgzfWriter w(output);
+  struct Rec {
+    uint64_t u0, u1, at;  // line start / end offsets; `at` into `lines`
+    uint32_t len;
+  };
+  std::vector<Rec> recs;
+  std::string lines;  // the record lines' first five columns (enough for the index)
+  std::vector<char> buf(4 << 20);
+  std::string carry;
+  uint64_t u = 0;  // uncompressed offset of buf[0] - carry.size()
+  auto take = [&](const char* s, size_t n, uint64_t u0) {
+    if (n == 0 || s[0] == '#') return false;
+    size_t keep = n, tabs = 0;
+    for (size_t k = 0; k < n; ++k)
+      if (s[k] == '\t' && ++tabs == 5) {
+        keep = k;
+        break;
+      }
+    recs.push_back({u0, u0 + n + 1, (uint64_t)lines.size(), (uint32_t)keep});
+    lines.append(s, keep);
+    return true;
+  };
+  for (;;) {
+    const size_t n = std::fread(buf.data(), 1, buf.size(), in);
+    if (n == 0) break;
+    w.write(buf.data(), n);
+    size_t p = 0;
+    if (!carry.empty()) {
+      const char* nl = static_cast<const char*>(std::memchr(buf.data(), '\n', n));
+      const size_t e = nl ? (size_t)(nl - buf.data()) : n;
+      carry.append(buf.data(), e);
+      if (!nl) {
+        u += n;
+        continue;
+      }
+      take(carry.data(), carry.size(), u - (carry.size() - e));
+      carry.clear();
+      p = e + 1;
+    }
+    while (p < n) {
+      const char* nl = static_cast<const char*>(std::memchr(buf.data() + p, '\n', n - p));
+      if (!nl) {
+        carry.assign(buf.data() + p, n - p);
+        break;
+      }
+      const size_t e = (size_t)(nl - buf.data());
+      take(buf.data() + p, e - p, u + p);
+      p = e + 1;
+    }
+    u += n;
+  }
+  std::fclose(in);
+  if (!carry.empty()) {  // a last line without '\n' ends at the end of the data
+    if (take(carry.data(), carry.size(), u - carry.size())) recs.back().u1 = UINT64_MAX;  // see voff
+  }
   w.close();
+  const std::vector<uint64_t>& co = w.block_offsets();
+  uint64_t file_size = 0;
+  if (std::FILE* f = std::fopen(output.c_str(), "rb")) {
+    std::fseek(f, 0, SEEK_END);
+    file_size = (uint64_t)std::ftell(f);
+    std::fclose(f);
+  }
+  auto voff = [&](uint64_t x) -> uint64_t {
+    // a last line without '\n': a reader's getline runs on through the EOF
+    // block, so tell() is the end of the file
+    if (x == UINT64_MAX) return file_size << 16;
+    const uint64_t B = kBgzfBlockData;
+    if (x > 0 && x % B == 0) return (co[x / B - 1] << 16) | B;
+    return (co[x / B] << 16) | (x % B);
+  };
+  TabixBuilder tb(output);
+  for (const Rec& r : recs) tb.add(lines.data() + r.at, r.len, voff(r.u0), voff(r.u1));
+  tb.write(output + ".tbi");
 }
 
 }  // namespace fcsg

@@ -51,5 +51,8 @@ void vcf_concat(const std::vector<std::string>& inputs, const std::string& outpu
 void bgzip_file(const std::string& input, const std::string& output);
 // Build <bgzipped VCF>.tbi (tabix spec: VCF preset, 14-bit binning, 16 kb linear index).
 void tabix_index_vcf(const std::string& vcf_gz);
+// bgzip_file + tabix_index_vcf in one pass over the plain VCF (the index from
+// the plain lines and the writer's block offsets; same files as the two calls).
+void bgzip_tabix_file(const std::string& input, const std::string& output);
 
 }  // namespace fcsg

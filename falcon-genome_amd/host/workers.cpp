@@ -172,13 +172,15 @@ int VCFConcatWorker::run(TaskContext&) {
   return 0;
 }
 
-ZIPWorker::ZIPWorker(std::string input, std::string output, bool)
-    : Worker(1, 1, {}, "bgzip"), input_(std::move(input)), output_(std::move(output)) {}
+ZIPWorker::ZIPWorker(std::string input, std::string output, bool, bool index)
+    : Worker(1, 1, {}, index ? "bgzip + tabix" : "bgzip"), input_(std::move(input)), output_(std::move(output)),
+      index_(index) {}
 
 void ZIPWorker::check() {}
 
 int ZIPWorker::run(TaskContext&) {
-  bgzip_file(input_, output_);
+  if (index_) bgzip_tabix_file(input_, output_);
+  else bgzip_file(input_, output_);
   return 0;
 }
 
@@ -192,17 +194,10 @@ int TabixWorker::run(TaskContext&) {
 DeviceWarmupWorker::DeviceWarmupWorker(std::vector<int> gpus) : Worker(1, 1, {}, "GPU warm-up"), gpus_(std::move(gpus)) {}
 
 int DeviceWarmupWorker::run(TaskContext&) {
-  // a 1x1 PairHMM call per device builds and uploads its GKL tables
-  static const uint8_t b[1] = {'A'}, q[1] = {30}, g[1] = {10}, iq[1] = {45};
-  const fcs_phmm_read r{b, q, iq, iq, g, 1};
-  const fcs_phmm_hap h{b, 1};
-  double out = 0;
-  for (int d : gpus_) {
-    fcs_phmm_opts o;
-    fcs_phmm_opts_default(&o);
-    o.device = d;
-    if (fcs_phmm_compute(&r, 1, &h, 1, &out, &o) != FCS_OK) return 1;
-  }
+  // runtime, code objects, GKL tables and the pooled call sessions of each
+  // device, while the shards decode their first reads
+  for (int d : gpus_)
+    if (fcs_device_warmup(d, 0) != FCS_OK) return 1;
   return 0;
 }
 

@@ -74,12 +74,14 @@ class VCFConcatWorker : public Worker {
 
 class ZIPWorker : public Worker {
  public:
-  ZIPWorker(std::string input, std::string output, bool flag_f = true);
+  // index: also write output.tbi from the same pass (bgzip + tabix as one stage)
+  ZIPWorker(std::string input, std::string output, bool flag_f = true, bool index = false);
   void check() override;
   int run(TaskContext& ctx) override;
 
  private:
   std::string input_, output_;
+  bool index_;
 };
 
 class TabixWorker : public Worker {

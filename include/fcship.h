@@ -62,6 +62,15 @@ const char* fcs_version(void);
 /* Build/ABI self-description: number of symbols this library exports that are
  * declared in this header (used by the loader test). */
 int fcs_abi_symbol_count(void);
+/* Brings `device` up ahead of the first real call: the HIP runtime, the code
+ * objects and the GKL tables (a 1x1 PairHMM call), and `sessions` pooled
+ * call sessions (<= 0: the pool's size, FCS_SESSIONS_PER_DEVICE, default 4).
+ * A session is the stream, side streams and staging arenas the host-pointer
+ * entry points lease for one call; a call finding every session busy waits
+ * for one.  fcs-genome runs this in the background while the first shards
+ * decode their reads (the reference's BackgroundExecutor role,
+ * /root/reference/include/fcs-genome/BackgroundExecutor.h:12). */
+int fcs_device_warmup(int32_t device, int32_t sessions);
 
 /* ----------------------------------------------------------------- PairHMM */
 /* One read: bases + the four per-base quality arrays GATK hands to the PairHMM

@@ -200,6 +200,51 @@ def test_vcf_concat_bgzip_tabix(tmp_path):
         b = H.reg2bin(beg, beg + len(ref))
         assert any(a <= voff < e for a, e in bins[b]), (line, voff)
         assert lin[beg >> 14] <= voff
+    # the one-pass bgzip + tabix (htc / mutect2's VCF tail) writes the same two files
+    gz2 = tmp_path / "one.vcf.gz"
+    H.check(H.lib.fcsg_bgzip_tabix(str(out).encode(), str(gz2).encode()))
+    assert gz2.read_bytes() == gz.read_bytes()
+    assert gzip.decompress((tmp_path / "one.vcf.gz.tbi").read_bytes()) == \
+        gzip.decompress((tmp_path / "all.vcf.gz.tbi").read_bytes())
+
+
+def test_bgzip_tabix_one_pass_block_edges(tmp_path):
+    """Lines ending exactly at a BGZF block's end (offset 0xff00), lines
+    spanning blocks and a last line without a newline: the one-pass index
+    equals the two-pass one (a reader's tell() semantics), and bulk concat
+    keeps part 0's header, drops the others' and ends the last line."""
+    B = 0xff00
+    hdr = "##fileformat=VCFv4.2\n#CHROM\tPOS\tID\tREF\tALT\tQUAL\tFILTER\tINFO\n"
+    body, pos = [], 1
+    total = len(hdr)
+    while total < 3 * B + 500:
+        line = f"c1\t{pos}\t.\tA\tT\t50\tPASS\t"
+        # pad the INFO column so that some lines end right at a block edge
+        nxt = (total // B + 1) * B
+        need = nxt - total - len(line) - 1
+        line += ("X" * need if 0 < need < 40 else "DP=1")
+        body.append(line)
+        total += len(line) + 1
+        pos += 7
+    text = hdr + "\n".join(body)  # no final newline
+    assert any((len(hdr) + sum(len(x) + 1 for x in body[:k + 1])) % B == 0 for k in range(len(body)))
+    parts = [tmp_path / "p0.vcf", tmp_path / "p1.vcf"]
+    half = len(body) // 2
+    parts[0].write_text(hdr + "".join(x + "\n" for x in body[:half]))
+    parts[1].write_text(hdr + "\n".join(body[half:]))
+    plain = tmp_path / "all.vcf"
+    arr = (C.c_char_p * 2)(*[str(p).encode() for p in parts])
+    H.check(H.lib.fcsg_vcf_concat(arr, 2, str(plain).encode()))
+    assert plain.read_text() == text + "\n"
+    plain.write_text(text)
+    gz = tmp_path / "two.vcf.gz"
+    H.check(H.lib.fcsg_bgzf_compress_file(str(plain).encode(), str(gz).encode()))
+    H.check(H.lib.fcsg_tabix(str(gz).encode()))
+    gz1 = tmp_path / "one.vcf.gz"
+    H.check(H.lib.fcsg_bgzip_tabix(str(plain).encode(), str(gz1).encode()))
+    assert gz1.read_bytes() == gz.read_bytes()
+    assert gzip.decompress((tmp_path / "one.vcf.gz.tbi").read_bytes()) == \
+        gzip.decompress((tmp_path / "two.vcf.gz.tbi").read_bytes())
 
 
 # ------------------------------------------------------------------ intervals

@@ -385,3 +385,34 @@ def test_multi_device_static_partition(gpu):
         assert rm.value == r1.value
     assert r1.value > 0
     check_parity(p, one, False)
+
+
+def test_session_pool_concurrent_calls(gpu):
+    """fcs_device_warmup brings up the device and the pooled call sessions;
+    then 16 host threads (the htc stage's shard threads) call
+    fcs_phmm_compute_pairs at once through a pool of at most 4 sessions (a call
+    finding them all busy waits).  Every thread's results equal its batch's
+    result computed alone."""
+    import threading
+    assert fcship.lib.fcs_device_warmup(0, 0) == 0, fcship.lib.fcs_last_error()
+    batches = []
+    for k in range(16):
+        reads, haps = random_batch(500 + k, 40, 6, 60, 151, 100, 300)
+        batches.append(fcship.make_pairs(reads, haps))
+    alone = [fcship.phmm_compute_pairs(p) for p in batches]
+    got, errs = [None] * 16, []
+
+    def run(k):
+        try:
+            for _ in range(3):
+                got[k] = fcship.phmm_compute_pairs(batches[k])
+        except Exception as e:  # noqa: BLE001
+            errs.append(repr(e))
+    th = [threading.Thread(target=run, args=(k,)) for k in range(16)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join()
+    assert not errs, errs
+    for k in range(16):
+        assert np.array_equal(got[k], alone[k]), k

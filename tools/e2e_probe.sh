@@ -3,12 +3,15 @@
 W=$(mktemp -d /tmp/e2e.XXXX)
 export FCS_GPU_DEVICES=0 FCS_LOG_DIR=$W/log FCS_TEMP_DIR=$W FCS_GATK_NPROCS=16
 B=$GRAFT_REPO_ROOT/falcon-genome_amd/bin/fcs-genome
-t() { local s=$(date +%s.%N); "$@"; local rc=$?; echo "  wall $(echo "$(date +%s.%N) - $s" | bc) s rc=$rc: $*" >&2; return $rc; }
+t() { local s=$(date +%s.%N); "$@"; local rc=$?; echo "  wall $(awk "BEGIN{print $(date +%s.%N) - $s}") s rc=$rc: $*" >&2; return $rc; }
 t timeout 300 $B synth -o $W/d -c chr1:4000000 -x 30 --tumor --noisy-frac 0.01 --paired 350 > /dev/null || exit 1
 for i in 1 2; do
   t timeout 300 $B htc -r $W/d/ref.fasta -i $W/d/sample.bam -o $W/h$i.g.vcf 2> $W/htc$i.err || { tail $W/htc$i.err; exit 1; }
   grep -E "finishes|Start" $W/htc$i.err
 done
+sed -e 's/^/  | /' $W/htc2.err | head -60
+t timeout 300 $B mutect2 -r $W/d/ref.fasta -t $W/d/tumor.bam -n $W/d/sample.bam -o $W/m2.vcf 2> $W/m2.err
+sed -e 's/^/  | /' $W/m2.err | head -60
 t timeout 300 $B htc -r $W/d/ref.fasta -i $W/d/sample.bam -o $W/hv.vcf -v 2> $W/htcv.err
 grep -E "finishes" $W/htcv.err
 grep -h "shard" $W/log/*.log 2>/dev/null | head -3
