@@ -4,6 +4,7 @@
 #include <cmath>
 #include <cstring>
 #include <fstream>
+#include <future>
 #include <iostream>
 #include <map>
 #include <thread>
@@ -716,52 +717,51 @@ int align_main(int argc, char** argv) {
     if (st.pe_pairs) tot.pe_pairs = st.pe_pairs, tot.pe_low = st.pe_low, tot.pe_high = st.pe_high,
                      tot.pe_avg = st.pe_avg, tot.pe_std = st.pe_std;
   };
-  if (fq2.empty()) {
-    std::ifstream in(fq1);
-    std::vector<std::string> names, seqs, quals;
-    std::string n, s, q;
-    auto flush = [&] {
-      if (names.empty()) return;
-      add(align_reads(ref, idx, names, seqs, quals, opt, recs));
-      names.clear();
-      seqs.clear();
-      quals.clear();
-    };
-    while (read_fastq(in, n, s, q)) {
-      names.push_back(n);
-      seqs.push_back(s);
-      quals.push_back(q);
-      if ((int)names.size() >= opt.chunk_size) flush();
-    }
-    flush();
-  } else {  // paired: both files in lockstep, bwa's per-batch insert-size estimate
-    std::ifstream in1(fq1), in2(fq2);
+  // FASTQ chunks are read on a second thread while the previous chunk aligns
+  struct Chunk {
     std::vector<std::string> names, s1, q1, s2, q2;
+  };
+  std::ifstream in1(fq1), in2;
+  if (!fq2.empty()) in2.open(fq2);
+  const size_t per_chunk = (size_t)std::max(1, fq2.empty() ? opt.chunk_size : opt.chunk_size / 2);
+  auto read_chunk = [&](Chunk& c) {
+    for (auto* v : {&c.names, &c.s1, &c.q1, &c.s2, &c.q2}) v->clear();
     std::string n1, a1, b1, n2, a2, b2;
-    auto flush = [&] {
-      if (names.empty()) return;
-      add(align_pairs(ref, idx, names, s1, q1, s2, q2, opt, recs));
-      for (auto* v : {&names, &s1, &q1, &s2, &q2}) v->clear();
-    };
-    for (;;) {
-      const bool g1 = read_fastq(in1, n1, a1, b1), g2 = read_fastq(in2, n2, a2, b2);
-      if (g1 != g2) throw formatError("paired FASTQ files differ in read count");
+    while (c.names.size() < per_chunk) {
+      const bool g1 = read_fastq(in1, n1, a1, b1);
+      if (!fq2.empty()) {  // paired: both files in lockstep
+        const bool g2 = read_fastq(in2, n2, a2, b2);
+        if (g1 != g2) throw formatError("paired FASTQ files differ in read count");
+        if (g1 && n1 != n2) throw formatError("paired FASTQ names differ: " + n1 + " vs " + n2);
+        if (g1) c.s2.push_back(std::move(a2)), c.q2.push_back(std::move(b2));
+      }
       if (!g1) break;
-      if (n1 != n2) throw formatError("paired FASTQ names differ: " + n1 + " vs " + n2);
-      names.push_back(n1);
-      s1.push_back(a1);
-      q1.push_back(b1);
-      s2.push_back(a2);
-      q2.push_back(b2);
-      if ((int)names.size() >= opt.chunk_size / 2) flush();
+      c.names.push_back(std::move(n1));
+      c.s1.push_back(std::move(a1));
+      c.q1.push_back(std::move(b1));
     }
-    flush();
+  };
+  Chunk cur, nxt;
+  read_chunk(cur);
+  while (!cur.names.empty()) {
+    auto ahead = std::async(std::launch::async, [&] { read_chunk(nxt); });
+    try {
+      if (fq2.empty()) add(align_reads(ref, idx, cur.names, cur.s1, cur.q1, opt, recs));
+      else add(align_pairs(ref, idx, cur.names, cur.s1, cur.q1, cur.s2, cur.q2, opt, recs));  // bwa's per-batch insert-size estimate
+    } catch (...) {
+      ahead.wait();
+      throw;
+    }
+    ahead.get();
+    std::swap(cur, nxt);
   }
   const uint64_t t_aln = now_us();
-  std::stable_sort(recs.begin(), recs.end(), [](const BamRecord& x, const BamRecord& y) {
-    const uint32_t a = (uint32_t)x.ref_id, b = (uint32_t)y.ref_id;  // unmapped (-1) last
-    return a != b ? a < b : x.pos < y.pos;
-  });
+  // coordinate order by packed keys (reference id as unsigned: unmapped last;
+  // the position's sign bit flipped; ties by input order, as a stable sort)
+  std::vector<std::pair<uint64_t, uint32_t>> order(recs.size());
+  for (size_t i = 0; i < recs.size(); ++i)
+    order[i] = {((uint64_t)(uint32_t)recs[i].ref_id << 32) | ((uint32_t)recs[i].pos ^ 0x80000000u), (uint32_t)i};
+  std::sort(order.begin(), order.end());
   BamHeader h;
   h.text = "@HD\tVN:1.6\tSO:coordinate\n";
   for (const Contig& c : ref.contigs) {
@@ -773,9 +773,9 @@ int align_main(int argc, char** argv) {
   h.text += "@PG\tID:fcs-genome\tPN:fcs-genome align\n";
   if (!disable_merge) {
     BamWriter w(output, h);
-    for (const BamRecord& r : recs) w.write(r);
+    w.index_on_close();
+    for (const auto& o : order) w.write(recs[o.second]);
     w.close();
-    bam_index_build(output);
   } else {
     // bwa-flow --merge_bams=0 (reference BWAWorker.cpp:140-147, worker-align.cpp:186-195):
     // num_buckets coordinate-sorted bucket BAMs; here the buckets are the
@@ -796,7 +796,8 @@ int align_main(int argc, char** argv) {
         span[c].emplace_back(iv.lb, iv.ub);
         span_b[c].push_back(k);
       }
-    for (const BamRecord& r : recs) {
+    for (const auto& o : order) {
+      const BamRecord& r = recs[o.second];
       int k = nb - 1;
       if (r.ref_id >= 0) {
         const auto& sp = span[r.ref_id];
@@ -812,9 +813,9 @@ int align_main(int argc, char** argv) {
     for (int k = 0; k < nb; ++k) {
       const std::string bam = get_contig_fname(output, k, "bam");
       BamWriter w(bam, h);
+      w.index_on_close();
       for (const BamRecord* r : per[k]) w.write(*r);
       w.close();
-      bam_index_build(bam);
       std::ofstream bed(get_contig_fname(output, k, "bed"));
       for (const Interval& iv : buckets[k]) bed << iv.chrom << '\t' << iv.lb - 1 << '\t' << iv.ub << '\n';
     }

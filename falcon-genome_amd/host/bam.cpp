@@ -245,7 +245,8 @@ void decode_bam_record(const uint8_t* p, size_t n, BamRecord& r) {
 }
 
 // ------------------------------------------------------------------ files
-BamWriter::BamWriter(const std::string& path, const BamHeader& h, int level) : bgzf_(path, level) {
+BamWriter::BamWriter(const std::string& path, const BamHeader& h, int level)
+    : path_(path), nref_(h.names.size()), bgzf_(path, level) {
   std::string s = "BAM\1";
   put<int32_t>(s, (int32_t)h.text.size());
   s += h.text;
@@ -263,8 +264,10 @@ BamWriter::BamWriter(const std::string& path, const BamHeader& h, int level) : b
 void BamWriter::write(const BamRecord& r) {
   encode_bam_record(r, rec_);
   const int32_t bs = (int32_t)rec_.size();
+  const uint64_t u0 = bgzf_.upos();
   bgzf_.write(&bs, 4);
   bgzf_.write(rec_);
+  if (index_) spans_.push_back({r.ref_id, r.pos, r.ref_id >= 0 ? r.end() : 0, u0, bgzf_.upos()});
 }
 
 BamReader::BamReader(const std::string& path) : bgzf_(path) {
@@ -303,57 +306,89 @@ bool BamReader::next(BamRecord& r) {
 
 namespace fcsg {
 
-void bam_index_build(const std::string& bam_path) {
-  BamReader rd(bam_path);
-  const size_t nref = rd.header().names.size();
-  std::vector<std::map<uint32_t, std::vector<std::pair<uint64_t, uint64_t>>>> bins(nref);
-  std::vector<std::vector<uint64_t>> linear(nref);
-  uint64_t n_no_coor = 0;
-  BamRecord r;
-  int last_tid = -1;
-  int64_t last_pos = -1;
-  for (;;) {
-    const uint64_t beg_off = rd.tell();
-    if (!rd.next(r)) break;
-    const uint64_t end_off = rd.tell();
-    if (r.ref_id < 0) {
-      ++n_no_coor;
-      continue;
+namespace {
+
+// The BAI of a coordinate-sorted BAM, fed record by record with the virtual
+// offsets of its start and of the next record.
+class BaiBuilder {
+ public:
+  BaiBuilder(size_t nref, std::string label) : bins_(nref), linear_(nref), label_(std::move(label)) {}
+  void add(int32_t ref_id, int64_t pos, int64_t rend, uint64_t beg_off, uint64_t end_off) {
+    if (ref_id < 0) {
+      ++n_no_coor_;
+      return;
     }
-    if (r.ref_id < last_tid || (r.ref_id == last_tid && r.pos < last_pos))
-      throw formatError(bam_path + " is not coordinate-sorted; cannot index");
-    last_tid = r.ref_id;
-    last_pos = r.pos;
-    const int64_t beg = r.pos, end = std::max<int64_t>(r.end(), beg + 1);
-    auto& ch = bins[r.ref_id][reg2bin(beg, end)];
+    if ((size_t)ref_id >= bins_.size()) throw formatError(label_ + ": record reference id outside the header");
+    if (ref_id < last_tid_ || (ref_id == last_tid_ && pos < last_pos_))
+      throw formatError(label_ + " is not coordinate-sorted; cannot index");
+    last_tid_ = ref_id;
+    last_pos_ = pos;
+    const int64_t beg = pos, end = std::max<int64_t>(rend, beg + 1);
+    auto& ch = bins_[ref_id][reg2bin(beg, end)];
     if (!ch.empty() && ch.back().second == beg_off) ch.back().second = end_off;
     else ch.emplace_back(beg_off, end_off);
-    auto& lin = linear[r.ref_id];
+    auto& lin = linear_[ref_id];
     const int64_t w1 = (end - 1) >> 14;
     if ((int64_t)lin.size() <= w1) lin.resize(w1 + 1, 0);
     for (int64_t w = beg >> 14; w <= w1; ++w)
       if (lin[w] == 0) lin[w] = beg_off;
   }
-  std::string s = "BAI\1";
-  put<int32_t>(s, (int32_t)nref);
-  for (size_t t = 0; t < nref; ++t) {
-    put<int32_t>(s, (int32_t)bins[t].size());
-    for (const auto& b : bins[t]) {
-      put<uint32_t>(s, b.first);
-      put<int32_t>(s, (int32_t)b.second.size());
-      for (const auto& c : b.second) {
-        put<uint64_t>(s, c.first);
-        put<uint64_t>(s, c.second);
+  void write(const std::string& path) {
+    std::string s = "BAI\1";
+    put<int32_t>(s, (int32_t)bins_.size());
+    for (size_t t = 0; t < bins_.size(); ++t) {
+      put<int32_t>(s, (int32_t)bins_[t].size());
+      for (const auto& b : bins_[t]) {
+        put<uint32_t>(s, b.first);
+        put<int32_t>(s, (int32_t)b.second.size());
+        for (const auto& c : b.second) {
+          put<uint64_t>(s, c.first);
+          put<uint64_t>(s, c.second);
+        }
       }
+      auto& lin = linear_[t];
+      for (size_t w = 1; w < lin.size(); ++w)
+        if (lin[w] == 0) lin[w] = lin[w - 1];
+      put<int32_t>(s, (int32_t)lin.size());
+      for (uint64_t o : lin) put<uint64_t>(s, o);
     }
-    auto& lin = linear[t];
-    for (size_t w = 1; w < lin.size(); ++w)
-      if (lin[w] == 0) lin[w] = lin[w - 1];
-    put<int32_t>(s, (int32_t)lin.size());
-    for (uint64_t o : lin) put<uint64_t>(s, o);
+    put<uint64_t>(s, n_no_coor_);
+    write_file(path, s);
   }
-  put<uint64_t>(s, n_no_coor);
-  write_file(bam_path + ".bai", s);
+
+ private:
+  std::vector<std::map<uint32_t, std::vector<std::pair<uint64_t, uint64_t>>>> bins_;
+  std::vector<std::vector<uint64_t>> linear_;
+  std::string label_;
+  uint64_t n_no_coor_ = 0;
+  int last_tid_ = -1;
+  int64_t last_pos_ = -1;
+};
+
+}  // namespace
+
+void bam_index_build(const std::string& bam_path) {
+  BamReader rd(bam_path);
+  BaiBuilder bb(rd.header().names.size(), bam_path);
+  BamRecord r;
+  for (;;) {
+    const uint64_t beg_off = rd.tell();
+    if (!rd.next(r)) break;
+    bb.add(r.ref_id, r.pos, r.ref_id >= 0 ? r.end() : 0, beg_off, rd.tell());
+  }
+  bb.write(bam_path + ".bai");
+}
+
+void BamWriter::close() {
+  if (closed_) return;
+  closed_ = true;
+  bgzf_.close();
+  if (!index_) return;
+  BaiBuilder bb(nref_, path_);
+  for (const Span& s : spans_) bb.add(s.ref_id, s.beg, s.end, bgzf_.voffset(s.u0), bgzf_.voffset(s.u1));
+  spans_.clear();
+  spans_.shrink_to_fit();
+  bb.write(path_ + ".bai");
 }
 
 BamIndex::BamIndex(const std::string& bai_path) {

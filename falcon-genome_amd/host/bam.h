@@ -61,12 +61,25 @@ class BamWriter {
  public:
   BamWriter(const std::string& path, const BamHeader& h, int level = 6);
   void write(const BamRecord& r);
-  void close() { bgzf_.close(); }
+  // Also write <path>.bai at close(), from the records as they are written
+  // (coordinate order required): the index bam_index_build would compute,
+  // without reading the file back.
+  void index_on_close() { index_ = true; }
+  void close();
   uint64_t tell() { return bgzf_.tell(); }
 
  private:
+  struct Span {
+    int32_t ref_id;
+    int64_t beg, end;
+    uint64_t u0, u1;
+  };
+  std::string path_;
+  size_t nref_ = 0;
   BgzfWriter bgzf_;
   std::string rec_;
+  bool index_ = false, closed_ = false;
+  std::vector<Span> spans_;
 };
 
 class BamReader {

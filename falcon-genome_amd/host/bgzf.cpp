@@ -166,6 +166,7 @@ BgzfWriter::~BgzfWriter() {
 }
 
 void BgzfWriter::emit_block(const uint8_t* data, size_t n) {
+  ustarts_.push_back(ubytes_ - n);
   std::vector<uint8_t> in(data, data + n);
   const int level = level_;
   pending_.push_back(std::async(std::launch::async, [in = std::move(in), level] {
@@ -189,6 +190,7 @@ void BgzfWriter::write(const void* data, size_t n) {
   while (n > 0) {
     const size_t take = std::min(n, kBgzfBlockData - buf_.size());
     buf_.insert(buf_.end(), p, p + take);
+    ubytes_ += take;
     p += take;
     n -= take;
     if (buf_.size() >= kBgzfBlockData) flush();
@@ -209,6 +211,14 @@ void BgzfWriter::close() {
   std::fclose(f_);
   f_ = nullptr;
   closed_ = true;
+}
+
+uint64_t BgzfWriter::voffset(uint64_t u) const {
+  if (!closed_ || coffs_.size() != ustarts_.size()) throw internalError("[E::bgzf] voffset before close");
+  if (ustarts_.empty()) return 0;
+  size_t k = (size_t)(std::upper_bound(ustarts_.begin(), ustarts_.end(), u) - ustarts_.begin()) - 1;
+  if (k > 0 && u == ustarts_[k]) --k;  // a block boundary reached by reading: the end of the earlier block
+  return (coffs_[k] << 16) | (u - ustarts_[k]);
 }
 
 // ------------------------------------------------------------------ reader

@@ -42,6 +42,13 @@ class BgzfWriter {
   // close()); with no flush() between writes, block k holds the uncompressed
   // bytes [k kBgzfBlockData, (k + 1) kBgzfBlockData).
   const std::vector<uint64_t>& block_offsets() const { return coffs_; }
+  // Uncompressed bytes written so far (buffered ones included): a position
+  // that voffset() turns into a virtual offset once the writer is closed.
+  uint64_t upos() const { return ubytes_; }
+  // The virtual offset a BgzfReader's tell() reports at uncompressed position
+  // u after reading up to it (a block's end is (that block, its length), not
+  // the next block's start).  Valid after close().
+  uint64_t voffset(uint64_t u) const;
 
  private:
   void emit_block(const uint8_t* data, size_t n);
@@ -51,6 +58,8 @@ class BgzfWriter {
   std::vector<uint8_t> buf_;
   uint64_t coff_ = 0;  // compressed offset of the block being filled (all pending blocks written)
   std::vector<uint64_t> coffs_;
+  std::vector<uint64_t> ustarts_;  // uncompressed start of every block, in order
+  uint64_t ubytes_ = 0;
   bool closed_ = false;
   // blocks compress on worker threads (htslib's thread pool role) and are
   // written in order; tell() first writes every pending block

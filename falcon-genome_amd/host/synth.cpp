@@ -134,10 +134,10 @@ void write_reads(std::vector<SimRead>& reads, const BamHeader& hdr, const std::s
   });
   {
     BamWriter w(bam, hdr);
+    w.index_on_close();
     for (const SimRead& sr : reads) w.write(sr.rec);
     w.close();
   }
-  bam_index_build(bam);
   if (!fastq.empty()) {
     std::ofstream fq(fastq);
     for (const SimRead& sr : reads) fq << '@' << sr.rec.name << '\n' << sr.fq_seq << "\n+\n" << sr.fq_qual << '\n';

@@ -240,11 +240,9 @@ void tabix_index_vcf(const std::string& vcf_gz) {
 
 void bgzip_tabix_file(const std::string& input, const std::string& output) {
   // One pass over the plain VCF: its bytes go to the (parallel) BGZF writer
-  // and its record lines to the index.  The writer packs exactly
-  // kBgzfBlockData bytes per block, so a line's uncompressed offset U names
-  // its block and in-block offset, and the blocks' compressed starts (known
-  // after close) give the virtual offsets — the same ones a BgzfReader's
-  // tell() reports (a line ending at a block's end is at (block, kBgzfBlockData)).
+  // and its record lines to the index, by uncompressed offset; the writer
+  // turns those into the virtual offsets a BgzfReader's tell() reports once
+  // the blocks' compressed starts are known (after close).
   std::FILE* in = std::fopen(input.c_str(), "rb");
   if (!in) throw fileNotFound(input);
   BgzfWriter w(output);
@@ -303,7 +301,6 @@ void bgzip_tabix_file(const std::string& input, const std::string& output) {
     if (take(carry.data(), carry.size(), u - carry.size())) recs.back().u1 = UINT64_MAX;  // see voff
   }
   w.close();
-  const std::vector<uint64_t>& co = w.block_offsets();
   uint64_t file_size = 0;
   if (std::FILE* f = std::fopen(output.c_str(), "rb")) {
     std::fseek(f, 0, SEEK_END);
@@ -313,10 +310,7 @@ void bgzip_tabix_file(const std::string& input, const std::string& output) {
   auto voff = [&](uint64_t x) -> uint64_t {
     // a last line without '\n': a reader's getline runs on through the EOF
     // block, so tell() is the end of the file
-    if (x == UINT64_MAX) return file_size << 16;
-    const uint64_t B = kBgzfBlockData;
-    if (x > 0 && x % B == 0) return (co[x / B - 1] << 16) | B;
-    return (co[x / B] << 16) | (x % B);
+    return x == UINT64_MAX ? file_size << 16 : w.voffset(x);
   };
   TabixBuilder tb(output);
   for (const Rec& r : recs) tb.add(lines.data() + r.at, r.len, voff(r.u0), voff(r.u1));

@@ -167,6 +167,21 @@ def test_bai_seek_lands_before_first_overlapping_read(synth_small):
                 assert a < b
 
 
+def test_bai_on_write_equals_rebuild(synth_small, tmp_path):
+    """BamWriter's index-on-close (align, synth) writes the same .bai as
+    bam_index_build reading the finished BAM back (record virtual offsets
+    from the writer's block table, incl. records ending at block edges)."""
+    import shutil
+    src = synth_small / "sample.bam"
+    on_write = (str(src) + ".bai")
+    bam = tmp_path / "copy.bam"
+    shutil.copy(src, bam)
+    H.check(H.lib.fcsg_bam_index(str(bam).encode()))
+    a = open(on_write, "rb").read()
+    b = open(str(bam) + ".bai", "rb").read()
+    assert len(H.bgzf_blocks(src)) > 20 and a == b
+
+
 # ------------------------------------------------------------------ VCF tail
 def test_vcf_concat_bgzip_tabix(tmp_path):
     hdr = "##fileformat=VCFv4.2\n##contig=<ID=c1,length=500000>\n##contig=<ID=c2,length=90000>\n" \
