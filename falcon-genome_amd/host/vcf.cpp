@@ -1,6 +1,7 @@
 #include "vcf.h"
 
 #include <algorithm>
+#include <charconv>
 #include <cstdint>
 #include <cstdio>
 #include <cstdlib>
@@ -15,25 +16,47 @@
 
 namespace fcsg {
 
-std::string VcfRecord::to_line() const {
-  std::ostringstream ss;
-  ss << chrom << '\t' << pos << '\t' << id << '\t' << ref << '\t';
-  if (alts.empty()) ss << '.';
-  for (size_t i = 0; i < alts.size(); ++i) ss << (i ? "," : "") << alts[i];
-  ss << '\t';
-  if (qual < 0) ss << '.';
-  else {
-    char b[32];
-    std::snprintf(b, sizeof b, "%.2f", qual);
-    ss << b;
+void VcfRecord::append_line(std::string& s) const {
+  char b[32];
+  s += chrom;
+  s += '\t';
+  s.append(b, std::to_chars(b, b + sizeof b, pos).ptr);
+  s += '\t';
+  s += id;
+  s += '\t';
+  s += ref;
+  s += '\t';
+  if (alts.empty()) s += '.';
+  for (size_t i = 0; i < alts.size(); ++i) {
+    if (i) s += ',';
+    s += alts[i];
   }
-  ss << '\t' << filter << '\t' << info;
+  s += '\t';
+  if (qual < 0) {
+    s += '.';
+  } else {
+    const int n = std::snprintf(b, sizeof b, "%.2f", qual);
+    s.append(b, (size_t)std::max(0, std::min<int>(n, (int)sizeof b - 1)));
+  }
+  s += '\t';
+  s += filter;
+  s += '\t';
+  s += info;
   if (!format.empty()) {
-    ss << '\t' << format;
-    for (const std::string& s : samples) ss << '\t' << s;
+    s += '\t';
+    s += format;
+    for (const std::string& x : samples) {
+      s += '\t';
+      s += x;
+    }
   }
-  ss << '\n';
-  return ss.str();
+  s += '\n';
+}
+
+std::string VcfRecord::to_line() const {
+  std::string s;
+  append_line(s);
+  return s;
 }
 
 std::string VcfHeader::to_text() const {
@@ -54,6 +77,7 @@ std::string VcfHeader::to_text() const {
 
 struct VcfWriter::Impl {
   std::ofstream out;
+  std::string buf;  // lines gathered here and written 1 MiB at a time
 };
 
 VcfWriter::VcfWriter(const std::string& path, const VcfHeader& h) : impl_(new Impl) {
@@ -63,14 +87,27 @@ VcfWriter::VcfWriter(const std::string& path, const VcfHeader& h) : impl_(new Im
 }
 
 VcfWriter::~VcfWriter() {
-  close();
+  try {
+    close();
+  } catch (...) {
+  }
   delete impl_;
 }
 
-void VcfWriter::write(const VcfRecord& r) { impl_->out << r.to_line(); }
+void VcfWriter::write(const VcfRecord& r) {
+  r.append_line(impl_->buf);
+  if (impl_->buf.size() >= (1u << 20)) {
+    impl_->out.write(impl_->buf.data(), (std::streamsize)impl_->buf.size());
+    impl_->buf.clear();
+  }
+}
 
 void VcfWriter::close() {
-  if (impl_->out.is_open()) impl_->out.close();
+  if (!impl_->out.is_open()) return;
+  impl_->out.write(impl_->buf.data(), (std::streamsize)impl_->buf.size());
+  impl_->buf.clear();
+  impl_->out.close();
+  if (impl_->out.fail()) throw internalError("[E::vcf] write failed");
 }
 
 void vcf_concat(const std::vector<std::string>& inputs, const std::string& output) {

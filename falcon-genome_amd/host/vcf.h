@@ -22,6 +22,7 @@ struct VcfRecord {
   std::string format;                // e.g. "GT:AD:DP:GQ:PL"
   std::vector<std::string> samples;  // one formatted column per sample
   std::string to_line() const;
+  void append_line(std::string& out) const;  // to_line() appended to out
 };
 
 struct VcfHeader {
