@@ -43,22 +43,6 @@ std::string revcomp(const std::string& s) {
   return o;
 }
 
-// Static split of [0, n) over up to `threads` std::threads.
-template <typename F>
-void parallel_for(size_t n, int threads, F&& fn) {
-  const size_t nt = std::max<size_t>(1, std::min<size_t>((size_t)std::max(threads, 1), n / 256 + 1));
-  if (nt == 1) {
-    for (size_t i = 0; i < n; ++i) fn(i);
-    return;
-  }
-  std::vector<std::thread> th;
-  for (size_t t = 0; t < nt; ++t)
-    th.emplace_back([&, t] {
-      for (size_t i = n * t / nt; i < n * (t + 1) / nt; ++i) fn(i);
-    });
-  for (auto& x : th) x.join();
-}
-
 // One candidate placement of a read: a chain's seed (a maximal exact match)
 // and, after the GPU extension round, its alignment.
 struct Cand {
@@ -223,6 +207,7 @@ void extend_cands(const KmerIndex& idx, const fcs_bsw_params& P, const AlignOpti
   so.w = opt.w;
   so.pen_clip5 = so.pen_clip3 = P.end_bonus;
   so.gpu = opt.gpu;
+  so.threads = opt.threads;
   std::vector<SeedAln> res;
   SeedExtStats xs;
   extend_seeds(jobs, P, so, res, xs);
@@ -472,6 +457,7 @@ BamRecord make_record(const Reference& ref, const ReadAln& R, const std::string&
 // Seeds, chains and the GPU extension round for a batch of reads.
 void align_batch(const Reference& ref, const KmerIndex& idx, const std::vector<std::string>& seqs,
                  const AlignOptions& opt, std::vector<ReadAln>& reads, AlignStats& st) {
+  const uint64_t t0 = now_us();
   reads.assign(seqs.size(), ReadAln{});
   parallel_for(seqs.size(), opt.threads, [&](size_t r) {
     ReadAln& R = reads[r];
@@ -481,10 +467,15 @@ void align_batch(const Reference& ref, const KmerIndex& idx, const std::vector<s
     R.code[1] = encode(R.seq[1]);
     seed_read(ref, idx, opt, R);
   });
+  const uint64_t t1 = now_us();
+  st.seed_seconds += (t1 - t0) / 1e6;
   std::vector<ReadAln*> ptr;
   for (ReadAln& R : reads) ptr.push_back(&R);
   extend_cands(idx, st.params, opt, ptr, false, st);
+  const uint64_t t2 = now_us();
+  st.extend_seconds += (t2 - t1) / 1e6;
   parallel_for(reads.size(), opt.threads, [&](size_t r) { pick_primary(reads[r], opt); });
+  st.pair_seconds += (now_us() - t2) / 1e6;
 }
 
 }  // namespace
@@ -509,8 +500,10 @@ AlignStats align_reads(const Reference& ref, const KmerIndex& idx, const std::ve
   st.reads = (int64_t)seqs.size();
   const size_t base = out.size();
   out.resize(base + reads.size());
+  const uint64_t tr = now_us();
   parallel_for(reads.size(), opt.threads,
                [&](size_t i) { out[base + i] = make_record(ref, reads[i], names[i], seqs[i], quals[i], opt); });
+  st.record_seconds += (now_us() - tr) / 1e6;
   for (const ReadAln& R : reads) st.mapped += R.best >= 0;
   st.seconds = (now_us() - t0) / 1e6;
   return st;
@@ -533,6 +526,7 @@ AlignStats align_pairs(const Reference& ref, const KmerIndex& idx, const std::ve
   std::vector<ReadAln> m1(std::make_move_iterator(all.begin()), std::make_move_iterator(all.begin() + n));
   std::vector<ReadAln> m2(std::make_move_iterator(all.begin() + n), std::make_move_iterator(all.end()));
   all.clear();
+  const uint64_t tp = now_us();
   const PeStat ps = pestat(m1, m2);
   st.pe_pairs = ps.n;
   st.pe_low = ps.low;
@@ -558,7 +552,10 @@ AlignStats align_pairs(const Reference& ref, const KmerIndex& idx, const std::ve
     std::sort(resc.begin(), resc.end());
     resc.erase(std::unique(resc.begin(), resc.end()), resc.end());
     st.rescued = (int64_t)resc.size();
+    const uint64_t te = now_us();
     extend_cands(idx, st.params, opt, resc, true, st);
+    st.extend_seconds += (now_us() - te) / 1e6;
+    st.pair_seconds -= (now_us() - te) / 1e6;
   }
   // pairing (bwa mem_pair): the best FR combination within [low, high] by
   // score + insert-size log-likelihood, against the unpaired best - pen_unpaired
@@ -594,6 +591,8 @@ AlignStats align_pairs(const Reference& ref, const KmerIndex& idx, const std::ve
       r.mapq = std::max(q_se, std::min(q_pe, q_se + 40));
     }
   }
+  const uint64_t tr = now_us();
+  st.pair_seconds += (tr - tp) / 1e6;
   const size_t base = out.size();
   out.resize(base + 2 * n);
   parallel_for(n, opt.threads, [&](size_t i) {
@@ -626,6 +625,7 @@ AlignStats align_pairs(const Reference& ref, const KmerIndex& idx, const std::ve
     out[base + 2 * i] = std::move(r1);
     out[base + 2 * i + 1] = std::move(r2);
   });
+  st.record_seconds += (now_us() - tr) / 1e6;
   for (size_t i = 0; i < n; ++i) st.mapped += (m1[i].best >= 0) + (m2[i].best >= 0);
   for (size_t i = 0; i < n; ++i) st.proper += 2 * proper[i];
   st.reads = 2 * (int64_t)n;
@@ -712,6 +712,10 @@ int align_main(int argc, char** argv) {
     tot.rescued += st.rescued;
     tot.seconds += st.seconds;
     tot.gpu_seconds += st.gpu_seconds;
+    tot.seed_seconds += st.seed_seconds;
+    tot.extend_seconds += st.extend_seconds;
+    tot.pair_seconds += st.pair_seconds;
+    tot.record_seconds += st.record_seconds;
     tot.ext_tasks += st.ext_tasks;
     tot.global_tasks += st.global_tasks;
     if (st.pe_pairs) tot.pe_pairs = st.pe_pairs, tot.pe_low = st.pe_low, tot.pe_high = st.pe_high,
@@ -831,7 +835,9 @@ int align_main(int argc, char** argv) {
   const uint64_t t_end = now_us();
   std::cerr << "[fcs-genome align] phases: reference " << (t_ref - t_start) / 1e6 << " s, FMD index "
             << (t_idx - t_ref) / 1e6 << " s, FASTQ + alignment " << (t_aln - t_idx) / 1e6 << " s (alignment "
-            << tot.seconds << " s), sort + BAM + index " << (t_end - t_aln) / 1e6 << " s" << std::endl;
+            << tot.seconds << " s: seeding " << tot.seed_seconds << " s, extension " << tot.extend_seconds
+            << " s, pairing " << tot.pair_seconds << " s, records " << tot.record_seconds << " s), sort + BAM + index "
+            << (t_end - t_aln) / 1e6 << " s" << std::endl;
   return 0;
 }
 

@@ -39,6 +39,9 @@ struct AlignStats {
   int64_t reads = 0, mapped = 0, ext_tasks = 0, ext_cells = 0, global_tasks = 0;
   int64_t proper = 0, rescued = 0;  // paired: reads flagged proper pair, mates rescued
   double seconds = 0, gpu_seconds = 0;
+  // wall seconds of the phases: seeding + chaining, extension (host protocol +
+  // GPU calls), pairing / primary choice, record building
+  double seed_seconds = 0, extend_seconds = 0, pair_seconds = 0, record_seconds = 0;
   // paired: the insert-size estimate of the (last) batch
   int pe_pairs = 0, pe_low = 0, pe_high = 0;
   double pe_avg = 0, pe_std = 0;

@@ -4,15 +4,34 @@
 // (get_contig_fname, :232-245) and timing.
 #pragma once
 
+#include <algorithm>
 #include <chrono>
 #include <cstdint>
 #include <iomanip>
 #include <sstream>
 #include <stdexcept>
 #include <string>
+#include <thread>
 #include <vector>
 
 namespace fcsg {
+
+// Static split of [0, n) over up to `threads` std::threads (one thread for
+// fewer than 256 items per extra thread).
+template <typename F>
+void parallel_for(size_t n, int threads, F&& fn) {
+  const size_t nt = std::max<size_t>(1, std::min<size_t>((size_t)std::max(threads, 1), n / 256 + 1));
+  if (nt == 1) {
+    for (size_t i = 0; i < n; ++i) fn(i);
+    return;
+  }
+  std::vector<std::thread> th;
+  for (size_t t = 0; t < nt; ++t)
+    th.emplace_back([&, t] {
+      for (size_t i = n * t / nt; i < n * (t + 1) / nt; ++i) fn(i);
+    });
+  for (auto& x : th) x.join();
+}
 
 // Exit codes of `fcs-genome` (reference main.cpp: helpRequest → 0 after help,
 // invalidParam/pathEmpty/fileNotFound → 1, failedCommand → 4, internal → 3).

@@ -123,33 +123,33 @@ FmdIndex::FmdIndex(const std::vector<std::vector<uint8_t>>& contigs) {
   for (uint8_t c : T) ++C_[c + 1];
   for (int c = 1; c < 7; ++c) C_[c] += C_[c - 1];
   const int64_t nb = (n_ + 63) / 64;
-  bits_.assign(4 * nb, 0);
-  cnt_.assign(4 * nb, 0);
+  occ_store_.assign(8 * (size_t)(nb + 1) + 8, 0);
+  uint64_t* occ = occ_store_.data();
+  while (reinterpret_cast<uintptr_t>(occ) & 63) ++occ;
+  occ_ = occ;
   uint64_t run[4] = {0, 0, 0, 0};
-  for (int64_t b = 0; b < nb; ++b) {
-    for (int c = 0; c < 4; ++c) cnt_[4 * b + c] = run[c];
+  for (int64_t b = 0; b <= nb; ++b) {
+    uint64_t* B = occ + 8 * b;
+    for (int c = 0; c < 4; ++c) B[c] = run[c];
     for (int64_t i = 64 * b; i < std::min(n_, 64 * b + 64); ++i) {
       const uint64_t p = sa_[i];
       const uint32_t ch = p ? T[p - 1] : 0;  // BWT symbol
       if (ch >= 1 && ch <= 4) {
-        bits_[4 * b + ch - 1] |= 1ull << (i & 63);
+        B[4 + ch - 1] |= 1ull << (i & 63);
         ++run[ch - 1];
       }
     }
   }
 }
 
-int64_t FmdIndex::occ(int c, int64_t i) const {
-  if (i <= 0) return 0;
-  const int64_t b = i >> 6;
-  const int r = (int)(i & 63);
-  int64_t v = b < (int64_t)(cnt_.size() / 4) ? cnt_[4 * b + c - 1] : cnt_[cnt_.size() - 4 + c - 1];
-  if (b < (int64_t)(bits_.size() / 4)) {
-    if (r) v += __builtin_popcountll(bits_[4 * b + c - 1] & ((1ull << r) - 1));
-  } else {  // i == n: the whole last block
-    v += __builtin_popcountll(bits_[bits_.size() - 4 + c - 1]);
+void FmdIndex::occ4(int64_t i, int64_t o[4]) const {
+  if (i <= 0) {
+    o[0] = o[1] = o[2] = o[3] = 0;
+    return;
   }
-  return v;
+  const uint64_t* B = occ_ + 8 * (i >> 6);  // i <= n: at most the totals block
+  const uint64_t m = (1ull << (i & 63)) - 1;
+  for (int c = 0; c < 4; ++c) o[c] = (int64_t)(B[c] + (uint64_t)__builtin_popcountll(B[4 + c] & m));
 }
 
 void FmdIndex::set_intv(int c, BiInterval& iv) const {
@@ -165,10 +165,12 @@ void FmdIndex::set_intv(int c, BiInterval& iv) const {
 // (the base before $ is a separator).
 void FmdIndex::extend(const BiInterval& ik, BiInterval ok[5], bool is_back) const {
   const int64_t base = is_back ? ik.k : ik.l;
+  int64_t tk[4], tl[4];
+  occ4(base, tk);
+  occ4(base + ik.s, tl);
   for (int c = 1; c <= 4; ++c) {
-    const int64_t tk = occ(c, base), tl = occ(c, base + ik.s);
-    (is_back ? ok[c].k : ok[c].l) = C_[c] + tk;
-    ok[c].s = tl - tk;
+    (is_back ? ok[c].k : ok[c].l) = C_[c] + tk[c - 1];
+    ok[c].s = tl[c - 1] - tk[c - 1];
   }
   int64_t o = is_back ? ik.l : ik.k;
   for (int c = 4; c >= 1; --c) {
@@ -181,7 +183,9 @@ int FmdIndex::smem1(const uint8_t* q, int len, int x, int64_t min_intv, std::vec
   mem.clear();
   if (q[x] > 3) return x + 1;
   if (min_intv < 1) min_intv = 1;
-  std::vector<BiInterval> a0, a1;
+  thread_local std::vector<BiInterval> a0, a1;  // reused: one smem1 call per query position
+  a0.clear();
+  a1.clear();
   std::vector<BiInterval>*prev = &a0, *curr = &a1;
   BiInterval ik, ok[5];
   set_intv(q[x] + 1, ik);

@@ -7,7 +7,7 @@
 // alphabet $ = 0, A = 1, C = 2, G = 3, T = 4, 5 = separator / N (a match never
 // runs through a 5, and revcomp(F) also starts and ends with 5).  The suffix
 // array comes from SA-IS; Occ from 64-position blocks of per-base bit vectors
-// plus block counts.  A bi-interval (k, l, s) holds the SA interval of P
+// plus block counts, interleaved so that one occurrence query reads one cache line.  A bi-interval (k, l, s) holds the SA interval of P
 // (k, s) and of revcomp(P) (l, s), so P extends in both directions (bwa's
 // bwt_extend); bwt_smem1 finds, for a query position x, the SMEMs overlapping
 // x, and mem_collect_intv's three rounds (all SMEMs of length >= min_len,
@@ -32,6 +32,8 @@ class FmdIndex {
  public:
   // contigs as codes 0..4 (A, C, G, T, other)
   explicit FmdIndex(const std::vector<std::vector<uint8_t>>& contigs);
+  FmdIndex(const FmdIndex&) = delete;
+  FmdIndex& operator=(const FmdIndex&) = delete;
   int64_t size() const { return n_; }
   // bwt_smem1: SMEMs of q (codes 0..4) overlapping position x with at least
   // min_intv occurrences; returns the next start position (bwa's return value).
@@ -50,13 +52,15 @@ class FmdIndex {
 
  private:
   void extend(const BiInterval& ik, BiInterval ok[5], bool is_back) const;
-  int64_t occ(int c, int64_t i) const;  // occurrences of c in BWT[0, i)
+  void occ4(int64_t i, int64_t o[4]) const;  // occurrences of A, C, G, T in BWT[0, i)
   void set_intv(int c, BiInterval& iv) const;
   int64_t n_ = 0, flen_ = 0;
   std::vector<int64_t> C_;               // C_[c] = symbols < c
   std::vector<uint64_t> sa_;             // suffix array
-  std::vector<uint64_t> bits_;           // per 64-block: bit vectors of A, C, G, T
-  std::vector<uint64_t> cnt_;            // per 64-block: counts of A, C, G, T before the block
+  // per 64-position block, one 64-byte line: the counts of A, C, G, T before
+  // the block, then their bit vectors in it; one extra block holds the totals
+  std::vector<uint64_t> occ_store_;
+  const uint64_t* occ_ = nullptr;        // occ_store_ aligned to 64 bytes
   std::vector<int64_t> cstart_;          // forward-text start of each contig
   std::vector<int64_t> clen_;
 };

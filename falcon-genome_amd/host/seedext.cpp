@@ -107,6 +107,9 @@ void extend_seeds(const std::vector<SeedJob>& jobs, const fcs_bsw_params& p_in, 
     if (J.seed_len <= 0 || J.seed_q < 0 || J.seed_q + J.seed_len > J.qlen || J.seed_r < 0 ||
         J.seed_r + J.seed_len > J.rlen)
       throw invalidParam("extend_seeds: seed outside its query or contig");
+  }
+  parallel_for(n, opt.threads, [&](size_t i) {
+    const SeedJob& J = jobs[i];
     const int rest = J.qlen - J.seed_q - J.seed_len;
     rmax0[i] = std::max<int64_t>(0, J.seed_r - (J.seed_q + bwa_cal_max_gap(p_in, J.seed_q, opt.w)));
     rmax1[i] = std::min<int64_t>(J.rlen, J.seed_r + J.seed_len + rest + bwa_cal_max_gap(p_in, rest, opt.w));
@@ -125,7 +128,7 @@ void extend_seeds(const std::vector<SeedJob>& jobs, const fcs_bsw_params& p_in, 
       A.qb = 0;
       A.rb = J.seed_r;
     }
-  }
+  });
   std::vector<fcs_bsw_result> lres, rres;
   extend_side(left, prev, pl, opt.w, opt.gpu, lres, st);
   for (size_t i = 0; i < n; ++i) {
@@ -146,7 +149,7 @@ void extend_seeds(const std::vector<SeedJob>& jobs, const fcs_bsw_params& p_in, 
     }
   }
   std::vector<int> sc0(n, 0);
-  for (size_t i = 0; i < n; ++i) {
+  parallel_for(n, opt.threads, [&](size_t i) {
     const SeedJob& J = jobs[i];
     SeedAln& A = out[i];
     const int qe = J.seed_q + J.seed_len;
@@ -163,7 +166,7 @@ void extend_seeds(const std::vector<SeedJob>& jobs, const fcs_bsw_params& p_in, 
       A.qe = J.qlen;
       A.re = J.seed_r + J.seed_len;
     }
-  }
+  });
   extend_side(right, prev, pr, opt.w, opt.gpu, rres, st);
   for (size_t i = 0; i < n; ++i) {
     if (!right[i].run) continue;
@@ -236,11 +239,11 @@ void extend_seeds(const std::vector<SeedJob>& jobs, const fcs_bsw_params& p_in, 
         throw failedCommand(std::string(fcs_last_error()));
       st.gpu_seconds += (now_us() - g0) / 1e6;
       st.global_tasks += (int64_t)tasks.size();
-      for (size_t k = 0; k < dp.size(); ++k) {
+      parallel_for(dp.size(), opt.threads, [&](size_t k) {
         SeedAln& A = out[dp[k]];
         A.cigar.assign(arena.begin() + off[k], arena.begin() + off[k] + ncig[k]);
         A.gscore = scores[k];
-      }
+      });
     }
     std::vector<int> again;
     for (int i : todo) {

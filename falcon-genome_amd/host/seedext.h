@@ -53,6 +53,7 @@ struct SeedExtOptions {
   int pen_clip3 = 5;
   int gpu = 0;
   bool want_cigar = true;
+  int threads = 1;  // host threads for the per-job protocol work around the GPU calls
 };
 
 struct SeedExtStats {
