@@ -4,6 +4,7 @@
 #include <climits>
 #include <cmath>
 #include <cstdlib>
+#include <memory>
 #include <string>
 
 #include "common.h"
@@ -232,16 +233,17 @@ void extend_seeds(const std::vector<SeedJob>& jobs, const fcs_bsw_params& p_in, 
     }
     if (!tasks.empty()) {
       std::vector<int32_t> scores(tasks.size()), ncig(tasks.size());
-      std::vector<uint32_t> arena((size_t)std::max<int64_t>(tot, 1));
+      // capacity l + rlen + 1 ops per task, mostly unused: not zero-filled
+      std::unique_ptr<uint32_t[]> arena(new uint32_t[(size_t)std::max<int64_t>(tot, 1)]);
       const uint64_t g0 = now_us();
-      if (fcs_bsw_global(tasks.data(), (int32_t)tasks.size(), &p_in, scores.data(), arena.data(), off.data(),
+      if (fcs_bsw_global(tasks.data(), (int32_t)tasks.size(), &p_in, scores.data(), arena.get(), off.data(),
                          cap.data(), ncig.data(), opt.gpu) != FCS_OK)
         throw failedCommand(std::string(fcs_last_error()));
       st.gpu_seconds += (now_us() - g0) / 1e6;
       st.global_tasks += (int64_t)tasks.size();
       parallel_for(dp.size(), opt.threads, [&](size_t k) {
         SeedAln& A = out[dp[k]];
-        A.cigar.assign(arena.begin() + off[k], arena.begin() + off[k] + ncig[k]);
+        A.cigar.assign(arena.get() + off[k], arena.get() + off[k] + ncig[k]);
         A.gscore = scores[k];
       });
     }

@@ -186,15 +186,16 @@ class TabixBuilder {
       if (!t[k]) throw formatError(label_ + ": malformed VCF line");
       p = t[k] + 1;
     }
-    const std::string chrom(line, t[0]);
     char* pe = nullptr;
     const int64_t pos = std::strtoll(t[0] + 1, &pe, 10);
     if (pe != t[1]) throw formatError(label_ + ": malformed VCF POS");
     const int64_t rlen = (int64_t)(t[3] - t[2] - 1);
+    const size_t clen = (size_t)(t[0] - line);
     int tid;
-    if (!names_.empty() && chrom == names_.back()) {
+    if (!names_.empty() && names_.back().size() == clen && std::memcmp(names_.back().data(), line, clen) == 0) {
       tid = (int)names_.size() - 1;
     } else {
+      const std::string chrom(line, clen);
       if (name_id_.count(chrom)) throw formatError(label_ + ": chromosome blocks not contiguous (unsorted VCF)");
       tid = (int)names_.size();
       name_id_[chrom] = tid;
@@ -206,7 +207,13 @@ class TabixBuilder {
     last_pos_ = pos;
     const int64_t beg = pos - 1, end = beg + std::max<int64_t>(rlen, 1);
     RefIndex& ri = idx_[tid];
-    auto& chunks = ri.bins[reg2bin(beg, end)];
+    const uint32_t bin = (uint32_t)reg2bin(beg, end);
+    if (tid != cache_tid_ || bin != cache_bin_) {  // records mostly repeat the previous bin
+      cache_tid_ = tid;
+      cache_bin_ = bin;
+      cache_chunks_ = &ri.bins[bin];
+    }
+    auto& chunks = *cache_chunks_;
     if (!chunks.empty() && chunks.back().second == beg_off) chunks.back().second = end_off;  // extend the run
     else chunks.emplace_back(beg_off, end_off);
     const int64_t w0 = beg >> 14, w1 = (end - 1) >> 14;
@@ -259,6 +266,9 @@ class TabixBuilder {
   std::vector<RefIndex> idx_;
   int last_tid_ = -1;
   int64_t last_pos_ = -1;
+  int cache_tid_ = -1;
+  uint32_t cache_bin_ = 0;
+  std::vector<std::pair<uint64_t, uint64_t>>* cache_chunks_ = nullptr;  // map values do not move
 };
 
 }  // namespace
