@@ -35,7 +35,12 @@ int main() {
   (void)hipSetDevice(0);
   (void)hipFree(nullptr);
   const double t2 = now_ms();
-  int rc = one_call(1);
+  fcs_phmm_plan* plan = nullptr;
+  int rc = fcs_phmm_plan_create(0, 16, &plan);
+  const double t2b = now_ms();
+  rc |= fcs_phmm_plan_destroy(plan);
+  const double t2c = now_ms();
+  rc |= one_call(1);
   const double t3 = now_ms();
   rc |= one_call(1);
   const double t4 = now_ms();
@@ -78,6 +83,7 @@ int main() {
   tp.join();
   std::printf("{\"four_streams_ms\": %.2f, \"seven_events_ms\": %.2f, \"host_malloc_16MB_ms\": %.2f, "
               "\"malloc_16MB_ms\": %.2f}\n", st_ms, ev_ms, hm_ms, dm_ms);
+  std::printf("{\"plan_create_ms\": %.1f, \"plan_destroy_ms\": %.1f}\n", t2b - t2, t2c - t2b);
   std::printf("{\"devices\": %d, \"hip_init_ms\": %.1f, \"context_ms\": %.1f, \"first_call_ms\": %.1f, "
               "\"second_call_ms\": %.2f, \"new_thread_first_call_ms\": %.1f, \"thread_total_ms\": %.1f, "
               "\"sixteen_new_threads_ms\": %.1f, \"rc\": %d}\n",
