@@ -593,6 +593,9 @@ CallerStats call_intervals(const Reference& ref, const std::vector<std::string>&
       if (grow_r) ext_r *= 2;
     }
     st.reads += (int64_t)(reads[0].size() + reads[1].size());
+    int64_t max_span[2] = {0, 0};
+    for (int s = 0; s < 2; ++s)
+      for (const Read& rd : reads[s]) max_span[s] = std::max<int64_t>(max_span[s], rd.end - rd.pos);
     const uint64_t tr = now_us();
     const double in_flush0 = st.phmm_seconds + st.genotype_seconds;
     for (const auto& [first, last] : clusters) {
@@ -621,9 +624,14 @@ CallerStats call_intervals(const Reference& ref, const std::vector<std::string>&
         build_haplotypes(seq, *g);
         // reads clipped to the window, GATK-prepared, deterministic downsampling
         for (int s = 0; s < (opt.somatic ? 2 : 1); ++s) {
+          // reads are in position order: start at the first that can reach beg
+          // (pos >= beg - the window's longest reference span), stop at end
           std::vector<const Read*> ov;
-          for (const Read& rd : reads[s])
-            if (rd.pos < g->end && rd.end > g->beg) ov.push_back(&rd);
+          const std::vector<Read>& rs = reads[s];
+          auto it = std::lower_bound(rs.begin(), rs.end(), g->beg - max_span[s],
+                                     [](const Read& rd, int64_t x) { return rd.pos < x; });
+          for (; it != rs.end() && it->pos < g->end; ++it)
+            if (it->end > g->beg) ov.push_back(&*it);
           const size_t cap = (size_t)opt.max_reads_per_region;
           const double stride = ov.size() > cap ? (double)ov.size() / cap : 1.0;
           for (double x = 0; (size_t)x < ov.size() && g->reads[s].size() < cap; x += stride) {
