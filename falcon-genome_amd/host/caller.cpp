@@ -96,7 +96,10 @@ struct Allele {
 struct Pileup {
   int64_t wb = 0;
   std::vector<int> depth, events;
-  std::map<Allele, int> support;
+  // allele events of the reads, then (finish_support) sorted and counted:
+  // the support of each distinct allele in (pos, ref, alt) order
+  std::vector<Allele> events_list;
+  std::vector<std::pair<Allele, int>> support;
   // GVCF reference model: per position, sum over bases of log10 P(base | 0/0,
   // 0/1, 1/1) with 1 = <NON_REF> (any other base)
   std::vector<double> gl;  // 3 per position; empty unless GVCF
@@ -139,7 +142,7 @@ void build_pileup(const std::string& ref, const std::vector<Read>& reads, int mi
             const bool nonref = b != ref[rp] && ref[rp] != 'N' && b != 'N';
             if (nonref) {
               ++pu.events[rp - pu.wb];
-              ++pu.support[{rp, std::string(1, ref[rp]), std::string(1, b)}];
+              pu.events_list.push_back({rp, std::string(1, ref[rp]), std::string(1, b)});
             }
             if (!pu.gl.empty()) {
               const double* t = ref_model().t[std::min<int>(rd.qual[q], 93)];
@@ -153,14 +156,14 @@ void build_pileup(const std::string& ref, const std::vector<Read>& reads, int mi
         case kI:
           if (rp > rd.pos && in(rp - 1)) {
             ++pu.events[rp - 1 - pu.wb];
-            ++pu.support[{rp - 1, std::string(1, ref[rp - 1]), ref[rp - 1] + rd.seq.substr(q, len)}];
+            pu.events_list.push_back({rp - 1, std::string(1, ref[rp - 1]), ref[rp - 1] + rd.seq.substr(q, len)});
           }
           q += len;
           break;
         case kD:
           if (rp > rd.pos && in(rp - 1) && rp + len <= (int64_t)ref.size()) {
             ++pu.events[rp - 1 - pu.wb];
-            ++pu.support[{rp - 1, ref.substr(rp - 1, len + 1), std::string(1, ref[rp - 1])}];
+            pu.events_list.push_back({rp - 1, ref.substr(rp - 1, len + 1), std::string(1, ref[rp - 1])});
           }
           for (uint32_t k = 0; k < len; ++k, ++rp)
             if (in(rp)) ++pu.depth[rp - pu.wb];
@@ -171,6 +174,18 @@ void build_pileup(const std::string& ref, const std::vector<Read>& reads, int mi
       }
     }
   }
+}
+
+// The distinct alleles of pu.events_list with their read counts, in order.
+void finish_support(Pileup& pu) {
+  std::sort(pu.events_list.begin(), pu.events_list.end());
+  pu.support.clear();
+  for (Allele& a : pu.events_list) {
+    if (!pu.support.empty() && !(pu.support.back().first < a)) ++pu.support.back().second;
+    else pu.support.emplace_back(std::move(a), 1);
+  }
+  pu.events_list.clear();
+  pu.events_list.shrink_to_fit();
 }
 
 // Query slice [qs, qe) of the read whose bases align inside [rb, re) (inserted
@@ -570,6 +585,7 @@ CallerStats call_intervals(const Reference& ref, const std::vector<std::string>&
       if (opt.gvcf && !opt.somatic) pu.gl.assign(3 * (we - wb), 0.0);
       build_pileup(seq, reads[0], opt.min_base_quality, pu);
       if (opt.somatic) build_pileup(seq, reads[1], opt.min_base_quality, pu);
+      finish_support(pu);
       std::vector<int64_t> sites;
       for (int64_t p = wb; p < we; ++p) {
         const int ev = pu.events[p - wb], dp = std::max(1, pu.depth[p - wb]);
@@ -606,7 +622,10 @@ CallerStats call_intervals(const Reference& ref, const std::vector<std::string>&
         g->end = std::min<int64_t>({L, last + opt.padding + 1, rb + opt.max_region});
         // candidates: supported by >= 2 reads and a fraction of the depth
         std::vector<std::pair<int, Allele>> cs;
-        for (auto it = pu.support.lower_bound({g->beg, "", ""}); it != pu.support.end() && it->first.pos < g->end; ++it) {
+        const Allele key{g->beg, "", ""};
+        for (auto it = std::lower_bound(pu.support.begin(), pu.support.end(), key,
+                                        [](const std::pair<Allele, int>& e, const Allele& k) { return e.first < k; });
+             it != pu.support.end() && it->first.pos < g->end; ++it) {
           const int dp = std::max(1, pu.depth[it->first.pos - wb]);
           if (it->first.ref_end() > g->end) continue;
           if (it->second >= 2 && it->second >= (opt.somatic ? 0.05 : 0.1) * dp) cs.emplace_back(it->second, it->first);
