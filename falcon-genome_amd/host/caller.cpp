@@ -1,6 +1,7 @@
 #include "caller.h"
 
 #include <algorithm>
+#include <array>
 #include <cmath>
 #include <cstdio>
 #include <map>
@@ -477,7 +478,10 @@ void emit_gvcf(const std::string& seq, const Pileup& pu, int64_t beg, int64_t en
                  std::to_string(blk.mindp) + ":" + std::to_string(blk.pl[0]) + "," + std::to_string(blk.pl[1]) + "," +
                  std::to_string(blk.pl[2])};
     out.push_back(std::move(r));
+    std::vector<int> keep = std::move(blk.dps);  // reuse the buffer
+    keep.clear();
     blk = Block();
+    blk.dps = std::move(keep);
   };
   size_t ci = 0;
   int64_t covered = beg;  // positions below are inside an emitted call's REF span
@@ -520,7 +524,14 @@ int gvcf_band(int gq) {
   static const int bounds[] = {1,  2,  3,  4,  5,  6,  7,  8,  9,  10, 11, 12, 13, 14, 15, 16, 17, 18, 19, 20, 21, 22,
                                23, 24, 25, 26, 27, 28, 29, 30, 31, 32, 33, 34, 35, 36, 37, 38, 39, 40, 41, 42, 43, 44,
                                45, 46, 47, 48, 49, 50, 51, 52, 53, 54, 55, 56, 57, 58, 59, 60, 70, 80, 90, 99};
-  return (int)(std::upper_bound(std::begin(bounds), std::end(bounds), gq) - std::begin(bounds));
+  auto band = [&](int g) { return (int)(std::upper_bound(std::begin(bounds), std::end(bounds), g) - std::begin(bounds)); };
+  // GQ is 0 .. 99 in emit_gvcf: a table; anything else by search
+  static const auto lut = [&] {
+    std::array<int, 100> t{};
+    for (int g = 0; g < 100; ++g) t[g] = band(g);
+    return t;
+  }();
+  return gq >= 0 && gq < 100 ? lut[gq] : band(gq);
 }
 
 CallerStats call_intervals(const Reference& ref, const std::vector<std::string>& bams,
@@ -687,11 +698,19 @@ CallerStats call_intervals(const Reference& ref, const std::vector<std::string>&
   const uint64_t tw = now_us();
   st.calls = (int64_t)calls.size();
   std::vector<VcfRecord>& recs = (opt.gvcf && !opt.somatic) ? gout : calls;
-  std::stable_sort(recs.begin(), recs.end(), [&](const VcfRecord& a, const VcfRecord& b) {
-    const int ia = ref.index(a.chrom), ib = ref.index(b.chrom);
-    return ia != ib ? ia < ib : a.pos < b.pos;
-  });
-  for (const VcfRecord& r : recs) out.write(r);
+  // (contig index, position) order, ties in emission order: keys computed once
+  // per record (the contig lookup is a name scan), then one key sort
+  std::vector<std::pair<std::pair<int, int64_t>, uint32_t>> order(recs.size());
+  {
+    const std::string* last = nullptr;
+    int last_i = -1;
+    for (size_t i = 0; i < recs.size(); ++i) {
+      if (!last || recs[i].chrom != *last) last = &recs[i].chrom, last_i = ref.index(recs[i].chrom);
+      order[i] = {{last_i, recs[i].pos}, (uint32_t)i};
+    }
+  }
+  std::sort(order.begin(), order.end());
+  for (const auto& o : order) out.write(recs[o.second]);
   st.output_seconds += (now_us() - tw) / 1e6;
   st.seconds = (now_us() - t0) / 1e6;
   return st;
