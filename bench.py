@@ -249,6 +249,12 @@ def bench_e2e(args, rank, local):
             return dt, logs, r.stderr
         d = work + "/d"
 
+        def best(name, cmd):
+            """Best of --e2e-reps runs (the first run of a fresh box also pays page-in
+            and clock ramp; every run's wall time is reported)."""
+            runs = [timed(name, cmd) for _ in range(max(1, args.e2e_reps))]
+            return min(runs, key=lambda r: r[0]), [round(r[0], 3) for r in runs]
+
         def stage_s(err, name):
             m = re.search(name + r" finishes in ([\d.]+) seconds", err)
             return float(m.group(1)) if m else None
@@ -272,21 +278,23 @@ def bench_e2e(args, rank, local):
             st["gpu_busy_frac"] = round(dev / dt, 4)  # PairHMM device time (HIP events) / wall time, one GPU
             st["effective_gcups"] = round(st["cells"] / dt / 1e9, 2)
             return st
-        dt, logs, err = timed("htc", ["htc", "-r", d + "/ref.fasta", "-i", d + "/sample.bam", "-o",
-                                      work + "/htc.g.vcf"])
+        (dt, logs, err), runs = best("htc", ["htc", "-f", "-r", d + "/ref.fasta", "-i", d + "/sample.bam", "-o",
+                                             work + "/htc.g.vcf"])
         out["htc"] = shard_stats(logs, dt)
+        out["htc"]["runs_seconds"] = runs
         out["htc"]["output"] = "GVCF (the reference's default)"
         hs = stage_s(err, "Haplotype Caller")
         out["htc"]["caller_stage_seconds"] = hs  # the 32-shard stage alone: no process start, GPU init, concat
         out["htc"]["caller_stage_regions_per_s"] = round(out["htc"]["regions"] / hs, 1) if hs else None
-        dt, logs, err = timed("mutect2", ["mutect2", "-r", d + "/ref.fasta", "-t", d + "/tumor.bam", "-n",
-                                          d + "/sample.bam", "-o", work + "/m2.vcf"])
+        (dt, logs, err), runs = best("mutect2", ["mutect2", "-f", "-r", d + "/ref.fasta", "-t", d + "/tumor.bam", "-n",
+                                                 d + "/sample.bam", "-o", work + "/m2.vcf"])
         out["mutect2"] = shard_stats(logs, dt)
+        out["mutect2"]["runs_seconds"] = runs
         ms = stage_s(err, "Mutect2")
         out["mutect2"]["caller_stage_seconds"] = ms
         out["mutect2"]["caller_stage_regions_per_s"] = round(out["mutect2"]["regions"] / ms, 1) if ms else None
-        dt, _, err = timed("align", ["align", "-r", d + "/ref.fasta", "-1", d + "/sample_1.fastq", "-2",
-                                     d + "/sample_2.fastq", "-o", work + "/aln.bam"])
+        (dt, _, err), runs = best("align", ["align", "-f", "-r", d + "/ref.fasta", "-1", d + "/sample_1.fastq", "-2",
+                                            d + "/sample_2.fastq", "-o", work + "/aln.bam"])
         m = re.search(r"(\d+) reads, (\d+) mapped, (\d+) extension tasks, (\d+) global alignments, ([\d.]+) s "
                       r"\(GPU calls ([\d.]+) s\)", err)
         pm = re.search(r"(\d+) reads properly paired, (\d+) mates rescued, insert ([\d.]+) \+- ([\d.]+)", err)
@@ -297,7 +305,7 @@ def bench_e2e(args, rank, local):
                         "gpu_call_seconds": float(m.group(6)) if m else None,
                         "proper_pair_reads": int(pm.group(1)) if pm else None,
                         "mates_rescued": int(pm.group(2)) if pm else None,
-                        "seconds": round(dt, 3), "reads_per_s": round(n / dt, 1)}
+                        "seconds": round(dt, 3), "runs_seconds": runs, "reads_per_s": round(n / dt, 1)}
         return out
     finally:
         shutil.rmtree(work, ignore_errors=True)
@@ -410,6 +418,7 @@ def main():
     ap.add_argument("--cpu-budget", type=float, default=12.0)
     ap.add_argument("--no-e2e", action="store_true")
     ap.add_argument("--e2e-mbp", type=float, default=4.0)
+    ap.add_argument("--e2e-reps", type=int, default=2, help="runs of each e2e command; the fastest is reported")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))

@@ -201,8 +201,13 @@ constexpr int kBswKeyBits = 24;
 // 0 .. kStreamClasses-1 run the row-streamed fp32 kernel (phmm_stream.h), the
 // next kPhmmClasses the grouped kernels (phmm2.h / phmm_kernel), each range
 // longest first.
-constexpr int kPhmmKeyClassShift = 20;
-constexpr int kPhmmKeyBits = 24;
+// PairHMM sort keys: 16 bits (two 8-bit radix passes; the in-class order keys
+// hap length only) or 24 (three passes; stream classes also order by read length).
+#ifndef FCS_PHMM_KEY16
+#define FCS_PHMM_KEY16 1
+#endif
+constexpr int kPhmmKeyClassShift = FCS_PHMM_KEY16 ? 12 : 20;
+constexpr int kPhmmKeyBits = FCS_PHMM_KEY16 ? 16 : 24;
 constexpr int kStreamClasses = 4;
 constexpr int kPhmmClasses = 6;
 constexpr int kPhmmLaunchClasses = kStreamClasses + kPhmmClasses;

@@ -27,6 +27,10 @@
 // t - 15 from the second block on (the first block's columns are negative).
 #pragma once
 
+#ifndef FCS_STREAM_DPPSEL
+#define FCS_STREAM_DPPSEL 0  // 1: row a's DPP inputs by v_cndmask_b32_dpp (A/B: slower)
+#endif
+
 // 3 waves per SIMD (<= 168 VGPRs; LDS allows ~3.5 at H ~ 225): capped at 128
 // VGPRs for 4 the kernel spills 33 VGPRs to scratch.
 #ifndef PHMM2_LB
@@ -104,10 +108,24 @@ __device__ __forceinline__ void phmm2_step(Lane2& L, PhRing<float> (&pf)[PFD], i
   // (lane 0: the ring), row b's half is this lane's own row a, already there;
   // the packed ops read them with op_sel swapped (no register moves).
   pf2 Xsw = L.Xn, Isw = L.In;
+#if FCS_STREAM_DPPSEL
+  // one VOP2-DPP select per value (see pstream_step in phmm_stream.h)
+  {
+    const unsigned long long smask = __ballot(lane0);
+    asm("s_mov_b64 vcc, %2\n\t"
+        "s_nop 0\n\t"
+        "v_cndmask_b32_dpp %0, %0, %3, vcc row_shr:1 row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
+        "v_cndmask_b32_dpp %1, %1, %4, vcc row_shr:1 row_mask:0xf bank_mask:0xf bound_ctrl:1"
+        : "+v"(Xsw.y), "+v"(Isw.y)
+        : "s"(smask), "v"(cur.X), "v"(cur.I)
+        : "vcc");
+  }
+#else
   Xsw.y = __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(L.Xn.y), kDppRowShr1, 0xF, 0xF, true));
   Isw.y = __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(L.In.y), kDppRowShr1, 0xF, 0xF, true));
   Xsw.y = lane0 ? cur.X : Xsw.y;
   Isw.y = lane0 ? cur.I : Isw.y;
+#endif
   const pf2 I = __builtin_shufflevector(Isw, Isw, 1, 0);
   pf2 prior;
   if constexpr (BC) {

@@ -418,13 +418,13 @@ __host__ __device__ inline int phmm_class(int H) {
   return c < 0 ? 0 : c > kPhmmClasses - 1 ? kPhmmClasses - 1 : c;
 }
 
-// Sort keys (24 bits, three 8-bit radix passes): a 4-bit launch class, then the
+// Sort keys (16 bits, two 8-bit radix passes; 24 / three under FCS_PHMM_KEY16=0): a 4-bit launch class, then the
 // in-class order, as ascending keys — each class is a contiguous range and the
 // longest work comes first.  Classes 0 .. kStreamClasses-1 are the row-streamed
 // kernel's (R >= kStreamMinR, longest hap-length class first), the rest the
 // grouped kernels' hap-length classes (longest first).  In-class order:
-// streamed, hap length then read length descending; grouped, stripe count then
-// hap length descending.  The clamps only change the order, never results.
+// streamed, hap length (24-bit keys: then read length) descending; grouped, stripe
+// count then hap length descending.  The clamps only change the order, never results.
 __host__ __device__ inline int phmm_launch_class(int R, int H, int& stream_cls) {
   stream_cls = (R >= kStreamMinR && H >= 1) ? stream_class(H) : -1;
   if (stream_cls >= 0) return kStreamClasses - 1 - stream_cls;
@@ -440,10 +440,19 @@ __global__ void phmm_keys_kernel(const PhmmDevBatch b, uint32_t* __restrict__ ke
   const uint32_t cf = (uint32_t)phmm_launch_class(R, H, sc);
   const uint32_t hh = 0xFFFu - (uint32_t)min(max(H, 0), 0xFFF);
   uint32_t low;
+#if FCS_PHMM_KEY16
+  // streamed: hap length (H <= 3700 fits 12 bits); grouped: stripe count (R < 33:
+  // at most 3), then hap length in steps of 4
+  if (sc >= 0)
+    low = hh;
+  else
+    low = ((3u - (uint32_t)min((max(R, 0) + 15) >> 4, 3)) << 10) | (0x3FFu - (uint32_t)min(max(H, 0) >> 2, 0x3FF));
+#else
   if (sc >= 0)
     low = (hh << 8) | (0xFFu - (uint32_t)min(R >> 4, 0xFF));
   else
     low = ((0xFFu - (uint32_t)min((max(R, 0) + 15) >> 4, 0xFF)) << 12) | hh;
+#endif
   keys[p] = (cf << kPhmmKeyClassShift) | low;
   idx[p] = (int32_t)p;
 }

@@ -157,10 +157,28 @@ __device__ __forceinline__ void pstream_step(Lane2& L, PhRing<float> (&pf)[PF], 
   const int hbb = L.hbp;
   L.hbp = hba;
   pf2 Xsw = L.Xn, Isw = L.In;
+#if FCS_STREAM_DPPSEL
+  // row a's inputs in one VOP2-DPP select each: start lanes take the boundary
+  // source, the others row b of the lane below (row_shr:1 on src0).  The
+  // compiler's form is a DPP move plus a VOP3 select per value (the start mask
+  // lives in an SGPR pair, not VCC).  s_mov + s_nop 0 give the two wait states
+  // a DPP read needs after a VALU write of its source.
+  {
+    const unsigned long long smask = __ballot(start);
+    asm("s_mov_b64 vcc, %2\n\t"
+        "s_nop 0\n\t"
+        "v_cndmask_b32_dpp %0, %0, %3, vcc row_shr:1 row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
+        "v_cndmask_b32_dpp %1, %1, %4, vcc row_shr:1 row_mask:0xf bank_mask:0xf bound_ctrl:1"
+        : "+v"(Xsw.y), "+v"(Isw.y)
+        : "s"(smask), "v"(cur.X), "v"(cur.I)
+        : "vcc");
+  }
+#else
   Xsw.y = __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(L.Xn.y), kDppRowShr1, 0xF, 0xF, true));
   Isw.y = __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(L.In.y), kDppRowShr1, 0xF, 0xF, true));
   Xsw.y = start ? cur.X : Xsw.y;
   Isw.y = start ? cur.I : Isw.y;
+#endif
   const pf2 I = __builtin_shufflevector(Isw, Isw, 1, 0);
   pf2 prior;
   prior.x = prior_code(p.ma, hba, p.e1.x, p.e3.x);
