@@ -600,11 +600,27 @@ int launch_phmm_forward(const PhmmDevBatch& b, const int32_t* order, int64_t cou
                  : w == 2 ? launch(phmm3_kernel<2>) : launch(phmm3_kernel<1>);
     if (rc != FCS_OK) return rc;
   }
+  // Grouped classes (reads shorter than kStreamMinR; empty in most batches):
+  // kept off fs[0], which carries the longest-haplotype stream class, so an
+  // empty grouped launch does not extend the pass after it; and launched with
+  // at most kGroupedGrid workgroups striding over the class (about 2.7 rounds of
+  // the chip's wave slots at 3 waves/SIMD), since the host does not know the
+  // class sizes and each of 64K empty workgroups still takes a dispatch, a wave
+  // slot and its LDS while it reads the bounds.
+#ifndef FCS_PHMM_GROUPED_GRID
+#define FCS_PHMM_GROUPED_GRID 8192
+#endif
+  constexpr long long kGroupedGrid = FCS_PHMM_GROUPED_GRID;
+  int gfork = 0;
   for (int j = kPhmmClasses - 1 - c_max; j < kPhmmClasses; ++j) {
     const int c = kPhmmClasses - 1 - j;
     const int lc = kStreamClasses + j;  // launch class of grouped class c
     const int ns = (c == kPhmmClasses - 1) ? ns_max : std::min(224 + 32 * c, ns_max);
-    hipStream_t st = fs[fork++ % kForkStreams];
+#if FCS_PHMM_GROUPED_GRID >= 65536
+    hipStream_t st = fs[fork++ % kForkStreams];  // A/B: the round-1 placement and grid
+#else
+    hipStream_t st = fs[1 + gfork++ % (kForkStreams - 1)];
+#endif
 #ifndef FCS_PHMM_ONEROW
     // the two-rows-per-lane kernel (phmm2.h) for the FMA-order pass when its
     // four rings fit (ring slots >= H + 65, hap bytes + 16)
@@ -614,7 +630,7 @@ int launch_phmm_forward(const PhmmDevBatch& b, const int32_t* order, int64_t cou
       if (lds2 > 64 * 1024)
         FCS_HIP_CHECK(
             hipFuncSetAttribute((const void*)phmm2_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds2));
-      const unsigned grid = (unsigned)std::min<long long>(std::max<long long>(groups, 1), 65536);
+      const unsigned grid = (unsigned)std::min<long long>(std::max<long long>(groups, 1), kGroupedGrid);
       hipLaunchKernelGGL(phmm2_kernel, dim3(grid), dim3(64), lds2, st, b, order, bounds, lc, ns2, t.tf, out,
                          rescue_list, rescue_count, thr, use_rescue ? 1 : 0);
       FCS_HIP_CHECK(hipGetLastError());
