@@ -332,8 +332,18 @@ int check_params(const fcs_bsw_params* p) {
 // a block sort + ~20 merge passes for n <= 2^20 (the C2 / C3 batch sizes:
 // 0.16 ms of 7 us launches); a merge-sort limit of 0 forces its onesweep path
 // (histogram + one pass per 8-bit digit) at every size.  Same order either way.
-using SortConfig = rocprim::radix_sort_config<rocprim::default_config, rocprim::default_config,
-                                              rocprim::default_config, 0>;
+// The onesweep kernels' default tile (1024 threads x ~16 items) gives a 1M-key
+// sort 62 workgroups on a 256-CU chip; 256 x 8 tiles give it ~490 but measured
+// slower (C2 2.86 vs 2.93 TCUPS, C3 1.95 vs 2.05, profiles/r2/abt_*).
+#ifndef FCS_SORT_SMALL_TILES
+#define FCS_SORT_SMALL_TILES 0  // 1 measured slower
+#endif
+#if FCS_SORT_SMALL_TILES
+using SortOnesweep = rocprim::radix_sort_onesweep_config<rocprim::kernel_config<256, 8>, rocprim::kernel_config<256, 8>, 8>;
+#else
+using SortOnesweep = rocprim::default_config;
+#endif
+using SortConfig = rocprim::radix_sort_config<rocprim::default_config, rocprim::default_config, SortOnesweep, 0>;
 hipError_t sort_pairs_u32(void* tmp, size_t& bytes, const uint32_t* kin, uint32_t* kout, const int32_t* vin,
                           int32_t* vout, int n, hipStream_t s, int end_bit) {
   return rocprim::radix_sort_pairs<SortConfig>(tmp, bytes, kin, kout, vin, vout, (size_t)n, 0, (unsigned)end_bit, s);
