@@ -618,6 +618,7 @@ int launch_phmm_forward(const PhmmDevBatch& b, const int32_t* order, int64_t cou
     const int ns = (c == kPhmmClasses - 1) ? ns_max : std::min(224 + 32 * c, ns_max);
 #if FCS_PHMM_GROUPED_GRID >= 65536
     hipStream_t st = fs[fork++ % kForkStreams];  // A/B: the round-1 placement and grid
+    (void)gfork;
 #else
     hipStream_t st = fs[1 + gfork++ % (kForkStreams - 1)];
 #endif
