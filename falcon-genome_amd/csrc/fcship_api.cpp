@@ -400,6 +400,7 @@ struct fcs_phmm_plan {
   unsigned long long* fb_count = nullptr;
   int64_t* bounds = nullptr;
   int64_t scheduled = -1;  // n_pairs of the last schedule
+  bool counters_zeroed = false;  // the last schedule's keys kernel zeroed rescue_count[0..1]
 };
 
 namespace fcs {
@@ -594,8 +595,9 @@ int fcs_phmm_dev_schedule(fcs_phmm_plan* plan, const fcs_phmm_batch* b, void* st
   FCS_HIP_CHECK(hipSetDevice(plan->device));
   hipStream_t s = (hipStream_t)stream;
   const PhmmDevBatch d = to_dev(b);
-  rc = launch_phmm_keys(d, plan->keys_in, plan->idx_in, s);
+  rc = launch_phmm_keys(d, plan->keys_in, plan->idx_in, plan->rescue_count, s);
   if (rc) return rc;
+  plan->counters_zeroed = b->n_pairs > 0;
   if (b->n_pairs > 0) {
     size_t tmp = plan->sort_tmp_bytes;
     FCS_HIP_CHECK(sort_pairs_u32(plan->sort_tmp, tmp, plan->keys_in, plan->keys_out, plan->idx_in, plan->idx_out,
@@ -620,7 +622,11 @@ int fcs_phmm_dev_forward(fcs_phmm_plan* plan, const fcs_phmm_batch* b, double* o
   rc = get_device_tables(plan->device, &t);
   if (rc) return rc;
   hipStream_t s = (hipStream_t)stream;
-  FCS_HIP_CHECK(hipMemsetAsync(plan->rescue_count, 0, 2 * sizeof(unsigned long long), s));  // rescue + fallback
+  // rescue + fallback counts: zeroed by the schedule's keys kernel for the first
+  // forward pass after it, by a memset for any further pass
+  if (!plan->counters_zeroed)
+    FCS_HIP_CHECK(hipMemsetAsync(plan->rescue_count, 0, 2 * sizeof(unsigned long long), s));
+  plan->counters_zeroed = false;
   return launch_phmm_forward(to_dev(b), plan->idx_out, b->n_pairs, std::max(b->max_hap_len, 1), plan->bounds, *t,
                              opts->exact_order != 0, out, plan->rescue_list, plan->rescue_count,
                              opts->rescue_threshold, opts->use_fp64_rescue != 0, plan->fb_list, plan->fb_count, s);

@@ -140,7 +140,9 @@ int fork_streams(hipStream_t s, hipStream_t (&fs)[kForkStreams]);
 int join_streams(hipStream_t s, const hipStream_t (&fs)[kForkStreams]);
 
 // ------------------------------------------------------------ kernel launchers
-int launch_phmm_keys(const PhmmDevBatch& b, uint32_t* keys, int32_t* idx, hipStream_t s);
+// Also zeroes counters[0..1] (the forward pass's rescue and fallback counts)
+// when it launches (n_pairs > 0), which saves the forward pass a memset.
+int launch_phmm_keys(const PhmmDevBatch& b, uint32_t* keys, int32_t* idx, unsigned long long* counters, hipStream_t s);
 // bounds: device int64[kPhmmLaunchClasses + 1] from launch_phmm_bounds over the sorted keys.
 int launch_phmm_bounds(const uint32_t* sorted_keys, int64_t n, int64_t* bounds, hipStream_t s);
 // fb_list / fb_count: pairs the streamed kernel hands back (haplotype bytes

@@ -431,8 +431,13 @@ __host__ __device__ inline int phmm_launch_class(int R, int H, int& stream_cls) 
   return kStreamClasses + kPhmmClasses - 1 - phmm_class(max(H, 0));
 }
 
-__global__ void phmm_keys_kernel(const PhmmDevBatch b, uint32_t* __restrict__ keys, int32_t* __restrict__ idx) {
+__global__ void phmm_keys_kernel(const PhmmDevBatch b, uint32_t* __restrict__ keys, int32_t* __restrict__ idx,
+                                 unsigned long long* __restrict__ counters) {
   const long long p = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (p == 0) {
+    counters[0] = 0ull;
+    counters[1] = 0ull;
+  }
   if (p >= b.n_pairs) return;
   const int R = b.read_len[b.pair_read[p]];
   const int H = b.hap_len[b.pair_hap[p]];
@@ -466,11 +471,12 @@ __global__ void phmm_bounds_kernel(const uint32_t* __restrict__ keys, long long 
   for (int j = prev + 1; j <= cur; ++j) bounds[j] = k;
 }
 
-int launch_phmm_keys(const PhmmDevBatch& b, uint32_t* keys, int32_t* idx, hipStream_t s) {
+int launch_phmm_keys(const PhmmDevBatch& b, uint32_t* keys, int32_t* idx, unsigned long long* counters,
+                     hipStream_t s) {
   if (b.n_pairs <= 0) return FCS_OK;
   const int bs = 256;
   const long long nb = (b.n_pairs + bs - 1) / bs;
-  hipLaunchKernelGGL(phmm_keys_kernel, dim3((unsigned)nb), dim3(bs), 0, s, b, keys, idx);
+  hipLaunchKernelGGL(phmm_keys_kernel, dim3((unsigned)nb), dim3(bs), 0, s, b, keys, idx, counters);
   FCS_HIP_CHECK(hipGetLastError());
   return FCS_OK;
 }

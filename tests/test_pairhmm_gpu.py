@@ -427,3 +427,40 @@ def test_grouped_class_grid_stride(gpu):
     assert p.n_pairs == 40_000
     out = fcship.phmm_compute_pairs(p)
     check_parity(p, out, False)
+
+
+def test_dev_path_forward_twice_after_one_schedule(gpu):
+    """Device-pointer path: the schedule's keys kernel zeroes the rescue and
+    fallback counts for the first forward pass; a second forward + rescue over
+    the same schedule must memset them itself (same outputs, same rescue count)."""
+    import torch
+    import bench
+
+    reads, haps = random_batch(3, 40, 4, 90, 150, 150, 300, n_frac=0.0, related=False)
+    reads = [(r[0], np.full(r[0].size, 40, np.uint8), np.full(r[0].size, 60, np.uint8),
+              np.full(r[0].size, 60, np.uint8), r[4]) for r in reads]
+    p = fcship.make_pairs(reads, haps)
+    dev = torch.device("cuda", 0)
+    b, keep = bench.phmm_dev_batch(p, dev)
+    out = torch.empty(p.n_pairs, dtype=torch.float64, device=dev)
+    plan = fcship.C.c_void_p()
+    fcship.check(fcship.lib.fcs_phmm_plan_create(0, p.n_pairs, fcship.C.byref(plan)))
+    try:
+        opts = fcship.phmm_opts(device=0)
+        sp = torch.cuda.current_stream(dev).cuda_stream
+        B, O = fcship.C.byref(b), fcship.C.byref(opts)
+        fcship.check(fcship.lib.fcs_phmm_dev_schedule(plan, B, sp))
+        results, counts = [], []
+        for _ in range(2):
+            fcship.check(fcship.lib.fcs_phmm_dev_forward(plan, B, out.data_ptr(), O, sp))
+            fcship.check(fcship.lib.fcs_phmm_dev_rescue(plan, B, out.data_ptr(), O, sp))
+            n = fcship.C.c_int64()
+            fcship.check(fcship.lib.fcs_phmm_plan_rescue_count(plan, sp, fcship.C.byref(n)))
+            counts.append(n.value)
+            results.append(out.cpu().numpy().copy())
+    finally:
+        fcship.lib.fcs_phmm_plan_destroy(plan)
+    del keep
+    assert counts[0] > 0 and counts[0] == counts[1]
+    np.testing.assert_array_equal(results[0], results[1])
+    check_parity(p, results[0], False)
