@@ -9,10 +9,14 @@ schedule (device radix sort into 4-pair wave groups) -> fp32 forward kernel ->
 fp64 rescue kernel.  `value` = total cells (sum of R*H) of all ranks * steps /
 max-over-ranks wall time, in GCUPS.
 
-Multi-GPU: one process per GPU (torch.distributed.run); every rank processes
-its own 1M-pair shard (weak scaling, static partition, no data-path
-collective — SURVEY.md §8e).  torch.distributed is used only for the barrier
-and the max-over-ranks timing reduction.
+Multi-GPU: one process per GPU.  Under torch.distributed.run (WORLD_SIZE set)
+this process is one rank; `--gpus N` without WORLD_SIZE starts the N rank
+processes itself (fresh children, before this parent touches the GPU) and
+relays rank 0's line.  Every rank processes its own 1M-pair shard (weak
+scaling, static partition, no data-path collective — SURVEY.md §8e);
+torch.distributed carries only the barrier and the max-over-ranks timing
+reduction.  `--dry-run` runs the same rank/launcher/reduction path on CPU
+(gloo) with a stand-in workload, for the CPU tests.
 
 Also reported (not the headline): banded-SW ksw_extend2 GCUPS on C3-shaped
 synthetic extension tasks (2x151 bp reads, bwa defaults) and on the fixed
@@ -31,7 +35,7 @@ import torch
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(ROOT, "falcon-genome_amd"))
-import fcship  # noqa: E402  (after torch: one HIP runtime per process)
+fcship = None  # the C-ABI binding, loaded by main() after the rank launcher (no HIP before the children start)
 
 METRIC = "PairHMM GCUPS + banded-SW GCUPS per GPU; end-to-end htc regions/sec at 8 GPUs"
 FLOPS_PER_CELL = 11          # M 5 + I 3 + D 3 (FMA = 2)
@@ -82,8 +86,8 @@ def load_traffic(name):
         return None
 
 
-def bench_phmm(args, dev, rank, world):
-    p = fcship.synth_phmm(args.seed + 7919 * rank, args.pairs, R=101, hmin=150, hmax=300)
+def bench_phmm(args, dev, rk):
+    p = fcship.synth_phmm(args.seed + 7919 * rk.rank, args.pairs, R=101, hmin=150, hmax=300)
     cells = p.cells()
     b, keep = phmm_dev_batch(p, dev)
     out = torch.empty(p.n_pairs, dtype=torch.float64, device=dev)
@@ -110,21 +114,16 @@ def bench_phmm(args, dev, rank, world):
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize(dev)
-    if world > 1:
-        torch.distributed.barrier()
+    rk.barrier()
     torch.cuda.synchronize(dev)
     evs = [[torch.cuda.Event(enable_timing=True) for _ in range(4)] for _ in range(args.steps)]
     t0 = time.perf_counter()
     for k in range(args.steps):
         step(evs[k])
     torch.cuda.synchronize(dev)
-    if world > 1:
-        torch.distributed.barrier()
+    rk.barrier()
     t1 = time.perf_counter()
-    elapsed = torch.tensor([t1 - t0], dtype=torch.float64, device=dev)
-    if world > 1:
-        torch.distributed.all_reduce(elapsed, op=torch.distributed.ReduceOp.MAX)
-    elapsed = float(elapsed.item())
+    elapsed = rk.max(t1 - t0)[0]
     sched_ms = float(np.mean([e[0].elapsed_time(e[1]) for e in evs]))
     fwd_ms = float(np.mean([e[1].elapsed_time(e[2]) for e in evs]))
     resc_ms = float(np.mean([e[2].elapsed_time(e[3]) for e in evs]))
@@ -215,10 +214,11 @@ def bench_bsw_global(args, dev, tasks, reps=3):
 
 def bench_e2e(args, rank, local):
     """End-to-end fcs-genome commands on this rank's own synthetic genome
-    (C4/C5-shaped: chr1-like random reference, 30x sample, 40x tumor with
-    somatic variants; weak scaling, one GPU per rank).  Wall time of each
-    command as a user runs it (process start, BAM decode, pileup, PairHMM on
-    the GPU, VCF tail)."""
+    (C4/C5-shaped: a chr1-like random reference of --e2e-mbp per GPU — 31 Mbp
+    is chr1 / 8, the C4 per-GPU share — a 30x sample, a 40x tumor with somatic
+    variants; weak scaling, one GPU per rank), and align on a separate
+    --e2e-align-mbp genome.  Wall time of each command as a user runs it
+    (process start, BAM decode, pileup, PairHMM on the GPU, VCF tail)."""
     import re
     import shutil
     import subprocess
@@ -229,12 +229,15 @@ def bench_e2e(args, rank, local):
                FCS_TEMP_DIR=work, FCS_GATK_NPROCS="16")
     try:
         L = int(args.e2e_mbp * 1e6)
-        subprocess.run([exe, "synth", "-o", work + "/d", "-c", f"chr1:{L}", "-x", "30", "--tumor",
-                        "--noisy-frac", "0.01", "--paired", "350", "--seed", str(args.seed + rank)], env=env, check=True,
+        t0 = time.perf_counter()
+        subprocess.run([exe, "synth", "-o", work + "/d", "-c", f"chr1:{L}", "-x", "30", "--tumor", "--no-fastq",
+                        "--noisy-frac", "0.01", "--seed", str(args.seed + rank)], env=env, check=True,
                        capture_output=True)
-        out = {"data": f"synthetic chr1-like {args.e2e_mbp:g} Mbp per GPU, sample 30x, tumor 40x (+1e-4 somatic), "
-                       "1% of reads mis-mapped-like (20% high-quality mismatches: their pairs reach the fp64 rescue)"}
-
+        synth_s = time.perf_counter() - t0
+        out = {"data": f"synthetic chr1-like {args.e2e_mbp:g} Mbp per GPU (chr1 / 8 = the C4 per-GPU share at 31), "
+                       "sample 30x, tumor 40x (+1e-4 somatic), 1% of reads mis-mapped-like (20% high-quality "
+                       "mismatches: their pairs reach the fp64 rescue)",
+               "synth_seconds": round(synth_s, 1)}
         def timed(name, cmd):
             shutil.rmtree(env["FCS_LOG_DIR"], ignore_errors=True)
             t0 = time.perf_counter()
@@ -293,13 +296,19 @@ def bench_e2e(args, rank, local):
         ms = stage_s(err, "Mutect2")
         out["mutect2"]["caller_stage_seconds"] = ms
         out["mutect2"]["caller_stage_regions_per_s"] = round(out["mutect2"]["regions"] / ms, 1) if ms else None
-        (dt, _, err), runs = best("align", ["align", "-f", "-r", d + "/ref.fasta", "-1", d + "/sample_1.fastq", "-2",
-                                            d + "/sample_2.fastq", "-o", work + "/aln.bam"])
+        shutil.rmtree(d, ignore_errors=True)
+        La = int(args.e2e_align_mbp * 1e6)
+        subprocess.run([exe, "synth", "-o", work + "/a", "-c", f"chr1:{La}", "-x", "30", "--no-fastq", "--paired",
+                        "350", "--seed", str(args.seed + rank)], env=env, check=True, capture_output=True)
+        a = work + "/a"
+        (dt, _, err), runs = best("align", ["align", "-f", "-r", a + "/ref.fasta", "-1", a + "/sample_1.fastq", "-2",
+                                            a + "/sample_2.fastq", "-o", work + "/aln.bam"])
         m = re.search(r"(\d+) reads, (\d+) mapped, (\d+) extension tasks, (\d+) global alignments, ([\d.]+) s "
                       r"\(GPU calls ([\d.]+) s\)", err)
         pm = re.search(r"(\d+) reads properly paired, (\d+) mates rescued, insert ([\d.]+) \+- ([\d.]+)", err)
         n = int(m.group(1)) if m else 0
-        out["align"] = {"mode": "paired-end 2x151, fragments N(350, 50)", "reads": n,
+        out["align"] = {"mode": f"paired-end 2x151, fragments N(350, 50), {args.e2e_align_mbp:g} Mbp genome, 30x "
+                                "of pairs", "reads": n,
                         "mapped": int(m.group(2)) if m else 0, "ext_tasks": int(m.group(3)) if m else 0,
                         "global_tasks": int(m.group(4)) if m else 0,
                         "gpu_call_seconds": float(m.group(6)) if m else None,
@@ -405,9 +414,101 @@ def cpu_baseline_bsw(tasks, budget_s, threads):
                        f"OpenMP {threads} threads (nproc {os.cpu_count()})")
 
 
+class Ranks:
+    """This process's place in the job (RANK / LOCAL_RANK / WORLD_SIZE from the
+    environment torch.distributed.run or launch_ranks sets) and the two
+    reductions the bench needs.  The backend is RCCL ("nccl") on the GPU and
+    gloo in --dry-run."""
+
+    def __init__(self, dry):
+        self.world = int(os.environ.get("WORLD_SIZE", "1"))
+        self.rank = int(os.environ.get("RANK", "0"))
+        self.local = int(os.environ.get("LOCAL_RANK", "0"))
+        self.dry = dry
+        self.dev = torch.device("cpu") if dry else torch.device("cuda", self.local)
+        if not dry:
+            torch.cuda.set_device(self.dev)
+        if self.world > 1:
+            os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+            if dry:
+                torch.distributed.init_process_group("gloo")
+            else:
+                torch.distributed.init_process_group("nccl", device_id=self.dev)
+
+    def barrier(self):
+        if self.world > 1:
+            torch.distributed.barrier()
+
+    def _reduce(self, vals, op):
+        t = torch.tensor(vals, dtype=torch.float64, device=self.dev)
+        if self.world > 1:
+            torch.distributed.all_reduce(t, op=op)
+        return t.tolist()
+
+    def max(self, *vals):
+        return self._reduce(list(vals), torch.distributed.ReduceOp.MAX)
+
+    def sum(self, *vals):
+        return self._reduce(list(vals), torch.distributed.ReduceOp.SUM)
+
+    def close(self):
+        if self.world > 1:
+            torch.distributed.destroy_process_group()
+
+
+def launch_ranks(n, dry):
+    """`bench.py --gpus N` outside torch.distributed.run: start N fresh rank
+    processes (RANK = LOCAL_RANK = r, WORLD_SIZE = N, MASTER_ADDR 127.0.0.1 and
+    a free MASTER_PORT) before this process makes any HIP call, wait for all of
+    them, and exit with the first failure.  Only rank 0 prints the JSON line.
+    If one rank fails, the others are stopped (they would wait in a barrier)."""
+    import signal
+    import socket
+    import subprocess
+    if not dry:
+        have = torch.cuda.device_count()  # counts devices without initialising HIP on this image
+        if have < n:
+            sys.exit(f"bench.py: --gpus {n} asks for {n} GPUs but {have} are visible")
+    with socket.socket() as so:
+        so.bind(("127.0.0.1", 0))
+        port = so.getsockname()[1]
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__), *sys.argv[1:]], env=env,
+                                      start_new_session=True))
+    rc = 0
+    live = list(procs)
+    while live:
+        for p in list(live):
+            code = p.poll()
+            if code is None:
+                continue
+            live.remove(p)
+            if code != 0 and rc == 0:
+                rc = code if code > 0 else 1
+                for q in live:  # exactly the rank processes this launcher started
+                    os.killpg(q.pid, signal.SIGTERM)
+        time.sleep(0.05)
+    sys.exit(rc)
+
+
+def dry_step(args):
+    """CPU stand-in for the PairHMM pass in --dry-run: a fixed amount of numpy work."""
+    a = np.random.default_rng(args.seed).random((256, 256))
+    for _ in range(4):
+        a = np.tanh(a @ a / 256)
+    return float(a.sum())
+
+
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=None,
+                    help="GPUs (one rank process each); without WORLD_SIZE in the environment, bench.py starts "
+                         "the rank processes itself")
+    ap.add_argument("--dry-run", action="store_true",
+                    help="CPU only: exercise the launcher, ranks and reductions over gloo with a stand-in workload")
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--pairs", type=int, default=1_000_000)
@@ -417,20 +518,26 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-budget", type=float, default=12.0)
     ap.add_argument("--no-e2e", action="store_true")
-    ap.add_argument("--e2e-mbp", type=float, default=4.0)
+    ap.add_argument("--e2e-mbp", type=float, default=31.0,
+                    help="per-GPU genome of the htc / mutect2 runs (31 Mbp = chr1 / 8 GPUs, the C4 share)")
+    ap.add_argument("--e2e-align-mbp", type=float, default=4.0, help="genome of the align run")
     ap.add_argument("--e2e-reps", type=int, default=2, help="runs of each e2e command; the fastest is reported")
     args = ap.parse_args()
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    dev = torch.device("cuda", local)
-    torch.cuda.set_device(dev)
-    if world > 1:
-        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        torch.distributed.init_process_group("nccl", device_id=dev)
+    if "WORLD_SIZE" not in os.environ and (args.gpus or 1) > 1:
+        launch_ranks(args.gpus, args.dry_run)  # exits
+    world_env = int(os.environ.get("WORLD_SIZE", "1"))
+    if args.gpus is not None and args.gpus != world_env:
+        sys.exit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world_env}")
+    rk = Ranks(args.dry_run)
+    world, rank, local, dev = rk.world, rk.rank, rk.local, rk.dev
+    if args.dry_run:
+        return dry_main(args, rk)
+    global fcship
+    import fcship as _fcship  # after torch: one HIP runtime per process
+    fcship = _fcship
 
-    ph = bench_phmm(args, dev, rank, world)
+    ph = bench_phmm(args, dev, rk)
     total_cells = ph["cells"] * world * args.steps
     value = total_cells / ph["elapsed"] / 1e9
     fwd_s = ph["fwd_ms"] * 1e-3
@@ -530,19 +637,43 @@ def main():
         e2e = bench_e2e(args, rank, local)
         if world > 1:  # whole-job rates: units of all ranks over the slowest rank's time
             for k, unit in (("htc", "regions"), ("mutect2", "regions"), ("align", "reads")):
-                t = torch.tensor([e2e[k][unit], e2e[k]["seconds"]], dtype=torch.float64, device=dev)
-                tot = t.clone()
-                torch.distributed.all_reduce(tot[:1])
-                torch.distributed.all_reduce(tot[1:], op=torch.distributed.ReduceOp.MAX)
-                e2e[k][unit] = int(tot[0].item())
-                e2e[k]["seconds"] = round(tot[1].item(), 3)
-                e2e[k][unit + "_per_s"] = round(tot[0].item() / tot[1].item(), 1)
+                tot, = rk.sum(e2e[k][unit])
+                slow, = rk.max(e2e[k]["seconds"])
+                e2e[k]["rank0_" + unit] = e2e[k][unit]
+                e2e[k][unit] = int(tot)
+                e2e[k]["seconds"] = round(slow, 3)
+                e2e[k][unit + "_per_s"] = round(tot / slow, 1)
+            e2e["n_gpus"] = world
         line["e2e"] = e2e
 
     if rank == 0:
         print(json.dumps(line), flush=True)
-    if world > 1:
-        torch.distributed.destroy_process_group()
+    rk.close()
+
+
+def dry_main(args, rk):
+    """--dry-run: the launcher, the barrier-bracketed timed region, the
+    max-over-ranks reduction and the whole-job sum, over gloo on CPU."""
+    if os.environ.get("FCS_BENCH_DRY_FAIL_RANK") == str(rk.rank):  # launcher test: one rank dies early
+        sys.exit(3)
+    for _ in range(args.warmup):
+        dry_step(args)
+    rk.barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        dry_step(args)
+    rk.barrier()
+    elapsed, = rk.max(time.perf_counter() - t0)
+    units, = rk.sum(float(args.steps))
+    ranks_seen, = rk.sum(1.0)
+    if rk.rank == 0:
+        print(json.dumps({"metric": METRIC, "value": round(units / elapsed, 3), "unit": "dry steps/s",
+                          "n_gpus": rk.world, "steps": args.steps, "warmup": args.warmup,
+                          "ms_per_step": round(elapsed / args.steps * 1e3, 3), "higher_is_better": True,
+                          "scaling": "weak", "vs_baseline": None, "dtype": "none", "data": "dry run (no GPU)",
+                          "config": {"workload": "dry run", "ranks_seen": int(ranks_seen),
+                                     "parallelism": f"static shard x{rk.world}"}}), flush=True)
+    rk.close()
 
 
 if __name__ == "__main__":

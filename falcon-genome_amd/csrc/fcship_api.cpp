@@ -58,12 +58,14 @@ struct ForkSet {
 // per call or per thread).  A launch stream is used by one call at a time:
 // a pooled session's stream by its lease holder, a caller's stream by the
 // caller.
+std::mutex g_fork_mu;
+auto* g_fork_sets = new std::map<std::pair<int, hipStream_t>, ForkSet>();  // outlives static teardown
+
 ForkSet* fork_set(hipStream_t s) {
   int device = 0;
   if (hipGetDevice(&device) != hipSuccess) return nullptr;
-  static std::mutex mu;
-  static auto* sets = new std::map<std::pair<int, hipStream_t>, ForkSet>();  // outlives static teardown
-  std::lock_guard<std::mutex> lk(mu);
+  std::lock_guard<std::mutex> lk(g_fork_mu);
+  auto* sets = g_fork_sets;
   auto it = sets->find({device, s});
   if (it != sets->end()) return &it->second;
   ForkSet f;
@@ -206,6 +208,15 @@ int prefill_sessions(int device, int n) {
     if (!S) return fail(FCS_ERR_DEVICE, "[E::fcship] stream creation failed");
   }
 }
+
+// Synchronises a session's stream when it goes out of scope (before the
+// lease returns the session to the pool): an error path must not hand the
+// next holder a session whose H2D copy is still reading the pinned staging
+// that holder is about to refill.
+struct StreamDrain {
+  hipStream_t s;
+  ~StreamDrain() { (void)hipStreamSynchronize(s); }
+};
 
 // A session of `device` (the current device) held for one call.
 class SessionLease {
@@ -655,6 +666,27 @@ int fcs_phmm_dev_run(fcs_phmm_plan* plan, const fcs_phmm_batch* b, double* out, 
   return fcs_phmm_dev_rescue(plan, b, out, opts, stream);
 }
 
+int fcs_stream_release(int32_t device, void* stream) {
+  int rc = check_device(device);
+  if (rc) return rc;
+  FCS_HIP_CHECK(hipSetDevice(device));
+  ForkSet f;
+  {
+    std::lock_guard<std::mutex> lk(g_fork_mu);
+    auto it = g_fork_sets->find({device, (hipStream_t)stream});
+    if (it == g_fork_sets->end()) return FCS_OK;
+    f = it->second;
+    g_fork_sets->erase(it);
+  }
+  for (int i = 0; i < kForkStreams - 1; ++i) {
+    FCS_HIP_CHECK(hipStreamSynchronize(f.side[i]));
+    FCS_HIP_CHECK(hipStreamDestroy(f.side[i]));
+    FCS_HIP_CHECK(hipEventDestroy(f.join[i]));
+  }
+  FCS_HIP_CHECK(hipEventDestroy(f.fork));
+  return FCS_OK;
+}
+
 int fcs_device_warmup(int32_t device, int32_t sessions) {
   int rc = check_device(device);
   if (rc) return rc;
@@ -735,6 +767,7 @@ int phmm_staged(const PhmmStage& g, const fcs_phmm_opts& opts, SessionLease& lea
   if ((rc = S->ensure_host(L.total)) || (rc = S->ensure_dev(L.total)) || (rc = S->ensure_phmm(g.n_pairs))) return rc;
   fill(S, off);
   hipStream_t s = S->s;
+  const StreamDrain drain{s};
   FCS_HIP_CHECK(hipMemcpyAsync(S->dev, S->host, in_bytes, hipMemcpyHostToDevice, s));
   fcs_phmm_batch d{};
   d.read_bases = S->d<uint8_t>(off[kRb]);
@@ -1129,6 +1162,7 @@ int fcs_bsw_extend_batch(const fcs_bsw_batch* b, const fcs_bsw_params* params, i
   std::memcpy(S->h<void>(oh0), b->h0, 4 * n);
   std::memcpy(S->h<void>(ow), b->w, 4 * n);
   hipStream_t s = S->s;
+  const StreamDrain drain{s};
   FCS_HIP_CHECK(hipMemcpyAsync(S->dev, S->host, in_bytes, hipMemcpyHostToDevice, s));
   BswDevBatch d;
   d.qbuf = S->d<uint8_t>(oq);
@@ -1295,6 +1329,7 @@ int fcs_bsw_global(const fcs_bsw_task* tasks, int32_t n, const fcs_bsw_params* p
     std::memcpy(S->h<void>(occ), cigar_cap, 4 * nn);
   }
   hipStream_t s = S->s;
+  const StreamDrain drain{s};
   FCS_HIP_CHECK(hipMemcpyAsync(S->dev, S->host, in_bytes, hipMemcpyHostToDevice, s));
   BswDevBatch d;
   d.qbuf = S->d<uint8_t>(oq);
@@ -1412,6 +1447,6 @@ int fcs_ksw_global2(int qlen, const uint8_t* query, int tlen, const uint8_t* tar
   return score;
 }
 
-int fcs_abi_symbol_count(void) { return 37; }
+int fcs_abi_symbol_count(void) { return 38; }
 
 }  // extern "C"

@@ -421,12 +421,12 @@ __host__ __device__ inline int phmm_class(int H) {
 // Sort keys (16 bits, two 8-bit radix passes; 24 / three under FCS_PHMM_KEY16=0): a 4-bit launch class, then the
 // in-class order, as ascending keys — each class is a contiguous range and the
 // longest work comes first.  Classes 0 .. kStreamClasses-1 are the row-streamed
-// kernel's (R >= kStreamMinR, longest hap-length class first), the rest the
+// kernel's (kStreamMinR <= R <= kStreamMaxR, longest hap-length class first), the rest the
 // grouped kernels' hap-length classes (longest first).  In-class order:
 // streamed, hap length (24-bit keys: then read length) descending; grouped, stripe
 // count then hap length descending.  The clamps only change the order, never results.
 __host__ __device__ inline int phmm_launch_class(int R, int H, int& stream_cls) {
-  stream_cls = (R >= kStreamMinR && H >= 1) ? stream_class(H) : -1;
+  stream_cls = (R >= kStreamMinR && R <= kStreamMaxR && H >= 1) ? stream_class(H) : -1;
   if (stream_cls >= 0) return kStreamClasses - 1 - stream_cls;
   return kStreamClasses + kPhmmClasses - 1 - phmm_class(max(H, 0));
 }
@@ -606,7 +606,7 @@ int launch_phmm_forward(const PhmmDevBatch& b, const int32_t* order, int64_t cou
                  : w == 2 ? launch(phmm3_kernel<2>) : launch(phmm3_kernel<1>);
     if (rc != FCS_OK) return rc;
   }
-  // Grouped classes (reads shorter than kStreamMinR; empty in most batches):
+  // Grouped classes (reads shorter than kStreamMinR or longer than kStreamMaxR; empty in most batches):
   // kept off fs[0], which carries the longest-haplotype stream class, so an
   // empty grouped launch does not extend the pass after it; and launched with
   // at most kGroupedGrid workgroups striding over the class (about 2.7 rounds of

@@ -51,6 +51,7 @@ constexpr int kStreamHalf = FCS_STREAM_HALF;  // a stripe's last block runs 8 st
 #endif
 constexpr int kStreamPfd = FCS_STREAM_PFD;  // LDS read-ahead of the 3/2/1-wave stream classes
 constexpr int kStreamMinR = 33;  // a pair spans >= 17 units: at most two pairs per stripe and segment
+constexpr int kStreamMaxR = 0xFFFF;  // a segment packs R | H << 16 between stripes; longer reads take phmm2
 constexpr int kStreamMaxK = 8;   // pairs per segment stream
 // Hap-length bounds of the stream classes: LDS <= 10,240 B per wave (4 waves per
 // SIMD), <= 13,312 B (3, at the 512-byte allocation granularity), <= 20 KB (2),

@@ -263,10 +263,14 @@ BamWriter::BamWriter(const std::string& path, const BamHeader& h, int level)
 
 void BamWriter::write(const BamRecord& r) {
   encode_bam_record(r, rec_);
-  const int32_t bs = (int32_t)rec_.size();
+  write_encoded(r, rec_);
+}
+
+void BamWriter::write_encoded(const BamRecord& r, const std::string& body) {
+  const int32_t bs = (int32_t)body.size();
   const uint64_t u0 = bgzf_.upos();
   bgzf_.write(&bs, 4);
-  bgzf_.write(rec_);
+  bgzf_.write(body);
   if (index_) spans_.push_back({r.ref_id, r.pos, r.ref_id >= 0 ? r.end() : 0, u0, bgzf_.upos()});
 }
 

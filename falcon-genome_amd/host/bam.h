@@ -61,6 +61,9 @@ class BamWriter {
  public:
   BamWriter(const std::string& path, const BamHeader& h, int level = 6);
   void write(const BamRecord& r);
+  // write(r) with the record body already encoded by encode_bam_record(r, body)
+  // (callers encode many records on worker threads and write them in order).
+  void write_encoded(const BamRecord& r, const std::string& body);
   // Also write <path>.bai at close(), from the records as they are written
   // (coordinate order required): the index bam_index_build would compute,
   // without reading the file back.

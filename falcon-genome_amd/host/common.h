@@ -5,6 +5,7 @@
 #pragma once
 
 #include <algorithm>
+#include <atomic>
 #include <chrono>
 #include <cstdint>
 #include <iomanip>
@@ -29,6 +30,24 @@ void parallel_for(size_t n, int threads, F&& fn) {
   for (size_t t = 0; t < nt; ++t)
     th.emplace_back([&, t] {
       for (size_t i = n * t / nt; i < n * (t + 1) / nt; ++i) fn(i);
+    });
+  for (auto& x : th) x.join();
+}
+
+// Dynamic split of [0, n) over up to `threads` std::threads: each thread takes
+// the next item from a shared counter (for a few coarse items of uneven cost).
+template <typename F>
+void parallel_tasks(size_t n, int threads, F&& fn) {
+  const size_t nt = std::min<size_t>((size_t)std::max(threads, 1), n);
+  if (nt <= 1) {
+    for (size_t i = 0; i < n; ++i) fn(i);
+    return;
+  }
+  std::atomic<size_t> next{0};
+  std::vector<std::thread> th;
+  for (size_t t = 0; t < nt; ++t)
+    th.emplace_back([&] {
+      for (size_t i; (i = next.fetch_add(1, std::memory_order_relaxed)) < n;) fn(i);
     });
   for (auto& x : th) x.join();
 }

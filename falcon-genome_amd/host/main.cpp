@@ -262,6 +262,7 @@ int synth_main(int argc, char** argv) {
   a.add("spike", "", false, false, "chr:pos[,chr:pos...] plant three het SNVs at pos-30, pos, pos+30 (1-based)");
   a.add("parts", "", false, false, "also split the sample into parts/part-XXXXXX.bam + .bed (N buckets)");
   a.add("paired", "", false, false, "also write sample_1/2.fastq: FR pairs with fragment length ~ N(ARG, 50)");
+  a.add("no-fastq", "", true, false, "do not write sample.fastq (the single-end FASTQ of the sample's reads)");
   a.parse(argc, argv);
   SynthSpec sp;
   if (a.has("contigs")) {
@@ -288,6 +289,7 @@ int synth_main(int argc, char** argv) {
       p = e + 1;
     }
   }
+  if (a.has("no-fastq")) sp.single_fastq = false;
   if (a.has("noisy-frac")) sp.noisy_frac = std::stod(a.get("noisy-frac"));
   if (a.has("parts")) sp.parts = std::stoi(a.get("parts"));
   if (a.has("paired")) sp.paired_insert = std::stoi(a.get("paired"));

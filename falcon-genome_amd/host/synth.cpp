@@ -3,6 +3,11 @@
 #include "intervals.h"
 
 #include <algorithm>
+#include <array>
+#include <atomic>
+#include <cstdio>
+#include <thread>
+#include <tuple>
 #include <cmath>
 #include <fstream>
 #include <map>
@@ -35,12 +40,6 @@ char other_base(Rng& r, char b) {
     const char c = kBases[r.below(4)];
     if (c != b) return c;
   }
-}
-
-std::string revcomp(const std::string& s) {
-  std::string o(s.rbegin(), s.rend());
-  for (char& c : o) c = c == 'A' ? 'T' : c == 'C' ? 'G' : c == 'G' ? 'C' : c == 'T' ? 'A' : 'N';
-  return o;
 }
 
 // One haplotype of a contig: sequence and, per base, its reference position (-1 = inserted).
@@ -78,8 +77,91 @@ Hap build_hap(const std::string& ref, const std::vector<const SynthVariant*>& va
 struct SimRead {
   int64_t pos;
   BamRecord rec;
-  std::string fq_seq, fq_qual;
 };
+
+// Reads are drawn in fixed chunks of kChunk draws, each chunk from its own
+// RNG stream and named by its draw index, so the data set does not depend on
+// how many threads generate it.
+constexpr int64_t kChunk = 1 << 15;
+
+Rng chunk_rng(uint64_t seed, uint64_t stream, int64_t chunk) {
+  return Rng(seed, stream ^ ((uint64_t)(chunk + 1) << 32));
+}
+
+int synth_threads() { return (int)std::min(16u, std::max(1u, std::thread::hardware_concurrency())); }
+
+// parallel_for whose bodies may be interrupted: the workers stop at the next
+// item and the caller raises interruptedError (an exception must not leave a
+// worker thread).
+template <typename F>
+void parallel_items(size_t n, F&& fn) {
+  std::atomic<bool> stop{false};
+  parallel_tasks(n, synth_threads(), [&](size_t i) {
+    if (stop.load(std::memory_order_relaxed)) return;
+    if (interrupted()) {
+      stop = true;
+      return;
+    }
+    fn(i);
+  });
+  if (stop) throw interruptedError();
+}
+
+// FASTQ text of a read as sequenced (a reverse-strand read is reverse-complemented).
+void append_fastq(std::string& o, const std::string& name, const std::string& seq, const std::vector<uint8_t>& qual,
+                  bool rev) {
+  o += '@';
+  o += name;
+  o += '\n';
+  const size_t n = seq.size();
+  if (!rev) {
+    o += seq;
+  } else {
+    for (size_t i = n; i-- > 0;) {
+      const char c = seq[i];
+      o += c == 'A' ? 'T' : c == 'C' ? 'G' : c == 'G' ? 'C' : c == 'T' ? 'A' : 'N';
+    }
+  }
+  o += "\n+\n";
+  for (size_t i = 0; i < n; ++i) o += (char)(33 + qual[rev ? n - 1 - i : i]);
+  o += '\n';
+}
+
+// Formats items [0, n) into text blocks on worker threads and writes the
+// blocks in order (a bounded window of blocks is held at a time).
+template <typename F>
+void write_text_parallel(const std::string& path, size_t n, F&& fmt) {
+  FILE* f = std::fopen(path.c_str(), "wb");
+  if (!f) throw std::runtime_error("cannot write " + path);
+  constexpr size_t kBlock = 1 << 14;
+  const size_t nblk = (n + kBlock - 1) / kBlock, win = (size_t)synth_threads() * 4;
+  std::vector<std::string> text(win);
+  for (size_t b0 = 0; b0 < nblk; b0 += win) {
+    const size_t nb = std::min(win, nblk - b0);
+    parallel_items(nb, [&](size_t k) {
+      std::string& s = text[k];
+      s.clear();
+      for (size_t i = (b0 + k) * kBlock; i < std::min(n, (b0 + k + 1) * kBlock); ++i) fmt(i, s);
+    });
+    for (size_t k = 0; k < nb; ++k) std::fwrite(text[k].data(), 1, text[k].size(), f);
+  }
+  if (std::fclose(f) != 0) throw std::runtime_error("cannot write " + path);
+}
+
+// Coordinate order of the reads (reference, position, then draw order: a stable sort).
+std::vector<uint32_t> coordinate_order(const std::vector<SimRead>& reads) {
+  struct Key {
+    uint64_t k;
+    uint32_t i;
+  };
+  std::vector<Key> keys(reads.size());
+  for (size_t i = 0; i < reads.size(); ++i)
+    keys[i] = {((uint64_t)(uint32_t)reads[i].rec.ref_id << 40) | (uint64_t)reads[i].pos, (uint32_t)i};
+  std::sort(keys.begin(), keys.end(), [](const Key& a, const Key& b) { return a.k != b.k ? a.k < b.k : a.i < b.i; });
+  std::vector<uint32_t> o(reads.size());
+  for (size_t i = 0; i < o.size(); ++i) o[i] = keys[i].i;
+  return o;
+}
 
 // Read covering hap[s, s + L): CIGAR from the haplotype's reference map.
 bool make_read(const Hap& h, int64_t s, int L, Rng& r, double err, SimRead& out) {
@@ -128,20 +210,30 @@ bool make_read(const Hap& h, int64_t s, int L, Rng& r, double err, SimRead& out)
   return true;
 }
 
-void write_reads(std::vector<SimRead>& reads, const BamHeader& hdr, const std::string& bam, const std::string& fastq) {
-  std::stable_sort(reads.begin(), reads.end(), [](const SimRead& a, const SimRead& b) {
-    return a.rec.ref_id != b.rec.ref_id ? a.rec.ref_id < b.rec.ref_id : a.pos < b.pos;
-  });
+void write_reads(const std::vector<SimRead>& reads, const std::vector<uint32_t>& order, const BamHeader& hdr,
+                 const std::string& bam, const std::string& fastq) {
   {
-    BamWriter w(bam, hdr);
+    BamWriter w(bam, hdr, 1);  // synthetic inputs: fastest deflate level
     w.index_on_close();
-    for (const SimRead& sr : reads) w.write(sr.rec);
+    // records encode on worker threads, a window at a time, and are written in order
+    constexpr size_t kBlock = 1 << 12;
+    const size_t win = (size_t)synth_threads() * 4 * kBlock;
+    std::vector<std::string> body(std::min(win, order.size()));
+    for (size_t i0 = 0; i0 < order.size(); i0 += win) {
+      const size_t n = std::min(win, order.size() - i0);
+      parallel_items((n + kBlock - 1) / kBlock, [&](size_t b) {
+        for (size_t k = b * kBlock; k < std::min(n, (b + 1) * kBlock); ++k)
+          encode_bam_record(reads[order[i0 + k]].rec, body[k]);
+      });
+      for (size_t k = 0; k < n; ++k) w.write_encoded(reads[order[i0 + k]].rec, body[k]);
+    }
     w.close();
   }
-  if (!fastq.empty()) {
-    std::ofstream fq(fastq);
-    for (const SimRead& sr : reads) fq << '@' << sr.rec.name << '\n' << sr.fq_seq << "\n+\n" << sr.fq_qual << '\n';
-  }
+  if (!fastq.empty())
+    write_text_parallel(fastq, order.size(), [&](size_t k, std::string& s) {
+      const BamRecord& r = reads[order[k]].rec;
+      append_fastq(s, r.name, r.seq, r.qual, r.flag & kReverse);
+    });
 }
 
 }  // namespace
@@ -238,70 +330,92 @@ SynthOutputs synth_dataset(const SynthSpec& spec, const std::string& dir) {
     hdr.lengths.push_back((int64_t)c.seq.size());
     hdr.text += "@SQ\tSN:" + c.name + "\tLN:" + std::to_string(c.seq.size()) + "\n";
   }
+  // haplotypes of contig c: [copy][somatic?] (germline variants only unless `som`)
+  auto contig_haps = [&](size_t c, bool tumor, Hap (&haps)[2][2]) {
+    for (int copy = 0; copy < 2; ++copy)
+      for (int som = 0; som < (tumor ? 2 : 1); ++som) {
+        std::vector<const SynthVariant*> vs;
+        for (const SynthVariant& v : per[c]) {
+          if (v.somatic && !som) continue;
+          // het germline and somatic variants sit on copy 0 or 1 by a per-site coin
+          const bool on = v.gt == 2 || ((v.pos * 2654435761u) >> 7 & 1) == (uint64_t)copy;
+          if (on) vs.push_back(&v);
+        }
+        haps[copy][som] = build_hap(ref.contigs[c].seq, vs);
+      }
+  };
+  const int L = spec.read_len;
+  // chunks of the n draws of one contig, and the draws of the contigs before c
+  // (the first global draw index of contig c: read names)
+  struct Chunk {
+    int64_t chunk, k0, k1;
+  };
+  auto chunks_of = [](int64_t n) {
+    std::vector<Chunk> v;
+    for (int64_t k0 = 0; k0 < n; k0 += kChunk) v.push_back({k0 / kChunk, k0, std::min(n, k0 + kChunk)});
+    return v;
+  };
+  auto draws = [&](size_t c, double cov) { return (int64_t)(cov * (double)ref.contigs[c].seq.size() / L); };
+  auto draws_before = [&](size_t c, double cov) {
+    int64_t b = 0;
+    for (size_t k = 0; k < c; ++k) b += draws(k, cov);
+    return b;
+  };
   auto sample_reads = [&](const std::string& sample, bool tumor, double coverage, uint64_t stream) {
     std::string h = hdr.text + "@RG\tID:" + sample + "\tSM:" + sample + "\n";
     std::vector<SimRead> reads;
-    int64_t idx = 0;
     for (size_t c = 0; c < ref.contigs.size(); ++c) {
-      Rng hr(spec.seed, stream + 0x10 * c);
-      // haplotypes: [copy][somatic?]
       Hap haps[2][2];
-      for (int copy = 0; copy < 2; ++copy)
-        for (int som = 0; som < (tumor ? 2 : 1); ++som) {
-          std::vector<const SynthVariant*> vs;
-          for (const SynthVariant& v : per[c]) {
-            if (v.somatic && !som) continue;
-            // het germline and somatic variants sit on copy 0 or 1 by a per-site coin
-            const bool on = v.gt == 2 || ((v.pos * 2654435761u) >> 7 & 1) == (uint64_t)copy;
-            if (on) vs.push_back(&v);
-          }
-          haps[copy][som] = build_hap(ref.contigs[c].seq, vs);
+      contig_haps(c, tumor, haps);
+      const auto chunks = chunks_of(draws(c, coverage));
+      const int64_t base = draws_before(c, coverage);
+      std::vector<std::vector<SimRead>> part(chunks.size());
+      parallel_items(chunks.size(), [&](size_t t) {
+        const Chunk& ch = chunks[t];
+        Rng hr = chunk_rng(spec.seed, stream + 0x10 * c, ch.chunk);
+        std::vector<SimRead>& o = part[t];
+        o.reserve((size_t)(ch.k1 - ch.k0));
+        for (int64_t k = ch.k0; k < ch.k1; ++k) {
+          const int copy = (int)hr.below(2);
+          const int som = tumor && hr.uniform() < 2 * spec.somatic_af ? 1 : 0;  // somatic on one copy → AF = somatic_af
+          const Hap& hp = haps[copy][som];
+          if ((int64_t)hp.seq.size() <= L) continue;
+          const int64_t s = (int64_t)hr.below(hp.seq.size() - L);
+          SimRead sr;
+          if (!make_read(hp, s, L, hr, spec.err_rate, sr)) continue;
+          if (spec.noisy_frac > 0 && hr.uniform() < spec.noisy_frac)
+            for (size_t i = 0; i < sr.rec.seq.size(); ++i)
+              if (hr.uniform() < 0.2) {
+                sr.rec.seq[i] = other_base(hr, sr.rec.seq[i]);
+                sr.rec.qual[i] = (uint8_t)(35 + hr.below(6));
+              }
+          sr.rec.ref_id = (int32_t)c;
+          sr.rec.name = sample + ":" + std::to_string(base + k);
+          sr.rec.flag = hr.uniform() < 0.5 ? kReverse : 0;
+          sr.rec.set_aux_string("RG", sample);
+          o.push_back(std::move(sr));
         }
-      const int L = spec.read_len;
-      const int64_t n = (int64_t)(coverage * (double)ref.contigs[c].seq.size() / L);
-      for (int64_t k = 0; k < n; ++k) {
-        if ((k & 0xFFFF) == 0 && interrupted()) throw interruptedError();
-        const int copy = (int)hr.below(2);
-        const int som = tumor && hr.uniform() < 2 * spec.somatic_af ? 1 : 0;  // somatic on one copy → AF = somatic_af
-        const Hap& hp = haps[copy][som];
-        if ((int64_t)hp.seq.size() <= L) continue;
-        const int64_t s = (int64_t)hr.below(hp.seq.size() - L);
-        SimRead sr;
-        if (!make_read(hp, s, L, hr, spec.err_rate, sr)) continue;
-        if (spec.noisy_frac > 0 && hr.uniform() < spec.noisy_frac)
-          for (size_t i = 0; i < sr.rec.seq.size(); ++i)
-            if (hr.uniform() < 0.2) {
-              sr.rec.seq[i] = other_base(hr, sr.rec.seq[i]);
-              sr.rec.qual[i] = (uint8_t)(35 + hr.below(6));
-            }
-        sr.rec.ref_id = (int32_t)c;
-        sr.rec.name = sample + ":" + std::to_string(idx++);
-        const bool rev = hr.uniform() < 0.5;
-        sr.rec.flag = rev ? kReverse : 0;
-        sr.rec.set_aux_string("RG", sample);
-        std::string qs(sr.rec.qual.size(), '!');
-        for (size_t i = 0; i < qs.size(); ++i) qs[i] = (char)(33 + sr.rec.qual[i]);
-        sr.fq_seq = rev ? revcomp(sr.rec.seq) : sr.rec.seq;
-        sr.fq_qual = rev ? std::string(qs.rbegin(), qs.rend()) : qs;
-        reads.push_back(std::move(sr));
+      });
+      size_t tot = reads.size();
+      for (const auto& v : part) tot += v.size();
+      reads.reserve(tot);
+      for (auto& v : part) {
+        for (SimRead& r : v) reads.push_back(std::move(r));
+        std::vector<SimRead>().swap(v);
       }
     }
-    if (spec.max_reads >= 0 && (int64_t)reads.size() > spec.max_reads) {
-      std::stable_sort(reads.begin(), reads.end(), [](const SimRead& a, const SimRead& b) {
-        return a.rec.ref_id != b.rec.ref_id ? a.rec.ref_id < b.rec.ref_id : a.pos < b.pos;
-      });
-      reads.resize(spec.max_reads);
-    }
+    std::vector<uint32_t> order = coordinate_order(reads);
+    if (spec.max_reads >= 0 && (int64_t)order.size() > spec.max_reads) order.resize(spec.max_reads);
     BamHeader hh = hdr;
     hh.text = h;
-    return std::make_pair(std::move(reads), hh);
+    return std::make_tuple(std::move(reads), std::move(order), hh);
   };
   {
-    auto rs = sample_reads("sample", false, spec.coverage, 0x3000);
+    auto [reads, order, hh] = sample_reads("sample", false, spec.coverage, 0x3000);
     out.bam = dir + "/sample.bam";
-    out.fastq = dir + "/sample.fastq";
-    out.n_reads = (int64_t)rs.first.size();
-    write_reads(rs.first, rs.second, out.bam, out.fastq);
+    out.fastq = spec.single_fastq ? dir + "/sample.fastq" : "";
+    out.n_reads = (int64_t)order.size();
+    write_reads(reads, order, hh, out.bam, out.fastq);
     if (spec.parts > 0) {
       std::vector<std::pair<std::string, int64_t>> dict;
       for (const Contig& c : ref.contigs) dict.emplace_back(c.name, (int64_t)c.seq.size());
@@ -309,16 +423,17 @@ SynthOutputs synth_dataset(const SynthSpec& spec, const std::string& dir) {
       out.parts_dir = dir + "/parts";
       create_dir(out.parts_dir);
       for (int k = 0; k < spec.parts; ++k) {
-        std::vector<SimRead> part;
-        for (const SimRead& sr : rs.first) {
+        std::vector<uint32_t> part;
+        for (uint32_t i : order) {
+          const SimRead& sr = reads[i];
           const std::string& chrom = ref.contigs[sr.rec.ref_id].name;
           for (const Interval& iv : buckets[k])
             if (iv.chrom == chrom && sr.pos + 1 >= iv.lb && sr.pos + 1 <= iv.ub) {
-              part.push_back(sr);
+              part.push_back(i);
               break;
             }
         }
-        write_reads(part, rs.second, get_contig_fname(out.parts_dir, k, "bam"), "");
+        write_reads(reads, part, hh, get_contig_fname(out.parts_dir, k, "bam"), "");
         std::ofstream bed(get_contig_fname(out.parts_dir, k, "bed"));
         for (const Interval& iv : buckets[k]) bed << iv.chrom << '\t' << iv.lb - 1 << '\t' << iv.ub << '\n';
       }
@@ -328,53 +443,58 @@ SynthOutputs synth_dataset(const SynthSpec& spec, const std::string& dir) {
     out.fastq1 = dir + "/sample_1.fastq";
     out.fastq2 = dir + "/sample_2.fastq";
     out.pairs_truth = dir + "/pairs_truth.tsv";
-    std::ofstream f1(out.fastq1), f2(out.fastq2), tt(out.pairs_truth);
-    int64_t idx = 0;
-    const int L = spec.read_len;
+    FILE* fo[3] = {std::fopen(out.fastq1.c_str(), "wb"), std::fopen(out.fastq2.c_str(), "wb"),
+                   std::fopen(out.pairs_truth.c_str(), "wb")};
+    for (FILE* f : fo)
+      if (!f) throw std::runtime_error("cannot write the paired FASTQ files in " + dir);
     for (size_t c = 0; c < ref.contigs.size(); ++c) {
-      Rng hr(spec.seed, 0x5000 + 0x10 * c);
-      Hap haps[2];
-      for (int copy = 0; copy < 2; ++copy) {
-        std::vector<const SynthVariant*> vs;
-        for (const SynthVariant& v : per[c])
-          if (!v.somatic && (v.gt == 2 || ((v.pos * 2654435761u) >> 7 & 1) == (uint64_t)copy)) vs.push_back(&v);
-        haps[copy] = build_hap(ref.contigs[c].seq, vs);
-      }
-      const int64_t n = (int64_t)(spec.coverage / 2 * (double)ref.contigs[c].seq.size() / L);
-      for (int64_t k = 0; k < n; ++k) {
-        if ((k & 0xFFFF) == 0 && interrupted()) throw interruptedError();
-        const Hap& hp = haps[hr.below(2)];
-        const double u1 = std::max(hr.uniform(), 1e-12), u2 = hr.uniform();
-        const double z = std::sqrt(-2. * std::log(u1)) * std::cos(6.283185307179586 * u2);
-        const int64_t ins = std::max<int64_t>(L, (int64_t)std::llround(spec.paired_insert + spec.paired_sd * z));
-        if ((int64_t)hp.seq.size() <= ins) continue;
-        const int64_t s0 = (int64_t)hr.below(hp.seq.size() - ins);
-        SimRead fw, rv;
-        if (!make_read(hp, s0, L, hr, spec.err_rate, fw) || !make_read(hp, s0 + ins - L, L, hr, spec.err_rate, rv))
-          continue;
-        const bool flip = hr.uniform() < 0.5;  // read 1 from the reverse strand
-        const std::string name = "pair:" + std::to_string(idx++);
-        auto fq = [](const SimRead& r, bool rev) {
-          std::string qs(r.rec.qual.size(), '!');
-          for (size_t i = 0; i < qs.size(); ++i) qs[i] = (char)(33 + r.rec.qual[i]);
-          return rev ? std::make_pair(revcomp(r.rec.seq), std::string(qs.rbegin(), qs.rend()))
-                     : std::make_pair(r.rec.seq, qs);
-        };
-        const SimRead& m1 = flip ? rv : fw;
-        const SimRead& m2 = flip ? fw : rv;
-        const auto a = fq(m1, flip), b = fq(m2, !flip);
-        f1 << '@' << name << "/1\n" << a.first << "\n+\n" << a.second << '\n';
-        f2 << '@' << name << "/2\n" << b.first << "\n+\n" << b.second << '\n';
-        tt << name << "\t1\t" << c << '\t' << m1.pos << '\t' << (flip ? 1 : 0) << '\n';
-        tt << name << "\t2\t" << c << '\t' << m2.pos << '\t' << (flip ? 0 : 1) << '\n';
+      Hap haps[2][2];
+      contig_haps(c, false, haps);
+      const auto chunks = chunks_of(draws(c, spec.coverage / 2));
+      const int64_t base = draws_before(c, spec.coverage / 2);
+      const size_t win = (size_t)synth_threads() * 2;
+      std::vector<std::array<std::string, 3>> text(win);
+      for (size_t t0 = 0; t0 < chunks.size(); t0 += win) {
+        const size_t nt = std::min(win, chunks.size() - t0);
+        parallel_items(nt, [&](size_t t) {
+          const Chunk& ch = chunks[t0 + t];
+          Rng hr = chunk_rng(spec.seed, 0x5000 + 0x10 * c, ch.chunk);
+          auto& [s1, s2, st] = text[t];
+          s1.clear();
+          s2.clear();
+          st.clear();
+          for (int64_t k = ch.k0; k < ch.k1; ++k) {
+            const Hap& hp = haps[hr.below(2)][0];
+            const double u1 = std::max(hr.uniform(), 1e-12), u2 = hr.uniform();
+            const double z = std::sqrt(-2. * std::log(u1)) * std::cos(6.283185307179586 * u2);
+            const int64_t ins = std::max<int64_t>(L, (int64_t)std::llround(spec.paired_insert + spec.paired_sd * z));
+            if ((int64_t)hp.seq.size() <= ins) continue;
+            const int64_t s0 = (int64_t)hr.below(hp.seq.size() - ins);
+            SimRead fw, rv;
+            if (!make_read(hp, s0, L, hr, spec.err_rate, fw) || !make_read(hp, s0 + ins - L, L, hr, spec.err_rate, rv))
+              continue;
+            const bool flip = hr.uniform() < 0.5;  // read 1 from the reverse strand
+            const std::string name = "pair:" + std::to_string(base + k);
+            const SimRead& m1 = flip ? rv : fw;
+            const SimRead& m2 = flip ? fw : rv;
+            append_fastq(s1, name + "/1", m1.rec.seq, m1.rec.qual, flip);
+            append_fastq(s2, name + "/2", m2.rec.seq, m2.rec.qual, !flip);
+            st += name + "\t1\t" + std::to_string(c) + '\t' + std::to_string(m1.pos) + '\t' + (flip ? "1" : "0") + '\n';
+            st += name + "\t2\t" + std::to_string(c) + '\t' + std::to_string(m2.pos) + '\t' + (flip ? "0" : "1") + '\n';
+          }
+        });
+        for (size_t t = 0; t < nt; ++t)
+          for (int j = 0; j < 3; ++j) std::fwrite(text[t][j].data(), 1, text[t][j].size(), fo[j]);
       }
     }
+    for (FILE* f : fo)
+      if (std::fclose(f) != 0) throw std::runtime_error("cannot write the paired FASTQ files in " + dir);
   }
   if (spec.somatic_rate > 0) {
-    auto rs = sample_reads("tumor", true, spec.tumor_coverage, 0x4000);
+    auto [reads, order, hh] = sample_reads("tumor", true, spec.tumor_coverage, 0x4000);
     out.tumor_bam = dir + "/tumor.bam";
-    out.n_tumor_reads = (int64_t)rs.first.size();
-    write_reads(rs.first, rs.second, out.tumor_bam, "");
+    out.n_tumor_reads = (int64_t)order.size();
+    write_reads(reads, order, hh, out.tumor_bam, "");
   }
 
   // ---- truth VCF (1-based, VCF alleles)

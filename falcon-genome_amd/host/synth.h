@@ -50,6 +50,8 @@ struct SynthSpec {
   // fragments), and <dir>/pairs_truth.tsv (name, mate, contig, pos, reverse)
   int paired_insert = 0;
   int paired_sd = 50;
+  // write <dir>/sample.fastq (the sample's reads as sequenced, BAM order)
+  bool single_fastq = true;
 };
 
 struct SynthOutputs {

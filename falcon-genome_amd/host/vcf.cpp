@@ -190,6 +190,26 @@ class TabixBuilder {
     const int64_t pos = std::strtoll(t[0] + 1, &pe, 10);
     if (pe != t[1]) throw formatError(label_ + ": malformed VCF POS");
     const int64_t rlen = (int64_t)(t[3] - t[2] - 1);
+    // htslib's VCF preset (tbx_parse1): INFO's END= (a GVCF <NON_REF> block,
+    // a symbolic allele) beyond POS sets the record's end (1-based inclusive =
+    // 0-based exclusive); the field is "END=" at the start of INFO or the
+    // first ";END="
+    int64_t info_end = -1;
+    {
+      const char* q = p;  // ALT
+      for (int k = 0; k < 3 && q; ++k) {  // -> QUAL -> FILTER -> INFO
+        q = static_cast<const char*>(std::memchr(q, '\t', (size_t)(e - q)));
+        if (q) ++q;
+      }
+      if (q && q < e) {
+        const char* ie = static_cast<const char*>(std::memchr(q, '\t', (size_t)(e - q)));
+        const std::string info(q, ie ? ie : e);
+        size_t at = std::string::npos;
+        if (info.compare(0, 4, "END=") == 0) at = 4;
+        else if (const size_t k = info.find(";END="); k != std::string::npos) at = k + 5;
+        if (at != std::string::npos && at < info.size() && info[at] != '.') info_end = std::strtoll(info.c_str() + at, nullptr, 10);
+      }
+    }
     const size_t clen = (size_t)(t[0] - line);
     int tid;
     if (!names_.empty() && names_.back().size() == clen && std::memcmp(names_.back().data(), line, clen) == 0) {
@@ -205,7 +225,7 @@ class TabixBuilder {
     if (tid == last_tid_ && pos < last_pos_) throw formatError(label_ + ": positions not sorted");
     last_tid_ = tid;
     last_pos_ = pos;
-    const int64_t beg = pos - 1, end = beg + std::max<int64_t>(rlen, 1);
+    const int64_t beg = pos - 1, end = info_end > beg ? info_end : beg + std::max<int64_t>(rlen, 1);
     RefIndex& ri = idx_[tid];
     const uint32_t bin = (uint32_t)reg2bin(beg, end);
     if (tid != cache_tid_ || bin != cache_bin_) {  // records mostly repeat the previous bin
@@ -298,7 +318,7 @@ void bgzip_tabix_file(const std::string& input, const std::string& output) {
     uint32_t len;
   };
   std::vector<Rec> recs;
-  std::string lines;  // the record lines' first five columns (enough for the index)
+  std::string lines;  // the record lines' first eight columns (through INFO: enough for the index)
   std::vector<char> buf(4 << 20);
   std::string carry;
   uint64_t u = 0;  // uncompressed offset of buf[0] - carry.size()
@@ -306,7 +326,7 @@ void bgzip_tabix_file(const std::string& input, const std::string& output) {
     if (n == 0 || s[0] == '#') return false;
     size_t keep = n, tabs = 0;
     for (size_t k = 0; k < n; ++k)
-      if (s[k] == '\t' && ++tabs == 5) {
+      if (s[k] == '\t' && ++tabs == 8) {
         keep = k;
         break;
       }

@@ -35,7 +35,10 @@
  *     HIP stream for the synchronous host-pointer calls;
  *   - `device` selects the GPU (the Executor's GPU slot);
  *   - the *_dev entry points take DEVICE pointers and a hipStream_t (passed as
- *     void*), enqueue work and return without synchronising.
+ *     void*), enqueue work and return without synchronising.  The library
+ *     keeps side streams and events per launch stream it has seen (a stream
+ *     costs ~3.5 ms to create): use long-lived launch streams, and call
+ *     fcs_stream_release before destroying one.
  *
  * Nothing here falls back to the CPU: if no gfx950 device is present the
  * calls fail with FCS_ERR_DEVICE.
@@ -71,6 +74,11 @@ int fcs_abi_symbol_count(void);
  * decode their reads (the reference's BackgroundExecutor role,
  * /root/reference/include/fcs-genome/BackgroundExecutor.h:12). */
 int fcs_device_warmup(int32_t device, int32_t sessions);
+/* Drops the side streams and events the library keeps for launch stream
+ * `stream` on `device` (created at its first *_dev call).  Call it after the
+ * stream's work has finished and before destroying the stream; a later *_dev
+ * call on the same stream recreates them. */
+int fcs_stream_release(int32_t device, void* stream);
 
 /* ----------------------------------------------------------------- PairHMM */
 /* One read: bases + the four per-base quality arrays GATK hands to the PairHMM

@@ -423,3 +423,35 @@ def test_cli_exit_codes(tmp_path, synth_small):
     assert "gatk.ncontigs = 7" in p.stderr
     p = H.run_cli("conf", cwd=tmp_path, env={"FCS_GATK_NCONTIGS": "9"})
     assert "gatk.ncontigs = 9" in p.stderr
+
+
+def test_tabix_gvcf_block_end_from_info(tmp_path):
+    """A GVCF <NON_REF> block is indexed over [POS, INFO END] as htslib's VCF
+    preset does (tbx_parse1): a query that starts inside a multi-window block
+    finds it through both its bin and the linear index."""
+    hdr = "##fileformat=VCFv4.2\n##contig=<ID=c1,length=200000>\n" \
+          "#CHROM\tPOS\tID\tREF\tALT\tQUAL\tFILTER\tINFO\tFORMAT\tS\n"
+    lines = ["c1\t100\t.\tA\tT\t50\tPASS\tDP=9\tGT\t0/1",
+             "c1\t101\t.\tC\t<NON_REF>\t.\t.\tEND=40000\tGT:DP\t0/0:30",     # spans windows 0..2
+             "c1\t40001\t.\tG\t<NON_REF>\t.\t.\tDP=3;END=40010\tGT:DP\t0/0:3",  # END= after another field
+             "c1\t40011\t.\tGTT\tG\t50\tPASS\tEND=.\tGT\t0/1",                # END=. is ignored
+             "c1\t50000\t.\tA\t<NON_REF>\t.\t.\tXEND=60000\tGT\t0/0"]         # not an END field
+    plain = tmp_path / "b.g.vcf"
+    plain.write_text(hdr + "".join(x + "\n" for x in lines))
+    gz = tmp_path / "b.g.vcf.gz"
+    H.check(H.lib.fcsg_bgzip_tabix(str(plain).encode(), str(gz).encode()))
+    names, refs = H.parse_index(gzip.decompress((tmp_path / "b.g.vcf.gz.tbi").read_bytes()), b"TBI\x01")
+    bins, lin = refs[0]
+    ends = {101: 40000, 40001: 40010, 40011: 40013, 100: 100, 50000: 50000}
+    voffs = {int(line.split("\t")[1]): v for v, line in H.bgzf_text_with_voffsets(gz) if not line.startswith("#")}
+    for pos, end in ends.items():
+        b = H.reg2bin(pos - 1, end)
+        assert any(a <= voffs[pos] < e for a, e in bins[b]), (pos, b)
+    # a query at 30,000 (window 1) must start no later than the block at 101
+    assert lin[30000 >> 14] <= voffs[101] and lin[(40000 - 1) >> 14] <= voffs[101]
+    # the two-pass indexer (read back from the .gz) builds the same index
+    gz2 = tmp_path / "c.g.vcf.gz"
+    H.check(H.lib.fcsg_bgzf_compress_file(str(plain).encode(), str(gz2).encode()))
+    H.check(H.lib.fcsg_tabix(str(gz2).encode()))
+    assert gzip.decompress((tmp_path / "c.g.vcf.gz.tbi").read_bytes()) == \
+        gzip.decompress((tmp_path / "b.g.vcf.gz.tbi").read_bytes())

@@ -301,6 +301,32 @@ def test_long_haplotypes(gpu, hlen):
         assert used.sum() > 0, "the fp64 rescue must run on long haplotypes"
 
 
+@pytest.mark.parametrize("exact", [False, True])
+def test_read_longer_than_65535(gpu, exact):
+    """the streamed kernel packs R in 16 bits between stripes, so a
+    read of more than 65,535 bases goes to the grouped kernel.  The qualities
+    keep the likelihood finite and make it depend on rows past 65,536: row 1
+    opens from D (GCP 10), insertions are free elsewhere (ins GOP 0, GCP 0,
+    so matchToMatch = 0 and I carries row 1's M down), and 31 rows near
+    66,000 (GCP 3) halve I and reopen M — the sum is taken at row R."""
+    rng = np.random.default_rng(65536)
+    R, H = 70000, 120
+    hap = rng.choice(np.frombuffer(b"ACGT", np.uint8), H)
+    b = rng.choice(np.frombuffer(b"ACGT", np.uint8), R)
+    b[:H] = hap
+    bq = np.full(R, 30, np.uint8)
+    iq = np.zeros(R, np.uint8)
+    dq = np.full(R, 45, np.uint8)
+    gq = np.zeros(R, np.uint8)
+    gq[0] = 10
+    gq[66000:66031] = 3
+    short = rand_read(rng, 101)  # a normal pair beside it in the same batch
+    p = fcship.make_pairs([(b, bq, iq, dq, gq), short], [hap, mutate(rng, hap, 120)])
+    out = fcship.phmm_compute_pairs(p, exact=exact)
+    assert np.all(np.isfinite(out))
+    check_parity(p, out, exact)
+
+
 def test_unwritten_results_are_an_error(gpu, tmp_path):
     """a schedule that drops pairs (the round-1 null-stream memset
     race zeroed the class bounds) must fail loudly, not return garbage: the

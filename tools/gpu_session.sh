@@ -2,7 +2,7 @@
 # One bounded GPU session on the gpurun box: parity tests, smoke, bench, and
 # rocprofv3 kernel-trace / PMC passes.  Every GPU step has its own time limit
 # and the script stops at the first failing step (no retries).
-# usage: tools/gpu_session.sh TAG [tests] [smoke] [bench] [prof] [pmc]
+# usage: tools/gpu_session.sh TAG [info] [tests] [smoke] [bench] [prof] [pmc]
 set -u
 TAG=$1; shift
 ROOT=${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}
@@ -21,7 +21,8 @@ run() {  # name seconds cmd...
 }
 for step in "$@"; do
   case $step in
-    tests) run pytest_gpu 900 python -m pytest tests -m gpu -q -p no:cacheprovider ;;
+    info) run info 60 bash -c 'nproc; free -g; df -h /tmp /dev/shm "$0"; rocm-smi --showuse --showmemuse | head -20' "$ROOT" ;;
+    tests) run pytest_gpu 600 python -u -m pytest tests -m gpu -x -v -p no:cacheprovider --timeout 120 --timeout-method thread ;;
     smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench) run bench 900 python bench.py ;;
     benchq) run benchq 600 python bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-e2e ;;
