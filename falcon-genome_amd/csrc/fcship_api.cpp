@@ -841,7 +841,7 @@ int fcs_phmm_partition(const fcs_phmm_batch* b, int32_t n_slices, int64_t* cuts)
     cum[p] = run;
   }
   // the cut where the running cost first reaches k/n of the total
-  // (falcon-genome_amd/sharding.py balanced_slices, its test oracle)
+  // (tests/sharding.py balanced_slices, its test oracle)
   cuts[0] = 0;
   for (int32_t k = 1; k < n_slices; ++k) {
     int64_t c;

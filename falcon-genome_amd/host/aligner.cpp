@@ -1,12 +1,20 @@
 #include "aligner.h"
 
+#include <zlib.h>
+
 #include <algorithm>
 #include <cmath>
+#include <condition_variable>
 #include <cstring>
+#include <deque>
 #include <fstream>
 #include <future>
 #include <iostream>
 #include <map>
+#include <mutex>
+#include <queue>
+#include <set>
+#include <sstream>
 #include <thread>
 #include <unordered_map>
 
@@ -16,6 +24,7 @@
 #include "fcship.h"
 #include "intervals.h"
 #include "seedext.h"
+#include "workers.h"
 
 namespace fcsg {
 
@@ -633,108 +642,121 @@ AlignStats align_pairs(const Reference& ref, const KmerIndex& idx, const std::ve
   return st;
 }
 
-// ------------------------------------------------------------------ align command
+// ------------------------------------------------------------------ align jobs
 namespace {
 
-bool read_fastq(std::ifstream& in, std::string& name, std::string& seq, std::string& qual) {
-  std::string plus;
-  if (!std::getline(in, name)) return false;
-  if (name.empty() || name[0] != '@') throw formatError("FASTQ record does not start with '@'");
-  name = name.substr(1);
-  const size_t ws = name.find_first_of(" \t");
-  if (ws != std::string::npos) name.resize(ws);
-  if (name.size() > 2 && name[name.size() - 2] == '/') name.resize(name.size() - 2);  // /1, /2
-  if (!std::getline(in, seq) || !std::getline(in, plus) || !std::getline(in, qual))
-    throw formatError("truncated FASTQ record " + name);
-  if (qual.size() != seq.size()) throw formatError("FASTQ quality length differs for " + name);
-  return true;
+// FASTQ records from a plain or gzip-compressed file (zlib's gz reader passes
+// plain files through), names without '@', comments or /1 /2.
+class FastqReader {
+ public:
+  explicit FastqReader(const std::string& path) : path_(path) {
+    f_ = gzopen(path.c_str(), "rb");
+    if (!f_) throw fileNotFound(path);
+    gzbuffer(f_, 1 << 18);
+  }
+  ~FastqReader() {
+    if (f_) gzclose(f_);
+  }
+  FastqReader(const FastqReader&) = delete;
+  FastqReader& operator=(const FastqReader&) = delete;
+  bool next(std::string& name, std::string& seq, std::string& qual) {
+    if (!line(name)) return false;
+    if (name.empty() || name[0] != '@') throw formatError(path_ + ": FASTQ record does not start with '@'");
+    name.erase(0, 1);
+    const size_t ws = name.find_first_of(" \t");
+    if (ws != std::string::npos) name.resize(ws);
+    if (name.size() > 2 && name[name.size() - 2] == '/') name.resize(name.size() - 2);  // /1, /2
+    std::string plus;
+    if (!line(seq) || !line(plus) || !line(qual)) throw formatError(path_ + ": truncated FASTQ record " + name);
+    if (qual.size() != seq.size()) throw formatError(path_ + ": FASTQ quality length differs for " + name);
+    return true;
+  }
+
+ private:
+  bool line(std::string& out) {
+    out.clear();
+    char buf[4096];
+    for (;;) {
+      if (!gzgets(f_, buf, sizeof buf)) return !out.empty();
+      out += buf;
+      if (!out.empty() && out.back() == '\n') {
+        out.pop_back();
+        if (!out.empty() && out.back() == '\r') out.pop_back();
+        return true;
+      }
+    }
+  }
+  std::string path_;
+  gzFile f_ = nullptr;
+};
+
+// The FMD-index of a reference, built once per process and shared by the
+// read-group jobs of one run (bwa-flow loads its prebuilt index per run).
+std::shared_ptr<const KmerIndex> index_cached(const std::string& path, const Reference& ref, int k) {
+  static std::mutex mu;
+  static std::map<std::pair<std::string, int>, std::shared_ptr<const KmerIndex>> cache;
+  std::lock_guard<std::mutex> g(mu);
+  auto& e = cache[{path, k}];
+  if (!e) e = std::make_shared<const KmerIndex>(ref, k);
+  return e;
+}
+
+void add_stats(AlignStats& tot, const AlignStats& st) {
+  tot.reads += st.reads;
+  tot.mapped += st.mapped;
+  tot.proper += st.proper;
+  tot.rescued += st.rescued;
+  tot.seconds += st.seconds;
+  tot.gpu_seconds += st.gpu_seconds;
+  tot.seed_seconds += st.seed_seconds;
+  tot.extend_seconds += st.extend_seconds;
+  tot.pair_seconds += st.pair_seconds;
+  tot.record_seconds += st.record_seconds;
+  tot.ext_tasks += st.ext_tasks;
+  tot.global_tasks += st.global_tasks;
+  if (st.pe_pairs) tot.pe_pairs = st.pe_pairs, tot.pe_low = st.pe_low, tot.pe_high = st.pe_high,
+                   tot.pe_avg = st.pe_avg, tot.pe_std = st.pe_std;
 }
 
 }  // namespace
 
-int align_main(int argc, char** argv) {
-  std::string ref_path, fq1, fq2, output, rg = "sample", sp = "sample", pl = "illumina", lb = "sample";
-  bool force = false, disable_merge = false;
-  for (int i = 1; i < argc; ++i) {
-    const std::string a = argv[i];
-    auto val = [&]() -> std::string {
-      if (i + 1 >= argc) throw invalidParam(a + " needs a value");
-      return argv[++i];
-    };
-    if (a == "-h" || a == "--help") {
-      std::cerr << "'fcs-genome align' options:\n  -r, --ref arg\n  -1, --fastq1 arg\n  -2, --fastq2 arg\n"
-                   "  -o, --output arg\n  -R, --rg arg\n  -S, --sp arg\n  -P, --pl arg\n  -L, --lb arg\n"
-                   "  -l, --align-only\n  --disable-merge   write bwa.num_buckets sorted bucket BAMs "
-                   "(part-XXXXXX.bam + .bai + .bed) into the output directory\n  -f, --force\n";
-      throw helpRequest();
-    } else if (a == "-r" || a == "--ref") ref_path = val();
-    else if (a == "-1" || a == "--fastq1") fq1 = val();
-    else if (a == "-2" || a == "--fastq2") fq2 = val();
-    else if (a == "-o" || a == "--output") output = val();
-    else if (a == "-R" || a == "--rg") rg = val();
-    else if (a == "-S" || a == "--sp") sp = val();
-    else if (a == "-P" || a == "--pl") pl = val();
-    else if (a == "-L" || a == "--lb") lb = val();
-    else if (a == "-f" || a == "--force") force = true;
-    else if (a == "--disable-merge") disable_merge = true;
-    else if (a == "-l" || a == "--align-only") continue;
-    else throw invalidParam(a);
-  }
-  if (ref_path.empty()) throw invalidParam("--ref is required");
-  if (fq1.empty()) throw invalidParam("--fastq1 is required");
-  if (output.empty()) throw invalidParam("--output is required");
-  if (!is_regular_file(ref_path)) throw fileNotFound(ref_path);
-  if (!is_regular_file(fq1)) throw fileNotFound(fq1);
-  if (!fq2.empty() && !is_regular_file(fq2)) throw fileNotFound(fq2);
-  if (!force && path_exists(output)) throw invalidParam("output " + output + " exists (use -f)");
-  const std::vector<int> gpus = conf().gpu_devices();
-  if (gpus.empty()) throw failedCommand("[E::fcs-genome] no GPU visible (gpu.devices); the GPU path has no CPU fallback");
-
+AlignStats align_fastq(const AlignJob& job, const std::vector<int>& gpus, std::string& report) {
+  if (gpus.empty()) throw failedCommand("[E::fcs-genome align] no GPU visible (gpu.devices); the GPU path has no CPU fallback");
   const uint64_t t_start = now_us();
-  const Reference ref = load_fasta(ref_path);
-  AlignOptions opt;
-  opt.gpu = gpus[0];
-  opt.rg = rg;
-  opt.chunk_size = conf().get_int("bwa.chunk_size");
+  const auto ref_p = load_reference_cached(job.ref_path);
+  const Reference& ref = *ref_p;
+  AlignOptions base;
+  base.rg = job.rg;
+  base.chunk_size = conf().get_int("bwa.chunk_size");
+  const int nslot = (int)gpus.size();
   {
+    // bwa.nt host threads for the whole job, shared by the device slots
     const int nt = conf().get_int("bwa.nt");
-    opt.threads = nt > 0 ? nt : (int)std::min(16u, std::max(1u, std::thread::hardware_concurrency()));
+    const int all = nt > 0 ? nt : (int)std::min(16u, std::max(1u, std::thread::hardware_concurrency()));
+    base.threads = std::max(1, all / nslot);
   }
   const uint64_t t_ref = now_us();
-  const KmerIndex idx(ref, opt.k);
+  const auto idx_p = index_cached(job.ref_path, ref, base.k);
+  const KmerIndex& idx = *idx_p;
   const uint64_t t_idx = now_us();
-  std::vector<BamRecord> recs;
-  AlignStats tot;
-  auto add = [&](const AlignStats& st) {
-    tot.reads += st.reads;
-    tot.mapped += st.mapped;
-    tot.proper += st.proper;
-    tot.rescued += st.rescued;
-    tot.seconds += st.seconds;
-    tot.gpu_seconds += st.gpu_seconds;
-    tot.seed_seconds += st.seed_seconds;
-    tot.extend_seconds += st.extend_seconds;
-    tot.pair_seconds += st.pair_seconds;
-    tot.record_seconds += st.record_seconds;
-    tot.ext_tasks += st.ext_tasks;
-    tot.global_tasks += st.global_tasks;
-    if (st.pe_pairs) tot.pe_pairs = st.pe_pairs, tot.pe_low = st.pe_low, tot.pe_high = st.pe_high,
-                     tot.pe_avg = st.pe_avg, tot.pe_std = st.pe_std;
-  };
-  // FASTQ chunks are read on a second thread while the previous chunk aligns
+
+  // FASTQ chunks: read on one thread into a short queue, aligned by one host
+  // thread per device slot as they come; each chunk's records and statistics
+  // are kept under its index, so the merged result is the one-slot result.
   struct Chunk {
     std::vector<std::string> names, s1, q1, s2, q2;
   };
-  std::ifstream in1(fq1), in2;
-  if (!fq2.empty()) in2.open(fq2);
-  const size_t per_chunk = (size_t)std::max(1, fq2.empty() ? opt.chunk_size : opt.chunk_size / 2);
+  const bool paired = !job.fq2.empty();
+  FastqReader in1(job.fq1);
+  std::unique_ptr<FastqReader> in2;
+  if (paired) in2 = std::make_unique<FastqReader>(job.fq2);
+  const size_t per_chunk = (size_t)std::max(1, paired ? base.chunk_size / 2 : base.chunk_size);
   auto read_chunk = [&](Chunk& c) {
-    for (auto* v : {&c.names, &c.s1, &c.q1, &c.s2, &c.q2}) v->clear();
     std::string n1, a1, b1, n2, a2, b2;
     while (c.names.size() < per_chunk) {
-      const bool g1 = read_fastq(in1, n1, a1, b1);
-      if (!fq2.empty()) {  // paired: both files in lockstep
-        const bool g2 = read_fastq(in2, n2, a2, b2);
+      const bool g1 = in1.next(n1, a1, b1);
+      if (paired) {  // both files in lockstep
+        const bool g2 = in2->next(n2, a2, b2);
         if (g1 != g2) throw formatError("paired FASTQ files differ in read count");
         if (g1 && n1 != n2) throw formatError("paired FASTQ names differ: " + n1 + " vs " + n2);
         if (g1) c.s2.push_back(std::move(a2)), c.q2.push_back(std::move(b2));
@@ -745,19 +767,82 @@ int align_main(int argc, char** argv) {
       c.q1.push_back(std::move(b1));
     }
   };
-  Chunk cur, nxt;
-  read_chunk(cur);
-  while (!cur.names.empty()) {
-    auto ahead = std::async(std::launch::async, [&] { read_chunk(nxt); });
+  std::mutex mu;
+  std::condition_variable cv;
+  std::deque<std::pair<size_t, Chunk>> queue;
+  bool eof = false, stop = false;
+  std::exception_ptr err;
+  std::vector<std::vector<BamRecord>> results;
+  std::vector<AlignStats> chunk_stats;
+  auto fail = [&](std::exception_ptr e) {
+    std::lock_guard<std::mutex> g(mu);
+    if (!err) err = e;
+    stop = true;
+    cv.notify_all();
+  };
+  std::thread reader([&] {
     try {
-      if (fq2.empty()) add(align_reads(ref, idx, cur.names, cur.s1, cur.q1, opt, recs));
-      else add(align_pairs(ref, idx, cur.names, cur.s1, cur.q1, cur.s2, cur.q2, opt, recs));  // bwa's per-batch insert-size estimate
+      for (size_t k = 0;; ++k) {
+        Chunk c;
+        read_chunk(c);
+        std::unique_lock<std::mutex> lk(mu);
+        if (c.names.empty() || stop) break;
+        cv.wait(lk, [&] { return stop || queue.size() <= (size_t)nslot; });
+        if (stop) break;
+        queue.emplace_back(k, std::move(c));
+        cv.notify_all();
+      }
     } catch (...) {
-      ahead.wait();
-      throw;
+      fail(std::current_exception());
     }
-    ahead.get();
-    std::swap(cur, nxt);
+    std::lock_guard<std::mutex> g(mu);
+    eof = true;
+    cv.notify_all();
+  });
+  std::vector<std::thread> slots;
+  for (int s = 0; s < nslot; ++s)
+    slots.emplace_back([&, s] {
+      AlignOptions opt = base;
+      opt.gpu = gpus[s];
+      for (;;) {
+        std::pair<size_t, Chunk> item;
+        {
+          std::unique_lock<std::mutex> lk(mu);
+          cv.wait(lk, [&] { return stop || eof || !queue.empty(); });
+          if (stop || queue.empty()) return;
+          item = std::move(queue.front());
+          queue.pop_front();
+          cv.notify_all();
+        }
+        if (interrupted()) return fail(std::make_exception_ptr(interruptedError()));
+        try {
+          const Chunk& c = item.second;
+          std::vector<BamRecord> recs;
+          const AlignStats st = paired ? align_pairs(ref, idx, c.names, c.s1, c.q1, c.s2, c.q2, opt, recs)
+                                       : align_reads(ref, idx, c.names, c.s1, c.q1, opt, recs);
+          std::lock_guard<std::mutex> g(mu);
+          if (results.size() <= item.first) results.resize(item.first + 1), chunk_stats.resize(item.first + 1);
+          results[item.first] = std::move(recs);
+          chunk_stats[item.first] = st;
+        } catch (...) {
+          return fail(std::current_exception());
+        }
+      }
+    });
+  reader.join();
+  for (auto& t : slots) t.join();
+  if (err) std::rethrow_exception(err);
+  AlignStats tot;
+  for (const AlignStats& st : chunk_stats) add_stats(tot, st);  // chunk order: the last batch's insert size
+  std::vector<BamRecord> recs;
+  {
+    size_t n = 0;
+    for (const auto& v : results) n += v.size();
+    recs.reserve(n);
+    for (auto& v : results) {
+      for (BamRecord& r : v) recs.push_back(std::move(r));
+      std::vector<BamRecord>().swap(v);
+    }
   }
   const uint64_t t_aln = now_us();
   // coordinate order by packed keys (reference id as unsigned: unmapped last;
@@ -773,10 +858,10 @@ int align_main(int argc, char** argv) {
     h.lengths.push_back((int64_t)c.seq.size());
     h.text += "@SQ\tSN:" + c.name + "\tLN:" + std::to_string(c.seq.size()) + "\n";
   }
-  h.text += "@RG\tID:" + rg + "\tSM:" + sp + "\tPL:" + pl + "\tLB:" + lb + "\n";
+  h.text += "@RG\tID:" + job.rg + "\tSM:" + job.sample + "\tPL:" + job.platform + "\tLB:" + job.library + "\n";
   h.text += "@PG\tID:fcs-genome\tPN:fcs-genome align\n";
-  if (!disable_merge) {
-    BamWriter w(output, h);
+  if (!job.disable_merge) {
+    BamWriter w(job.output, h);
     w.index_on_close();
     for (const auto& o : order) w.write(recs[o.second]);
     w.close();
@@ -790,7 +875,7 @@ int align_main(int argc, char** argv) {
     std::vector<std::pair<std::string, int64_t>> dict;
     for (const Contig& c : ref.contigs) dict.emplace_back(c.name, (int64_t)c.seq.size());
     const auto buckets = partition_contigs(dict, nb, false);
-    create_dir(output);
+    create_dir(job.output);
     std::vector<std::vector<const BamRecord*>> per(nb);
     std::vector<std::vector<std::pair<int64_t, int64_t>>> span(ref.contigs.size());  // per contig: [lb, ub] -> bucket
     std::vector<std::vector<int>> span_b(ref.contigs.size());
@@ -815,30 +900,71 @@ int align_main(int argc, char** argv) {
       per[k].push_back(&r);
     }
     for (int k = 0; k < nb; ++k) {
-      const std::string bam = get_contig_fname(output, k, "bam");
+      const std::string bam = get_contig_fname(job.output, k, "bam");
       BamWriter w(bam, h);
       w.index_on_close();
       for (const BamRecord* r : per[k]) w.write(*r);
       w.close();
-      std::ofstream bed(get_contig_fname(output, k, "bed"));
+      std::ofstream bed(get_contig_fname(job.output, k, "bed"));
       for (const Interval& iv : buckets[k]) bed << iv.chrom << '\t' << iv.lb - 1 << '\t' << iv.ub << '\n';
     }
   }
-  std::cerr << "[fcs-genome align] " << tot.reads << " reads, " << tot.mapped << " mapped, " << tot.ext_tasks
-            << " extension tasks, " << tot.global_tasks << " global alignments, " << tot.seconds << " s (GPU calls "
-            << tot.gpu_seconds << " s)";
-  if (!fq2.empty())
-    std::cerr << "; pairs: " << tot.proper << " reads properly paired, " << tot.rescued << " mates rescued, insert "
-              << tot.pe_avg << " +- " << tot.pe_std << " [" << tot.pe_low << ", " << tot.pe_high << "] from "
-              << tot.pe_pairs << " pairs";
-  std::cerr << std::endl;
   const uint64_t t_end = now_us();
-  std::cerr << "[fcs-genome align] phases: reference " << (t_ref - t_start) / 1e6 << " s, FMD index "
-            << (t_idx - t_ref) / 1e6 << " s, FASTQ + alignment " << (t_aln - t_idx) / 1e6 << " s (alignment "
-            << tot.seconds << " s: seeding " << tot.seed_seconds << " s, extension " << tot.extend_seconds
-            << " s, pairing " << tot.pair_seconds << " s, records " << tot.record_seconds << " s), sort + BAM + index "
-            << (t_end - t_aln) / 1e6 << " s" << std::endl;
-  return 0;
+  std::ostringstream rep;
+  rep << "[fcs-genome align] " << tot.reads << " reads, " << tot.mapped << " mapped, " << tot.ext_tasks
+      << " extension tasks, " << tot.global_tasks << " global alignments, " << tot.seconds << " s (GPU calls "
+      << tot.gpu_seconds << " s)";
+  if (paired)
+    rep << "; pairs: " << tot.proper << " reads properly paired, " << tot.rescued << " mates rescued, insert "
+        << tot.pe_avg << " +- " << tot.pe_std << " [" << tot.pe_low << ", " << tot.pe_high << "] from " << tot.pe_pairs
+        << " pairs";
+  rep << "\n[fcs-genome align] read group " << job.rg << " on " << nslot << " device slot(s), " << results.size()
+      << " chunks; phases: reference " << (t_ref - t_start) / 1e6 << " s, FMD index " << (t_idx - t_ref) / 1e6
+      << " s, FASTQ + alignment " << (t_aln - t_idx) / 1e6 << " s (alignment thread-seconds " << tot.seconds
+      << ": seeding " << tot.seed_seconds << ", extension " << tot.extend_seconds << ", pairing " << tot.pair_seconds
+      << ", records " << tot.record_seconds << "), sort + BAM + index " << (t_end - t_aln) / 1e6 << " s\n";
+  report = rep.str();
+  return tot;
+}
+
+void merge_sorted_bams(const std::vector<std::string>& inputs, const std::string& output) {
+  if (inputs.empty()) throw invalidParam("merge_sorted_bams: no input");
+  std::vector<std::unique_ptr<BamReader>> rd;
+  for (const std::string& p : inputs) rd.push_back(std::make_unique<BamReader>(p));
+  BamHeader h = rd[0]->header();
+  for (const auto& r : rd)
+    if (r->header().names != h.names || r->header().lengths != h.lengths)
+      throw formatError("merge: " + output + " inputs have different reference dictionaries");
+  // header: the first input's lines with the @RG lines of every input after its @SQ lines
+  std::string head, rgs, tail;
+  std::set<std::string> seen;
+  for (size_t i = 0; i < rd.size(); ++i) {
+    std::istringstream ss(rd[i]->header().text);
+    for (std::string line; std::getline(ss, line);) {
+      if (line.rfind("@RG", 0) == 0) {
+        if (seen.insert(line).second) rgs += line + "\n";
+      } else if (i == 0) {
+        (line.rfind("@HD", 0) == 0 || line.rfind("@SQ", 0) == 0 ? head : tail) += line + "\n";
+      }
+    }
+  }
+  h.text = head + rgs + tail;
+  BamWriter w(output, h);
+  w.index_on_close();
+  // k-way merge by (reference as unsigned: unmapped last, position), ties by input order
+  auto key = [](const BamRecord& r) { return ((uint64_t)(uint32_t)r.ref_id << 32) | ((uint32_t)r.pos ^ 0x80000000u); };
+  std::vector<BamRecord> cur(rd.size());
+  typedef std::pair<uint64_t, size_t> Item;
+  std::priority_queue<Item, std::vector<Item>, std::greater<Item>> pq;
+  for (size_t i = 0; i < rd.size(); ++i)
+    if (rd[i]->next(cur[i])) pq.push({key(cur[i]), i});
+  while (!pq.empty()) {
+    const size_t i = pq.top().second;
+    pq.pop();
+    w.write(cur[i]);
+    if (rd[i]->next(cur[i])) pq.push({key(cur[i]), i});
+  }
+  w.close();
 }
 
 }  // namespace fcsg

@@ -82,4 +82,26 @@ AlignStats align_pairs(const Reference& ref, const KmerIndex& idx, const std::ve
                        const std::vector<std::string>& seqs2, const std::vector<std::string>& quals2,
                        const AlignOptions& opt, std::vector<BamRecord>& out);
 
+// One read group of `fcs-genome align` (the work of one reference
+// BWAWorker: /root/reference/src/workers/BWAWorker.cpp:94-186).
+struct AlignJob {
+  std::string ref_path, fq1, fq2, output;  // fq2 empty: single-end
+  std::string rg = "sample", sample = "sample", platform = "illumina", library = "sample";
+  bool disable_merge = false;  // bwa.num_buckets sorted bucket BAMs (+ .bai, .bed) in the directory `output`
+};
+
+// Aligns one read group on the device slots `gpus`: FASTQ chunks
+// (bwa.chunk_size reads) go to the slots as they free up, one host thread per
+// slot; every chunk's records are kept under the chunk's index and merged in
+// chunk order, so the output is the same for any slot list.  Writes the
+// sorted BAM + BAI (or the bucket directory) and returns the statistics;
+// `report` receives the summary lines.
+AlignStats align_fastq(const AlignJob& job, const std::vector<int>& gpus, std::string& report);
+
+// k-way merge of coordinate-sorted BAMs with the same reference dictionary
+// into one sorted BAM + BAI; the header keeps the first input's lines and the
+// @RG lines of every input (the reference's sambamba merge step,
+// src/worker-align.cpp:218-246).
+void merge_sorted_bams(const std::vector<std::string>& inputs, const std::string& output);
+
 }  // namespace fcsg

@@ -17,7 +17,9 @@
 #include "fmindex.h"
 #include "gatk_prep.h"
 #include "seedext.h"
+#include "aligner.h"
 #include "intervals.h"
+#include "sample_sheet.h"
 #include "vcf.h"
 
 using namespace fcsg;
@@ -55,6 +57,26 @@ int fcsg_prepare_read(const char* bases, const uint8_t* quals, int len, const ch
     std::memcpy(dq, pr.del_q.data(), len);
     std::memcpy(gcp, pr.gcp.data(), len);
   });
+}
+
+// "sample\tfastq1\tfastq2\trg\tplatform\tlibrary\n" lines of a sample sheet
+// (file or FASTQ folder), samples in name order, read groups in sheet order.
+int fcsg_sample_sheet(const char* path, char* buf, int cap) {
+  int rc = 0;
+  const int g = guard([&] {
+    std::string s;
+    for (const auto& [sample, list] : read_sample_sheet(path))
+      for (const SampleDetails& d : list)
+        s += sample + "\t" + d.fastqR1 + "\t" + d.fastqR2 + "\t" + d.ReadGroup + "\t" + d.Platform + "\t" +
+             d.LibraryID + "\n";
+    rc = copy_out(s, buf, cap);
+  });
+  return g ? g : rc;
+}
+
+// merge_sorted_bams (align's per-sample merge of read-group BAMs).
+int fcsg_merge_bams(const char* const* inputs, int n, const char* output) {
+  return guard([&] { merge_sorted_bams(std::vector<std::string>(inputs, inputs + n), output); });
 }
 
 // "shard\tchrom\tlb\tub\n" lines of the init_contig_intv partition of a .dict.
@@ -218,7 +240,8 @@ int fcsg_bam_to_text(const char* bam, const char* out) {
   });
 }
 
-// SAM-like text (name flag ref_id pos mapq cigar seq qual) → BAM with the library's writer.
+// SAM-like text (name flag ref_id pos mapq cigar seq qual; leading '@' lines
+// are header lines) → BAM with the library's writer.
 int fcsg_text_to_bam(const char* text, const char* bam, const char* names_csv, const char* lengths_csv) {
   return guard([&] {
     BamHeader h;
@@ -235,8 +258,13 @@ int fcsg_text_to_bam(const char* text, const char* bam, const char* names_csv, c
     }
     for (size_t i = 0; i < h.names.size(); ++i)
       h.text += "@SQ\tSN:" + h.names[i] + "\tLN:" + std::to_string(h.lengths[i]) + "\n";
-    BamWriter w(bam, h);
     std::string body = read_file(text);
+    while (!body.empty() && body[0] == '@') {  // leading header lines (@RG, @PG) join the header
+      const size_t e = std::min(body.find('\n'), body.size());
+      h.text += body.substr(0, e) + "\n";
+      body.erase(0, e + 1);
+    }
+    BamWriter w(bam, h);
     size_t p = 0;
     while (p < body.size()) {
       const size_t e = std::min(body.find('\n', p), body.size());

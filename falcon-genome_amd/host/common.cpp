@@ -2,6 +2,7 @@
 
 #include <dirent.h>
 #include <sys/stat.h>
+#include <sys/statvfs.h>
 #include <unistd.h>
 
 #include <algorithm>
@@ -80,6 +81,17 @@ std::vector<std::string> list_dir(const std::string& p, const std::string& suffi
   }
   std::sort(out.begin(), out.end());
   return out;
+}
+
+uint64_t file_size(const std::string& p) {
+  struct stat st;
+  return ::stat(p.c_str(), &st) == 0 ? (uint64_t)st.st_size : 0;
+}
+
+uint64_t available_space(const std::string& dir) {
+  struct statvfs v;
+  if (::statvfs(dir.c_str(), &v) != 0) return UINT64_MAX;  // unknown: do not block the run
+  return (uint64_t)v.f_bavail * v.f_frsize;
 }
 
 std::string read_file(const std::string& p) {

@@ -126,6 +126,8 @@ void create_dir(const std::string& p);   // mkdir -p
 void remove_path(const std::string& p);  // rm -rf
 std::vector<std::string> list_dir(const std::string& p, const std::string& suffix = "");
 std::string read_file(const std::string& p);
+uint64_t file_size(const std::string& p);         // 0 if absent
+uint64_t available_space(const std::string& dir);  // bytes free to this user (statvfs)
 void write_file(const std::string& p, const std::string& data);
 
 }  // namespace fcsg

@@ -4,8 +4,9 @@
 // src/worker-align.cpp:29-42), config keys (`conf`) and exit codes
 // (src/main.cpp:165-240: help 0, bad option 1/2, missing file 3, failed
 // stage 4, other error -1), plus `synth` for the synthetic C1/C4/C5 inputs.
-#include <pthread.h>
 #include <unistd.h>
+
+#include <cerrno>
 
 #include <csignal>
 #include <cstring>
@@ -21,12 +22,11 @@
 #include "executor.h"
 #include "fcship.h"
 #include "intervals.h"
+#include "sample_sheet.h"
 #include "synth.h"
 #include "workers.h"
 
 namespace fcsg {
-
-int align_main(int argc, char** argv);  // align.cpp
 
 namespace {
 
@@ -248,6 +248,99 @@ int mutect2_main(int argc, char** argv) {
   return 0;
 }
 
+// `fcs-genome align` (reference src/worker-align.cpp:19-256): a single read
+// group (-1/-2, -R/-S/-P/-L) or a sample sheet (-F; file or FASTQ folder).
+// One BWAWorker per (sample, read group), each in its own stage and on every
+// GPU slot; a sample with several read groups gets a merge stage.  The
+// reference's sambamba INDEX stage is not needed: BAMs are written with their
+// index.  Without -F a single-end run (-1 only) is accepted as well.
+int align_main(int argc, char** argv) {
+  Args a;
+  common_opts(a);
+  a.add("ref", "r", false, true, "reference genome path");
+  a.add("fastq1", "1", false, false, "input pair-end fastq file (plain or .gz)");
+  a.add("fastq2", "2", false, false, "input pair-end fastq file (plain or .gz)");
+  a.add("output", "o", false, true,
+        "output BAM file (with --disable-merge a directory of bucket BAMs; with --sample_sheet the folder of the "
+        "samples' outputs)");
+  a.add("sample_sheet", "F", false, false, "sample sheet (#sample_id,fastq1,fastq2,rg,platform_id,library_id) or "
+        "folder of *_1.fastq.gz / *_2.fastq.gz");
+  a.add("rg", "R", false, false, "read group id ('ID' in BAM header)");
+  a.add("sp", "S", false, false, "sample id ('SM' in BAM header)");
+  a.add("pl", "P", false, false, "platform id ('PL' in BAM header)");
+  a.add("lb", "L", false, false, "library id ('LB' in BAM header)");
+  a.add("align-only", "l", true, false, "skip mark duplicates");
+  a.add("disable-merge", "", true, false, "give bucket bams instead of the whole bam");
+  try {
+    a.parse(argc, argv);
+  } catch (helpRequest&) {
+    std::cerr << "'fcs-genome align' options:\n" << a.help();
+    throw;
+  }
+  const std::string ref = a.get("ref"), sheet = a.get("sample_sheet"), fq1 = a.get("fastq1"), fq2 = a.get("fastq2");
+  const std::string output = a.get("output");
+  const bool force = a.has("force"), disable_merge = a.has("disable-merge");
+  const std::vector<std::string> extra = a.all("extra-options");
+  SampleSheetMap samples;
+  if (sheet.empty()) {
+    if (fq1.empty()) throw invalidParam("Either --sample_sheet or --fastq1,fastq2 needs to be specified");
+    SampleDetails d;
+    d.fastqR1 = fq1;
+    d.fastqR2 = fq2;
+    d.ReadGroup = a.get("rg", "sample");
+    d.Platform = a.get("pl", "illumina");
+    d.LibraryID = a.get("lb", "sample");
+    samples[a.get("sp", "sample")].push_back(d);
+  } else {
+    if (!fq1.empty() || !fq2.empty())
+      throw invalidParam("--sample_sheet and --fastq1,fastq2 cannot be specified at the same time");
+    samples = read_sample_sheet(sheet);
+  }
+  if (!is_regular_file(ref)) throw fileNotFound(ref);
+  if (sheet.empty() && !disable_merge) {
+    if (!force && path_exists(output)) throw invalidParam("output " + output + " exists (use -f)");
+  } else {
+    if (path_exists(output) && !is_directory(output))
+      throw fileNotFound("Output path " + output + " is not a directory");
+    create_dir(output);
+  }
+  const std::vector<int> gpus = slots();
+  const std::string temp_dir = conf().temp_dir() + "/align";
+  create_dir(temp_dir);
+  for (const auto& [sample_id, list] : samples) {
+    // one Executor per sample (the reference runs it inside the sample loop);
+    // one task at a time, each task on every GPU slot
+    Executor ex("align", 1, gpus);
+    const std::string merge_dir = temp_dir + "/" + sample_id + "merge";
+    create_dir(merge_dir);
+    const std::string merged = sheet.empty() ? output : output + "/" + sample_id + ".bam";
+    std::vector<std::string> rg_out;
+    for (const SampleDetails& d : list) {
+      const std::string out_rg = list.size() == 1 ? merged : merge_dir + "/" + sample_id + "_" + d.ReadGroup + ".bam";
+      rg_out.push_back(out_rg);
+      ex.addTask(std::make_shared<BWAWorker>(ref, d.fastqR1, d.fastqR2, out_rg, extra, sample_id, d.ReadGroup,
+                                             d.Platform, d.LibraryID, !disable_merge, force || list.size() > 1, gpus),
+                 sample_id, true);
+    }
+    if (list.size() > 1) {
+      if (!disable_merge) {
+        ex.addTask(std::make_shared<MergeBamWorker>(rg_out, merged, force), sample_id, true);
+      } else {  // bucket i of every read group -> bucket i of the sample (worker-align.cpp:226-246)
+        create_dir(merged);
+        const int nb = std::max(1, conf().get_int("bwa.num_buckets"));
+        for (int i = 0; i < nb; ++i) {
+          std::vector<std::string> in;
+          for (const std::string& r : rg_out) in.push_back(get_contig_fname(r, i, "bam"));
+          ex.addTask(std::make_shared<MergeBamWorker>(in, get_contig_fname(merged, i, "bam"), true), sample_id,
+                     i == 0);
+        }
+      }
+    }
+    ex.run();
+  }
+  return 0;
+}
+
 int synth_main(int argc, char** argv) {
   Args a;
   a.add("output", "o", false, true, "output directory");
@@ -310,24 +403,42 @@ int synth_main(int argc, char** argv) {
 }
 
 // SIGINT / SIGTERM / SIGHUP (the reference's sigint_handler, src/main.cpp:43-54):
-// blocked in every thread and taken by one sigwait thread, which announces the
-// interrupt and sets the flag the Executor and the workers poll; the run then
-// unwinds, removes its temp dir and exits 128 + signal.  A second signal exits
-// at once.
+// an async-signal-safe handler writes the signal number to a pipe, and a
+// watcher thread announces the interrupt and sets the flag the Executor and
+// the workers poll; the run then unwinds, removes its temp dir and exits
+// 128 + signal.  A second signal exits at once.  No signal is blocked, so the
+// threads of the HIP runtime and of a profiler (rocprofv3) see the process's
+// signals as they would without fcs-genome's handling (round 2 blocked the
+// three signals in every thread, and a profiled run hung at exit).
+int g_sig_pipe[2] = {-1, -1};
+volatile sig_atomic_t g_sig_seen = 0;
+
+extern "C" void on_signal(int sig) {
+  if (g_sig_seen) _exit(128 + sig);
+  g_sig_seen = sig;
+  const unsigned char b = (unsigned char)sig;
+  if (write(g_sig_pipe[1], &b, 1) < 0) _exit(128 + sig);
+}
+
 void start_signal_thread() {
-  sigset_t set;
-  sigemptyset(&set);
-  sigaddset(&set, SIGINT);
-  sigaddset(&set, SIGTERM);
-  sigaddset(&set, SIGHUP);
-  pthread_sigmask(SIG_BLOCK, &set, nullptr);
-  std::thread([set] {
-    int sig = 0;
-    if (sigwait(&set, &sig) != 0) return;
+  if (pipe(g_sig_pipe) != 0) return;
+  std::thread([] {
+    unsigned char b = 0;
+    for (;;) {
+      const ssize_t n = read(g_sig_pipe[0], &b, 1);
+      if (n == 1) break;
+      if (n < 0 && errno == EINTR) continue;
+      return;
+    }
     std::cerr << "[fcs-genome] Caught interrupt, cleaning up..." << std::endl;
-    set_interrupted(sig);
-    if (sigwait(&set, &sig) == 0) _exit(128 + sig);
+    set_interrupted((int)b);
   }).detach();
+  struct sigaction sa;
+  std::memset(&sa, 0, sizeof sa);
+  sa.sa_handler = on_signal;
+  sigemptyset(&sa.sa_mask);
+  sa.sa_flags = SA_RESTART;
+  for (int sig : {SIGINT, SIGTERM, SIGHUP}) sigaction(sig, &sa, nullptr);
 }
 
 int print_help() {
@@ -359,7 +470,7 @@ int main(int argc, char** argv) {
     const size_t k = self.find_last_of('/');
     root = k == std::string::npos ? "." : self.substr(0, k) + "/..";
   }
-  start_signal_thread();  // before any other thread exists, so all inherit the mask
+  start_signal_thread();
   try {
     conf().init(root);
     if (cmd == "htc") ret = htc_main(argc - 1, argv + 1);

@@ -1,7 +1,10 @@
 #include "workers.h"
 
+#include <iostream>
 #include <map>
 #include <mutex>
+
+#include "aligner.h"
 
 #include "common.h"
 #include "config.h"
@@ -188,6 +191,81 @@ TabixWorker::TabixWorker(std::string path) : Worker(1, 1, {}, "tabix"), path_(st
 
 int TabixWorker::run(TaskContext&) {
   tabix_index_vcf(path_);
+  return 0;
+}
+
+// ------------------------------------------------------------------ align
+BWAWorker::BWAWorker(std::string ref_path, std::string fq1_path, std::string fq2_path, std::string output_path,
+                     std::vector<std::string> extra_opts, std::string sample_id, std::string read_group,
+                     std::string platform_id, std::string library_id, bool flag_merge_bams, bool flag_f,
+                     std::vector<int> gpus)
+    : Worker(1, 1, std::move(extra_opts), "bwa mem"),
+      ref_path_(std::move(ref_path)),
+      fq1_path_(std::move(fq1_path)),
+      fq2_path_(std::move(fq2_path)),
+      output_path_(std::move(output_path)),
+      sample_id_(std::move(sample_id)),
+      read_group_(std::move(read_group)),
+      platform_id_(std::move(platform_id)),
+      library_id_(std::move(library_id)),
+      flag_merge_bams_(flag_merge_bams),
+      flag_f_(flag_f),
+      gpus_(std::move(gpus)) {}
+
+void BWAWorker::check() {
+  if (flag_merge_bams_ && !flag_f_ && path_exists(output_path_))
+    throw invalidParam("output " + output_path_ + " exists (use -f)");
+  if (sample_id_.empty() || read_group_.empty() || platform_id_.empty() || library_id_.empty())
+    throw invalidParam("Invalid @RG info");
+  for (const std::string* p : {&ref_path_, &fq1_path_})
+    if (!is_regular_file(*p)) throw fileNotFound(*p);
+  if (!fq2_path_.empty() && !is_regular_file(fq2_path_)) throw fileNotFound(fq2_path_);
+  // temporary storage >= 3x the FASTQ input (BWAWorker.cpp:70-91)
+  const uint64_t need = 3 * (file_size(fq1_path_) + (fq2_path_.empty() ? 0 : file_size(fq2_path_)));
+  const std::string tmp = conf().temp_dir();
+  const size_t k = tmp.find_last_of('/');
+  const uint64_t avail = available_space(k == std::string::npos ? "." : k == 0 ? "/" : tmp.substr(0, k));
+  if (avail < need) {
+    std::cerr << "[fcs-genome] ERROR: Not enough space in temporary storage. The size of the temporary folder "
+                 "should be at least 3 times the size of input FASTQ files"
+              << std::endl;
+    throw silentExit();
+  }
+}
+
+int BWAWorker::run(TaskContext& ctx) {
+  AlignJob job;
+  job.ref_path = ref_path_;
+  job.fq1 = fq1_path_;
+  job.fq2 = fq2_path_;
+  job.output = output_path_;
+  job.rg = read_group_;
+  job.sample = sample_id_;
+  job.platform = platform_id_;
+  job.library = library_id_;
+  job.disable_merge = !flag_merge_bams_;
+  std::string report;
+  align_fastq(job, gpus_, report);
+  if (ctx.log) std::fputs(report.c_str(), ctx.log);
+  std::cerr << report << std::flush;
+  return 0;
+}
+
+MergeBamWorker::MergeBamWorker(std::vector<std::string> inputs, std::string output, bool flag_f)
+    : Worker(1, 1, {}, "Merge BAM"), inputs_(std::move(inputs)), output_(std::move(output)), flag_f_(flag_f) {}
+
+void MergeBamWorker::check() {
+  if (inputs_.empty()) throw invalidParam("no BAM to merge into " + output_);
+  if (!flag_f_ && path_exists(output_)) throw invalidParam("output " + output_ + " exists (use -f)");
+}
+
+int MergeBamWorker::run(TaskContext&) {
+  for (const std::string& p : inputs_)
+    if (!is_regular_file(p)) throw fileNotFound(p);
+  merge_sorted_bams(inputs_, output_);
+  const std::string bed_in = inputs_[0].substr(0, inputs_[0].size() - 4) + ".bed";
+  if (inputs_[0].size() > 4 && is_regular_file(bed_in))
+    write_file(output_.substr(0, output_.size() - 4) + ".bed", read_file(bed_in));
   return 0;
 }
 

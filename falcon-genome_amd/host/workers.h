@@ -93,6 +93,43 @@ class TabixWorker : public Worker {
   std::string path_;
 };
 
+// One read group of `fcs-genome align` (reference BWAWorker,
+// src/workers/BWAWorker.cpp:17-186, run per (sample, RG) by
+// src/worker-align.cpp:168-183).  check(): @RG fields non-empty, inputs
+// present, the output free (unless -f) and temp space >= 3x the FASTQ
+// (BWAWorker.cpp:48-92); run(): align_fastq on every GPU slot of the run
+// instead of bwa-flow on the FPGA.
+class BWAWorker : public Worker {
+ public:
+  BWAWorker(std::string ref_path, std::string fq1_path, std::string fq2_path, std::string output_path,
+            std::vector<std::string> extra_opts, std::string sample_id, std::string read_group,
+            std::string platform_id, std::string library_id, bool flag_merge_bams, bool flag_f,
+            std::vector<int> gpus);
+  void check() override;
+  int run(TaskContext& ctx) override;
+
+ private:
+  std::string ref_path_, fq1_path_, fq2_path_, output_path_, sample_id_, read_group_, platform_id_, library_id_;
+  bool flag_merge_bams_, flag_f_;
+  std::vector<int> gpus_;
+};
+
+// Merges coordinate-sorted BAMs into one sorted, indexed BAM (the reference's
+// SambambaWorker MERGE action, src/workers/SambambaWorker.cpp, used by
+// src/worker-align.cpp:218-246 for samples with several read groups); a
+// bucket's .bed region file is carried over when the inputs have one.
+class MergeBamWorker : public Worker {
+ public:
+  MergeBamWorker(std::vector<std::string> inputs, std::string output, bool flag_f);
+  void check() override;
+  int run(TaskContext& ctx) override;
+
+ private:
+  std::vector<std::string> inputs_;
+  std::string output_;
+  bool flag_f_;
+};
+
 // Loads libfcship's per-device tables on every GPU slot before the shard
 // tasks start (the role the Blaze NAM daemon plays for the FPGA:
 // src/worker-htc.cpp:100-112).  Run by a BackgroundExecutor.

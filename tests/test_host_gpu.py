@@ -209,6 +209,52 @@ def test_align_paired_end(gpu, tmp_path):
     assert resc_ok >= 0.8 * len(damaged), (resc_ok, len(damaged))
 
 
+def test_align_sample_sheet_over_two_slots(gpu, tmp_path):
+    """`align -F` runs one BWAWorker per (sample, read group)
+    under the Executor, then merges the sample's read groups; FASTQ chunks of
+    a read group are dealt over every GPU slot.  Two slots (both device 0 —
+    the dealing is the same over two devices) with small chunks give the same
+    BAM as one slot, byte for byte; both @RG lines are in the header and every
+    read is in the merged BAM once.  One read group's FASTQs are gzipped."""
+    import gzip
+    import shutil
+    d = tmp_path / "fq"
+    p = H.run_cli("synth", "-o", d, "-c", "chr1:300000", "-x", "12", "--paired", "350", "--seed", "5", "--no-fastq",
+                  env=ENV, cwd=tmp_path, timeout=600)
+    assert p.returncode == 0, p.stderr[-2000:]
+    halves = {}
+    for m in (1, 2):
+        lines = open(d / f"sample_{m}.fastq").read().splitlines(keepends=True)
+        n = len(lines) // 8 * 4
+        halves[m] = ("".join(lines[:n]), "".join(lines[n:]))
+    for m in (1, 2):
+        (d / f"A_{m}.fastq").write_text(halves[m][0])
+        with gzip.open(d / f"B_{m}.fastq.gz", "wt") as f:
+            f.write(halves[m][1])
+    sheet = tmp_path / "sheet.csv"
+    sheet.write_text("#sample_id,fastq1,fastq2,rg,platform_id,library_id\n"
+                     f"S,{d}/A_1.fastq,{d}/A_2.fastq,rgA,illumina,libA\n"
+                     f"S,{d}/B_1.fastq.gz,{d}/B_2.fastq.gz,rgB,illumina,libB\n")
+    outs = {}
+    for devs in ("0", "0,0"):
+        o = tmp_path / f"out_{devs.replace(',', '_')}"
+        env = dict(ENV, FCS_GPU_DEVICES=devs, FCS_BWA_CHUNK_SIZE="4000")
+        p = H.run_cli("align", "-r", d / "ref.fasta", "-F", sheet, "-o", o, env=env, cwd=tmp_path)
+        assert p.returncode == 0, p.stderr[-3000:]
+        assert ("on 2 device slot(s)" in p.stderr) == (devs == "0,0"), p.stderr[-2000:]
+        assert os.path.exists(o / "S.bam.bai")
+        outs[devs] = (o / "S.bam").read_bytes()
+    assert outs["0"] == outs["0,0"]
+    names, _, recs = H.read_bam(tmp_path / "out_0" / "S.bam")
+    text = gzip.decompress(outs["0"])
+    assert b"@RG\tID:rgA\tSM:S\tPL:illumina\tLB:libA" in text and b"@RG\tID:rgB" in text
+    n_reads = sum(1 for _ in open(d / "sample_1.fastq")) // 4 * 2
+    assert len(recs) == n_reads and len({(r["name"], r["flag"] & 0xC0) for r in recs}) == n_reads
+    keys = [((r["ref_id"] & 0xFFFFFFFF), r["pos"]) for r in recs]
+    assert keys == sorted(keys)
+    shutil.rmtree(d)
+
+
 def test_htc_gpu_slots_do_not_change_calls(gpu, data, tmp_path):
     """Shards dealt over two GPU slots (both on device 0 here — the dealing
     rule is the same as over two devices) and more concurrent tasks give the

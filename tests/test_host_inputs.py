@@ -3,6 +3,7 @@ BamInput directory mode (reference src/BamInput.cpp:27-149), region files
 (BED / GATK interval lists) and GATK's -isr INTERSECTION of several -L sets,
 the GVCF GQ bands, and SIGINT teardown (reference src/main.cpp:43-54)."""
 import ctypes as C
+import gzip
 import os
 import signal
 import subprocess
@@ -137,3 +138,69 @@ def test_sigint_tears_down(tmp_path):
     assert p.returncode == 128 + signal.SIGINT, (p.returncode, err[-2000:])
     assert "Caught interrupt, cleaning up..." in err
     assert not tmp.exists()
+
+
+# ------------------------------------------------------------ align inputs
+def _sheet(path):
+    buf = C.create_string_buffer(1 << 16)
+    H.check(H.lib.fcsg_sample_sheet(str(path).encode(), buf, len(buf)))
+    return [ln.split("\t") for ln in buf.value.decode().splitlines()]
+
+
+def test_sample_sheet_file(tmp_path):
+    """`align -F` sheet (reference src/SampleSheet.cpp:40-121): the '#'
+    header names the columns in any order; rows of one sample are its read
+    groups in sheet order; a row with a different field count is an error."""
+    f = tmp_path / "s.csv"
+    f.write_text("#sample_id,rg,fastq1,fastq2,platform_id,library_id\n"
+                 "NA2,rgA,/d/a_1.fq,/d/a_2.fq,illumina,libA\n"
+                 "NA1,rgB,/d/b_1.fq,/d/b_2.fq,illumina,libB\n"
+                 "NA2,rgC,/d/c_1.fq,/d/c_2.fq,ILLUMINA,libC\n")
+    assert _sheet(f) == [["NA1", "/d/b_1.fq", "/d/b_2.fq", "rgB", "illumina", "libB"],
+                         ["NA2", "/d/a_1.fq", "/d/a_2.fq", "rgA", "illumina", "libA"],
+                         ["NA2", "/d/c_1.fq", "/d/c_2.fq", "rgC", "ILLUMINA", "libC"]]
+    bad = tmp_path / "bad.csv"
+    bad.write_text("#sample_id,fastq1,fastq2,rg,platform_id,library_id\nNA1,/a,/b,rg\n")
+    buf = C.create_string_buffer(1024)
+    assert H.lib.fcsg_sample_sheet(str(bad).encode(), buf, len(buf)) < 0
+    assert "inconsistent" in H.lib.fcsg_last_error().decode()
+    nohdr = tmp_path / "nohdr.csv"
+    nohdr.write_text("sample_id,fastq1\nNA1,/a\n")
+    assert H.lib.fcsg_sample_sheet(str(nohdr).encode(), buf, len(buf)) < 0
+
+
+def test_sample_sheet_folder(tmp_path):
+    """A folder of <sample>_..._1.fastq.gz / _2.fastq.gz pairs (src/SampleSheet.cpp:123-200)."""
+    for n in ("S1_L001_1.fastq.gz", "S1_L001_2.fastq.gz", "S1_L002_1.fastq.gz", "S1_L002_2.fastq.gz",
+              "S2_L001_1.fastq.gz", "S2_L001_2.fastq.gz", "notes.txt"):
+        (tmp_path / n).write_bytes(b"")
+    got = _sheet(tmp_path)
+    d = str(tmp_path)
+    assert got == [["S1", d + "/S1_L001_1.fastq.gz", d + "/S1_L001_2.fastq.gz", "RG-S1_0000", "Illumina", "LIBS1_00"],
+                   ["S1", d + "/S1_L002_1.fastq.gz", d + "/S1_L002_2.fastq.gz", "RG-S1_0101", "Illumina", "LIBS1_01"],
+                   ["S2", d + "/S2_L001_1.fastq.gz", d + "/S2_L001_2.fastq.gz", "RG-S2_0000", "Illumina", "LIBS2_00"]]
+
+
+def test_merge_sorted_bams(tmp_path):
+    """align's per-sample merge of read-group BAMs: records in coordinate
+    order (unmapped last, ties by input order), the @RG lines of every input,
+    and an index identical to one built by reading the merged file back."""
+    rows = [["a1\t0\t0\t10\t60\t5M\tACGTA\t*", "a2\t0\t0\t40\t60\t5M\tACGTA\t*", "a3\t16\t1\t5\t60\t5M\tACGTA\t*",
+             "a4\t4\t-1\t-1\t0\t*\tACGTA\t*"],
+            ["b1\t0\t0\t10\t60\t5M\tACGTA\t*", "b2\t0\t0\t20\t60\t5M\tACGTA\t*", "b3\t0\t1\t1\t60\t5M\tACGTA\t*"]]
+    ins = []
+    for k, rs in enumerate(rows):
+        t = tmp_path / f"in{k}.txt"
+        t.write_text(f"@RG\tID:rg{k}\tSM:s\n" + "\n".join(rs) + "\n")
+        b = tmp_path / f"in{k}.bam"
+        H.check(H.lib.fcsg_text_to_bam(str(t).encode(), str(b).encode(), b"c1,c2", b"1000,500"))
+        ins.append(str(b).encode())
+    out = tmp_path / "m.bam"
+    H.check(H.lib.fcsg_merge_bams((C.c_char_p * 2)(*ins), 2, str(out).encode()))
+    names, lens, recs = H.read_bam(out)
+    assert [r["name"] for r in recs] == ["a1", "b1", "b2", "a2", "b3", "a3", "a4"]
+    text = gzip.decompress(out.read_bytes())
+    assert b"@RG\tID:rg0" in text and b"@RG\tID:rg1" in text
+    on_write = (tmp_path / "m.bam.bai").read_bytes()
+    H.check(H.lib.fcsg_bam_index(str(out).encode()))
+    assert (tmp_path / "m.bam.bai").read_bytes() == on_write
