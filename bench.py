@@ -494,6 +494,14 @@ def launch_ranks(n, dry):
     sys.exit(rc)
 
 
+def load_fcship():
+    """Imports the C-ABI binding (after torch: one HIP runtime per process)."""
+    global fcship
+    import fcship as _fcship
+    fcship = _fcship
+    return fcship
+
+
 def dry_step(args):
     """CPU stand-in for the PairHMM pass in --dry-run: a fixed amount of numpy work."""
     a = np.random.default_rng(args.seed).random((256, 256))
@@ -533,9 +541,7 @@ def main():
     world, rank, local, dev = rk.world, rk.rank, rk.local, rk.dev
     if args.dry_run:
         return dry_main(args, rk)
-    global fcship
-    import fcship as _fcship  # after torch: one HIP runtime per process
-    fcship = _fcship
+    load_fcship()
 
     ph = bench_phmm(args, dev, rk)
     total_cells = ph["cells"] * world * args.steps

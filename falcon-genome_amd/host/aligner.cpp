@@ -489,13 +489,27 @@ void align_batch(const Reference& ref, const KmerIndex& idx, const std::vector<s
 
 }  // namespace
 
-KmerIndex::KmerIndex(const Reference& ref, int k) : k_(k) {
+KmerIndex::KmerIndex(const Reference& ref, int k, const std::string& index_path) : k_(k) {
   if (k < 8 || k > 63) throw invalidParam("minimum seed length must be in [8, 63]");
   for (const Contig& c : ref.contigs) {
     codes_.emplace_back(c.seq.size());
     for (size_t p = 0; p < c.seq.size(); ++p) codes_.back()[p] = code_of(c.seq[p]);
   }
-  fmd_ = std::make_unique<FmdIndex>(codes_);
+  if (!index_path.empty()) fmd_ = FmdIndex::load(index_path, codes_);
+  loaded_ = fmd_ != nullptr;
+  if (!fmd_) fmd_ = std::make_unique<FmdIndex>(codes_);
+}
+
+std::string fmd_index_path(const std::string& fasta) { return fasta + ".fcsidx"; }
+
+void build_fmd_index(const std::string& fasta, int sa_intv) {
+  const Reference ref = load_fasta(fasta);
+  std::vector<std::vector<uint8_t>> codes;
+  for (const Contig& c : ref.contigs) {
+    codes.emplace_back(c.seq.size());
+    for (size_t p = 0; p < c.seq.size(); ++p) codes.back()[p] = code_of(c.seq[p]);
+  }
+  FmdIndex(codes, sa_intv).save(fmd_index_path(fasta));
 }
 
 AlignStats align_reads(const Reference& ref, const KmerIndex& idx, const std::vector<std::string>& names,
@@ -697,7 +711,7 @@ std::shared_ptr<const KmerIndex> index_cached(const std::string& path, const Ref
   static std::map<std::pair<std::string, int>, std::shared_ptr<const KmerIndex>> cache;
   std::lock_guard<std::mutex> g(mu);
   auto& e = cache[{path, k}];
-  if (!e) e = std::make_shared<const KmerIndex>(ref, k);
+  if (!e) e = std::make_shared<const KmerIndex>(ref, k, fmd_index_path(path));
   return e;
 }
 
@@ -920,7 +934,8 @@ AlignStats align_fastq(const AlignJob& job, const std::vector<int>& gpus, std::s
         << " pairs";
   rep << "\n[fcs-genome align] read group " << job.rg << " on " << nslot << " device slot(s), " << results.size()
       << " chunks; phases: reference " << (t_ref - t_start) / 1e6 << " s, FMD index " << (t_idx - t_ref) / 1e6
-      << " s, FASTQ + alignment " << (t_aln - t_idx) / 1e6 << " s (alignment thread-seconds " << tot.seconds
+      << " s (" << (idx.loaded() ? "mapped " + fmd_index_path(job.ref_path) : std::string("built in memory")) << ", sa_intv "
+      << idx.fmd().sa_intv() << "), FASTQ + alignment " << (t_aln - t_idx) / 1e6 << " s (alignment thread-seconds " << tot.seconds
       << ": seeding " << tot.seed_seconds << ", extension " << tot.extend_seconds << ", pairing " << tot.pair_seconds
       << ", records " << tot.record_seconds << "), sort + BAM + index " << (t_end - t_aln) / 1e6 << " s\n";
   report = rep.str();

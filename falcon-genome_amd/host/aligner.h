@@ -52,7 +52,10 @@ struct AlignStats {
 // (host/fmindex.h) for SMEM seeding.
 class KmerIndex {
  public:
-  KmerIndex(const Reference& ref, int k);
+  // index_path: a saved FMD-index of `ref` (fcs-genome index) to map instead
+  // of building one; empty or unusable: built in memory
+  KmerIndex(const Reference& ref, int k, const std::string& index_path = "");
+  bool loaded() const { return loaded_; }  // the saved index was used
   int k() const { return k_; }  // minimum seed length (bwa -k)
   // the contig's bases as codes 0..4 (A, C, G, T, other)
   const std::vector<uint8_t>& codes(int contig) const { return codes_[contig]; }
@@ -60,9 +63,15 @@ class KmerIndex {
 
  private:
   int k_;
+  bool loaded_ = false;
   std::vector<std::vector<uint8_t>> codes_;
   std::unique_ptr<FmdIndex> fmd_;
 };
+
+// The saved FMD-index of a FASTA (fcs-genome index): <fasta>.fcsidx.
+std::string fmd_index_path(const std::string& fasta);
+// Builds and saves it (bwa index's role); sa_intv 0: automatic.
+void build_fmd_index(const std::string& fasta, int sa_intv);
 
 // Aligns FASTQ reads; records appended to `out` (unsorted).  Up to
 // max_chains candidate chains per read are extended; the best by truesc is

@@ -595,13 +595,18 @@ CallerStats call_intervals(const Reference& ref, const std::vector<std::string>&
       pu.events.assign(we - wb, 0);
       if (opt.gvcf && !opt.somatic) pu.gl.assign(3 * (we - wb), 0.0);
       build_pileup(seq, reads[0], opt.min_base_quality, pu);
-      if (opt.somatic) build_pileup(seq, reads[1], opt.min_base_quality, pu);
-      finish_support(pu);
+      // activity: the sample's evidence, or in Mutect2 mode the tumor's alone
+      // (Mutect2's activity profile is a tumor-evidence test; over tumor +
+      // normal depth a somatic allele at the tumor's fraction reads as half
+      // of it and its site is missed)
       std::vector<int64_t> sites;
+      const double frac = opt.somatic ? opt.somatic_active_fraction : opt.active_fraction;
       for (int64_t p = wb; p < we; ++p) {
         const int ev = pu.events[p - wb], dp = std::max(1, pu.depth[p - wb]);
-        if (ev >= 2 && ev >= opt.active_fraction * dp) sites.push_back(p);
+        if (ev >= 2 && ev >= frac * dp) sites.push_back(p);
       }
+      if (opt.somatic) build_pileup(seq, reads[1], opt.min_base_quality, pu);
+      finish_support(pu);
       clusters.clear();
       bool grow_l = false, grow_r = false;
       for (size_t i = 0; i < sites.size();) {

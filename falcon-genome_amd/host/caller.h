@@ -34,6 +34,7 @@ struct CallerOptions {
   int pcr_indel_model = 3;  // PcrIndelModel (gatk_prep.h): GATK's default CONSERVATIVE
   int min_mapq = 20;
   double active_fraction = 0.15;
+  double somatic_active_fraction = 0.10;  // Mutect2 mode: of the tumor's depth
   int padding = 50;
   int max_region = 300;
   int max_reads_per_region = 250;

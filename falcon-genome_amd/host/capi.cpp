@@ -4,6 +4,7 @@
 // executor's stage/error semantics.  Not part of the hot-path ABI (include/fcship.h).
 #include <cstring>
 #include <functional>
+#include <memory>
 #include <string>
 
 #include "bam.h"
@@ -127,9 +128,11 @@ int fcsg_gvcf_band(int gq) { return gvcf_band(gq); }
 // loc = {contig, offset, reverse} of every occurrence (at most loc_cap rows,
 // SMEM by SMEM, each SMEM's occurrences in suffix-array order).  Returns the
 // SMEM count, or < 0 on error.
+// sa_intv: the index's SA sampling; index_path non-empty: the index is saved
+// there and the query runs on the file mapped back (FmdIndex::load).
 int fcsg_fmd_smems(const uint8_t* ref, const int64_t* clen, int ncontig, const uint8_t* q, int qlen, int min_len,
                    int split_len, int split_width, int max_mem_intv, int32_t* out, int cap, int64_t* loc,
-                   int loc_cap) {
+                   int loc_cap, int sa_intv, const char* index_path) {
   int n = -1;
   const int rc = guard([&] {
     std::vector<std::vector<uint8_t>> cs;
@@ -138,7 +141,14 @@ int fcsg_fmd_smems(const uint8_t* ref, const int64_t* clen, int ncontig, const u
       cs.emplace_back(ref + o, ref + o + clen[i]);
       o += clen[i];
     }
-    const FmdIndex fmd(cs);
+    std::unique_ptr<FmdIndex> built = std::make_unique<FmdIndex>(cs, sa_intv), mapped;
+    if (index_path && *index_path) {
+      built->save(index_path);
+      built.reset();
+      mapped = FmdIndex::load(index_path, cs);
+      if (!mapped) throw internalError("saved FMD-index did not load");
+    }
+    const FmdIndex& fmd = mapped ? *mapped : *built;
     std::vector<BiInterval> v;
     fmd.collect(q, qlen, min_len, split_len, split_width, max_mem_intv, v);
     if ((int)v.size() > cap) throw invalidParam("fcsg_fmd_smems: capacity");

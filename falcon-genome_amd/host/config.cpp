@@ -53,6 +53,7 @@ void Config::init(const std::string& root_dir) {
           "GATK --pcr-indel-model: NONE, HOSTILE, AGGRESSIVE, CONSERVATIVE (gap-open caps in tandem repeats)");
   declare("htc.min_mapq", "20", "reads below this mapping quality are ignored");
   declare("htc.active_fraction", "0.15", "mismatch/indel fraction that makes a site active");
+  declare("mutect2.active_fraction", "0.10", "tumor mismatch/indel fraction that makes a site active (mutect2)");
   declare("htc.padding", "50", "bases added either side of an active site");
   declare("htc.max_region", "300", "max active region length");
   declare("htc.max_reads_per_region", "250", "downsampling cap per region");

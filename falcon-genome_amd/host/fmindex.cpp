@@ -1,6 +1,14 @@
 #include "fmindex.h"
 
+#include <fcntl.h>
+#include <sys/mman.h>
+#include <sys/stat.h>
+#include <unistd.h>
+
 #include <algorithm>
+#include <climits>
+#include <cstdio>
+#include <cstring>
 #include <stdexcept>
 
 #include "common.h"
@@ -100,7 +108,7 @@ void sais_t(const C* s, I* sa, int64_t n, int64_t K) {
 
 void sais(const uint8_t* s, uint64_t* sa, int64_t n, int K) { sais_t<uint8_t, uint64_t>(s, sa, n, K); }
 
-FmdIndex::FmdIndex(const std::vector<std::vector<uint8_t>>& contigs) {
+FmdIndex::FmdIndex(const std::vector<std::vector<uint8_t>>& contigs, int sa_intv) {
   // F = 5 C_1 5 C_2 ... 5 C_n 5;  T = F revcomp(F) $
   std::vector<uint8_t> T;
   int64_t total = 1;
@@ -117,8 +125,9 @@ FmdIndex::FmdIndex(const std::vector<std::vector<uint8_t>>& contigs) {
   for (int64_t i = flen_ - 1; i >= 0; --i) T.push_back(T[i] == 5 ? (uint8_t)5 : (uint8_t)(5 - T[i]));
   T.push_back(0);
   n_ = (int64_t)T.size();
-  sa_.resize(n_);
-  sais(T.data(), sa_.data(), n_, 6);
+  digest_ = text_digest(contigs);
+  std::vector<uint64_t> sa(n_);
+  sais(T.data(), sa.data(), n_, 6);
   C_.assign(7, 0);
   for (uint8_t c : T) ++C_[c + 1];
   for (int c = 1; c < 7; ++c) C_[c] += C_[c - 1];
@@ -127,18 +136,176 @@ FmdIndex::FmdIndex(const std::vector<std::vector<uint8_t>>& contigs) {
   uint64_t* occ = occ_store_.data();
   while (reinterpret_cast<uintptr_t>(occ) & 63) ++occ;
   occ_ = occ;
+  nocc_ = 8 * (nb + 1);
   uint64_t run[4] = {0, 0, 0, 0};
   for (int64_t b = 0; b <= nb; ++b) {
     uint64_t* B = occ + 8 * b;
     for (int c = 0; c < 4; ++c) B[c] = run[c];
     for (int64_t i = 64 * b; i < std::min(n_, 64 * b + 64); ++i) {
-      const uint64_t p = sa_[i];
+      const uint64_t p = sa[i];
       const uint32_t ch = p ? T[p - 1] : 0;  // BWT symbol
       if (ch >= 1 && ch <= 4) {
         B[4 + ch - 1] |= 1ull << (i & 63);
         ++run[ch - 1];
+      } else {
+        special_store_.emplace_back(i, (int64_t)p);  // no LF step from this row
       }
     }
+  }
+  if (sa_intv <= 0) {
+    sa_intv = 1;
+    while ((uint64_t)n_ / sa_intv * 8 > (8ull << 30)) sa_intv *= 2;
+  }
+  intv_ = sa_intv;
+  if (intv_ == 1) {
+    sa_store_ = std::move(sa);
+    special_store_.clear();
+  } else {
+    sa_store_.resize((size_t)((n_ + intv_ - 1) / intv_));
+    for (size_t k = 0; k < sa_store_.size(); ++k) sa_store_[k] = sa[k * intv_];
+    std::vector<std::pair<int64_t, int64_t>> sp;  // sampled rows need no special entry
+    for (const auto& e : special_store_)
+      if (e.first % intv_ != 0) sp.push_back(e);
+    special_store_.swap(sp);
+  }
+  sa_ = sa_store_.data();
+  nsa_ = (int64_t)sa_store_.size();
+  special_ = special_store_.data();
+  nspecial_ = (int64_t)special_store_.size();
+}
+
+FmdIndex::~FmdIndex() {
+  if (map_) ::munmap(map_, map_len_);
+}
+
+// A digest of the contigs (lengths and every 997th base): a saved index is
+// used only for the reference it was built from.
+uint64_t FmdIndex::text_digest(const std::vector<std::vector<uint8_t>>& contigs) {
+  uint64_t h = 1469598103934665603ull;
+  auto mix = [&](uint64_t v) {
+    h ^= v;
+    h *= 1099511628211ull;
+  };
+  for (const auto& c : contigs) {
+    mix(c.size());
+    for (size_t i = 0; i < c.size(); i += 997) mix(c[i]);
+  }
+  return h;
+}
+
+namespace {
+constexpr char kFmdMagic[8] = {'F', 'C', 'S', 'F', 'M', 'D', '0', '1'};
+struct FmdHeader {
+  char magic[8];
+  int64_t n, flen, intv, ncontig, nocc, nsa, nspecial;
+  uint64_t digest;
+  int64_t C[7];
+};
+size_t align64(size_t x) { return (x + 63) & ~(size_t)63; }
+}  // namespace
+
+void FmdIndex::save(const std::string& path) const {
+  FmdHeader h{};
+  std::memcpy(h.magic, kFmdMagic, 8);
+  h.n = n_;
+  h.flen = flen_;
+  h.intv = intv_;
+  h.ncontig = (int64_t)cstart_.size();
+  h.nocc = nocc_;
+  h.nsa = nsa_;
+  h.nspecial = nspecial_;
+  h.digest = digest_;
+  for (int c = 0; c < 7; ++c) h.C[c] = C_[c];
+  const std::string tmp = path + ".tmp";
+  std::FILE* f = std::fopen(tmp.c_str(), "wb");
+  if (!f) throw fileNotFound(tmp + " (cannot open for writing)");
+  size_t off = 0;
+  auto put = [&](const void* p, size_t n) {
+    if (n && std::fwrite(p, 1, n, f) != n) {
+      std::fclose(f);
+      throw internalError("[E::fcsg] cannot write " + tmp);
+    }
+    off += n;
+  };
+  auto pad = [&] {
+    static const char z[64] = {0};
+    put(z, align64(off) - off);
+  };
+  put(&h, sizeof h);
+  put(cstart_.data(), 8 * cstart_.size());
+  put(clen_.data(), 8 * clen_.size());
+  pad();
+  put(occ_, 8 * (size_t)nocc_);
+  pad();
+  put(sa_, 8 * (size_t)nsa_);
+  pad();
+  put(special_, 16 * (size_t)nspecial_);
+  if (std::fclose(f) != 0) throw internalError("[E::fcsg] cannot write " + tmp);
+  if (std::rename(tmp.c_str(), path.c_str()) != 0) throw internalError("[E::fcsg] cannot rename " + tmp);
+}
+
+std::unique_ptr<FmdIndex> FmdIndex::load(const std::string& path, const std::vector<std::vector<uint8_t>>& contigs) {
+  const int fd = ::open(path.c_str(), O_RDONLY);
+  if (fd < 0) return nullptr;
+  struct stat st;
+  if (::fstat(fd, &st) != 0 || (size_t)st.st_size < sizeof(FmdHeader)) {
+    ::close(fd);
+    return nullptr;
+  }
+  void* m = ::mmap(nullptr, (size_t)st.st_size, PROT_READ, MAP_SHARED, fd, 0);
+  ::close(fd);
+  if (m == MAP_FAILED) return nullptr;
+  std::unique_ptr<FmdIndex> ix(new FmdIndex());
+  ix->map_ = m;
+  ix->map_len_ = (size_t)st.st_size;
+  const char* base = static_cast<const char*>(m);
+  FmdHeader h;
+  std::memcpy(&h, base, sizeof h);
+  if (std::memcmp(h.magic, kFmdMagic, 8) != 0 || h.ncontig != (int64_t)contigs.size() || h.intv < 1 ||
+      h.digest != text_digest(contigs))
+    return nullptr;
+  size_t off = sizeof h;
+  ix->cstart_.assign(reinterpret_cast<const int64_t*>(base + off), reinterpret_cast<const int64_t*>(base + off) + h.ncontig);
+  off += 8 * (size_t)h.ncontig;
+  ix->clen_.assign(reinterpret_cast<const int64_t*>(base + off), reinterpret_cast<const int64_t*>(base + off) + h.ncontig);
+  off = align64(off + 8 * (size_t)h.ncontig);
+  for (int64_t c = 0; c < h.ncontig; ++c)
+    if (ix->clen_[c] != (int64_t)contigs[c].size()) return nullptr;
+  const size_t need = align64(align64(off + 8 * (size_t)h.nocc) + 8 * (size_t)h.nsa) + 16 * (size_t)h.nspecial;
+  if (need > ix->map_len_) return nullptr;
+  ix->n_ = h.n;
+  ix->flen_ = h.flen;
+  ix->intv_ = (int)h.intv;
+  ix->digest_ = h.digest;
+  ix->C_.assign(h.C, h.C + 7);
+  ix->occ_ = reinterpret_cast<const uint64_t*>(base + off);
+  ix->nocc_ = h.nocc;
+  off = align64(off + 8 * (size_t)h.nocc);
+  ix->sa_ = reinterpret_cast<const uint64_t*>(base + off);
+  ix->nsa_ = h.nsa;
+  off = align64(off + 8 * (size_t)h.nsa);
+  ix->special_ = reinterpret_cast<const std::pair<int64_t, int64_t>*>(base + off);
+  ix->nspecial_ = h.nspecial;
+  return ix;
+}
+
+int64_t FmdIndex::sa_at(int64_t row) const {
+  // SA[LF(i)] = SA[i] - 1: walk back to a sampled row (bwa bwt_sa)
+  int64_t steps = 0;
+  for (;;) {
+    if (row % intv_ == 0) return (int64_t)sa_[row / intv_] + steps;
+    const uint64_t* B = occ_ + 8 * (row >> 6);
+    const uint64_t bit = 1ull << (row & 63);
+    int c = -1;
+    for (int k = 0; k < 4; ++k)
+      if (B[4 + k] & bit) c = k;
+    if (c < 0) {  // $ or a separator precedes this suffix: stored
+      const auto* e = std::lower_bound(special_, special_ + nspecial_, std::make_pair(row, (int64_t)INT64_MIN));
+      if (e == special_ + nspecial_ || e->first != row) throw internalError("[E::fcsg] FMD-index special row missing");
+      return e->second + steps;
+    }
+    row = C_[c + 1] + (int64_t)(B[c] + (uint64_t)__builtin_popcountll(B[4 + c] & (bit - 1)));
+    ++steps;
   }
 }
 
@@ -295,7 +462,7 @@ void FmdIndex::collect(const uint8_t* q, int len, int min_len, int split_len, in
 }
 
 void FmdIndex::locate(const BiInterval& iv, int64_t j, int& contig, int64_t& off, bool& rev) const {
-  int64_t p = sa_[iv.k + j];
+  int64_t p = sa_at(iv.k + j);
   const int64_t len = iv.qe - iv.qb;
   rev = p >= flen_;
   if (rev) p = 2 * flen_ - p - len;  // start of the reverse-strand match on F

@@ -16,7 +16,9 @@
 #pragma once
 
 #include <cstdint>
+#include <memory>
 #include <string>
+#include <utility>
 #include <vector>
 
 #include "fasta.h"
@@ -30,11 +32,20 @@ struct BiInterval {
 
 class FmdIndex {
  public:
-  // contigs as codes 0..4 (A, C, G, T, other)
-  explicit FmdIndex(const std::vector<std::vector<uint8_t>>& contigs);
+  // contigs as codes 0..4 (A, C, G, T, other).  sa_intv: keep SA[i] for rows
+  // i % sa_intv == 0 (bwa's sa_intv; rows in between are located by LF-mapping
+  // walks); 0 picks the smallest power of two whose sample fits 8 GiB.
+  explicit FmdIndex(const std::vector<std::vector<uint8_t>>& contigs, int sa_intv = 0);
+  ~FmdIndex();
   FmdIndex(const FmdIndex&) = delete;
   FmdIndex& operator=(const FmdIndex&) = delete;
+  // Writes the index (bwa-index's role: built once, loaded by every align run).
+  void save(const std::string& path) const;
+  // Memory-maps an index written by save(); null if the file is absent, from
+  // another version, or was built from contigs of other lengths or content.
+  static std::unique_ptr<FmdIndex> load(const std::string& path, const std::vector<std::vector<uint8_t>>& contigs);
   int64_t size() const { return n_; }
+  int sa_intv() const { return intv_; }
   // bwt_smem1: SMEMs of q (codes 0..4) overlapping position x with at least
   // min_intv occurrences; returns the next start position (bwa's return value).
   int smem1(const uint8_t* q, int len, int x, int64_t min_intv, std::vector<BiInterval>& out) const;
@@ -51,18 +62,32 @@ class FmdIndex {
   void locate(const BiInterval& iv, int64_t j, int& contig, int64_t& off, bool& rev) const;
 
  private:
+  FmdIndex() = default;
   void extend(const BiInterval& ik, BiInterval ok[5], bool is_back) const;
   void occ4(int64_t i, int64_t o[4]) const;  // occurrences of A, C, G, T in BWT[0, i)
   void set_intv(int c, BiInterval& iv) const;
+  int64_t sa_at(int64_t row) const;          // SA[row]: sampled, special, or by LF walk
+  static uint64_t text_digest(const std::vector<std::vector<uint8_t>>& contigs);
   int64_t n_ = 0, flen_ = 0;
+  int intv_ = 1;
+  uint64_t digest_ = 0;
   std::vector<int64_t> C_;               // C_[c] = symbols < c
-  std::vector<uint64_t> sa_;             // suffix array
   // per 64-position block, one 64-byte line: the counts of A, C, G, T before
   // the block, then their bit vectors in it; one extra block holds the totals
-  std::vector<uint64_t> occ_store_;
-  const uint64_t* occ_ = nullptr;        // occ_store_ aligned to 64 bytes
+  const uint64_t* occ_ = nullptr;
+  int64_t nocc_ = 0;                     // uint64 words of occ_
+  const uint64_t* sa_ = nullptr;         // SA of rows 0, intv, 2 intv, ...
+  int64_t nsa_ = 0;
+  // rows whose BWT symbol is $ or a separator (no LF step): (row, SA) sorted by row
+  const std::pair<int64_t, int64_t>* special_ = nullptr;
+  int64_t nspecial_ = 0;
   std::vector<int64_t> cstart_;          // forward-text start of each contig
   std::vector<int64_t> clen_;
+  // storage: built in memory, or the mapped file
+  std::vector<uint64_t> occ_store_, sa_store_;
+  std::vector<std::pair<int64_t, int64_t>> special_store_;
+  void* map_ = nullptr;
+  size_t map_len_ = 0;
 };
 
 // SA-IS suffix array of s[0, n) over the alphabet [0, K) with s[n-1] == 0

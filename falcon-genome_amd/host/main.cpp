@@ -21,6 +21,7 @@
 #include "config.h"
 #include "executor.h"
 #include "fcship.h"
+#include "aligner.h"
 #include "intervals.h"
 #include "sample_sheet.h"
 #include "synth.h"
@@ -341,6 +342,29 @@ int align_main(int argc, char** argv) {
   return 0;
 }
 
+// `fcs-genome index -r ref.fasta`: the aligner's FMD-index, saved next to the
+// FASTA (<ref>.fcsidx) so that align maps it instead of building one per run
+// (bwa-flow reads the prebuilt bwa index; the reference expects it beside the
+// FASTA, src/workers/BWAWorker.cpp:134-147).
+int index_main(int argc, char** argv) {
+  Args a;
+  a.add("ref", "r", false, true, "reference genome path");
+  a.add("sa-intv", "", false, false, "suffix-array sampling interval (default: automatic, <= 8 GiB of samples)");
+  try {
+    a.parse(argc, argv);
+  } catch (helpRequest&) {
+    std::cerr << "'fcs-genome index' options:\n" << a.help();
+    throw;
+  }
+  const std::string ref = a.get("ref");
+  if (!is_regular_file(ref)) throw fileNotFound(ref);
+  const uint64_t t0 = now_us();
+  build_fmd_index(ref, a.has("sa-intv") ? std::stoi(a.get("sa-intv")) : 0);
+  std::cerr << "[fcs-genome index] " << fmd_index_path(ref) << " written in " << (now_us() - t0) / 1e6 << " s"
+            << std::endl;
+  return 0;
+}
+
 int synth_main(int argc, char** argv) {
   Args a;
   a.add("output", "o", false, true, "output directory");
@@ -448,6 +472,7 @@ int print_help() {
                "  htc             variant calling, HaplotypeCaller-style (GPU PairHMM)\n"
                "  mutect2         somatic variant calling, tumor/normal (GPU PairHMM)\n"
                "  conf            print configuration keys\n"
+               "  index           build the aligner's FMD-index of a reference (<ref>.fcsidx)\n"
                "  synth           write synthetic reference/BAM/FASTQ/truth inputs\n";
   return 0;
 }
@@ -477,6 +502,7 @@ int main(int argc, char** argv) {
     else if (cmd == "mutect2") ret = mutect2_main(argc - 1, argv + 1);
     else if (cmd == "align" || cmd == "al") ret = align_main(argc - 1, argv + 1);
     else if (cmd == "synth") ret = synth_main(argc - 1, argv + 1);
+    else if (cmd == "index") ret = index_main(argc - 1, argv + 1);
     else if (cmd == "conf") {
       std::cerr << "fcs-genome configuration options:\n" << conf().dump();
       ret = 1;  // the reference exits through silentExit here

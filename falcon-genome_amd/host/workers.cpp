@@ -35,6 +35,7 @@ CallerOptions caller_options_from_config(int gpu) {
   o.pcr_indel_model = (int)parse_pcr_indel_model(c.get_string("htc.pcr_indel_model"));
   o.min_mapq = c.get_int("htc.min_mapq");
   o.active_fraction = std::stod(c.get_string("htc.active_fraction"));
+  o.somatic_active_fraction = std::stod(c.get_string("mutect2.active_fraction"));
   o.padding = c.get_int("htc.padding");
   o.max_region = c.get_int("htc.max_region");
   o.max_reads_per_region = c.get_int("htc.max_reads_per_region");

@@ -27,7 +27,8 @@ def make_ref(rng):
     return contigs
 
 
-def smems(contigs, q, min_len=1, split_len=10**9, split_width=10, max_mem_intv=0, loc_cap=100000):
+def smems(contigs, q, min_len=1, split_len=10**9, split_width=10, max_mem_intv=0, loc_cap=100000, sa_intv=1,
+          index_path=""):
     code = {"A": 0, "C": 1, "G": 2, "T": 3}
     ref = np.array([code.get(b, 4) for b in "".join(contigs)], np.uint8)
     cl = np.array([len(c) for c in contigs], np.int64)
@@ -36,7 +37,8 @@ def smems(contigs, q, min_len=1, split_len=10**9, split_width=10, max_mem_intv=0
     loc = np.zeros((loc_cap, 3), np.int64)
     n = H.lib.fcsg_fmd_smems(ref.ctypes.data_as(C.c_void_p), cl.ctypes.data_as(C.c_void_p), len(contigs),
                              qa.ctypes.data_as(C.c_void_p), len(q), min_len, split_len, split_width, max_mem_intv,
-                             out.ctypes.data_as(C.c_void_p), len(out), loc.ctypes.data_as(C.c_void_p), loc_cap)
+                             out.ctypes.data_as(C.c_void_p), len(out), loc.ctypes.data_as(C.c_void_p), loc_cap,
+                             sa_intv, str(index_path).encode())
     assert n >= 0, H.lib.fcsg_last_error()
     return [tuple(int(x) for x in r) for r in out[:n]], loc
 
@@ -133,3 +135,20 @@ def test_third_round_forward_seeds():
                 break
         x = nxt
     assert sorted(third) == sorted(want)
+
+
+def test_saved_index_with_sampled_sa(tmp_path):
+    """`fcs-genome index`: the FMD-index saved with a sampled suffix array
+    (bwa's sa_intv; rows between samples located by LF-mapping walks, rows
+    after a separator stored) and mapped back gives the same SMEMs and the same
+    located occurrences as the in-memory index with the full suffix array."""
+    rng = np.random.default_rng(11)
+    contigs = make_ref(rng)
+    qs = [contigs[0][950:1100], revcomp(contigs[2][50:200]), contigs[1][2000:2080] + "NN" + contigs[0][10:60],
+          "".join(rng.choice(list("ACGT"), 120))]
+    for q in qs:
+        want, wloc = smems(contigs, q, min_len=5)
+        for intv, path in ((4, tmp_path / "a.fcsidx"), (32, tmp_path / "b.fcsidx"), (7, "")):
+            got, gloc = smems(contigs, q, min_len=5, sa_intv=intv, index_path=path)
+            assert got == want
+            assert np.array_equal(gloc, wloc), (intv, q[:20])

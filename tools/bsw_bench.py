@@ -15,7 +15,8 @@ sys.path.insert(0, os.path.join(ROOT, "falcon-genome_amd"))
 import torch  # noqa: E402  (first: one HIP runtime per process)
 
 import bench  # noqa: E402
-import fcship  # noqa: E402
+
+fcship = bench.load_fcship()
 
 
 def main():

@@ -20,9 +20,9 @@ def main():
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--seed", type=int, default=20261015)
     args = ap.parse_args()
-    dev = torch.device("cuda", 0)
-    torch.cuda.set_device(dev)
-    ph = bench.bench_phmm(args, dev, 0, 1)
+    bench.load_fcship()
+    rk = bench.Ranks(False)
+    ph = bench.bench_phmm(args, rk.dev, rk)
     print(json.dumps({"gcups": round(ph["cells"] * args.steps / ph["elapsed"] / 1e9, 1),
                       "fwd_ms": round(ph["fwd_ms"], 3), "kernel_gcups": round(ph["cells"] / ph["fwd_ms"] / 1e6, 1)}))
 
