@@ -53,22 +53,12 @@ constexpr int kStreamPfd = FCS_STREAM_PFD;  // LDS read-ahead of the 3/2/1-wave 
 constexpr int kStreamMinR = 33;  // a pair spans >= 17 units: at most two pairs per stripe and segment
 constexpr int kStreamMaxR = 0xFFFF;  // a segment packs R | H << 16 between stripes; longer reads take phmm2
 constexpr int kStreamMaxK = 8;   // pairs per segment stream
-#ifndef FCS_STREAM_PTAB
-#define FCS_STREAM_PTAB 0
-#endif
-// FCS_STREAM_PTAB: the emission priors come from a per-lane LDS table indexed
-// by hap code (one ds_read_b64 of {row a, row b} priors per step and one
-// address add) instead of a bit extract + select per row (five VALU per step
-// with the code's zero-extension).  The table is 5 codes x 64 lanes x 8 B.
-constexpr int kStreamPtab = FCS_STREAM_PTAB;
-constexpr int kPtabBytes = kStreamPtab ? 5 * 64 * 8 : 0;
-constexpr int kHapSlack = kStreamPtab ? 48 : 0;  // valid codes below the first hap buffer (reads start 30 + PF early)
+constexpr uint64_t kTopLanes = 0x8000800080008000ull;  // lane 15 of each 16-lane segment
 // Hap-length bounds of the stream classes: LDS <= 10,240 B per wave (4 waves per
 // SIMD), <= 13,312 B (3, at the 512-byte allocation granularity), <= 20 KB (2),
 // and the 160 KB limit.
 __host__ __device__ constexpr int stream_class_hmax(int c) {
-  return kStreamPtab ? (c == 0 ? 158 : c == 1 ? 235 : c == 2 ? 414 : 3700)
-                     : (c == 0 ? 224 : c == 1 ? 300 : c == 2 ? 472 : 3700);
+  return c == 0 ? 224 : c == 1 ? 300 : c == 2 ? 472 : 3700;
 }
 // Waves per SIMD the class's launch bounds ask for (its LDS allows as many).
 __host__ __device__ constexpr int stream_class_waves(int c) { return c == 0 ? 4 : c == 1 ? 3 : c == 2 ? 2 : 1; }
@@ -77,16 +67,15 @@ __host__ __device__ inline int stream_class(int H) {
     if (H <= stream_class_hmax(c)) return c;
   return -1;
 }
-// LDS per wave: Z (64 ring entries) | [PTAB: prior table] | four rings of
-// hmax + 18 slots (slot = column; a stripe runs to step 16 * ceil((H + 33) /
-// 16) - 1 <= H + 47, so lane 15 writes columns 1 .. hmax + 16) | [PTAB: slack]
-// | eight hap-code buffers of hmax + 10 bytes (column c at 3 + (address & 3) +
-// c: whole aligned dwords of the hap bytes are converted in place) | 64 bytes
-// of read-ahead tail.
+// LDS per wave: Z (64 ring entries) | four rings of hmax + 18 slots (slot =
+// column; a stripe runs to step 16 * ceil((H + 33) / 16) - 1 <= H + 47, so lane
+// 15 writes columns 1 .. hmax + 16) | eight hap-code buffers of hmax + 10 bytes
+// (column c at 3 + (address & 3) + c: whole aligned dwords of the hap bytes are
+// converted in place) | 64 bytes of read-ahead tail.
 __host__ __device__ constexpr int stream_nslot(int hmax) { return hmax + 18; }
 __host__ __device__ constexpr int stream_hstride(int hmax) { return (hmax + 12) & ~3; }
 __host__ __device__ constexpr int stream_lds(int hmax) {
-  return 512 + kPtabBytes + 4 * 8 * stream_nslot(hmax) + kHapSlack + 8 * stream_hstride(hmax) + 64;
+  return 512 + 4 * 8 * stream_nslot(hmax) + 8 * stream_hstride(hmax) + 64;
 }
 
 // Per-row constants of one half (role: 0 idle, 1 pad, 2 row r < R, 3 row R, 4 V).
@@ -152,26 +141,14 @@ __device__ __forceinline__ int srole(int r, int R) { return r == 0 ? 1 : r < R ?
 // One step: phmm2_step without the byte-compare and summing variants; the
 // boundary source is this block's per-lane pointer `rd` (ring or Z) and COND
 // captures the V lanes' X at their column H + 1.
-// Prior-table read-ahead (steps) under FCS_STREAM_PTAB: pt[k] holds the
-// {row a, row b} priors of the hap code of step t + k; it is read from the code
-// hq[k] loaded PF - k steps earlier, so PT < PF.
-constexpr int kPtabAhead = 2;
-constexpr uint64_t kTopLanes = 0x8000800080008000ull;  // lane 15 of each 16-lane segment
-struct PtabPipe {
-  pf2 pt[kPtabAhead];
-  float pbp;  // row b's prior for this step: the previous step's table entry, row b half
-};
-
 template <bool COND, bool WRITE, int S, int PF>
 __device__ __forceinline__ void pstream_step(Lane2& L, PhRing<float> (&pf)[PF], int (&hq)[PF],
                                              const unsigned char* __restrict__ hp, const PhRing<float>* __restrict__ rd,
                                              const RowP2& p, const bool start, const bool top, const int t0,
-                                             const int dl, float& acc, const uint32_t wbase, PtabPipe& pp,
-                                             const pf2* __restrict__ ptab) {
+                                             const int dl, float& acc, const uint32_t wbase) {
   const int t = t0 + S;
   const PhRing<float> cur = pf[0];
   const int hba = hq[0];
-  const pf2 ptc = pp.pt[0];
 #pragma unroll
   for (int k = 0; k + 1 < PF; ++k) {
     pf[k] = pf[k + 1];
@@ -179,12 +156,6 @@ __device__ __forceinline__ void pstream_step(Lane2& L, PhRing<float> (&pf)[PF], 
   }
   pf[PF - 1] = rd[S];     // boundary input for step t + PF
   hq[PF - 1] = hp[t];     // row a's hap code for column t + PF - 2l
-  if constexpr (kStreamPtab) {
-    static_assert(kPtabAhead < PF, "the table read needs its code loaded a step earlier");
-#pragma unroll
-    for (int k = 0; k + 1 < kPtabAhead; ++k) pp.pt[k] = pp.pt[k + 1];
-    pp.pt[kPtabAhead - 1] = ptab[64u * (uint32_t)hq[kPtabAhead - 1]];  // priors of the code of step t + kPtabAhead
-  }
   const int hbb = L.hbp;
   L.hbp = hba;
   pf2 Xsw = L.Xn, Isw = L.In;
@@ -211,33 +182,13 @@ __device__ __forceinline__ void pstream_step(Lane2& L, PhRing<float> (&pf)[PF], 
   Isw.y = start ? cur.I : Isw.y;
 #endif
   const pf2 I = __builtin_shufflevector(Isw, Isw, 1, 0);
-  pf2 M;
-  if constexpr (kStreamPtab) {
-    // two scalar multiplies, the same VALU cycles as one packed one (kept
-    // scalar: the compiler's SLP packing would first move both operands into
-    // a register pair)
-    asm("v_mul_f32 %0, %1, %2" : "=v"(M.x) : "v"(L.Xp.y), "v"(ptc.x));
-    asm("v_mul_f32 %0, %1, %2" : "=v"(M.y) : "v"(L.Xp.x), "v"(pp.pbp));
-    pp.pbp = ptc.y;
-    (void)hbb;
-  } else {
-    pf2 prior;
-    prior.x = prior_code(p.ma, hba, p.e1.x, p.e3.x);
-    prior.y = prior_code(p.mb, hbb, p.e1.y, p.e3.y);
-    M = __builtin_shufflevector(L.Xp, L.Xp, 1, 0) * prior;
-  }
+  pf2 prior;
+  prior.x = prior_code(p.ma, hba, p.e1.x, p.e3.x);
+  prior.y = prior_code(p.mb, hbb, p.e1.y, p.e3.y);
+  const pf2 M = __builtin_shufflevector(L.Xp, L.Xp, 1, 0) * prior;
   const pf2 D = __builtin_elementwise_fma(L.Mo, p.my, L.Do * p.yy);
   const pf2 Xn = __builtin_elementwise_fma(M, p.mm, __builtin_elementwise_fma(I, p.gm, D));
   const pf2 In = __builtin_elementwise_fma(M, p.mx, I * p.xx);
-#if FCS_STREAM_BRANCHWRITE  // A/B: the round-2 form, a branch around the write per step
-  if constexpr (WRITE) {
-    if (top)
-      asm volatile("ds_write2_b32 %0, %1, %2 offset0:%3 offset1:%4"
-                   :
-                   : "v"(wbase), "v"(Xn.y), "v"(In.y), "i"(2 * S), "i"(2 * S + 1)
-                   : "memory");
-  }
-#else
   if constexpr (WRITE) {
     // row b of lane 15, column t - 31 -> ring slot t - 31: EXEC narrowed to the
     // four lanes 15 inside the statement, so the step stays one basic block (a
@@ -254,7 +205,6 @@ __device__ __forceinline__ void pstream_step(Lane2& L, PhRing<float> (&pf)[PF], 
         : "memory");
     (void)top;
   }
-#endif
   else
     asm volatile("" ::: "memory");  // keep each step's LDS reads in their step (hoisted, they cost registers)
   if constexpr (COND)  // V lanes: take X at the step dl = lim - t0 (a compare-select in place, not
@@ -275,9 +225,9 @@ __device__ __forceinline__ void pstream_block(Lane2& L, PhRing<float> (&pf)[PF],
                                               const unsigned char* __restrict__ hp,
                                               const PhRing<float>* __restrict__ rd, const RowP2& p, const bool start,
                                               const bool top, const int t0, const int dl, float& acc,
-                                              const uint32_t wbase, PtabPipe& pp, const pf2* __restrict__ ptab) {
+                                              const uint32_t wbase) {
   [&]<int... S>(std::integer_sequence<int, S...>) {
-    (pstream_step<COND, WRITE, S, PF>(L, pf, hq, hp, rd, p, start, top, t0, dl, acc, wbase, pp, ptab), ...);
+    (pstream_step<COND, WRITE, S, PF>(L, pf, hq, hp, rd, p, start, top, t0, dl, acc, wbase), ...);
   }(std::make_integer_sequence<int, NS>{});
 }
 
@@ -286,9 +236,7 @@ __device__ __forceinline__ void pstream_block(Lane2& L, PhRing<float> (&pf)[PF],
 // byte whose code does not map back to itself is outside A/C/G/T/N.
 __device__ __forceinline__ uint32_t hap_codes4(uint32_t x, uint32_t valid, bool& other) {
   const uint32_t sel = (x >> 1) & 0x07070707u;
-  // under PTAB a byte outside A/C/G/T/N takes code 4 (N), which maps back to
-  // 'N' != the byte, so it is still flagged; the table then has five codes
-  const uint32_t code = __builtin_amdgcn_perm(kStreamPtab ? 0x04040404u : 0x04050505u, 0x02030100u, sel);
+  const uint32_t code = __builtin_amdgcn_perm(0x04050505u, 0x02030100u, sel);
   const uint32_t back = __builtin_amdgcn_perm(0x0000004Eu, 0x54474341u, code);
   other |= ((back ^ x) & valid) != 0u;
   return code;
@@ -308,31 +256,10 @@ __global__ __launch_bounds__(64, LB) void phmm3_kernel(
   const int sl2 = 2 * sl;
   const bool top = sl == 15;
   // LDS read-ahead (steps): the 4-wave class has no VGPRs to spare beyond 2
-  constexpr int PF = kStreamPtab ? 4 : (LB >= 4 ? 2 : kStreamPfd);
+  constexpr int PF = LB >= 4 ? 2 : kStreamPfd;
   PhRing<float>* const Z = reinterpret_cast<PhRing<float>*>(smem_raw);
-  pf2* const ptab = reinterpret_cast<pf2*>(smem_raw + 512) + lane;  // entry of code c: ptab[64 * c]
-  PhRing<float>* const ring = reinterpret_cast<PhRing<float>*>(smem_raw + 512 + kPtabBytes) + seg * nslot;
-  unsigned char* const hbase = smem_raw + 512 + kPtabBytes + 32 * nslot + kHapSlack;
-  unsigned char* const hbufs = hbase + 2 * seg * hstride;  // this segment's two buffers
-  if constexpr (kStreamPtab) {
-    // every hap byte a step can read (slack, the eight buffers, the tail) holds
-    // a valid code before the first batch: the table is indexed by it
-    uint32_t* const h32 = reinterpret_cast<uint32_t*>(hbase - kHapSlack);
-    for (int i = lane; i < (kHapSlack + 8 * hstride + 64) / 4; i += 64) h32[i] = 0u;
-    __syncthreads();
-  }
-  // the stripe's priors by hap code (rows a, b): written when its row constants are
-  auto write_ptab = [&](const RowP2& q) {
-    if constexpr (kStreamPtab) {
-#pragma unroll
-      for (int c = 0; c < 5; ++c) {
-        pf2 e;
-        e.x = prior_code(q.ma, c, q.e1.x, q.e3.x);
-        e.y = prior_code(q.mb, c, q.e1.y, q.e3.y);
-        ptab[64 * c] = e;
-      }
-    }
-  };
+  PhRing<float>* const ring = reinterpret_cast<PhRing<float>*>(smem_raw + 512) + seg * nslot;
+  unsigned char* const hbufs = smem_raw + 512 + 32 * nslot + 2 * seg * hstride;  // this segment's two buffers
   {
     PhRing<float> z;
     z.X = lane >= 32 ? 1.f : 0.f;
@@ -499,7 +426,6 @@ __global__ __launch_bounds__(64, LB) void phmm3_kernel(
       const SLane s0 = locate(0);
       cur_pk = pack(s0);
       prm = params_of(s0, raw_of(s0, s0.ra, s0.role_a), raw_of(s0, s0.rb, s0.role_b));
-      write_ptab(prm);
       hap_issue(0, s0);
     }
     for (int st = 0; st < nstr; ++st) {
@@ -542,16 +468,10 @@ __global__ __launch_bounds__(64, LB) void phmm3_kernel(
       L.hbp = 6;
       PhRing<float> pf[PF];
       int hq[PF];
-      PtabPipe pp;
 #pragma unroll
       for (int q = 0; q < PF; ++q) {
         pf[q] = is_z ? Z[32 + q - sl2 + zsh] : ring[q];
         hq[q] = hp[q - PF];
-      }
-      pp.pbp = 0.f;  // row b at step 0 sits at a column < 1: its M is 0 whatever the prior
-      if constexpr (kStreamPtab) {
-#pragma unroll
-        for (int q = 0; q < kPtabAhead; ++q) pp.pt[q] = ptab[64u * (uint32_t)hq[q]];
       }
       float acc = 0.f;
       for (int blk = 0; blk < nblk; ++blk) {
@@ -562,14 +482,14 @@ __global__ __launch_bounds__(64, LB) void phmm3_kernel(
         const int dl = lim - t0;
         if (blk >= 2) {
           if (cond)
-            pstream_block<true, true, PF>(L, pf, hq, hp, rd, prm, start, top, t0, dl, acc, wbase, pp, ptab);
+            pstream_block<true, true, PF>(L, pf, hq, hp, rd, prm, start, top, t0, dl, acc, wbase);
           else
-            pstream_block<false, true, PF>(L, pf, hq, hp, rd, prm, start, top, t0, dl, acc, wbase, pp, ptab);
+            pstream_block<false, true, PF>(L, pf, hq, hp, rd, prm, start, top, t0, dl, acc, wbase);
         } else {
           if (cond)
-            pstream_block<true, false, PF>(L, pf, hq, hp, rd, prm, start, top, t0, dl, acc, wbase, pp, ptab);
+            pstream_block<true, false, PF>(L, pf, hq, hp, rd, prm, start, top, t0, dl, acc, wbase);
           else
-            pstream_block<false, false, PF>(L, pf, hq, hp, rd, prm, start, top, t0, dl, acc, wbase, pp, ptab);
+            pstream_block<false, false, PF>(L, pf, hq, hp, rd, prm, start, top, t0, dl, acc, wbase);
         }
       }
       if (half) {
@@ -580,14 +500,14 @@ __global__ __launch_bounds__(64, LB) void phmm3_kernel(
         const int dl = lim - t0;
         if (nblk >= 2) {
           if (cond)
-            pstream_block<true, true, PF, 8>(L, pf, hq, hp, rd, prm, start, top, t0, dl, acc, wbase, pp, ptab);
+            pstream_block<true, true, PF, 8>(L, pf, hq, hp, rd, prm, start, top, t0, dl, acc, wbase);
           else
-            pstream_block<false, true, PF, 8>(L, pf, hq, hp, rd, prm, start, top, t0, dl, acc, wbase, pp, ptab);
+            pstream_block<false, true, PF, 8>(L, pf, hq, hp, rd, prm, start, top, t0, dl, acc, wbase);
         } else {
           if (cond)
-            pstream_block<true, false, PF, 8>(L, pf, hq, hp, rd, prm, start, top, t0, dl, acc, wbase, pp, ptab);
+            pstream_block<true, false, PF, 8>(L, pf, hq, hp, rd, prm, start, top, t0, dl, acc, wbase);
           else
-            pstream_block<false, false, PF, 8>(L, pf, hq, hp, rd, prm, start, top, t0, dl, acc, wbase, pp, ptab);
+            pstream_block<false, false, PF, 8>(L, pf, hq, hp, rd, prm, start, top, t0, dl, acc, wbase);
         }
       }
       if (lim >= 0) {
@@ -607,7 +527,6 @@ __global__ __launch_bounds__(64, LB) void phmm3_kernel(
       // the next stripe's constants, at the stripe end: computed after block
       // 0 (as phmm2 does) their values add ~60 VGPRs of pressure
       prm = params_of(unpack(nxt_pk), na, nb);
-      write_ptab(prm);
       cur_pk = nxt_pk;
     }
     __syncthreads();  // the next batch rewrites the hap buffers

@@ -169,15 +169,19 @@ int fcsg_fmd_smems(const uint8_t* ref, const int64_t* clen, int ncontig, const u
 }
 
 // bwa's seed-extension protocol (host/seedext.h) over n seeds on one reference
-// sequence (codes 0..4); per job out_i = {qb, qe, score, truesc, w, gscore, gw},
+// sequence (codes 0..4), each with its chain's window (win_lo / win_hi, or
+// null / -1 for the seed's own); per job out_i = {qb, qe, score, truesc, w, gscore, gw},
 // out_r = {rb, re}, the CIGAR (ksw ops) in cig[cig_off[i] ...] (ncig[i] ops).
 int fcsg_extend_seeds(int n, const uint8_t* qbuf, const int64_t* qoff, const int32_t* qlen, const uint8_t* ref,
                       int64_t rlen, const int32_t* seed_q, const int64_t* seed_r, const int32_t* seed_len, int w,
                       int pen_clip5, int pen_clip3, int gpu, int32_t* out_i, int64_t* out_r, uint32_t* cig,
-                      const int64_t* cig_off, const int32_t* cig_cap, int32_t* ncig) {
+                      const int64_t* cig_off, const int32_t* cig_cap, int32_t* ncig, const int64_t* win_lo,
+                      const int64_t* win_hi) {
   return guard([&] {
     std::vector<SeedJob> jobs(n);
     for (int i = 0; i < n; ++i) {
+      if (win_lo) jobs[i].win_lo = win_lo[i];
+      if (win_hi) jobs[i].win_hi = win_hi[i];
       jobs[i].q = qbuf + qoff[i];
       jobs[i].qlen = qlen[i];
       jobs[i].ref = ref;

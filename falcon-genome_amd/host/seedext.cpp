@@ -112,8 +112,15 @@ void extend_seeds(const std::vector<SeedJob>& jobs, const fcs_bsw_params& p_in, 
   parallel_for(n, opt.threads, [&](size_t i) {
     const SeedJob& J = jobs[i];
     const int rest = J.qlen - J.seed_q - J.seed_len;
-    rmax0[i] = std::max<int64_t>(0, J.seed_r - (J.seed_q + bwa_cal_max_gap(p_in, J.seed_q, opt.w)));
-    rmax1[i] = std::min<int64_t>(J.rlen, J.seed_r + J.seed_len + rest + bwa_cal_max_gap(p_in, rest, opt.w));
+    if (J.win_lo >= 0 || J.win_hi >= 0) {  // the chain's window (bwa's rmax over all its seeds)
+      rmax0[i] = std::max<int64_t>(0, J.win_lo);
+      rmax1[i] = std::min<int64_t>(J.rlen, J.win_hi);
+      if (rmax0[i] > J.seed_r || rmax1[i] < J.seed_r + J.seed_len)
+        throw invalidParam("extend_seeds: chain window does not contain the seed");
+    } else {
+      rmax0[i] = std::max<int64_t>(0, J.seed_r - (J.seed_q + bwa_cal_max_gap(p_in, J.seed_q, opt.w)));
+      rmax1[i] = std::min<int64_t>(J.rlen, J.seed_r + J.seed_len + rest + bwa_cal_max_gap(p_in, rest, opt.w));
+    }
     SeedAln& A = out[i];
     if (J.seed_q > 0) {
       Side& s = left[i];
@@ -189,13 +196,19 @@ void extend_seeds(const std::vector<SeedJob>& jobs, const fcs_bsw_params& p_in, 
     }
   }
   for (size_t i = 0; i < n; ++i) out[i].w = std::max(aw0[i], aw1[i]);
-  if (!opt.want_cigar) return;
+  if (opt.want_cigar) global_cigars(jobs, p_in, opt, out, st);
+}
 
+void global_cigars(const std::vector<SeedJob>& jobs, const fcs_bsw_params& p_in, const SeedExtOptions& opt,
+                   std::vector<SeedAln>& out, SeedExtStats& st) {
+  const size_t n = jobs.size();
+  const int a = p_in.mat[0];
   // ---- mem_reg2aln: the CIGAR by banded global alignment, widened up to three times
   std::vector<int> w2(n, 0), last_sc(n, INT_MIN), tries(n, 0);
   std::vector<int> todo;
   for (size_t i = 0; i < n; ++i) {
     SeedAln& A = out[i];
+    A.cigar.clear();
     if (A.qe <= A.qb || A.re <= A.rb) continue;
     const int l1 = A.qe - A.qb, l2 = (int)(A.re - A.rb);
     int w = std::max(bwa_infer_bw(l1, l2, A.truesc, a, p_in.o_del, p_in.e_del),
@@ -258,6 +271,35 @@ void extend_seeds(const std::vector<SeedJob>& jobs, const fcs_bsw_params& p_in, 
     }
     todo.swap(again);
   }
+}
+
+void global_scores(const std::vector<GlobalScoreJob>& jobs, const fcs_bsw_params& p, int gpu, std::vector<int>& scores,
+                   SeedExtStats& st) {
+  scores.assign(jobs.size(), 0);
+  std::vector<fcs_bsw_task> tasks;
+  std::vector<size_t> who;
+  for (size_t i = 0; i < jobs.size(); ++i) {
+    const GlobalScoreJob& J = jobs[i];
+    const int l = J.qe - J.qb;
+    const int64_t rlen = J.re - J.rb;
+    if (l == rlen && J.w == 0) {
+      int sc = 0;
+      for (int k = 0; k < l; ++k) sc += p.mat[J.q[J.qb + k] * 5 + J.ref[J.rb + k]];
+      scores[i] = sc;
+      continue;
+    }
+    tasks.push_back({(int32_t)l, (int32_t)rlen, 0, bwa_cigar_band(p, l, rlen, J.w), J.q + J.qb, J.ref + J.rb});
+    who.push_back(i);
+  }
+  if (tasks.empty()) return;
+  std::vector<int32_t> sc(tasks.size());
+  const uint64_t g0 = now_us();
+  if (fcs_bsw_global(tasks.data(), (int32_t)tasks.size(), &p, sc.data(), nullptr, nullptr, nullptr, nullptr, gpu) !=
+      FCS_OK)
+    throw failedCommand(std::string(fcs_last_error()));
+  st.gpu_seconds += (now_us() - g0) / 1e6;
+  st.global_tasks += (int64_t)tasks.size();
+  for (size_t k = 0; k < who.size(); ++k) scores[who[k]] = sc[k];
 }
 
 }  // namespace fcsg

@@ -35,6 +35,10 @@ struct SeedJob {
   int seed_q = 0;  // seed: query offset, contig offset, length
   int64_t seed_r = 0;
   int seed_len = 0;
+  // reference window [win_lo, win_hi) of the seed's chain (mem_chain2aln's
+  // rmax: min / max over ALL the chain's seeds, clipped to the contig); -1:
+  // the window of this seed alone
+  int64_t win_lo = -1, win_hi = -1;
 };
 
 struct SeedAln {
@@ -70,5 +74,23 @@ int bwa_cigar_band(const fcs_bsw_params& p, int l, int64_t rlen, int w_);
 
 void extend_seeds(const std::vector<SeedJob>& jobs, const fcs_bsw_params& p, const SeedExtOptions& opt,
                   std::vector<SeedAln>& out, SeedExtStats& st);
+
+// mem_reg2aln's CIGAR stage alone, for alignments whose qb, qe, rb, re,
+// truesc and w are set (extend_seeds runs it when opt.want_cigar): fills
+// cigar, gscore and gw.  Entries with qe <= qb or re <= rb are left empty.
+void global_cigars(const std::vector<SeedJob>& jobs, const fcs_bsw_params& p, const SeedExtOptions& opt,
+                   std::vector<SeedAln>& alns, SeedExtStats& st);
+
+// ksw_global2 scores (no CIGAR) of query[qb, qe) x ref[rb, re) at bwa_gen_cigar2's
+// band for w_ (bwa_cigar_band; the no-gap case scored directly): mem_patch_reg's test.
+struct GlobalScoreJob {
+  const uint8_t* q = nullptr;
+  const uint8_t* ref = nullptr;
+  int qb = 0, qe = 0;
+  int64_t rb = 0, re = 0;
+  int w = 0;
+};
+void global_scores(const std::vector<GlobalScoreJob>& jobs, const fcs_bsw_params& p, int gpu, std::vector<int>& scores,
+                   SeedExtStats& st);
 
 }  // namespace fcsg

@@ -89,19 +89,21 @@ static int gen_cigar(const ext_opt* o, int w_, int l, const uint8_t* query, int6
  * path), out_r = {rb, re}; the CIGAR (ksw ops) in cigar[0 .. *n_cigar).
  * Returns 0, or -1 when the seed lies outside its query or reference.
  */
-int oracle_extend_seed(int l_query, const uint8_t* query, int64_t l_ref, const uint8_t* rseq_all, int qbeg,
-                       int64_t rbeg, int len, const int8_t* mat, int o_del, int e_del, int o_ins, int e_ins,
-                       int zdrop, int w, int pen_clip5, int pen_clip3, int32_t* out_i, int64_t* out_r,
-                       uint32_t* cigar, int cigar_cap, int* n_cigar) {
+int oracle_extend_seed_w(int l_query, const uint8_t* query, int64_t l_ref, const uint8_t* rseq_all, int qbeg,
+                         int64_t rbeg, int len, int64_t win_lo, int64_t win_hi, const int8_t* mat, int o_del,
+                         int e_del, int o_ins, int e_ins, int zdrop, int w, int pen_clip5, int pen_clip3,
+                         int32_t* out_i, int64_t* out_r, uint32_t* cigar, int cigar_cap, int* n_cigar) {
   ext_opt o = {mat, mat[0], o_del, e_del, o_ins, e_ins, zdrop, w, pen_clip5, pen_clip3};
   int64_t rmax[2], b, e;
   int aw[2], max_off, i, score, truesc, qb, qe;
   int64_t rb, re;
   const uint8_t* rseq;
   if (len <= 0 || qbeg < 0 || qbeg + len > l_query || rbeg < 0 || rbeg + len > l_ref) return -1;
-  /* the window of the chain's (single) seed, clipped to the sequence */
+  /* the chain's window: mem_chain2aln's rmax, min / max over the chain's
+     seeds (win_lo, win_hi), or that of this seed alone (-1), clipped to the sequence */
   b = rbeg - (qbeg + cal_max_gap(&o, qbeg));
   e = rbeg + len + ((l_query - qbeg - len) + cal_max_gap(&o, l_query - qbeg - len));
+  if (win_lo >= 0 || win_hi >= 0) b = win_lo, e = win_hi;
   rmax[0] = b > 0 ? b : 0;
   rmax[1] = e < l_ref ? e : l_ref;
   rseq = rseq_all + rmax[0];
@@ -192,4 +194,12 @@ int oracle_extend_seed(int l_query, const uint8_t* query, int64_t l_ref, const u
     out_i[5] = gsc;
   }
   return 0;
+}
+
+int oracle_extend_seed(int l_query, const uint8_t* query, int64_t l_ref, const uint8_t* rseq_all, int qbeg,
+                       int64_t rbeg, int len, const int8_t* mat, int o_del, int e_del, int o_ins, int e_ins,
+                       int zdrop, int w, int pen_clip5, int pen_clip3, int32_t* out_i, int64_t* out_r,
+                       uint32_t* cigar, int cigar_cap, int* n_cigar) {
+  return oracle_extend_seed_w(l_query, query, l_ref, rseq_all, qbeg, rbeg, len, -1, -1, mat, o_del, e_del, o_ins,
+                              e_ins, zdrop, w, pen_clip5, pen_clip3, out_i, out_r, cigar, cigar_cap, n_cigar);
 }

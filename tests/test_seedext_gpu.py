@@ -16,6 +16,10 @@ vp = C.c_void_p
 oracle_lib.lib.oracle_extend_seed.restype = C.c_int
 oracle_lib.lib.oracle_extend_seed.argtypes = ([C.c_int, vp, C.c_int64, vp, C.c_int, C.c_int64, C.c_int, vp] +
                                               [C.c_int] * 8 + [vp, vp, vp, C.c_int, vp])
+oracle_lib.lib.oracle_extend_seed_w.restype = C.c_int
+oracle_lib.lib.oracle_extend_seed_w.argtypes = ([C.c_int, vp, C.c_int64, vp, C.c_int, C.c_int64, C.c_int,
+                                                 C.c_int64, C.c_int64, vp] +
+                                                [C.c_int] * 8 + [vp, vp, vp, C.c_int, vp])
 MAT = np.array([1 if i == j else -4 for i in range(4) for j in range(4)], np.int8)
 MAT5 = np.zeros(25, np.int8)
 for i in range(5):
@@ -23,15 +27,20 @@ for i in range(5):
         MAT5[i * 5 + j] = -1 if (i == 4 or j == 4) else (1 if i == j else -4)
 
 
-def oracle(q, ref, sq, sr, sl, w=100, clip5=5, clip3=5):
+def oracle(q, ref, sq, sr, sl, w=100, clip5=5, clip3=5, win=None):
     oi = np.zeros(7, np.int32)
     orr = np.zeros(2, np.int64)
     cap = len(q) + 4 * w + 64
     cig = np.zeros(cap, np.uint32)
     nc = C.c_int()
-    rc = oracle_lib.lib.oracle_extend_seed(len(q), q.ctypes.data, len(ref), ref.ctypes.data, sq, sr, sl,
-                                           MAT5.ctypes.data, 6, 1, 6, 1, 100, w, clip5, clip3, oi.ctypes.data,
-                                           orr.ctypes.data, cig.ctypes.data, cap, C.byref(nc))
+    if win is None:
+        rc = oracle_lib.lib.oracle_extend_seed(len(q), q.ctypes.data, len(ref), ref.ctypes.data, sq, sr, sl,
+                                               MAT5.ctypes.data, 6, 1, 6, 1, 100, w, clip5, clip3, oi.ctypes.data,
+                                               orr.ctypes.data, cig.ctypes.data, cap, C.byref(nc))
+    else:
+        rc = oracle_lib.lib.oracle_extend_seed_w(len(q), q.ctypes.data, len(ref), ref.ctypes.data, sq, sr, sl,
+                                                 win[0], win[1], MAT5.ctypes.data, 6, 1, 6, 1, 100, w, clip5, clip3,
+                                                 oi.ctypes.data, orr.ctypes.data, cig.ctypes.data, cap, C.byref(nc))
     assert rc == 0
     return oi, orr, cig[:nc.value]
 
@@ -129,13 +138,27 @@ def test_extend_seeds_match_oracle(gpu, w):
     oi = np.zeros((n, 7), np.int32)
     orr = np.zeros((n, 2), np.int64)
     nc = np.zeros(n, np.int32)
+    # every third job carries a chain window (mem_chain2aln's rmax spans all
+    # the chain's seeds): the seed's own window widened by up to 80 bases per side
+    rng = np.random.default_rng(w)
+    wlo = np.full(n, -1, np.int64)
+    whi = np.full(n, -1, np.int64)
+    for i in range(0, n, 3):
+        L = int(qlen[i])
+        mg = lambda x: max(1, min(max(int((x - 6) / 1 + 1.), int((x - 6) / 1 + 1.)), 2 * w))  # noqa: E731
+        b = int(sr[i]) - (int(sq[i]) + mg(int(sq[i])))
+        rest = L - int(sq[i]) - int(sl[i])
+        e = int(sr[i]) + int(sl[i]) + rest + mg(rest)
+        wlo[i] = max(0, b - int(rng.integers(0, 81)))
+        whi[i] = min(len(ref), e + int(rng.integers(0, 81)))
     P = lambda a: a.ctypes.data  # noqa: E731
     H.check(H.lib.fcsg_extend_seeds(n, vp(P(qbuf)), vp(P(qoff)), vp(P(qlen)), vp(P(ref)), C.c_int64(len(ref)),
                                     vp(P(sq)), vp(P(sr)), vp(P(sl)), w, 5, 5, 0, vp(P(oi)), vp(P(orr)), vp(P(cig)),
-                                    vp(P(coff)), vp(P(cap)), vp(P(nc))))
+                                    vp(P(coff)), vp(P(cap)), vp(P(nc)), vp(P(wlo)), vp(P(whi))))
     kinds = set()
     for i in range(n):
-        e_i, e_r, e_c = oracle(qs[i], ref, int(sq[i]), int(sr[i]), int(sl[i]), w=w)
+        win = None if wlo[i] < 0 else (int(wlo[i]), int(whi[i]))
+        e_i, e_r, e_c = oracle(qs[i], ref, int(sq[i]), int(sr[i]), int(sl[i]), w=w, win=win)
         got_c = cig[coff[i]:coff[i] + nc[i]]
         assert list(oi[i]) == list(e_i) and list(orr[i]) == list(e_r), (i, oi[i], e_i, orr[i], e_r)
         assert np.array_equal(got_c, e_c), i
