@@ -3,6 +3,7 @@
 #include <zlib.h>
 
 #include <algorithm>
+#include <array>
 #include <cmath>
 #include <condition_variable>
 #include <cstring>
@@ -52,65 +53,124 @@ std::string revcomp(const std::string& s) {
   return o;
 }
 
-// One candidate placement of a read: a chain's seed (a maximal exact match)
-// and, after the GPU extension round, its alignment.
+// A seed: one exact match of the oriented read on a contig (bwa's mem_seed_t;
+// reverse-strand hits use the reverse-complemented read on the forward contig).
+struct Seed {
+  int contig = -1;
+  bool rev = false;
+  int qbeg = 0, len = 0;  // on the oriented read
+  int64_t rbeg = 0;       // forward-contig offset
+};
+
+// A chain of colinear seeds (bwa's mem_chain_t), with mem_chain_flt's marks.
+struct Chain {
+  int contig = -1;
+  bool rev = false;
+  std::vector<Seed> s;  // in the order they joined (query start)
+  int weight = 0;
+  int kept = 0, first = -1;
+  int qb = 0, qe = 0;   // query span [first seed start, last seed end) on the ORIGINAL read
+};
+
+// One alignment region of a read (bwa's mem_alnreg_t): the extension of one
+// seed (or a mate-rescue hit), on the oriented read / forward contig.
 struct Cand {
   bool rev = false;
   int contig = -1;
-  int hits = 0;  // k-mer hits of the chain
   int seed_q = 0, seed_len = 0;
   int64_t seed_r = 0;
-  SeedAln aln;
+  int64_t win_lo = -1, win_hi = -1;  // the chain's reference window (-1: the seed's own)
+  int seedcov = 0;                   // query bases of the chain's seeds inside the region
+  SeedAln aln;                       // qb, qe, rb, re, score, truesc, w (+ CIGAR for output regions)
+  int sub = 0, sub_n = 0, secondary = -1;
+  uint64_t hash = 0;
+  double frac_rep = 0;  // the read's repetitive fraction (bwa's frac_rep; 0 for rescued hits)
+  bool rescued = false; // a mate-rescue hit (seedcov = half the shorter span)
   bool done = false;  // extended
-  bool ok = false;    // extension produced an alignment with a CIGAR
+  bool ok = false;    // has an alignment (qe > qb, re > rb)
 };
 
-// One read: both orientations and its candidates.
+// One read: both orientations, chains, regions and the extension cursor.
 struct ReadAln {
   std::string seq[2];            // forward, reverse complement
   std::vector<uint8_t> code[2];  // codes of seq[]
+  std::vector<Chain> chains;
   std::vector<Cand> cands;
-  int best = -1;      // index into cands of the primary alignment
-  int sub = 0;        // best score of another locus (bwa's a->sub), 0 if none
-  int sub_n = 0;      // other loci scoring close to the best
+  // mem_chain2aln's loop state: chain ci, its seeds by score (srt), position k
+  size_t ci = 0;
+  int k = -1;
+  std::vector<uint64_t> srt;
+  int best = -1;     // primary region
+  std::vector<int> supp;  // supplementary regions (non-overlapping parts of a chimeric read)
   int mapq = 0;
+  double frac_rep = 0;  // query fraction under SMEMs with more than max_occ hits
+  std::vector<std::pair<int, int>> outs;  // output regions and their MAPQ (first: primary)
 };
-
-// bwa mem_approx_mapq_se (MEM_MAPQ_COEF 30, mapQ_coef_len 0): the primary's
-// score against the best other locus, scaled by the seed coverage and identity.
-int approx_mapq_se(const SeedAln& a, int sub, int sub_n, int seedcov, int min_seed_len, int match, int mismatch) {
-  sub = sub ? sub : min_seed_len * match;
-  if (sub >= a.truesc || a.truesc <= 0) return 0;
-  const int l = std::max(a.qe - a.qb, (int)(a.re - a.rb));
-  const double identity = 1. - (double)(l * match - a.truesc) / (match + mismatch) / l;
-  int mapq = (int)(30.0 * (1. - (double)sub / a.truesc) * std::log((double)std::max(seedcov, 1)) + .499);
-  if (identity < 0.95) mapq = (int)(mapq * identity * identity + .499);
-  if (sub_n > 0) mapq -= (int)(4.343 * std::log((double)sub_n + 1) + .499);
-  return std::max(0, std::min(60, mapq));
-}
 
 int64_t aln_pos(const Cand& c) { return c.aln.rb; }
 int64_t aln_end(const Cand& c) { return c.aln.re; }
+// query span of a region on the ORIGINAL read
+int orig_qb(const Cand& c, int L) { return c.rev ? L - c.aln.qe : c.aln.qb; }
+int orig_qe(const Cand& c, int L) { return c.rev ? L - c.aln.qb : c.aln.qe; }
 
-// Seeds and chains of one read (bwa mem_collect_intv + mem_chain): SMEMs of
-// length >= min_seed_len on the FMD-index (both strands at once), re-seeds
-// inside long, rare SMEMs and the third-round forward seeds; every occurrence (sampled down to max_occ per
-// SMEM) is a seed; seeds join a chain of the same contig and strand when they
-// continue it (bwa test_and_merge: colinear, diagonal within w, gaps below
-// max_chain_gap); chains weighed by the query bases their seeds cover; up to
-// max_chains chains with at least drop_ratio x the best weight become
-// candidates, each extended from its longest seed.
-void seed_read(const Reference& ref, const KmerIndex& idx, const AlignOptions& opt, ReadAln& R) {
+uint64_t hash64(uint64_t key) {  // bwa's hash_64 (Thomas Wang)
+  key += ~(key << 32);
+  key ^= (key >> 22);
+  key += ~(key << 13);
+  key ^= (key >> 8);
+  key += (key << 3);
+  key ^= (key >> 15);
+  key += ~(key << 27);
+  key ^= (key >> 31);
+  return key;
+}
+
+// bwa raw_mapq.
+int raw_mapq(int diff, int a) { return (int)(6.02 * diff / a + .499); }
+
+// bwa mem_approx_mapq_se (MEM_MAPQ_COEF 30, mapQ_coef_len 0; csub is 0: no
+// sub-optimal score comes out of ksw_extend2).
+int approx_mapq_se(const Cand& c, int min_seed_len, int match, int mismatch) {
+  const SeedAln& a = c.aln;
+  int sub = c.sub ? c.sub : min_seed_len * match;
+  if (sub >= a.score || a.score <= 0) return 0;
+  const int l = std::max(a.qe - a.qb, (int)(a.re - a.rb));
+  const double identity = 1. - (double)(l * match - a.score) / (match + mismatch) / l;
+  int mapq = (int)(30.0 * (1. - (double)sub / a.score) * std::log((double)std::max(c.seedcov, 1)) + .499);
+  if (identity < 0.95) mapq = (int)(mapq * identity * identity + .499);
+  if (c.sub_n > 0) mapq -= (int)(4.343 * std::log((double)c.sub_n + 1) + .499);
+  mapq = std::max(0, std::min(60, mapq));
+  return (int)(mapq * (1. - c.frac_rep) + .499);
+}
+
+// Seeds and chains of one read (bwa mem_collect_intv + mem_chain +
+// mem_chain_flt): SMEMs of length >= min_seed_len on the FMD-index (both
+// strands at once), re-seeds inside long, rare SMEMs and the third-round
+// forward seeds; every occurrence (sampled down to max_occ per SMEM) is a seed;
+// seeds join a chain of the same contig and strand when they continue it (bwa
+// test_and_merge: colinear, diagonal within w, gaps below max_chain_gap);
+// chains are weighed by the query bases their seeds cover, then filtered:
+// a chain that overlaps a kept heavier one on the query by >= mask_level of
+// the shorter and weighs < drop_ratio of it (and 2 min_seed_len less) is
+// dropped (the first such shadowed chain is kept for MAPQ, as bwa does).
+void seed_read(const KmerIndex& idx, const AlignOptions& opt, ReadAln& R) {
   const std::vector<uint8_t>& q = R.code[0];
   const int L = (int)q.size();
   std::vector<BiInterval> mems;
   idx.fmd().collect(q.data(), L, opt.k, (int)(opt.k * 1.5 + .499), 10, 20, mems);  // bwa -r 1.5, -y 20
-  struct Seed {
-    int contig;
-    bool rev;
-    int qbeg, len;
-    int64_t rbeg;
-  };
+  {  // bwa mem_chain's frac_rep: the union of the query spans of SMEMs with > max_occ hits
+    std::vector<std::pair<int, int>> rep;
+    for (const BiInterval& m : mems)
+      if (m.s > opt.max_occ) rep.emplace_back(m.qb, m.qe);
+    std::sort(rep.begin(), rep.end());
+    int b = 0, e = 0, l_rep = 0;
+    for (const auto& [sb, se] : rep) {
+      if (sb > e) l_rep += e - b, b = sb, e = se;
+      else e = std::max(e, se);
+    }
+    l_rep += e - b;
+    R.frac_rep = L ? (double)l_rep / L : 0.;
+  }
   std::vector<Seed> seeds;
   for (const BiInterval& m : mems) {
     const int64_t step = m.s > opt.max_occ ? m.s / opt.max_occ : 1;
@@ -127,14 +187,7 @@ void seed_read(const Reference& ref, const KmerIndex& idx, const AlignOptions& o
     return a.contig != b.contig ? a.contig < b.contig : a.rev != b.rev ? a.rev < b.rev
          : a.qbeg != b.qbeg ? a.qbeg < b.qbeg : a.rbeg < b.rbeg;
   });
-  struct Chain {
-    int contig;
-    bool rev;
-    std::vector<Seed> s;
-    int weight = 0;
-  };
   std::vector<Chain> chains;
-  const int max_chain_gap = 10000;
   size_t group0 = 0;
   for (size_t i = 0; i < seeds.size(); ++i) {
     const Seed& sd = seeds[i];
@@ -148,12 +201,19 @@ void seed_read(const Reference& ref, const KmerIndex& idx, const AlignOptions& o
         break;
       }
       const int64_t x = sd.qbeg - last.qbeg, y = sd.rbeg - last.rbeg;
-      if (y >= 0 && x - y <= opt.w && y - x <= opt.w && x - last.len < max_chain_gap && y - last.len < max_chain_gap) {
+      if (y >= 0 && x - y <= opt.w && y - x <= opt.w && x - last.len < opt.max_chain_gap &&
+          y - last.len < opt.max_chain_gap) {
         chains[c].s.push_back(sd);
         merged = true;
       }
     }
-    if (!merged) chains.push_back({sd.contig, sd.rev, {sd}, 0});
+    if (!merged) {
+      Chain ch;
+      ch.contig = sd.contig;
+      ch.rev = sd.rev;
+      ch.s.push_back(sd);
+      chains.push_back(std::move(ch));
+    }
   }
   for (Chain& ch : chains) {  // bwa mem_chain_weight: query bases covered by the seeds (min with the reference's)
     int64_t wq = 0, wr = 0, endq = 0, endr = 0;
@@ -165,40 +225,203 @@ void seed_read(const Reference& ref, const KmerIndex& idx, const AlignOptions& o
     std::vector<const Seed*> byr;
     for (const Seed& sd : ch.s) byr.push_back(&sd);
     std::sort(byr.begin(), byr.end(), [](const Seed* a, const Seed* b) { return a->rbeg < b->rbeg; });
-    endr = 0;
     for (const Seed* sd : byr) {
       if (sd->rbeg >= endr) wr += sd->len;
       else if (sd->rbeg + sd->len > endr) wr += sd->rbeg + sd->len - endr;
       endr = std::max<int64_t>(endr, sd->rbeg + sd->len);
     }
     ch.weight = (int)std::min(wq, wr);
+    const int b = ch.s.front().qbeg, e = ch.s.back().qbeg + ch.s.back().len;  // oriented
+    ch.qb = ch.rev ? L - e : b;
+    ch.qe = ch.rev ? L - b : e;
   }
+  // ---- bwa mem_chain_flt
   std::stable_sort(chains.begin(), chains.end(), [](const Chain& a, const Chain& b) { return a.weight > b.weight; });
-  const int best_w = chains[0].weight;
-  for (const Chain& ch : chains) {
-    if ((int)R.cands.size() >= opt.max_chains || ch.weight < opt.drop_ratio * best_w) break;
-    const Seed* top = &ch.s[0];
-    for (const Seed& sd : ch.s)
-      if (sd.len > top->len) top = &sd;
-    Cand C;
-    C.rev = ch.rev;
-    C.contig = ch.contig;
-    C.hits = ch.weight;
-    C.seed_q = top->qbeg;
-    C.seed_len = top->len;
-    C.seed_r = top->rbeg;
-    R.cands.push_back(std::move(C));
+  std::vector<int> kept{0};
+  chains[0].kept = 3;
+  for (int i = 1; i < (int)chains.size(); ++i) {
+    bool large_ovlp = false;
+    size_t k = 0;
+    for (; k < kept.size(); ++k) {
+      Chain& cj = chains[kept[k]];
+      const Chain& ci = chains[i];
+      const int b_max = std::max(cj.qb, ci.qb), e_min = std::min(cj.qe, ci.qe);
+      if (e_min > b_max) {
+        const int li = ci.qe - ci.qb, lj = cj.qe - cj.qb, min_l = std::min(li, lj);
+        if (e_min - b_max >= min_l * opt.mask_level && min_l < opt.max_chain_gap) {
+          large_ovlp = true;
+          if (cj.first < 0) cj.first = i;
+          if (ci.weight < cj.weight * opt.drop_ratio && cj.weight - ci.weight >= opt.k << 1) break;
+        }
+      }
+    }
+    if (k == kept.size()) {
+      kept.push_back(i);
+      chains[i].kept = large_ovlp ? 2 : 3;
+    }
+  }
+  for (int j : kept)
+    if (chains[j].first >= 0) chains[chains[j].first].kept = 1;
+  for (Chain& ch : chains)
+    if (ch.kept > 0) R.chains.push_back(std::move(ch));
+}
+
+// mem_chain2aln's test: is seed s (almost) inside a region already made? (then
+// extending it would repeat that alignment)
+bool seed_covered(const Seed& s, const std::vector<Cand>& regs, int L, const fcs_bsw_params& P, int w) {
+  for (const Cand& p : regs) {
+    if (!p.done || p.contig != s.contig || p.rev != s.rev) continue;
+    const SeedAln& a = p.aln;
+    if (s.rbeg < a.rb || s.rbeg + s.len > a.re || s.qbeg < a.qb || s.qbeg + s.len > a.qe) continue;
+    if (s.len - p.seed_len > .1 * L) continue;  // this seed may give a better alignment
+    int64_t qd = s.qbeg - a.qb, rd = s.rbeg - a.rb;  // ahead of the seed
+    int mg = bwa_cal_max_gap(P, (int)std::min<int64_t>(qd, rd), w);
+    int ww = std::min(mg, a.w);
+    if (qd - rd < ww && rd - qd < ww) return true;
+    qd = a.qe - (s.qbeg + s.len), rd = a.re - (s.rbeg + s.len);  // behind it
+    mg = bwa_cal_max_gap(P, (int)std::min<int64_t>(qd, rd), w);
+    ww = std::min(mg, a.w);
+    if (qd - rd < ww && rd - qd < ww) return true;
+  }
+  return false;
+}
+
+// One GPU extension round per step of mem_chain2aln over every read: each read
+// with work left extends its next seed that no earlier region covers (chains
+// in mem_chain_flt order, seeds by length, longest first); the extension's
+// region joins the read's list before the read's next seed is tested, as in
+// bwa's sequential loop.  Regions get the chain's reference window.
+void extend_chains(const KmerIndex& idx, const fcs_bsw_params& P, const AlignOptions& opt,
+                   std::vector<ReadAln>& reads, AlignStats& st) {
+  std::vector<ReadAln*> active;
+  for (ReadAln& R : reads) {
+    R.ci = 0;
+    R.k = -1;
+    R.srt.clear();
+    if (!R.chains.empty()) active.push_back(&R);
+  }
+  // the next seed of read R to extend: its region is appended (not yet done);
+  // false when the read's chains are exhausted
+  auto next_seed = [&](ReadAln& R) {
+    const int L = (int)R.code[0].size();
+    while (R.ci < R.chains.size()) {
+      const Chain& c = R.chains[R.ci];
+      if (R.k < 0 && R.srt.empty()) {
+        R.srt.resize(c.s.size());
+        for (size_t i = 0; i < c.s.size(); ++i) R.srt[i] = (uint64_t)c.s[i].len << 32 | i;
+        std::sort(R.srt.begin(), R.srt.end());
+        R.k = (int)c.s.size() - 1;
+      }
+      int pick = -1;
+      for (; R.k >= 0; --R.k) {
+        const Seed& s = c.s[(uint32_t)R.srt[R.k]];
+        if (seed_covered(s, R.cands, L, P, opt.w)) {
+          // unless an already extended, long overlapping seed of this chain sits on another diagonal
+          size_t i = R.k + 1;
+          for (; i < c.s.size(); ++i) {
+            if (R.srt[i] == 0) continue;
+            const Seed& t = c.s[(uint32_t)R.srt[i]];
+            if (t.len < s.len * .95) continue;
+            if (s.qbeg <= t.qbeg && s.qbeg + s.len - t.qbeg >= s.len >> 2 && t.qbeg - s.qbeg != t.rbeg - s.rbeg)
+              break;
+            if (t.qbeg <= s.qbeg && t.qbeg + t.len - s.qbeg >= s.len >> 2 && s.qbeg - t.qbeg != s.rbeg - t.rbeg)
+              break;
+          }
+          if (i == c.s.size()) {
+            R.srt[R.k] = 0;  // not extended
+            continue;
+          }
+        }
+        pick = (int)(uint32_t)R.srt[R.k];
+        --R.k;
+        break;
+      }
+      if (pick < 0) {  // chain done
+        ++R.ci;
+        R.k = -1;
+        R.srt.clear();
+        continue;
+      }
+      // the chain's window: min / max over its seeds (bwa's rmax), clipped to the contig
+      int64_t lo = INT64_MAX, hi = INT64_MIN;
+      for (const Seed& t : c.s) {
+        const int rest = L - t.qbeg - t.len;
+        lo = std::min(lo, t.rbeg - (t.qbeg + bwa_cal_max_gap(P, t.qbeg, opt.w)));
+        hi = std::max(hi, t.rbeg + t.len + rest + bwa_cal_max_gap(P, rest, opt.w));
+      }
+      const Seed& s = c.s[pick];
+      Cand C;
+      C.rev = c.rev;
+      C.contig = c.contig;
+      C.seed_q = s.qbeg;
+      C.seed_len = s.len;
+      C.seed_r = s.rbeg;
+      C.win_lo = std::max<int64_t>(0, lo);
+      C.win_hi = std::min<int64_t>(hi, (int64_t)idx.codes(c.contig).size());
+      C.frac_rep = R.frac_rep;
+      R.cands.push_back(std::move(C));
+      return true;
+    }
+    return false;
+  };
+  while (!active.empty()) {
+    std::vector<char> has(active.size());
+    parallel_for(active.size(), opt.threads, [&](size_t i) { has[i] = next_seed(*active[i]); });
+    std::vector<ReadAln*> now;
+    for (size_t i = 0; i < active.size(); ++i)
+      if (has[i]) now.push_back(active[i]);
+    active.swap(now);
+    if (active.empty()) break;
+    std::vector<SeedJob> jobs(active.size());
+    for (size_t i = 0; i < active.size(); ++i) {
+      const ReadAln& R = *active[i];
+      const Cand& cc = R.cands.back();
+      const std::vector<uint8_t>& rc = idx.codes(cc.contig);
+      SeedJob& J = jobs[i];
+      J.q = R.code[cc.rev].data();
+      J.qlen = (int)R.code[0].size();
+      J.ref = rc.data();
+      J.rlen = (int64_t)rc.size();
+      J.seed_q = cc.seed_q;
+      J.seed_r = cc.seed_r;
+      J.seed_len = cc.seed_len;
+      J.win_lo = cc.win_lo;
+      J.win_hi = cc.win_hi;
+    }
+    SeedExtOptions so;
+    so.w = opt.w;
+    so.pen_clip5 = so.pen_clip3 = P.end_bonus;
+    so.gpu = opt.gpu;
+    so.threads = opt.threads;
+    so.want_cigar = false;
+    std::vector<SeedAln> res;
+    SeedExtStats xs;
+    extend_seeds(jobs, P, so, res, xs);
+    st.ext_tasks += xs.ext_tasks;
+    st.gpu_seconds += xs.gpu_seconds;
+    parallel_for(active.size(), opt.threads, [&](size_t i) {
+      ReadAln& R = *active[i];
+      Cand& C = R.cands.back();
+      C.aln = std::move(res[i]);
+      C.done = true;
+      C.ok = C.aln.qe > C.aln.qb && C.aln.re > C.aln.rb;
+      for (const Seed& t : R.chains[R.ci].s)  // bwa's seedcov over the chain's seeds
+        if (t.qbeg >= C.aln.qb && t.qbeg + t.len <= C.aln.qe && t.rbeg >= C.aln.rb && t.rbeg + t.len <= C.aln.re)
+          C.seedcov += t.len;
+    });
   }
 }
 
-// One GPU extension round over every pending candidate of `reads`.
-void extend_cands(const KmerIndex& idx, const fcs_bsw_params& P, const AlignOptions& opt, std::vector<ReadAln*>& reads,
-                  bool only_new, AlignStats& st) {
+// Extension round for the mate-rescue hits (regions without a chain): each
+// extends inside its rescue window; bwa mem_matesw keeps a hit scoring >=
+// min_seed_len (x match) with seedcov = half the shorter span.
+void extend_loose(const KmerIndex& idx, const fcs_bsw_params& P, const AlignOptions& opt, std::vector<ReadAln*>& reads,
+                  AlignStats& st) {
   std::vector<SeedJob> jobs;
   std::vector<Cand*> who;
   for (ReadAln* R : reads)
     for (Cand& C : R->cands) {
-      if (only_new && C.done) continue;
+      if (C.done) continue;
       const std::vector<uint8_t>& rc = idx.codes(C.contig);
       SeedJob J;
       J.q = R->code[C.rev].data();
@@ -208,6 +431,8 @@ void extend_cands(const KmerIndex& idx, const fcs_bsw_params& P, const AlignOpti
       J.seed_q = C.seed_q;
       J.seed_r = C.seed_r;
       J.seed_len = C.seed_len;
+      J.win_lo = C.win_lo;
+      J.win_hi = C.win_hi;
       jobs.push_back(J);
       who.push_back(&C);
     }
@@ -217,186 +442,595 @@ void extend_cands(const KmerIndex& idx, const fcs_bsw_params& P, const AlignOpti
   so.pen_clip5 = so.pen_clip3 = P.end_bonus;
   so.gpu = opt.gpu;
   so.threads = opt.threads;
+  so.want_cigar = false;
   std::vector<SeedAln> res;
   SeedExtStats xs;
   extend_seeds(jobs, P, so, res, xs);
   st.ext_tasks += xs.ext_tasks;
-  st.global_tasks += xs.global_tasks;
   st.gpu_seconds += xs.gpu_seconds;
   for (size_t i = 0; i < who.size(); ++i) {
     Cand& C = *who[i];
     C.aln = std::move(res[i]);
     C.done = true;
-    C.ok = C.aln.qe > C.aln.qb && C.aln.re > C.aln.rb && !C.aln.cigar.empty();
+    C.ok = C.aln.qe > C.aln.qb && C.aln.re > C.aln.rb && C.aln.score >= opt.k * P.mat[0];
+    C.seedcov = (int)(std::min<int64_t>(C.aln.re - C.aln.rb, C.aln.qe - C.aln.qb) >> 1);
   }
 }
 
-// Primary alignment, the best other locus (bwa's sub) and the single-end MAPQ.
-void pick_primary(ReadAln& R, const AlignOptions& opt) {
+// bwa mem_sort_dedup_patch for every read: regions redundant with a
+// better one (overlap > mask_level_redun of both the query and the reference
+// spans) are dropped; colinear neighbours on one strand whose joint global
+// alignment keeps >= 90% of the predicted score are merged into one region
+// (mem_patch_reg: the joint ksw_global2 scores run as GPU rounds); then
+// identical hits are dropped.  patch false: redundancy and identity only (bwa
+// calls it so on the mate-rescue list, mem_matesw).
+void dedup_patch(const KmerIndex& idx, const fcs_bsw_params& P, const AlignOptions& opt,
+                 const std::vector<ReadAln*>& reads, bool patch, AlignStats& st) {
+  // bwa's loop `for i, for j = i - 1 down`, resumable where a patch needs its
+  // global score (one GPU batch per round over all reads)
+  struct Scan {
+    std::vector<int> order;  // region indices by reference end
+    size_t i = 1;
+    int j = -2;              // -2: p's inner loop not started
+    int w = 0;               // band of the pending patch (q = order[j])
+    bool done = false;
+  };
+  std::vector<Scan> sc(reads.size());
+  for (size_t r = 0; r < reads.size(); ++r) {
+    ReadAln& R = *reads[r];
+    std::vector<Cand> keep;
+    for (Cand& c : R.cands)
+      if (c.ok) keep.push_back(std::move(c));
+    R.cands.swap(keep);
+    Scan& S = sc[r];
+    for (size_t k = 0; k < R.cands.size(); ++k) S.order.push_back((int)k);
+    // bwa sorts by the END position (mem_ars2), contig and strand first (its 2L coordinates)
+    std::stable_sort(S.order.begin(), S.order.end(), [&](int a, int b) {
+      const Cand &x = R.cands[a], &y = R.cands[b];
+      if (x.contig != y.contig) return x.contig < y.contig;
+      if (x.rev != y.rev) return x.rev < y.rev;
+      return x.aln.re < y.aln.re;
+    });
+    S.done = R.cands.size() <= 1;
+  }
+  const double redun = opt.mask_level_redun;
+  for (;;) {
+    std::vector<GlobalScoreJob> jobs;
+    std::vector<size_t> jr;
+    for (size_t r = 0; r < reads.size(); ++r) {
+      Scan& S = sc[r];
+      ReadAln& R = *reads[r];
+      while (!S.done) {
+        if (S.i >= S.order.size()) {
+          S.done = true;
+          break;
+        }
+        Cand& p = R.cands[S.order[S.i]];
+        auto near = [&](const Cand& q) {
+          return q.contig == p.contig && q.rev == p.rev && p.aln.rb < q.aln.re + opt.max_chain_gap;
+        };
+        if (S.j == -2) {
+          if (!near(R.cands[S.order[S.i - 1]])) {
+            ++S.i;
+            continue;
+          }
+          S.j = (int)S.i - 1;
+        }
+        bool wait = false;
+        for (; S.j >= 0 && near(R.cands[S.order[S.j]]); --S.j) {
+          Cand& q = R.cands[S.order[S.j]];
+          if (q.aln.qe == q.aln.qb) continue;  // excluded
+          const int64_t or_ = q.aln.re - p.aln.rb;
+          const int64_t oq = q.aln.qb < p.aln.qb ? q.aln.qe - p.aln.qb : p.aln.qe - q.aln.qb;
+          const int64_t mr = std::min(q.aln.re - q.aln.rb, p.aln.re - p.aln.rb);
+          const int64_t mq = std::min(q.aln.qe - q.aln.qb, p.aln.qe - p.aln.qb);
+          if (or_ > redun * mr && oq > redun * mq) {  // one of the hits is redundant
+            if (p.aln.score < q.aln.score) {
+              p.aln.qe = p.aln.qb;
+              break;
+            }
+            q.aln.qe = q.aln.qb;
+            continue;
+          }
+          if (!patch || q.aln.rb >= p.aln.rb) continue;
+          // mem_patch_reg(q, p): colinear, a band within 2w (4w when they overlap) and a
+          // relative band below 0.05 (0.10)
+          const SeedAln &a = q.aln, &b = p.aln;
+          if (a.qb >= b.qb || a.qe >= b.qe || a.re >= b.re) continue;
+          int w = (int)std::llabs((a.re - b.rb) - (int64_t)(a.qe - b.qb));
+          const double rr = std::fabs((double)(a.re - b.rb) / (double)(b.re - a.rb) -
+                                      (double)(a.qe - b.qb) / (double)(b.qe - a.qb));
+          if (a.re < b.rb || a.qe < b.qb) {
+            if (w > opt.w << 1 || rr >= 0.05) continue;
+          } else if (w > opt.w << 2 || rr >= 0.10) {
+            continue;
+          }
+          S.w = std::min(w + a.w + b.w, opt.w << 2);
+          GlobalScoreJob J;
+          J.q = R.code[p.rev].data();
+          J.ref = idx.codes(p.contig).data();
+          J.qb = a.qb;
+          J.qe = b.qe;
+          J.rb = a.rb;
+          J.re = b.re;
+          J.w = S.w;
+          jobs.push_back(J);
+          jr.push_back(r);
+          wait = true;
+          break;
+        }
+        if (wait) break;
+        ++S.i;
+        S.j = -2;
+      }
+    }
+    if (jobs.empty()) break;
+    std::vector<int> scores;
+    SeedExtStats xs;
+    global_scores(jobs, P, opt.gpu, scores, xs);
+    st.global_tasks += xs.global_tasks;
+    st.gpu_seconds += xs.gpu_seconds;
+    for (size_t k = 0; k < jr.size(); ++k) {
+      Scan& S = sc[jr[k]];
+      ReadAln& R = *reads[jr[k]];
+      Cand& p = R.cands[S.order[S.i]];
+      Cand& q = R.cands[S.order[S.j]];
+      const SeedAln &a = q.aln, &b = p.aln;
+      const int score = scores[k];
+      // predicted scores from the query and the reference spans; merge at >= 90% of the larger
+      const int q_s = (int)((double)(b.qe - a.qb) / ((b.qe - b.qb) + (a.qe - a.qb)) * (b.score + a.score) + .499);
+      const int r_s = (int)((double)(b.re - a.rb) / ((b.re - b.rb) + (a.re - a.rb)) * (b.score + a.score) + .499);
+      if (score > 0 && (double)score / std::max(q_s, r_s) >= 0.90) {  // merge q into p
+        p.seedcov = std::max(p.seedcov, q.seedcov);
+        p.aln.qb = q.aln.qb;
+        p.aln.rb = q.aln.rb;
+        p.aln.truesc = p.aln.score = score;
+        p.aln.w = S.w;
+        q.aln.qb = q.aln.qe;  // excluded
+      }
+      --S.j;  // the inner loop goes on below q
+    }
+  }
+  for (ReadAln* Rp : reads) {
+    ReadAln& R = *Rp;
+    std::vector<Cand> keep;
+    for (Cand& c : R.cands)
+      if (c.aln.qe > c.aln.qb) keep.push_back(std::move(c));
+    // identical hits: same score and start on the query and the reference (mem_ars order)
+    std::stable_sort(keep.begin(), keep.end(), [](const Cand& x, const Cand& y) {
+      if (x.aln.score != y.aln.score) return x.aln.score > y.aln.score;
+      if (x.contig != y.contig) return x.contig < y.contig;
+      if (x.rev != y.rev) return x.rev < y.rev;
+      if (x.aln.rb != y.aln.rb) return x.aln.rb < y.aln.rb;
+      return x.aln.qb < y.aln.qb;
+    });
+    R.cands.clear();
+    for (Cand& c : keep) {
+      const Cand* prev = R.cands.empty() ? nullptr : &R.cands.back();
+      if (prev && prev->aln.score == c.aln.score && prev->contig == c.contig && prev->rev == c.rev &&
+          prev->aln.rb == c.aln.rb && prev->aln.qb == c.aln.qb)
+        continue;
+      R.cands.push_back(std::move(c));
+    }
+  }
+}
+
+// Primary = the first non-secondary region scoring >= min_out_score (bwa -T),
+// supplementary = the later ones (bwa mem_reg2sam); MAPQ of the primary.
+void pick_outputs(ReadAln& R, const AlignOptions& opt, const fcs_bsw_params& P) {
   R.best = -1;
-  for (int i = 0; i < (int)R.cands.size(); ++i) {
-    const Cand& C = R.cands[i];
-    if (!C.ok) continue;
-    if (R.best < 0 || C.aln.truesc > R.cands[R.best].aln.truesc ||
-        (C.aln.truesc == R.cands[R.best].aln.truesc && C.hits > R.cands[R.best].hits))
-      R.best = i;
-  }
-  R.sub = 0;
-  R.sub_n = 0;
+  R.supp.clear();
   R.mapq = 0;
-  if (R.best < 0) return;
-  const Cand& B = R.cands[R.best];
-  const int L = (int)R.code[0].size();
   for (int i = 0; i < (int)R.cands.size(); ++i) {
-    const Cand& C = R.cands[i];
-    if (i == R.best || !C.ok) continue;
-    const bool same_locus = C.contig == B.contig && C.rev == B.rev && std::llabs(C.aln.rb - B.aln.rb) < L / 2;
-    if (same_locus) continue;
-    R.sub = std::max(R.sub, C.aln.truesc);
-    if (C.aln.truesc >= B.aln.truesc - 5) ++R.sub_n;  // bwa: other hits within the mapQ_coef window
+    const Cand& c = R.cands[i];
+    if (c.secondary >= 0 || c.aln.score < opt.min_out_score) continue;
+    if (R.best < 0) R.best = i;
+    else R.supp.push_back(i);
   }
-  R.mapq = approx_mapq_se(B.aln, R.sub, R.sub_n, std::max(B.hits, B.seed_len), opt.k, 1, 4);
+  if (R.best >= 0) R.mapq = approx_mapq_se(R.cands[R.best], opt.k, P.mat[0], -P.mat[1]);
 }
 
-// Insert-size distribution of one batch (bwa mem_pestat, FR orientation):
-// quartiles of the fragment lengths of confidently placed pairs; proper pairs
-// lie in [p25 - 3 IQR, p75 + 3 IQR] (at least mean +- 4 sd), mean / sd over the
-// values within [p25 - 2 IQR, p75 + 2 IQR].
+// bwa mem_mark_primary_se: regions by score (ties by a hash of the read id and
+// region index); a region whose ORIGINAL-read span overlaps a higher one's by
+// >= mask_level of the shorter is its secondary (and sets that one's sub /
+// sub_n); then pick_outputs.
+void mark_primary(ReadAln& R, const AlignOptions& opt, uint64_t read_id, const fcs_bsw_params& P) {
+  const int L = (int)R.code[0].size();
+  for (size_t i = 0; i < R.cands.size(); ++i) {
+    Cand& c = R.cands[i];
+    c.sub = c.sub_n = 0;
+    c.secondary = -1;
+    c.hash = hash64(read_id + i);
+  }
+  std::stable_sort(R.cands.begin(), R.cands.end(), [](const Cand& a, const Cand& b) {
+    return a.aln.score != b.aln.score ? a.aln.score > b.aln.score : a.hash < b.hash;
+  });
+  const int tmp = std::max({P.mat[0] - P.mat[1], P.o_del + P.e_del, P.o_ins + P.e_ins});
+  std::vector<int> z;
+  if (!R.cands.empty()) z.push_back(0);
+  for (int i = 1; i < (int)R.cands.size(); ++i) {
+    Cand& ci = R.cands[i];
+    size_t k = 0;
+    for (; k < z.size(); ++k) {
+      Cand& cj = R.cands[z[k]];
+      const int b_max = std::max(orig_qb(cj, L), orig_qb(ci, L)), e_min = std::min(orig_qe(cj, L), orig_qe(ci, L));
+      if (e_min > b_max) {
+        const int min_l = std::min(orig_qe(ci, L) - orig_qb(ci, L), orig_qe(cj, L) - orig_qb(cj, L));
+        if (e_min - b_max >= min_l * opt.mask_level) {
+          if (cj.sub == 0) cj.sub = ci.aln.score;
+          if (cj.aln.score - ci.aln.score <= tmp) ++cj.sub_n;
+          break;
+        }
+      }
+    }
+    if (k == z.size()) z.push_back(i);
+    else ci.secondary = z[k];
+  }
+  pick_outputs(R, opt, P);
+}
+
+// bwa's strand-aware coordinates of a region (its 2 x contig-length space:
+// the reverse strand runs backwards after the forward one): the start.
+int64_t rb2(const KmerIndex& idx, const Cand& c) {
+  return c.rev ? 2 * (int64_t)idx.codes(c.contig).size() - c.aln.re : c.aln.rb;
+}
+
+// bwa mem_infer_dir: orientation 0 FF, 1 FR, 2 RF, 3 RR of two regions of one
+// contig (starts b1, b2 in the 2 x l space) and their distance.
+int infer_dir(int64_t l, int64_t b1, int64_t b2, int64_t& dist) {
+  const bool r1 = b1 >= l, r2 = b2 >= l;
+  const int64_t p2 = r1 == r2 ? b2 : 2 * l - 1 - b2;  // read 2 on read 1's strand
+  dist = p2 > b1 ? p2 - b1 : b1 - p2;
+  return (r1 == r2 ? 0 : 1) ^ (p2 > b1 ? 0 : 3);
+}
+
+// Insert-size distribution per orientation of one batch (bwa mem_pestat).
 struct PeStat {
-  bool ok = false;
+  bool failed = true;
   int low = 0, high = 0;
-  double avg = 0, std = 1;
+  double avg = 0, std = 0;
   int n = 0;
 };
 
-int64_t frag_len(const Cand& a, const Cand& b) {
-  return std::max(aln_end(a), aln_end(b)) - std::min(aln_pos(a), aln_pos(b));
+// bwa cal_sub: score of the best region overlapping the top one by >=
+// mask_level on the query, else min_seed_len x match.
+int cal_sub(const ReadAln& R, const AlignOptions& opt, int match) {
+  const int L = (int)R.code[0].size();
+  const Cand& a0 = R.cands[0];
+  for (size_t j = 1; j < R.cands.size(); ++j) {
+    const Cand& aj = R.cands[j];
+    const int b_max = std::max(orig_qb(aj, L), orig_qb(a0, L)), e_min = std::min(orig_qe(aj, L), orig_qe(a0, L));
+    if (e_min > b_max) {
+      const int min_l = std::min(orig_qe(aj, L) - orig_qb(aj, L), orig_qe(a0, L) - orig_qb(a0, L));
+      if (e_min - b_max >= min_l * opt.mask_level) return aj.aln.score;
+    }
+  }
+  return opt.k * match;
 }
 
-bool fr_pair(const Cand& a, const Cand& b) {
-  if (a.contig != b.contig || a.rev == b.rev) return false;
-  const Cand& f = a.rev ? b : a;  // forward mate starts at the left
-  const Cand& r = a.rev ? a : b;
-  return aln_pos(f) <= aln_pos(r) && aln_end(f) <= aln_end(r) + 16;
-}
-
-PeStat pestat(const std::vector<ReadAln>& m1, const std::vector<ReadAln>& m2) {
-  PeStat ps;
-  std::vector<int64_t> v;
+// bwa mem_pestat over the top regions (score order) of pairs whose both ends
+// are unique (cal_sub <= 0.8 x score) on one contig, distances <= 10000;
+// an orientation with < 10 pairs, or < 5% of the commonest, fails.  Per
+// orientation: quartiles; mean / sd over [p25 - 2 IQR, p75 + 2 IQR]; proper
+// pairs within [p25 - 3 IQR, p75 + 3 IQR], at least mean +- 4 sd, low >= 1.
+std::array<PeStat, 4> pestat(const KmerIndex& idx, const std::vector<ReadAln>& m1, const std::vector<ReadAln>& m2,
+                             const AlignOptions& opt, int match) {
+  std::array<std::vector<int64_t>, 4> isize;
   for (size_t i = 0; i < m1.size(); ++i) {
     const ReadAln &a = m1[i], &b = m2[i];
-    if (a.best < 0 || b.best < 0 || a.mapq < 20 || b.mapq < 20) continue;
-    const Cand &x = a.cands[a.best], &y = b.cands[b.best];
-    if (!fr_pair(x, y)) continue;
-    const int64_t f = frag_len(x, y);
-    if (f > 0 && f < 10000) v.push_back(f);
+    if (a.cands.empty() || b.cands.empty()) continue;
+    if (cal_sub(a, opt, match) > 0.8 * a.cands[0].aln.score) continue;
+    if (cal_sub(b, opt, match) > 0.8 * b.cands[0].aln.score) continue;
+    if (a.cands[0].contig != b.cands[0].contig) continue;
+    int64_t dist;
+    const int d = infer_dir((int64_t)idx.codes(a.cands[0].contig).size(), rb2(idx, a.cands[0]), rb2(idx, b.cands[0]), dist);
+    if (dist > 10000) continue;
+    isize[d].push_back(dist);
   }
-  ps.n = (int)v.size();
-  if (v.size() < 25) return ps;  // bwa: too few pairs to estimate
-  std::sort(v.begin(), v.end());
-  const double p25 = (double)v[(size_t)(.25 * v.size() + .499)], p75 = (double)v[(size_t)(.75 * v.size() + .499)];
-  const double iqr = p75 - p25;
-  const double lo2 = p25 - 2. * iqr, hi2 = p75 + 2. * iqr;
-  double s = 0, s2 = 0;
-  int n = 0;
-  for (int64_t x : v)
-    if (x >= lo2 && x <= hi2) s += (double)x, s2 += (double)x * (double)x, ++n;
-  ps.avg = s / n;
-  ps.std = std::sqrt(std::max(1e-9, s2 / n - ps.avg * ps.avg));
-  ps.low = (int)(p25 - 3. * iqr + .499);
-  ps.high = (int)(p75 + 3. * iqr + .499);
-  if (ps.low > ps.avg - 4. * ps.std) ps.low = (int)(ps.avg - 4. * ps.std + .499);
-  if (ps.high < ps.avg + 4. * ps.std) ps.high = (int)(ps.avg + 4. * ps.std + .499);
-  ps.low = std::max(ps.low, 1);
-  ps.ok = true;
-  return ps;
+  std::array<PeStat, 4> pes;
+  size_t most = 0;
+  for (int d = 0; d < 4; ++d) {
+    std::vector<int64_t>& q = isize[d];
+    PeStat& r = pes[d];
+    r.n = (int)q.size();
+    most = std::max(most, q.size());
+    if (q.size() < 10) continue;
+    std::sort(q.begin(), q.end());
+    const double n = (double)q.size();
+    const int64_t p25 = q[(size_t)(.25 * n + .499)], p75 = q[(size_t)(.75 * n + .499)];
+    r.low = std::max(1, (int)(p25 - 2. * (p75 - p25) + .499));
+    r.high = (int)(p75 + 2. * (p75 - p25) + .499);
+    int x = 0;
+    for (int64_t v : q)
+      if (v >= r.low && v <= r.high) r.avg += (double)v, ++x;
+    r.avg /= x;
+    for (int64_t v : q)
+      if (v >= r.low && v <= r.high) r.std += ((double)v - r.avg) * ((double)v - r.avg);
+    r.std = std::sqrt(r.std / x);
+    r.low = (int)(p25 - 3. * (p75 - p25) + .499);
+    r.high = (int)(p75 + 3. * (p75 - p25) + .499);
+    if (r.low > r.avg - 4. * r.std) r.low = (int)(r.avg - 4. * r.std + .499);
+    if (r.high < r.avg + 4. * r.std) r.high = (int)(r.avg + 4. * r.std + .499);
+    if (r.low < 1) r.low = 1;
+    r.failed = false;
+  }
+  for (int d = 0; d < 4; ++d)
+    if (!pes[d].failed && (double)pes[d].n < most * 0.05) pes[d].failed = true;
+  return pes;
 }
 
-// bwa mem_pair's insert-size log-likelihood term in score units.
-int pair_penalty(const PeStat& ps, int64_t dist, int match) {
-  const double ns = ((double)dist - ps.avg) / ps.std;
-  return (int)(.721 * std::log(2. * std::erfc(std::fabs(ns) * M_SQRT1_2)) * match + .499);
-}
-
-// Mate rescue (bwa mem_matesw's role): the mate is searched in the window the
-// insert-size distribution allows opposite `anchor`, on the other strand, by
-// 12-mer exact hits of the window; the best-supported diagonal becomes a seed
-// for the regular extension round.  Returns false when nothing seeds.
-bool rescue_seed(const KmerIndex& idx, const PeStat& ps, const Cand& anchor, ReadAln& mate) {
+// Mate rescue (bwa mem_matesw's windows): for each orientation whose
+// distribution holds and in which no region of the mate already pairs with
+// `anchor`, the window where the mate must lie (bwa's arithmetic in the
+// 2 x l space, then clipped to the strand half holding its middle).  bwa runs
+// a local Smith-Waterman (ksw_align2) over the window; here the window's
+// best-supported diagonal of 12-mer exact hits seeds an extension confined to
+// the window (extend_loose, one GPU round for the batch).  Appends the seeds
+// as regions to extend; returns how many.
+int rescue_seeds(const KmerIndex& idx, const std::array<PeStat, 4>& pes, const Cand& anchor, ReadAln& mate,
+                 const AlignOptions& opt) {
   const int kk = 12;
   const std::vector<uint8_t>& rc = idx.codes(anchor.contig);
-  const int64_t L = (int64_t)mate.code[0].size();
-  const bool rev = !anchor.rev;
-  int64_t wb, we;
-  if (!anchor.rev) {  // anchor forward at the left: the mate ends within [pos + low, pos + high]
-    wb = aln_pos(anchor) + ps.low - L;
-    we = aln_pos(anchor) + ps.high;
-  } else {  // anchor reverse at the right: the mate starts within [end - high, end - low]
-    wb = aln_end(anchor) - ps.high;
-    we = aln_end(anchor) - ps.low + L;
+  const int64_t l = (int64_t)rc.size(), lms = (int64_t)mate.code[0].size();
+  bool skip[4];
+  for (int r = 0; r < 4; ++r) skip[r] = pes[r].failed;
+  for (const Cand& m : mate.cands) {
+    if (!m.done || m.contig != anchor.contig) continue;
+    int64_t dist;
+    const int r = infer_dir(l, rb2(idx, anchor), rb2(idx, m), dist);
+    if (dist >= pes[r].low && dist <= pes[r].high) skip[r] = true;
   }
-  wb = std::max<int64_t>(0, wb);
-  we = std::min<int64_t>((int64_t)rc.size(), we);
-  if (we - wb < kk || we - wb > 100000) return false;
-  std::unordered_multimap<uint32_t, int64_t> win;
-  win.reserve((size_t)(we - wb));
-  uint32_t key = 0;
-  int valid = 0;
-  const uint32_t mask = (1u << (2 * kk)) - 1;
-  for (int64_t p = wb; p < we; ++p) {
-    if (rc[p] > 3) {
-      valid = 0;
-      continue;
+  int added = 0;
+  const int64_t a_rb = rb2(idx, anchor);
+  for (int r = 0; r < 4; ++r) {
+    if (skip[r]) continue;
+    const bool is_rev = (r >> 1) != (r & 1), is_larger = !(r >> 1);
+    int64_t rb, re;
+    if (!is_rev) {
+      rb = is_larger ? a_rb + pes[r].low : a_rb - pes[r].high;
+      re = (is_larger ? a_rb + pes[r].high : a_rb - pes[r].low) + lms;
+    } else {
+      rb = (is_larger ? a_rb + pes[r].low : a_rb - pes[r].high) - lms;
+      re = is_larger ? a_rb + pes[r].high : a_rb - pes[r].low;
     }
-    key = ((key << 2) | rc[p]) & mask;
-    if (++valid >= kk) win.emplace(key, p - kk + 1);
+    rb = std::max<int64_t>(rb, 0);
+    re = std::min<int64_t>(re, 2 * l);
+    if (rb >= re) continue;
+    const bool rhalf = ((rb + re) >> 1) >= l;  // bns_fetch_seq: the half holding the middle
+    if (rhalf) rb = std::max(rb, l);
+    else re = std::min(re, l);
+    if (re - rb < opt.k || re - rb > 100000) continue;
+    const int64_t wb = rhalf ? 2 * l - re : rb, we = rhalf ? 2 * l - rb : re;  // forward coordinates
+    const bool rev = is_rev != rhalf;  // the mate's strand on the forward contig
+    std::unordered_multimap<uint32_t, int64_t> win;
+    win.reserve((size_t)(we - wb));
+    uint32_t key = 0;
+    int valid = 0;
+    const uint32_t mask = (1u << (2 * kk)) - 1;
+    for (int64_t p = wb; p < we; ++p) {
+      if (rc[p] > 3) {
+        valid = 0;
+        continue;
+      }
+      key = ((key << 2) | rc[p]) & mask;
+      if (++valid >= kk) win.emplace(key, p - kk + 1);
+    }
+    const std::vector<uint8_t>& q = mate.code[rev];
+    std::map<int64_t, std::pair<int, int>> diag;  // diagonal -> (hits, first query pos)
+    key = 0;
+    valid = 0;
+    for (int i = 0; i < (int)q.size(); ++i) {
+      if (q[i] > 3) {
+        valid = 0;
+        continue;
+      }
+      key = ((key << 2) | q[i]) & mask;
+      if (++valid < kk) continue;
+      const int qp = i - kk + 1;
+      auto range = win.equal_range(key);
+      for (auto it = range.first; it != range.second; ++it) {
+        auto& d = diag[it->second - qp];
+        if (d.first++ == 0) d.second = qp;
+      }
+    }
+    int best = 0;
+    int64_t bd = 0;
+    int bq = 0;
+    for (const auto& [d, h] : diag)
+      if (h.first > best) best = h.first, bd = d, bq = h.second;
+    if (best < 1) continue;
+    int qs = bq, qe = bq + kk;
+    int64_t rs = bd + bq;
+    while (qs > 0 && rs > wb && q[qs - 1] < 4 && q[qs - 1] == rc[rs - 1]) --qs, --rs;
+    while (qe < (int)q.size() && rs + (qe - qs) < we && q[qe] < 4 && q[qe] == rc[rs + (qe - qs)]) ++qe;
+    Cand C;
+    C.rev = rev;
+    C.contig = anchor.contig;
+    C.seed_q = qs;
+    C.seed_len = qe - qs;
+    C.seed_r = rs;
+    C.win_lo = wb;
+    C.win_hi = we;
+    C.rescued = true;
+    mate.cands.push_back(std::move(C));
+    ++added;
   }
-  const std::vector<uint8_t>& q = mate.code[rev];
-  std::map<int64_t, std::pair<int, int>> diag;  // diagonal -> (hits, first query pos)
-  key = 0;
-  valid = 0;
-  for (int i = 0; i < (int)q.size(); ++i) {
-    if (q[i] > 3) {
-      valid = 0;
-      continue;
-    }
-    key = ((key << 2) | q[i]) & mask;
-    if (++valid < kk) continue;
-    const int qp = i - kk + 1;
-    auto range = win.equal_range(key);
-    for (auto it = range.first; it != range.second; ++it) {
-      auto& d = diag[it->second - qp];
-      if (d.first++ == 0) d.second = qp;
-    }
-  }
-  int best = 0;
-  int64_t bd = 0;
-  int bq = 0;
-  for (const auto& [d, h] : diag)
-    if (h.first > best) best = h.first, bd = d, bq = h.second;
-  if (best < 2) return false;
-  Cand C;
-  C.rev = rev;
-  C.contig = anchor.contig;
-  C.hits = best;
-  int qs = bq, qe = bq + kk;
-  int64_t rs = bd + bq;
-  while (qs > 0 && rs > 0 && q[qs - 1] < 4 && q[qs - 1] == rc[rs - 1]) --qs, --rs;
-  while (qe < (int)q.size() && rs + (qe - qs) < (int64_t)rc.size() && q[qe] < 4 && q[qe] == rc[rs + (qe - qs)]) ++qe;
-  C.seed_q = qs;
-  C.seed_len = qe - qs;
-  C.seed_r = rs;
-  mate.cands.push_back(std::move(C));
-  return true;
+  return added;
 }
 
-// The BAM record of one read: its primary alignment (soft clips, NM / MD /
-// AS) or an unmapped record.
-BamRecord make_record(const Reference& ref, const ReadAln& R, const std::string& name, const std::string& fq_seq,
-                      const std::string& fq_qual, const AlignOptions& opt) {
-  BamRecord rec;
-  rec.name = name;
-  rec.set_aux_string("RG", opt.rg);
+// bwa mem_pair: every (region of read 1, region of read 2) in a valid
+// orientation with distance in [low, high] scores s1 + s2 + the insert-size
+// log-likelihood (.721 log(2 erfc(|z| / sqrt 2)) x match, >= 0); ties by a
+// hash of the pair and the pair id.  Returns the best score (0: none), the
+// second best (sub), how many others lie within the mismatch/gap cost of it
+// (n_sub) and the regions z of the best.
+int mem_pair(const KmerIndex& idx, const std::array<PeStat, 4>& pes, const ReadAln* a[2], uint64_t id,
+             const fcs_bsw_params& P, int& sub, int& n_sub, int z[2]) {
+  struct K {
+    uint64_t x, y;
+  };
+  std::vector<K> v;
+  for (int r = 0; r < 2; ++r)
+    for (size_t i = 0; i < a[r]->cands.size(); ++i) {
+      const Cand& e = a[r]->cands[i];
+      const uint64_t fpos = e.rev ? (uint64_t)(e.aln.re - 1) : (uint64_t)e.aln.rb;  // forward position of the 5' end
+      v.push_back({(uint64_t)e.contig << 32 | fpos, (uint64_t)(uint32_t)e.aln.score << 32 | i << 2 | (uint64_t)e.rev << 1 | r});
+    }
+  auto lt = [](const K& p, const K& q) { return p.x != q.x ? p.x < q.x : p.y < q.y; };
+  std::sort(v.begin(), v.end(), lt);
+  std::vector<K> u;
+  int y[4] = {-1, -1, -1, -1};
+  for (int i = 0; i < (int)v.size(); ++i) {
+    for (int r = 0; r < 2; ++r) {
+      const int dir = r << 1 | (int)(v[i].y >> 1 & 1);
+      if (pes[dir].failed) continue;
+      const int which = r << 1 | (int)((v[i].y & 1) ^ 1);
+      if (y[which] < 0) continue;
+      for (int k = y[which]; k >= 0; --k) {
+        if ((int)(v[k].y & 3) != which) continue;
+        const int64_t dist = (int64_t)v[i].x - (int64_t)v[k].x;
+        if (dist > pes[dir].high) break;
+        if (dist < pes[dir].low) continue;
+        const double ns = (dist - pes[dir].avg) / pes[dir].std;
+        int q = (int)((double)(v[i].y >> 32) + (double)(v[k].y >> 32) +
+                      .721 * std::log(2. * std::erfc(std::fabs(ns) * M_SQRT1_2)) * P.mat[0] + .499);
+        if (q < 0) q = 0;
+        K p;
+        p.y = (uint64_t)k << 32 | (uint64_t)i;
+        p.x = (uint64_t)q << 32 | (hash64(p.y ^ id << 8) & 0xffffffffu);
+        u.push_back(p);
+      }
+    }
+    y[v[i].y & 3] = i;
+  }
+  sub = n_sub = 0;
+  if (u.empty()) return 0;
+  const int tmp = std::max({P.mat[0] - P.mat[1], P.o_del + P.e_del, P.o_ins + P.e_ins});
+  std::sort(u.begin(), u.end(), lt);
+  const int i = (int)(u.back().y >> 32), k = (int)(uint32_t)u.back().y;
+  z[v[i].y & 1] = (int)((uint32_t)v[i].y >> 2);
+  z[v[k].y & 1] = (int)((uint32_t)v[k].y >> 2);
+  const int ret = (int)(u.back().x >> 32);
+  sub = u.size() > 1 ? (int)(u[u.size() - 2].x >> 32) : 0;
+  for (int j = (int)u.size() - 2; j >= 0; --j)
+    if (sub - (int)(u[j].x >> 32) <= tmp) ++n_sub;
+  return ret;
+}
+
+// The CIGARs (mem_reg2aln / bwa_gen_cigar2) of every output region of the
+// batch (R.outs of each read) in one round of GPU global alignments.
+void output_cigars(const KmerIndex& idx, const fcs_bsw_params& P, const AlignOptions& opt,
+                   const std::vector<ReadAln*>& reads, AlignStats& st) {
+  std::vector<SeedJob> jobs;
+  std::vector<SeedAln> alns;
+  std::vector<Cand*> who;
+  for (ReadAln* R : reads)
+    for (const auto& o : R->outs) {
+      Cand& C = R->cands[o.first];
+      const std::vector<uint8_t>& rc = idx.codes(C.contig);
+      SeedJob J;
+      J.q = R->code[C.rev].data();
+      J.qlen = (int)R->code[C.rev].size();
+      J.ref = rc.data();
+      J.rlen = (int64_t)rc.size();
+      jobs.push_back(J);
+      alns.push_back(C.aln);
+      who.push_back(&C);
+    }
+  if (jobs.empty()) return;
+  SeedExtOptions so;
+  so.w = opt.w;
+  so.gpu = opt.gpu;
+  so.threads = opt.threads;
+  SeedExtStats xs;
+  global_cigars(jobs, P, so, alns, xs);
+  st.global_tasks += xs.global_tasks;
+  st.gpu_seconds += xs.gpu_seconds;
+  for (size_t i = 0; i < who.size(); ++i) who[i]->aln = std::move(alns[i]);
+}
+
+// The single-end outputs of a read (bwa mem_reg2sam): the primary, then the
+// supplementaries with MAPQ capped at the primary's.
+void se_outputs(ReadAln& R, const AlignOptions& opt, const fcs_bsw_params& P) {
+  R.outs.clear();
+  if (R.best < 0) return;
+  R.outs.emplace_back(R.best, R.mapq);
+  for (int i : R.supp)
+    R.outs.emplace_back(i, std::min(R.mapq, approx_mapq_se(R.cands[i], opt.k, P.mat[0], -P.mat[1])));
+}
+
+// One output alignment of a read: SAM CIGAR with soft clips, NM, MD, MAPQ.
+struct OutAln {
+  const Cand* c = nullptr;
+  std::vector<uint32_t> cig;
+  int nm = 0, mapq = 0;
+  std::string md;
+};
+
+OutAln out_aln(const Reference& ref, const ReadAln& R, int i, int mapq) {
+  OutAln o;
+  o.c = &R.cands[i];
+  o.mapq = mapq;
+  const Cand& C = *o.c;
+  const SeedAln& A = C.aln;
+  const std::vector<uint8_t>& q = R.code[C.rev];
+  if (A.qb > 0) o.cig.push_back(cigar_pack((uint32_t)A.qb, kS));
+  for (uint32_t c : A.cigar) {
+    const uint32_t op = c & 0xf;  // ksw ops: 0 = M, 1 = I, 2 = D
+    o.cig.push_back(cigar_pack(c >> 4, op == 0 ? kM : op == 1 ? kI : kD));
+  }
+  if (A.qe < (int)q.size()) o.cig.push_back(cigar_pack((uint32_t)(q.size() - A.qe), kS));
+  const std::string& Rs = ref.contigs[C.contig].seq;
+  int run = 0;
+  int qi = A.qb;
+  int64_t ri = A.rb;
+  for (uint32_t c : A.cigar) {
+    const uint32_t len = c >> 4, op = c & 0xf;
+    if (op == 0) {
+      for (uint32_t j = 0; j < len; ++j, ++qi, ++ri) {
+        if (q[qi] != code_of(Rs[ri]) || q[qi] > 3) {
+          ++o.nm;
+          o.md += std::to_string(run);
+          o.md += Rs[ri];
+          run = 0;
+        } else {
+          ++run;
+        }
+      }
+    } else if (op == 1) {
+      o.nm += (int)len;
+      qi += (int)len;
+    } else {
+      o.nm += (int)len;
+      o.md += std::to_string(run) + "^" + Rs.substr(ri, len);
+      run = 0;
+      ri += len;
+    }
+  }
+  o.md += std::to_string(run);
+  return o;
+}
+
+// SA:Z of output alignment `self`: the read's other primary / supplementary
+// alignments, "rname,pos,strand,CIGAR,mapQ,NM;" (bwa mem_aln2sam; soft clips).
+std::string sa_tag(const Reference& ref, const std::vector<OutAln>& v, size_t self) {
+  std::string s;
+  for (size_t k = 0; k < v.size(); ++k) {
+    if (k == self) continue;
+    const OutAln& o = v[k];
+    s += ref.contigs[o.c->contig].name + "," + std::to_string(o.c->aln.rb + 1) + "," + (o.c->rev ? "-" : "+") + ",";
+    for (uint32_t c : o.cig) s += std::to_string(cigar_len(c)) + "MIDNSHP=X"[cigar_op(c)];
+    s += "," + std::to_string(o.mapq) + "," + std::to_string(o.nm) + ";";
+  }
+  return s;
+}
+
+// The BAM records of one read (R.outs): the first alignment with soft clips,
+// NM / MD / AS / XS, then the supplementary ones (flag 0x800, hard clips: SEQ
+// and QUAL of the aligned part only), SA tags when there are several; or one
+// unmapped record.
+std::vector<BamRecord> make_records(const Reference& ref, const ReadAln& R, const std::string& name,
+                                    const std::string& fq_seq, const std::string& fq_qual, const AlignOptions& opt) {
   auto quals = [&](bool rev) {
     std::vector<uint8_t> q(fq_seq.size());
     for (size_t i = 0; i < q.size(); ++i) {
@@ -405,67 +1039,92 @@ BamRecord make_record(const Reference& ref, const ReadAln& R, const std::string&
     }
     return q;
   };
-  if (R.best < 0) {
+  std::vector<BamRecord> out;
+  if (R.outs.empty()) {
+    BamRecord rec;
+    rec.name = name;
+    rec.set_aux_string("RG", opt.rg);
     rec.flag = kUnmapped;
     rec.seq = fq_seq;
     rec.qual = quals(false);
-    return rec;
+    out.push_back(std::move(rec));
+    return out;
   }
-  const Cand& C = R.cands[R.best];
-  const SeedAln& A = C.aln;
-  const std::vector<uint8_t>& q = R.code[C.rev];
-  std::vector<uint32_t> cig;
-  if (A.qb > 0) cig.push_back(cigar_pack((uint32_t)A.qb, kS));
-  for (uint32_t c : A.cigar) {
-    const uint32_t op = c & 0xf;  // ksw ops: 0 = M, 1 = I, 2 = D
-    cig.push_back(cigar_pack(c >> 4, op == 0 ? kM : op == 1 ? kI : kD));
-  }
-  if (A.qe < (int)q.size()) cig.push_back(cigar_pack((uint32_t)(q.size() - A.qe), kS));
-  const std::string& Rs = ref.contigs[C.contig].seq;
-  int nm = 0, run = 0;
-  std::string md;
-  int qi = A.qb;
-  int64_t ri = A.rb;
-  for (uint32_t c : A.cigar) {
-    const uint32_t len = c >> 4, op = c & 0xf;
-    if (op == 0) {
-      for (uint32_t j = 0; j < len; ++j, ++qi, ++ri) {
-        if (q[qi] != code_of(Rs[ri]) || q[qi] > 3) {
-          ++nm;
-          md += std::to_string(run);
-          md += Rs[ri];
-          run = 0;
-        } else {
-          ++run;
-        }
-      }
-    } else if (op == 1) {
-      nm += (int)len;
-      qi += (int)len;
-    } else {
-      nm += (int)len;
-      md += std::to_string(run) + "^" + Rs.substr(ri, len);
-      run = 0;
-      ri += len;
+  std::vector<OutAln> v;
+  for (const auto& o : R.outs) v.push_back(out_aln(ref, R, o.first, o.second));
+  for (size_t k = 0; k < v.size(); ++k) {
+    const OutAln& o = v[k];
+    const Cand& C = *o.c;
+    BamRecord rec;
+    rec.name = name;
+    rec.set_aux_string("RG", opt.rg);
+    rec.ref_id = C.contig;
+    rec.pos = (int32_t)C.aln.rb;
+    rec.mapq = (uint8_t)o.mapq;
+    rec.flag = (C.rev ? kReverse : 0) | (k ? kSupplementary : 0);
+    rec.cigar = o.cig;
+    rec.seq = R.seq[C.rev];
+    rec.qual = quals(C.rev);
+    if (k) {  // supplementary: hard-clipped
+      for (uint32_t& c : rec.cigar)
+        if (cigar_op(c) == kS) c = cigar_pack(cigar_len(c), kH);
+      rec.seq = rec.seq.substr(C.aln.qb, C.aln.qe - C.aln.qb);
+      rec.qual = std::vector<uint8_t>(rec.qual.begin() + C.aln.qb, rec.qual.begin() + C.aln.qe);
     }
+    rec.set_aux_int("NM", o.nm);
+    rec.set_aux_string("MD", o.md);
+    rec.set_aux_int("AS", C.aln.score);
+    rec.set_aux_int("XS", C.sub);
+    if (v.size() > 1) rec.set_aux_string("SA", sa_tag(ref, v, k));
+    out.push_back(std::move(rec));
   }
-  md += std::to_string(run);
-  rec.ref_id = C.contig;
-  rec.pos = (int32_t)A.rb;
-  rec.mapq = (uint8_t)R.mapq;
-  rec.flag = C.rev ? kReverse : 0;
-  rec.cigar = cig;
-  rec.seq = R.seq[C.rev];
-  rec.qual = quals(C.rev);
-  rec.set_aux_int("NM", nm);
-  rec.set_aux_string("MD", md);
-  rec.set_aux_int("AS", A.truesc);
-  return rec;
+  return out;
 }
 
-// Seeds, chains and the GPU extension round for a batch of reads.
-void align_batch(const Reference& ref, const KmerIndex& idx, const std::vector<std::string>& seqs,
-                 const AlignOptions& opt, std::vector<ReadAln>& reads, AlignStats& st) {
+// Mate fields of a paired read's records (bwa mem_aln2sam): `mate` is the
+// other read's first record.  An unmapped record takes its mate's place and
+// strand (its SEQ / QUAL then reverse-complemented, as bwa prints them); TLEN
+// from the 5' ends, 0 when either is unmapped.
+void link_mate(std::vector<BamRecord>& recs, const BamRecord& mate_in, bool read1, bool proper) {
+  for (BamRecord& p : recs) {
+    BamRecord m;
+    m.ref_id = mate_in.ref_id;
+    m.pos = mate_in.pos;
+    m.flag = mate_in.flag;
+    m.cigar = mate_in.cigar;
+    const bool p_unmapped = p.flag & kUnmapped, m_unmapped = m.flag & kUnmapped;
+    p.flag |= kPaired | (read1 ? kRead1 : kRead2) | (proper ? kProperPair : 0);
+    if (m_unmapped) p.flag |= kMateUnmapped;
+    if (p_unmapped && !m_unmapped) {
+      p.ref_id = m.ref_id;
+      p.pos = m.pos;
+      if (m.flag & kReverse) {
+        p.flag |= kReverse;
+        p.seq = revcomp(p.seq);
+        std::reverse(p.qual.begin(), p.qual.end());
+      }
+    }
+    if (m_unmapped && !p_unmapped) {
+      m.ref_id = p.ref_id;
+      m.pos = p.pos;
+      m.flag = (uint16_t)((m.flag & ~kReverse) | (p.flag & kReverse));
+    }
+    if (m.flag & kReverse) p.flag |= kMateReverse;
+    p.next_ref_id = m.ref_id;
+    p.next_pos = m.ref_id >= 0 ? m.pos : -1;
+    p.tlen = 0;
+    if (m.ref_id >= 0 && p.ref_id == m.ref_id && !p_unmapped && !m_unmapped) {
+      const int64_t p0 = p.pos + ((p.flag & kReverse) ? cigar_ref_len(p.cigar) - 1 : 0);
+      const int64_t p1 = m.pos + ((m.flag & kReverse) ? cigar_ref_len(m.cigar) - 1 : 0);
+      p.tlen = (int32_t)(-(p0 - p1 + (p0 > p1 ? 1 : p0 < p1 ? -1 : 0)));
+    }
+  }
+}
+
+// Seeds, chains, the GPU extension rounds and dedup / patch for a batch of
+// reads; regions sorted by score (mem_sort_dedup_patch's order).
+void align_batch(const KmerIndex& idx, const std::vector<std::string>& seqs, const AlignOptions& opt,
+                 std::vector<ReadAln>& reads, AlignStats& st) {
   const uint64_t t0 = now_us();
   reads.assign(seqs.size(), ReadAln{});
   parallel_for(seqs.size(), opt.threads, [&](size_t r) {
@@ -474,17 +1133,16 @@ void align_batch(const Reference& ref, const KmerIndex& idx, const std::vector<s
     R.seq[1] = revcomp(seqs[r]);
     R.code[0] = encode(R.seq[0]);
     R.code[1] = encode(R.seq[1]);
-    seed_read(ref, idx, opt, R);
+    seed_read(idx, opt, R);
   });
   const uint64_t t1 = now_us();
   st.seed_seconds += (t1 - t0) / 1e6;
+  extend_chains(idx, st.params, opt, reads, st);
   std::vector<ReadAln*> ptr;
   for (ReadAln& R : reads) ptr.push_back(&R);
-  extend_cands(idx, st.params, opt, ptr, false, st);
-  const uint64_t t2 = now_us();
-  st.extend_seconds += (t2 - t1) / 1e6;
-  parallel_for(reads.size(), opt.threads, [&](size_t r) { pick_primary(reads[r], opt); });
-  st.pair_seconds += (now_us() - t2) / 1e6;
+  dedup_patch(idx, st.params, opt, ptr, true, st);
+  for (ReadAln& R : reads) std::vector<Chain>().swap(R.chains);
+  st.extend_seconds += (now_us() - t1) / 1e6;
 }
 
 }  // namespace
@@ -519,15 +1177,27 @@ AlignStats align_reads(const Reference& ref, const KmerIndex& idx, const std::ve
   fcs_bsw_params_default(&st.params);
   const uint64_t t0 = now_us();
   std::vector<ReadAln> reads;
-  align_batch(ref, idx, seqs, opt, reads, st);
-  st.reads = (int64_t)seqs.size();
-  const size_t base = out.size();
-  out.resize(base + reads.size());
+  align_batch(idx, seqs, opt, reads, st);
+  const uint64_t tp = now_us();
+  parallel_for(reads.size(), opt.threads, [&](size_t r) {
+    mark_primary(reads[r], opt, opt.read_id0 + r, st.params);
+    se_outputs(reads[r], opt, st.params);
+  });
+  std::vector<ReadAln*> ptr;
+  for (ReadAln& R : reads) ptr.push_back(&R);
+  const uint64_t tc = now_us();
+  st.pair_seconds += (tc - tp) / 1e6;
+  output_cigars(idx, st.params, opt, ptr, st);
   const uint64_t tr = now_us();
+  st.extend_seconds += (tr - tc) / 1e6;
+  st.reads = (int64_t)seqs.size();
+  std::vector<std::vector<BamRecord>> recs(reads.size());
   parallel_for(reads.size(), opt.threads,
-               [&](size_t i) { out[base + i] = make_record(ref, reads[i], names[i], seqs[i], quals[i], opt); });
+               [&](size_t i) { recs[i] = make_records(ref, reads[i], names[i], seqs[i], quals[i], opt); });
+  for (auto& v : recs)
+    for (BamRecord& r : v) out.push_back(std::move(r));
   st.record_seconds += (now_us() - tr) / 1e6;
-  for (const ReadAln& R : reads) st.mapped += R.best >= 0;
+  for (const ReadAln& R : reads) st.mapped += R.best >= 0, st.supplementary += R.supp.size();
   st.seconds = (now_us() - t0) / 1e6;
   return st;
 }
@@ -538,119 +1208,127 @@ AlignStats align_pairs(const Reference& ref, const KmerIndex& idx, const std::ve
                        const AlignOptions& opt, std::vector<BamRecord>& out) {
   AlignStats st;
   fcs_bsw_params_default(&st.params);
+  const fcs_bsw_params& P = st.params;
   const uint64_t t0 = now_us();
   const size_t n = names.size();
   if (seqs1.size() != n || seqs2.size() != n) throw invalidParam("align_pairs: mate lists differ in length");
-  // both mates in one batch: one GPU extension round for all
+  // both mates in one batch: one GPU round per extension step for all
   std::vector<std::string> both(seqs1);
   both.insert(both.end(), seqs2.begin(), seqs2.end());
   std::vector<ReadAln> all;
-  align_batch(ref, idx, both, opt, all, st);
+  align_batch(idx, both, opt, all, st);
   std::vector<ReadAln> m1(std::make_move_iterator(all.begin()), std::make_move_iterator(all.begin() + n));
   std::vector<ReadAln> m2(std::make_move_iterator(all.begin() + n), std::make_move_iterator(all.end()));
   all.clear();
   const uint64_t tp = now_us();
-  const PeStat ps = pestat(m1, m2);
-  st.pe_pairs = ps.n;
-  st.pe_low = ps.low;
-  st.pe_high = ps.high;
-  st.pe_avg = ps.avg;
-  st.pe_std = ps.std;
-  // mate rescue: a confidently placed mate whose partner has no alignment in the
-  // allowed window gets the window searched for the partner
-  if (ps.ok) {
-    std::vector<ReadAln*> resc;
-    for (size_t i = 0; i < n; ++i)
-      for (int side = 0; side < 2; ++side) {
-        ReadAln& a = side ? m2[i] : m1[i];
-        ReadAln& b = side ? m1[i] : m2[i];
-        if (a.best < 0 || a.mapq < 20) continue;
-        const Cand& A = a.cands[a.best];
-        bool have = false;
-        for (const Cand& C : b.cands)
-          if (C.ok && fr_pair(A, C) && frag_len(A, C) >= ps.low && frag_len(A, C) <= ps.high) have = true;
-        if (have) continue;
-        if (rescue_seed(idx, ps, A, b)) resc.push_back(&b);
+  const std::array<PeStat, 4> pes = pestat(idx, m1, m2, opt, P.mat[0]);
+  st.pe_pairs = pes[1].n;
+  st.pe_low = pes[1].low;
+  st.pe_high = pes[1].high;
+  st.pe_avg = pes[1].avg;
+  st.pe_std = pes[1].std;
+  // mate rescue (bwa mem_sam_pe): every region of a read within pen_unpaired of
+  // its best (at most max_matesw) searches the mate's windows
+  if (!pes[0].failed || !pes[1].failed || !pes[2].failed || !pes[3].failed) {
+    std::vector<std::array<int, 2>> added(n);
+    parallel_for(n, opt.threads, [&](size_t i) {
+      ReadAln* r[2] = {&m1[i], &m2[i]};
+      std::vector<Cand> anchors[2];
+      for (int s = 0; s < 2; ++s)
+        for (const Cand& c : r[s]->cands)
+          if (c.aln.score >= r[s]->cands[0].aln.score - opt.pen_unpaired && (int)anchors[s].size() < opt.max_matesw)
+            anchors[s].push_back(c);
+      for (int s = 0; s < 2; ++s) {
+        added[i][!s] = 0;
+        for (const Cand& a : anchors[s]) added[i][!s] += rescue_seeds(idx, pes, a, *r[!s], opt);
       }
-    std::sort(resc.begin(), resc.end());
-    resc.erase(std::unique(resc.begin(), resc.end()), resc.end());
+    });
+    std::vector<ReadAln*> resc;
+    for (size_t i = 0; i < n; ++i) {
+      if (added[i][0]) resc.push_back(&m1[i]);
+      if (added[i][1]) resc.push_back(&m2[i]);
+    }
     st.rescued = (int64_t)resc.size();
     const uint64_t te = now_us();
-    extend_cands(idx, st.params, opt, resc, true, st);
+    extend_loose(idx, P, opt, resc, st);
+    dedup_patch(idx, P, opt, resc, false, st);
     st.extend_seconds += (now_us() - te) / 1e6;
     st.pair_seconds -= (now_us() - te) / 1e6;
   }
-  // pairing (bwa mem_pair): the best FR combination within [low, high] by
-  // score + insert-size log-likelihood, against the unpaired best - pen_unpaired
-  const int pen_unpaired = 17;
+  // pairing (bwa mem_sam_pe after mem_matesw)
   std::vector<char> proper(n, 0);
-  for (size_t i = 0; i < n; ++i) {
-    ReadAln &a = m1[i], &b = m2[i];
-    pick_primary(a, opt);
-    pick_primary(b, opt);
-    if (!ps.ok) continue;
-    int bi = -1, bj = -1, best = INT32_MIN, second = INT32_MIN;
-    for (int x = 0; x < (int)a.cands.size(); ++x)
-      for (int y = 0; y < (int)b.cands.size(); ++y) {
-        const Cand &A = a.cands[x], &B = b.cands[y];
-        if (!A.ok || !B.ok || !fr_pair(A, B)) continue;
-        const int64_t f = frag_len(A, B);
-        if (f < ps.low || f > ps.high) continue;
-        const int s = A.aln.truesc + B.aln.truesc + pair_penalty(ps, f, 1);
-        if (s > best) second = best, best = s, bi = x, bj = y;
-        else if (s > second) second = s;
-      }
-    if (bi < 0) continue;
-    const int unpaired = (a.best >= 0 ? a.cands[a.best].aln.truesc : 0) +
-                         (b.best >= 0 ? b.cands[b.best].aln.truesc : 0) - pen_unpaired;
-    if (best < unpaired) continue;
-    proper[i] = 1;
-    const int q_pe = second == INT32_MIN ? 60 : std::min(60, (int)(6.02 * (best - second) + .499));
-    for (int side = 0; side < 2; ++side) {
-      ReadAln& r = side ? b : a;
-      const int pick = side ? bj : bi;
-      const int q_se = pick == r.best ? r.mapq : 0;
-      r.best = pick;
-      r.mapq = std::max(q_se, std::min(q_pe, q_se + 40));
-    }
-  }
-  const uint64_t tr = now_us();
-  st.pair_seconds += (tr - tp) / 1e6;
-  const size_t base = out.size();
-  out.resize(base + 2 * n);
   parallel_for(n, opt.threads, [&](size_t i) {
-    BamRecord r1 = make_record(ref, m1[i], names[i], seqs1[i], quals1[i], opt);
-    BamRecord r2 = make_record(ref, m2[i], names[i], seqs2[i], quals2[i], opt);
-    r1.flag |= kPaired | kRead1;
-    r2.flag |= kPaired | kRead2;
-    const bool u1 = r1.flag & kUnmapped, u2 = r2.flag & kUnmapped;
-    if (!u1 && u2) r2.ref_id = r1.ref_id, r2.pos = r1.pos;  // SAM: an unmapped mate takes its partner's place
-    if (u1 && !u2) r1.ref_id = r2.ref_id, r1.pos = r2.pos;
-    auto link = [](BamRecord& x, const BamRecord& y) {
-      x.next_ref_id = y.ref_id;
-      x.next_pos = y.pos;
-      if (y.flag & kUnmapped) x.flag |= kMateUnmapped;
-      if (y.flag & kReverse) x.flag |= kMateReverse;
-    };
-    link(r1, r2);
-    link(r2, r1);
-    if (proper[i]) {
-      r1.flag |= kProperPair;
-      r2.flag |= kProperPair;
+    ReadAln* a[2] = {&m1[i], &m2[i]};
+    const uint64_t id = opt.read_id0 + i;
+    for (int s = 0; s < 2; ++s) mark_primary(*a[s], opt, id << 1 | s, P);
+    int z[2] = {0, 0}, sub = 0, n_sub = 0;
+    const ReadAln* ca[2] = {a[0], a[1]};
+    const int o = !a[0]->cands.empty() && !a[1]->cands.empty() ? mem_pair(idx, pes, ca, id, P, sub, n_sub, z) : 0;
+    bool multi = false;
+    for (int s = 0; s < 2 && o > 0; ++s)  // an end with more than one hit (a split read): no pairing
+      for (size_t j = 1; j < a[s]->cands.size(); ++j)
+        if (a[s]->cands[j].secondary < 0 && a[s]->cands[j].aln.score >= opt.min_out_score) multi = true;
+    if (o > 0 && !multi) {
+      const int score_un = a[0]->cands[0].aln.score + a[1]->cands[0].aln.score - opt.pen_unpaired;
+      const int subo = std::max(sub, score_un);
+      int q_pe = raw_mapq(o - subo, P.mat[0]);
+      if (n_sub > 0) q_pe -= (int)(4.343 * std::log((double)n_sub + 1) + .499);
+      q_pe = std::max(0, std::min(60, q_pe));
+      q_pe = (int)(q_pe * (1. - .5 * (a[0]->cands[0].frac_rep + a[1]->cands[0].frac_rep)) + .499);
+      int q_se[2];
+      if (o > score_un) {  // the pair is preferred: its regions are output, re-rooted if secondary
+        for (int s = 0; s < 2; ++s) {
+          Cand& c = a[s]->cands[z[s]];
+          if (c.secondary >= 0) c.sub = a[s]->cands[c.secondary].aln.score, c.secondary = -2;
+          q_se[s] = approx_mapq_se(c, opt.k, P.mat[0], -P.mat[1]);
+          q_se[s] = q_se[s] > q_pe ? q_se[s] : q_pe < q_se[s] + 40 ? q_pe : q_se[s] + 40;
+          q_se[s] = std::min(q_se[s], raw_mapq(c.aln.score, P.mat[0]));  // csub 0: bwa's tandem-repeat cap
+        }
+        proper[i] = 1;
+      } else {
+        z[0] = z[1] = 0;
+        for (int s = 0; s < 2; ++s) q_se[s] = approx_mapq_se(a[s]->cands[0], opt.k, P.mat[0], -P.mat[1]);
+      }
+      for (int s = 0; s < 2; ++s) {
+        a[s]->outs.clear();
+        a[s]->outs.emplace_back(z[s], q_se[s]);
+      }
+      return;
     }
-    if (!u1 && !u2 && r1.ref_id == r2.ref_id) {  // TLEN: leftmost to rightmost mapped base, signed
-      const int64_t b = std::min<int64_t>(r1.pos, r2.pos), e = std::max(r1.end(), r2.end());
-      const int32_t t = (int32_t)(e - b);
-      const bool first = r1.pos < r2.pos || (r1.pos == r2.pos && !(r1.flag & kReverse));
-      r1.tlen = first ? t : -t;
-      r2.tlen = first ? -t : t;
+    // no pairing: single-end outputs; proper if the top hits make a pair
+    for (int s = 0; s < 2; ++s) se_outputs(*a[s], opt, P);
+    if (a[0]->best >= 0 && a[1]->best >= 0 && a[0]->cands[0].contig == a[1]->cands[0].contig) {
+      int64_t dist;
+      const int d = infer_dir((int64_t)idx.codes(a[0]->cands[0].contig).size(), rb2(idx, a[0]->cands[0]),
+                              rb2(idx, a[1]->cands[0]), dist);
+      if (!pes[d].failed && dist >= pes[d].low && dist <= pes[d].high) proper[i] = 1;
     }
-    out[base + 2 * i] = std::move(r1);
-    out[base + 2 * i + 1] = std::move(r2);
   });
+  std::vector<ReadAln*> ptr;
+  for (size_t i = 0; i < n; ++i) ptr.push_back(&m1[i]), ptr.push_back(&m2[i]);
+  const uint64_t tc = now_us();
+  st.pair_seconds += (tc - tp) / 1e6;
+  output_cigars(idx, P, opt, ptr, st);
+  const uint64_t tr = now_us();
+  st.extend_seconds += (tr - tc) / 1e6;
+  std::vector<std::vector<BamRecord>> recs(n);
+  parallel_for(n, opt.threads, [&](size_t i) {
+    std::vector<BamRecord> r1 = make_records(ref, m1[i], names[i], seqs1[i], quals1[i], opt);
+    std::vector<BamRecord> r2 = make_records(ref, m2[i], names[i], seqs2[i], quals2[i], opt);
+    const BamRecord h1 = r1[0], h2 = r2[0];
+    link_mate(r1, h2, true, proper[i]);
+    link_mate(r2, h1, false, proper[i]);
+    recs[i] = std::move(r1);
+    for (BamRecord& r : r2) recs[i].push_back(std::move(r));
+  });
+  for (auto& v : recs)
+    for (BamRecord& r : v) out.push_back(std::move(r));
   st.record_seconds += (now_us() - tr) / 1e6;
-  for (size_t i = 0; i < n; ++i) st.mapped += (m1[i].best >= 0) + (m2[i].best >= 0);
-  for (size_t i = 0; i < n; ++i) st.proper += 2 * proper[i];
+  for (size_t i = 0; i < n; ++i) {
+    st.mapped += !m1[i].outs.empty() + !m2[i].outs.empty();
+    st.supplementary += (m1[i].outs.empty() ? 0 : m1[i].outs.size() - 1) + (m2[i].outs.empty() ? 0 : m2[i].outs.size() - 1);
+    st.proper += 2 * proper[i];
+  }
   st.reads = 2 * (int64_t)n;
   st.seconds = (now_us() - t0) / 1e6;
   return st;
@@ -719,6 +1397,7 @@ void add_stats(AlignStats& tot, const AlignStats& st) {
   tot.reads += st.reads;
   tot.mapped += st.mapped;
   tot.proper += st.proper;
+  tot.supplementary += st.supplementary;
   tot.rescued += st.rescued;
   tot.seconds += st.seconds;
   tot.gpu_seconds += st.gpu_seconds;
@@ -832,6 +1511,7 @@ AlignStats align_fastq(const AlignJob& job, const std::vector<int>& gpus, std::s
         try {
           const Chunk& c = item.second;
           std::vector<BamRecord> recs;
+          opt.read_id0 = (int64_t)(item.first * per_chunk);  // bwa's n_processed: the hash seed of ties
           const AlignStats st = paired ? align_pairs(ref, idx, c.names, c.s1, c.q1, c.s2, c.q2, opt, recs)
                                        : align_reads(ref, idx, c.names, c.s1, c.q1, opt, recs);
           std::lock_guard<std::mutex> g(mu);
@@ -925,7 +1605,7 @@ AlignStats align_fastq(const AlignJob& job, const std::vector<int>& gpus, std::s
   }
   const uint64_t t_end = now_us();
   std::ostringstream rep;
-  rep << "[fcs-genome align] " << tot.reads << " reads, " << tot.mapped << " mapped, " << tot.ext_tasks
+  rep << "[fcs-genome align] " << tot.reads << " reads, " << tot.mapped << " mapped, " << tot.supplementary << " supplementary, " << tot.ext_tasks
       << " extension tasks, " << tot.global_tasks << " global alignments, " << tot.seconds << " s (GPU calls "
       << tot.gpu_seconds << " s)";
   if (paired)

@@ -2,13 +2,33 @@
 // bwa bwamem.c mem_chain2aln / mem_reg2aln and bwa.c bwa_gen_cigar2, reached
 // in the reference through BWAWorker: /root/reference/src/workers/BWAWorker.cpp:94-186).
 //
-// Per chunk of reads (bwa.chunk_size): SMEM seeds, up to max_chains chains
-// per read, then bwa's extension protocol on the GPU (host/seedext.h: mem_chain2aln's windows, left / right extensions with
-// band retry, local vs to-end, mem_reg2aln / bwa_gen_cigar2's global
-// alignment for the CIGAR).  NM / MD / AS tags, soft clips, sorted BAM + BAI.
-// Seeds are bwa's SMEMs on an FMD-index of the reference (host/fmindex.h),
-// chained as bwa's mem_chain does; [EXT] bwa is not vendored, so this is a
-// restatement (parity unpinned against bwa itself).
+// Per chunk of reads (bwa.chunk_size), bwa mem's steps:
+//   * seeds: SMEMs on an FMD-index of the reference (host/fmindex.h), re-seeds
+//     and third-round seeds (mem_collect_intv), every hit (max_occ sampled);
+//   * chains (mem_chain's colinearity test) weighed by covered query bases,
+//     filtered by mem_chain_flt (shadowed lighter chains dropped, the first
+//     shadowed one kept for MAPQ);
+//   * mem_chain2aln: seeds of each chain longest first, a seed (almost)
+//     inside an earlier region skipped; each extension (left / right
+//     ksw_extend2 with band retry, inside the chain's reference window) is a
+//     GPU task, one GPU round per step over the whole chunk (host/seedext.h);
+//   * mem_sort_dedup_patch: redundant regions dropped, colinear neighbours
+//     merged when their joint ksw_global2 score (GPU) keeps >= 90%;
+//   * mem_mark_primary_se: secondary by query overlap, sub / sub_n, MAPQ
+//     (mem_approx_mapq_se with frac_rep); supplementary = further
+//     non-overlapping regions (split reads: flag 0x800, hard clips, SA tags);
+//   * paired ends (mem_sam_pe): mem_pestat per orientation, mate rescue in
+//     mem_matesw's windows, mem_pair's best pair by score + insert-size
+//     likelihood, secondary regions re-rooted when they make the pair, paired
+//     MAPQ; split reads and unpaired best hits go out single-end style;
+//   * CIGARs by mem_reg2aln / bwa_gen_cigar2 (GPU ksw_global2); NM / MD / AS /
+//     XS tags; sorted BAM + BAI.
+// [EXT] bwa is not vendored, so this is a restatement (parity unpinned against
+// bwa itself).  Known differences: the mate rescue finds its hit by 12-mer
+// seeds + a window-confined extension where bwa runs a local Smith-Waterman
+// (ksw_align2; no csub), reverse-strand regions are extended right-first
+// where bwa extends its reverse-complement space left-first (tie-breaking
+// only), and mem_flt_chained_seeds (long reads only) is not applied.
 #pragma once
 
 #include <cstdint>
@@ -30,14 +50,21 @@ struct AlignOptions {
   int w = 100;           // band width
   int chunk_size = 100000;
   int threads = 16;        // host threads for seeding / task building (bwa.nt)
-  int max_chains = 3;      // candidate chains extended per read
-  double drop_ratio = 0.5; // ... with at least this fraction of the best chain's hits (bwa -D)
+  double drop_ratio = 0.5;   // mem_chain_flt: a shadowed chain lighter than this x the heavier is dropped (bwa -D)
+  double mask_level = 0.5;   // query overlap that makes a region secondary / a chain shadowed (bwa mask_level)
+  double mask_level_redun = 0.95;  // mem_sort_dedup_patch's redundancy overlap
+  int max_chain_gap = 10000; // bwa max_chain_gap
+  int min_out_score = 30;    // bwa -T: regions scoring below are not output
+  int pen_unpaired = 17;     // bwa -U
+  int max_matesw = 50;       // bwa max_matesw: rescue anchors per read
+  int64_t read_id0 = 0;      // index of the batch's first read (pair) in the input: bwa's hash seed for ties
   std::string rg = "sample", sample = "sample", platform = "illumina", library = "sample";
 };
 
 struct AlignStats {
   int64_t reads = 0, mapped = 0, ext_tasks = 0, ext_cells = 0, global_tasks = 0;
-  int64_t proper = 0, rescued = 0;  // paired: reads flagged proper pair, mates rescued
+  int64_t proper = 0, rescued = 0;  // paired: reads flagged proper pair, reads given rescue windows
+  int64_t supplementary = 0;        // supplementary records (split reads)
   double seconds = 0, gpu_seconds = 0;
   // wall seconds of the phases: seeding + chaining, extension (host protocol +
   // GPU calls), pairing / primary choice, record building
@@ -73,19 +100,17 @@ std::string fmd_index_path(const std::string& fasta);
 // Builds and saves it (bwa index's role); sa_intv 0: automatic.
 void build_fmd_index(const std::string& fasta, int sa_intv);
 
-// Aligns FASTQ reads; records appended to `out` (unsorted).  Up to
-// max_chains candidate chains per read are extended; the best by truesc is
-// primary, the best other locus sets bwa's single-end MAPQ.
+// Aligns FASTQ reads single-end; records (primary, supplementary ones or an
+// unmapped one per read) appended to `out` (unsorted).
 AlignStats align_reads(const Reference& ref, const KmerIndex& idx, const std::vector<std::string>& names,
                        const std::vector<std::string>& seqs, const std::vector<std::string>& quals,
                        const AlignOptions& opt, std::vector<BamRecord>& out);
 
 // Paired-end batch (bwa mem_sam_pe's role): both mates seeded and extended in
-// one GPU round, the insert-size distribution estimated from the batch (FR
-// pairs, bwa mem_pestat's quartile bounds), mates rescued in the window the
-// distribution allows, the best pair chosen by score + insert-size likelihood
-// against the unpaired best - 17, then proper-pair / mate flags, RNEXT / PNEXT
-// / TLEN and paired MAPQ.  Records (read 1, read 2 per pair) appended to `out`.
+// the same GPU rounds, the insert-size distribution estimated from the batch,
+// mates rescued, the best pair chosen against the unpaired best - pen_unpaired,
+// then proper-pair / mate flags, RNEXT / PNEXT / TLEN (bwa's 5'-end rule) and
+// paired MAPQ.  Records (read 1's, then read 2's per pair) appended to `out`.
 AlignStats align_pairs(const Reference& ref, const KmerIndex& idx, const std::vector<std::string>& names,
                        const std::vector<std::string>& seqs1, const std::vector<std::string>& quals1,
                        const std::vector<std::string>& seqs2, const std::vector<std::string>& quals2,

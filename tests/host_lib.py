@@ -97,6 +97,28 @@ def read_bam(path):
     return names, lens, recs
 
 
+def parse_aux(aux):
+    """BAM aux bytes -> {tag: value} (Z strings, integer types)."""
+    out, k = {}, 0
+    ints = {"c": "<b", "C": "<B", "s": "<h", "S": "<H", "i": "<i", "I": "<I"}
+    while k < len(aux):
+        tag, t = aux[k:k + 2].decode(), chr(aux[k + 2])
+        k += 3
+        if t == "Z":
+            e = aux.index(0, k)
+            out[tag] = aux[k:e].decode()
+            k = e + 1
+        elif t in ints:
+            out[tag] = struct.unpack_from(ints[t], aux, k)[0]
+            k += struct.calcsize(ints[t])
+        elif t == "A":
+            out[tag] = chr(aux[k])
+            k += 1
+        else:
+            raise ValueError(f"aux type {t}")
+    return out
+
+
 def cigar_ref_len(cig):
     n = 0
     for c in cig:

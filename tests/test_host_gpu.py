@@ -144,6 +144,78 @@ def test_align_end_to_end(gpu, data, tmp_path):
     assert same_cig / mapped >= 0.9, (same_cig, mapped)
 
 
+def test_align_split_reads_supplementary(gpu, data, tmp_path):
+    """Split reads (bwa mem_mark_primary_se + mem_reg2sam):
+    each chimeric read joins 55-70 bases of chr20 (forward) with the reverse
+    complement of 80-95 bases of chr21.  The longer part is the primary (soft
+    clips, its start exact), the shorter one a supplementary record (flag
+    0x800, hard clips, SEQ of the aligned part only, MAPQ <= the primary's),
+    and each carries an SA tag naming the other.  Unsplit reads of the same
+    run keep one record each."""
+    rng = np.random.default_rng(3)
+    contigs, name = {}, None
+    for ln in open(data / "ref.fasta").read().split("\n"):
+        if ln.startswith(">"):
+            name = ln[1:].split()[0]
+            contigs[name] = []
+        elif ln:
+            contigs[name].append(ln)
+    contigs = {k: "".join(v) for k, v in contigs.items()}
+    comp = str.maketrans("ACGTN", "TGCAN")
+    rc = lambda s: s.translate(comp)[::-1]
+    truth, lines = {}, []
+    for i in range(300):
+        l1 = int(rng.integers(55, 71))
+        l2 = 150 - l1
+        while True:
+            a = int(rng.integers(1000, len(contigs["chr20"]) - 1000))
+            b = int(rng.integers(1000, len(contigs["chr21"]) - 1000))
+            p1, p2 = contigs["chr20"][a:a + l1], contigs["chr21"][b:b + l2]
+            if "N" not in p1 + p2:
+                break
+        truth[f"split{i}"] = (a, l1, b, l2)
+        lines += [f"@split{i}", p1 + rc(p2), "+", "I" * 150]
+    for i in range(200):
+        a = int(rng.integers(1000, len(contigs["chr20"]) - 1000))
+        lines += [f"@whole{i}", contigs["chr20"][a:a + 150], "+", "I" * 150]
+        truth[f"whole{i}"] = (a,)
+    fq = tmp_path / "split.fastq"
+    fq.write_text("\n".join(lines) + "\n")
+    out = tmp_path / "split.bam"
+    p = H.run_cli("align", "-r", data / "ref.fasta", "-1", fq, "-o", out, env=ENV, cwd=tmp_path)
+    assert p.returncode == 0, p.stderr[-3000:]
+    names, _, recs = H.read_bam(out)
+    by = {}
+    for r in recs:
+        by.setdefault(r["name"], []).append(r)
+    cig = lambda r: "".join(r["cigar"])
+    good = 0
+    for nm, t in truth.items():
+        rs = by[nm]
+        prim = [r for r in rs if not r["flag"] & 0x800]
+        assert len(prim) == 1, (nm, [cig(r) for r in rs])
+        if len(t) == 1:
+            assert len(rs) == 1 and prim[0]["pos"] == t[0] and names[prim[0]["ref_id"]] == "chr20"
+            continue
+        a, l1, b, l2 = t
+        sup = [r for r in rs if r["flag"] & 0x800]
+        if len(sup) != 1:
+            continue
+        P, S = prim[0], sup[0]
+        ok = (names[P["ref_id"]], P["pos"], bool(P["flag"] & 0x10)) == ("chr21", b, True)
+        ok &= (names[S["ref_id"]], S["pos"], bool(S["flag"] & 0x10)) == ("chr20", a, False)
+        assert "H" not in cig(P) and "S" in cig(P), cig(P)
+        assert "S" not in cig(S) and "H" in cig(S), cig(S)
+        aligned = sum(int(c[:-1]) for c in S["cigar"] if c[-1] in "MI")
+        assert len(S["seq"]) == aligned
+        assert S["mapq"] <= P["mapq"]
+        xp, xs = H.parse_aux(P["aux"]), H.parse_aux(S["aux"])
+        assert xp["SA"] == f"chr20,{a + 1},+,{cig(S).replace('H', 'S')},{S['mapq']},{xs['NM']};", xp["SA"]
+        assert xs["SA"] == f"chr21,{b + 1},-,{cig(P)},{P['mapq']},{xp['NM']};", xs["SA"]
+        good += ok
+    assert good >= 0.95 * 300, good
+
+
 def test_align_paired_end(gpu, tmp_path):
     """Paired-end align (row f4): FR pairs of N(350, 50) fragments; 4% of the
     read-2 mates carry a mismatch every 16 bases, so no 19-mer seeds them and
