@@ -107,8 +107,6 @@ struct ReadAln {
   std::vector<std::pair<int, int>> outs;  // output regions and their MAPQ (first: primary)
 };
 
-int64_t aln_pos(const Cand& c) { return c.aln.rb; }
-int64_t aln_end(const Cand& c) { return c.aln.re; }
 // query span of a region on the ORIGINAL read
 int orig_qb(const Cand& c, int L) { return c.rev ? L - c.aln.qe : c.aln.qb; }
 int orig_qe(const Cand& c, int L) { return c.rev ? L - c.aln.qb : c.aln.qe; }

@@ -1,0 +1,90 @@
+/*
+ * TEST INFRASTRUCTURE ONLY — never shipped, never on a product path.
+ *
+ * A CPU stand-in for libfcship.so's banded Smith-Waterman entry points
+ * (fcs_bsw_extend, fcs_bsw_global), computed by the oracle's ksw_extend2 /
+ * ksw_global2 restatement (oracle/ksw_oracle.c), so that the `-m "not gpu"`
+ * tests can drive the aligner's host logic (chains, dedup / patch, primary /
+ * supplementary marking, pairing, SAM fields) in a container without a GPU.
+ * tests/test_align_host_cpu.py compiles it into a temporary directory and
+ * puts that directory first on LD_LIBRARY_PATH of the fcs-genome child it
+ * starts; the PairHMM entry points fail (FCS_ERR_DEVICE).  The GPU tests run
+ * the same commands on the real library.
+ */
+#include <stdlib.h>
+#include <string.h>
+
+#include "fcship.h"
+
+int oracle_ksw_extend2(int qlen, const uint8_t* query, int tlen, const uint8_t* target, int m, const int8_t* mat,
+                       int o_del, int e_del, int o_ins, int e_ins, int w, int end_bonus, int zdrop, int h0, int* qle_,
+                       int* tle_, int* gtle_, int* gscore_, int* max_off_, int64_t* cells);
+int oracle_ksw_global2(int qlen, const uint8_t* query, int tlen, const uint8_t* target, int m, const int8_t* mat,
+                       int o_del, int e_del, int o_ins, int e_ins, int w, int* n_cigar, uint32_t* cigar_out,
+                       int cigar_cap);
+
+static __thread const char* g_err = "";
+
+const char* fcs_last_error(void) { return g_err; }
+const char* fcs_version(void) { return "cpu-mock"; }
+int fcs_device_count(void) { return 1; }
+int fcs_device_warmup(int32_t device, int32_t sessions) {
+  (void)device;
+  (void)sessions;
+  return FCS_OK;
+}
+
+void fcs_bsw_params_default(fcs_bsw_params* p) {
+  memset(p, 0, sizeof *p);
+  for (int i = 0; i < 25; ++i) p->mat[i] = (i / 5 == 4 || i % 5 == 4) ? -1 : (i / 5 == i % 5 ? 1 : -4);
+  p->o_del = p->o_ins = 6;
+  p->e_del = p->e_ins = 1;
+  p->end_bonus = 5;
+  p->zdrop = 100;
+}
+
+int fcs_bsw_extend(const fcs_bsw_task* t, int32_t n, const fcs_bsw_params* p, fcs_bsw_result* r, int32_t device) {
+  (void)device;
+  for (int32_t k = 0; k < n; ++k) {
+    fcs_bsw_result* o = &r[k];
+    o->score = oracle_ksw_extend2(t[k].qlen, t[k].query, t[k].tlen, t[k].target, 5, p->mat, p->o_del, p->e_del,
+                                  p->o_ins, p->e_ins, t[k].w, p->end_bonus, p->zdrop, t[k].h0, &o->qle, &o->tle,
+                                  &o->gtle, &o->gscore, &o->max_off, NULL);
+  }
+  return FCS_OK;
+}
+
+int fcs_bsw_global(const fcs_bsw_task* t, int32_t n, const fcs_bsw_params* p, int32_t* scores, uint32_t* arena,
+                   const int64_t* off, const int32_t* cap, int32_t* n_cigar, int32_t device) {
+  (void)device;
+  int rc = FCS_OK;
+  for (int32_t k = 0; k < n; ++k) {
+    int nc = 0;
+    scores[k] = oracle_ksw_global2(t[k].qlen, t[k].query, t[k].tlen, t[k].target, 5, p->mat, p->o_del, p->e_del,
+                                   p->o_ins, p->e_ins, t[k].w, arena ? &nc : NULL, arena ? arena + off[k] : NULL,
+                                   arena ? cap[k] : 0);
+    if (arena) {
+      n_cigar[k] = nc;
+      if (nc > cap[k]) rc = FCS_ERR_INVALID;
+    }
+  }
+  if (rc != FCS_OK) g_err = "fcs_bsw_global: CIGAR longer than its cap";
+  return rc;
+}
+
+void fcs_phmm_opts_default(fcs_phmm_opts* o) { memset(o, 0, sizeof *o); }
+int fcs_phmm_compute_regions(const fcs_phmm_region* regions, int32_t n_regions, const fcs_phmm_opts* opts) {
+  (void)regions;
+  (void)n_regions;
+  (void)opts;
+  g_err = "CPU mock of libfcship: no PairHMM";
+  return FCS_ERR_DEVICE;
+}
+int fcs_phmm_last_rescued(int64_t* count) {
+  *count = 0;
+  return FCS_OK;
+}
+int fcs_phmm_last_device_ms(double* device_ms, double* rescue_ms) {
+  *device_ms = *rescue_ms = 0;
+  return FCS_OK;
+}

@@ -1,0 +1,77 @@
+"""CPU tests of `fcs-genome align`'s host logic (chains,
+mem_chain2aln rounds, dedup / patch, primary / supplementary marking, mate
+rescue, pairing, SAM fields).  The fcs-genome child process runs against
+tests/cpu_mock/libfcship.so — the banded-SW entry points computed by the
+oracle's ksw_extend2 / ksw_global2 (test infrastructure only; the product
+library has no CPU path).  The same cases run on the GPU in test_host_gpu.py."""
+import re
+import subprocess
+
+import pytest
+
+import align_cases as A
+import host_lib as H
+
+ROOT = __import__("os").path.dirname(__import__("os").path.dirname(__import__("os").path.abspath(__file__)))
+
+
+@pytest.fixture(scope="module")
+def mock_env(tmp_path_factory):
+    d = tmp_path_factory.mktemp("mock")
+    subprocess.run(["gcc", "-O2", "-shared", "-fPIC", "-I", f"{ROOT}/include", f"{ROOT}/tests/cpu_mock/fcship_mock.c",
+                    f"{ROOT}/oracle/ksw_oracle.c", "-o", str(d / "libfcship.so")], check=True)
+    return {"LD_LIBRARY_PATH": str(d), "FCS_GPU_DEVICES": "0"}
+
+
+@pytest.fixture(scope="module")
+def ref(tmp_path_factory, mock_env):
+    d = tmp_path_factory.mktemp("ref")
+    p = H.run_cli("synth", "-o", d, "-c", "chr20:150000,chr21:60000", "-x", "1", "--seed", "11", "--no-fastq")
+    assert p.returncode == 0, p.stderr[-2000:]
+    return d / "ref.fasta"
+
+
+def test_mock_is_loaded(mock_env, ref, tmp_path):
+    fq = tmp_path / "r.fastq"
+    A.split_reads_fastq(ref, fq, n_split=2, n_whole=2, seed=1)
+    p = H.run_cli("align", "-r", ref, "-1", fq, "-o", tmp_path / "o.bam", env=mock_env, cwd=tmp_path)
+    assert p.returncode == 0, p.stderr[-2000:]
+    p = H.run_cli("--version", env=mock_env, cwd=tmp_path)
+    assert "cpu-mock" in p.stdout + p.stderr, (p.stdout, p.stderr)
+
+
+def test_split_reads_cpu(mock_env, ref, tmp_path):
+    fq = tmp_path / "split.fastq"
+    truth = A.split_reads_fastq(ref, fq, n_split=120, n_whole=60, seed=3)
+    out = tmp_path / "split.bam"
+    p = H.run_cli("align", "-r", ref, "-1", fq, "-o", out, env=mock_env, cwd=tmp_path)
+    assert p.returncode == 0, p.stderr[-3000:]
+    good, bad = A.check_split_reads(out, truth)
+    assert good >= 0.95 * 120, (good, len(bad), bad[:5])
+    assert re.search(r"(\d+) supplementary", p.stderr).group(1) == str(sum(len(t) == 4 for t in truth.values()) - len(bad))
+
+
+def test_paired_end_cpu(mock_env, tmp_path):
+    d = tmp_path / "pe"
+    p = H.run_cli("synth", "-o", d, "-c", "chr1:150000", "-x", "6", "--paired", "350", "--seed", "77")
+    assert p.returncode == 0, p.stderr[-2000:]
+    damaged = A.damage_mates(d / "sample_2.fastq")
+    out = tmp_path / "pe.bam"
+    p = H.run_cli("align", "-r", d / "ref.fasta", "-1", d / "sample_1.fastq", "-2", d / "sample_2.fastq", "-o", out,
+                  env=mock_env, cwd=tmp_path)
+    assert p.returncode == 0, p.stderr[-3000:]
+    A.check_pairs(p.stderr, out, d / "pairs_truth.tsv", damaged)
+
+
+def test_paired_split_reads_cpu(mock_env, tmp_path):
+    """A split read 1 (bwa is_multi): no pairing, read 1 as primary +
+    supplementary, mate fields of the other read's primary on every record."""
+    d = tmp_path / "pe"
+    p = H.run_cli("synth", "-o", d, "-c", "chr1:150000,chr2:60000", "-x", "4", "--paired", "350", "--seed", "78")
+    assert p.returncode == 0, p.stderr[-2000:]
+    chim = A.append_chimeric_pairs(d / "ref.fasta", d / "sample_1.fastq", d / "sample_2.fastq", 40, 5, "chr1", "chr2")
+    out = tmp_path / "pe.bam"
+    p = H.run_cli("align", "-r", d / "ref.fasta", "-1", d / "sample_1.fastq", "-2", d / "sample_2.fastq", "-o", out,
+                  env=mock_env, cwd=tmp_path)
+    assert p.returncode == 0, p.stderr[-3000:]
+    assert A.check_chimeric_pairs(out, chim, "chr1", "chr2") >= 38

@@ -145,75 +145,17 @@ def test_align_end_to_end(gpu, data, tmp_path):
 
 
 def test_align_split_reads_supplementary(gpu, data, tmp_path):
-    """Split reads (bwa mem_mark_primary_se + mem_reg2sam):
-    each chimeric read joins 55-70 bases of chr20 (forward) with the reverse
-    complement of 80-95 bases of chr21.  The longer part is the primary (soft
-    clips, its start exact), the shorter one a supplementary record (flag
-    0x800, hard clips, SEQ of the aligned part only, MAPQ <= the primary's),
-    and each carries an SA tag naming the other.  Unsplit reads of the same
-    run keep one record each."""
-    rng = np.random.default_rng(3)
-    contigs, name = {}, None
-    for ln in open(data / "ref.fasta").read().split("\n"):
-        if ln.startswith(">"):
-            name = ln[1:].split()[0]
-            contigs[name] = []
-        elif ln:
-            contigs[name].append(ln)
-    contigs = {k: "".join(v) for k, v in contigs.items()}
-    comp = str.maketrans("ACGTN", "TGCAN")
-    rc = lambda s: s.translate(comp)[::-1]
-    truth, lines = {}, []
-    for i in range(300):
-        l1 = int(rng.integers(55, 71))
-        l2 = 150 - l1
-        while True:
-            a = int(rng.integers(1000, len(contigs["chr20"]) - 1000))
-            b = int(rng.integers(1000, len(contigs["chr21"]) - 1000))
-            p1, p2 = contigs["chr20"][a:a + l1], contigs["chr21"][b:b + l2]
-            if "N" not in p1 + p2:
-                break
-        truth[f"split{i}"] = (a, l1, b, l2)
-        lines += [f"@split{i}", p1 + rc(p2), "+", "I" * 150]
-    for i in range(200):
-        a = int(rng.integers(1000, len(contigs["chr20"]) - 1000))
-        lines += [f"@whole{i}", contigs["chr20"][a:a + 150], "+", "I" * 150]
-        truth[f"whole{i}"] = (a,)
+    """Split reads on the GPU: tests/align_cases.py builds the
+    chimeric reads and checks primary / supplementary placement, hard clips,
+    MAPQ and the SA tags."""
+    import align_cases as A
     fq = tmp_path / "split.fastq"
-    fq.write_text("\n".join(lines) + "\n")
+    truth = A.split_reads_fastq(data / "ref.fasta", fq, n_split=300, n_whole=200, seed=3)
     out = tmp_path / "split.bam"
     p = H.run_cli("align", "-r", data / "ref.fasta", "-1", fq, "-o", out, env=ENV, cwd=tmp_path)
     assert p.returncode == 0, p.stderr[-3000:]
-    names, _, recs = H.read_bam(out)
-    by = {}
-    for r in recs:
-        by.setdefault(r["name"], []).append(r)
-    cig = lambda r: "".join(r["cigar"])
-    good = 0
-    for nm, t in truth.items():
-        rs = by[nm]
-        prim = [r for r in rs if not r["flag"] & 0x800]
-        assert len(prim) == 1, (nm, [cig(r) for r in rs])
-        if len(t) == 1:
-            assert len(rs) == 1 and prim[0]["pos"] == t[0] and names[prim[0]["ref_id"]] == "chr20"
-            continue
-        a, l1, b, l2 = t
-        sup = [r for r in rs if r["flag"] & 0x800]
-        if len(sup) != 1:
-            continue
-        P, S = prim[0], sup[0]
-        ok = (names[P["ref_id"]], P["pos"], bool(P["flag"] & 0x10)) == ("chr21", b, True)
-        ok &= (names[S["ref_id"]], S["pos"], bool(S["flag"] & 0x10)) == ("chr20", a, False)
-        assert "H" not in cig(P) and "S" in cig(P), cig(P)
-        assert "S" not in cig(S) and "H" in cig(S), cig(S)
-        aligned = sum(int(c[:-1]) for c in S["cigar"] if c[-1] in "MI")
-        assert len(S["seq"]) == aligned
-        assert S["mapq"] <= P["mapq"]
-        xp, xs = H.parse_aux(P["aux"]), H.parse_aux(S["aux"])
-        assert xp["SA"] == f"chr20,{a + 1},+,{cig(S).replace('H', 'S')},{S['mapq']},{xs['NM']};", xp["SA"]
-        assert xs["SA"] == f"chr21,{b + 1},-,{cig(P)},{P['mapq']},{xp['NM']};", xs["SA"]
-        good += ok
-    assert good >= 0.95 * 300, good
+    good, bad = A.check_split_reads(out, truth)
+    assert good >= 0.95 * 300, (good, len(bad), bad[:5])
 
 
 def test_align_paired_end(gpu, tmp_path):
@@ -227,10 +169,6 @@ def test_align_paired_end(gpu, tmp_path):
     p = H.run_cli("synth", "-o", d, "-c", "chr1:400000", "-x", "16", "--paired", "350", "--seed", "77",
                   env=ENV, cwd=tmp_path, timeout=600)
     assert p.returncode == 0, p.stderr[-2000:]
-    truth = {}
-    for line in open(d / "pairs_truth.tsv"):
-        name, mate, contig, pos, rev = line.split()
-        truth[(name, int(mate))] = (int(contig), int(pos), int(rev))
     # damage some read-2 mates: a mismatch every 16 bases defeats 19-mer seeding
     lines = open(d / "sample_2.fastq").read().split("\n")
     damaged = set()
@@ -247,38 +185,8 @@ def test_align_paired_end(gpu, tmp_path):
     p = H.run_cli("align", "-r", d / "ref.fasta", "-1", d / "sample_1.fastq", "-2", d / "sample_2.fastq", "-o", out,
                   env=ENV, cwd=tmp_path)
     assert p.returncode == 0, p.stderr[-3000:]
-    m = re.search(r"insert ([\d.]+) \+- ([\d.]+) \[(\d+), (\d+)\] from (\d+) pairs", p.stderr)
-    assert m, p.stderr[-1000:]
-    avg, sd = float(m.group(1)), float(m.group(2))
-    assert abs(avg - 350) < 15 and 35 < sd < 65, (avg, sd)
-    _, _, recs = H.read_bam(out)
-    by = {}
-    for r in recs:
-        by[(r["name"], 1 if r["flag"] & 0x40 else 2)] = r
-    assert len(by) == len(truth) and len(recs) == len(truth)
-    ok = mapped = proper = resc_ok = 0
-    for (name, mate), r in by.items():
-        assert r["flag"] & 0x1 and (r["flag"] & 0xC0) in (0x40, 0x80)
-        o = by[(name, 3 - mate)]
-        assert r["next_pos"] == o["pos"] and r["next_ref_id"] == o["ref_id"]
-        assert bool(r["flag"] & 0x8) == bool(o["flag"] & 0x4)
-        if r["flag"] & 0x4:
-            continue
-        mapped += 1
-        assert bool(r["flag"] & 0x20) == bool(o["flag"] & 0x10)
-        c, pos, rev = truth[(name, mate)]
-        hit = (r["ref_id"], r["pos"], bool(r["flag"] & 0x10)) == (c, pos, bool(rev))
-        ok += hit
-        if r["flag"] & 0x2:
-            proper += 1
-            assert r["tlen"] == -o["tlen"] and abs(r["tlen"]) > 0
-        if mate == 2 and name in damaged:
-            resc_ok += hit
-    n = len(truth)
-    assert mapped / n >= 0.99, (mapped, n)
-    assert ok / mapped >= 0.97, (ok, mapped)
-    assert proper / n >= 0.95, (proper, n)
-    assert resc_ok >= 0.8 * len(damaged), (resc_ok, len(damaged))
+    import align_cases as A
+    A.check_pairs(p.stderr, out, d / "pairs_truth.tsv", damaged)
 
 
 def test_align_sample_sheet_over_two_slots(gpu, tmp_path):
