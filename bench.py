@@ -268,6 +268,7 @@ def bench_e2e(args, rank, local):
             tot = lambda pat, f=float: sum(f(x) for x in re.findall(pat, logs))  # noqa: E731
             st = {"regions": tot(r"(\d+) regions", int), "pairs": tot(r"(\d+) pairs", int),
                   "cells": tot(r"(\d+) cells", int), "rescued_pairs": tot(r"(\d+) rescued", int),
+                  "device_passes": tot(r"(\d+) device passes", int),
                   "seconds": round(dt, 3)}
             st["regions_per_s"] = round(st["regions"] / dt, 1)
             brk = {k: round(tot(pat), 3) for k, pat in (

@@ -73,6 +73,26 @@ __device__ __forceinline__ double sel_bits(uint32_t m, double a, double b) {
                                           ((unsigned long long)__double_as_longlong(b) & ~mm)));
 }
 
+// Hand-off to the next lane of a W-lane segment: row_shr:1 inside 16-lane DPP
+// rows, wave_shr:1 over the whole wave (the fp64 rescue's one-pair waves);
+// lane 0 of the segment keeps `old`.
+template <typename T, int W>
+__device__ __forceinline__ T dpp_shr1(T old, T src) {
+  if constexpr (W == 16) {
+    return dpp_row_shr1<T>(old, src);
+  } else {
+    static_assert(W == 64, "segments are 16 or 64 lanes");
+    if constexpr (sizeof(T) == 4) {
+      return __int_as_float(dpp_wave_shr1_i(__float_as_int(old), __float_as_int(src)));
+    } else {
+      const long long o = __double_as_longlong(old), v = __double_as_longlong(src);
+      const int lo = dpp_wave_shr1_i((int)o, (int)v);
+      const int hi = dpp_wave_shr1_i((int)(o >> 32), (int)(v >> 32));
+      return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
+    }
+  }
+}
+
 // Last-row accumulation as a plain VALU add: left to the compiler, the two
 // running sums get packed into v_pk_add_f32 with register moves around them.
 __device__ __forceinline__ void acc_add(float& a, float x) { asm("v_add_f32 %0, %1, %2" : "=v"(a) : "v"(a), "v"(x)); }
@@ -96,7 +116,7 @@ struct LaneState {
 };
 
 // One anti-diagonal step at t = t0 + S.
-template <typename T, bool EXACT, bool SUM, bool BC, bool COND, int S>
+template <typename T, bool EXACT, bool SUM, bool BC, bool COND, int W, int S>
 __device__ __forceinline__ void phmm_step(LaneState<T>& L, PhRing<T> (&pf)[PFD], int (&hq)[PFD],
                                           const unsigned char* __restrict__ hapl, const RowP<T>& p,
                                           PhRing<T>* __restrict__ ring, const int t0, const int sl, const bool top,
@@ -109,10 +129,10 @@ __device__ __forceinline__ void phmm_step(LaneState<T>& L, PhRing<T> (&pf)[PFD],
     pf[k] = pf[k + 1];
     hq[k] = hq[k + 1];
   }
-  pf[PFD - 1] = ring[t + 16 + PFD];  // lane-0 input for column t + PFD
-  hq[PFD - 1] = hapl[t + 16 + PFD - sl];  // this lane's hap base for column t + PFD - l
-  const T Xu = dpp_row_shr1<T>(cur.X, L.Xo);
-  const T I = dpp_row_shr1<T>(cur.I, L.Io);
+  pf[PFD - 1] = ring[t + W + PFD];  // lane-0 input for column t + PFD
+  hq[PFD - 1] = hapl[t + W + PFD - sl];  // this lane's hap base for column t + PFD - l
+  const T Xu = dpp_shr1<T, W>(cur.X, L.Xo);
+  const T I = dpp_shr1<T, W>(cur.I, L.Io);
   T prior;
   if constexpr (BC) {  // group with bytes outside A/C/G/T/N: GKL's byte compare
     prior = (hb == p.rbase || hb == 'N') ? p.e1 : p.e3;
@@ -134,7 +154,7 @@ __device__ __forceinline__ void phmm_step(LaneState<T>& L, PhRing<T> (&pf)[PFD],
     PhRing<T> o;
     o.X = Xn;
     o.I = In;
-    ring[t + 1] = o;  // column t - 15
+    ring[t + 1] = o;  // column t - (W - 1)
   }
   if constexpr (SUM) {
     // The summing lane runs the last row with my = yy = 1, so its D is the
@@ -156,13 +176,13 @@ __device__ __forceinline__ void phmm_step(LaneState<T>& L, PhRing<T> (&pf)[PFD],
   L.Do = D;
 }
 
-template <typename T, bool EXACT, bool SUM, bool BC, bool COND>
+template <typename T, bool EXACT, bool SUM, bool BC, bool COND, int W>
 __device__ __forceinline__ void phmm_block(LaneState<T>& L, PhRing<T> (&pf)[PFD], int (&hq)[PFD],
                                            const unsigned char* __restrict__ hapl, const RowP<T>& p,
                                            PhRing<T>* __restrict__ ring, const int t0, const int sl, const bool top,
                                            const int lim, T& accM, T& accI) {
   [&]<int... S>(std::integer_sequence<int, S...>) {
-    (phmm_step<T, EXACT, SUM, BC, COND, S>(L, pf, hq, hapl, p, ring, t0, sl, top, lim, accM, accI), ...);
+    (phmm_step<T, EXACT, SUM, BC, COND, W, S>(L, pf, hq, hapl, p, ring, t0, sl, top, lim, accM, accI), ...);
   }(std::make_integer_sequence<int, 16>{});
 }
 
@@ -217,7 +237,7 @@ __device__ __forceinline__ RowP<T> row_params(const PhmmTables<T>& tab, const Ra
 
 // One stripe: nblk blocks of 16 steps; the next stripe's parameters are
 // gathered after the first block (their bytes were requested at stripe start).
-template <typename T, bool EXACT, bool SUM, bool BC>
+template <typename T, bool EXACT, bool SUM, bool BC, int W>
 __device__ __forceinline__ void phmm_stripe(const RowP<T>& p, PhRing<T>* __restrict__ ring,
                                             const unsigned char* __restrict__ hapl, const int sl, const int nblk,
                                             const int lim, const int ulim, T& accM, T& accI,
@@ -229,21 +249,21 @@ __device__ __forceinline__ void phmm_stripe(const RowP<T>& p, PhRing<T>* __restr
   int hq[PFD];
 #pragma unroll
   for (int k = 0; k < PFD; ++k) {
-    pf[k] = ring[16 + k];
-    hq[k] = hapl[16 + k - sl];
+    pf[k] = ring[W + k];
+    hq[k] = hapl[W + k - sl];
   }
   // ulim: the smallest last-column step of the summing lanes (wave-uniform);
   // blocks that end before it need no compare
   if (!SUM || 15 < ulim)
-    phmm_block<T, EXACT, SUM, BC, false>(L, pf, hq, hapl, p, ring, 0, sl, top, lim, accM, accI);
+    phmm_block<T, EXACT, SUM, BC, false, W>(L, pf, hq, hapl, p, ring, 0, sl, top, lim, accM, accI);
   else
-    phmm_block<T, EXACT, SUM, BC, true>(L, pf, hq, hapl, p, ring, 0, sl, top, lim, accM, accI);
+    phmm_block<T, EXACT, SUM, BC, true, W>(L, pf, hq, hapl, p, ring, 0, sl, top, lim, accM, accI);
   np = row_params<T, EXACT>(tab, nraw);
   for (int blk = 1; blk < nblk; ++blk) {
     if (!SUM || 16 * blk + 15 < ulim)
-      phmm_block<T, EXACT, SUM, BC, false>(L, pf, hq, hapl, p, ring, 16 * blk, sl, top, lim, accM, accI);
+      phmm_block<T, EXACT, SUM, BC, false, W>(L, pf, hq, hapl, p, ring, 16 * blk, sl, top, lim, accM, accI);
     else
-      phmm_block<T, EXACT, SUM, BC, true>(L, pf, hq, hapl, p, ring, 16 * blk, sl, top, lim, accM, accI);
+      phmm_block<T, EXACT, SUM, BC, true, W>(L, pf, hq, hapl, p, ring, 16 * blk, sl, top, lim, accM, accI);
   }
 }
 
@@ -257,7 +277,7 @@ __host__ __device__ constexpr int ring_stride(int nslot) {
   return nslot * (int)sizeof(PhRing<T>);
 }
 
-template <typename T, bool EXACT, bool RESCUE_PASS>
+template <typename T, bool EXACT, bool RESCUE_PASS, int W = 16>
 __global__ __launch_bounds__(64, (sizeof(T) == 4 && !EXACT) ? 4 : 1) void phmm_kernel(const PhmmDevBatch b, const int32_t* __restrict__ order,
                                                   const unsigned long long* __restrict__ count_dev,
                                                   long long count_host, const int64_t* __restrict__ bounds,
@@ -267,8 +287,8 @@ __global__ __launch_bounds__(64, (sizeof(T) == 4 && !EXACT) ? 4 : 1) void phmm_k
                                                   const int use_rescue, const int nseg) {
   extern __shared__ __align__(16) unsigned char smem_raw[];
   const int lane = threadIdx.x;
-  const int seg = lane >> 4;
-  const int sl = lane & 15;
+  const int seg = lane / W;
+  const int sl = lane & (W - 1);
   // nseg = 4: four pairs per wave, one LDS ring each.  nseg = 1 (haplotypes too
   // long for four rings in 160 KB): one pair per wave, segments 1..3 idle on
   // segment 0's ring (they never write it: `top` and the setup are theirs only
@@ -277,7 +297,7 @@ __global__ __launch_bounds__(64, (sizeof(T) == 4 && !EXACT) ? 4 : 1) void phmm_k
   const int rseg = own_seg ? seg : 0;
   PhRing<T>* const ring = reinterpret_cast<PhRing<T>*>(smem_raw + rseg * ring_stride<T>(nslot));
   unsigned char* const hapl = smem_raw + (size_t)nseg * ring_stride<T>(nslot) + rseg * nslot;
-  const bool top = own_seg && sl == 15;
+  const bool top = own_seg && sl == W - 1;
   // forward pass: this launch's hap-length class of the sorted schedule; rescue: the device-side list count
   long long count = count_dev ? (long long)(*count_dev) : count_host;
   if (bounds) {
@@ -300,7 +320,7 @@ __global__ __launch_bounds__(64, (sizeof(T) == 4 && !EXACT) ? 4 : 1) void phmm_k
     }
     const bool active = (p >= 0) && R > 0 && H > 0;
     if (p >= 0 && !active && sl == 0) out[p] = -INFINITY;
-    const int nstr = active ? (R + 15) >> 4 : 0;
+    const int nstr = active ? (R + W - 1) / W : 0;
     const int Hmax = wave_max(active ? H : 0);
     const int nstr_max = wave_max(nstr);
     if (nstr_max == 0) continue;
@@ -318,16 +338,16 @@ __global__ __launch_bounds__(64, (sizeof(T) == 4 && !EXACT) ? 4 : 1) void phmm_k
     // any is used, so a haplotype costs ~3 memory round trips, not one per slot.
     bool other = false;
     constexpr int kHB = 8;
-    for (int s0 = sl; s0 < nslot; s0 += 16 * kHB) {
+    for (int s0 = sl; s0 < nslot; s0 += W * kHB) {
       unsigned char raw[kHB];
 #pragma unroll
       for (int u = 0; u < kHB; ++u) {
-        const int c = s0 + 16 * u - 16;
-        raw[u] = (active && c >= 1 && c <= H && c + 16 < nslot) ? b.hb[ho + c - 1] : (unsigned char)0;
+        const int c = s0 + W * u - W;
+        raw[u] = (active && c >= 1 && c <= H && c + W < nslot) ? b.hb[ho + c - 1] : (unsigned char)0;
       }
 #pragma unroll
       for (int u = 0; u < kHB; ++u) {
-        const int s = s0 + 16 * u, c = s - 16;
+        const int s = s0 + W * u, c = s - W;
         if (own_seg && s < nslot) {
           PhRing<T> v;
           v.X = (c >= 0 && c <= H) ? x0 : (T)0;
@@ -342,18 +362,18 @@ __global__ __launch_bounds__(64, (sizeof(T) == 4 && !EXACT) ? 4 : 1) void phmm_k
     }
     const bool bytecmp = __ballot(other) != 0ull;
     if (bytecmp && own_seg)
-      for (int s = sl; s < nslot; s += 16) {
-        const int c = s - 16;
+      for (int s = sl; s < nslot; s += W) {
+        const int c = s - W;
         hapl[s] = (active && c >= 1 && c <= H) ? b.hb[ho + c - 1] : (unsigned char)0;
       }
     __syncthreads();
 
     RowP<T> prm = row_params<T, EXACT>(tab, load_raw(b, active ? R : 0, ro, sl));
     T accM = 0, accI = 0;
-    const int sum_stripe = active ? (R - 1) >> 4 : -1;
-    const int sum_lane = active ? (R - 1) & 15 : -1;
+    const int sum_stripe = active ? (R - 1) / W : -1;
+    const int sum_lane = active ? (R - 1) % W : -1;
     for (int st = 0; st < nstr_max; ++st) {
-      const RawRow nraw = load_raw(b, active ? R : 0, ro, (st + 1) * 16 + sl);
+      const RawRow nraw = load_raw(b, active ? R : 0, ro, (st + 1) * W + sl);
       RowP<T> nprm;
       const bool seg_sums = (st == sum_stripe);
       const int any_sum = wave_max(seg_sums ? 1 : 0);
@@ -363,13 +383,13 @@ __global__ __launch_bounds__(64, (sizeof(T) == 4 && !EXACT) ? 4 : 1) void phmm_k
         const int lim = (seg_sums && sl == sum_lane) ? sl + H : -1;
         const int ulim = -wave_max((seg_sums && sl == sum_lane) ? -(sl + H) : -0x7FFFFFFF);
         accM = accI = 0;  // a sum lives within its stripe; drop what unconditional blocks added before
-        const int tend = cont ? Hmax + 15 : wave_max(seg_sums ? sum_lane + H : 0);
+        const int tend = cont ? Hmax + W - 1 : wave_max(seg_sums ? sum_lane + H : 0);
         RowP<T> sp = prm;  // the last row's D feeds only rows past R: reuse it as the M sum
         if (lim >= 0) sp.my = sp.yy = (T)1;
         if (bytecmp)
-          phmm_stripe<T, EXACT, true, true>(sp, ring, hapl, sl, (tend + 16) >> 4, lim, ulim, accM, accI, tab, nraw, nprm, top);
+          phmm_stripe<T, EXACT, true, true, W>(sp, ring, hapl, sl, (tend + 16) >> 4, lim, ulim, accM, accI, tab, nraw, nprm, top);
         else
-          phmm_stripe<T, EXACT, true, false>(sp, ring, hapl, sl, (tend + 16) >> 4, lim, ulim, accM, accI, tab, nraw, nprm, top);
+          phmm_stripe<T, EXACT, true, false, W>(sp, ring, hapl, sl, (tend + 16) >> 4, lim, ulim, accM, accI, tab, nraw, nprm, top);
         if (seg_sums && sl == sum_lane) {
           const T sum = accM + accI;
           if constexpr (RESCUE_PASS) {
@@ -386,9 +406,9 @@ __global__ __launch_bounds__(64, (sizeof(T) == 4 && !EXACT) ? 4 : 1) void phmm_k
         }
       } else {
         if (bytecmp)
-          phmm_stripe<T, EXACT, false, true>(prm, ring, hapl, sl, (Hmax + 31) >> 4, -1, -1, accM, accI, tab, nraw, nprm, top);
+          phmm_stripe<T, EXACT, false, true, W>(prm, ring, hapl, sl, (Hmax + W + 15) >> 4, -1, -1, accM, accI, tab, nraw, nprm, top);
         else
-          phmm_stripe<T, EXACT, false, false>(prm, ring, hapl, sl, (Hmax + 31) >> 4, -1, -1, accM, accI, tab, nraw, nprm, top);
+          phmm_stripe<T, EXACT, false, false, W>(prm, ring, hapl, sl, (Hmax + W + 15) >> 4, -1, -1, accM, accI, tab, nraw, nprm, top);
       }
       prm = nprm;
     }
@@ -406,6 +426,10 @@ namespace fcs {
 // stripes run to Hmax + 15 rounded up to a 16-step block, plus up to four steps of
 // read-ahead.
 static __host__ __device__ int nslot_for(int max_hap_len) { return ((max_hap_len + 51 + 15) / 16) * 16; }
+// The same for W-lane segments: columns -W .. Hmax + 2W + 14 + PFD.
+static __host__ __device__ int nslot_for_w(int max_hap_len, int W) {
+  return ((max_hap_len + 2 * W + 19 + 15) / 16) * 16;
+}
 
 // Hap-length classes of the forward pass: class c < kPhmmClasses - 1 holds
 // pairs with nslot_for(H) <= 224 + 32c (LDS 8.1 .. 12.7 KB per wave), the last
@@ -491,16 +515,17 @@ int launch_phmm_bounds(const uint32_t* sorted_keys, int64_t n, int64_t* bounds, 
 
 constexpr size_t kLdsBytes = 160 * 1024;
 
-template <typename T, bool EXACT, bool RESCUE>
+template <typename T, bool EXACT, bool RESCUE, int W = 16>
 static int launch_one(const PhmmDevBatch& b, const int32_t* order, const unsigned long long* count_dev,
                       long long count_host, const int64_t* bounds, int cls, int nslot, long long max_groups,
                       const PhmmTables<T>& tab, double* out, int32_t* rescue_list, unsigned long long* rescue_count,
                       float thr, bool use_rescue, hipStream_t s) {
   // Four rings per wave when they fit the 160 KB of LDS, else one (long
   // haplotypes: fp32 up to ~4.5 kb at four, ~18 kb at one; fp64 ~2.3 / ~9.5 kb).
-  int nseg = 4;
-  size_t lds = (size_t)4 * (ring_stride<T>(nslot) + nslot);
-  if (lds > kLdsBytes) {
+  // 64-lane segments: one pair (one ring) per wave.
+  int nseg = 64 / W;
+  size_t lds = (size_t)nseg * (ring_stride<T>(nslot) + nslot);
+  if (lds > kLdsBytes && nseg > 1) {
     nseg = 1;
     lds = (size_t)ring_stride<T>(nslot) + nslot;
     max_groups *= 4;
@@ -508,7 +533,7 @@ static int launch_one(const PhmmDevBatch& b, const int32_t* order, const unsigne
   if (lds > kLdsBytes)
     return fail(FCS_ERR_UNSUPPORTED, "[E::fcship] haplotype too long for the LDS boundary ring (max_hap_len " +
                                          std::to_string(nslot - 67) + ")");
-  auto kern = phmm_kernel<T, EXACT, RESCUE>;
+  auto kern = phmm_kernel<T, EXACT, RESCUE, W>;
   if (lds > 64 * 1024)
     FCS_HIP_CHECK(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
   long long grid = max_groups;
@@ -663,8 +688,20 @@ int launch_phmm_rescue(const PhmmDevBatch& b, const int32_t* list, const unsigne
                        int64_t max_count, int max_hap_len, const DeviceTables& t, bool exact, double* out,
                        hipStream_t s) {
   if (max_count <= 0) return FCS_OK;
-  // The rescued subset is usually tiny: a modest grid that strides over the
-  // device-side count, so no host round trip is needed.
+  // The rescued subset is usually tiny (tens to hundreds of pairs per call), so
+  // its time is one pair's latency: 64-lane segments, one pair per wave, run
+  // 64-row stripes — a third of the 16-row stripes' sequential steps at 150-base
+  // reads.  A modest grid strides over the device-side count (no host round
+  // trip).  Haplotypes too long for a 64-lane ring take the 16-lane kernel.
+  const int ns64 = nslot_for_w(max_hap_len, 64);
+  if ((size_t)ring_stride<double>(ns64) + ns64 <= kLdsBytes) {
+    const long long g64 = std::min<long long>(max_count, 4096);
+    if (exact)
+      return launch_one<double, true, true, 64>(b, list, count_dev, 0, nullptr, 0, ns64, g64, t.td, out, nullptr,
+                                                nullptr, 0.f, false, s);
+    return launch_one<double, false, true, 64>(b, list, count_dev, 0, nullptr, 0, ns64, g64, t.td, out, nullptr,
+                                               nullptr, 0.f, false, s);
+  }
   long long groups = (max_count + 3) / 4;
   if (groups > 2048) groups = 2048;
   if (exact)

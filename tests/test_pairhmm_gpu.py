@@ -120,6 +120,28 @@ def test_rescue_path(gpu, exact):
     assert used.sum() > 0, "test must exercise the fp64 rescue"
 
 
+@pytest.mark.parametrize("exact", [True, False])
+def test_rescue_every_pair(gpu, exact):
+    """Threshold 1e30 sends every pair to the fp64 rescue (64-lane segments,
+    64-row stripes, one pair per wave): read lengths on both sides of each
+    multiple of 64 and haplotypes from 1 base up, against the oracle's fp64
+    forward sum (log10(sum) - log10(2^1020), GKL's rescue value)."""
+    rng = np.random.default_rng(64)
+    reads = []
+    for R in (1, 2, 15, 16, 17, 63, 64, 65, 100, 127, 128, 129, 150, 191, 192, 193, 300):
+        rd = list(rand_read(rng, R))
+        reads.append(tuple(rd))
+    haps = [rng.choice(np.frombuffer(b"ACGT", np.uint8), n) for n in (1, 7, 64, 65, 200, 333)]
+    haps.append(np.frombuffer(b"ACGTNACGRT", np.uint8))  # a byte outside A/C/G/T/N: the byte-compare path
+    p = fcship.make_pairs(reads, haps)
+    out = fcship.phmm_compute_pairs(p, exact=exact, threshold=1e30)
+    ref = np.array([np.log10(oracle_lib.phmm_prob_d(reads[i // len(haps)], haps[i % len(haps)])) -
+                    np.log10(2.0 ** 1020) for i in range(p.n_pairs)])
+    tol = (1e-12 if exact else 1e-9) * np.abs(ref) + 1e-12
+    bad = np.abs(out - ref) > tol
+    assert not bad.any(), (np.flatnonzero(bad)[:5], out[bad][:5], ref[bad][:5])
+
+
 def test_no_rescue_option(gpu):
     reads, haps = random_batch(5, 8, 2, 100, 101, 200, 200, related=False)
     p = fcship.make_pairs(reads, haps)
