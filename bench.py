@@ -304,17 +304,21 @@ def bench_e2e(args, rank, local):
         a = work + "/a"
         (dt, _, err), runs = best("align", ["align", "-f", "-r", a + "/ref.fasta", "-1", a + "/sample_1.fastq", "-2",
                                             a + "/sample_2.fastq", "-o", work + "/aln.bam"])
-        m = re.search(r"(\d+) reads, (\d+) mapped, (\d+) extension tasks, (\d+) global alignments, ([\d.]+) s "
-                      r"\(GPU calls ([\d.]+) s\)", err)
+        m = re.search(r"(\d+) reads, (\d+) mapped, (\d+) supplementary, (\d+) extension tasks, (\d+) global "
+                      r"alignments, ([\d.]+) s \(GPU calls ([\d.]+) s\)", err)
         pm = re.search(r"(\d+) reads properly paired, (\d+) mates rescued, insert ([\d.]+) \+- ([\d.]+)", err)
-        n = int(m.group(1)) if m else 0
+        ph = re.search(r"alignment thread-seconds ([\d.]+): seeding ([\d.]+), extension ([\d.]+), pairing ([\d.]+), "
+                       r"records ([\d.]+)", err)
+        if not (m and pm and ph):
+            raise RuntimeError("fcs-genome align report not understood: " + err[-2000:])
+        n = int(m.group(1))
         out["align"] = {"mode": f"paired-end 2x151, fragments N(350, 50), {args.e2e_align_mbp:g} Mbp genome, 30x "
-                                "of pairs", "reads": n,
-                        "mapped": int(m.group(2)) if m else 0, "ext_tasks": int(m.group(3)) if m else 0,
-                        "global_tasks": int(m.group(4)) if m else 0,
-                        "gpu_call_seconds": float(m.group(6)) if m else None,
-                        "proper_pair_reads": int(pm.group(1)) if pm else None,
-                        "mates_rescued": int(pm.group(2)) if pm else None,
+                                "of pairs", "reads": n, "mapped": int(m.group(2)), "supplementary": int(m.group(3)),
+                        "ext_tasks": int(m.group(4)), "global_tasks": int(m.group(5)),
+                        "gpu_call_seconds": float(m.group(7)),
+                        "thread_seconds": {k: float(ph.group(i + 1)) for i, k in
+                                           enumerate(("total", "seeding", "extension", "pairing", "records"))},
+                        "proper_pair_reads": int(pm.group(1)), "mates_rescued": int(pm.group(2)),
                         "seconds": round(dt, 3), "runs_seconds": runs, "reads_per_s": round(n / dt, 1)}
         return out
     finally:

@@ -1246,7 +1246,6 @@ AlignStats align_pairs(const Reference& ref, const KmerIndex& idx, const std::ve
       if (added[i][0]) resc.push_back(&m1[i]);
       if (added[i][1]) resc.push_back(&m2[i]);
     }
-    st.rescued = (int64_t)resc.size();
     const uint64_t te = now_us();
     extend_loose(idx, P, opt, resc, st);
     dedup_patch(idx, P, opt, resc, false, st);
@@ -1326,6 +1325,8 @@ AlignStats align_pairs(const Reference& ref, const KmerIndex& idx, const std::ve
     st.mapped += !m1[i].outs.empty() + !m2[i].outs.empty();
     st.supplementary += (m1[i].outs.empty() ? 0 : m1[i].outs.size() - 1) + (m2[i].outs.empty() ? 0 : m2[i].outs.size() - 1);
     st.proper += 2 * proper[i];
+    for (const ReadAln* R : {&m1[i], &m2[i]})  // placed by the mate rescue
+      st.rescued += !R->outs.empty() && R->cands[R->outs[0].first].rescued;
   }
   st.reads = 2 * (int64_t)n;
   st.seconds = (now_us() - t0) / 1e6;

@@ -63,7 +63,7 @@ struct AlignOptions {
 
 struct AlignStats {
   int64_t reads = 0, mapped = 0, ext_tasks = 0, ext_cells = 0, global_tasks = 0;
-  int64_t proper = 0, rescued = 0;  // paired: reads flagged proper pair, reads given rescue windows
+  int64_t proper = 0, rescued = 0;  // paired: reads flagged proper pair, reads placed by the mate rescue
   int64_t supplementary = 0;        // supplementary records (split reads)
   double seconds = 0, gpu_seconds = 0;
   // wall seconds of the phases: seeding + chaining, extension (host protocol +

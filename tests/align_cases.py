@@ -138,6 +138,8 @@ def check_pairs(stderr, bam, truth_tsv, damaged, sd_range=(35, 65)):
     assert ok / mapped >= 0.97, (ok, mapped)
     assert proper / n >= 0.95, (proper, n)
     assert resc_ok >= 0.8 * len(damaged), (resc_ok, len(damaged))
+    nres = int(re.search(r"(\d+) mates rescued", stderr).group(1))  # reads placed by the mate rescue
+    assert nres >= 0.8 * len(damaged), (nres, len(damaged))
 
 
 def damage_mates(fastq, every=25, offset=7):

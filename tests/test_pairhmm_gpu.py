@@ -122,7 +122,7 @@ def test_rescue_path(gpu, exact):
 
 @pytest.mark.parametrize("exact", [True, False])
 def test_rescue_every_pair(gpu, exact):
-    """Threshold 1e30 sends every pair to the fp64 rescue (64-lane segments,
+    """Threshold 1e37 (above 2^120, the fp32 pass's largest possible sum) sends every pair to the fp64 rescue (64-lane segments,
     64-row stripes, one pair per wave): read lengths on both sides of each
     multiple of 64 and haplotypes from 1 base up, against the oracle's fp64
     forward sum (log10(sum) - log10(2^1020), GKL's rescue value)."""
@@ -134,7 +134,7 @@ def test_rescue_every_pair(gpu, exact):
     haps = [rng.choice(np.frombuffer(b"ACGT", np.uint8), n) for n in (1, 7, 64, 65, 200, 333)]
     haps.append(np.frombuffer(b"ACGTNACGRT", np.uint8))  # a byte outside A/C/G/T/N: the byte-compare path
     p = fcship.make_pairs(reads, haps)
-    out = fcship.phmm_compute_pairs(p, exact=exact, threshold=1e30)
+    out = fcship.phmm_compute_pairs(p, exact=exact, threshold=1e37)
     ref = np.array([np.log10(oracle_lib.phmm_prob_d(reads[i // len(haps)], haps[i % len(haps)])) -
                     np.log10(2.0 ** 1020) for i in range(p.n_pairs)])
     tol = (1e-12 if exact else 1e-9) * np.abs(ref) + 1e-12
