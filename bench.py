@@ -309,7 +309,9 @@ def bench_e2e(args, rank, local):
         pm = re.search(r"(\d+) reads properly paired, (\d+) mates rescued, insert ([\d.]+) \+- ([\d.]+)", err)
         ph = re.search(r"alignment thread-seconds ([\d.]+): seeding ([\d.]+), extension ([\d.]+), pairing ([\d.]+), "
                        r"records ([\d.]+)", err)
-        if not (m and pm and ph):
+        wp = re.search(r"phases: reference ([\d.e-]+) s, FMD index ([\d.e-]+) s .*FASTQ \+ alignment ([\d.e-]+) s .*"
+                       r"sort \+ BAM \+ index ([\d.e-]+) s", err)
+        if not (m and pm and ph and wp):
             raise RuntimeError("fcs-genome align report not understood: " + err[-2000:])
         n = int(m.group(1))
         out["align"] = {"mode": f"paired-end 2x151, fragments N(350, 50), {args.e2e_align_mbp:g} Mbp genome, 30x "
@@ -318,6 +320,9 @@ def bench_e2e(args, rank, local):
                         "gpu_call_seconds": float(m.group(7)),
                         "thread_seconds": {k: float(ph.group(i + 1)) for i, k in
                                            enumerate(("total", "seeding", "extension", "pairing", "records"))},
+                        "wall_phases_seconds": {k: float(wp.group(i + 1)) for i, k in
+                                                enumerate(("reference", "fmd_index", "fastq_and_alignment",
+                                                           "sort_bam_index"))},
                         "proper_pair_reads": int(pm.group(1)), "mates_rescued": int(pm.group(2)),
                         "seconds": round(dt, 3), "runs_seconds": runs, "reads_per_s": round(n / dt, 1)}
         return out
