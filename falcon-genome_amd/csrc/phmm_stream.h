@@ -141,11 +141,23 @@ __device__ __forceinline__ int srole(int r, int R) { return r == 0 ? 1 : r < R ?
 // One step: phmm2_step without the byte-compare and summing variants; the
 // boundary source is this block's per-lane pointer `rd` (ring or Z) and COND
 // captures the V lanes' X at their column H + 1.
+// Start-lane select as one full-rate v_bitop3_b32 on a per-lane mask VGPR:
+// v_cndmask_b32 on an SGPR lane mask issues at half the rate (4 cycles per
+// wave64 instruction on gfx950 vs 2; tools/micro/valu_rate.hip, gpurun_out/r3m).
+#ifndef FCS_STREAM_SELV
+#define FCS_STREAM_SELV 1
+#endif
+__device__ __forceinline__ float sel_v(uint32_t m, float a, float b) {
+  float r;
+  asm("v_bitop3_b32 %0, %1, %2, %3 bitop3:0xe4" : "=v"(r) : "v"(a), "v"(b), "v"(m));
+  return r;
+}
+
 template <bool COND, bool WRITE, int S, int PF>
 __device__ __forceinline__ void pstream_step(Lane2& L, PhRing<float> (&pf)[PF], int (&hq)[PF],
                                              const unsigned char* __restrict__ hp, const PhRing<float>* __restrict__ rd,
-                                             const RowP2& p, const bool start, const bool top, const int t0,
-                                             const int dl, float& acc, const uint32_t wbase) {
+                                             const RowP2& p, const bool start, const uint32_t smask, const bool top,
+                                             const int t0, const int dl, float& acc, const uint32_t wbase) {
   const int t = t0 + S;
   const PhRing<float> cur = pf[0];
   const int hba = hq[0];
@@ -178,8 +190,15 @@ __device__ __forceinline__ void pstream_step(Lane2& L, PhRing<float> (&pf)[PF], 
 #else
   Xsw.y = __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(L.Xn.y), kDppRowShr1, 0xF, 0xF, true));
   Isw.y = __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(L.In.y), kDppRowShr1, 0xF, 0xF, true));
+#if FCS_STREAM_SELV
+  Xsw.y = sel_v(smask, cur.X, Xsw.y);
+  Isw.y = sel_v(smask, cur.I, Isw.y);
+  (void)start;
+#else
   Xsw.y = start ? cur.X : Xsw.y;
   Isw.y = start ? cur.I : Isw.y;
+  (void)smask;
+#endif
 #endif
   const pf2 I = __builtin_shufflevector(Isw, Isw, 1, 0);
   pf2 prior;
@@ -208,8 +227,10 @@ __device__ __forceinline__ void pstream_step(Lane2& L, PhRing<float> (&pf)[PF], 
   else
     asm volatile("" ::: "memory");  // keep each step's LDS reads in their step (hoisted, they cost registers)
   if constexpr (COND)  // V lanes: take X at the step dl = lim - t0 (a compare-select in place, not
-                       // sixteen compares hoisted into SGPR pairs)
-    asm volatile("v_cmp_eq_u32 vcc, %2, %3\n\tv_cndmask_b32 %0, %0, %1, vcc"
+                       // sixteen compares hoisted into SGPR pairs; the VOP3 form of the select:
+                       // the VOP2 form reading VCC issues at ~1/5 of its rate on gfx950,
+                       // tools/micro/valu_rate.hip)
+    asm volatile("v_cmp_eq_u32 vcc, %2, %3\n\tv_cndmask_b32_e64 %0, %0, %1, vcc"
                  : "+v"(acc)
                  : "v"(Xn.y), "i"(S), "v"(dl)
                  : "vcc");
@@ -224,10 +245,10 @@ template <bool COND, bool WRITE, int PF, int NS = 16>
 __device__ __forceinline__ void pstream_block(Lane2& L, PhRing<float> (&pf)[PF], int (&hq)[PF],
                                               const unsigned char* __restrict__ hp,
                                               const PhRing<float>* __restrict__ rd, const RowP2& p, const bool start,
-                                              const bool top, const int t0, const int dl, float& acc,
-                                              const uint32_t wbase) {
+                                              const uint32_t smask, const bool top, const int t0, const int dl,
+                                              float& acc, const uint32_t wbase) {
   [&]<int... S>(std::integer_sequence<int, S...>) {
-    (pstream_step<COND, WRITE, S, PF>(L, pf, hq, hp, rd, p, start, top, t0, dl, acc, wbase), ...);
+    (pstream_step<COND, WRITE, S, PF>(L, pf, hq, hp, rd, p, start, smask, top, t0, dl, acc, wbase), ...);
   }(std::make_integer_sequence<int, NS>{});
 }
 
@@ -435,6 +456,7 @@ __global__ __launch_bounds__(64, LB) void phmm3_kernel(
 
       // This lane's role in the stripe.
       const bool start = cur.act && (sl == 0 || cur.u == 0);
+      const uint32_t smask = start ? ~0u : 0u;
       const bool is_z = cur.act && cur.u == 0;
       const int zsh = (cur.role_a == 1) ? 1 : 0;  // the pad row reads Z one column on
       const int lim = (cur.role_b == 4) ? cur.H + sl2 + 2 : -1;  // V at its column H + 1
@@ -482,14 +504,14 @@ __global__ __launch_bounds__(64, LB) void phmm3_kernel(
         const int dl = lim - t0;
         if (blk >= 2) {
           if (cond)
-            pstream_block<true, true, PF>(L, pf, hq, hp, rd, prm, start, top, t0, dl, acc, wbase);
+            pstream_block<true, true, PF>(L, pf, hq, hp, rd, prm, start, smask, top, t0, dl, acc, wbase);
           else
-            pstream_block<false, true, PF>(L, pf, hq, hp, rd, prm, start, top, t0, dl, acc, wbase);
+            pstream_block<false, true, PF>(L, pf, hq, hp, rd, prm, start, smask, top, t0, dl, acc, wbase);
         } else {
           if (cond)
-            pstream_block<true, false, PF>(L, pf, hq, hp, rd, prm, start, top, t0, dl, acc, wbase);
+            pstream_block<true, false, PF>(L, pf, hq, hp, rd, prm, start, smask, top, t0, dl, acc, wbase);
           else
-            pstream_block<false, false, PF>(L, pf, hq, hp, rd, prm, start, top, t0, dl, acc, wbase);
+            pstream_block<false, false, PF>(L, pf, hq, hp, rd, prm, start, smask, top, t0, dl, acc, wbase);
         }
       }
       if (half) {
@@ -500,14 +522,14 @@ __global__ __launch_bounds__(64, LB) void phmm3_kernel(
         const int dl = lim - t0;
         if (nblk >= 2) {
           if (cond)
-            pstream_block<true, true, PF, 8>(L, pf, hq, hp, rd, prm, start, top, t0, dl, acc, wbase);
+            pstream_block<true, true, PF, 8>(L, pf, hq, hp, rd, prm, start, smask, top, t0, dl, acc, wbase);
           else
-            pstream_block<false, true, PF, 8>(L, pf, hq, hp, rd, prm, start, top, t0, dl, acc, wbase);
+            pstream_block<false, true, PF, 8>(L, pf, hq, hp, rd, prm, start, smask, top, t0, dl, acc, wbase);
         } else {
           if (cond)
-            pstream_block<true, false, PF, 8>(L, pf, hq, hp, rd, prm, start, top, t0, dl, acc, wbase);
+            pstream_block<true, false, PF, 8>(L, pf, hq, hp, rd, prm, start, smask, top, t0, dl, acc, wbase);
           else
-            pstream_block<false, false, PF, 8>(L, pf, hq, hp, rd, prm, start, top, t0, dl, acc, wbase);
+            pstream_block<false, false, PF, 8>(L, pf, hq, hp, rd, prm, start, smask, top, t0, dl, acc, wbase);
         }
       }
       if (lim >= 0) {

@@ -1,0 +1,283 @@
+// VALU issue-rate microbenchmark for the PairHMM step's instruction mix on
+// gfx950: cycles per wave-instruction per SIMD of one instruction kind, run by
+// `waves` waves per SIMD (independent chains: eight accumulators per lane).
+// Clock from s_memtime / s_memrealtime stamps of block 0 (diagnostic buffer
+// only).  usage: valu_rate [waves_per_simd]
+#include <hip/hip_runtime.h>
+
+#include <cstdio>
+#include <cstdlib>
+
+#define CHECK(x)                                                              \
+  do {                                                                        \
+    hipError_t e = (x);                                                       \
+    if (e != hipSuccess) {                                                    \
+      std::fprintf(stderr, "%s: %s\n", #x, hipGetErrorString(e));           \
+      std::exit(1);                                                           \
+    }                                                                         \
+  } while (0)
+
+constexpr int kIters = 4096;
+
+#define BODY8(INSN) INSN(0) INSN(1) INSN(2) INSN(3) INSN(4) INSN(5) INSN(6) INSN(7)
+
+typedef float f2 __attribute__((ext_vector_type(2)));
+
+template <int K>
+__global__ __launch_bounds__(256) void kern(float* out, unsigned long long* stamps, int iters) {
+  float a[8];
+  float b[8];
+  f2 c[8], d[8];
+  for (int i = 0; i < 8; ++i) {
+    a[i] = threadIdx.x * 0.001f + i, b[i] = 1.0f + i * 1e-3f;
+    c[i] = f2{a[i], b[i]};
+    d[i] = f2{b[i], a[i] * 1e-3f};
+  }
+  const unsigned long long t0 = __builtin_amdgcn_s_memtime(), r0 = __builtin_amdgcn_s_memrealtime();
+  unsigned long long m = 0x5555555555555555ull;
+  if constexpr (K == 31) asm volatile("v_cmp_gt_f32 vcc, %0, %1" : : "v"(a[0]), "v"(b[1]) : "vcc");
+  for (int it = 0; it < iters; ++it) {
+#pragma unroll
+    for (int rep = 0; rep < 2; ++rep) {
+      if constexpr (K == 0) {  // v_fma_f32
+#define I(j) asm volatile("v_fma_f32 %0, %1, %2, %0" : "+v"(a[j]) : "v"(b[j]), "v"(b[(j + 1) & 7]));
+        BODY8(I)
+#undef I
+      } else if constexpr (K == 1) {  // v_pk_fma_f32 (two lanes' worth)
+#define I(j) asm volatile("v_pk_fma_f32 %0, %1, %2, %0" : "+v"(c[j]) : "v"(d[j]), "v"(d[(j + 1) & 7]));
+        BODY8(I)
+#undef I
+      } else if constexpr (K == 2) {  // v_mov_b32_dpp row_shr:1
+#define I(j) asm volatile("v_mov_b32_dpp %0, %1 row_shr:1 row_mask:0xf bank_mask:0xf bound_ctrl:1" : "=v"(a[j]) : "v"(b[j]));
+        BODY8(I)
+#undef I
+      } else if constexpr (K == 3) {  // v_bfe_i32
+#define I(j) asm volatile("v_bfe_i32 %0, %1, %2, 1" : "=v"(a[j]) : "v"(b[j]), "v"(b[(j + 3) & 7]));
+        BODY8(I)
+#undef I
+      } else if constexpr (K == 4) {  // v_bitop3_b32
+#define I(j) asm volatile("v_bitop3_b32 %0, %1, %2, %0 bitop3:0xe4" : "+v"(a[j]) : "v"(b[j]), "v"(b[(j + 1) & 7]));
+        BODY8(I)
+#undef I
+      } else if constexpr (K == 5) {  // v_cndmask_b32_e64 with an SGPR-pair mask
+#define I(j) asm volatile("v_cndmask_b32_e64 %0, %0, %1, %2" : "+v"(a[j]) : "v"(b[j]), "s"(m));
+        BODY8(I)
+#undef I
+      } else if constexpr (K == 6) {  // v_mul_f32
+#define I(j) asm volatile("v_mul_f32 %0, %1, %0" : "+v"(a[j]) : "v"(b[j]));
+        BODY8(I)
+#undef I
+      } else if constexpr (K == 7) {  // v_add_u32
+#define I(j) asm volatile("v_add_u32 %0, %1, %0" : "+v"(a[j]) : "v"(b[j]));
+        BODY8(I)
+#undef I
+      } else if constexpr (K == 8) {  // v_pk_mul_f32
+#define I(j) asm volatile("v_pk_mul_f32 %0, %1, %0" : "+v"(c[j]) : "v"(d[j]));
+        BODY8(I)
+#undef I
+      } else if constexpr (K == 9) {  // v_cndmask_b32_dpp (VOP2 DPP, VCC)
+#define I(j) asm volatile("v_cndmask_b32_dpp %0, %0, %1, vcc row_shr:1 row_mask:0xf bank_mask:0xf bound_ctrl:1" : "+v"(a[j]) : "v"(b[j]) : "vcc");
+        BODY8(I)
+#undef I
+      } else if constexpr (K == 10) {  // v_perm_b32
+#define I(j) asm volatile("v_perm_b32 %0, %1, %2, %0" : "+v"(a[j]) : "v"(b[j]), "v"(b[(j + 1) & 7]));
+        BODY8(I)
+#undef I
+      } else if constexpr (K == 11) {  // v_fmac_f32 (VOP2)
+#define I(j) asm volatile("v_fmac_f32 %0, %1, %2" : "+v"(a[j]) : "v"(b[j]), "v"(b[(j + 1) & 7]));
+        BODY8(I)
+#undef I
+      } else if constexpr (K == 12) {
+#define I(j) asm volatile("v_lshrrev_b32 %0, %1, %0" : "+v"(a[j]) : "v"(b[j]));
+        BODY8(I)
+#undef I
+      } else if constexpr (K == 13) {
+#define I(j) asm volatile("v_ashrrev_i32 %0, %1, %0" : "+v"(a[j]) : "v"(b[j]));
+        BODY8(I)
+#undef I
+      } else if constexpr (K == 14) {
+#define I(j) asm volatile("v_and_b32 %0, %1, %0" : "+v"(a[j]) : "v"(b[j]));
+        BODY8(I)
+#undef I
+      } else if constexpr (K == 15) {  // VOPC compare -> VCC
+#define I(j) asm volatile("v_cmp_eq_u32 vcc, %0, %1" : : "v"(a[j]), "v"(b[j]) : "vcc");
+        BODY8(I)
+#undef I
+      } else if constexpr (K == 16) {  // VOP2 cndmask on VCC
+#define I(j) asm volatile("v_cndmask_b32 %0, %0, %1, vcc" : "+v"(a[j]) : "v"(b[j]));
+        BODY8(I)
+#undef I
+      } else if constexpr (K == 17) {  // VOP2 DPP multiply
+#define I(j) asm volatile("v_mul_f32_dpp %0, %1, %0 row_shr:1 row_mask:0xf bank_mask:0xf bound_ctrl:1" : "+v"(a[j]) : "v"(b[j]));
+        BODY8(I)
+#undef I
+      } else if constexpr (K == 18) {
+#define I(j) asm volatile("v_add_f32_dpp %0, %1, %0 row_shr:1 row_mask:0xf bank_mask:0xf bound_ctrl:1" : "+v"(a[j]) : "v"(b[j]));
+        BODY8(I)
+#undef I
+      } else if constexpr (K == 19) {
+#define I(j) asm volatile("v_mov_b32 %0, %1" : "=v"(a[j]) : "v"(b[j]));
+        BODY8(I)
+#undef I
+      } else if constexpr (K == 20) {
+#define I(j) asm volatile("v_bfe_u32 %0, %1, %2, 1" : "=v"(a[j]) : "v"(b[j]), "v"(b[(j + 3) & 7]));
+        BODY8(I)
+#undef I
+      } else if constexpr (K == 21) {
+#define I(j) asm volatile("v_cndmask_b32_e64 %0, %0, %1, vcc" : "+v"(a[j]) : "v"(b[j]));
+        BODY8(I)
+#undef I
+      } else if constexpr (K == 23) {
+#define I(j) asm volatile("v_bfi_b32 %0, %1, %2, %0" : "+v"(a[j]) : "v"(b[j]), "v"(b[(j + 1) & 7]));
+        BODY8(I)
+#undef I
+      } else if constexpr (K == 24) {
+#define I(j) asm volatile("v_fmac_f32_dpp %0, %1, %2 row_shr:1 row_mask:0xf bank_mask:0xf bound_ctrl:1" : "+v"(a[j]) : "v"(b[j]), "v"(b[(j + 1) & 7]));
+        BODY8(I)
+#undef I
+      } else if constexpr (K == 25) {  // dpp move keeping `old` in lane 0 of each row
+#define I(j) asm volatile("v_mov_b32_dpp %0, %1 row_shr:1 row_mask:0xf bank_mask:0xf" : "+v"(a[j]) : "v"(b[j]));
+        BODY8(I)
+#undef I
+      } else if constexpr (K == 26) {  // VOP2 DPP multiply, wave_shr:1
+#define I(j) asm volatile("v_mul_f32_dpp %0, %1, %0 wave_shr:1 row_mask:0xf bank_mask:0xf bound_ctrl:1" : "+v"(a[j]) : "v"(b[j]));
+        BODY8(I)
+#undef I
+      } else if constexpr (K == 27) {  // v_pk_add_f32
+#define I(j) asm volatile("v_pk_add_f32 %0, %1, %0" : "+v"(c[j]) : "v"(d[j]));
+        BODY8(I)
+#undef I
+      } else if constexpr (K == 28) {  // v_sub_f32
+#define I(j) asm volatile("v_sub_f32 %0, %1, %0" : "+v"(a[j]) : "v"(b[j]));
+        BODY8(I)
+#undef I
+      } else if constexpr (K == 29) {  // v_mul_f32 VOP3 with abs/neg modifiers
+#define I(j) asm volatile("v_mul_f32_e64 %0, |%1|, -%0" : "+v"(a[j]) : "v"(b[j]));
+        BODY8(I)
+#undef I
+      } else if constexpr (K == 30) {  // one VOPC write of VCC, then eight VOP2 cndmask reads
+        asm volatile("v_cmp_gt_f32 vcc, %0, %1" : : "v"(a[0]), "v"(b[1]) : "vcc");
+#define I(j) asm volatile("v_cndmask_b32_e32 %0, %0, %1, vcc" : "+v"(a[j]) : "v"(b[j]));
+        BODY8(I)
+#undef I
+      } else if constexpr (K == 31) {  // VOP2 cndmask, VCC written once before the loop
+#define I(j) asm volatile("v_cndmask_b32_e32 %0, %0, %1, vcc" : "+v"(a[j]) : "v"(b[j]));
+        BODY8(I)
+#undef I
+      } else if constexpr (K == 32) {  // one VOPC write, eight e64 cndmask reads of VCC
+        asm volatile("v_cmp_gt_f32 vcc, %0, %1" : : "v"(a[0]), "v"(b[1]) : "vcc");
+#define I(j) asm volatile("v_cndmask_b32_e64 %0, %0, %1, vcc" : "+v"(a[j]) : "v"(b[j]));
+        BODY8(I)
+#undef I
+      } else if constexpr (K == 33) {
+#define I(j) asm volatile("v_max_i32 %0, %1, %0" : "+v"(a[j]) : "v"(b[j]));
+        BODY8(I)
+#undef I
+      } else if constexpr (K == 34) {
+#define I(j) asm volatile("v_max3_i32 %0, %1, %2, %0" : "+v"(a[j]) : "v"(b[j]), "v"(b[(j + 1) & 7]));
+        BODY8(I)
+#undef I
+      } else if constexpr (K == 35) {
+#define I(j) asm volatile("v_pk_max_i16 %0, %1, %0" : "+v"(a[j]) : "v"(b[j]));
+        BODY8(I)
+#undef I
+      } else if constexpr (K == 36) {
+#define I(j) asm volatile("v_pk_add_u16 %0, %1, %0" : "+v"(a[j]) : "v"(b[j]));
+        BODY8(I)
+#undef I
+      } else if constexpr (K == 37) {  // VOPC to an SGPR pair (e64)
+#define I(j) asm volatile("v_cmp_gt_i32_e64 s[40:41], %0, %1" : : "v"(a[j]), "v"(b[j]) : "s40", "s41");
+        BODY8(I)
+#undef I
+      } else if constexpr (K == 38) {
+#define I(j) asm volatile("v_sub_u32 %0, %1, %0" : "+v"(a[j]) : "v"(b[j]));
+        BODY8(I)
+#undef I
+      } else if constexpr (K == 39) {
+#define I(j) asm volatile("v_max_f32 %0, %1, %0" : "+v"(a[j]) : "v"(b[j]));
+        BODY8(I)
+#undef I
+      } else if constexpr (K == 40) {
+#define I(j) asm volatile("v_pk_sub_u16 %0, %1, %0" : "+v"(a[j]) : "v"(b[j]));
+        BODY8(I)
+#undef I
+      } else if constexpr (K == 41) {
+#define I(j) asm volatile("v_pk_max_u16 %0, %1, %0" : "+v"(a[j]) : "v"(b[j]));
+        BODY8(I)
+#undef I
+      } else if constexpr (K == 42) {  // 16-bit scalar VOP3 max (op_sel capable)
+#define I(j) asm volatile("v_max_i16 %0, %1, %0" : "+v"(a[j]) : "v"(b[j]));
+        BODY8(I)
+#undef I
+      } else if constexpr (K == 43) {
+#define I(j) asm volatile("v_cmp_gt_i32 vcc, %0, %1" : : "v"(a[j]), "v"(b[j]) : "vcc");
+        BODY8(I)
+#undef I
+      } else if constexpr (K == 44) {
+#define I(j) asm volatile("v_med3_i32 %0, %1, %2, %0" : "+v"(a[j]) : "v"(b[j]), "v"(b[(j + 1) & 7]));
+        BODY8(I)
+#undef I
+      }
+    }
+  }
+  const unsigned long long t1 = __builtin_amdgcn_s_memtime(), r1 = __builtin_amdgcn_s_memrealtime();
+  float s = 0;
+  for (int i = 0; i < 8; ++i) s += a[i] + c[i].x + c[i].y;
+  out[blockIdx.x * blockDim.x + threadIdx.x] = s;
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    stamps[0] = t1 - t0;
+    stamps[1] = r1 - r0;
+  }
+}
+
+template <int K>
+static void run(const char* name, int waves, float* out, unsigned long long* st, int ncu) {
+  const int blocks = ncu * 4 * waves / 4;  // 256-thread blocks: 4 waves each
+  auto k = kern<K>;
+  hipLaunchKernelGGL(k, dim3(blocks), dim3(256), 0, 0, out, st, 64);  // warm
+  CHECK(hipDeviceSynchronize());
+  hipEvent_t e0, e1;
+  CHECK(hipEventCreate(&e0));
+  CHECK(hipEventCreate(&e1));
+  CHECK(hipEventRecord(e0));
+  hipLaunchKernelGGL(k, dim3(blocks), dim3(256), 0, 0, out, st, kIters);
+  CHECK(hipEventRecord(e1));
+  CHECK(hipDeviceSynchronize());
+  float ms = 0;
+  CHECK(hipEventElapsedTime(&ms, e0, e1));
+  unsigned long long h[2];
+  CHECK(hipMemcpy(h, st, sizeof h, hipMemcpyDeviceToHost));
+  const double ghz = (double)h[0] / ((double)h[1] / 100e6) / 1e9;
+  const double instr_per_simd = (double)blocks * 4 * kIters * 16 / (ncu * 4);
+  std::printf("%-22s waves/SIMD %d  %.3f ms  clock %.2f GHz  cycles/instr/SIMD %.2f\n", name, waves, ms, ghz,
+              ms * 1e-3 * ghz * 1e9 / instr_per_simd);
+}
+
+int main(int argc, char** argv) {
+  const int waves = argc > 1 ? std::atoi(argv[1]) : 4;
+  hipDeviceProp_t p;
+  CHECK(hipGetDeviceProperties(&p, 0));
+  const int ncu = p.multiProcessorCount;
+  float* out;
+  unsigned long long* st;
+  CHECK(hipMalloc(&out, sizeof(float) * ncu * 4 * waves * 64 * 2));
+  CHECK(hipMalloc(&st, 16));
+  run<0>("v_fma_f32", waves, out, st, ncu);
+  run<16>("v_cndmask_b32 vcc (no write)", waves, out, st, ncu);
+  run<30>("vopc + 8 VOP2 cndmask", waves, out, st, ncu);
+  run<31>("VOP2 cndmask, vcc set once", waves, out, st, ncu);
+  run<32>("vopc + 8 e64 cndmask vcc", waves, out, st, ncu);
+  run<43>("v_cmp_gt_i32 vcc", waves, out, st, ncu);
+  run<37>("v_cmp_gt_i32_e64 sgpr", waves, out, st, ncu);
+  run<33>("v_max_i32", waves, out, st, ncu);
+  run<34>("v_max3_i32", waves, out, st, ncu);
+  run<44>("v_med3_i32", waves, out, st, ncu);
+  run<39>("v_max_f32", waves, out, st, ncu);
+  run<38>("v_sub_u32", waves, out, st, ncu);
+  run<42>("v_max_i16", waves, out, st, ncu);
+  run<35>("v_pk_max_i16", waves, out, st, ncu);
+  run<41>("v_pk_max_u16", waves, out, st, ncu);
+  run<36>("v_pk_add_u16", waves, out, st, ncu);
+  run<40>("v_pk_sub_u16", waves, out, st, ncu);
+  return 0;
+}
