@@ -144,6 +144,12 @@ __device__ __forceinline__ int srole(int r, int R) { return r == 0 ? 1 : r < R ?
 // Start-lane select as one full-rate v_bitop3_b32 on a per-lane mask VGPR:
 // v_cndmask_b32 on an SGPR lane mask issues at half the rate (4 cycles per
 // wave64 instruction on gfx950 vs 2; tools/micro/valu_rate.hip, gpurun_out/r3m).
+#ifndef FCS_DIAG_NOREAD
+#define FCS_DIAG_NOREAD 0
+#endif
+#ifndef FCS_DIAG_NOWRITE
+#define FCS_DIAG_NOWRITE 0
+#endif
 #ifndef FCS_STREAM_SELV
 #define FCS_STREAM_SELV 1
 #endif
@@ -166,8 +172,15 @@ __device__ __forceinline__ void pstream_step(Lane2& L, PhRing<float> (&pf)[PF], 
     pf[k] = pf[k + 1];
     hq[k] = hq[k + 1];
   }
+#if FCS_DIAG_NOREAD  // diagnostic builds only (timing of the VALU part; results are wrong)
+  pf[PF - 1] = PhRing<float>{pf[0].I, pf[0].X};
+  hq[PF - 1] = hq[0] ^ 1;
+  (void)rd;
+  (void)hp;
+#else
   pf[PF - 1] = rd[S];     // boundary input for step t + PF
   hq[PF - 1] = hp[t];     // row a's hap code for column t + PF - 2l
+#endif
   const int hbb = L.hbp;
   L.hbp = hba;
   pf2 Xsw = L.Xn, Isw = L.In;
@@ -208,7 +221,7 @@ __device__ __forceinline__ void pstream_step(Lane2& L, PhRing<float> (&pf)[PF], 
   const pf2 D = __builtin_elementwise_fma(L.Mo, p.my, L.Do * p.yy);
   const pf2 Xn = __builtin_elementwise_fma(M, p.mm, __builtin_elementwise_fma(I, p.gm, D));
   const pf2 In = __builtin_elementwise_fma(M, p.mx, I * p.xx);
-  if constexpr (WRITE) {
+  if constexpr (WRITE && !FCS_DIAG_NOWRITE) {
     // row b of lane 15, column t - 31 -> ring slot t - 31: EXEC narrowed to the
     // four lanes 15 inside the statement, so the step stays one basic block (a
     // branch per step cost six SALU, and values carried across the blocks were
@@ -538,7 +551,7 @@ __global__ __launch_bounds__(64, LB) void phmm3_kernel(
           const unsigned long long k = atomicAdd(fb_count, 1ull);
           fb_list[k] = p;
           out[p] = __builtin_nan("");
-        } else if (use_rescue && acc < thr) {
+        } else if (use_rescue && acc < thr && !(FCS_DIAG_NOREAD || FCS_DIAG_NOWRITE)) {
           const unsigned long long k = atomicAdd(rescue_count, 1ull);
           rescue_list[k] = p;
           out[p] = __builtin_nan("");

@@ -217,6 +217,24 @@ __global__ __launch_bounds__(256) void kern(float* out, unsigned long long* stam
 #define I(j) asm volatile("v_med3_i32 %0, %1, %2, %0" : "+v"(a[j]) : "v"(b[j]), "v"(b[(j + 1) & 7]));
         BODY8(I)
 #undef I
+      } else if constexpr (K == 45) {  // one VOP2 cndmask (VCC) among seven v_fma_f32
+        asm volatile("v_cndmask_b32_e32 %0, %0, %1, vcc" : "+v"(a[0]) : "v"(b[0]));
+#define I(j) asm volatile("v_fma_f32 %0, %1, %2, %0" : "+v"(a[j]) : "v"(b[j]), "v"(b[(j + 1) & 7]));
+        I(1) I(2) I(3) I(4) I(5) I(6) I(7)
+#undef I
+      } else if constexpr (K == 46) {  // one VOP3 cndmask (VCC) among seven v_fma_f32
+        asm volatile("v_cndmask_b32_e64 %0, %0, %1, vcc" : "+v"(a[0]) : "v"(b[0]));
+#define I(j) asm volatile("v_fma_f32 %0, %1, %2, %0" : "+v"(a[j]) : "v"(b[j]), "v"(b[(j + 1) & 7]));
+        I(1) I(2) I(3) I(4) I(5) I(6) I(7)
+#undef I
+      } else if constexpr (K == 47) {  // VOP2 v_addc_co_u32 (VCC carry in and out)
+#define I(j) asm volatile("v_addc_co_u32 %0, vcc, %0, %1, vcc" : "+v"(a[j]) : "v"(b[j]) : "vcc");
+        BODY8(I)
+#undef I
+      } else if constexpr (K == 48) {  // VOP2 cndmask reading an SGPR-pair alias? (e32 with vcc, src0 SGPR)
+#define I(j) asm volatile("v_cndmask_b32_e32 %0, 0, %0, vcc" : "+v"(a[j]));
+        BODY8(I)
+#undef I
       }
     }
   }
@@ -263,21 +281,10 @@ int main(int argc, char** argv) {
   CHECK(hipMalloc(&out, sizeof(float) * ncu * 4 * waves * 64 * 2));
   CHECK(hipMalloc(&st, 16));
   run<0>("v_fma_f32", waves, out, st, ncu);
-  run<16>("v_cndmask_b32 vcc (no write)", waves, out, st, ncu);
-  run<30>("vopc + 8 VOP2 cndmask", waves, out, st, ncu);
+  run<45>("1 VOP2 cndmask + 7 fma", waves, out, st, ncu);
+  run<46>("1 e64 cndmask + 7 fma", waves, out, st, ncu);
   run<31>("VOP2 cndmask, vcc set once", waves, out, st, ncu);
-  run<32>("vopc + 8 e64 cndmask vcc", waves, out, st, ncu);
-  run<43>("v_cmp_gt_i32 vcc", waves, out, st, ncu);
-  run<37>("v_cmp_gt_i32_e64 sgpr", waves, out, st, ncu);
-  run<33>("v_max_i32", waves, out, st, ncu);
-  run<34>("v_max3_i32", waves, out, st, ncu);
-  run<44>("v_med3_i32", waves, out, st, ncu);
-  run<39>("v_max_f32", waves, out, st, ncu);
-  run<38>("v_sub_u32", waves, out, st, ncu);
-  run<42>("v_max_i16", waves, out, st, ncu);
-  run<35>("v_pk_max_i16", waves, out, st, ncu);
-  run<41>("v_pk_max_u16", waves, out, st, ncu);
-  run<36>("v_pk_add_u16", waves, out, st, ncu);
-  run<40>("v_pk_sub_u16", waves, out, st, ncu);
+  run<48>("VOP2 cndmask, src0 inline 0", waves, out, st, ncu);
+  run<47>("v_addc_co_u32 vcc", waves, out, st, ncu);
   return 0;
 }
