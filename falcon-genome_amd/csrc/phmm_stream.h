@@ -74,8 +74,18 @@ __host__ __device__ inline int stream_class(int H) {
 // converted in place) | 64 bytes of read-ahead tail.
 __host__ __device__ constexpr int stream_nslot(int hmax) { return hmax + 18; }
 __host__ __device__ constexpr int stream_hstride(int hmax) { return (hmax + 12) & ~3; }
+// Ring stride in slots: FCS_STREAM_RINGPAD extra slots put the four segments'
+// one-address ring reads on different LDS banks.
+#ifndef FCS_STREAM_RINGPAD
+#define FCS_STREAM_RINGPAD 0
+#endif
+__host__ __device__ constexpr int stream_rstride(int nslot) { return nslot + FCS_STREAM_RINGPAD; }
+#ifndef FCS_STREAM_WRITEALL
+#define FCS_STREAM_WRITEALL 0  // diagnostic: every lane writes (others to a dummy area), no EXEC changes
+#endif
 __host__ __device__ constexpr int stream_lds(int hmax) {
-  return 512 + 4 * 8 * stream_nslot(hmax) + 8 * stream_hstride(hmax) + 64;
+  return 512 + 4 * 8 * stream_rstride(stream_nslot(hmax)) + 8 * stream_hstride(hmax) + 64 +
+         (FCS_STREAM_WRITEALL ? 640 : 0);
 }
 
 // Per-row constants of one half (role: 0 idle, 1 pad, 2 row r < R, 3 row R, 4 V).
@@ -150,6 +160,12 @@ __device__ __forceinline__ int srole(int r, int R) { return r == 0 ? 1 : r < R ?
 #ifndef FCS_DIAG_NOWRITE
 #define FCS_DIAG_NOWRITE 0
 #endif
+#ifndef FCS_DIAG_NORING
+#define FCS_DIAG_NORING 0
+#endif
+#ifndef FCS_DIAG_NOHAP
+#define FCS_DIAG_NOHAP 0
+#endif
 #ifndef FCS_STREAM_SELV
 #define FCS_STREAM_SELV 1
 #endif
@@ -172,13 +188,16 @@ __device__ __forceinline__ void pstream_step(Lane2& L, PhRing<float> (&pf)[PF], 
     pf[k] = pf[k + 1];
     hq[k] = hq[k + 1];
   }
-#if FCS_DIAG_NOREAD  // diagnostic builds only (timing of the VALU part; results are wrong)
+#if FCS_DIAG_NOREAD || FCS_DIAG_NORING  // diagnostic builds only (timing; results are wrong)
   pf[PF - 1] = PhRing<float>{pf[0].I, pf[0].X};
-  hq[PF - 1] = hq[0] ^ 1;
   (void)rd;
-  (void)hp;
 #else
   pf[PF - 1] = rd[S];     // boundary input for step t + PF
+#endif
+#if FCS_DIAG_NOREAD || FCS_DIAG_NOHAP
+  hq[PF - 1] = hq[0] ^ 1;
+  (void)hp;
+#else
   hq[PF - 1] = hp[t];     // row a's hap code for column t + PF - 2l
 #endif
   const int hbb = L.hbp;
@@ -226,6 +245,12 @@ __device__ __forceinline__ void pstream_step(Lane2& L, PhRing<float> (&pf)[PF], 
     // four lanes 15 inside the statement, so the step stays one basic block (a
     // branch per step cost six SALU, and values carried across the blocks were
     // re-zero-extended at each use)
+#if FCS_STREAM_WRITEALL
+    asm volatile("ds_write2_b32 %0, %1, %2 offset0:%3 offset1:%4"
+                 :
+                 : "v"(wbase), "v"(Xn.y), "v"(In.y), "i"(2 * S), "i"(2 * S + 1)
+                 : "memory");
+#else
     uint64_t keep;
     asm volatile(
         "s_mov_b64 %0, exec\n\t"
@@ -235,6 +260,7 @@ __device__ __forceinline__ void pstream_step(Lane2& L, PhRing<float> (&pf)[PF], 
         : "=&s"(keep)
         : "v"(wbase), "v"(Xn.y), "v"(In.y), "s"(kTopLanes), "i"(2 * S), "i"(2 * S + 1)
         : "memory");
+#endif
     (void)top;
   }
   else
@@ -292,8 +318,9 @@ __global__ __launch_bounds__(64, LB) void phmm3_kernel(
   // LDS read-ahead (steps): the 4-wave class has no VGPRs to spare beyond 2
   constexpr int PF = LB >= 4 ? 2 : kStreamPfd;
   PhRing<float>* const Z = reinterpret_cast<PhRing<float>*>(smem_raw);
-  PhRing<float>* const ring = reinterpret_cast<PhRing<float>*>(smem_raw + 512) + seg * nslot;
-  unsigned char* const hbufs = smem_raw + 512 + 32 * nslot + 2 * seg * hstride;  // this segment's two buffers
+  PhRing<float>* const ring = reinterpret_cast<PhRing<float>*>(smem_raw + 512) + seg * stream_rstride(nslot);
+  unsigned char* const hbufs = smem_raw + 512 + 32 * stream_rstride(nslot) + 2 * seg * hstride;  // this segment's two buffers
+  const uint32_t wdummy = lds_addr(smem_raw + 512 + 32 * stream_rstride(nslot) + 8 * hstride + 64 + 8 * lane);
   {
     PhRing<float> z;
     z.X = lane >= 32 ? 1.f : 0.f;
@@ -513,7 +540,7 @@ __global__ __launch_bounds__(64, LB) void phmm3_kernel(
         const int t0 = 16 * blk;
         const PhRing<float>* const rd = is_z ? Z + 32 + min(t0 + PF - sl2 + zsh, 16) : ring + t0 + PF;
         const bool cond = __ballot(lim >= t0 && lim < t0 + 16) != 0ull;
-        const uint32_t wbase = lds_addr(ring + (t0 - 31));
+        const uint32_t wbase = (!FCS_STREAM_WRITEALL || top) ? lds_addr(ring + (t0 - 31)) : wdummy;
         const int dl = lim - t0;
         if (blk >= 2) {
           if (cond)
@@ -531,7 +558,7 @@ __global__ __launch_bounds__(64, LB) void phmm3_kernel(
         const int t0 = 16 * nblk;
         const PhRing<float>* const rd = is_z ? Z + 32 + min(t0 + PF - sl2 + zsh, 16) : ring + t0 + PF;
         const bool cond = __ballot(lim >= t0 && lim < t0 + 8) != 0ull;
-        const uint32_t wbase = lds_addr(ring + (t0 - 31));
+        const uint32_t wbase = (!FCS_STREAM_WRITEALL || top) ? lds_addr(ring + (t0 - 31)) : wdummy;
         const int dl = lim - t0;
         if (nblk >= 2) {
           if (cond)
@@ -551,7 +578,7 @@ __global__ __launch_bounds__(64, LB) void phmm3_kernel(
           const unsigned long long k = atomicAdd(fb_count, 1ull);
           fb_list[k] = p;
           out[p] = __builtin_nan("");
-        } else if (use_rescue && acc < thr && !(FCS_DIAG_NOREAD || FCS_DIAG_NOWRITE)) {
+        } else if (use_rescue && acc < thr && !(FCS_DIAG_NOREAD || FCS_DIAG_NOWRITE || FCS_DIAG_NORING || FCS_DIAG_NOHAP)) {
           const unsigned long long k = atomicAdd(rescue_count, 1ull);
           rescue_list[k] = p;
           out[p] = __builtin_nan("");
