@@ -175,8 +175,14 @@ __device__ __forceinline__ float sel_v(uint32_t m, float a, float b) {
   return r;
 }
 
-template <bool COND, bool WRITE, int S, int PF>
-__device__ __forceinline__ void pstream_step(Lane2& L, PhRing<float> (&pf)[PF], int (&hq)[PF],
+// Hap-code read-ahead in steps (FCS_STREAM_HPF; 0: the ring's PF).
+#ifndef FCS_STREAM_HPF
+#define FCS_STREAM_HPF 0
+#endif
+template <int PF> constexpr int stream_hpf() { return FCS_STREAM_HPF > 0 ? FCS_STREAM_HPF : PF; }
+
+template <bool COND, bool WRITE, int S, int PF, int HPF = stream_hpf<PF>()>
+__device__ __forceinline__ void pstream_step(Lane2& L, PhRing<float> (&pf)[PF], int (&hq)[HPF],
                                              const unsigned char* __restrict__ hp, const PhRing<float>* __restrict__ rd,
                                              const RowP2& p, const bool start, const uint32_t smask, const bool top,
                                              const int t0, const int dl, float& acc, const uint32_t wbase) {
@@ -184,10 +190,9 @@ __device__ __forceinline__ void pstream_step(Lane2& L, PhRing<float> (&pf)[PF], 
   const PhRing<float> cur = pf[0];
   const int hba = hq[0];
 #pragma unroll
-  for (int k = 0; k + 1 < PF; ++k) {
-    pf[k] = pf[k + 1];
-    hq[k] = hq[k + 1];
-  }
+  for (int k = 0; k + 1 < PF; ++k) pf[k] = pf[k + 1];
+#pragma unroll
+  for (int k = 0; k + 1 < HPF; ++k) hq[k] = hq[k + 1];
 #if FCS_DIAG_NOREAD || FCS_DIAG_NORING  // diagnostic builds only (timing; results are wrong)
   pf[PF - 1] = PhRing<float>{pf[0].I, pf[0].X};
   (void)rd;
@@ -195,10 +200,10 @@ __device__ __forceinline__ void pstream_step(Lane2& L, PhRing<float> (&pf)[PF], 
   pf[PF - 1] = rd[S];     // boundary input for step t + PF
 #endif
 #if FCS_DIAG_NOREAD || FCS_DIAG_NOHAP
-  hq[PF - 1] = hq[0] ^ 1;
+  hq[HPF - 1] = hq[0] ^ 1;
   (void)hp;
 #else
-  hq[PF - 1] = hp[t];     // row a's hap code for column t + PF - 2l
+  hq[HPF - 1] = hp[t];    // row a's hap code for column t + HPF - 2l
 #endif
   const int hbb = L.hbp;
   L.hbp = hba;
@@ -281,7 +286,7 @@ __device__ __forceinline__ void pstream_step(Lane2& L, PhRing<float> (&pf)[PF], 
 }
 
 template <bool COND, bool WRITE, int PF, int NS = 16>
-__device__ __forceinline__ void pstream_block(Lane2& L, PhRing<float> (&pf)[PF], int (&hq)[PF],
+__device__ __forceinline__ void pstream_block(Lane2& L, PhRing<float> (&pf)[PF], int (&hq)[stream_hpf<PF>()],
                                               const unsigned char* __restrict__ hp,
                                               const PhRing<float>* __restrict__ rd, const RowP2& p, const bool start,
                                               const uint32_t smask, const bool top, const int t0, const int dl,
@@ -508,7 +513,7 @@ __global__ __launch_bounds__(64, LB) void phmm3_kernel(
       const bool half = (nmax & 15) != 0 && (nmax & 15) <= kStreamHalf;
       const int hoff = 3 + ((cur_pk.w >> 5) & 3);
       const unsigned char* const hp =
-          (cur.act ? hbufs + (cur.k & 1) * hstride + hoff : hbufs) + PF - sl2;  // hp[t]: column t + PF - 2l
+          (cur.act ? hbufs + (cur.k & 1) * hstride + hoff : hbufs) + stream_hpf<PF>() - sl2;  // hp[t]: column t + HPF - 2l
 
       // Next stripe: its lane state, raw rows and new haplotype, all in flight
       // during this stripe.
@@ -529,12 +534,11 @@ __global__ __launch_bounds__(64, LB) void phmm3_kernel(
       L.Xp.y = (is_z && zsh && sl == 0) ? 1.f : 0.f;
       L.hbp = 6;
       PhRing<float> pf[PF];
-      int hq[PF];
+      int hq[stream_hpf<PF>()];
 #pragma unroll
-      for (int q = 0; q < PF; ++q) {
-        pf[q] = is_z ? Z[32 + q - sl2 + zsh] : ring[q];
-        hq[q] = hp[q - PF];
-      }
+      for (int q = 0; q < PF; ++q) pf[q] = is_z ? Z[32 + q - sl2 + zsh] : ring[q];
+#pragma unroll
+      for (int q = 0; q < stream_hpf<PF>(); ++q) hq[q] = hp[q - stream_hpf<PF>()];
       float acc = 0.f;
       for (int blk = 0; blk < nblk; ++blk) {
         const int t0 = 16 * blk;
