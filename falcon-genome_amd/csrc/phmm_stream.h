@@ -181,14 +181,43 @@ __device__ __forceinline__ float sel_v(uint32_t m, float a, float b) {
 #endif
 template <int PF> constexpr int stream_hpf() { return FCS_STREAM_HPF > 0 ? FCS_STREAM_HPF : PF; }
 
+// Hap codes by aligned dword pairs (FCS_STREAM_HAP4): one ds_read2_b32 per
+// four steps brings the eight code bytes around a lane's next four columns
+// (the lane's column sequence is contiguous bytes), and a v_perm_b32 per step
+// picks the step's byte.  A per-step ds_read_u8 at a lane-varying, unaligned
+// address cost ~19% of the kernel (the no-hap-read diagnostic build).
+#ifndef FCS_STREAM_HAP4
+#define FCS_STREAM_HAP4 1
+#endif
+struct HapG {
+  uint32_t lo, hi;    // the current four steps' bytes: byte o + k is step k's code
+  uint32_t nlo, nhi;  // the next four steps', in flight
+  uint32_t sel;       // v_perm selector of step 0's byte: 0x0C0C0C00 | o
+};
+
 template <bool COND, bool WRITE, int S, int PF, int HPF = stream_hpf<PF>()>
-__device__ __forceinline__ void pstream_step(Lane2& L, PhRing<float> (&pf)[PF], int (&hq)[HPF],
+__device__ __forceinline__ void pstream_step(Lane2& L, PhRing<float> (&pf)[PF], int (&hq)[HPF], HapG& hg,
+                                             const uint32_t* __restrict__ hw,
                                              const unsigned char* __restrict__ hp, const PhRing<float>* __restrict__ rd,
                                              const RowP2& p, const bool start, const uint32_t smask, const bool top,
                                              const int t0, const int dl, float& acc, const uint32_t wbase) {
-  const int t = t0 + S;
+  [[maybe_unused]] const int t = t0 + S;
   const PhRing<float> cur = pf[0];
+#if FCS_STREAM_HAP4
+  if constexpr (S % 4 == 0) {
+    hg.lo = hg.nlo;
+    hg.hi = hg.nhi;
+    hg.nlo = hw[S / 4 + 1];
+    hg.nhi = hw[S / 4 + 2];
+  }
+  const int hba = (int)__builtin_amdgcn_perm(hg.hi, hg.lo, hg.sel + (uint32_t)(S % 4));
+  (void)hq;
+  (void)hp;
+#else
   const int hba = hq[0];
+  (void)hg;
+  (void)hw;
+#endif
 #pragma unroll
   for (int k = 0; k + 1 < PF; ++k) pf[k] = pf[k + 1];
 #pragma unroll
@@ -201,8 +230,7 @@ __device__ __forceinline__ void pstream_step(Lane2& L, PhRing<float> (&pf)[PF], 
 #endif
 #if FCS_DIAG_NOREAD || FCS_DIAG_NOHAP
   hq[HPF - 1] = hq[0] ^ 1;
-  (void)hp;
-#else
+#elif !FCS_STREAM_HAP4
   hq[HPF - 1] = hp[t];    // row a's hap code for column t + HPF - 2l
 #endif
   const int hbb = L.hbp;
@@ -287,12 +315,13 @@ __device__ __forceinline__ void pstream_step(Lane2& L, PhRing<float> (&pf)[PF], 
 
 template <bool COND, bool WRITE, int PF, int NS = 16>
 __device__ __forceinline__ void pstream_block(Lane2& L, PhRing<float> (&pf)[PF], int (&hq)[stream_hpf<PF>()],
+                                              HapG& hg, const uint32_t* __restrict__ hw,
                                               const unsigned char* __restrict__ hp,
                                               const PhRing<float>* __restrict__ rd, const RowP2& p, const bool start,
                                               const uint32_t smask, const bool top, const int t0, const int dl,
                                               float& acc, const uint32_t wbase) {
   [&]<int... S>(std::integer_sequence<int, S...>) {
-    (pstream_step<COND, WRITE, S, PF>(L, pf, hq, hp, rd, p, start, smask, top, t0, dl, acc, wbase), ...);
+    (pstream_step<COND, WRITE, S, PF>(L, pf, hq, hg, hw, hp, rd, p, start, smask, top, t0, dl, acc, wbase), ...);
   }(std::make_integer_sequence<int, NS>{});
 }
 
@@ -538,7 +567,19 @@ __global__ __launch_bounds__(64, LB) void phmm3_kernel(
 #pragma unroll
       for (int q = 0; q < PF; ++q) pf[q] = is_z ? Z[32 + q - sl2 + zsh] : ring[q];
 #pragma unroll
-      for (int q = 0; q < stream_hpf<PF>(); ++q) hq[q] = hp[q - stream_hpf<PF>()];
+      for (int q = 0; q < stream_hpf<PF>(); ++q) hq[q] = FCS_STREAM_HAP4 ? 0 : hp[q - stream_hpf<PF>()];
+      // HAP4: the lane's code bytes for steps t sit at A + t (A = hp - HPF);
+      // hw = the dword-aligned base, o = A & 3
+      HapG hg;
+      const uint32_t* hw;
+      {
+        const uint32_t A = lds_addr(hp) - (uint32_t)stream_hpf<PF>();
+        hw = reinterpret_cast<const uint32_t*>(hp - stream_hpf<PF>() - (A & 3u));
+        hg.sel = 0x0C0C0C00u | (A & 3u);
+        hg.nlo = FCS_STREAM_HAP4 ? hw[0] : 0u;
+        hg.nhi = FCS_STREAM_HAP4 ? hw[1] : 0u;
+        hg.lo = hg.hi = 0u;
+      }
       float acc = 0.f;
       for (int blk = 0; blk < nblk; ++blk) {
         const int t0 = 16 * blk;
@@ -548,14 +589,14 @@ __global__ __launch_bounds__(64, LB) void phmm3_kernel(
         const int dl = lim - t0;
         if (blk >= 2) {
           if (cond)
-            pstream_block<true, true, PF>(L, pf, hq, hp, rd, prm, start, smask, top, t0, dl, acc, wbase);
+            pstream_block<true, true, PF>(L, pf, hq, hg, hw + t0 / 4, hp, rd, prm, start, smask, top, t0, dl, acc, wbase);
           else
-            pstream_block<false, true, PF>(L, pf, hq, hp, rd, prm, start, smask, top, t0, dl, acc, wbase);
+            pstream_block<false, true, PF>(L, pf, hq, hg, hw + t0 / 4, hp, rd, prm, start, smask, top, t0, dl, acc, wbase);
         } else {
           if (cond)
-            pstream_block<true, false, PF>(L, pf, hq, hp, rd, prm, start, smask, top, t0, dl, acc, wbase);
+            pstream_block<true, false, PF>(L, pf, hq, hg, hw + t0 / 4, hp, rd, prm, start, smask, top, t0, dl, acc, wbase);
           else
-            pstream_block<false, false, PF>(L, pf, hq, hp, rd, prm, start, smask, top, t0, dl, acc, wbase);
+            pstream_block<false, false, PF>(L, pf, hq, hg, hw + t0 / 4, hp, rd, prm, start, smask, top, t0, dl, acc, wbase);
         }
       }
       if (half) {
@@ -566,14 +607,14 @@ __global__ __launch_bounds__(64, LB) void phmm3_kernel(
         const int dl = lim - t0;
         if (nblk >= 2) {
           if (cond)
-            pstream_block<true, true, PF, 8>(L, pf, hq, hp, rd, prm, start, smask, top, t0, dl, acc, wbase);
+            pstream_block<true, true, PF, 8>(L, pf, hq, hg, hw + t0 / 4, hp, rd, prm, start, smask, top, t0, dl, acc, wbase);
           else
-            pstream_block<false, true, PF, 8>(L, pf, hq, hp, rd, prm, start, smask, top, t0, dl, acc, wbase);
+            pstream_block<false, true, PF, 8>(L, pf, hq, hg, hw + t0 / 4, hp, rd, prm, start, smask, top, t0, dl, acc, wbase);
         } else {
           if (cond)
-            pstream_block<true, false, PF, 8>(L, pf, hq, hp, rd, prm, start, smask, top, t0, dl, acc, wbase);
+            pstream_block<true, false, PF, 8>(L, pf, hq, hg, hw + t0 / 4, hp, rd, prm, start, smask, top, t0, dl, acc, wbase);
           else
-            pstream_block<false, false, PF, 8>(L, pf, hq, hp, rd, prm, start, smask, top, t0, dl, acc, wbase);
+            pstream_block<false, false, PF, 8>(L, pf, hq, hg, hw + t0 / 4, hp, rd, prm, start, smask, top, t0, dl, acc, wbase);
         }
       }
       if (lim >= 0) {
