@@ -187,7 +187,7 @@ template <int PF> constexpr int stream_hpf() { return FCS_STREAM_HPF > 0 ? FCS_S
 // picks the step's byte.  A per-step ds_read_u8 at a lane-varying, unaligned
 // address cost ~19% of the kernel (the no-hap-read diagnostic build).
 #ifndef FCS_STREAM_HAP4
-#define FCS_STREAM_HAP4 1
+#define FCS_STREAM_HAP4 0  // measured neutral (gpurun_out/r3s) and +9 spilled VGPRs in the 4-wave class
 #endif
 struct HapG {
   uint32_t lo, hi;    // the current four steps' bytes: byte o + k is step k's code

@@ -19,6 +19,11 @@ for pass in 1 2; do
     echo "$f: $(FCSHIP_LIB=$PWD/$f timeout -k 10 300 $BENCH 2>/dev/null | tail -1)" | tee -a "$O/ab.log" || exit 1
   done
 done
+timeout -k 10 600 python -u -m pytest $TESTS -q -x -p no:cacheprovider --timeout 120 --timeout-method thread \
+  > "$O/pytest_in_tree.log" 2>&1
+rc=$?
+echo "in-tree parity rc=$rc: $(tail -1 "$O/pytest_in_tree.log")" | tee -a "$O/ab.log"
+[ $rc -le 1 ] || exit $rc
 for f in alt/*.so; do
   [ -e "$f" ] || continue
   FCSHIP_LIB=$PWD/$f timeout -k 10 600 python -u -m pytest $TESTS -q -x -p no:cacheprovider --timeout 120 \
