@@ -7,7 +7,14 @@ W=$(mktemp -d /tmp/ovl.XXXX)
 export FCS_GPU_DEVICES=0 FCS_LOG_DIR=$W/log FCS_TEMP_DIR=$W FCS_GATK_NPROCS=4 TMPDIR=/tmp
 B=$GRAFT_REPO_ROOT/falcon-genome_amd/bin/fcs-genome
 timeout -k 10 300 $B synth -o $W/d -c chr1:4000000 -x 30 > /dev/null || exit 1
+# the profiled process must exit by itself (it once hung at exit);
+# the wall time of the whole rocprofv3 command is recorded next to the trace
+t0=$(date +%s.%N)
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/prof -o run --output-format csv -- \
-  $B htc -r $W/d/ref.fasta -i $W/d/sample.bam -o $W/h.g.vcf > $O/htc.log 2>&1 || { tail $O/htc.log; exit 1; }
+  $B htc -r $W/d/ref.fasta -i $W/d/sample.bam -o $W/h.g.vcf > $O/htc.log 2>&1
+rc=$?
+t1=$(date +%s.%N)
+echo "rocprofv3 + htc rc=$rc wall $(python3 -c "print(round($t1 - $t0, 1))") s" | tee $O/exit.log
+[ $rc -eq 0 ] || { tail $O/htc.log; exit 1; }
 python3 $GRAFT_REPO_ROOT/tools/htc_overlap.py $O/prof/run_kernel_trace.csv | tee $O/overlap.json
 rm -rf $W
