@@ -228,7 +228,11 @@ __device__ __forceinline__ void pstream_step(Lane2& L, PhRing<float> (&pf)[PF], 
 #else
   pf[PF - 1] = rd[S];     // boundary input for step t + PF
 #endif
-#if FCS_DIAG_NOREAD || FCS_DIAG_NOHAP
+#if FCS_DIAG_NOHAP == 2  // constant code N: every cell matches
+  hq[HPF - 1] = 4;
+#elif FCS_DIAG_NOHAP == 3  // constant padding code: every cell mismatches
+  hq[HPF - 1] = 6;
+#elif FCS_DIAG_NOREAD || FCS_DIAG_NOHAP
   hq[HPF - 1] = hq[0] ^ 1;
 #elif !FCS_STREAM_HAP4
   hq[HPF - 1] = hp[t];    // row a's hap code for column t + HPF - 2l
