@@ -599,7 +599,7 @@ def main():
                      "kernel": "phmm3_kernel (row-streamed segments, two read rows per lane, packed FP32): fp32 forward pass = one launch "
                                "per launch class, overlapped on 4 streams; achieved = algorithmic FLOPs / pass "
                                "time (HIP events on the launch stream; rocprof pass span in "
-                               "profiles/r2/r2d_phmm_summary.json)",
+                               "profiles/r3/r3x_phmm_summary.json)",
                      "valu_instr_per_cell": vipc,
                      "valu_issue_frac": (round(ph["cells"] / fwd_s * vipc / VALU_LANE_INSTR_PEAK, 4) if vipc
                                          else None),
