@@ -235,6 +235,46 @@ __global__ __launch_bounds__(256) void kern(float* out, unsigned long long* stam
 #define I(j) asm volatile("v_cndmask_b32_e32 %0, 0, %0, vcc" : "+v"(a[j]));
         BODY8(I)
 #undef I
+      } else if constexpr (K == 50) {
+#define I(j) asm volatile("v_add_u16 %0, %1, %0" : "+v"(a[j]) : "v"(b[j]));
+        BODY8(I)
+#undef I
+      } else if constexpr (K == 51) {
+#define I(j) asm volatile("v_sub_i16 %0, %1, %0 clamp" : "+v"(a[j]) : "v"(b[j]));
+        BODY8(I)
+#undef I
+      } else if constexpr (K == 52) {
+#define I(j) asm volatile("v_max3_i16 %0, %1, %2, %0" : "+v"(a[j]) : "v"(b[j]), "v"(b[(j + 1) & 7]));
+        BODY8(I)
+#undef I
+      } else if constexpr (K == 53) {
+#define I(j) asm volatile("v_add_u32_sdwa %0, %1, %0 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:BYTE_1 src1_sel:DWORD" : "+v"(a[j]) : "v"(b[j]));
+        BODY8(I)
+#undef I
+      } else if constexpr (K == 54) {
+#define I(j) asm volatile("v_max_i32_sdwa %0, sext(%1), %0 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:WORD_0 src1_sel:DWORD" : "+v"(a[j]) : "v"(b[j]));
+        BODY8(I)
+#undef I
+      } else if constexpr (K == 55) {
+#define I(j) asm volatile("v_add3_u32 %0, %1, %2, %0" : "+v"(a[j]) : "v"(b[j]), "v"(b[(j + 1) & 7]));
+        BODY8(I)
+#undef I
+      } else if constexpr (K == 56) {
+#define I(j) asm volatile("v_max_i16_e64 %0, %1, %0" : "+v"(a[j]) : "v"(b[j]));
+        BODY8(I)
+#undef I
+      } else if constexpr (K == 57) {
+#define I(j) asm volatile("v_min_i32 %0, %1, %0" : "+v"(a[j]) : "v"(b[j]));
+        BODY8(I)
+#undef I
+      } else if constexpr (K == 58) {
+#define I(j) asm volatile("v_sub_u16 %0, %1, %0" : "+v"(a[j]) : "v"(b[j]));
+        BODY8(I)
+#undef I
+      } else if constexpr (K == 59) {
+#define I(j) asm volatile("v_max_u32 %0, %1, %0" : "+v"(a[j]) : "v"(b[j]));
+        BODY8(I)
+#undef I
       }
     }
   }
@@ -281,10 +321,17 @@ int main(int argc, char** argv) {
   CHECK(hipMalloc(&out, sizeof(float) * ncu * 4 * waves * 64 * 2));
   CHECK(hipMalloc(&st, 16));
   run<0>("v_fma_f32", waves, out, st, ncu);
-  run<45>("1 VOP2 cndmask + 7 fma", waves, out, st, ncu);
-  run<46>("1 e64 cndmask + 7 fma", waves, out, st, ncu);
-  run<31>("VOP2 cndmask, vcc set once", waves, out, st, ncu);
-  run<48>("VOP2 cndmask, src0 inline 0", waves, out, st, ncu);
-  run<47>("v_addc_co_u32 vcc", waves, out, st, ncu);
+  run<42>("v_max_i16", waves, out, st, ncu);
+  run<50>("v_add_u16", waves, out, st, ncu);
+  run<58>("v_sub_u16", waves, out, st, ncu);
+  run<51>("v_sub_i16 clamp", waves, out, st, ncu);
+  run<52>("v_max3_i16", waves, out, st, ncu);
+  run<56>("v_max_i16 e64", waves, out, st, ncu);
+  run<53>("v_add_u32_sdwa byte", waves, out, st, ncu);
+  run<54>("v_max_i32_sdwa sext word", waves, out, st, ncu);
+  run<55>("v_add3_u32", waves, out, st, ncu);
+  run<57>("v_min_i32", waves, out, st, ncu);
+  run<59>("v_max_u32", waves, out, st, ncu);
+  run<33>("v_max_i32", waves, out, st, ncu);
   return 0;
 }
