@@ -1058,7 +1058,11 @@ static BswDevBatch bsw_dev(const fcs_bsw_batch* b) {
 
 static int check_bsw_batch(const fcs_bsw_batch* b) {
   if (!b || b->n < 0) return fail(FCS_ERR_INVALID, "[E::fcship] bad SW batch");
-  if (b->n > 0 && (!b->qbuf || !b->qoff || !b->qlen || !b->tbuf || !b->toff || !b->tlen || !b->h0 || !b->w))
+  // byte buffers may be null when empty: a batch whose every target (or query)
+  // is empty, e.g. left extensions of seeds that start at their window's edge
+  // (bwa calls ksw_extend2 with tlen 0 there)
+  if (b->n > 0 && ((!b->qbuf && b->qbytes > 0) || !b->qoff || !b->qlen || (!b->tbuf && b->tbytes > 0) || !b->toff ||
+                   !b->tlen || !b->h0 || !b->w))
     return fail(FCS_ERR_INVALID, "[E::fcship] null pointer in SW batch");
   return FCS_OK;
 }

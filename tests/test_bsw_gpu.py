@@ -77,6 +77,21 @@ def test_extend_random(gpu):
     assert_extend_equal(random_tasks(1, 600))
 
 
+def test_extend_all_targets_empty(gpu):
+    """A round whose every task has an empty target (left extensions of seeds
+    at their window's edge: bwa calls ksw_extend2 with tlen 0 there) packs no
+    target bytes; the host-pointer entry point must still run it (ksw_extend2
+    returns h0, qle = tle = gtle = 0, gscore = -1)."""
+    rng = np.random.default_rng(5)
+    items = [(rng.integers(0, 4, int(rng.integers(1, 30))).astype(np.uint8), np.zeros(0, np.uint8),
+              int(rng.integers(1, 60)), int(rng.integers(0, 40))) for _ in range(50)]
+    t = fcship.make_tasks(items)
+    res = fcship.bsw_extend_tasks(t)
+    ref, _ = oracle_lib.ksw_extend2_batch(t, fcship.default_mat())
+    assert (res == ref).all(), (res[:3], ref[:3])
+    assert (res[:, 0] == t.h0).all() and (res[:, 1:4] == 0).all()
+
+
 def test_extend_zdrop_and_penalties(gpu):
     t = random_tasks(2, 300, qmax=180)
     assert_extend_equal(t, dict(o_del=5, e_del=2, o_ins=4, e_ins=3, end_bonus=0, zdrop=20))
