@@ -36,6 +36,7 @@ void Config::init(const std::string& root_dir) {
   declare("bwa.nt", "-1", "host threads of the aligner (-1: all)");
   declare("bwa.num_buckets", "1024", "number of BAM buckets");
   declare("bwa.chunk_size", "100000", "reads per SW batch handed to the GPU");
+  declare("bwa.gpu_slots", "4", "aligner host threads (chunks in flight) per GPU");
   declare("gatk.intv.path", "", "default path to existing contig intervals");
   declare("gatk.ncontigs", "32", "contig partition num in htc/mutect2");
   declare("gatk.nprocs", std::to_string(std::min(32u, ncpu)), "default concurrent shard tasks");

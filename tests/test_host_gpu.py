@@ -218,7 +218,7 @@ def test_align_sample_sheet_over_two_slots(gpu, tmp_path):
     outs = {}
     for devs in ("0", "0,0"):
         o = tmp_path / f"out_{devs.replace(',', '_')}"
-        env = dict(ENV, FCS_GPU_DEVICES=devs, FCS_BWA_CHUNK_SIZE="4000")
+        env = dict(ENV, FCS_GPU_DEVICES=devs, FCS_BWA_CHUNK_SIZE="4000", FCS_BWA_GPU_SLOTS="1")
         p = H.run_cli("align", "-r", d / "ref.fasta", "-F", sheet, "-o", o, env=env, cwd=tmp_path)
         assert p.returncode == 0, p.stderr[-3000:]
         assert ("on 2 device slot(s)" in p.stderr) == (devs == "0,0"), p.stderr[-2000:]
