@@ -4,9 +4,11 @@
 #include <zlib.h>
 
 #include <algorithm>
+#include <condition_variable>
 #include <cstdlib>
 #include <cstring>
 #include <memory>
+#include <mutex>
 #include <thread>
 
 #include "common.h"
@@ -149,13 +151,71 @@ std::vector<uint8_t> make_block(const uint8_t* data, size_t n, int level) {
 
 }  // namespace
 
+// ------------------------------------------------------------------ pool
+namespace {
+
+class HostPool {
+ public:
+  HostPool() {
+    // a GPU box's CPU share is 16 threads whatever hardware_concurrency says
+    n_ = std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
+    for (unsigned k = 0; k < n_; ++k) threads_.emplace_back([this] { loop(); });
+  }
+  ~HostPool() {
+    {
+      std::lock_guard<std::mutex> g(mu_);
+      stop_ = true;
+    }
+    cv_.notify_all();
+    for (std::thread& t : threads_) t.join();
+  }
+  void run(std::function<void()> job) {
+    {
+      std::lock_guard<std::mutex> g(mu_);
+      jobs_.push_back(std::move(job));
+    }
+    cv_.notify_one();
+  }
+  unsigned size() const { return n_; }
+
+ private:
+  void loop() {
+    for (;;) {
+      std::function<void()> job;
+      {
+        std::unique_lock<std::mutex> g(mu_);
+        cv_.wait(g, [this] { return stop_ || !jobs_.empty(); });
+        if (jobs_.empty()) return;  // stop_ with nothing left
+        job = std::move(jobs_.front());
+        jobs_.pop_front();
+      }
+      job();  // packaged tasks keep their exceptions for the waiter
+    }
+  }
+  unsigned n_ = 1;
+  std::mutex mu_;
+  std::condition_variable cv_;
+  std::deque<std::function<void()>> jobs_;
+  std::vector<std::thread> threads_;
+  bool stop_ = false;
+};
+
+HostPool& host_pool() {
+  static HostPool p;
+  return p;
+}
+
+}  // namespace
+
+void host_pool_run(std::function<void()> job) { host_pool().run(std::move(job)); }
+unsigned host_pool_size() { return host_pool().size(); }
+
 // ------------------------------------------------------------------ writer
 BgzfWriter::BgzfWriter(const std::string& path, int level) : level_(level) {
   f_ = std::fopen(path.c_str(), "wb");
   if (!f_) throw fileNotFound(path + " (cannot open for writing)");
   buf_.reserve(kBgzfMaxBlock);
-  const unsigned hc = std::max(1u, std::thread::hardware_concurrency());
-  max_pending_ = 2 * (size_t)std::min(8u, hc);
+  max_pending_ = 4 * (size_t)host_pool_size();
 }
 
 BgzfWriter::~BgzfWriter() {
@@ -169,9 +229,7 @@ void BgzfWriter::emit_block(const uint8_t* data, size_t n) {
   ustarts_.push_back(ubytes_ - n);
   std::vector<uint8_t> in(data, data + n);
   const int level = level_;
-  pending_.push_back(std::async(std::launch::async, [in = std::move(in), level] {
-    return make_block(in.data(), in.size(), level);
-  }));
+  pending_.push_back(host_pool_async([in = std::move(in), level] { return make_block(in.data(), in.size(), level); }));
   drain(max_pending_);
 }
 
@@ -199,13 +257,17 @@ void BgzfWriter::write(const void* data, size_t n) {
 
 void BgzfWriter::flush() {
   if (buf_.empty()) return;
+  if (buf_.size() != kBgzfBlockData) uniform_ = false;  // a short block before more data
   emit_block(buf_.data(), buf_.size());
   buf_.clear();
 }
 
 void BgzfWriter::close() {
   if (closed_ || !f_) return;
-  flush();
+  if (!buf_.empty()) {  // the last block may be short without breaking uniform_
+    emit_block(buf_.data(), buf_.size());
+    buf_.clear();
+  }
   drain(0);
   std::fwrite(kBgzfEof, 1, sizeof kBgzfEof, f_);
   std::fclose(f_);
@@ -216,7 +278,11 @@ void BgzfWriter::close() {
 uint64_t BgzfWriter::voffset(uint64_t u) const {
   if (!closed_ || coffs_.size() != ustarts_.size()) throw internalError("[E::bgzf] voffset before close");
   if (ustarts_.empty()) return 0;
-  size_t k = (size_t)(std::upper_bound(ustarts_.begin(), ustarts_.end(), u) - ustarts_.begin()) - 1;
+  size_t k;
+  if (uniform_)
+    k = std::min<size_t>((size_t)(u / kBgzfBlockData), ustarts_.size() - 1);  // block k starts at k kBgzfBlockData
+  else
+    k = (size_t)(std::upper_bound(ustarts_.begin(), ustarts_.end(), u) - ustarts_.begin()) - 1;
   if (k > 0 && u == ustarts_[k]) --k;  // a block boundary reached by reading: the end of the earlier block
   return (coffs_[k] << 16) | (u - ustarts_[k]);
 }

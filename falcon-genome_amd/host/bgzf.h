@@ -11,11 +11,27 @@
 #include <cstdint>
 #include <cstdio>
 #include <deque>
+#include <functional>
 #include <future>
+#include <memory>
 #include <string>
 #include <vector>
 
 namespace fcsg {
+
+// Process-wide host worker threads (htslib's thread-pool role): BGZF blocks
+// compress here and the one-pass VCF indexer parses its chunks here.  Jobs
+// must not wait on other pool jobs.  Workers keep their (thread-local)
+// deflate state between blocks.
+void host_pool_run(std::function<void()> job);
+unsigned host_pool_size();
+template <class F>
+auto host_pool_async(F f) -> std::future<decltype(f())> {
+  auto t = std::make_shared<std::packaged_task<decltype(f())()>>(std::move(f));
+  auto fut = t->get_future();
+  host_pool_run([t] { (*t)(); });
+  return fut;
+}
 
 constexpr size_t kBgzfMaxBlock = 0x10000;   // max uncompressed bytes per block
 constexpr size_t kBgzfBlockData = 0xff00;   // what the writer packs per block (as htslib)
@@ -61,8 +77,9 @@ class BgzfWriter {
   std::vector<uint64_t> ustarts_;  // uncompressed start of every block, in order
   uint64_t ubytes_ = 0;
   bool closed_ = false;
-  // blocks compress on worker threads (htslib's thread pool role) and are
-  // written in order; tell() first writes every pending block
+  bool uniform_ = true;  // every block but the last holds kBgzfBlockData bytes (voffset by division)
+  // blocks compress on the host pool and are written in order; tell() first
+  // writes every pending block
   std::deque<std::future<std::vector<uint8_t>>> pending_;
   size_t max_pending_ = 0;
 };

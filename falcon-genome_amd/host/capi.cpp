@@ -320,6 +320,10 @@ int fcsg_vcf_concat(const char* const* inputs, int n, const char* output) {
   return guard([&] { vcf_concat(std::vector<std::string>(inputs, inputs + n), output); });
 }
 
+int fcsg_vcf_concat_bgzip_tabix(const char* const* inputs, int n, const char* plain, const char* gz) {
+  return guard([&] { vcf_concat_bgzip_tabix(std::vector<std::string>(inputs, inputs + n), plain, gz); });
+}
+
 int fcsg_bgzip_tabix(const char* in, const char* out) {
   return guard([&] { bgzip_tabix_file(in, out); });
 }

@@ -9,6 +9,8 @@
 #include <cerrno>
 
 #include <csignal>
+#include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <iostream>
 #include <thread>
@@ -149,6 +151,35 @@ std::vector<std::vector<std::string>> dir_shards(const std::string& intv_list) {
   return out;
 }
 
+// FCS_TIMELINE=1: seconds since the process started at named points
+// (where a command's wall time goes outside its stages)
+void timeline(const char* what) {
+  static const bool on = [] {
+    const char* e = std::getenv("FCS_TIMELINE");
+    return e && *e && *e != '0';
+  }();
+  if (!on) return;
+  double up = 0, start = 0;
+  if (std::FILE* f = std::fopen("/proc/uptime", "r")) {
+    if (std::fscanf(f, "%lf", &up) != 1) up = 0;
+    std::fclose(f);
+  }
+  if (std::FILE* f = std::fopen("/proc/self/stat", "r")) {
+    char buf[1024];
+    const size_t n = std::fread(buf, 1, sizeof buf - 1, f);
+    std::fclose(f);
+    buf[n] = 0;
+    const char* p = std::strrchr(buf, ')');  // fields after the command name; starttime is field 22
+    unsigned long long ticks = 0;
+    for (int field = 3; p && *p && field <= 22; ++field) {
+      p = std::strchr(p + 1, ' ');
+      if (p && field == 21) ticks = std::strtoull(p + 1, nullptr, 10);
+    }
+    start = (double)ticks / (double)sysconf(_SC_CLK_TCK);
+  }
+  std::cerr << "[fcs-genome timeline] " << what << " " << (up - start) << " s" << std::endl;
+}
+
 int htc_main(int argc, char** argv) {
   Args a;
   common_opts(a);
@@ -176,7 +207,9 @@ int htc_main(int argc, char** argv) {
   const std::string out_dir = conf().temp_dir() + "/htc";
   create_dir(out_dir);
   const bool flag_vcf = a.has("produce-vcf");
+  timeline("options parsed");
   const auto shards = is_directory(input) ? dir_shards(a.get("intervalList")) : shard_intervals(ref, a.get("intervalList"));
+  timeline("shards");
   // the GPU runtime and tables come up in the background while the first
   // shards decode and pile up their reads (the reference's BackgroundExecutor
   // NAM daemon runs beside its Executor the same way)
@@ -189,13 +222,18 @@ int htc_main(int argc, char** argv) {
     ex.addTask(std::make_shared<HTCWorker>(ref, shards[k], input, part, extra, (int)k, flag_vcf, true), sample_id);
   }
   const std::string plain = output;
-  ex.addTask(std::make_shared<VCFConcatWorker>(parts, plain), sample_id, true);
   if (!a.has("skip-concat")) {
     if (!force && path_exists(plain + ".gz")) throw invalidParam("output " + plain + ".gz exists (use -f)");
-    ex.addTask(std::make_shared<ZIPWorker>(plain, plain + ".gz", force, true), sample_id, true);
+    // concat -> bgzip -> tabix as one pass over the parts
+    ex.addTask(std::make_shared<VCFConcatWorker>(parts, plain, plain + ".gz"), sample_id, true);
+  } else {
+    ex.addTask(std::make_shared<VCFConcatWorker>(parts, plain), sample_id, true);
   }
+  timeline("stages queued");
   ex.run();
+  timeline("stages done");
   warm.wait();
+  timeline("warm-up joined");
   if (warm.status() != 0) throw failedCommand(std::string("[E::fcs-genome] GPU warm-up failed: ") + fcs_last_error());
   return 0;
 }
@@ -241,8 +279,7 @@ int mutect2_main(int argc, char** argv) {
                                                true),
                sample_id);
   }
-  ex.addTask(std::make_shared<VCFConcatWorker>(parts, output), sample_id, true);
-  ex.addTask(std::make_shared<ZIPWorker>(output, output + ".gz", true, true), sample_id, true);
+  ex.addTask(std::make_shared<VCFConcatWorker>(parts, output, output + ".gz"), sample_id, true);
   ex.run();
   warm.wait();
   if (warm.status() != 0) throw failedCommand(std::string("[E::fcs-genome] GPU warm-up failed: ") + fcs_last_error());
@@ -495,6 +532,7 @@ int main(int argc, char** argv) {
     const size_t k = self.find_last_of('/');
     root = k == std::string::npos ? "." : self.substr(0, k) + "/..";
   }
+  timeline("main");
   start_signal_thread();
   try {
     conf().init(root);
@@ -513,6 +551,7 @@ int main(int argc, char** argv) {
       ret = 1;
     }
     remove_path(conf().temp_dir());
+    timeline("temp removed");
   } catch (helpRequest&) {
     ret = 0;
   } catch (invalidParam& e) {

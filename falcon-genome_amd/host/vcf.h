@@ -55,5 +55,8 @@ void tabix_index_vcf(const std::string& vcf_gz);
 // bgzip_file + tabix_index_vcf in one pass over the plain VCF (the index from
 // the plain lines and the writer's block offsets; same files as the two calls).
 void bgzip_tabix_file(const std::string& input, const std::string& output);
+// vcf_concat(inputs, plain) + bgzip_tabix_file(plain, gz) in one pass over
+// the parts (HTC's concat → bgzip → tabix tail as one stage).
+void vcf_concat_bgzip_tabix(const std::vector<std::string>& inputs, const std::string& plain, const std::string& gz);
 
 }  // namespace fcsg

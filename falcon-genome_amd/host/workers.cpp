@@ -164,15 +164,19 @@ int Mutect2Worker::run(TaskContext& ctx) {
 }
 
 // ------------------------------------------------------------------ VCF tail
-VCFConcatWorker::VCFConcatWorker(std::vector<std::string> inputs, std::string output)
-    : Worker(1, 1, {}, "VCF concat"), inputs_(std::move(inputs)), output_(std::move(output)) {}
+VCFConcatWorker::VCFConcatWorker(std::vector<std::string> inputs, std::string output, std::string gz)
+    : Worker(1, 1, {}, gz.empty() ? "VCF concat" : "VCF concat + bgzip + tabix"),
+      inputs_(std::move(inputs)),
+      output_(std::move(output)),
+      gz_(std::move(gz)) {}
 
 void VCFConcatWorker::check() {
   if (inputs_.empty()) throw invalidParam("no VCF to concatenate");
 }
 
 int VCFConcatWorker::run(TaskContext&) {
-  vcf_concat(inputs_, output_);
+  if (gz_.empty()) vcf_concat(inputs_, output_);
+  else vcf_concat_bgzip_tabix(inputs_, output_, gz_);
   return 0;
 }
 

@@ -63,13 +63,14 @@ class Mutect2Worker : public Worker {
 
 class VCFConcatWorker : public Worker {
  public:
-  VCFConcatWorker(std::vector<std::string> inputs, std::string output);
+  // gz non-empty: also gz + gz.tbi from the same pass (concat + bgzip + tabix as one stage)
+  VCFConcatWorker(std::vector<std::string> inputs, std::string output, std::string gz = "");
   void check() override;
   int run(TaskContext& ctx) override;
 
  private:
   std::vector<std::string> inputs_;
-  std::string output_;
+  std::string output_, gz_;
 };
 
 class ZIPWorker : public Worker {

@@ -221,6 +221,53 @@ def test_vcf_concat_bgzip_tabix(tmp_path):
     assert gz2.read_bytes() == gz.read_bytes()
     assert gzip.decompress((tmp_path / "one.vcf.gz.tbi").read_bytes()) == \
         gzip.decompress((tmp_path / "all.vcf.gz.tbi").read_bytes())
+    # concat + bgzip + tabix in one pass over the parts (htc's tail): the same three files
+    fused, gz3 = tmp_path / "fused.vcf", tmp_path / "fused.vcf.gz"
+    H.check(H.lib.fcsg_vcf_concat_bgzip_tabix(arr, 3, str(fused).encode(), str(gz3).encode()))
+    assert fused.read_bytes() == out.read_bytes() and gz3.read_bytes() == gz.read_bytes()
+    assert gzip.decompress((tmp_path / "fused.vcf.gz.tbi").read_bytes()) == \
+        gzip.decompress((tmp_path / "all.vcf.gz.tbi").read_bytes())
+
+
+def test_vcf_concat_bgzip_tabix_fused_edges(tmp_path):
+    """The fused tail on parts that are header-only, empty, end without '\\n',
+    carry GVCF END= blocks and run past many 64 KiB blocks: the same files as
+    vcf_concat + bgzip + tabix."""
+    hdr = "##fileformat=VCFv4.2\n#CHROM\tPOS\tID\tREF\tALT\tQUAL\tFILTER\tINFO\tFORMAT\tS\n"
+    rng = random.Random(3)
+    pos, lines = 1, []
+    for _ in range(30000):
+        n = rng.randrange(1, 9)
+        info = f"END={pos + n - 1}" if rng.random() < 0.8 else "DP=3;END=." if rng.random() < 0.5 else f"X=1;END={pos + 2}"
+        lines.append(f"c1\t{pos}\t.\tA\t<NON_REF>\t.\t.\t{info}\tGT:DP\t0/0:{rng.randrange(40)}")
+        pos += n
+    bodies = ["".join(x + "\n" for x in lines[:12000]), "", "".join(x + "\n" for x in lines[12000:29000]),
+              "\n".join(lines[29000:])]  # the last part ends without '\n'
+    paths = []
+    for i, body in enumerate(bodies):
+        f = tmp_path / f"p{i}.g.vcf"
+        f.write_text(hdr + body)
+        paths.append(str(f).encode())
+    (tmp_path / "empty.g.vcf").write_text("")
+    paths.insert(2, str(tmp_path / "empty.g.vcf").encode())
+    arr = (C.c_char_p * len(paths))(*paths)
+    two, gz_two = tmp_path / "two.g.vcf", tmp_path / "two.g.vcf.gz"
+    H.check(H.lib.fcsg_vcf_concat(arr, len(paths), str(two).encode()))
+    H.check(H.lib.fcsg_bgzip_tabix(str(two).encode(), str(gz_two).encode()))
+    one, gz_one = tmp_path / "one.g.vcf", tmp_path / "one.g.vcf.gz"
+    H.check(H.lib.fcsg_vcf_concat_bgzip_tabix(arr, len(paths), str(one).encode(), str(gz_one).encode()))
+    assert one.read_text() == hdr + "".join(x + "\n" for x in lines)
+    assert one.read_bytes() == two.read_bytes() and gz_one.read_bytes() == gz_two.read_bytes()
+    assert len(H.bgzf_blocks(gz_one)) > 20
+    assert gzip.decompress((tmp_path / "one.g.vcf.gz.tbi").read_bytes()) == \
+        gzip.decompress((tmp_path / "two.g.vcf.gz.tbi").read_bytes())
+    # and tabix of the bgzipped file (the two-pass path) agrees
+    H.check(H.lib.fcsg_tabix(str(gz_two).encode()))
+    assert gzip.decompress((tmp_path / "one.g.vcf.gz.tbi").read_bytes()) == \
+        gzip.decompress((tmp_path / "two.g.vcf.gz.tbi").read_bytes())
+    # a missing part fails the call
+    bad = (C.c_char_p * 2)(paths[0], str(tmp_path / "nope.g.vcf").encode())
+    assert H.lib.fcsg_vcf_concat_bgzip_tabix(bad, 2, str(tmp_path / "x").encode(), str(tmp_path / "x.gz").encode()) != 0
 
 
 def test_bgzip_tabix_one_pass_block_edges(tmp_path):

@@ -1,15 +1,17 @@
 #!/bin/bash
 # Wall-time probe of the e2e commands on a GPU box (stage lines from stderr).
 W=$(mktemp -d /tmp/e2e.XXXX)
-export FCS_GPU_DEVICES=0 FCS_LOG_DIR=$W/log FCS_TEMP_DIR=$W FCS_GATK_NPROCS=16
+export FCS_TIMELINE=1 FCS_GPU_DEVICES=0 FCS_LOG_DIR=$W/log FCS_TEMP_DIR=$W FCS_GATK_NPROCS=${NPROCS:-16}
+MBP=${MBP:-4}
 B=$GRAFT_REPO_ROOT/falcon-genome_amd/bin/fcs-genome
 t() { local s=$(date +%s.%N); "$@"; local rc=$?; echo "  wall $(awk "BEGIN{print $(date +%s.%N) - $s}") s rc=$rc: $*" >&2; return $rc; }
-t timeout 300 $B synth -o $W/d -c chr1:4000000 -x 30 --tumor --noisy-frac 0.01 --paired 350 > /dev/null || exit 1
+t timeout 300 $B synth -o $W/d -c chr1:$((MBP * 1000000)) -x 30 --tumor --noisy-frac 0.01 --paired 350 > /dev/null || exit 1
 for i in 1 2; do
-  t timeout 300 $B htc -r $W/d/ref.fasta -i $W/d/sample.bam -o $W/h$i.g.vcf 2> $W/htc$i.err || { tail $W/htc$i.err; exit 1; }
-  grep -E "finishes|Start" $W/htc$i.err
+  { time timeout 300 $B htc -f -r $W/d/ref.fasta -i $W/d/sample.bam -o $W/h$i.g.vcf 2> $W/htc$i.err; } 2> $W/htc$i.time || { tail $W/htc$i.err; exit 1; }
+  grep -E "finishes|Start|phase|timeline" $W/htc$i.err; grep -E "^(real|user|sys)" $W/htc$i.time
 done
 sed -e 's/^/  | /' $W/htc2.err | head -60
+[ -n "${HTC_ONLY:-}" ] && { ls -la $W/h2.g.vcf* >&2; rm -rf $W; exit 0; }
 t timeout 300 $B mutect2 -r $W/d/ref.fasta -t $W/d/tumor.bam -n $W/d/sample.bam -o $W/m2.vcf 2> $W/m2.err
 sed -e 's/^/  | /' $W/m2.err | head -60
 t timeout 300 $B htc -r $W/d/ref.fasta -i $W/d/sample.bam -o $W/hv.vcf -v 2> $W/htcv.err
