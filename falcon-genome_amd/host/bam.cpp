@@ -64,10 +64,9 @@ size_t aux_value_size(char t, const uint8_t* p, const uint8_t* end) {
   }
 }
 
-// Offset of tag in aux (pointing at the 2 tag bytes), or npos.
-size_t find_aux(const std::string& aux, const char tag[2]) {
-  const uint8_t* b = reinterpret_cast<const uint8_t*>(aux.data());
-  const uint8_t* e = b + aux.size();
+// Offset of tag in the raw aux bytes b[0, n) (pointing at the 2 tag bytes), or npos.
+size_t find_aux_raw(const uint8_t* b, size_t n, const char tag[2]) {
+  const uint8_t* e = b + n;
   const uint8_t* p = b;
   while (p + 3 <= e) {
     const size_t vs = aux_value_size((char)p[2], p + 3, e);
@@ -77,6 +76,21 @@ size_t find_aux(const std::string& aux, const char tag[2]) {
   }
   return std::string::npos;
 }
+
+size_t find_aux(const std::string& aux, const char tag[2]) {
+  return find_aux_raw(reinterpret_cast<const uint8_t*>(aux.data()), aux.size(), tag);
+}
+
+// Both bases of every packed byte (high nibble first).
+struct SeqPairTable {
+  char pair[256][2];
+  SeqPairTable() {
+    for (int b = 0; b < 256; ++b) {
+      pair[b][0] = kSeqNt16[b >> 4];
+      pair[b][1] = kSeqNt16[b & 0xf];
+    }
+  }
+};
 
 void erase_aux(std::string& aux, const char tag[2]) {
   const size_t k = find_aux(aux, tag);
@@ -138,10 +152,21 @@ uint16_t reg2bin(int64_t beg, int64_t end) {
 }
 
 bool BamRecord::get_aux_string(const char tag[2], std::string& out) const {
-  const size_t k = find_aux(aux, tag);
+  return bam_aux_string(reinterpret_cast<const uint8_t*>(aux.data()), aux.size(), tag, out);
+}
+
+bool bam_aux_string(const uint8_t* aux, size_t n, const char tag[2], std::string& out) {
+  const size_t k = find_aux_raw(aux, n, tag);
   if (k == std::string::npos || aux[k + 2] != 'Z') return false;
-  out.assign(aux.c_str() + k + 3);
+  out.assign(reinterpret_cast<const char*>(aux) + k + 3);  // NUL-terminated: find_aux_raw checked
   return true;
+}
+
+void decode_bam_seq(const uint8_t* packed, int32_t l_seq, char* out) {
+  static const SeqPairTable t;
+  int32_t i = 0;
+  for (; i + 1 < l_seq; i += 2) std::memcpy(out + i, t.pair[packed[i / 2]], 2);
+  if (i < l_seq) out[i] = t.pair[packed[i / 2]][0];
 }
 
 bool BamRecord::get_aux_int(const char tag[2], int64_t& out) const {
@@ -233,10 +258,7 @@ void decode_bam_record(const uint8_t* p, size_t n, BamRecord& r) {
   for (uint16_t i = 0; i < n_cigar; ++i) r.cigar[i] = get<uint32_t>(p + k + 4 * i);
   k += 4 * (size_t)n_cigar;
   r.seq.resize(l_seq);
-  for (int32_t i = 0; i < l_seq; ++i) {
-    const uint8_t b = p[k + i / 2];
-    r.seq[i] = kSeqNt16[(i & 1) ? (b & 0xf) : (b >> 4)];
-  }
+  decode_bam_seq(p + k, l_seq, r.seq.data());
   k += (l_seq + 1) / 2;
   if (l_seq > 0 && p[k] == 0xff) r.qual.clear();
   else r.qual.assign(p + k, p + k + l_seq);
@@ -297,12 +319,21 @@ BamReader::BamReader(const std::string& path) : bgzf_(path) {
 }
 
 bool BamReader::next(BamRecord& r) {
+  const uint8_t* body;
+  size_t n;
+  if (!next_raw(body, n)) return false;
+  decode_bam_record(body, n, r);
+  return true;
+}
+
+bool BamReader::next_raw(const uint8_t*& body, size_t& n) {
   int32_t bs = 0;
   if (!bgzf_.read_exact(&bs, 4)) return false;
   if (bs < 32) throw formatError("bad BAM block_size");
   buf_.resize(bs);
   bgzf_.read_exact(buf_.data(), bs);
-  decode_bam_record(buf_.data(), buf_.size(), r);
+  body = buf_.data();
+  n = buf_.size();
   return true;
 }
 

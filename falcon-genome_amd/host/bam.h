@@ -90,6 +90,9 @@ class BamReader {
   explicit BamReader(const std::string& path);
   const BamHeader& header() const { return hdr_; }
   bool next(BamRecord& r);  // false at end
+  // The next record's raw body (after block_size), valid until the next call;
+  // false at end.  For readers that decode only the fields they use.
+  bool next_raw(const uint8_t*& body, size_t& n);
   uint64_t tell() const { return bgzf_.tell(); }
   void seek(uint64_t voff) { bgzf_.seek(voff); }
 
@@ -102,6 +105,10 @@ class BamReader {
 // Serialisation of one record body (after block_size), exposed for tests.
 void encode_bam_record(const BamRecord& r, std::string& out);
 void decode_bam_record(const uint8_t* p, size_t n, BamRecord& r);
+// The l_seq bases of a packed 4-bit BAM SEQ field as ASCII (=ACMGRSVTWYHKDBN).
+void decode_bam_seq(const uint8_t* packed, int32_t l_seq, char* out);
+// A 'Z' aux value of tag in the raw aux bytes aux[0, n); false when absent.
+bool bam_aux_string(const uint8_t* aux, size_t n, const char tag[2], std::string& out);
 
 }  // namespace fcsg
 

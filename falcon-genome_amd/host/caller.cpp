@@ -1,11 +1,17 @@
 #include "caller.h"
 
+#include <sys/resource.h>
+#include <time.h>
+
 #include <algorithm>
 #include <array>
+#include <charconv>
 #include <cmath>
 #include <cstdio>
+#include <cstring>
 #include <map>
 #include <memory>
+#include <string_view>
 #include <tuple>
 
 #include "bam.h"
@@ -13,6 +19,7 @@
 #include "common.h"
 #include "fcship.h"
 #include "gatk_prep.h"
+#include "hugebuf.h"
 
 namespace fcsg {
 
@@ -23,6 +30,9 @@ void CallerStats::add(const CallerStats& o) {
   cells += o.cells;
   calls += o.calls;
   device_passes += o.device_passes;
+  decode_passes += o.decode_passes;
+  cpu_seconds += o.cpu_seconds;
+  for (int k = 0; k < 4; ++k) faults[k] += o.faults[k];
   rescued += o.rescued;
   seconds += o.seconds;
   phmm_seconds += o.phmm_seconds;
@@ -37,18 +47,30 @@ void CallerStats::add(const CallerStats& o) {
 
 namespace {
 
+// A read of the window: its CIGAR, bases, qualities and BI / BD strings live
+// in the window's HugeSlab (no per-read heap blocks).
+template <typename T>
+struct View {
+  const T* p = nullptr;
+  size_t n = 0;
+  const T* begin() const { return p; }
+  const T* end() const { return p + n; }
+  size_t size() const { return n; }
+  bool empty() const { return n == 0; }
+  const T& operator[](size_t i) const { return p[i]; }
+};
 struct Read {
   int32_t pos = 0;
   int64_t end = 0;
-  std::vector<uint32_t> cigar;
-  std::string seq;
-  std::vector<uint8_t> qual;
+  View<uint32_t> cigar;
+  std::string_view seq;
+  View<uint8_t> qual;
   int mapq = 0;
-  std::string bi, bd;
+  std::string_view bi, bd;
 };
 
 void load_reads_one(const std::string& bam, const std::string& chrom, int64_t beg, int64_t end,
-                    const CallerOptions& opt, std::vector<Read>& out) {
+                    const CallerOptions& opt, HugeSlab& slab, std::vector<Read>& out) {
   BamReader rd(bam);
   const int tid = rd.header().ref_index(chrom);
   if (tid < 0) return;
@@ -57,32 +79,68 @@ void load_reads_one(const std::string& bam, const std::string& chrom, int64_t be
     const uint64_t off = BamIndex(bai).seek_offset(tid, beg);
     if (off) rd.seek(off);
   }
-  BamRecord r;
-  while (rd.next(r)) {
-    if (r.ref_id < tid) continue;
-    if (r.ref_id > tid || r.pos >= end) break;
-    if (r.flag & (kUnmapped | kSecondary | kQcFail | kDuplicate | kSupplementary)) continue;
-    if (r.mapq < opt.min_mapq || r.cigar.empty() || r.qual.size() != r.seq.size()) continue;
-    const int64_t e = r.end();
+  // fields read straight from the raw record (decode_bam_record's layout),
+  // filters applied before SEQ / QUAL are decoded
+  auto get32 = [](const uint8_t* q) {
+    int32_t v;
+    std::memcpy(&v, q, 4);
+    return v;
+  };
+  auto get16 = [](const uint8_t* q) {
+    uint16_t v;
+    std::memcpy(&v, q, 2);
+    return v;
+  };
+  const uint8_t* p;
+  size_t n;
+  std::string tag;
+  while (rd.next_raw(p, n)) {
+    const int32_t ref_id = get32(p), pos = get32(p + 4);
+    if (ref_id < tid) continue;
+    if (ref_id > tid || pos >= end) break;
+    const uint8_t l_name = p[8], mapq = p[9];
+    const uint16_t n_cigar = get16(p + 12), flag = get16(p + 14);
+    const int32_t l_seq = get32(p + 16);
+    const size_t kc = 32 + (size_t)l_name, ks = kc + 4 * (size_t)n_cigar, kq = ks + (size_t)(l_seq + 1) / 2,
+                 ka = kq + (size_t)l_seq;
+    if (l_seq < 0 || ka > n) throw formatError("truncated BAM record");
+    if (flag & (kUnmapped | kSecondary | kQcFail | kDuplicate | kSupplementary)) continue;
+    if (mapq < opt.min_mapq || n_cigar == 0) continue;
+    if (l_seq > 0 && p[kq] == 0xff) continue;  // QUAL absent
+    int64_t rlen = 0;
+    for (uint16_t i = 0; i < n_cigar; ++i) {
+      const uint32_t c = (uint32_t)get32(p + kc + 4 * i);
+      const CigarOp op = cigar_op(c);
+      if (op == kM || op == kD || op == kN || op == kEq || op == kX) rlen += cigar_len(c);
+    }
+    const int64_t e = pos + rlen;
     if (e <= beg) continue;
-    Read x;
-    x.pos = r.pos;
+    Read& x = out.emplace_back();
+    x.pos = pos;
     x.end = e;
-    x.cigar = std::move(r.cigar);
-    x.seq = std::move(r.seq);
-    x.qual = std::move(r.qual);
-    x.mapq = r.mapq;
-    r.get_aux_string("BI", x.bi);
-    r.get_aux_string("BD", x.bd);
-    out.push_back(std::move(x));
+    uint8_t* m = slab.alloc(4 * (size_t)n_cigar + 2 * (size_t)l_seq, 4);
+    std::memcpy(m, p + kc, 4 * (size_t)n_cigar);
+    x.cigar = {reinterpret_cast<const uint32_t*>(m), n_cigar};
+    m += 4 * (size_t)n_cigar;
+    decode_bam_seq(p + ks, l_seq, reinterpret_cast<char*>(m));
+    x.seq = std::string_view(reinterpret_cast<const char*>(m), (size_t)l_seq);
+    std::memcpy(m + l_seq, p + kq, (size_t)l_seq);
+    x.qual = {m + l_seq, (size_t)l_seq};
+    x.mapq = mapq;
+    for (int t = 0; t < 2; ++t) {
+      if (!bam_aux_string(p + ka, n - ka, t ? "BD" : "BI", tag)) continue;
+      char* c = reinterpret_cast<char*>(slab.alloc(tag.size(), 1));
+      std::memcpy(c, tag.data(), tag.size());
+      (t ? x.bd : x.bi) = std::string_view(c, tag.size());
+    }
   }
 }
 
 // Reads of the window from every part of the sample, in coordinate order
 // (parts of a `--disable-merge` alignment are each sorted).
 void load_reads(const std::vector<std::string>& bams, const std::string& chrom, int64_t beg, int64_t end,
-                const CallerOptions& opt, std::vector<Read>& out) {
-  for (const std::string& b : bams) load_reads_one(b, chrom, beg, end, opt, out);
+                const CallerOptions& opt, HugeSlab& slab, std::vector<Read>& out) {
+  for (const std::string& b : bams) load_reads_one(b, chrom, beg, end, opt, slab, out);
   if (bams.size() > 1)
     std::stable_sort(out.begin(), out.end(), [](const Read& a, const Read& b) { return a.pos < b.pos; });
 }
@@ -96,14 +154,16 @@ struct Allele {
 
 struct Pileup {
   int64_t wb = 0;
-  std::vector<int> depth, events;
-  // allele events of the reads, then (finish_support) sorted and counted:
-  // the support of each distinct allele in (pos, ref, alt) order
-  std::vector<Allele> events_list;
+  HugeArray<int> depth, events;
+  // allele events of the reads — SNVs as packed (pos, ref, alt) keys, indels
+  // as Alleles — then (finish_support) sorted and counted: the support of
+  // each distinct allele in (pos, ref, alt) order
+  std::vector<uint64_t> snv_events;
+  std::vector<Allele> indel_events;
   std::vector<std::pair<Allele, int>> support;
   // GVCF reference model: per position, sum over bases of log10 P(base | 0/0,
   // 0/1, 1/1) with 1 = <NON_REF> (any other base)
-  std::vector<double> gl;  // 3 per position; empty unless GVCF
+  HugeArray<double> gl;  // 3 per position; empty unless GVCF
 };
 
 // log10 P(base | genotype) per base quality: [q][0] ref base under 0/0 (1 - e),
@@ -125,49 +185,65 @@ const RefModel& ref_model() {
   return m;
 }
 
+inline uint64_t snv_key(int64_t pos, char ref, char alt) {
+  return ((uint64_t)pos << 16) | ((uint64_t)(uint8_t)ref << 8) | (uint8_t)alt;
+}
+
 // Walks every read's CIGAR once: depth, mismatch/indel events and allele support.
 void build_pileup(const std::string& ref, const std::vector<Read>& reads, int min_bq, Pileup& pu) {
   const int64_t n = (int64_t)pu.depth.size();
-  auto in = [&](int64_t p) { return p >= pu.wb && p < pu.wb + n; };
+  const int64_t wb = pu.wb, we = pu.wb + n;
+  auto in = [&](int64_t p) { return p >= wb && p < we; };
+  const RefModel& M = ref_model();
+  int* depth = pu.depth.data();
+  int* events = pu.events.data();
+  double* gl = pu.gl.empty() ? nullptr : pu.gl.data();
   for (const Read& rd : reads) {
     int64_t rp = rd.pos;
     size_t q = 0;
     for (uint32_t c : rd.cigar) {
       const uint32_t len = cigar_len(c);
       switch (cigar_op(c)) {
-        case kM: case kEq: case kX:
-          for (uint32_t k = 0; k < len; ++k, ++rp, ++q) {
-            if (!in(rp) || rd.qual[q] < min_bq) continue;
-            ++pu.depth[rp - pu.wb];
-            const char b = rd.seq[q];
-            const bool nonref = b != ref[rp] && ref[rp] != 'N' && b != 'N';
+        case kM: case kEq: case kX: {
+          // only the bases inside the window
+          const int64_t lo = std::max<int64_t>(rp, wb), hi = std::min<int64_t>(rp + len, we);
+          for (int64_t p = lo; p < hi; ++p) {
+            const size_t qi = q + (size_t)(p - rp);
+            const uint8_t bq = rd.qual[qi];
+            if (bq < min_bq) continue;
+            ++depth[p - wb];
+            const char b = rd.seq[qi], r = ref[p];
+            const bool nonref = b != r && r != 'N' && b != 'N';
             if (nonref) {
-              ++pu.events[rp - pu.wb];
-              pu.events_list.push_back({rp, std::string(1, ref[rp]), std::string(1, b)});
+              ++events[p - wb];
+              pu.snv_events.push_back(snv_key(p, r, b));
             }
-            if (!pu.gl.empty()) {
-              const double* t = ref_model().t[std::min<int>(rd.qual[q], 93)];
-              double* g = &pu.gl[3 * (rp - pu.wb)];
-              g[0] += nonref ? t[2] : t[0];
+            if (gl) {
+              const double* t = M.t[std::min<int>(bq, 93)];
+              double* g = gl + 3 * (p - wb);
+              g[0] += t[nonref ? 2 : 0];
               g[1] += t[1];
-              g[2] += nonref ? t[0] : t[2];
+              g[2] += t[nonref ? 0 : 2];
             }
           }
+          rp += len;
+          q += len;
           break;
+        }
         case kI:
           if (rp > rd.pos && in(rp - 1)) {
-            ++pu.events[rp - 1 - pu.wb];
-            pu.events_list.push_back({rp - 1, std::string(1, ref[rp - 1]), ref[rp - 1] + rd.seq.substr(q, len)});
+            ++events[rp - 1 - wb];
+            pu.indel_events.push_back({rp - 1, std::string(1, ref[rp - 1]), std::string(1, ref[rp - 1]).append(rd.seq.substr(q, len))});
           }
           q += len;
           break;
         case kD:
           if (rp > rd.pos && in(rp - 1) && rp + len <= (int64_t)ref.size()) {
-            ++pu.events[rp - 1 - pu.wb];
-            pu.events_list.push_back({rp - 1, ref.substr(rp - 1, len + 1), std::string(1, ref[rp - 1])});
+            ++events[rp - 1 - wb];
+            pu.indel_events.push_back({rp - 1, ref.substr(rp - 1, len + 1), std::string(1, ref[rp - 1])});
           }
-          for (uint32_t k = 0; k < len; ++k, ++rp)
-            if (in(rp)) ++pu.depth[rp - pu.wb];
+          for (int64_t p = std::max<int64_t>(rp, wb), hi = std::min<int64_t>(rp + len, we); p < hi; ++p) ++depth[p - wb];
+          rp += len;
           break;
         case kN: rp += len; break;
         case kS: q += len; break;
@@ -177,16 +253,36 @@ void build_pileup(const std::string& ref, const std::vector<Read>& reads, int mi
   }
 }
 
-// The distinct alleles of pu.events_list with their read counts, in order.
+// The distinct alleles of the pileup's events with their read counts, in
+// (pos, ref, alt) order: the SNV keys sort as integers (a one-base REF and
+// ALT compare as their bytes), the indels as Alleles, and the two runs merge
+// (an indel never equals an SNV: its REF or ALT is longer than one base).
 void finish_support(Pileup& pu) {
-  std::sort(pu.events_list.begin(), pu.events_list.end());
+  std::sort(pu.snv_events.begin(), pu.snv_events.end());
+  std::sort(pu.indel_events.begin(), pu.indel_events.end());
   pu.support.clear();
-  for (Allele& a : pu.events_list) {
-    if (!pu.support.empty() && !(pu.support.back().first < a)) ++pu.support.back().second;
-    else pu.support.emplace_back(std::move(a), 1);
+  size_t i = 0, j = 0;
+  const size_t ns = pu.snv_events.size(), ni = pu.indel_events.size();
+  while (i < ns || j < ni) {
+    if (i < ns) {
+      const uint64_t k = pu.snv_events[i];
+      Allele a{(int64_t)(k >> 16), std::string(1, (char)((k >> 8) & 0xff)), std::string(1, (char)(k & 0xff))};
+      if (j >= ni || a < pu.indel_events[j]) {
+        size_t e = i;
+        while (e < ns && pu.snv_events[e] == k) ++e;
+        pu.support.emplace_back(std::move(a), (int)(e - i));
+        i = e;
+        continue;
+      }
+    }
+    Allele& a = pu.indel_events[j];
+    size_t e = j + 1;
+    while (e < ni && !(a < pu.indel_events[e])) ++e;
+    pu.support.emplace_back(std::move(a), (int)(e - j));
+    j = e;
   }
-  pu.events_list.clear();
-  pu.events_list.shrink_to_fit();
+  std::vector<uint64_t>().swap(pu.snv_events);
+  std::vector<Allele>().swap(pu.indel_events);
 }
 
 // Query slice [qs, qe) of the read whose bases align inside [rb, re) (inserted
@@ -453,43 +549,49 @@ void genotype_somatic(const Region& g, const CallerOptions& opt, int64_t own_beg
 // gets the hom-ref genotype likelihoods of its pileup (RefModel); runs of
 // positions whose GQ falls in one band become one record
 // "<NON_REF> END=..  GT:DP:GQ:MIN_DP:PL" with the block's median DP, minimum
-// GQ / DP and element-wise minimum PLs.
-void emit_gvcf(const std::string& seq, const Pileup& pu, int64_t beg, int64_t end, const std::string& chrom,
-               std::vector<const VcfRecord*>& ic, std::vector<VcfRecord>& out) {
-  std::stable_sort(ic.begin(), ic.end(), [](const VcfRecord* a, const VcfRecord* b) { return a->pos < b->pos; });
+// GQ / DP and element-wise minimum PLs.  Blocks are kept as plain numbers
+// (GvcfBlock) and the output sequence as entries naming a block or a call:
+// the GVCF's hundreds of thousands of block lines are formatted straight into
+// the writer's buffer, never built as VcfRecord strings.
+struct GvcfBlock {
+  int64_t b, e;  // 0-based first / last position
+  int dp, gq, mindp;
+  int pl[3];
+};
+struct OutEntry {
+  int32_t contig;  // reference contig index
+  int32_t block;   // into the GvcfBlock list, or -1
+  int64_t call;    // into the calls, or -1
+  int64_t pos;     // 1-based POS
+};
+
+void emit_gvcf(const Pileup& pu, int64_t beg, int64_t end, int contig, const std::vector<VcfRecord>& calls,
+               size_t c0, std::vector<GvcfBlock>& blocks, std::vector<OutEntry>& out) {
+  std::vector<size_t> ic;  // this interval's calls in POS order (stable)
+  for (size_t i = c0; i < calls.size(); ++i) ic.push_back(i);
+  std::stable_sort(ic.begin(), ic.end(), [&](size_t a, size_t b) { return calls[a].pos < calls[b].pos; });
   struct Block {
     int64_t b = -1, e = -1;
     int band = -1, gq = 99, mindp = 0;
     int pl[3] = {0, 0, 0};
-    std::vector<int> dps;
   } blk;
+  std::vector<int> dps;
   auto flush = [&] {
     if (blk.b < 0) return;
-    VcfRecord r;
-    r.chrom = chrom;
-    r.pos = blk.b + 1;
-    r.ref = std::string(1, seq[blk.b]);
-    r.alts = {"<NON_REF>"};
-    r.filter = ".";
-    r.info = "END=" + std::to_string(blk.e + 1);
-    r.format = "GT:DP:GQ:MIN_DP:PL";
-    std::nth_element(blk.dps.begin(), blk.dps.begin() + blk.dps.size() / 2, blk.dps.end());
-    r.samples = {"0/0:" + std::to_string(blk.dps[blk.dps.size() / 2]) + ":" + std::to_string(blk.gq) + ":" +
-                 std::to_string(blk.mindp) + ":" + std::to_string(blk.pl[0]) + "," + std::to_string(blk.pl[1]) + "," +
-                 std::to_string(blk.pl[2])};
-    out.push_back(std::move(r));
-    std::vector<int> keep = std::move(blk.dps);  // reuse the buffer
-    keep.clear();
+    std::nth_element(dps.begin(), dps.begin() + dps.size() / 2, dps.end());
+    out.push_back({contig, (int32_t)blocks.size(), -1, blk.b + 1});
+    blocks.push_back({blk.b, blk.e, dps[dps.size() / 2], blk.gq, blk.mindp, {blk.pl[0], blk.pl[1], blk.pl[2]}});
+    dps.clear();
     blk = Block();
-    blk.dps = std::move(keep);
   };
   size_t ci = 0;
   int64_t covered = beg;  // positions below are inside an emitted call's REF span
   for (int64_t p = beg; p < end; ++p) {
-    while (ci < ic.size() && ic[ci]->pos - 1 <= p) {
+    while (ci < ic.size() && calls[ic[ci]].pos - 1 <= p) {
       flush();
-      out.push_back(*ic[ci]);
-      covered = std::max<int64_t>(covered, ic[ci]->pos - 1 + (int64_t)ic[ci]->ref.size());
+      const VcfRecord& c = calls[ic[ci]];
+      out.push_back({contig, -1, (int64_t)ic[ci], c.pos});
+      covered = std::max<int64_t>(covered, c.pos - 1 + (int64_t)c.ref.size());
       ++ci;
     }
     if (p < covered) continue;
@@ -512,10 +614,53 @@ void emit_gvcf(const std::string& seq, const Pileup& pu, int64_t beg, int64_t en
     blk.gq = std::min(blk.gq, gq);
     blk.mindp = std::min(blk.mindp, dp);
     for (int k = 0; k < 3; ++k) blk.pl[k] = std::min(blk.pl[k], pl[k]);
-    blk.dps.push_back(dp);
+    dps.push_back(dp);
   }
   flush();
-  for (; ci < ic.size(); ++ci) out.push_back(*ic[ci]);
+  for (; ci < ic.size(); ++ci) out.push_back({contig, -1, (int64_t)ic[ci], calls[ic[ci]].pos});
+}
+
+// One GVCF block line, as VcfRecord::append_line writes the record
+// {chrom, b + 1, ".", REF, "<NON_REF>", ".", ".", "END=e + 1",
+//  "GT:DP:GQ:MIN_DP:PL", "0/0:DP:GQ:MIN_DP:PL0,PL1,PL2"}.
+void append_block_line(const std::string& chrom, char ref, const GvcfBlock& k, std::string& s) {
+  char b[256];  // 2 x 20 + 6 x 11 digits + 60 literal bytes at most
+  char* p = b;
+  auto num = [&](int64_t v) {  // decimal, as std::to_chars
+    uint64_t u = v < 0 ? (*p++ = '-', 0 - (uint64_t)v) : (uint64_t)v;
+    char d[20];
+    int k = 0;
+    do {
+      d[k++] = (char)('0' + u % 10);
+      u /= 10;
+    } while (u);
+    while (k) *p++ = d[--k];
+  };
+  auto lit = [&](std::string_view t) {
+    std::memcpy(p, t.data(), t.size());
+    p += t.size();
+  };
+  s += chrom;
+  *p++ = '\t';
+  num(k.b + 1);
+  lit("\t.\t");
+  *p++ = ref;
+  lit("\t<NON_REF>\t.\t.\tEND=");
+  num(k.e + 1);
+  lit("\tGT:DP:GQ:MIN_DP:PL\t0/0:");
+  num(k.dp);
+  *p++ = ':';
+  num(k.gq);
+  *p++ = ':';
+  num(k.mindp);
+  *p++ = ':';
+  num(k.pl[0]);
+  *p++ = ',';
+  num(k.pl[1]);
+  *p++ = ',';
+  num(k.pl[2]);
+  *p++ = '\n';
+  s.append(b, (size_t)(p - b));
 }
 
 }  // namespace
@@ -534,13 +679,29 @@ int gvcf_band(int gq) {
   return gq >= 0 && gq < 100 ? lut[gq] : band(gq);
 }
 
+namespace {
+int64_t thread_faults() {
+  struct rusage ru {};
+  getrusage(RUSAGE_THREAD, &ru);
+  return ru.ru_minflt;
+}
+double thread_cpu() {
+  timespec ts{};
+  clock_gettime(CLOCK_THREAD_CPUTIME_ID, &ts);
+  return ts.tv_sec + ts.tv_nsec / 1e9;
+}
+}  // namespace
+
 CallerStats call_intervals(const Reference& ref, const std::vector<std::string>& bams,
                            const std::vector<std::string>& normal_bams, const std::vector<Interval>& intervals_in,
                            const CallerOptions& opt, VcfWriter& out) {
   CallerStats st;
   const uint64_t t0 = now_us();
+  const double cpu0 = thread_cpu();
   std::FILE* dump = opt.dump_path.empty() ? nullptr : std::fopen(opt.dump_path.c_str(), "ab");
-  std::vector<VcfRecord> calls, gout;
+  std::vector<VcfRecord> calls;
+  std::vector<GvcfBlock> blocks;  // GVCF mode: reference blocks and the output sequence
+  std::vector<OutEntry> gout;
   const std::vector<Interval>& intervals = intervals_in;
   std::vector<std::unique_ptr<Region>> pending;
   std::vector<std::tuple<int64_t, int64_t, std::string>> own;  // per pending region: owned range + chrom
@@ -577,6 +738,7 @@ CallerStats call_intervals(const Reference& ref, const std::vector<std::string>&
     // do not depend on where gatk.ncontigs put the shard boundaries.
     int64_t ext_l = opt.max_region, ext_r = opt.max_region, wb = 0, we = 0;
     std::vector<Read> reads[2];
+    HugeSlab slab;  // the reads' bytes
     Pileup pu;
     std::vector<std::pair<int64_t, int64_t>> clusters;  // [first site, last site] overlapping the own range
     for (;;) {
@@ -584,16 +746,24 @@ CallerStats call_intervals(const Reference& ref, const std::vector<std::string>&
       we = std::min<int64_t>(L, own_end + ext_r);
       reads[0].clear();
       reads[1].clear();
+      slab.clear();
+      // ~0.2 reads per base at 30x of 150 bp: reserving address space (untouched
+      // pages cost nothing) saves the vector's doubling copies
+      for (int s = 0; s < (opt.somatic ? 2 : 1); ++s) reads[s].reserve((size_t)(we - wb) / 2);
       const uint64_t td = now_us();
-      load_reads(bams, iv.chrom, wb, we, opt, reads[0]);
-      if (opt.somatic) load_reads(normal_bams, iv.chrom, wb, we, opt, reads[1]);
+      const int64_t f0 = thread_faults();
+      load_reads(bams, iv.chrom, wb, we, opt, slab, reads[0]);
+      if (opt.somatic) load_reads(normal_bams, iv.chrom, wb, we, opt, slab, reads[1]);
       const uint64_t tp = now_us();
       st.decode_seconds += (tp - td) / 1e6;
+      ++st.decode_passes;
+      const int64_t f1 = thread_faults();
+      st.faults[0] += f1 - f0;
       pu = Pileup();
       pu.wb = wb;
-      pu.depth.assign(we - wb, 0);
-      pu.events.assign(we - wb, 0);
-      if (opt.gvcf && !opt.somatic) pu.gl.assign(3 * (we - wb), 0.0);
+      pu.depth = HugeArray<int>((size_t)(we - wb));  // zero-filled
+      pu.events = HugeArray<int>((size_t)(we - wb));
+      if (opt.gvcf && !opt.somatic) pu.gl = HugeArray<double>(3 * (size_t)(we - wb));
       build_pileup(seq, reads[0], opt.min_base_quality, pu);
       // activity: the sample's evidence, or in Mutect2 mode the tumor's alone
       // (Mutect2's activity profile is a tumor-evidence test; over tumor +
@@ -620,6 +790,7 @@ CallerStats call_intervals(const Reference& ref, const std::vector<std::string>&
         clusters.emplace_back(first, last);
       }
       st.pileup_seconds += (now_us() - tp) / 1e6;
+      st.faults[1] += thread_faults() - f1;
       if (!grow_l && !grow_r) break;
       if (grow_l) ext_l *= 2;
       if (grow_r) ext_r *= 2;
@@ -629,6 +800,7 @@ CallerStats call_intervals(const Reference& ref, const std::vector<std::string>&
     for (int s = 0; s < 2; ++s)
       for (const Read& rd : reads[s]) max_span[s] = std::max<int64_t>(max_span[s], rd.end - rd.pos);
     const uint64_t tr = now_us();
+    const int64_t fr = thread_faults();
     const double in_flush0 = st.phmm_seconds + st.genotype_seconds;
     for (const auto& [first, last] : clusters) {
       for (int64_t rb = std::max<int64_t>(0, first - opt.padding); rb < std::min<int64_t>(L, last + opt.padding + 1);
@@ -675,8 +847,9 @@ CallerStats call_intervals(const Reference& ref, const std::vector<std::string>&
             if (!clip_to_window(rd, g->beg, g->end, qs, qe) || qe - qs < 20) continue;
             std::vector<uint8_t> q(rd.qual.begin() + qs, rd.qual.begin() + qe);
             PreparedRead pr;
-            gatk_prepare_read(rd.seq.substr(qs, qe - qs), q, rd.bi.empty() ? "" : rd.bi.substr(qs, qe - qs),
-                              rd.bd.empty() ? "" : rd.bd.substr(qs, qe - qs), rd.mapq, pr,
+            gatk_prepare_read(std::string(rd.seq.substr(qs, qe - qs)), q,
+                              rd.bi.empty() ? std::string() : std::string(rd.bi.substr(qs, qe - qs)),
+                              rd.bd.empty() ? std::string() : std::string(rd.bd.substr(qs, qe - qs)), rd.mapq, pr,
                               opt.base_quality_threshold, (PcrIndelModel)opt.pcr_indel_model);
             g->reads[s].push_back(std::move(pr));
           }
@@ -690,34 +863,61 @@ CallerStats call_intervals(const Reference& ref, const std::vector<std::string>&
     }
     st.region_seconds += (now_us() - tr) / 1e6 - (st.phmm_seconds + st.genotype_seconds - in_flush0);
     flush();
+    st.faults[2] += thread_faults() - fr;
     if (opt.gvcf && !opt.somatic) {
       const uint64_t tv = now_us();
-      std::vector<const VcfRecord*> ic;
-      for (size_t i = c0; i < calls.size(); ++i) ic.push_back(&calls[i]);
-      emit_gvcf(seq, pu, own_beg, own_end, iv.chrom, ic, gout);
+      const int64_t fv = thread_faults();
+      emit_gvcf(pu, own_beg, own_end, ci, calls, c0, blocks, gout);
       st.output_seconds += (now_us() - tv) / 1e6;
+      st.faults[3] += thread_faults() - fv;
     }
   }
   flush();
   if (dump) std::fclose(dump);
   const uint64_t tw = now_us();
+  const int64_t fw = thread_faults();
   st.calls = (int64_t)calls.size();
-  std::vector<VcfRecord>& recs = (opt.gvcf && !opt.somatic) ? gout : calls;
   // (contig index, position) order, ties in emission order: keys computed once
   // per record (the contig lookup is a name scan), then one key sort
-  std::vector<std::pair<std::pair<int, int64_t>, uint32_t>> order(recs.size());
-  {
-    const std::string* last = nullptr;
-    int last_i = -1;
-    for (size_t i = 0; i < recs.size(); ++i) {
-      if (!last || recs[i].chrom != *last) last = &recs[i].chrom, last_i = ref.index(recs[i].chrom);
-      order[i] = {{last_i, recs[i].pos}, (uint32_t)i};
+  if (opt.gvcf && !opt.somatic) {
+    std::vector<std::pair<std::pair<int, int64_t>, uint32_t>> order(gout.size());
+    for (size_t i = 0; i < gout.size(); ++i) order[i] = {{gout[i].contig, gout[i].pos}, (uint32_t)i};
+    std::sort(order.begin(), order.end());
+    std::string text;
+    text.reserve(1u << 21);
+    for (const auto& o : order) {
+      const OutEntry& e = gout[o.second];
+      if (e.block >= 0) {
+        const GvcfBlock& k = blocks[e.block];
+        const Contig& c = ref.contigs[e.contig];
+        append_block_line(c.name, c.seq[k.b], k, text);
+      } else {
+        calls[e.call].append_line(text);
+      }
+      if (text.size() >= (1u << 20)) {
+        out.write_text(text);
+        text.clear();
+      }
     }
+    out.write_text(text);
+  } else {
+    std::vector<VcfRecord>& recs = calls;
+    std::vector<std::pair<std::pair<int, int64_t>, uint32_t>> order(recs.size());
+    {
+      const std::string* last = nullptr;
+      int last_i = -1;
+      for (size_t i = 0; i < recs.size(); ++i) {
+        if (!last || recs[i].chrom != *last) last = &recs[i].chrom, last_i = ref.index(recs[i].chrom);
+        order[i] = {{last_i, recs[i].pos}, (uint32_t)i};
+      }
+    }
+    std::sort(order.begin(), order.end());
+    for (const auto& o : order) out.write(recs[o.second]);
   }
-  std::sort(order.begin(), order.end());
-  for (const auto& o : order) out.write(recs[o.second]);
   st.output_seconds += (now_us() - tw) / 1e6;
+  st.faults[3] += thread_faults() - fw;
   st.seconds = (now_us() - t0) / 1e6;
+  st.cpu_seconds = thread_cpu() - cpu0;
   return st;
 }
 

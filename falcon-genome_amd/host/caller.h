@@ -47,13 +47,17 @@ struct CallerOptions {
 };
 
 struct CallerStats {
-  int64_t reads = 0, regions = 0, pairs = 0, cells = 0, calls = 0, device_passes = 0;
+  int64_t reads = 0, regions = 0, pairs = 0, cells = 0, calls = 0, device_passes = 0, decode_passes = 0;
   int64_t rescued = 0;  // pairs the fp64 rescue recomputed (fp32 sum < 1e-28)
   double seconds = 0, phmm_seconds = 0;
   // wall-time breakdown of `seconds`: BAM decode, pileup + active sites,
   // regions (candidates, haplotypes, read preparation), genotyping, GVCF
   // blocks + record sort + VCF write; phmm_seconds = the PairHMM calls
   double decode_seconds = 0, pileup_seconds = 0, region_seconds = 0, genotype_seconds = 0, output_seconds = 0;
+  // the calling thread's CPU seconds and minor page faults (decode, pileup,
+  // regions + PairHMM + genotyping, output): where host time goes
+  double cpu_seconds = 0;
+  int64_t faults[4] = {0, 0, 0, 0};
   // device time of the PairHMM calls (HIP events: schedule + forward + rescue) and of the fp64 rescue alone
   double phmm_device_seconds = 0, rescue_device_seconds = 0;
   void add(const CallerStats& o);

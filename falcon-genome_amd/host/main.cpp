@@ -4,6 +4,7 @@
 // src/worker-align.cpp:29-42), config keys (`conf`) and exit codes
 // (src/main.cpp:165-240: help 0, bad option 1/2, missing file 3, failed
 // stage 4, other error -1), plus `synth` for the synthetic C1/C4/C5 inputs.
+#include <sys/resource.h>
 #include <unistd.h>
 
 #include <cerrno>
@@ -173,11 +174,17 @@ void timeline(const char* what) {
     unsigned long long ticks = 0;
     for (int field = 3; p && *p && field <= 22; ++field) {
       p = std::strchr(p + 1, ' ');
-      if (p && field == 21) ticks = std::strtoull(p + 1, nullptr, 10);
+      if (p && field == 22) ticks = std::strtoull(p + 1, nullptr, 10);
     }
     start = (double)ticks / (double)sysconf(_SC_CLK_TCK);
   }
-  std::cerr << "[fcs-genome timeline] " << what << " " << (up - start) << " s" << std::endl;
+  struct rusage ru {};
+  getrusage(RUSAGE_SELF, &ru);
+  char line[256];
+  std::snprintf(line, sizeof line, "[fcs-genome timeline] %s %.2f s (user %.2f s, sys %.2f s, minor faults %ld, csw %ld/%ld)",
+                what, up - start, ru.ru_utime.tv_sec + ru.ru_utime.tv_usec / 1e6,
+                ru.ru_stime.tv_sec + ru.ru_stime.tv_usec / 1e6, ru.ru_minflt, ru.ru_nvcsw, ru.ru_nivcsw);
+  std::cerr << line << std::endl;
 }
 
 int htc_main(int argc, char** argv) {

@@ -106,6 +106,14 @@ void VcfWriter::write(const VcfRecord& r) {
   }
 }
 
+void VcfWriter::write_text(const std::string& lines) {
+  if (!impl_->buf.empty()) {
+    impl_->out.write(impl_->buf.data(), (std::streamsize)impl_->buf.size());
+    impl_->buf.clear();
+  }
+  impl_->out.write(lines.data(), (std::streamsize)lines.size());
+}
+
 void VcfWriter::close() {
   if (!impl_->out.is_open()) return;
   impl_->out.write(impl_->buf.data(), (std::streamsize)impl_->buf.size());

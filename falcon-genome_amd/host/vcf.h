@@ -39,6 +39,8 @@ class VcfWriter {
   VcfWriter(const std::string& path, const VcfHeader& h);
   ~VcfWriter();
   void write(const VcfRecord& r);
+  // whole, already formatted record lines
+  void write_text(const std::string& lines);
   void close();
 
  private:

@@ -8,8 +8,11 @@
  * supplementary marking, pairing, SAM fields) in a container without a GPU.
  * tests/test_align_host_cpu.py compiles it into a temporary directory and
  * puts that directory first on LD_LIBRARY_PATH of the fcs-genome child it
- * starts; the PairHMM entry points fail (FCS_ERR_DEVICE).  The GPU tests run
- * the same commands on the real library.
+ * starts; the PairHMM entry points fail (FCS_ERR_DEVICE), unless
+ * FCS_MOCK_PHMM=1 (2) — then every haplotype but the first (last) scores -10
+ * (placeholder likelihoods, no PairHMM at all), which lets a developer time the caller's
+ * host stages (decode, pileup, regions, GVCF output) on a CPU-only machine.
+ * The GPU tests run the same commands on the real library.
  */
 #include <stdlib.h>
 #include <string.h>
@@ -74,11 +77,17 @@ int fcs_bsw_global(const fcs_bsw_task* t, int32_t n, const fcs_bsw_params* p, in
 
 void fcs_phmm_opts_default(fcs_phmm_opts* o) { memset(o, 0, sizeof *o); }
 int fcs_phmm_compute_regions(const fcs_phmm_region* regions, int32_t n_regions, const fcs_phmm_opts* opts) {
-  (void)regions;
-  (void)n_regions;
   (void)opts;
-  g_err = "CPU mock of libfcship: no PairHMM";
-  return FCS_ERR_DEVICE;
+  const char* e = getenv("FCS_MOCK_PHMM");
+  if (!e || (strcmp(e, "1") != 0 && strcmp(e, "2") != 0)) {
+    g_err = "CPU mock of libfcship: no PairHMM";
+    return FCS_ERR_DEVICE;
+  }
+  for (int32_t k = 0; k < n_regions; ++k)
+    for (int32_t r = 0; r < regions[k].n_reads; ++r)
+      for (int32_t h = 0; h < regions[k].n_haps; ++h)
+        regions[k].out_log10[(int64_t)r * regions[k].n_haps + h] = h == (e[0] == '1' ? 0 : regions[k].n_haps - 1) ? -1.0 : -10.0;
+  return FCS_OK;
 }
 int fcs_phmm_last_rescued(int64_t* count) {
   *count = 0;

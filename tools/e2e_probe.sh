@@ -1,5 +1,6 @@
 #!/bin/bash
 # Wall-time probe of the e2e commands on a GPU box (stage lines from stderr).
+echo "cpu quota: $(cat /sys/fs/cgroup/cpu.max 2>/dev/null); THP: $(cat /sys/kernel/mm/transparent_hugepage/enabled 2>/dev/null); nproc $(nproc)"
 W=$(mktemp -d /tmp/e2e.XXXX)
 export FCS_TIMELINE=1 FCS_GPU_DEVICES=0 FCS_LOG_DIR=$W/log FCS_TEMP_DIR=$W FCS_GATK_NPROCS=${NPROCS:-16}
 MBP=${MBP:-4}
@@ -11,7 +12,11 @@ for i in 1 2; do
   grep -E "finishes|Start|phase|timeline" $W/htc$i.err; grep -E "^(real|user|sys)" $W/htc$i.time
 done
 sed -e 's/^/  | /' $W/htc2.err | head -60
-[ -n "${HTC_ONLY:-}" ] && { ls -la $W/h2.g.vcf* >&2; rm -rf $W; exit 0; }
+if [ -n "${HTC_ONLY:-}" ]; then
+  grep -h "htc\] shard" $W/log/*.log | head -4
+  grep -h "htc\] shard" $W/log/*.log | awk '{for(i=1;i<=NF;i++){if($i=="(decode"||$i=="decode"){d+=$(i+1)} if($i=="passes),"){p+=$(i-1)}}} END{print "decode thread-s", d, "decode passes", p, "shards", NR}'
+  ls -la $W/h2.g.vcf* >&2; rm -rf $W; exit 0
+fi
 t timeout 300 $B mutect2 -r $W/d/ref.fasta -t $W/d/tumor.bam -n $W/d/sample.bam -o $W/m2.vcf 2> $W/m2.err
 sed -e 's/^/  | /' $W/m2.err | head -60
 t timeout 300 $B htc -r $W/d/ref.fasta -i $W/d/sample.bam -o $W/hv.vcf -v 2> $W/htcv.err
