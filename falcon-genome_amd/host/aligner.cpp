@@ -1417,9 +1417,12 @@ AlignStats align_fastq(const AlignJob& job, const std::vector<int>& devices, std
     throw failedCommand("[E::fcs-genome align] no GPU visible (gpu.devices); the GPU path has no CPU fallback");
   // bwa.gpu_slots host threads per device: a chunk's seeding and host protocol
   // work overlap other chunks' GPU rounds (one slot left the GPU idle between
-  // its rounds: 4.6 s vs 2.6 s of alignment wall for 795K reads, gpurun_out/r3y)
+  // its rounds: 4.6 s vs 2.6 s of alignment wall for 795K reads, gpurun_out/r3y).
+  // Seeding is host work (~16 us per read), so by default (0) every host
+  // thread gets a slot: hardware threads / devices, at least 4.
   std::vector<int> gpus;
-  const int per = std::max(1, conf().get_int("bwa.gpu_slots"));
+  int per = conf().get_int("bwa.gpu_slots");
+  if (per <= 0) per = std::max<int>(4, (int)(host_cpus() / devices.size()));
   for (int k = 0; k < per; ++k) gpus.insert(gpus.end(), devices.begin(), devices.end());
   const uint64_t t_start = now_us();
   const auto ref_p = load_reference_cached(job.ref_path);
@@ -1431,7 +1434,7 @@ AlignStats align_fastq(const AlignJob& job, const std::vector<int>& devices, std
   {
     // bwa.nt host threads for the whole job, shared by the device slots
     const int nt = conf().get_int("bwa.nt");
-    const int all = nt > 0 ? nt : (int)std::min(16u, std::max(1u, std::thread::hardware_concurrency()));
+    const int all = nt > 0 ? nt : (int)host_cpus();
     base.threads = std::max(1, all / nslot);
   }
   const uint64_t t_ref = now_us();

@@ -157,8 +157,7 @@ namespace {
 class HostPool {
  public:
   HostPool() {
-    // a GPU box's CPU share is 16 threads whatever hardware_concurrency says
-    n_ = std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
+    n_ = host_cpus();
     for (unsigned k = 0; k < n_; ++k) threads_.emplace_back([this] { loop(); });
   }
   ~HostPool() {

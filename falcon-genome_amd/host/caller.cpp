@@ -13,6 +13,7 @@
 #include <memory>
 #include <string_view>
 #include <tuple>
+#include <type_traits>
 
 #include "bam.h"
 #include "bam_input.h"
@@ -68,9 +69,10 @@ struct Read {
   int mapq = 0;
   std::string_view bi, bd;
 };
+static_assert(std::is_trivially_copyable_v<Read>, "Read lives in a HugeVec");
 
 void load_reads_one(const std::string& bam, const std::string& chrom, int64_t beg, int64_t end,
-                    const CallerOptions& opt, HugeSlab& slab, std::vector<Read>& out) {
+                    const CallerOptions& opt, HugeSlab& slab, HugeVec<Read>& out) {
   BamReader rd(bam);
   const int tid = rd.header().ref_index(chrom);
   if (tid < 0) return;
@@ -139,7 +141,7 @@ void load_reads_one(const std::string& bam, const std::string& chrom, int64_t be
 // Reads of the window from every part of the sample, in coordinate order
 // (parts of a `--disable-merge` alignment are each sorted).
 void load_reads(const std::vector<std::string>& bams, const std::string& chrom, int64_t beg, int64_t end,
-                const CallerOptions& opt, HugeSlab& slab, std::vector<Read>& out) {
+                const CallerOptions& opt, HugeSlab& slab, HugeVec<Read>& out) {
   for (const std::string& b : bams) load_reads_one(b, chrom, beg, end, opt, slab, out);
   if (bams.size() > 1)
     std::stable_sort(out.begin(), out.end(), [](const Read& a, const Read& b) { return a.pos < b.pos; });
@@ -190,7 +192,7 @@ inline uint64_t snv_key(int64_t pos, char ref, char alt) {
 }
 
 // Walks every read's CIGAR once: depth, mismatch/indel events and allele support.
-void build_pileup(const std::string& ref, const std::vector<Read>& reads, int min_bq, Pileup& pu) {
+void build_pileup(const std::string& ref, const HugeVec<Read>& reads, int min_bq, Pileup& pu) {
   const int64_t n = (int64_t)pu.depth.size();
   const int64_t wb = pu.wb, we = pu.wb + n;
   auto in = [&](int64_t p) { return p >= wb && p < we; };
@@ -737,7 +739,7 @@ CallerStats call_intervals(const Reference& ref, const std::vector<std::string>&
     // regions, their candidates and reads, and so the likelihoods and calls,
     // do not depend on where gatk.ncontigs put the shard boundaries.
     int64_t ext_l = opt.max_region, ext_r = opt.max_region, wb = 0, we = 0;
-    std::vector<Read> reads[2];
+    HugeVec<Read> reads[2];
     HugeSlab slab;  // the reads' bytes
     Pileup pu;
     std::vector<std::pair<int64_t, int64_t>> clusters;  // [first site, last site] overlapping the own range
@@ -834,7 +836,7 @@ CallerStats call_intervals(const Reference& ref, const std::vector<std::string>&
           // reads are in position order: start at the first that can reach beg
           // (pos >= beg - the window's longest reference span), stop at end
           std::vector<const Read*> ov;
-          const std::vector<Read>& rs = reads[s];
+          const HugeVec<Read>& rs = reads[s];
           auto it = std::lower_bound(rs.begin(), rs.end(), g->beg - max_span[s],
                                      [](const Read& rd, int64_t x) { return rd.pos < x; });
           for (; it != rs.end() && it->pos < g->end; ++it)

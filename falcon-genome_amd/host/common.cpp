@@ -1,6 +1,7 @@
 #include "common.h"
 
 #include <dirent.h>
+#include <sched.h>
 #include <sys/stat.h>
 #include <sys/statvfs.h>
 #include <unistd.h>
@@ -9,9 +10,11 @@
 #include <atomic>
 #include <cerrno>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <fstream>
 #include <sstream>
+#include <thread>
 
 namespace fcsg {
 
@@ -106,6 +109,31 @@ void write_file(const std::string& p, const std::string& data) {
   std::ofstream out(p, std::ios::binary);
   if (!out) throw fileNotFound(p + " (cannot write)");
   out << data;
+}
+
+unsigned host_cpus() {
+  static const unsigned n = [] {
+    unsigned c = std::max(1u, std::thread::hardware_concurrency());
+    cpu_set_t set;
+    if (sched_getaffinity(0, sizeof set, &set) == 0) c = std::min(c, (unsigned)std::max(1, CPU_COUNT(&set)));
+    // cgroup v2 "quota period" (or "max period"); v1 cfs_quota_us / cfs_period_us
+    long long quota = -1, period = 0;
+    if (std::FILE* f = std::fopen("/sys/fs/cgroup/cpu.max", "r")) {
+      char q[32] = {0};
+      if (std::fscanf(f, "%31s %lld", q, &period) == 2 && std::strcmp(q, "max") != 0) quota = std::atoll(q);
+      std::fclose(f);
+    } else if (std::FILE* g = std::fopen("/sys/fs/cgroup/cpu/cpu.cfs_quota_us", "r")) {
+      if (std::fscanf(g, "%lld", &quota) != 1) quota = -1;
+      std::fclose(g);
+      if (std::FILE* h = std::fopen("/sys/fs/cgroup/cpu/cpu.cfs_period_us", "r")) {
+        if (std::fscanf(h, "%lld", &period) != 1) period = 0;
+        std::fclose(h);
+      }
+    }
+    if (quota > 0 && period > 0) c = std::min(c, (unsigned)std::max(1LL, (quota + period - 1) / period));
+    return c;
+  }();
+  return n;
 }
 
 }  // namespace fcsg

@@ -93,6 +93,11 @@ class formatError : public std::runtime_error {
   explicit formatError(const std::string& what) : std::runtime_error("[E::fcsg] " + what) {}
 };
 
+// CPUs this process may use: the hardware threads, narrowed by the affinity
+// mask and by a cgroup CPU quota (a GPU box grants 16 of its many cores;
+// hardware_concurrency alone reports them all).
+unsigned host_cpus();
+
 inline uint64_t now_us() {
   return (uint64_t)std::chrono::duration_cast<std::chrono::microseconds>(
              std::chrono::steady_clock::now().time_since_epoch())

@@ -25,7 +25,7 @@ void Config::declare(const std::string& key, const std::string& def, const std::
 
 void Config::init(const std::string& root_dir) {
   kv_.clear();
-  const unsigned ncpu = std::max(1u, std::thread::hardware_concurrency());
+  const unsigned ncpu = host_cpus();
   // common (config.cpp:274-296)
   declare("temp_dir", "/tmp", "temp dir for fast access");
   declare("log_dir", "./log", "log dir");
@@ -36,7 +36,7 @@ void Config::init(const std::string& root_dir) {
   declare("bwa.nt", "-1", "host threads of the aligner (-1: all)");
   declare("bwa.num_buckets", "1024", "number of BAM buckets");
   declare("bwa.chunk_size", "100000", "reads per SW batch handed to the GPU");
-  declare("bwa.gpu_slots", "4", "aligner host threads (chunks in flight) per GPU");
+  declare("bwa.gpu_slots", "0", "aligner host threads (chunks in flight) per GPU; 0: host threads / GPUs, at least 4");
   declare("gatk.intv.path", "", "default path to existing contig intervals");
   declare("gatk.ncontigs", "32", "contig partition num in htc/mutect2");
   declare("gatk.nprocs", std::to_string(std::min(32u, ncpu)), "default concurrent shard tasks");

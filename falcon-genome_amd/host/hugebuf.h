@@ -78,6 +78,38 @@ class HugeArray {
   size_t n_ = 0;
 };
 
+// A growable array of trivially copyable T on a HugeBuf (the subset of
+// std::vector the caller uses); growth doubles and copies.
+template <typename T>
+class HugeVec {
+ public:
+  T* begin() { return data(); }
+  T* end() { return data() + n_; }
+  const T* begin() const { return data(); }
+  const T* end() const { return data() + n_; }
+  T* data() { return reinterpret_cast<T*>(buf_.data()); }
+  const T* data() const { return reinterpret_cast<const T*>(buf_.data()); }
+  size_t size() const { return n_; }
+  bool empty() const { return n_ == 0; }
+  T& operator[](size_t i) { return data()[i]; }
+  const T& operator[](size_t i) const { return data()[i]; }
+  void clear() { n_ = 0; }
+  void reserve(size_t cap) {
+    if (cap * sizeof(T) <= buf_.capacity()) return;
+    HugeBuf nb(cap * sizeof(T));
+    if (n_) std::memcpy(nb.data(), buf_.data(), n_ * sizeof(T));
+    buf_ = std::move(nb);
+  }
+  T& emplace_back() {
+    if ((n_ + 1) * sizeof(T) > buf_.capacity()) reserve(std::max<size_t>(2 * n_, 1024));
+    return *new (data() + n_++) T();
+  }
+
+ private:
+  HugeBuf buf_;
+  size_t n_ = 0;
+};
+
 // Bump allocator over a list of HugeBuf chunks; everything is freed together.
 class HugeSlab {
  public:

@@ -4,6 +4,7 @@
 // src/worker-align.cpp:29-42), config keys (`conf`) and exit codes
 // (src/main.cpp:165-240: help 0, bad option 1/2, missing file 3, failed
 // stage 4, other error -1), plus `synth` for the synthetic C1/C4/C5 inputs.
+#include <malloc.h>
 #include <sys/resource.h>
 #include <unistd.h>
 
@@ -540,6 +541,12 @@ int main(int argc, char** argv) {
     root = k == std::string::npos ? "." : self.substr(0, k) + "/..";
   }
   timeline("main");
+  // Shard threads allocate and free large blocks in batches (PairHMM region
+  // batches, per-window vectors): keep freed memory in the allocator instead
+  // of returning it (munmap / heap trim) only to fault it back in — with 32
+  // threads in one process those faults serialize on the memory-map lock.
+  mallopt(M_MMAP_THRESHOLD, 256 << 20);
+  mallopt(M_TRIM_THRESHOLD, 1 << 30);
   start_signal_thread();
   try {
     conf().init(root);

@@ -88,7 +88,7 @@ Rng chunk_rng(uint64_t seed, uint64_t stream, int64_t chunk) {
   return Rng(seed, stream ^ ((uint64_t)(chunk + 1) << 32));
 }
 
-int synth_threads() { return (int)std::min(16u, std::max(1u, std::thread::hardware_concurrency())); }
+int synth_threads() { return (int)host_cpus(); }
 
 // parallel_for whose bodies may be interrupted: the workers stop at the next
 // item and the caller raises interruptedError (an exception must not leave a

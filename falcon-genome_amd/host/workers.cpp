@@ -156,13 +156,16 @@ int Mutect2Worker::run(TaskContext& ctx) {
   if (ctx.log)
     std::fprintf(ctx.log,
                  "[fcs-genome mutect2] shard %d gpu %d: %lld reads, %lld regions, %lld pairs, %lld cells, %lld rescued, "
-                 "%lld calls, %.3f s (PairHMM %.3f s, device %.4f s, rescue %.4f s, %lld device passes; decode %.3f s, pileup %.3f s, "
-                 "regions %.3f s, genotype %.3f s, output %.3f s)\n",
+                 "%lld calls, %.3f s (PairHMM %.3f s, device %.4f s, rescue %.4f s, %lld device passes; decode %.3f s "
+                 "(%lld passes), pileup %.3f s, regions %.3f s, genotype %.3f s, output %.3f s; thread cpu %.3f s, "
+                 "minor faults %lld/%lld/%lld/%lld)\n",
                  contig_, ctx.gpu, (long long)stats_.reads, (long long)stats_.regions, (long long)stats_.pairs,
                  (long long)stats_.cells, (long long)stats_.rescued, (long long)stats_.calls, stats_.seconds,
                  stats_.phmm_seconds, stats_.phmm_device_seconds, stats_.rescue_device_seconds,
-                 (long long)stats_.device_passes, stats_.decode_seconds, stats_.pileup_seconds,
-                 stats_.region_seconds, stats_.genotype_seconds, stats_.output_seconds);
+                 (long long)stats_.device_passes, stats_.decode_seconds, (long long)stats_.decode_passes, stats_.pileup_seconds,
+                 stats_.region_seconds, stats_.genotype_seconds, stats_.output_seconds, stats_.cpu_seconds,
+                 (long long)stats_.faults[0], (long long)stats_.faults[1], (long long)stats_.faults[2],
+                 (long long)stats_.faults[3]);
   return 0;
 }
 

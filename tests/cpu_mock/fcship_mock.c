@@ -10,7 +10,8 @@
  * puts that directory first on LD_LIBRARY_PATH of the fcs-genome child it
  * starts; the PairHMM entry points fail (FCS_ERR_DEVICE), unless
  * FCS_MOCK_PHMM=1 (2) — then every haplotype but the first (last) scores -10
- * (placeholder likelihoods, no PairHMM at all), which lets a developer time the caller's
+ * (placeholder likelihoods, no PairHMM at all), or FCS_MOCK_PHMM=3 — then
+ * the oracle's PairHMM (oracle/pairhmm_oracle.c, slow) computes them, which lets a developer time the caller's
  * host stages (decode, pileup, regions, GVCF output) on a CPU-only machine.
  * The GPU tests run the same commands on the real library.
  */
@@ -22,6 +23,8 @@
 int oracle_ksw_extend2(int qlen, const uint8_t* query, int tlen, const uint8_t* target, int m, const int8_t* mat,
                        int o_del, int e_del, int o_ins, int e_ins, int w, int end_bonus, int zdrop, int h0, int* qle_,
                        int* tle_, int* gtle_, int* gscore_, int* max_off_, int64_t* cells);
+double oracle_phmm_log10(const uint8_t* rb, const uint8_t* bq, const uint8_t* iq, const uint8_t* dq, const uint8_t* gq,
+                         int R, const uint8_t* hb, int H, int* used_double);
 int oracle_ksw_global2(int qlen, const uint8_t* query, int tlen, const uint8_t* target, int m, const int8_t* mat,
                        int o_del, int e_del, int o_ins, int e_ins, int w, int* n_cigar, uint32_t* cigar_out,
                        int cigar_cap);
@@ -79,9 +82,20 @@ void fcs_phmm_opts_default(fcs_phmm_opts* o) { memset(o, 0, sizeof *o); }
 int fcs_phmm_compute_regions(const fcs_phmm_region* regions, int32_t n_regions, const fcs_phmm_opts* opts) {
   (void)opts;
   const char* e = getenv("FCS_MOCK_PHMM");
-  if (!e || (strcmp(e, "1") != 0 && strcmp(e, "2") != 0)) {
+  if (!e || (strcmp(e, "1") != 0 && strcmp(e, "2") != 0 && strcmp(e, "3") != 0)) {
     g_err = "CPU mock of libfcship: no PairHMM";
     return FCS_ERR_DEVICE;
+  }
+  if (e[0] == '3') {
+    for (int32_t k = 0; k < n_regions; ++k)
+      for (int32_t r = 0; r < regions[k].n_reads; ++r)
+        for (int32_t h = 0; h < regions[k].n_haps; ++h) {
+          const fcs_phmm_read* x = &regions[k].reads[r];
+          const fcs_phmm_hap* y = &regions[k].haps[h];
+          regions[k].out_log10[(int64_t)r * regions[k].n_haps + h] = oracle_phmm_log10(
+              x->bases, x->base_q, x->ins_q, x->del_q, x->gcp, x->len, y->bases, y->len, NULL);
+        }
+    return FCS_OK;
   }
   for (int32_t k = 0; k < n_regions; ++k)
     for (int32_t r = 0; r < regions[k].n_reads; ++r)
