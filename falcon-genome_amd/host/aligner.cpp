@@ -1566,7 +1566,9 @@ AlignStats align_fastq(const AlignJob& job, const std::vector<int>& devices, std
   if (!job.disable_merge) {
     BamWriter w(job.output, h);
     w.index_on_close();
-    for (const auto& o : order) w.write(recs[o.second]);
+    std::vector<const BamRecord*> sorted(order.size());
+    for (size_t i = 0; i < order.size(); ++i) sorted[i] = &recs[order[i].second];
+    w.write_all(sorted);
     w.close();
   } else {
     // bwa-flow --merge_bams=0 (reference BWAWorker.cpp:140-147, worker-align.cpp:186-195):
@@ -1606,7 +1608,7 @@ AlignStats align_fastq(const AlignJob& job, const std::vector<int>& devices, std
       const std::string bam = get_contig_fname(job.output, k, "bam");
       BamWriter w(bam, h);
       w.index_on_close();
-      for (const BamRecord* r : per[k]) w.write(*r);
+      w.write_all(per[k]);
       w.close();
       std::ofstream bed(get_contig_fname(job.output, k, "bed"));
       for (const Interval& iv : buckets[k]) bed << iv.chrom << '\t' << iv.lb - 1 << '\t' << iv.ub << '\n';

@@ -3,9 +3,12 @@
 #include <algorithm>
 #include <cctype>
 #include <cstring>
+#include <deque>
+#include <future>
 #include <map>
 #include <sstream>
 
+#include "bgzf.h"
 #include "common.h"
 
 namespace fcsg {
@@ -286,6 +289,52 @@ BamWriter::BamWriter(const std::string& path, const BamHeader& h, int level)
 void BamWriter::write(const BamRecord& r) {
   encode_bam_record(r, rec_);
   write_encoded(r, rec_);
+}
+
+void BamWriter::write_all(const std::vector<const BamRecord*>& recs) {
+  // pieces of records encoded on the host pool, written in order; the
+  // uncompressed stream (and so the file and its index) is write()'s
+  struct Piece {
+    std::string bytes;                // [block_size][body] per record
+    std::vector<int64_t> meta;        // per record: ref_id, pos, end, encoded size
+  };
+  constexpr size_t kPiece = 8192;
+  const size_t npieces = (recs.size() + kPiece - 1) / kPiece;
+  const size_t window = 4 * (size_t)host_pool_size();
+  std::deque<std::future<Piece>> inflight;
+  size_t next = 0;
+  auto submit = [&] {
+    const size_t a = next * kPiece, b = std::min(recs.size(), a + kPiece);
+    ++next;
+    inflight.push_back(host_pool_async([&recs, a, b, index = index_] {
+      Piece pc;
+      std::string body;
+      if (index) pc.meta.reserve(4 * (b - a));
+      for (size_t i = a; i < b; ++i) {
+        const BamRecord& r = *recs[i];
+        encode_bam_record(r, body);
+        const int32_t bs = (int32_t)body.size();
+        pc.bytes.append(reinterpret_cast<const char*>(&bs), 4);
+        pc.bytes += body;
+        if (index) pc.meta.insert(pc.meta.end(), {r.ref_id, r.pos, r.ref_id >= 0 ? r.end() : 0, 4 + (int64_t)bs});
+      }
+      return pc;
+    }));
+  };
+  while (next < npieces && inflight.size() < window) submit();
+  while (!inflight.empty()) {
+    const Piece pc = inflight.front().get();
+    inflight.pop_front();
+    if (next < npieces) submit();
+    uint64_t u = bgzf_.upos();
+    bgzf_.write(pc.bytes);
+    if (index_)
+      for (size_t k = 0; k < pc.meta.size(); k += 4) {
+        const uint64_t u1 = u + (uint64_t)pc.meta[k + 3];
+        spans_.push_back({(int32_t)pc.meta[k], pc.meta[k + 1], pc.meta[k + 2], u, u1});
+        u = u1;
+      }
+  }
 }
 
 void BamWriter::write_encoded(const BamRecord& r, const std::string& body) {

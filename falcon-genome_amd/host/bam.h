@@ -64,6 +64,8 @@ class BamWriter {
   // write(r) with the record body already encoded by encode_bam_record(r, body)
   // (callers encode many records on worker threads and write them in order).
   void write_encoded(const BamRecord& r, const std::string& body);
+  // write() of every record in order, the encoding spread over the host pool.
+  void write_all(const std::vector<const BamRecord*>& recs);
   // Also write <path>.bai at close(), from the records as they are written
   // (coordinate order required): the index bam_index_build would compute,
   // without reading the file back.

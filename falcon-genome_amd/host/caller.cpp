@@ -160,7 +160,7 @@ struct Pileup {
   // allele events of the reads — SNVs as packed (pos, ref, alt) keys, indels
   // as Alleles — then (finish_support) sorted and counted: the support of
   // each distinct allele in (pos, ref, alt) order
-  std::vector<uint64_t> snv_events;
+  HugeVec<uint64_t> snv_events;
   std::vector<Allele> indel_events;
   std::vector<std::pair<Allele, int>> support;
   // GVCF reference model: per position, sum over bases of log10 P(base | 0/0,
@@ -218,7 +218,7 @@ void build_pileup(const std::string& ref, const HugeVec<Read>& reads, int min_bq
             const bool nonref = b != r && r != 'N' && b != 'N';
             if (nonref) {
               ++events[p - wb];
-              pu.snv_events.push_back(snv_key(p, r, b));
+              pu.snv_events.emplace_back() = snv_key(p, r, b);
             }
             if (gl) {
               const double* t = M.t[std::min<int>(bq, 93)];
@@ -255,7 +255,8 @@ void build_pileup(const std::string& ref, const HugeVec<Read>& reads, int min_bq
   }
 }
 
-// The distinct alleles of the pileup's events with their read counts, in
+// The distinct alleles of the pileup's events seen in at least two reads
+// (the least support a candidate allele needs), with their read counts, in
 // (pos, ref, alt) order: the SNV keys sort as integers (a one-base REF and
 // ALT compare as their bytes), the indels as Alleles, and the two runs merge
 // (an indel never equals an SNV: its REF or ALT is longer than one base).
@@ -265,6 +266,14 @@ void finish_support(Pileup& pu) {
   pu.support.clear();
   size_t i = 0, j = 0;
   const size_t ns = pu.snv_events.size(), ni = pu.indel_events.size();
+  auto next_snv = [&] {  // skip SNVs seen once
+    while (i < ns && (i + 1 >= ns || pu.snv_events[i + 1] != pu.snv_events[i])) ++i;
+  };
+  auto next_indel = [&] {
+    while (j < ni && (j + 1 >= ni || pu.indel_events[j] < pu.indel_events[j + 1])) ++j;
+  };
+  next_snv();
+  next_indel();
   while (i < ns || j < ni) {
     if (i < ns) {
       const uint64_t k = pu.snv_events[i];
@@ -274,6 +283,7 @@ void finish_support(Pileup& pu) {
         while (e < ns && pu.snv_events[e] == k) ++e;
         pu.support.emplace_back(std::move(a), (int)(e - i));
         i = e;
+        next_snv();
         continue;
       }
     }
@@ -282,8 +292,9 @@ void finish_support(Pileup& pu) {
     while (e < ni && !(a < pu.indel_events[e])) ++e;
     pu.support.emplace_back(std::move(a), (int)(e - j));
     j = e;
+    next_indel();
   }
-  std::vector<uint64_t>().swap(pu.snv_events);
+  pu.snv_events = HugeVec<uint64_t>();
   std::vector<Allele>().swap(pu.indel_events);
 }
 
@@ -568,7 +579,7 @@ struct OutEntry {
 };
 
 void emit_gvcf(const Pileup& pu, int64_t beg, int64_t end, int contig, const std::vector<VcfRecord>& calls,
-               size_t c0, std::vector<GvcfBlock>& blocks, std::vector<OutEntry>& out) {
+               size_t c0, HugeVec<GvcfBlock>& blocks, HugeVec<OutEntry>& out) {
   std::vector<size_t> ic;  // this interval's calls in POS order (stable)
   for (size_t i = c0; i < calls.size(); ++i) ic.push_back(i);
   std::stable_sort(ic.begin(), ic.end(), [&](size_t a, size_t b) { return calls[a].pos < calls[b].pos; });
@@ -581,8 +592,8 @@ void emit_gvcf(const Pileup& pu, int64_t beg, int64_t end, int contig, const std
   auto flush = [&] {
     if (blk.b < 0) return;
     std::nth_element(dps.begin(), dps.begin() + dps.size() / 2, dps.end());
-    out.push_back({contig, (int32_t)blocks.size(), -1, blk.b + 1});
-    blocks.push_back({blk.b, blk.e, dps[dps.size() / 2], blk.gq, blk.mindp, {blk.pl[0], blk.pl[1], blk.pl[2]}});
+    out.emplace_back() = {contig, (int32_t)blocks.size(), -1, blk.b + 1};
+    blocks.emplace_back() = {blk.b, blk.e, dps[dps.size() / 2], blk.gq, blk.mindp, {blk.pl[0], blk.pl[1], blk.pl[2]}};
     dps.clear();
     blk = Block();
   };
@@ -592,7 +603,7 @@ void emit_gvcf(const Pileup& pu, int64_t beg, int64_t end, int contig, const std
     while (ci < ic.size() && calls[ic[ci]].pos - 1 <= p) {
       flush();
       const VcfRecord& c = calls[ic[ci]];
-      out.push_back({contig, -1, (int64_t)ic[ci], c.pos});
+      out.emplace_back() = {contig, -1, (int64_t)ic[ci], c.pos};
       covered = std::max<int64_t>(covered, c.pos - 1 + (int64_t)c.ref.size());
       ++ci;
     }
@@ -619,7 +630,7 @@ void emit_gvcf(const Pileup& pu, int64_t beg, int64_t end, int contig, const std
     dps.push_back(dp);
   }
   flush();
-  for (; ci < ic.size(); ++ci) out.push_back({contig, -1, (int64_t)ic[ci], calls[ic[ci]].pos});
+  for (; ci < ic.size(); ++ci) out.emplace_back() = {contig, -1, (int64_t)ic[ci], calls[ic[ci]].pos};
 }
 
 // One GVCF block line, as VcfRecord::append_line writes the record
@@ -702,8 +713,8 @@ CallerStats call_intervals(const Reference& ref, const std::vector<std::string>&
   const double cpu0 = thread_cpu();
   std::FILE* dump = opt.dump_path.empty() ? nullptr : std::fopen(opt.dump_path.c_str(), "ab");
   std::vector<VcfRecord> calls;
-  std::vector<GvcfBlock> blocks;  // GVCF mode: reference blocks and the output sequence
-  std::vector<OutEntry> gout;
+  HugeVec<GvcfBlock> blocks;  // GVCF mode: reference blocks and the output sequence
+  HugeVec<OutEntry> gout;
   const std::vector<Interval>& intervals = intervals_in;
   std::vector<std::unique_ptr<Region>> pending;
   std::vector<std::tuple<int64_t, int64_t, std::string>> own;  // per pending region: owned range + chrom
@@ -882,8 +893,9 @@ CallerStats call_intervals(const Reference& ref, const std::vector<std::string>&
   // (contig index, position) order, ties in emission order: keys computed once
   // per record (the contig lookup is a name scan), then one key sort
   if (opt.gvcf && !opt.somatic) {
-    std::vector<std::pair<std::pair<int, int64_t>, uint32_t>> order(gout.size());
-    for (size_t i = 0; i < gout.size(); ++i) order[i] = {{gout[i].contig, gout[i].pos}, (uint32_t)i};
+    HugeVec<std::pair<std::pair<int, int64_t>, uint32_t>> order;
+    order.reserve(gout.size());
+    for (size_t i = 0; i < gout.size(); ++i) order.emplace_back() = {{gout[i].contig, gout[i].pos}, (uint32_t)i};
     std::sort(order.begin(), order.end());
     std::string text;
     text.reserve(1u << 21);
