@@ -225,8 +225,11 @@ def bench_e2e(args, rank, local):
     import tempfile
     exe = os.path.join(ROOT, "falcon-genome_amd", "bin", "fcs-genome")
     work = tempfile.mkdtemp(prefix=f"fcs-e2e-{rank}-")
+    # the ranks of one node share its CPUs: each command's host threads (VCF /
+    # BAM codec pool, aligner slots) get this rank's share of the CPU quota
+    per_rank = max(2, host_cpu_quota() // max(1, int(os.environ.get("LOCAL_WORLD_SIZE", "1"))))
     env = dict(os.environ, FCS_GPU_DEVICES=str(local), FCS_LOG_DIR=os.path.join(work, "log"),
-               FCS_TEMP_DIR=work, FCS_GATK_NPROCS="16")
+               FCS_TEMP_DIR=work, FCS_GATK_NPROCS="16", FCS_HOST_THREADS=str(per_rank))
     try:
         L = int(args.e2e_mbp * 1e6)
         t0 = time.perf_counter()
@@ -334,6 +337,19 @@ def bench_e2e(args, rank, local):
         return out
     finally:
         shutil.rmtree(work, ignore_errors=True)
+
+
+def host_cpu_quota():
+    """CPUs this process may use: the affinity mask narrowed by a cgroup CPU
+    quota (as fcs-genome's host_cpus())."""
+    n = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    try:
+        q, period = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max" and int(period) > 0:
+            n = min(n, max(1, -(-int(q) // int(period))))
+    except (OSError, ValueError):
+        pass
+    return n
 
 
 def cpu_threads():

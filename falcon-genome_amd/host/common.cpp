@@ -113,6 +113,8 @@ void write_file(const std::string& p, const std::string& data) {
 
 unsigned host_cpus() {
   static const unsigned n = [] {
+    // FCS_HOST_THREADS: an explicit share (several GPU ranks on one node)
+    if (const char* e = std::getenv("FCS_HOST_THREADS"); e && std::atoi(e) > 0) return (unsigned)std::atoi(e);
     unsigned c = std::max(1u, std::thread::hardware_concurrency());
     cpu_set_t set;
     if (sched_getaffinity(0, sizeof set, &set) == 0) c = std::min(c, (unsigned)std::max(1, CPU_COUNT(&set)));

@@ -95,7 +95,8 @@ class formatError : public std::runtime_error {
 
 // CPUs this process may use: the hardware threads, narrowed by the affinity
 // mask and by a cgroup CPU quota (a GPU box grants 16 of its many cores;
-// hardware_concurrency alone reports them all).
+// hardware_concurrency alone reports them all).  FCS_HOST_THREADS > 0 sets it
+// (ranks sharing a node each take their share).
 unsigned host_cpus();
 
 inline uint64_t now_us() {
