@@ -589,5 +589,6 @@ int main(int argc, char** argv) {
     std::cerr << "[fcs-genome] ERROR: Encountered an error: " << e.what() << std::endl;
     ret = -1;
   }
+  timeline("exit");
   return ret;
 }
