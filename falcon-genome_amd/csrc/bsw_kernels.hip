@@ -273,18 +273,68 @@ __device__ __forceinline__ uint32_t* glane_zrow0(uint8_t* zbuf, const int64_t* z
   return reinterpret_cast<uint32_t*>(((uintptr_t)(zbuf + zoff[task]) + 3) & ~(uintptr_t)3);
 }
 
+// FCS_GLANE_ARITH (default): the row's direction bits and the masked row's
+// band selects as sign-bit arithmetic and v_bitop3_b32 selects (full rate)
+// instead of compares feeding v_cndmask (the compiler's VOP2 form costs ~7
+// extra cycles each in a mix, gfx950_sq_counters) and per-cell branches.
+// Every score stays within +-2^30 + 2^10, so the differences never overflow:
+// (uint32)(a - b) >> 31 is exactly a < b.
+#ifndef FCS_GLANE_ARITH
+#define FCS_GLANE_ARITH 1
+#endif
+
+__device__ __forceinline__ int gsel(int mask, int a, int b) {  // mask ? a : b, mask all-ones or zero
+  int r;
+  asm("v_bitop3_b32 %0, %1, %2, %3 bitop3:0xe4" : "=v"(r) : "v"(a), "v"(b), "v"(mask));  // as phmm's sel_v
+  return r;
+}
+
 template <int NB, bool CIG, bool MASKED>
 __device__ __forceinline__ void glane_row(int (&Hd)[NB], int (&Ed)[NB + 1], const uint32_t (&Qb)[(NB + 4) / 4],
                                           uint32_t (&nib)[(NB + 7) / 8], const int rowpack, const int lo,
                                           const int hi, const int hb, const int oe_del, const int oe_ins,
                                           const int e_del, const int e_ins, int& h1) {
   int f = kMinusInf;
+#if FCS_GLANE_ARITH
+  const int minf = kMinusInf;
+#endif
 #pragma unroll
   for (int k = 0; k < NB; ++k) {
     const int qoff = (int)((Qb[k >> 2] >> (8 * (k & 3))) & 0xFFu);
     const int s = __builtin_amdgcn_sbfe(rowpack, qoff, 5);
     const int m = Hd[k] + s;
     int e = Ed[k + 1];
+#if FCS_GLANE_ARITH
+    uint32_t d = 0;
+    if constexpr (CIG) d = (uint32_t)(m - e) >> 31;  // m < e: H from E
+    int h = max(m, e);
+    if constexpr (CIG) {
+      const int ltf = (h - f) >> 31;  // h < f: H from F
+      d = (uint32_t)gsel(ltf, 2, (int)d);
+    }
+    h = max(h, f);
+    int t = m - oe_del;
+    e -= e_del;
+    if constexpr (CIG) d |= ((uint32_t)(t - e) >> 31) << 2;  // e > t
+    e = max(e, t);
+    t = m - oe_ins;
+    int fn = f - e_ins;
+    if constexpr (CIG) d |= ((uint32_t)(t - fn) >> 31) << 3;  // fn > t
+    fn = max(fn, t);
+    if constexpr (MASKED) {
+      const int below = (k - lo) >> 31;                  // k < lo
+      const int vm = ~((k - lo) | (hi - 1 - k)) >> 31;   // lo <= k < hi
+      Hd[k] = gsel(vm, h, gsel(below, hb, Hd[k]));
+      Ed[k] = gsel(vm, e, minf);
+      f = gsel(vm, fn, minf);
+      h1 = gsel(vm, h, h1);
+    } else {
+      Hd[k] = h;
+      Ed[k] = e;
+      f = fn;
+      if (k == NB - 1) h1 = h;
+    }
+#else
     int h = m >= e ? m : e;
     int d = 0;
     if constexpr (CIG) d = m >= e ? 0 : 1;
@@ -310,6 +360,7 @@ __device__ __forceinline__ void glane_row(int (&Hd)[NB], int (&Ed)[NB + 1], cons
       f = fn;
       if (k == NB - 1) h1 = h;
     }
+#endif
     if constexpr (CIG) {
       if ((k & 7) == 0) nib[k >> 3] = (uint32_t)d;
       else nib[k >> 3] |= (uint32_t)d << (4 * (k & 7));
