@@ -131,6 +131,28 @@ __device__ __forceinline__ uint32_t launder(uint32_t x) {
   return x;
 }
 __device__ __forceinline__ uint32_t pbfi(uint32_t m, uint32_t a, uint32_t b) { return (m & a) | (~m & b); }
+// m ? a : b per bit in one full-rate v_bitop3_b32 (as phmm's sel_v): compiler
+// selects on a compare come out as VOP2 v_cndmask_b32 reading VCC, ~20 cycles
+// each on gfx950
+__device__ __forceinline__ uint32_t bsel(uint32_t m, uint32_t a, uint32_t b) {
+  uint32_t r;
+  asm("v_bitop3_b32 %0, %1, %2, %3 bitop3:0xe4" : "=v"(r) : "v"(a), "v"(b), "v"(m));
+  return r;
+}
+// v_ffbl_b32 / v_ffbh_u32 (lowest set bit / leading zeros) OR a word offset:
+// both return ~0u for a zero word, so an empty word yields ~0u and a v_min_u32
+// chain finds the first / last set bit.  As builtins (ctz with a -1 default)
+// the compiler turns that min chain into compare + VOP2 select pairs.
+__device__ __forceinline__ uint32_t ffbl_or(uint32_t w, uint32_t off) {
+  uint32_t r;
+  asm("v_ffbl_b32 %0, %1" : "=v"(r) : "v"(w));
+  return r | off;
+}
+__device__ __forceinline__ uint32_t ffbh_or(uint32_t w, uint32_t off) {
+  uint32_t r;
+  asm("v_ffbh_u32 %0, %1" : "=v"(r) : "v"(w));
+  return r | off;
+}
 
 __device__ __forceinline__ uint32_t pack2(int a, int b) { return ((uint32_t)a & 0xFFFFu) | ((uint32_t)b << 16); }
 
@@ -432,12 +454,14 @@ __device__ __forceinline__ void pair_wave(const BswDevBatch& b, const BswParams&
     const uint32_t H1r = pk_subs(S.H0, ode) & pk_lt(S.BEG, ONE);
     const uint32_t WORK = ALIVE & pk_lt(S.BEG, S.END);
     const uint32_t EMPTY = ALIVE ^ WORK;  // beg >= end: bwa stores eh[end] and stops
-    const int begA = (int)(int16_t)(S.BEG & 0xFFFFu), begB = (int)(int16_t)(S.BEG >> 16);
     const int endA = (int)(int16_t)(S.END & 0xFFFFu), endB = (int)(int16_t)(S.END >> 16);
-    const bool workA = WORK & 1u, workB = (WORK >> 16) & 1u;
-    const int cmin = -wave_max(-min(workA ? begA : (1 << 20), workB ? begB : (1 << 20)));
-    const int cmax = wave_max(max(workA ? endA : -1, workB ? endB : -1));
-    const int emin = -wave_max(-min(workA ? endA : (1 << 20), workB ? endB : (1 << 20)));
+    // wave range of the working tasks' bands (idle halves as 32767 / -1 by
+    // bitop3 selects on the WORK half masks)
+    const uint32_t BW = bsel(WORK, S.BEG, 0x7FFF7FFFu), EW = bsel(WORK, S.END, 0x7FFF7FFFu);
+    const uint32_t EX = bsel(WORK, S.END, ~0u);
+    const int cmin = -wave_max(-min((int)(int16_t)(BW & 0xFFFFu), (int)BW >> 16));
+    const int cmax = wave_max(max((int)(int16_t)(EX & 0xFFFFu), (int)EX >> 16));
+    const int emin = -wave_max(-min((int)(int16_t)(EW & 0xFFFFu), (int)EW >> 16));
     PAIR_STAT(1, 1);
 #ifdef FCS_BSW_STATS
     {  // task-rows of the wave that still work / are alive in this row
@@ -520,19 +544,18 @@ __device__ __forceinline__ void pair_wave(const BswDevBatch& b, const BswParams&
         if (32 * m + 31 < cmin || 32 * m > cmax) continue;  // wave-uniform: outside every band
         const uint32_t lo = r.nz[2 * m], hi = (2 * m + 1 < PNZ<NC>) ? r.nz[2 * m + 1] : 0u;
         const uint32_t wa = __builtin_amdgcn_perm(hi, lo, 0x05040100u), wb = __builtin_amdgcn_perm(hi, lo, 0x07060302u);
-        fa = min(fa, (uint32_t)__builtin_ctzg(wa, -1) | (uint32_t)(m << 5));
-        la = min(la, (uint32_t)__builtin_ctzg(__builtin_bitreverse32(wa), -1) | (uint32_t)((NM - 1 - m) << 5));
-        fb = min(fb, (uint32_t)__builtin_ctzg(wb, -1) | (uint32_t)(m << 5));
-        lb = min(lb, (uint32_t)__builtin_ctzg(__builtin_bitreverse32(wb), -1) | (uint32_t)((NM - 1 - m) << 5));
+        fa = min(fa, ffbl_or(wa, (uint32_t)(m << 5)));
+        la = min(la, ffbh_or(wa, (uint32_t)((NM - 1 - m) << 5)));
+        fb = min(fb, ffbl_or(wb, (uint32_t)(m << 5)));
+        lb = min(lb, ffbh_or(wb, (uint32_t)((NM - 1 - m) << 5)));
       }
+      // f and l are ~0u together (no bit set: bwa's beg = end, end = end + 1);
+      // the sign bit of f is that mask (a found position is < 32 * NM)
       auto trim = [&](uint32_t f, uint32_t l, int endv, int qlen, int& nb, int& ne) __attribute__((always_inline)) {
-        if (f != ~0u) {
-          nb = (int)f;
-          ne = min(32 * (NM - 1 - (int)(l >> 5)) + 31 - (int)(l & 31u) + 2, qlen);
-        } else {
-          nb = endv;
-          ne = min(endv + 1, qlen);
-        }
+        const uint32_t none = (uint32_t)((int)f >> 31);
+        nb = (int)bsel(none, (uint32_t)endv, f);
+        const int last = bsel(none, (uint32_t)(endv - 1), (uint32_t)(32 * (NM - 1) + 31) - ((l >> 5) << 5) - (l & 31u));
+        ne = min(last + 2, qlen);
       };
       int nba, nea, nbb, neb;
       trim(fa, la, endA, A.qlen, nba, nea);
