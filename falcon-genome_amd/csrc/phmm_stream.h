@@ -169,12 +169,6 @@ __device__ __forceinline__ int srole(int r, int R) { return r == 0 ? 1 : r < R ?
 #ifndef FCS_STREAM_SELV
 #define FCS_STREAM_SELV 1
 #endif
-#ifndef FCS_STREAM_RINGX
-#define FCS_STREAM_RINGX 0
-#endif
-#ifndef FCS_STREAM_HAPDPP
-#define FCS_STREAM_HAPDPP 0
-#endif
 __device__ __forceinline__ float sel_v(uint32_t m, float a, float b) {
   float r;
   asm("v_bitop3_b32 %0, %1, %2, %3 bitop3:0xe4" : "=v"(r) : "v"(a), "v"(b), "v"(m));
@@ -231,10 +225,6 @@ __device__ __forceinline__ void pstream_step(Lane2& L, PhRing<float> (&pf)[PF], 
 #if FCS_DIAG_NOREAD || FCS_DIAG_NORING  // diagnostic builds only (timing; results are wrong)
   pf[PF - 1] = PhRing<float>{pf[0].I, pf[0].X};
   (void)rd;
-#elif FCS_STREAM_RINGX
-  // only start lanes consume the boundary input: the read under their EXEC
-  // (LDS return bandwidth is paid per active lane; the CU's LDS is saturated)
-  if (start) pf[PF - 1] = rd[S];
 #else
   pf[PF - 1] = rd[S];     // boundary input for step t + PF
 #endif
@@ -244,13 +234,6 @@ __device__ __forceinline__ void pstream_step(Lane2& L, PhRing<float> (&pf)[PF], 
   hq[HPF - 1] = 6;
 #elif FCS_DIAG_NOREAD || FCS_DIAG_NOHAP
   hq[HPF - 1] = hq[0] ^ 1;
-#elif FCS_STREAM_HAPDPP
-  // lane l's code for step t + 2 (column t + 2 - 2l) is lane l - 1's code of
-  // this step: carried by DPP; only start lanes (segment lane 0, a pair's
-  // first lane) read LDS, under their EXEC
-  static_assert(HPF == 2, "the DPP carry assumes a two-step read-ahead");
-  hq[HPF - 1] = __builtin_amdgcn_update_dpp(0, hba, kDppRowShr1, 0xF, 0xF, true);
-  if (start) hq[HPF - 1] = hp[t];
 #elif !FCS_STREAM_HAP4
   hq[HPF - 1] = hp[t];    // row a's hap code for column t + HPF - 2l
 #endif
