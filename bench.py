@@ -42,6 +42,7 @@ FLOPS_PER_CELL = 11          # M 5 + I 3 + D 3 (FMA = 2)
 VALU_LANE_INSTR_PEAK = 256 * 4 * 32 * 2.4e9  # lane-instructions/s: one wave64 VALU op per 2 cycles per SIMD
 FP32_VECTOR_PEAK_TF = 157.3  # MI355X_MICROARCH.md chip table (spec)
 HBM_PEAK_GBS = 8000.0
+SW_OPS_PER_CELL = 12         # BASELINE.md §3 / SURVEY §8d: ~12 int ops per ksw_extend2 cell
 
 
 def phmm_dev_batch(p: "fcship.PhmmPairs", dev):
@@ -159,7 +160,8 @@ def bench_bsw(args, dev, tasks, reps=3):
     fcship.lib.fcs_bsw_plan_destroy(plan)
     del keep
     return dict(ms=ms, cells=ncell, gcups=ncell / (ms * 1e-3) / 1e9, tasks=tasks.n,
-                bytes=int(tasks.qbuf.size + tasks.tbuf.size + 24 * tasks.n))
+                bytes=int(tasks.qbuf.size + tasks.tbuf.size + 24 * tasks.n),
+                res=res.cpu().numpy(), cell_counts=cells.cpu().numpy())
 
 
 def bench_bsw_global(args, dev, tasks, reps=3):
@@ -212,6 +214,119 @@ def bench_bsw_global(args, dev, tasks, reps=3):
     return dict(tasks=n, w=int(tasks.w[0]) if n else 0, cells=cells, **out)
 
 
+def shard_stats(logs, dt):
+    """Per-shard caller lines summed over the shards (workers/*.cpp): counts,
+    and the stage times as thread-seconds (shards run concurrently)."""
+    import re
+    tot = lambda pat, f=float: sum(f(x) for x in re.findall(pat, logs))  # noqa: E731
+    st = {"regions": tot(r"(\d+) regions", int), "pairs": tot(r"(\d+) pairs", int),
+          "cells": tot(r"(\d+) cells", int), "rescued_pairs": tot(r"(\d+) rescued", int),
+          "device_passes": tot(r"(\d+) device passes", int),
+          "seconds": round(dt, 3)}
+    st["regions_per_s"] = round(st["regions"] / dt, 1)
+    brk = {k: round(tot(pat), 3) for k, pat in (
+        ("decode", r"decode ([\d.]+) s"), ("pileup", r"pileup ([\d.]+) s"),
+        ("regions", r"regions ([\d.]+) s\b"), ("phmm_call", r"PairHMM ([\d.]+) s"),
+        ("genotype", r"genotype ([\d.]+) s"), ("output", r"output ([\d.]+) s"))}
+    st["stage_thread_seconds"] = brk
+    dev, res = tot(r"device ([\d.]+) s"), tot(r"rescue ([\d.]+) s")
+    st["phmm_device_seconds"] = round(dev, 4)
+    st["rescue_fp64_device_seconds"] = round(res, 4)
+    st["gpu_busy_frac"] = round(dev / dt, 4)  # PairHMM device time (HIP events) / wall time, one GPU
+    st["effective_gcups"] = round(st["cells"] / dt / 1e9, 2)
+    return st
+
+
+def cpu_mock_env(env):
+    """Environment of an fcs-genome child that runs the reference's CPU
+    PairHMM path: tests/cpu_mock/build/libfcship.so (test infrastructure: the
+    oracle's Java-semantics or GKL-style AVX-512 PairHMM behind the same
+    C-ABI) first on its LD_LIBRARY_PATH.  Only that child sees it."""
+    import subprocess
+    mock = os.path.join(ROOT, "tests", "cpu_mock", "build")
+    if not os.path.exists(os.path.join(mock, "libfcship.so")):
+        subprocess.run(["make", "-C", os.path.join(ROOT, "tests", "cpu_mock")], check=True, capture_output=True)
+    return dict(env, LD_LIBRARY_PATH=mock + os.pathsep + env.get("LD_LIBRARY_PATH", ""))
+
+
+def vcf_calls(path):
+    """(chrom, pos, ref, alt) of the variant records of a VCF or GVCF (GVCF
+    reference blocks and the <NON_REF> allele left out)."""
+    out = set()
+    for ln in open(path):
+        if ln.startswith("#"):
+            continue
+        f = ln.split("\t", 5)
+        alts = [a for a in f[4].split(",") if a != "<NON_REF>"]
+        if alts:
+            out.add((f[0], int(f[1]), f[3], ",".join(alts)))
+    return out
+
+
+def htc_cpu_baseline(exe, env, work, ref, bam, gpu_out, modes=("gkl", "java"), vcf=False):
+    """`fcs-genome htc` with the PairHMM on the host CPU (BASELINE.json
+    configs[0]'s path: GATK HaplotypeCaller with --native-pair-hmm-threads,
+    /root/reference/src/workers/HTCWorker.cpp:85,105), same command, genome and
+    shard threads as the GPU run: gkl = GKL's AVX-512 float PairHMM with the
+    double rescue restated, java = GATK's Java LoglessPairHMM (double).  Calls
+    compared with the GPU run's output."""
+    import subprocess
+    cenv = cpu_mock_env(env)
+    gpu_calls = vcf_calls(gpu_out)
+    res = {}
+    for m in modes:
+        o = os.path.join(work, f"htc_cpu_{m}" + (".vcf" if vcf else ".g.vcf"))
+        logd = os.path.join(work, f"log_cpu_{m}")
+        e = dict(cenv, FCS_MOCK_PHMM=m, FCS_LOG_DIR=logd)
+        t0 = time.perf_counter()
+        r = subprocess.run([exe, "htc", "-f", "-r", ref, "-i", bam, "-o", o] + (["-v"] if vcf else []),
+                           env=e, capture_output=True, text=True, cwd=work)
+        dt = time.perf_counter() - t0
+        if r.returncode != 0:
+            raise RuntimeError(f"CPU-path htc ({m}) failed ({r.returncode}): {r.stderr[-2000:]}")
+        logs = "".join(open(os.path.join(logd, f)).read() for f in os.listdir(logd) if ".part-" not in f)
+        st = shard_stats(logs, dt)
+        for k in ("phmm_device_seconds", "rescue_fp64_device_seconds", "gpu_busy_frac", "device_passes"):
+            st.pop(k, None)
+        c = vcf_calls(o)
+        st.update(kind="port", cores=int(env.get("FCS_GATK_NPROCS", "16")),
+                  pairhmm={"gkl": "GKL-style AVX-512 restatement (float pass, double rescue below 1e-28), one "
+                                  "shard thread per region batch",
+                           "java": "GATK Java LoglessPairHMM semantics (double), scalar, one shard thread per "
+                                   "region batch"}[m],
+                  calls=len(c), calls_equal_to_gpu=c == gpu_calls,
+                  calls_only_gpu=len(gpu_calls - c), calls_only_cpu=len(c - gpu_calls))
+        res[m] = st
+    return res
+
+
+def bench_c1(exe, env, work, seed):
+    """BASELINE.json configs[0] (C1): `fcs-genome htc` on a 1,000-read
+    synthetic chr20 BAM, on the GPU and through the reference's CPU PairHMM
+    path (Java semantics and GKL-style AVX-512), VCF output; wall time of each
+    command and whether the calls agree."""
+    import subprocess
+    c1 = os.path.join(work, "c1")
+    subprocess.run([exe, "synth", "-o", c1, "-c", "chr20:1000000", "-x", "30", "-n", "1000", "--no-fastq",
+                    "--seed", str(seed)], env=env, check=True, capture_output=True)
+    logd = os.path.join(work, "log_c1")
+    t0 = time.perf_counter()
+    r = subprocess.run([exe, "htc", "-f", "-r", c1 + "/ref.fasta", "-i", c1 + "/sample.bam", "-o", work + "/c1.vcf",
+                        "-v"], env=dict(env, FCS_LOG_DIR=logd), capture_output=True, text=True, cwd=work)
+    dt = time.perf_counter() - t0
+    if r.returncode != 0:
+        raise RuntimeError(f"C1 htc failed ({r.returncode}): {r.stderr[-2000:]}")
+    logs = "".join(open(os.path.join(logd, f)).read() for f in os.listdir(logd) if ".part-" not in f)
+    gpu = shard_stats(logs, dt)
+    gpu["calls"] = len(vcf_calls(work + "/c1.vcf"))
+    out = {"workload": "C1: fcs-genome htc -v on a 1,000-read synthetic chr20 BAM (chr20-like 1 Mbp reference, "
+                       "the first 1,000 reads of a 30x sample)", "gpu": gpu}
+    out["cpu_baseline"] = htc_cpu_baseline(exe, env, work, c1 + "/ref.fasta", c1 + "/sample.bam", work + "/c1.vcf",
+                                           modes=("java", "gkl"),
+                                           vcf=True)
+    return out
+
+
 def bench_e2e(args, rank, local):
     """End-to-end fcs-genome commands on this rank's own synthetic genome
     (C4/C5-shaped: a chr1-like random reference of --e2e-mbp per GPU — 31 Mbp
@@ -230,6 +345,7 @@ def bench_e2e(args, rank, local):
     per_rank = max(2, host_cpu_quota() // max(1, int(os.environ.get("LOCAL_WORLD_SIZE", "1"))))
     env = dict(os.environ, FCS_GPU_DEVICES=str(local), FCS_LOG_DIR=os.path.join(work, "log"),
                FCS_TEMP_DIR=work, FCS_GATK_NPROCS="16", FCS_HOST_THREADS=str(per_rank))
+    cpu_htc = rank == 0 and int(os.environ.get("WORLD_SIZE", "1")) == 1 and not args.no_cpu_baseline
     try:
         L = int(args.e2e_mbp * 1e6)
         t0 = time.perf_counter()
@@ -265,26 +381,6 @@ def bench_e2e(args, rank, local):
             m = re.search(name + r" finishes in ([\d.]+) seconds", err)
             return float(m.group(1)) if m else None
 
-        def shard_stats(logs, dt):
-            """Per-shard caller lines summed over the shards (workers/*.cpp): counts,
-            and the stage times as thread-seconds (shards run concurrently)."""
-            tot = lambda pat, f=float: sum(f(x) for x in re.findall(pat, logs))  # noqa: E731
-            st = {"regions": tot(r"(\d+) regions", int), "pairs": tot(r"(\d+) pairs", int),
-                  "cells": tot(r"(\d+) cells", int), "rescued_pairs": tot(r"(\d+) rescued", int),
-                  "device_passes": tot(r"(\d+) device passes", int),
-                  "seconds": round(dt, 3)}
-            st["regions_per_s"] = round(st["regions"] / dt, 1)
-            brk = {k: round(tot(pat), 3) for k, pat in (
-                ("decode", r"decode ([\d.]+) s"), ("pileup", r"pileup ([\d.]+) s"),
-                ("regions", r"regions ([\d.]+) s\b"), ("phmm_call", r"PairHMM ([\d.]+) s"),
-                ("genotype", r"genotype ([\d.]+) s"), ("output", r"output ([\d.]+) s"))}
-            st["stage_thread_seconds"] = brk
-            dev, res = tot(r"device ([\d.]+) s"), tot(r"rescue ([\d.]+) s")
-            st["phmm_device_seconds"] = round(dev, 4)
-            st["rescue_fp64_device_seconds"] = round(res, 4)
-            st["gpu_busy_frac"] = round(dev / dt, 4)  # PairHMM device time (HIP events) / wall time, one GPU
-            st["effective_gcups"] = round(st["cells"] / dt / 1e9, 2)
-            return st
         (dt, logs, err), runs = best("htc", ["htc", "-f", "-r", d + "/ref.fasta", "-i", d + "/sample.bam", "-o",
                                              work + "/htc.g.vcf"])
         out["htc"] = shard_stats(logs, dt)
@@ -293,6 +389,9 @@ def bench_e2e(args, rank, local):
         hs = stage_s(err, "Haplotype Caller")
         out["htc"]["caller_stage_seconds"] = hs  # the 32-shard stage alone: no process start, GPU init, concat
         out["htc"]["caller_stage_regions_per_s"] = round(out["htc"]["regions"] / hs, 1) if hs else None
+        if cpu_htc:  # the reference's CPU path beside it, on the same genome (rank 0, N=1 only)
+            out["htc"]["cpu_baseline"] = htc_cpu_baseline(exe, env, work, d + "/ref.fasta", d + "/sample.bam",
+                                                          work + "/htc.g.vcf")
         (dt, logs, err), runs = best("mutect2", ["mutect2", "-f", "-r", d + "/ref.fasta", "-t", d + "/tumor.bam", "-n",
                                                  d + "/sample.bam", "-o", work + "/m2.vcf"])
         out["mutect2"] = shard_stats(logs, dt)
@@ -301,6 +400,8 @@ def bench_e2e(args, rank, local):
         out["mutect2"]["caller_stage_seconds"] = ms
         out["mutect2"]["caller_stage_regions_per_s"] = round(out["mutect2"]["regions"] / ms, 1) if ms else None
         shutil.rmtree(d, ignore_errors=True)
+        if cpu_htc:
+            out["c1"] = bench_c1(exe, env, work, args.seed + rank)
         La = int(args.e2e_align_mbp * 1e6)
         subprocess.run([exe, "synth", "-o", work + "/a", "-c", f"chr1:{La}", "-x", "30", "--no-fastq", "--paired",
                         "350", "--seed", str(args.seed + rank)], env=env, check=True, capture_output=True)
@@ -382,7 +483,7 @@ def cpu_baseline_phmm(p, budget_s, threads):
     times = []
     for _ in range(5):
         t0 = time.perf_counter()
-        run(s, threads=threads)
+        ref, used_d = run(s, threads=threads)
         times.append(time.perf_counter() - t0)
     best = min(times)
     kind = "GKL-style AVX-512 restatement (float, 16-lane anti-diagonal stripes; double rescue, 8 lanes)" if simd \
@@ -390,7 +491,24 @@ def cpu_baseline_phmm(p, budget_s, threads):
     return dict(value=s.cells() / best / 1e9, unit="GCUPS", cores=threads, kind="port",
                 sample=f"first {n} of the {p.n_pairs} C2 pairs ({s.cells() / 1e9:.2f} G cells), best of 5 "
                        f"({', '.join(f'{t:.2f}' for t in times)} s); {kind}; OpenMP {threads} threads "
-                       f"(nproc {os.cpu_count()})")
+                       f"(nproc {os.cpu_count()})"), ref, used_d
+
+
+def phmm_parity(gpu, ref, used_d, tol=1e-5):
+    """The headline run's own outputs (the last timed step's) against the CPU
+    baseline's outputs for the same pairs: |gpu - ref| <= tol * |ref|
+    (north_star: log10 likelihoods within 1e-5 of GATK's AVX path).  A pair is
+    non-finite-consistent when both sides are the same inf, or both finite."""
+    gpu = np.asarray(gpu[:ref.size], np.float64)
+    fin = np.isfinite(ref) & np.isfinite(gpu)
+    same_inf = ~np.isfinite(ref) & (gpu == ref)
+    rel = np.abs(gpu[fin] - ref[fin]) / np.maximum(np.abs(ref[fin]), 1e-300)
+    return {"n": int(ref.size), "max_rel_err": float(rel.max()) if rel.size else 0.0,
+            "n_over_1e-5": int((rel > tol).sum()), "tolerance": tol,
+            "nonfinite_mismatch": int(ref.size - fin.sum() - same_inf.sum()),
+            "rescued_by_oracle": int(np.asarray(used_d).sum()),
+            "pass": bool((rel <= tol).all() and fin.sum() + same_inf.sum() == ref.size),
+            "against": "oracle/pairhmm_simd.c (GKL-style AVX-512 restatement, bit-identical to the scalar oracle)"}
 
 
 def bsw_roofline(r3, rf):
@@ -416,6 +534,10 @@ def bsw_roofline(r3, rf):
         ach = r3["gcups"] * 1e9 * per3
         out.update(achieved=round(ach / 1e12, 3), frac=round(ach / VALU_LANE_INSTR_PEAK, 4),
                    valu_instr_per_cell=per3, valu_source=meas.get("source"))
+    # the algorithmic fraction: BASELINE.md §3's ~12 int ops per cell, whatever
+    # the kernel issues for them (rises only when the kernel gets faster)
+    out["algorithmic_ops_per_cell"] = SW_OPS_PER_CELL
+    out["algorithmic_frac"] = round(r3["gcups"] * 1e9 * SW_OPS_PER_CELL / VALU_LANE_INSTR_PEAK, 4)
     try:
         ck = json.load(open(os.path.join(ROOT, "profiles", "clock.json"))).get("bsw_ext")
     except (OSError, ValueError):
@@ -429,21 +551,37 @@ def bsw_roofline(r3, rf):
     return out
 
 
-def cpu_baseline_bsw(tasks, budget_s, threads):
+def cpu_baseline_bsw(tasks, gpu, budget_s, threads):
     """bwa's ksw_extend2 is scalar C (bwa ksw.c; bwa-mem's own SIMD is only in
     ksw_align2/SSE2 local alignment), so the scalar restatement over OpenMP is
-    the like-for-like CPU path; best of 3."""
+    the like-for-like CPU path; best of 3 over a leading slice of the timed C3
+    tasks sized to budget_s, whose outputs are compared with the GPU's outputs
+    for the same tasks (six ints and the cell count, bit-exact)."""
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     import oracle_lib
-    n = tasks.n
+
+    def head(n):
+        return fcship.BswTasks(tasks.qbuf, tasks.qoff[:n], tasks.qlen[:n], tasks.tbuf, tasks.toff[:n], tasks.tlen[:n],
+                               tasks.h0[:n], tasks.w[:n])
+    cal = head(min(tasks.n, 2000 * threads))
+    t0 = time.perf_counter()
+    oracle_lib.ksw_extend2_batch(cal, fcship.default_mat(), threads=threads)
+    per_task = max(time.perf_counter() - t0, 1e-6) / cal.n
+    n = int(min(tasks.n, max(cal.n, budget_s / 3 / per_task)))
+    s = head(n)
     times = []
     for _ in range(3):
         t0 = time.perf_counter()
-        _, cells = oracle_lib.ksw_extend2_batch(tasks, fcship.default_mat(), threads=threads)
+        res, cells = oracle_lib.ksw_extend2_batch(s, fcship.default_mat(), threads=threads)
         times.append(time.perf_counter() - t0)
+    same = (res == gpu["res"][:n]).all(axis=1) & (cells == gpu["cell_counts"][:n])
+    parity = {"n": n, "bit_exact": int(same.sum()), "mismatched": int(n - same.sum()), "pass": bool(same.all()),
+              "fields": "score, qle, tle, gtle, gscore, max_off and the evaluated-cell count",
+              "against": "oracle/ksw_oracle.c (bwa ksw_extend2 restatement)"}
     return dict(value=int(cells.sum()) / min(times) / 1e9, unit="GCUPS", cores=threads, kind="port",
-                sample=f"{n} C3 extension tasks, scalar C ksw_extend2 restatement (bwa's is scalar too), best of 3, "
-                       f"OpenMP {threads} threads (nproc {os.cpu_count()})")
+                sample=f"first {n} of the {tasks.n} timed C3 extension tasks, scalar C ksw_extend2 restatement "
+                       f"(bwa's is scalar too), best of 3 ({', '.join(f'{t:.2f}' for t in times)} s), "
+                       f"OpenMP {threads} threads (nproc {os.cpu_count()})"), parity
 
 
 class Ranks:
@@ -665,11 +803,12 @@ def main():
                 "valu_instr_per_cell": vpc, "of": "scores-only pass (DP kernels)",
                 "valu_source": "profiles/pmc_bsw.json global (SQ_INSTS_VALU x 64 / band cells)"}
         if world == 1 and not args.no_cpu_baseline:
-            line["bsw"]["cpu_baseline"] = cpu_baseline_bsw(
-                fcship.synth_bsw(args.seed + 1, 20000, read_len=151, ref_len=10_000_000), 0, cpu_threads())
+            line["bsw"]["cpu_baseline"], line["bsw"]["parity"] = cpu_baseline_bsw(c3, r3, args.cpu_budget,
+                                                                                  cpu_threads())
 
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        line["cpu_baseline"] = cpu_baseline_phmm(p, args.cpu_budget, cpu_threads())
+        line["cpu_baseline"], ref, used_d = cpu_baseline_phmm(p, args.cpu_budget, cpu_threads())
+        line["parity"] = phmm_parity(ph["out"], ref, used_d)
 
     if not args.no_e2e:
         e2e = bench_e2e(args, rank, local)

@@ -366,7 +366,7 @@ int get_device_tables(int device, DeviceTables** out) {
   if (!slot) slot.reset(new DeviceTables());
   DeviceTables& t = *slot;
   if (!t.ready) {
-    FCS_HIP_CHECK(hipSetDevice(device));
+    FCS_SET_DEVICE((device));
     const size_t n = 3 * 128 + kMmEntries;
     std::vector<float> hf(n);
     std::vector<double> hd(n);
@@ -553,7 +553,7 @@ int fcs_phmm_plan_create(int32_t device, int64_t max_pairs, fcs_phmm_plan** plan
   if (!plan || max_pairs < 0) return fail(FCS_ERR_INVALID, "[E::fcs_phmm_plan_create] bad arguments");
   int rc = check_device(device);
   if (rc) return rc;
-  FCS_HIP_CHECK(hipSetDevice(device));
+  FCS_SET_DEVICE((device));
   DeviceTables* t = nullptr;
   rc = get_device_tables(device, &t);
   if (rc) return rc;
@@ -585,6 +585,7 @@ int fcs_phmm_plan_create(int32_t device, int64_t max_pairs, fcs_phmm_plan** plan
 
 int fcs_phmm_plan_destroy(fcs_phmm_plan* p) {
   if (!p) return FCS_OK;
+  ::fcs::DeviceScope dev_scope;
   (void)hipSetDevice(p->device);
   (void)hipFree(p->keys_in);
   (void)hipFree(p->keys_out);
@@ -603,7 +604,7 @@ int fcs_phmm_dev_schedule(fcs_phmm_plan* plan, const fcs_phmm_batch* b, void* st
   int rc = check_batch_shape(b);
   if (rc) return rc;
   if (b->n_pairs > plan->max_pairs) return fail(FCS_ERR_INVALID, "[E::fcs_phmm_dev_schedule] batch exceeds plan");
-  FCS_HIP_CHECK(hipSetDevice(plan->device));
+  FCS_SET_DEVICE((plan->device));
   hipStream_t s = (hipStream_t)stream;
   const PhmmDevBatch d = to_dev(b);
   rc = launch_phmm_keys(d, plan->keys_in, plan->idx_in, plan->rescue_count, s);
@@ -628,7 +629,7 @@ int fcs_phmm_dev_forward(fcs_phmm_plan* plan, const fcs_phmm_batch* b, double* o
   if (plan->scheduled != b->n_pairs)
     return fail(FCS_ERR_INVALID, "[E::fcs_phmm_dev_forward] batch not scheduled (call fcs_phmm_dev_schedule)");
   if (b->n_pairs > 0 && !out) return fail(FCS_ERR_INVALID, "[E::fcs_phmm_dev_forward] null output");
-  FCS_HIP_CHECK(hipSetDevice(plan->device));
+  FCS_SET_DEVICE((plan->device));
   DeviceTables* t = nullptr;
   rc = get_device_tables(plan->device, &t);
   if (rc) return rc;
@@ -649,7 +650,7 @@ int fcs_phmm_dev_rescue(fcs_phmm_plan* plan, const fcs_phmm_batch* b, double* ou
   int rc = check_batch_shape(b);
   if (rc) return rc;
   if (!opts->use_fp64_rescue) return FCS_OK;
-  FCS_HIP_CHECK(hipSetDevice(plan->device));
+  FCS_SET_DEVICE((plan->device));
   DeviceTables* t = nullptr;
   rc = get_device_tables(plan->device, &t);
   if (rc) return rc;
@@ -669,7 +670,7 @@ int fcs_phmm_dev_run(fcs_phmm_plan* plan, const fcs_phmm_batch* b, double* out, 
 int fcs_stream_release(int32_t device, void* stream) {
   int rc = check_device(device);
   if (rc) return rc;
-  FCS_HIP_CHECK(hipSetDevice(device));
+  FCS_SET_DEVICE((device));
   ForkSet f;
   {
     std::lock_guard<std::mutex> lk(g_fork_mu);
@@ -678,12 +679,21 @@ int fcs_stream_release(int32_t device, void* stream) {
     f = it->second;
     g_fork_sets->erase(it);
   }
+  // tear down every side stream and event (best effort), then report the
+  // first failure: an early return would leak the rest unreachably
+  hipError_t first = hipSuccess;
+  const char* what = nullptr;
+  auto note = [&](hipError_t e, const char* w) {
+    if (e != hipSuccess && first == hipSuccess) first = e, what = w;
+  };
   for (int i = 0; i < kForkStreams - 1; ++i) {
-    FCS_HIP_CHECK(hipStreamSynchronize(f.side[i]));
-    FCS_HIP_CHECK(hipStreamDestroy(f.side[i]));
-    FCS_HIP_CHECK(hipEventDestroy(f.join[i]));
+    note(hipStreamSynchronize(f.side[i]), "hipStreamSynchronize");
+    note(hipStreamDestroy(f.side[i]), "hipStreamDestroy");
+    note(hipEventDestroy(f.join[i]), "hipEventDestroy");
   }
-  FCS_HIP_CHECK(hipEventDestroy(f.fork));
+  note(hipEventDestroy(f.fork), "hipEventDestroy");
+  if (first != hipSuccess)
+    return fail(FCS_ERR_DEVICE, std::string("[E::fcs_stream_release] ") + what + ": " + hipGetErrorString(first));
   return FCS_OK;
 }
 
@@ -699,7 +709,7 @@ int fcs_device_warmup(int32_t device, int32_t sessions) {
   fcs_phmm_opts_default(&o);
   o.device = device;
   if ((rc = fcs_phmm_compute(&r, 1, &h, 1, &out, &o))) return rc;
-  FCS_HIP_CHECK(hipSetDevice(device));
+  FCS_SET_DEVICE((device));
   return prefill_sessions(device, sessions <= 0 ? sessions_per_device() : sessions);
 }
 
@@ -718,7 +728,7 @@ int fcs_phmm_last_rescued(int64_t* count) {
 
 int fcs_phmm_plan_rescue_count(fcs_phmm_plan* plan, void* stream, int64_t* count) {
   if (!plan || !count) return fail(FCS_ERR_INVALID, "[E::fcs_phmm_plan_rescue_count] bad arguments");
-  FCS_HIP_CHECK(hipSetDevice(plan->device));
+  FCS_SET_DEVICE((plan->device));
   unsigned long long v = 0;
   FCS_HIP_CHECK(hipMemcpyAsync(&v, plan->rescue_count, sizeof(v), hipMemcpyDeviceToHost, (hipStream_t)stream));
   FCS_HIP_CHECK(hipStreamSynchronize((hipStream_t)stream));
@@ -748,7 +758,7 @@ int phmm_staged(const PhmmStage& g, const fcs_phmm_opts& opts, SessionLease& lea
                 const double** host_out) {
   int rc = check_device(opts.device);
   if (rc) return rc;
-  FCS_HIP_CHECK(hipSetDevice(opts.device));
+  FCS_SET_DEVICE((opts.device));
   if ((rc = lease.acquire(opts.device))) return rc;
   Session* S = lease.get();
   const size_t RB = (size_t)g.read_bytes, HB = (size_t)g.hap_bytes, nr = (size_t)g.n_reads, nh = (size_t)g.n_haps,
@@ -1075,7 +1085,7 @@ int fcs_bsw_extend_dev(const fcs_bsw_batch* b, const fcs_bsw_params* params, int
   if (b->n > 0 && !res) return fail(FCS_ERR_INVALID, "[E::fcs_bsw_extend_dev] null result buffer");
   if ((rc = check_device(device))) return rc;
   if (b->n == 0) return FCS_OK;
-  FCS_HIP_CHECK(hipSetDevice(device));
+  FCS_SET_DEVICE((device));
   hipStream_t s = (hipStream_t)stream;
   BswWorkspace ws;
   if ((rc = ws_alloc(ws, b->n, s, true))) {
@@ -1092,7 +1102,7 @@ int fcs_bsw_plan_create(int32_t device, int64_t max_tasks, fcs_bsw_plan** plan) 
   if (!plan || max_tasks < 0) return fail(FCS_ERR_INVALID, "[E::fcs_bsw_plan_create] bad arguments");
   int rc = check_device(device);
   if (rc) return rc;
-  FCS_HIP_CHECK(hipSetDevice(device));
+  FCS_SET_DEVICE((device));
   std::unique_ptr<fcs_bsw_plan> p(new fcs_bsw_plan());
   p->device = device;
   if ((rc = ws_alloc(p->ws, max_tasks, nullptr, false))) {
@@ -1105,6 +1115,7 @@ int fcs_bsw_plan_create(int32_t device, int64_t max_tasks, fcs_bsw_plan** plan) 
 
 int fcs_bsw_plan_destroy(fcs_bsw_plan* plan) {
   if (!plan) return FCS_OK;
+  ::fcs::DeviceScope dev_scope;
   (void)hipSetDevice(plan->device);
   ws_free(plan->ws, nullptr, false);
   delete plan;
@@ -1120,7 +1131,7 @@ int fcs_bsw_extend_plan(fcs_bsw_plan* plan, const fcs_bsw_batch* b, const fcs_bs
   if (b->n > plan->ws.cap) return fail(FCS_ERR_INVALID, "[E::fcs_bsw_extend_plan] batch exceeds plan");
   if (b->n > 0 && !res) return fail(FCS_ERR_INVALID, "[E::fcs_bsw_extend_plan] null result buffer");
   if (b->n == 0) return FCS_OK;
-  FCS_HIP_CHECK(hipSetDevice(plan->device));
+  FCS_SET_DEVICE((plan->device));
   return launch_bsw_extend_sorted(bsw_dev(b), to_params(params), std::max(b->max_qlen, 0), std::max(b->max_tlen, 0),
                                   res, cells, plan->ws, (hipStream_t)stream);
 }
@@ -1147,7 +1158,7 @@ int fcs_bsw_extend_batch(const fcs_bsw_batch* b, const fcs_bsw_params* params, i
   for (int64_t i = 0; i < b->tbytes; ++i)
     if (b->tbuf[i] > 4) return fail(FCS_ERR_INVALID, "[E::fcs_bsw_extend_batch] target base code > 4");
   if ((rc = check_device(device))) return rc;
-  FCS_HIP_CHECK(hipSetDevice(device));
+  FCS_SET_DEVICE((device));
   SessionLease lease;
   if ((rc = lease.acquire(device))) return rc;
   Session* S = lease.get();
@@ -1304,7 +1315,7 @@ int fcs_bsw_global(const fcs_bsw_task* tasks, int32_t n, const fcs_bsw_params* p
   for (int64_t i = 0; i < pk.b.tbytes; ++i)
     if (pk.t[i] > 4) return fail(FCS_ERR_INVALID, "[E::fcs_bsw_global] target base code > 4");
   if ((rc = check_device(device))) return rc;
-  FCS_HIP_CHECK(hipSetDevice(device));
+  FCS_SET_DEVICE((device));
   SessionLease lease;
   if ((rc = lease.acquire(device))) return rc;
   Session* S = lease.get();
@@ -1378,7 +1389,7 @@ int fcs_bsw_global_dev(const fcs_bsw_batch* b, const fcs_bsw_params* params, int
   if (b->n == 0) return FCS_OK;
   if (b->n > 0x7FFFFFFF) return fail(FCS_ERR_UNSUPPORTED, "[E::fcs_bsw_global_dev] more than 2^31-1 tasks");
   if ((rc = check_device(device))) return rc;
-  FCS_HIP_CHECK(hipSetDevice(device));
+  FCS_SET_DEVICE((device));
   BswDevBatch d;
   d.qbuf = b->qbuf;
   d.qoff = b->qoff;

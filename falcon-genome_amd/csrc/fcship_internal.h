@@ -21,6 +21,23 @@ int fail(int code, const std::string& msg);
                                              hipGetErrorString(_e));                         \
   } while (0)
 
+// The caller's current device, restored when an entry point returns (every
+// path): a host thread that drives another GPU is not switched by a call.
+struct DeviceScope {
+  int prev = -1;
+  DeviceScope() {
+    if (hipGetDevice(&prev) != hipSuccess) prev = -1;
+  }
+  ~DeviceScope() {
+    if (prev >= 0) (void)hipSetDevice(prev);
+  }
+  DeviceScope(const DeviceScope&) = delete;
+  DeviceScope& operator=(const DeviceScope&) = delete;
+};
+#define FCS_SET_DEVICE(d)                 \
+  ::fcs::DeviceScope _fcs_device_scope;   \
+  FCS_HIP_CHECK(hipSetDevice(d))
+
 // ------------------------------------------------------------ DPP cross-lane
 // CDNA (gfx9) DPP controls.  row = 16 lanes.
 enum : int {

@@ -464,6 +464,21 @@ void extend_loose(const KmerIndex& idx, const fcs_bsw_params& P, const AlignOpti
 // calls it so on the mate-rescue list, mem_matesw).
 void dedup_patch(const KmerIndex& idx, const fcs_bsw_params& P, const AlignOptions& opt,
                  const std::vector<ReadAln*>& reads, bool patch, AlignStats& st) {
+  // bwa works in its packed 2 x l_pac reference space (a reverse-strand region
+  // [rb, re) of contig c is [2 l_pac - (off_c + re), 2 l_pac - (off_c + rb)))
+  // and on original-read query coordinates; regions here hold forward
+  // reference coordinates and, on the reverse strand, coordinates of the
+  // reverse-complemented read.  Every order and comparison below is bwa's,
+  // in bwa's space.
+  struct Span2 {
+    int64_t rb, re;  // packed 2 l_pac space
+    int qb, qe;      // original read
+  };
+  auto to2 = [&](const Cand& c, int Lq) -> Span2 {
+    const int64_t o = idx.offset(c.contig), L2 = 2 * idx.l_pac();
+    if (!c.rev) return {o + c.aln.rb, o + c.aln.re, c.aln.qb, c.aln.qe};
+    return {L2 - (o + c.aln.re), L2 - (o + c.aln.rb), Lq - c.aln.qe, Lq - c.aln.qb};
+  };
   // bwa's loop `for i, for j = i - 1 down`, resumable where a patch needs its
   // global score (one GPU batch per round over all reads)
   struct Scan {
@@ -476,18 +491,16 @@ void dedup_patch(const KmerIndex& idx, const fcs_bsw_params& P, const AlignOptio
   std::vector<Scan> sc(reads.size());
   for (size_t r = 0; r < reads.size(); ++r) {
     ReadAln& R = *reads[r];
+    const int Lq = (int)R.code[0].size();
     std::vector<Cand> keep;
     for (Cand& c : R.cands)
       if (c.ok) keep.push_back(std::move(c));
     R.cands.swap(keep);
     Scan& S = sc[r];
     for (size_t k = 0; k < R.cands.size(); ++k) S.order.push_back((int)k);
-    // bwa sorts by the END position (mem_ars2), contig and strand first (its 2L coordinates)
+    // bwa sorts by the END position in its packed space (mem_ars2)
     std::stable_sort(S.order.begin(), S.order.end(), [&](int a, int b) {
-      const Cand &x = R.cands[a], &y = R.cands[b];
-      if (x.contig != y.contig) return x.contig < y.contig;
-      if (x.rev != y.rev) return x.rev < y.rev;
-      return x.aln.re < y.aln.re;
+      return to2(R.cands[a], Lq).re < to2(R.cands[b], Lq).re;
     });
     S.done = R.cands.size() <= 1;
   }
@@ -498,14 +511,17 @@ void dedup_patch(const KmerIndex& idx, const fcs_bsw_params& P, const AlignOptio
     for (size_t r = 0; r < reads.size(); ++r) {
       Scan& S = sc[r];
       ReadAln& R = *reads[r];
+      const int Lq = (int)R.code[0].size();
       while (!S.done) {
         if (S.i >= S.order.size()) {
           S.done = true;
           break;
         }
         Cand& p = R.cands[S.order[S.i]];
+        const Span2 p2 = to2(p, Lq);
+        // same rid (bwa's test) and, as the packed space implies, same strand
         auto near = [&](const Cand& q) {
-          return q.contig == p.contig && q.rev == p.rev && p.aln.rb < q.aln.re + opt.max_chain_gap;
+          return q.contig == p.contig && q.rev == p.rev && p2.rb < to2(q, Lq).re + opt.max_chain_gap;
         };
         if (S.j == -2) {
           if (!near(R.cands[S.order[S.i - 1]])) {
@@ -518,10 +534,11 @@ void dedup_patch(const KmerIndex& idx, const fcs_bsw_params& P, const AlignOptio
         for (; S.j >= 0 && near(R.cands[S.order[S.j]]); --S.j) {
           Cand& q = R.cands[S.order[S.j]];
           if (q.aln.qe == q.aln.qb) continue;  // excluded
-          const int64_t or_ = q.aln.re - p.aln.rb;
-          const int64_t oq = q.aln.qb < p.aln.qb ? q.aln.qe - p.aln.qb : p.aln.qe - q.aln.qb;
-          const int64_t mr = std::min(q.aln.re - q.aln.rb, p.aln.re - p.aln.rb);
-          const int64_t mq = std::min(q.aln.qe - q.aln.qb, p.aln.qe - p.aln.qb);
+          const Span2 q2 = to2(q, Lq);
+          const int64_t or_ = q2.re - p2.rb;
+          const int64_t oq = q2.qb < p2.qb ? q2.qe - p2.qb : p2.qe - q2.qb;
+          const int64_t mr = std::min(q2.re - q2.rb, p2.re - p2.rb);
+          const int64_t mq = std::min(q2.qe - q2.qb, p2.qe - p2.qb);
           if (or_ > redun * mr && oq > redun * mq) {  // one of the hits is redundant
             if (p.aln.score < q.aln.score) {
               p.aln.qe = p.aln.qb;
@@ -530,10 +547,10 @@ void dedup_patch(const KmerIndex& idx, const fcs_bsw_params& P, const AlignOptio
             q.aln.qe = q.aln.qb;
             continue;
           }
-          if (!patch || q.aln.rb >= p.aln.rb) continue;
+          if (!patch || q2.rb >= p2.rb) continue;
           // mem_patch_reg(q, p): colinear, a band within 2w (4w when they overlap) and a
           // relative band below 0.05 (0.10)
-          const SeedAln &a = q.aln, &b = p.aln;
+          const Span2 &a = q2, &b = p2;
           if (a.qb >= b.qb || a.qe >= b.qe || a.re >= b.re) continue;
           int w = (int)std::llabs((a.re - b.rb) - (int64_t)(a.qe - b.qb));
           const double rr = std::fabs((double)(a.re - b.rb) / (double)(b.re - a.rb) -
@@ -543,14 +560,19 @@ void dedup_patch(const KmerIndex& idx, const fcs_bsw_params& P, const AlignOptio
           } else if (w > opt.w << 2 || rr >= 0.10) {
             continue;
           }
-          S.w = std::min(w + a.w + b.w, opt.w << 2);
+          S.w = std::min(w + q.aln.w + p.aln.w, opt.w << 2);
+          // the joint span [a.rb, b.re) x [a.qb, b.qe) in bwa's space; on the
+          // reverse strand the same span of the forward reference against the
+          // reverse-complemented read (both sequences reversed and
+          // complemented: the same global score)
           GlobalScoreJob J;
           J.q = R.code[p.rev].data();
           J.ref = idx.codes(p.contig).data();
-          J.qb = a.qb;
-          J.qe = b.qe;
-          J.rb = a.rb;
-          J.re = b.re;
+          if (!p.rev) {
+            J.qb = q.aln.qb, J.qe = p.aln.qe, J.rb = q.aln.rb, J.re = p.aln.re;
+          } else {
+            J.qb = p.aln.qb, J.qe = q.aln.qe, J.rb = p.aln.rb, J.re = q.aln.re;
+          }
           J.w = S.w;
           jobs.push_back(J);
           jr.push_back(r);
@@ -571,17 +593,24 @@ void dedup_patch(const KmerIndex& idx, const fcs_bsw_params& P, const AlignOptio
     for (size_t k = 0; k < jr.size(); ++k) {
       Scan& S = sc[jr[k]];
       ReadAln& R = *reads[jr[k]];
+      const int Lq = (int)R.code[0].size();
       Cand& p = R.cands[S.order[S.i]];
       Cand& q = R.cands[S.order[S.j]];
-      const SeedAln &a = q.aln, &b = p.aln;
+      const Span2 a = to2(q, Lq), b = to2(p, Lq);
+      const int as = q.aln.score, bs = p.aln.score;
       const int score = scores[k];
       // predicted scores from the query and the reference spans; merge at >= 90% of the larger
-      const int q_s = (int)((double)(b.qe - a.qb) / ((b.qe - b.qb) + (a.qe - a.qb)) * (b.score + a.score) + .499);
-      const int r_s = (int)((double)(b.re - a.rb) / ((b.re - b.rb) + (a.re - a.rb)) * (b.score + a.score) + .499);
-      if (score > 0 && (double)score / std::max(q_s, r_s) >= 0.90) {  // merge q into p
+      const int q_s = (int)((double)(b.qe - a.qb) / ((b.qe - b.qb) + (a.qe - a.qb)) * (bs + as) + .499);
+      const int r_s = (int)((double)(b.re - a.rb) / ((b.re - b.rb) + (a.re - a.rb)) * (bs + as) + .499);
+      if (score > 0 && (double)score / std::max(q_s, r_s) >= 0.90) {  // merge q into p: p->qb = q->qb, p->rb = q->rb
         p.seedcov = std::max(p.seedcov, q.seedcov);
-        p.aln.qb = q.aln.qb;
-        p.aln.rb = q.aln.rb;
+        if (!p.rev) {
+          p.aln.qb = q.aln.qb;
+          p.aln.rb = q.aln.rb;
+        } else {  // bwa-space starts are the forward / reverse-complement ends here
+          p.aln.qe = q.aln.qe;
+          p.aln.re = q.aln.re;
+        }
         p.aln.truesc = p.aln.score = score;
         p.aln.w = S.w;
         q.aln.qb = q.aln.qe;  // excluded
@@ -591,22 +620,23 @@ void dedup_patch(const KmerIndex& idx, const fcs_bsw_params& P, const AlignOptio
   }
   for (ReadAln* Rp : reads) {
     ReadAln& R = *Rp;
+    const int Lq = (int)R.code[0].size();
     std::vector<Cand> keep;
     for (Cand& c : R.cands)
       if (c.aln.qe > c.aln.qb) keep.push_back(std::move(c));
-    // identical hits: same score and start on the query and the reference (mem_ars order)
-    std::stable_sort(keep.begin(), keep.end(), [](const Cand& x, const Cand& y) {
+    // identical hits: same score and start on the query and the reference, in
+    // bwa's order (alnreg_slt: score, then packed-space start, then query start)
+    std::stable_sort(keep.begin(), keep.end(), [&](const Cand& x, const Cand& y) {
       if (x.aln.score != y.aln.score) return x.aln.score > y.aln.score;
-      if (x.contig != y.contig) return x.contig < y.contig;
-      if (x.rev != y.rev) return x.rev < y.rev;
-      if (x.aln.rb != y.aln.rb) return x.aln.rb < y.aln.rb;
-      return x.aln.qb < y.aln.qb;
+      const Span2 a = to2(x, Lq), b = to2(y, Lq);
+      if (a.rb != b.rb) return a.rb < b.rb;
+      return a.qb < b.qb;
     });
     R.cands.clear();
     for (Cand& c : keep) {
       const Cand* prev = R.cands.empty() ? nullptr : &R.cands.back();
-      if (prev && prev->aln.score == c.aln.score && prev->contig == c.contig && prev->rev == c.rev &&
-          prev->aln.rb == c.aln.rb && prev->aln.qb == c.aln.qb)
+      if (prev && prev->aln.score == c.aln.score && to2(*prev, Lq).rb == to2(c, Lq).rb &&
+          to2(*prev, Lq).qb == to2(c, Lq).qb)
         continue;
       R.cands.push_back(std::move(c));
     }
@@ -722,7 +752,7 @@ std::array<PeStat, 4> pestat(const KmerIndex& idx, const std::vector<ReadAln>& m
     if (a.cands[0].contig != b.cands[0].contig) continue;
     int64_t dist;
     const int d = infer_dir((int64_t)idx.codes(a.cands[0].contig).size(), rb2(idx, a.cands[0]), rb2(idx, b.cands[0]), dist);
-    if (dist > 10000) continue;
+    if (dist == 0 || dist > 10000) continue;  // bwa: `if (is && is <= max_ins)`
     isize[d].push_back(dist);
   }
   std::array<PeStat, 4> pes;
@@ -1150,6 +1180,8 @@ KmerIndex::KmerIndex(const Reference& ref, int k, const std::string& index_path)
   for (const Contig& c : ref.contigs) {
     codes_.emplace_back(c.seq.size());
     for (size_t p = 0; p < c.seq.size(); ++p) codes_.back()[p] = code_of(c.seq[p]);
+    off_.push_back(l_pac_);
+    l_pac_ += (int64_t)c.seq.size();
   }
   if (!index_path.empty()) fmd_ = FmdIndex::load(index_path, codes_);
   loaded_ = fmd_ != nullptr;

@@ -87,11 +87,18 @@ class KmerIndex {
   // the contig's bases as codes 0..4 (A, C, G, T, other)
   const std::vector<uint8_t>& codes(int contig) const { return codes_[contig]; }
   const FmdIndex& fmd() const { return *fmd_; }
+  // bwa's packed-reference coordinates: the contig's start in the
+  // concatenated forward strand, and its total length l_pac (the reverse
+  // strand occupies [l_pac, 2 l_pac))
+  int64_t offset(int contig) const { return off_[contig]; }
+  int64_t l_pac() const { return l_pac_; }
 
  private:
   int k_;
   bool loaded_ = false;
   std::vector<std::vector<uint8_t>> codes_;
+  std::vector<int64_t> off_;
+  int64_t l_pac_ = 0;
   std::unique_ptr<FmdIndex> fmd_;
 };
 

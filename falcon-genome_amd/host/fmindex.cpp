@@ -178,23 +178,34 @@ FmdIndex::~FmdIndex() {
   if (map_) ::munmap(map_, map_len_);
 }
 
-// A digest of the contigs (lengths and every 997th base): a saved index is
-// used only for the reference it was built from.
+// A digest of the whole reference text (every contig's length and every base
+// code, eight codes per mixing step): a saved index is used only for the exact
+// text it was built from.  An edit that keeps the lengths (IUPAC -> N, a
+// masked or patched base) changes it.
 uint64_t FmdIndex::text_digest(const std::vector<std::vector<uint8_t>>& contigs) {
   uint64_t h = 1469598103934665603ull;
   auto mix = [&](uint64_t v) {
     h ^= v;
     h *= 1099511628211ull;
+    h ^= h >> 29;
   };
   for (const auto& c : contigs) {
     mix(c.size());
-    for (size_t i = 0; i < c.size(); i += 997) mix(c[i]);
+    const size_t n8 = c.size() / 8;
+    for (size_t i = 0; i < n8; ++i) {
+      uint64_t w;
+      std::memcpy(&w, c.data() + 8 * i, 8);
+      mix(w);
+    }
+    uint64_t tail = 0;
+    for (size_t i = 8 * n8; i < c.size(); ++i) tail = tail << 8 | c[i];
+    mix(tail);
   }
   return h;
 }
 
 namespace {
-constexpr char kFmdMagic[8] = {'F', 'C', 'S', 'F', 'M', 'D', '0', '1'};
+constexpr char kFmdMagic[8] = {'F', 'C', 'S', 'F', 'M', 'D', '0', '2'};  // 02: whole-text digest
 struct FmdHeader {
   char magic[8];
   int64_t n, flen, intv, ncontig, nocc, nsa, nspecial;
@@ -269,8 +280,19 @@ std::unique_ptr<FmdIndex> FmdIndex::load(const std::string& path, const std::vec
   off += 8 * (size_t)h.ncontig;
   ix->clen_.assign(reinterpret_cast<const int64_t*>(base + off), reinterpret_cast<const int64_t*>(base + off) + h.ncontig);
   off = align64(off + 8 * (size_t)h.ncontig);
-  for (int64_t c = 0; c < h.ncontig; ++c)
+  int64_t total = 1;
+  for (int64_t c = 0; c < h.ncontig; ++c) {
     if (ix->clen_[c] != (int64_t)contigs[c].size()) return nullptr;
+    total += ix->clen_[c] + 1;
+  }
+  // the header's sizes must be the ones this text gives (the constructor's
+  // layout), so that no lookup can leave the mapped arrays
+  const int64_t n = 2 * total + 1;
+  if (h.flen != total || h.n != n || h.nocc != 8 * ((n + 63) / 64 + 1) || h.nsa != (n + h.intv - 1) / h.intv ||
+      h.nspecial < 0 || h.nspecial > n || h.C[0] != 0 || h.C[6] != n)
+    return nullptr;
+  for (int c = 1; c < 7; ++c)
+    if (h.C[c] < h.C[c - 1]) return nullptr;
   const size_t need = align64(align64(off + 8 * (size_t)h.nocc) + 8 * (size_t)h.nsa) + 16 * (size_t)h.nspecial;
   if (need > ix->map_len_) return nullptr;
   ix->n_ = h.n;

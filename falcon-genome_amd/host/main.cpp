@@ -4,6 +4,7 @@
 // src/worker-align.cpp:29-42), config keys (`conf`) and exit codes
 // (src/main.cpp:165-240: help 0, bad option 1/2, missing file 3, failed
 // stage 4, other error -1), plus `synth` for the synthetic C1/C4/C5 inputs.
+#include <algorithm>
 #include <malloc.h>
 #include <sys/resource.h>
 #include <unistd.h>
@@ -363,6 +364,11 @@ int align_main(int argc, char** argv) {
     std::vector<std::string> rg_out;
     for (const SampleDetails& d : list) {
       const std::string out_rg = list.size() == 1 ? merged : merge_dir + "/" + sample_id + "_" + d.ReadGroup + ".bam";
+      // two read groups of one sample writing one BAM would lose one lane and
+      // merge the other twice, silently
+      if (std::find(rg_out.begin(), rg_out.end(), out_rg) != rg_out.end())
+        throw invalidParam("sample " + sample_id + " lists read group " + d.ReadGroup +
+                           " more than once (each read group is aligned to its own BAM)");
       rg_out.push_back(out_rg);
       ex.addTask(std::make_shared<BWAWorker>(ref, d.fastqR1, d.fastqR2, out_rg, extra, sample_id, d.ReadGroup,
                                              d.Platform, d.LibraryID, !disable_merge, force || list.size() > 1, gpus),

@@ -66,9 +66,11 @@ SampleSheetMap from_file(const std::string& path) {
 }
 
 // <dir>/<sample>_<anything>1.fastq.gz with its ...2.fastq.gz mate; read groups
-// RG-<sample>_<NN><NN> and libraries LIB<sample>_<NN> as the reference names
-// them (src/SampleSheet.cpp:146-200; it restarts NN at 00 and 01 only, which
-// is kept: the names are labels, the files are what matter).
+// RG-<sample>_<NN><NN> and libraries LIB<sample>_<NN>, the reference's name
+// pattern (src/SampleSheet.cpp:146-200).  The reference restarts NN at 00 and
+// 01 only, so a sample's third pair would share the second's read group; the
+// per-read-group BAM path comes from that name (align_main: <s>_<RG>.bam), so
+// here NN is the pair's index within the sample (00, 01, 02, ...).
 SampleSheetMap from_folder(const std::string& dir) {
   std::vector<std::string> r1;
   for (const std::string& f : list_dir(dir, "1.fastq.gz")) r1.push_back(basename_of(f));
@@ -81,7 +83,8 @@ SampleSheetMap from_folder(const std::string& dir) {
     const std::string sample = f.substr(0, us);
     std::string f2 = f;
     f2.replace(f2.rfind("1.fastq.gz"), std::string("1.fastq.gz").size(), "2.fastq.gz");
-    const std::string nn = out.count(sample) ? "01" : "00";
+    const size_t idx = out.count(sample) ? out[sample].size() : 0;
+    const std::string nn = (idx < 10 ? "0" : "") + std::to_string(idx);
     SampleDetails d;
     d.fastqR1 = dir + "/" + f;
     d.fastqR2 = dir + "/" + f2;

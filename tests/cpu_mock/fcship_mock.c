@@ -14,6 +14,20 @@
  * the oracle's PairHMM (oracle/pairhmm_oracle.c, slow) computes them, which lets a developer time the caller's
  * host stages (decode, pileup, regions, GVCF output) on a CPU-only machine.
  * The GPU tests run the same commands on the real library.
+ *
+ * The reference's CPU path for htc (BASELINE.json configs[0], "C1": GATK
+ * HaplotypeCaller with the CPU PairHMM, /root/reference/src/workers/
+ * HTCWorker.cpp:85,105) is timed by bench.py's cpu_baseline leg through two
+ * more modes:
+ *   FCS_MOCK_PHMM=java — GATK's Java LoglessPairHMM semantics (double
+ *     throughout, oracle_phmm_java_log10), one pair at a time;
+ *   FCS_MOCK_PHMM=gkl  — GKL's AVX-512 PairHMM restated (float pass, double
+ *     rescue below 1e-28; oracle/pairhmm_simd.c), the region's pairs as one
+ *     batch on FCS_MOCK_PHMM_THREADS OpenMP threads (default 1: the caller's
+ *     shard threads are the parallelism, as GATK's -nct processes are).
+ * Built by tests/cpu_mock/Makefile into tests/cpu_mock/build/ (never into
+ * falcon-genome_amd/), and loaded only through LD_LIBRARY_PATH of the one
+ * fcs-genome child process that a CPU test or the bench's baseline leg starts.
  */
 #include <stdlib.h>
 #include <string.h>
@@ -23,6 +37,17 @@
 int oracle_ksw_extend2(int qlen, const uint8_t* query, int tlen, const uint8_t* target, int m, const int8_t* mat,
                        int o_del, int e_del, int o_ins, int e_ins, int w, int end_bonus, int zdrop, int h0, int* qle_,
                        int* tle_, int* gtle_, int* gscore_, int* max_off_, int64_t* cells);
+double oracle_phmm_java_log10(const uint8_t* rb, const uint8_t* bq, const uint8_t* iq, const uint8_t* dq,
+                              const uint8_t* gq, int R, const uint8_t* hb, int H);
+int oracle_phmm_simd_batch(const uint8_t* rb, const uint8_t* bq, const uint8_t* iq, const uint8_t* dq,
+                           const uint8_t* gq, const int64_t* read_off, const int32_t* read_len, const uint8_t* hb,
+                           const int64_t* hap_off, const int32_t* hap_len, const int32_t* pair_read,
+                           const int32_t* pair_hap, int64_t n_pairs, float* out_raw_f, double* out_log10,
+                           int32_t* used_double, int n_threads);
+void oracle_phmm_batch(const uint8_t* rb, const uint8_t* bq, const uint8_t* iq, const uint8_t* dq, const uint8_t* gq,
+                       const int64_t* read_off, const int32_t* read_len, const uint8_t* hb, const int64_t* hap_off,
+                       const int32_t* hap_len, const int32_t* pair_read, const int32_t* pair_hap, int64_t n_pairs,
+                       float* out_raw_f, double* out_log10, int32_t* used_double, int n_threads);
 double oracle_phmm_log10(const uint8_t* rb, const uint8_t* bq, const uint8_t* iq, const uint8_t* dq, const uint8_t* gq,
                          int R, const uint8_t* hb, int H, int* used_double);
 int oracle_ksw_global2(int qlen, const uint8_t* query, int tlen, const uint8_t* target, int m, const int8_t* mat,
@@ -79,9 +104,75 @@ int fcs_bsw_global(const fcs_bsw_task* t, int32_t n, const fcs_bsw_params* p, in
 }
 
 void fcs_phmm_opts_default(fcs_phmm_opts* o) { memset(o, 0, sizeof *o); }
+
+static __thread int64_t g_rescued;
+
+/* FCS_MOCK_PHMM=gkl: one region's reads x haps as the oracle's SoA batch. */
+static int mock_gkl_region(const fcs_phmm_region* g, int threads) {
+  const int32_t nr = g->n_reads, nh = g->n_haps;
+  const int64_t np = (int64_t)nr * nh;
+  if (np == 0) return FCS_OK;
+  int64_t rbytes = 0, hbytes = 0;
+  for (int32_t r = 0; r < nr; ++r) rbytes += g->reads[r].len;
+  for (int32_t h = 0; h < nh; ++h) hbytes += g->haps[h].len;
+  uint8_t* rb = malloc(5 * (size_t)(rbytes + 1) + (size_t)hbytes + 1);
+  int64_t* ro = malloc(sizeof(int64_t) * ((size_t)nr + nh));
+  int32_t* rl = malloc(sizeof(int32_t) * ((size_t)nr + nh + 4 * (size_t)np));
+  if (!rb || !ro || !rl) {
+    free(rb), free(ro), free(rl);
+    g_err = "CPU mock: out of memory";
+    return FCS_ERR_INVALID;
+  }
+  uint8_t *bq = rb + rbytes + 1, *iq = bq + rbytes + 1, *dq = iq + rbytes + 1, *gq = dq + rbytes + 1;
+  uint8_t* hb = gq + rbytes + 1;
+  int64_t* ho = ro + nr;
+  int32_t *hl = rl + nr, *pr = hl + nh, *ph = pr + np, *ud = ph + np;
+  int64_t o = 0;
+  for (int32_t r = 0; r < nr; ++r) {
+    const fcs_phmm_read* x = &g->reads[r];
+    ro[r] = o, rl[r] = x->len;
+    memcpy(rb + o, x->bases, x->len), memcpy(bq + o, x->base_q, x->len), memcpy(iq + o, x->ins_q, x->len);
+    memcpy(dq + o, x->del_q, x->len), memcpy(gq + o, x->gcp, x->len);
+    o += x->len;
+  }
+  o = 0;
+  for (int32_t h = 0; h < nh; ++h) {
+    ho[h] = o, hl[h] = g->haps[h].len;
+    memcpy(hb + o, g->haps[h].bases, g->haps[h].len);
+    o += g->haps[h].len;
+  }
+  for (int64_t p = 0; p < np; ++p) pr[p] = (int32_t)(p / nh), ph[p] = (int32_t)(p % nh);
+  if (oracle_phmm_simd_batch(rb, bq, iq, dq, gq, ro, rl, hb, ho, hl, pr, ph, np, NULL, g->out_log10, ud, threads) < 0)
+    oracle_phmm_batch(rb, bq, iq, dq, gq, ro, rl, hb, ho, hl, pr, ph, np, NULL, g->out_log10, ud, threads);
+  for (int64_t p = 0; p < np; ++p) g_rescued += ud[p];
+  free(rb), free(ro), free(rl);
+  return FCS_OK;
+}
+
 int fcs_phmm_compute_regions(const fcs_phmm_region* regions, int32_t n_regions, const fcs_phmm_opts* opts) {
   (void)opts;
   const char* e = getenv("FCS_MOCK_PHMM");
+  g_rescued = 0;
+  if (e && strcmp(e, "gkl") == 0) {
+    const char* t = getenv("FCS_MOCK_PHMM_THREADS");
+    const int threads = t && atoi(t) > 0 ? atoi(t) : 1;
+    for (int32_t k = 0; k < n_regions; ++k) {
+      const int rc = mock_gkl_region(&regions[k], threads);
+      if (rc != FCS_OK) return rc;
+    }
+    return FCS_OK;
+  }
+  if (e && strcmp(e, "java") == 0) {
+    for (int32_t k = 0; k < n_regions; ++k)
+      for (int32_t r = 0; r < regions[k].n_reads; ++r)
+        for (int32_t h = 0; h < regions[k].n_haps; ++h) {
+          const fcs_phmm_read* x = &regions[k].reads[r];
+          const fcs_phmm_hap* y = &regions[k].haps[h];
+          regions[k].out_log10[(int64_t)r * regions[k].n_haps + h] =
+              oracle_phmm_java_log10(x->bases, x->base_q, x->ins_q, x->del_q, x->gcp, x->len, y->bases, y->len);
+        }
+    return FCS_OK;
+  }
   if (!e || (strcmp(e, "1") != 0 && strcmp(e, "2") != 0 && strcmp(e, "3") != 0)) {
     g_err = "CPU mock of libfcship: no PairHMM";
     return FCS_ERR_DEVICE;
@@ -92,8 +183,10 @@ int fcs_phmm_compute_regions(const fcs_phmm_region* regions, int32_t n_regions, 
         for (int32_t h = 0; h < regions[k].n_haps; ++h) {
           const fcs_phmm_read* x = &regions[k].reads[r];
           const fcs_phmm_hap* y = &regions[k].haps[h];
+          int ud = 0;
           regions[k].out_log10[(int64_t)r * regions[k].n_haps + h] = oracle_phmm_log10(
-              x->bases, x->base_q, x->ins_q, x->del_q, x->gcp, x->len, y->bases, y->len, NULL);
+              x->bases, x->base_q, x->ins_q, x->del_q, x->gcp, x->len, y->bases, y->len, &ud);
+          g_rescued += ud;
         }
     return FCS_OK;
   }
@@ -104,7 +197,7 @@ int fcs_phmm_compute_regions(const fcs_phmm_region* regions, int32_t n_regions, 
   return FCS_OK;
 }
 int fcs_phmm_last_rescued(int64_t* count) {
-  *count = 0;
+  *count = g_rescued;
   return FCS_OK;
 }
 int fcs_phmm_last_device_ms(double* device_ms, double* rescue_ms) {

@@ -76,3 +76,25 @@ def test_paired_split_reads_cpu(mock_env, tmp_path):
                   env=mock_env, cwd=tmp_path)
     assert p.returncode == 0, p.stderr[-3000:]
     assert A.check_chimeric_pairs(out, chim, "chr1", "chr2") >= 38
+
+
+def test_saved_index_rejected_after_same_length_edit(mock_env, tmp_path):
+    """a saved .fcsidx is used only for the exact reference text it
+    was built from.  Editing one base (contig lengths unchanged) makes align
+    build the index in memory instead of mapping the stale one."""
+    d = tmp_path / "r"
+    p = H.run_cli("synth", "-o", d, "-c", "chr20:60000,chr21:30000", "-x", "2", "--seed", "9")
+    assert p.returncode == 0, p.stderr[-2000:]
+    ref = d / "ref.fasta"
+    p = H.run_cli("index", "-r", ref, "--sa-intv", "8")
+    assert p.returncode == 0, p.stderr[-2000:]
+    fq = tmp_path / "r.fastq"
+    A.split_reads_fastq(ref, fq, n_split=1, n_whole=4, seed=2)
+    p = H.run_cli("align", "-f", "-r", ref, "-1", fq, "-o", tmp_path / "a.bam", env=mock_env, cwd=tmp_path)
+    assert p.returncode == 0 and "mapped " + str(ref) + ".fcsidx" in p.stderr, p.stderr[-2000:]
+    lines = ref.read_text().split("\n")
+    k = 1 + len(lines) // 2  # a sequence line in the middle of chr1
+    lines[k] = ("C" if lines[k][0] != "C" else "G") + lines[k][1:]
+    ref.write_text("\n".join(lines))
+    p = H.run_cli("align", "-f", "-r", ref, "-1", fq, "-o", tmp_path / "b.bam", env=mock_env, cwd=tmp_path)
+    assert p.returncode == 0 and "built in memory" in p.stderr, p.stderr[-2000:]

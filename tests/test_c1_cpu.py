@@ -1,0 +1,90 @@
+"""BASELINE.json configs[0] ("C1"): `fcs-genome htc` on a 1,000-read synthetic
+chr20 BAM with the PairHMM on the CPU — the reference's path, GATK
+HaplotypeCaller with the CPU PairHMM (/root/reference/src/workers/
+HTCWorker.cpp:85,105).  The fcs-genome child runs against the test-only CPU
+mock of libfcship.so (tests/cpu_mock: the oracle's Java LoglessPairHMM
+restatement, or its GKL-style AVX-512 restatement, behind the same C-ABI).
+Calls are checked against the generator's truth at the GPU tests' bars
+(test_host_gpu.py), and the two CPU PairHMM semantics give the same calls.
+bench.py times the same command (e2e.c1.cpu_baseline)."""
+import os
+import subprocess
+
+import pytest
+
+import host_lib as H
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+@pytest.fixture(scope="module")
+def mock_dir():
+    subprocess.run(["make", "-C", os.path.join(ROOT, "tests", "cpu_mock")], check=True, capture_output=True)
+    return os.path.join(ROOT, "tests", "cpu_mock", "build")
+
+
+@pytest.fixture(scope="module")
+def c1(tmp_path_factory):
+    d = tmp_path_factory.mktemp("c1")
+    p = H.run_cli("synth", "-o", d, "-c", "chr20:1000000", "-x", "30", "-n", "1000", "--no-fastq", "--seed", "20261015")
+    assert p.returncode == 0, p.stderr[-2000:]
+    return d
+
+
+def calls(vcf):
+    out = set()
+    for ln in open(vcf):
+        if not ln.startswith("#"):
+            f = ln.split("\t")
+            out.add((f[0], int(f[1]), f[3], f[4]))
+    return out
+
+
+def covered_truth(d):
+    """Truth variants inside the span the 1,000 reads cover (150 bp in from
+    either end, where a variant can still be seen by >= 2 reads)."""
+    _, _, recs = H.read_bam(d / "sample.bam")
+    lo = min(r["pos"] for r in recs) + 150
+    hi = max(r["pos"] + H.cigar_ref_len(r["cigar"]) for r in recs) - 150
+    out = set()
+    for ln in (d / "truth.vcf").read_text().splitlines():
+        if not ln.startswith("#"):
+            f = ln.split("\t")
+            if lo < int(f[1]) <= hi:
+                out.add((f[0], int(f[1]), f[3], f[4]))
+    return out, len(recs), (lo, hi)
+
+
+def run_cpu(mode, c1, mock_dir, tmp_path, name):
+    out = tmp_path / f"{name}.vcf"
+    env = {"LD_LIBRARY_PATH": mock_dir, "FCS_GPU_DEVICES": "0", "FCS_MOCK_PHMM": mode,
+           "FCS_LOG_DIR": str(tmp_path / f"log_{name}")}
+    p = H.run_cli("htc", "-f", "-r", c1 / "ref.fasta", "-i", c1 / "sample.bam", "-o", out, "-v", env=env,
+                  cwd=tmp_path)
+    assert p.returncode == 0, p.stderr[-3000:]
+    return out
+
+
+def test_c1_htc_cpu_java_pairhmm(c1, mock_dir, tmp_path):
+    out = run_cpu("java", c1, mock_dir, tmp_path, "java")
+    t, n_reads, (lo, hi) = covered_truth(c1)
+    assert n_reads == 1000
+    c = {v for v in calls(out) if lo < v[1] <= hi}
+    assert len(t) >= 3, t  # the covered span holds some variants
+    snv = {v for v in t if len(v[2]) == len(v[3]) == 1}
+    tp = len(t & c)
+    assert len(snv & c) / len(snv) >= 0.95, (sorted(snv - c), sorted(c))
+    assert tp / len(t) >= 0.9, (sorted(t - c), sorted(c))
+    assert tp / max(1, len(c)) >= 0.95, (sorted(c - t), sorted(t))
+    # bgzip + tabix tail ran as on the GPU path
+    assert (tmp_path / "java.vcf.gz").exists() and (tmp_path / "java.vcf.gz.tbi").exists()
+
+
+def test_c1_java_and_gkl_semantics_agree(c1, mock_dir, tmp_path):
+    """GATK's Java LoglessPairHMM (double) and GKL's AVX float pass with the
+    double rescue differ by <= 1e-5 relative in log10; the calls are the same."""
+    a = run_cpu("java", c1, mock_dir, tmp_path, "java")
+    b = run_cpu("gkl", c1, mock_dir, tmp_path, "gkl")
+    strip = lambda f: [ln for ln in open(f) if not ln.startswith("##")]  # noqa: E731
+    assert calls(a) == calls(b)
+    assert strip(a) == strip(b)

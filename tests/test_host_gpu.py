@@ -456,3 +456,36 @@ def test_align_disable_merge_buckets_feed_htc(gpu, data, tmp_path):
     assert p.returncode == 0, p.stderr[-3000:]
     t = truth(data, False)
     assert len(t & calls(vcf)) / len(t) >= 0.88
+
+
+def test_c1_gpu_calls_equal_cpu_path(gpu, tmp_path):
+    """C1 (BASELINE.json configs[0]) on the GPU gives the calls of the
+    reference's CPU PairHMM path (GATK Java LoglessPairHMM semantics, run
+    through the test-only CPU mock of the C-ABI, tests/cpu_mock), and every
+    likelihood the GPU caller used is within 1e-5 of the Java-semantics value."""
+    import subprocess
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    subprocess.run(["make", "-C", os.path.join(root, "tests", "cpu_mock")], check=True, capture_output=True)
+    d = tmp_path / "c1"
+    p = H.run_cli("synth", "-o", d, "-c", "chr20:1000000", "-x", "30", "-n", "1000", "--no-fastq", "--seed",
+                  "20261015")
+    assert p.returncode == 0, p.stderr[-2000:]
+    outs = {}
+    for name, env in (("gpu", ENV), ("cpu", {"LD_LIBRARY_PATH": os.path.join(root, "tests", "cpu_mock", "build"),
+                                             "FCS_GPU_DEVICES": "0", "FCS_MOCK_PHMM": "java"})):
+        out = tmp_path / f"{name}.vcf"
+        extra = ["--dump-regions", tmp_path / "dump"] if name == "gpu" else []
+        p = H.run_cli("htc", "-f", "-r", d / "ref.fasta", "-i", d / "sample.bam", "-o", out, "-v", *extra, env=env,
+                      cwd=tmp_path)
+        assert p.returncode == 0, p.stderr[-3000:]
+        outs[name] = [ln for ln in out.read_text().splitlines() if not ln.startswith("##")]
+    assert outs["gpu"] == outs["cpu"]
+    checked = 0
+    for f in sorted(tmp_path.glob("dump.*")):
+        for reads, haps, lik in read_dump(f):
+            for r in range(len(reads)):
+                for h in range(len(haps)):
+                    ref = oracle_lib.phmm_java_log10(reads[r], haps[h])
+                    assert abs(lik[r, h] - ref) <= 1e-5 * abs(ref), (lik[r, h], ref)
+                    checked += 1
+    assert checked > 100

@@ -172,13 +172,34 @@ def test_sample_sheet_file(tmp_path):
 def test_sample_sheet_folder(tmp_path):
     """A folder of <sample>_..._1.fastq.gz / _2.fastq.gz pairs (src/SampleSheet.cpp:123-200)."""
     for n in ("S1_L001_1.fastq.gz", "S1_L001_2.fastq.gz", "S1_L002_1.fastq.gz", "S1_L002_2.fastq.gz",
-              "S2_L001_1.fastq.gz", "S2_L001_2.fastq.gz", "notes.txt"):
+              "S1_L003_1.fastq.gz", "S1_L003_2.fastq.gz", "S2_L001_1.fastq.gz", "S2_L001_2.fastq.gz", "notes.txt"):
         (tmp_path / n).write_bytes(b"")
     got = _sheet(tmp_path)
     d = str(tmp_path)
+    # NN is the pair's index within the sample: a third pair gets its own read
+    # group (the reference restarts at 01, and align's per-RG BAM path would
+    # then collide — ADVICE r3)
     assert got == [["S1", d + "/S1_L001_1.fastq.gz", d + "/S1_L001_2.fastq.gz", "RG-S1_0000", "Illumina", "LIBS1_00"],
                    ["S1", d + "/S1_L002_1.fastq.gz", d + "/S1_L002_2.fastq.gz", "RG-S1_0101", "Illumina", "LIBS1_01"],
+                   ["S1", d + "/S1_L003_1.fastq.gz", d + "/S1_L003_2.fastq.gz", "RG-S1_0202", "Illumina", "LIBS1_02"],
                    ["S2", d + "/S2_L001_1.fastq.gz", d + "/S2_L001_2.fastq.gz", "RG-S2_0000", "Illumina", "LIBS2_00"]]
+    assert len({r[3] for r in got if r[0] == "S1"}) == 3
+
+
+def test_align_rejects_duplicate_read_group(tmp_path):
+    """Two sheet rows of one sample with the same read group would write the
+    same per-read-group BAM: align refuses the sheet (exit 1, invalid
+    parameter) before aligning anything."""
+    ref = tmp_path / "ref"
+    p = H.run_cli("synth", "-o", ref, "-c", "chr1:20000", "-x", "1", "--seed", "3")
+    assert p.returncode == 0, p.stderr[-2000:]
+    sheet = tmp_path / "s.csv"
+    fq = ref / "sample.fastq"
+    sheet.write_text("#sample_id,fastq1,fastq2,rg,platform_id,library_id\n"
+                     f"S,{fq},{fq},rgA,illumina,libA\nS,{fq},{fq},rgA,illumina,libB\n")
+    p = H.run_cli("align", "-r", ref / "ref.fasta", "-F", sheet, "-o", tmp_path / "out", cwd=tmp_path,
+                  env={"FCS_GPU_DEVICES": "0"})
+    assert p.returncode != 0 and "more than once" in p.stderr, (p.returncode, p.stderr[-2000:])
 
 
 def test_merge_sorted_bams(tmp_path):
