@@ -77,14 +77,28 @@ def load_pmc_phmm():
         return {}, None
 
 
+def fetch_factor():
+    """HBM read bytes per FETCH_SIZE byte on gfx950, measured by
+    tools/micro/fetch_calib.hip (profiles/fetch_calibration.json): 2."""
+    try:
+        with open(os.path.join(ROOT, "profiles", "fetch_calibration.json")) as f:
+            return 1.0 / float(json.load(f)["fetch_size_fraction_of_bytes"])
+    except (OSError, ValueError, KeyError):
+        return 1.0
+
+
 def load_traffic(name):
-    """Per-launch HBM bytes of a kernel from a committed rocprofv3 PMC summary."""
+    """Per-launch HBM bytes of a kernel from a committed rocprofv3 PMC summary:
+    fetch_factor() x FETCH_SIZE + WRITE_SIZE."""
     path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     try:
         with open(path) as f:
-            return json.load(f).get(name)
+            t = json.load(f)
     except (OSError, ValueError):
         return None
+    if name == "phmm_fwd_fp32" and "fetch_kib" in t and "write_kib" in t:
+        return int(round((fetch_factor() * t["fetch_kib"] + t["write_kib"]) * 1024))
+    return t.get(name)
 
 
 def bench_phmm(args, dev, rk):
@@ -263,7 +277,7 @@ def vcf_calls(path):
     return out
 
 
-def htc_cpu_baseline(exe, env, work, ref, bam, gpu_out, modes=("gkl", "java"), vcf=False):
+def htc_cpu_baseline(exe, env, work, ref, bam, gpu_out, modes=("gkl", "java"), vcf=False, tag="c4"):
     """`fcs-genome htc` with the PairHMM on the host CPU (BASELINE.json
     configs[0]'s path: GATK HaplotypeCaller with --native-pair-hmm-threads,
     /root/reference/src/workers/HTCWorker.cpp:85,105), same command, genome and
@@ -275,8 +289,10 @@ def htc_cpu_baseline(exe, env, work, ref, bam, gpu_out, modes=("gkl", "java"), v
     gpu_calls = vcf_calls(gpu_out)
     res = {}
     for m in modes:
-        o = os.path.join(work, f"htc_cpu_{m}" + (".vcf" if vcf else ".g.vcf"))
-        logd = os.path.join(work, f"log_cpu_{m}")
+        import shutil
+        o = os.path.join(work, f"htc_cpu_{tag}_{m}" + (".vcf" if vcf else ".g.vcf"))
+        logd = os.path.join(work, f"log_cpu_{tag}_{m}")
+        shutil.rmtree(logd, ignore_errors=True)
         e = dict(cenv, FCS_MOCK_PHMM=m, FCS_LOG_DIR=logd)
         t0 = time.perf_counter()
         r = subprocess.run([exe, "htc", "-f", "-r", ref, "-i", bam, "-o", o] + (["-v"] if vcf else []),
@@ -310,6 +326,8 @@ def bench_c1(exe, env, work, seed):
     subprocess.run([exe, "synth", "-o", c1, "-c", "chr20:1000000", "-x", "30", "-n", "1000", "--no-fastq",
                     "--seed", str(seed)], env=env, check=True, capture_output=True)
     logd = os.path.join(work, "log_c1")
+    import shutil
+    shutil.rmtree(logd, ignore_errors=True)
     t0 = time.perf_counter()
     r = subprocess.run([exe, "htc", "-f", "-r", c1 + "/ref.fasta", "-i", c1 + "/sample.bam", "-o", work + "/c1.vcf",
                         "-v"], env=dict(env, FCS_LOG_DIR=logd), capture_output=True, text=True, cwd=work)
@@ -322,8 +340,7 @@ def bench_c1(exe, env, work, seed):
     out = {"workload": "C1: fcs-genome htc -v on a 1,000-read synthetic chr20 BAM (chr20-like 1 Mbp reference, "
                        "the first 1,000 reads of a 30x sample)", "gpu": gpu}
     out["cpu_baseline"] = htc_cpu_baseline(exe, env, work, c1 + "/ref.fasta", c1 + "/sample.bam", work + "/c1.vcf",
-                                           modes=("java", "gkl"),
-                                           vcf=True)
+                                           modes=("java", "gkl"), vcf=True, tag="c1")
     return out
 
 
@@ -527,9 +544,10 @@ def bsw_roofline(r3, rf):
            "hbm_GBs": round(r3["bytes"] / (r3["ms"] * 1e-3) / 1e9, 2),
            "hbm_frac": round(r3["bytes"] / (r3["ms"] * 1e-3) / 1e9 / HBM_PEAK_GBS, 5)}
     c3m = meas.get("c3", {})
-    if c3m.get("hbm_bytes_per_batch"):
-        out["traffic"] = c3m["hbm_bytes_per_batch"]
-        out["traffic_note"] = "FETCH_SIZE + WRITE_SIZE of one C3 batch (profiles/pmc_bsw.json)"
+    if c3m.get("fetch_kib") and c3m.get("write_kib"):
+        out["traffic"] = int(round((fetch_factor() * c3m["fetch_kib"] + c3m["write_kib"]) * 1024))
+        out["traffic_note"] = ("2 x FETCH_SIZE + WRITE_SIZE of one C3 batch (profiles/pmc_bsw.json; the x2 is the "
+                               "gfx950 FETCH_SIZE calibration, profiles/fetch_calibration.json)")
     if per3:
         ach = r3["gcups"] * 1e9 * per3
         out.update(achieved=round(ach / 1e12, 3), frac=round(ach / VALU_LANE_INSTR_PEAK, 4),
@@ -750,10 +768,13 @@ def main():
         "roofline": {"bound": "valu", "achieved": round(achieved_tf, 3), "peak": FP32_VECTOR_PEAK_TF,
                      "unit": "TFLOP/s", "frac": round(achieved_tf / FP32_VECTOR_PEAK_TF, 4),
                      "traffic": traffic,
+                     "traffic_note": "HBM bytes per forward pass: 2 x FETCH_SIZE + WRITE_SIZE from separate rocprofv3 "
+                                     "--pmc passes (profiles/pmc_traffic.json; the x2 is the gfx950 FETCH_SIZE "
+                                     "calibration, profiles/fetch_calibration.json)",
                      "kernel": "phmm3_kernel (row-streamed segments, two read rows per lane, packed FP32): fp32 forward pass = one launch "
                                "per launch class, overlapped on 4 streams; achieved = algorithmic FLOPs / pass "
-                               "time (HIP events on the launch stream; rocprof pass span in "
-                               "profiles/r3/r3x_phmm_summary.json)",
+                               "time (HIP events on the launch stream; rocprofv3 kernel stats of this bench in "
+                               "profiles/r4/)",
                      "valu_instr_per_cell": vipc,
                      "valu_issue_frac": (round(ph["cells"] / fwd_s * vipc / VALU_LANE_INSTR_PEAK, 4) if vipc
                                          else None),
@@ -787,8 +808,9 @@ def main():
             "tasks": g["tasks"], "w": g["w"], "band_cells": g["cells"],
             "scores_gcups": g["scores"]["gcups"], "scores_ms": g["scores"]["ms"],
             "cigar_gcups": g["cigar"]["gcups"], "cigar_ms": g["cigar"]["ms"],
-            "kernel": "bsw_global_lane_kernel<33> (one task per lane, band in registers, nibble direction rows) + "
-                      "bsw_traceback_kernel; wider bands go to bsw_global_kernel (one wave per task)"}
+            "kernel": "bsw_global_lane_kernel<33> (one task per lane, band in registers, nibble direction rows "
+                      "interleaved across the wave's 64 tasks, bwa's traceback fused at the end of the same launch); "
+                      "wider bands go to bsw_global_kernel (one wave per task) + bsw_traceback_kernel"}
         gm = {}
         try:
             gm = json.load(open(os.path.join(ROOT, "profiles", "pmc_bsw.json"))).get("global", {})

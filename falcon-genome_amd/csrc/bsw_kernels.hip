@@ -273,6 +273,124 @@ __device__ __forceinline__ uint32_t* glane_zrow0(uint8_t* zbuf, const int64_t* z
   return reinterpret_cast<uint32_t*>(((uintptr_t)(zbuf + zoff[task]) + 3) & ~(uintptr_t)3);
 }
 
+// Where a lane-path task's nibble dwords live: dword d of row i at
+// base + i * rs + d * ds.
+//  * interleaved (every existing task of the 64-task wave takes the lane path
+//    and their direction regions are contiguous and large enough): the wave's
+//    tasks share the union of their regions, dword d of row i of lane L at
+//    start + (i * ndw + d) * 64 + L — each row's stores are 64 consecutive
+//    dwords, and the traceback walks, which all move up from the last row,
+//    read neighbouring lines;
+//  * otherwise the task's own region, row i at zrow0 + i * nd.
+// Both the DP and the traceback compute it from the same inputs (the wave
+// partition is task / 64 in every launch).
+struct GLayout {
+  uint32_t* base;
+  int rs, ds;
+};
+__device__ __forceinline__ GLayout glane_layout(const BswDevBatch& b, const BswParams& p, uint8_t* zbuf,
+                                                const int64_t* __restrict__ zoff, long long task, bool ok) {
+  const int lane = (int)(threadIdx.x & 63);
+  const bool exists = task < b.n;
+  int w = 0, tlen = 0;
+  int64_t z0 = 0, zend = 0;
+  bool good = !exists || ok;
+  if (exists) {
+    const int qlen = b.qlen[task];
+    w = b.w[task];
+    tlen = b.tlen[task];
+    z0 = zoff[task];
+    zend = z0 + (int64_t)min(qlen, 2 * w + 1) * tlen;
+    if (lane < 63 && task + 1 < b.n && zoff[task + 1] != zend) good = false;
+  }
+  const int ndw = (2 * wave_max(exists ? w : 0) + 1 + 7) >> 3;
+  const int tmax = wave_max(tlen);
+  const int last = 63 - __builtin_clzll(__ballot(exists));  // highest lane holding a task
+  const int64_t start = (int64_t)(((uint64_t)(uint32_t)read_lane((int)(z0 >> 32), 0) << 32) |
+                                  (uint32_t)read_lane((int)z0, 0));
+  const int64_t end = (int64_t)(((uint64_t)(uint32_t)read_lane((int)(zend >> 32), last) << 32) |
+                                (uint32_t)read_lane((int)zend, last));
+  const bool il = __ballot(!good) == 0ull && 4LL * 64 * ndw * tmax + 3 <= end - start;
+  GLayout L;
+  if (il) {
+    L.base = reinterpret_cast<uint32_t*>(((uintptr_t)(zbuf + start) + 3) & ~(uintptr_t)3) + lane;
+    L.rs = ndw * 64;
+    L.ds = 64;
+  } else {
+    L.base = ok ? glane_zrow0(zbuf, zoff, task) : nullptr;
+    L.rs = (2 * w + 1 + 7) >> 3;
+    L.ds = 1;
+  }
+  return L;
+}
+
+// bwa's traceback (ksw_global2) of a lane-path task, one lane per task, on its
+// nibble rows: bwa's byte (row i, band offset c) is cell k = beg_i + c - i + w
+// of nibble row i; c past the row's band end reads 0, as bwa's zeroed bytes
+// there do; a column left of the row's band start indexes bwa's flat matrix
+// backwards into the rows above (row-major, n_col bytes a row), as bwa does.
+__device__ __forceinline__ void glane_traceback(const GLayout& L, int qlen, int tlen, int w,
+                                                uint32_t* __restrict__ cg, int cap, int32_t* __restrict__ n_out) {
+  const int n_col = min(qlen, 2 * w + 1);
+  const long long zsize = (long long)n_col * tlen;
+  int crow = -1, cdw = -1;
+  uint32_t cval = 0;
+  auto byte_at = [&](int i, int k) -> int {
+    int r = i, c = k - (i > w ? i - w : 0);
+    if (c < 0 || c >= n_col) {  // bwa's flat index left of the band: an earlier row's bytes
+      const long long zi = (long long)i * n_col + c;
+      if (zi < 0 || zi >= zsize) return 0;
+      r = (int)(zi / n_col);
+      c = (int)(zi - (long long)r * n_col);
+    }
+    const int beg = r > w ? r - w : 0, end = r + w + 1 < qlen ? r + w + 1 : qlen;
+    if (beg + c >= end) return 0;
+    const int kb = beg + c - r + w;
+    const int dw = kb >> 3;
+    if (r != crow || dw != cdw) {
+      crow = r, cdw = dw;
+      cval = L.base[(long long)r * L.rs + dw * L.ds];
+    }
+    const int nbl = (int)((cval >> (4 * (kb & 7))) & 15u);
+    return (nbl & 3) | ((nbl >> 2) & 1) << 2 | ((nbl >> 3) & 1) << 5;
+  };
+  int n = 0, which = 0, curop = -1;
+  uint32_t curlen = 0;
+  auto push = [&](int op, int len) {
+    if (op == curop) {
+      curlen += (uint32_t)len;
+    } else {
+      if (curop >= 0) {
+        if (n < cap) cg[n] = curlen << 4 | (uint32_t)curop;
+        ++n;
+      }
+      curop = op;
+      curlen = (uint32_t)len;
+    }
+  };
+  int i = tlen - 1;
+  int k = (i + w + 1 < qlen ? i + w + 1 : qlen) - 1;
+  while (i >= 0 && k >= 0) {
+    which = byte_at(i, k) >> (which << 1) & 3;
+    if (which == 0) push(0, 1), --i, --k;
+    else if (which == 1) push(2, 1), --i;
+    else push(1, 1), --k;
+  }
+  if (i >= 0) push(2, i + 1);
+  if (k >= 0) push(1, k + 1);
+  if (curop >= 0) {
+    if (n < cap) cg[n] = curlen << 4 | (uint32_t)curop;
+    ++n;
+  }
+  const int nn = n < cap ? n : cap;
+  for (int a = 0; a < nn >> 1; ++a) {
+    const uint32_t t = cg[a];
+    cg[a] = cg[nn - 1 - a];
+    cg[nn - 1 - a] = t;
+  }
+  *n_out = n;
+}
+
 // FCS_GLANE_ARITH (default): the row's direction bits and the masked row's
 // band selects as sign-bit arithmetic and v_bitop3_b32 selects (full rate)
 // instead of compares feeding v_cndmask (the compiler's VOP2 form costs ~7
@@ -370,7 +488,9 @@ __device__ __forceinline__ void glane_row(int (&Hd)[NB], int (&Ed)[NB + 1], cons
 
 template <int NB, bool CIG>
 __device__ void glane_run(const BswDevBatch& b, const BswParams& p, long long task, bool ok,
-                          int32_t* __restrict__ scores, uint8_t* __restrict__ zbuf, const int64_t* __restrict__ zoff) {
+                          int32_t* __restrict__ scores, uint8_t* __restrict__ zbuf, const int64_t* __restrict__ zoff,
+                          uint32_t* __restrict__ cigar, const int64_t* __restrict__ cigar_off,
+                          const int32_t* __restrict__ cigar_cap, int32_t* __restrict__ n_cigar) {
   constexpr int NQ = (NB + 4) / 4, NW = (NB + 7) / 8;
   int qlen = 0, tlen = 0, w = 0;
   const uint8_t* __restrict__ q = nullptr;
@@ -385,7 +505,8 @@ __device__ void glane_run(const BswDevBatch& b, const BswParams& p, long long ta
   const int tmax = wave_max(tlen);
   const int oe_del = p.o_del + p.e_del, oe_ins = p.o_ins + p.e_ins, e_del = p.e_del, e_ins = p.e_ins;
   const int nb = 2 * w + 1, nd = (nb + 7) >> 3;
-  uint32_t* __restrict__ z = (CIG && ok) ? glane_zrow0(zbuf, zoff, task) : nullptr;
+  GLayout zl{nullptr, 0, 0};
+  if constexpr (CIG) zl = glane_layout(b, p, zbuf, zoff, task, ok);
   int Hd[NB], Ed[NB + 1];
   uint32_t Qb[NQ], nib[NW];
   auto qbyte = [&](int j) -> uint32_t { return (ok && j >= 0 && j < qlen) ? 5u * (uint32_t)q[j] : 0u; };
@@ -431,10 +552,10 @@ __device__ void glane_run(const BswDevBatch& b, const BswParams& p, long long ta
       glane_row<NB, CIG, true>(Hd, Ed, Qb, nib, rowpack, lo, hi, hb, oe_del, oe_ins, e_del, e_ins, h1);
     if constexpr (CIG) {
       if (live) {
-        uint32_t* const zr = z + (long long)i * nd;
+        uint32_t* const zr = zl.base + (long long)i * zl.rs;
 #pragma unroll
         for (int d = 0; d < NW; ++d)
-          if (d < nd) zr[d] = nib[d];
+          if (d < nd) zr[d * zl.ds] = nib[d];
       }
     }
     // next row's query bytes: the band moves one column right
@@ -444,6 +565,13 @@ __device__ void glane_run(const BswDevBatch& b, const BswParams& p, long long ta
   }
   // bwa: score = eh[qlen].h, written by the last row when its band reaches qlen
   if (ok) scores[task] = qlen <= tlen + w ? h1 : kMinusInf;
+  if constexpr (CIG) {
+    // the traceback of the task's own rows, read back by the lane that wrote
+    // them (stores complete before the loads)
+    __builtin_amdgcn_s_waitcnt(0);
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    if (ok) glane_traceback(zl, qlen, tlen, w, cigar + cigar_off[task], cigar_cap[task], n_cigar + task);
+  }
 }
 
 // One launch per band class (each with its own register budget): a wave runs
@@ -451,7 +579,11 @@ __device__ void glane_run(const BswDevBatch& b, const BswParams& p, long long ta
 template <int NB, bool CIG>
 __global__ __launch_bounds__(64) void bsw_global_lane_kernel(const BswDevBatch b, const BswParams p,
                                                              int32_t* __restrict__ scores, uint8_t* __restrict__ zbuf,
-                                                             const int64_t* __restrict__ zoff) {
+                                                             const int64_t* __restrict__ zoff,
+                                                             uint32_t* __restrict__ cigar,
+                                                             const int64_t* __restrict__ cigar_off,
+                                                             const int32_t* __restrict__ cigar_cap,
+                                                             int32_t* __restrict__ n_cigar) {
   const long long task = (long long)blockIdx.x * 64 + threadIdx.x;
   bool ok = false;
   int w = -1;
@@ -462,7 +594,7 @@ __global__ __launch_bounds__(64) void bsw_global_lane_kernel(const BswDevBatch b
   const int nbw = 2 * wave_max(ok ? w : -1) + 1;
   constexpr int lo = NB == 17 ? 0 : NB == 33 ? 17 : 33;
   if (nbw <= lo || nbw > NB) return;
-  glane_run<NB, CIG>(b, p, task, ok, scores, zbuf, zoff);
+  glane_run<NB, CIG>(b, p, task, ok, scores, zbuf, zoff, cigar, cigar_off, cigar_cap, n_cigar);
 }
 
 template <int NS>
@@ -477,6 +609,8 @@ __device__ void global_task(const BswDevBatch& b, const BswParams& p, long long 
   const int e_del = p.e_del, e_ins = p.e_ins;
   const int n_col = qlen < 2 * w + 1 ? qlen : 2 * w + 1;
   uint8_t* __restrict__ z = zbuf ? zbuf + zoff[task] : nullptr;
+  if (z)  // bwa's traceback may read cells outside the band: they read 0 (the oracle zeroes its matrix too)
+    for (long long x = lane; x < (long long)n_col * tlen; x += 64) z[x] = 0;
   int H[NS], E[NS], plo[NS], phi[NS];
 #pragma unroll
   for (int k = 0; k < NS; ++k) {
@@ -577,24 +711,12 @@ __global__ void bsw_traceback_kernel(const BswDevBatch b, const BswParams p, uin
   const long long task = (long long)blockIdx.x * blockDim.x + threadIdx.x;
   if (task >= b.n) return;
   const int qlen = b.qlen[task], tlen = b.tlen[task], w = b.w[task];
+  // lane-path tasks were traced back by bsw_global_lane_kernel itself
+  if (glane_ok(qlen, tlen, w, p.lane_ok != 0)) return;
   const int n_col = qlen < 2 * w + 1 ? qlen : 2 * w + 1;
   const uint8_t* z = zbuf + zoff[task];
   const long long zsize = (long long)n_col * (tlen > 0 ? tlen : 0);
-  // the lane kernel's nibble rows: bwa's byte (row i, band offset c) is cell
-  // k = beg_i + c - i + w of nibble row i; c past the row's band end reads 0,
-  // as bwa's zeroed bytes there do
-  const bool lane = glane_ok(qlen, tlen, w, p.lane_ok != 0);
-  const uint32_t* const zl = lane ? glane_zrow0(zbuf, zoff, task) : nullptr;
-  const int nd = (2 * w + 1 + 7) >> 3;
-  auto zbyte = [&](long long zi) -> int {
-    if (!lane) return z[zi];
-    const int r = (int)(zi / n_col), c = (int)(zi - (long long)r * n_col);
-    const int beg = r > w ? r - w : 0, end = r + w + 1 < qlen ? r + w + 1 : qlen;
-    if (beg + c >= end) return 0;
-    const int k = beg + c - r + w;
-    const int nbl = (int)((zl[(long long)r * nd + (k >> 3)] >> (4 * (k & 7))) & 15u);
-    return (nbl & 3) | ((nbl >> 2) & 1) << 2 | ((nbl >> 3) & 1) << 5;
-  };
+  auto zbyte = [&](long long zi) -> int { return z[zi]; };
   uint32_t* cg = cigar + cigar_off[task];
   const int cap = cigar_cap[task];
   int n = 0, which = 0, curop = -1;
@@ -644,7 +766,8 @@ int launch_bsw_global(const BswDevBatch& b, const BswParams& p, int max_qlen, in
                       const int32_t* cigar_cap, int32_t* n_cigar, hipStream_t s) {
   if (b.n <= 0) return FCS_OK;
   if (max_qlen > 1023) return fail(FCS_ERR_UNSUPPORTED, "[E::fcship] ksw_global2: qlen > 1023 unsupported");
-  if (zbuf && zbytes > 0) FCS_HIP_CHECK(hipMemsetAsync(zbuf, 0, (size_t)zbytes, s));
+  (void)zbytes;  // no arena-wide memset: lane-path tasks write every nibble their traceback reads, and the
+                // wave kernel zeroes its own tasks' regions
   const size_t lds = (size_t)((max_tlen + 64 + 15) / 16) * 16;
   if (lds > 64 * 1024) return fail(FCS_ERR_UNSUPPORTED, "[E::fcship] ksw_global2: tlen too large");
   // grid-stride over the sorted tail; 2048 waves (2 per SIMD) fill the chip,
@@ -656,7 +779,8 @@ int launch_bsw_global(const BswDevBatch& b, const BswParams& p, int max_qlen, in
   const long long lane_waves = (b.n + 63) / 64;
   if (lane_waves > 0x7FFFFFFFLL) return fail(FCS_ERR_UNSUPPORTED, "[E::fcship] ksw_global2: batch too large");
   auto lane_launch = [&](auto kern) -> int {
-    hipLaunchKernelGGL(kern, dim3((unsigned)lane_waves), dim3(64), 0, s, b, p, scores, zbuf, zoff);
+    hipLaunchKernelGGL(kern, dim3((unsigned)lane_waves), dim3(64), 0, s, b, p, scores, zbuf, zoff, cigar, cigar_off,
+                       cigar_cap, n_cigar);
     FCS_HIP_CHECK(hipGetLastError());
     return FCS_OK;
   };

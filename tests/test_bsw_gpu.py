@@ -291,3 +291,54 @@ def test_extend_multi_device_static_partition(gpu):
     assert np.array_equal(one, ref)
     for devs in ([0, 0], [0, 0, 0, 0]):
         assert np.array_equal(fcship.bsw_extend_tasks(t, devices=devs), ref)
+
+
+@pytest.mark.parametrize("gap", [0, 24])
+def test_global_dev_direction_layouts(gpu, gap):
+    """fcs_bsw_global_dev with caller-sized direction regions filled with
+    garbage (0xA5: nothing may rely on a zeroed arena).  gap 0: contiguous
+    regions, so 64-task waves whose tasks all take the lane path share them in
+    the interleaved row layout; gap 24: a gap after every region, so each task
+    keeps its own rows.  Mixed bands put wave-path tasks in some waves.  Scores
+    and CIGARs bit-exact against the oracle either way."""
+    import torch
+    rng = np.random.default_rng(90 + gap)
+    items = []
+    for k in range(700):
+        w = 16 if k % 9 else int(rng.integers(40, 120))  # mostly lane-path bands, some wave-path
+        qlen = 151
+        tlen = 151 - (3 if k % 7 == 0 else 0)
+        q, t = related_pair(rng, qlen, tlen, sub=0.01, indel=0.01)
+        items.append((q, t, 1, w))
+    t = fcship.make_tasks(items)
+    n = t.n
+    dev = torch.device("cuda", 0)
+    keep = {k: torch.from_numpy(np.ascontiguousarray(getattr(t, k))).to(dev)
+            for k in ("qbuf", "qoff", "qlen", "tbuf", "toff", "tlen", "h0", "w")}
+    b = t.to_struct()
+    for k, v in keep.items():
+        setattr(b, k, v.data_ptr())
+    zsz = np.minimum(t.qlen.astype(np.int64), 2 * t.w.astype(np.int64) + 1) * t.tlen
+    zoff = np.concatenate([[0], np.cumsum(zsz + gap)[:-1]]).astype(np.int64)
+    ztot = int(zoff[-1] + zsz[-1] + gap)
+    zbuf = torch.full((ztot,), 0xA5, dtype=torch.uint8, device=dev)
+    cap = (t.qlen + t.tlen + 2).astype(np.int32)
+    coff = np.concatenate([[0], np.cumsum(cap.astype(np.int64))[:-1]]).astype(np.int64)
+    cig = torch.zeros(int(cap.sum()), dtype=torch.int32, device=dev)
+    ncig = torch.zeros(n, dtype=torch.int32, device=dev)
+    scores = torch.zeros(n, dtype=torch.int32, device=dev)
+    d_zoff, d_coff, d_cap = (torch.from_numpy(x).to(dev) for x in (zoff, coff, cap))
+    params = fcship.bsw_params()
+    s = torch.cuda.current_stream(dev)
+    fcship.check(fcship.lib.fcs_bsw_global_dev(fcship.C.byref(b), fcship.C.byref(params), scores.data_ptr(),
+                                               zbuf.data_ptr(), ztot, d_zoff.data_ptr(), cig.data_ptr(),
+                                               d_coff.data_ptr(), d_cap.data_ptr(), ncig.data_ptr(), 0, s.cuda_stream))
+    torch.cuda.synchronize(dev)
+    sc, cg, nc = scores.cpu().numpy(), cig.cpu().numpy().view(np.uint32), ncig.cpu().numpy()
+    m = fcship.default_mat()
+    for k in range(n):
+        q, tg, _, ww = t.task(k)
+        rs, rc = oracle_lib.ksw_global2(q, tg, ww, m)
+        assert sc[k] == rs, f"task {k}: score {sc[k]} != {rs}"
+        got = cg[coff[k]:coff[k] + nc[k]]
+        assert np.array_equal(got, rc), f"task {k}: {fcship.cigar_str(got)} != {fcship.cigar_str(rc)}"

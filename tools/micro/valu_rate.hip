@@ -275,6 +275,38 @@ __global__ __launch_bounds__(256) void kern(float* out, unsigned long long* stam
 #define I(j) asm volatile("v_max_u32 %0, %1, %0" : "+v"(a[j]) : "v"(b[j]));
         BODY8(I)
 #undef I
+      } else if constexpr (K == 60) {  // funnel shift: acc = (acc << 1) | (x >> 31)
+#define I(j) asm volatile("v_alignbit_b32 %0, %0, %1, 31" : "+v"(a[j]) : "v"(b[j]));
+        BODY8(I)
+#undef I
+      } else if constexpr (K == 61) {
+#define I(j) asm volatile("v_lshl_or_b32 %0, %1, 4, %0" : "+v"(a[j]) : "v"(b[j]));
+        BODY8(I)
+#undef I
+      } else if constexpr (K == 62) {
+#define I(j) asm volatile("v_or3_b32 %0, %1, %2, %0" : "+v"(a[j]) : "v"(b[j]), "v"(b[(j + 1) & 7]));
+        BODY8(I)
+#undef I
+      } else if constexpr (K == 63) {
+#define I(j) asm volatile("v_and_or_b32 %0, %1, %2, %0" : "+v"(a[j]) : "v"(b[j]), "v"(b[(j + 1) & 7]));
+        BODY8(I)
+#undef I
+      } else if constexpr (K == 64) {
+#define I(j) asm volatile("v_lshl_add_u32 %0, %1, 2, %0" : "+v"(a[j]) : "v"(b[j]));
+        BODY8(I)
+#undef I
+      } else if constexpr (K == 65) {
+#define I(j) asm volatile("v_alignbyte_b32 %0, %0, %1, 3" : "+v"(a[j]) : "v"(b[j]));
+        BODY8(I)
+#undef I
+      } else if constexpr (K == 66) {
+#define I(j) asm volatile("v_min3_i32 %0, %1, %2, %0" : "+v"(a[j]) : "v"(b[j]), "v"(b[(j + 1) & 7]));
+        BODY8(I)
+#undef I
+      } else if constexpr (K == 67) {
+#define I(j) asm volatile("v_sub_u32 %0, %1, %0\n\tv_alignbit_b32 %0, %0, %1, 31" : "+v"(a[j]) : "v"(b[j]));
+        BODY8(I)
+#undef I
       }
     }
   }
@@ -321,6 +353,14 @@ int main(int argc, char** argv) {
   CHECK(hipMalloc(&out, sizeof(float) * ncu * 4 * waves * 64 * 2));
   CHECK(hipMalloc(&st, 16));
   run<0>("v_fma_f32", waves, out, st, ncu);
+  run<60>("v_alignbit_b32", waves, out, st, ncu);
+  run<61>("v_lshl_or_b32", waves, out, st, ncu);
+  run<62>("v_or3_b32", waves, out, st, ncu);
+  run<63>("v_and_or_b32", waves, out, st, ncu);
+  run<64>("v_lshl_add_u32", waves, out, st, ncu);
+  run<65>("v_alignbyte_b32", waves, out, st, ncu);
+  run<66>("v_min3_i32", waves, out, st, ncu);
+  run<67>("sub + alignbit (2 instr)", waves, out, st, ncu);
   run<42>("v_max_i16", waves, out, st, ncu);
   run<50>("v_add_u16", waves, out, st, ncu);
   run<58>("v_sub_u16", waves, out, st, ncu);
