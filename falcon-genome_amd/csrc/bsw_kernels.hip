@@ -19,31 +19,10 @@
 //     wave-uniform and every integer matches bwa bit for bit.
 #include <hip/hip_runtime.h>
 
+#include "bsw_scan.h"
 #include "fcship_internal.h"
 
 namespace fcs {
-
-static constexpr int kMinusInf = -0x40000000;       // ksw.c MINUS_INF
-static constexpr int kScanNeg = (-2147483647 - 1) + (1 << 24);  // below any reachable scan value
-
-__device__ __forceinline__ unsigned long long ballot64(bool v) { return __ballot(v); }
-
-// Exclusive prefix max of u across slots (column order), seeded with carry.
-template <int NS>
-__device__ __forceinline__ void excl_scan(const int (&u)[NS], int carry, int (&ex)[NS]) {
-#pragma unroll
-  for (int k = 0; k < NS; ++k) {
-    const int incl = wave_incl_max(u[k], kScanNeg);
-    int e = dpp_wave_shr1_i(carry, incl);
-    ex[k] = max(e, carry);
-    carry = max(carry, read_lane(incl, 63));
-  }
-}
-
-// Query profile for column j: bytes mat[t*5 + q_j] for t = 0..3 packed, and t = 4.
-__device__ __forceinline__ int prof_score(int lo, int hi, int tb) {
-  return tb < 4 ? (int)(int8_t)(lo >> (tb << 3)) : hi;
-}
 
 template <int NS>
 __device__ void extend_task(const BswDevBatch& b, const BswParams& p, long long task, uint8_t* __restrict__ tl,
@@ -391,15 +370,12 @@ __device__ __forceinline__ void glane_traceback(const GLayout& L, int qlen, int 
   *n_out = n;
 }
 
-// FCS_GLANE_ARITH (default): the row's direction bits and the masked row's
-// band selects as sign-bit arithmetic and v_bitop3_b32 selects (full rate)
-// instead of compares feeding v_cndmask (the compiler's VOP2 form costs ~7
-// extra cycles each in a mix, gfx950_sq_counters) and per-cell branches.
-// Every score stays within +-2^30 + 2^10, so the differences never overflow:
-// (uint32)(a - b) >> 31 is exactly a < b.
-#ifndef FCS_GLANE_ARITH
-#define FCS_GLANE_ARITH 1
-#endif
+// The row's direction bits and the masked row's band selects as sign-bit
+// arithmetic and v_bitop3_b32 selects (full rate) instead of compares feeding
+// v_cndmask (the compiler's VOP2 form costs ~7 extra cycles each in a mix,
+// profiles/r3/gfx950_sq_counters.txt) and per-cell branches.  Every score stays
+// within +-2^30 + 2^10, so the differences never overflow: (uint32)(a - b) >> 31
+// is exactly a < b.
 
 __device__ __forceinline__ int gsel(int mask, int a, int b) {  // mask ? a : b, mask all-ones or zero
   int r;
@@ -413,16 +389,13 @@ __device__ __forceinline__ void glane_row(int (&Hd)[NB], int (&Ed)[NB + 1], cons
                                           const int hi, const int hb, const int oe_del, const int oe_ins,
                                           const int e_del, const int e_ins, int& h1) {
   int f = kMinusInf;
-#if FCS_GLANE_ARITH
   const int minf = kMinusInf;
-#endif
 #pragma unroll
   for (int k = 0; k < NB; ++k) {
     const int qoff = (int)((Qb[k >> 2] >> (8 * (k & 3))) & 0xFFu);
     const int s = __builtin_amdgcn_sbfe(rowpack, qoff, 5);
     const int m = Hd[k] + s;
     int e = Ed[k + 1];
-#if FCS_GLANE_ARITH
     uint32_t d = 0;
     if constexpr (CIG) d = (uint32_t)(m - e) >> 31;  // m < e: H from E
     int h = max(m, e);
@@ -452,33 +425,6 @@ __device__ __forceinline__ void glane_row(int (&Hd)[NB], int (&Ed)[NB + 1], cons
       f = fn;
       if (k == NB - 1) h1 = h;
     }
-#else
-    int h = m >= e ? m : e;
-    int d = 0;
-    if constexpr (CIG) d = m >= e ? 0 : 1;
-    if constexpr (CIG) d = h >= f ? d : 2;
-    h = h >= f ? h : f;
-    int t = m - oe_del;
-    e -= e_del;
-    if constexpr (CIG) d |= e > t ? 4 : 0;
-    e = e > t ? e : t;
-    t = m - oe_ins;
-    int fn = f - e_ins;
-    if constexpr (CIG) d |= fn > t ? 8 : 0;
-    fn = fn > t ? fn : t;
-    if constexpr (MASKED) {
-      const bool v = k >= lo && k < hi;
-      Hd[k] = v ? h : (k < lo ? hb : Hd[k]);
-      Ed[k] = v ? e : kMinusInf;
-      f = v ? fn : kMinusInf;
-      h1 = v ? h : h1;
-    } else {
-      Hd[k] = h;
-      Ed[k] = e;
-      f = fn;
-      if (k == NB - 1) h1 = h;
-    }
-#endif
     if constexpr (CIG) {
       if ((k & 7) == 0) nib[k >> 3] = (uint32_t)d;
       else nib[k >> 3] |= (uint32_t)d << (4 * (k & 7));
@@ -683,9 +629,17 @@ template <int MAXNS>
 __global__ __launch_bounds__(64) void bsw_global_kernel(const BswDevBatch b, const BswParams p, int32_t* __restrict__ scores,
                                                         uint8_t* __restrict__ zbuf, const int64_t* __restrict__ zoff) {
   extern __shared__ __align__(16) unsigned char tl[];
-  for (long long task = blockIdx.x; task < b.n; task += gridDim.x) {
+  // 64 tasks per probe, one per lane: this kernel's tasks (those the lane
+  // kernels do not take) found by one ballot, then taken one at a time
+  const int lane = (int)threadIdx.x;
+  for (long long base = (long long)blockIdx.x * 64; base < b.n; base += (long long)gridDim.x * 64) {
+    const long long mine = base + lane;
+    const bool wave_task = mine < b.n && !glane_ok(b.qlen[mine], b.tlen[mine], b.w[mine], p.lane_ok != 0);
+    unsigned long long todo = __ballot(wave_task);
+    while (todo) {
+    const long long task = base + __builtin_ctzll(todo);
+    todo &= todo - 1;
     const int qlen = b.qlen[task];
-    if (glane_ok(qlen, b.tlen[task], b.w[task], p.lane_ok != 0)) continue;  // bsw_global_lane_kernel's
     const int ns = (qlen + 1 + 63) >> 6;
     if (MAXNS <= 4) {
       switch (ns) {
@@ -700,6 +654,7 @@ __global__ __launch_bounds__(64) void bsw_global_kernel(const BswDevBatch b, con
       else global_task<16>(b, p, task, tl, scores, zbuf, zoff);
     }
     __syncthreads();
+    }
   }
 }
 
@@ -772,7 +727,7 @@ int launch_bsw_global(const BswDevBatch& b, const BswParams& p, int max_qlen, in
   if (lds > 64 * 1024) return fail(FCS_ERR_UNSUPPORTED, "[E::fcship] ksw_global2: tlen too large");
   // grid-stride over the sorted tail; 2048 waves (2 per SIMD) fill the chip,
   // and an empty tail (the common bwa case) costs only that many exits
-  long long grid = b.n;
+  long long grid = (b.n + 63) / 64;  // one 64-task probe per wave and round
   const long long cap = 2048;
   if (grid > cap) grid = cap;
   // narrow bands: one lane per task (64 consecutive tasks per wave)

@@ -346,15 +346,7 @@ int check_params(const fcs_bsw_params* p) {
 // The onesweep kernels' default tile (1024 threads x ~16 items) gives a 1M-key
 // sort 62 workgroups on a 256-CU chip; 256 x 8 tiles give it ~490 but measured
 // slower (C2 2.86 vs 2.93 TCUPS, C3 1.95 vs 2.05, profiles/r2/abt_*).
-#ifndef FCS_SORT_SMALL_TILES
-#define FCS_SORT_SMALL_TILES 0  // 1 measured slower
-#endif
-#if FCS_SORT_SMALL_TILES
-using SortOnesweep = rocprim::radix_sort_onesweep_config<rocprim::kernel_config<256, 8>, rocprim::kernel_config<256, 8>, 8>;
-#else
-using SortOnesweep = rocprim::default_config;
-#endif
-using SortConfig = rocprim::radix_sort_config<rocprim::default_config, rocprim::default_config, SortOnesweep, 0>;
+using SortConfig = rocprim::radix_sort_config<rocprim::default_config, rocprim::default_config, rocprim::default_config, 0>;
 hipError_t sort_pairs_u32(void* tmp, size_t& bytes, const uint32_t* kin, uint32_t* kout, const int32_t* vin,
                           int32_t* vout, int n, hipStream_t s, int end_bit) {
   return rocprim::radix_sort_pairs<SortConfig>(tmp, bytes, kin, kout, vin, vout, (size_t)n, 0, (unsigned)end_bit, s);
@@ -1406,6 +1398,100 @@ int fcs_bsw_global_dev(const fcs_bsw_batch* b, const fcs_bsw_params* params, int
                            want_cigar ? dev_n_cigar : nullptr, (hipStream_t)stream);
 }
 
+int fcs_bsw_align(const fcs_bsw_task* tasks, int32_t n, const fcs_bsw_params* params, const int32_t* xtra,
+                  fcs_kswr* out, int32_t device) {
+  if (n < 0 || (n > 0 && (!tasks || !xtra || !out))) return fail(FCS_ERR_INVALID, "[E::fcs_bsw_align] bad arguments");
+  int rc = check_params(params);
+  if (rc) return rc;
+  if (n == 0) return FCS_OK;
+  PackedTasks pk;
+  if ((rc = pack_tasks(tasks, n, pk))) return rc;
+  int32_t mq = 0, mt = 0;
+  for (int32_t k = 0; k < n; ++k) mq = std::max(mq, pk.qlen[k]), mt = std::max(mt, pk.tlen[k]);
+  for (int64_t i = 0; i < pk.b.qbytes; ++i)
+    if (pk.q[i] > 4) return fail(FCS_ERR_INVALID, "[E::fcs_bsw_align] query base code > 4");
+  for (int64_t i = 0; i < pk.b.tbytes; ++i)
+    if (pk.t[i] > 4) return fail(FCS_ERR_INVALID, "[E::fcs_bsw_align] target base code > 4");
+  if ((rc = check_device(device))) return rc;
+  FCS_SET_DEVICE((device));
+  SessionLease lease;
+  if ((rc = lease.acquire(device))) return rc;
+  Session* S = lease.get();
+  const size_t nn = (size_t)n;
+  Layout L;
+  const size_t oq = L.add(pk.q.size()), oqo = L.add(8 * nn), oql = L.add(4 * nn), ot = L.add(pk.t.size()),
+               oto = L.add(8 * nn), otl = L.add(4 * nn), ox = L.add(4 * nn);
+  const size_t in_bytes = L.total, oo = L.add(sizeof(fcs_kswr) * nn);
+  if ((rc = S->ensure_host(L.total + 1024)) || (rc = S->ensure_dev(L.total))) return rc;
+  std::memcpy(S->h<void>(oq), pk.q.data(), pk.q.size());
+  std::memcpy(S->h<void>(oqo), pk.qoff.data(), 8 * nn);
+  std::memcpy(S->h<void>(oql), pk.qlen.data(), 4 * nn);
+  std::memcpy(S->h<void>(ot), pk.t.data(), pk.t.size());
+  std::memcpy(S->h<void>(oto), pk.toff.data(), 8 * nn);
+  std::memcpy(S->h<void>(otl), pk.tlen.data(), 4 * nn);
+  std::memcpy(S->h<void>(ox), xtra, 4 * nn);
+  hipStream_t s = S->s;
+  const StreamDrain drain{s};
+  FCS_HIP_CHECK(hipMemcpyAsync(S->dev, S->host, in_bytes, hipMemcpyHostToDevice, s));
+  BswDevBatch d{};
+  d.qbuf = S->d<uint8_t>(oq);
+  d.qoff = S->d<int64_t>(oqo);
+  d.qlen = S->d<int32_t>(oql);
+  d.tbuf = S->d<uint8_t>(ot);
+  d.toff = S->d<int64_t>(oto);
+  d.tlen = S->d<int32_t>(otl);
+  d.n = n;
+  if ((rc = launch_bsw_align(d, to_params(params), S->d<int32_t>(ox), mq, mt, S->d<int32_t>(oo), s))) return rc;
+  FCS_HIP_CHECK(hipMemcpyAsync(S->h<void>(oo), S->d<void>(oo), sizeof(fcs_kswr) * nn, hipMemcpyDeviceToHost, s));
+  FCS_HIP_CHECK(hipStreamSynchronize(s));
+  std::memcpy(out, S->h<void>(oo), sizeof(fcs_kswr) * nn);
+  return FCS_OK;
+}
+
+int fcs_bsw_align_dev(const fcs_bsw_batch* b, const fcs_bsw_params* params, const int32_t* dev_xtra, fcs_kswr* dev_out,
+                      int32_t device, void* stream) {
+  if (!b || b->n < 0 || (b->n > 0 && (!dev_xtra || !dev_out)))
+    return fail(FCS_ERR_INVALID, "[E::fcs_bsw_align_dev] bad arguments");
+  int rc = check_params(params);
+  if (rc) return rc;
+  if (b->n == 0) return FCS_OK;
+  if (b->n > 0x7FFFFFFF) return fail(FCS_ERR_UNSUPPORTED, "[E::fcs_bsw_align_dev] more than 2^31-1 tasks");
+  if ((rc = check_device(device))) return rc;
+  FCS_SET_DEVICE((device));
+  BswDevBatch d{};
+  d.qbuf = b->qbuf;
+  d.qoff = b->qoff;
+  d.qlen = b->qlen;
+  d.tbuf = b->tbuf;
+  d.toff = b->toff;
+  d.tlen = b->tlen;
+  d.h0 = b->h0;
+  d.w = b->w;
+  d.n = b->n;
+  return launch_bsw_align(d, to_params(params), dev_xtra, std::max(b->max_qlen, 1), std::max(b->max_tlen, 1),
+                          reinterpret_cast<int32_t*>(dev_out), (hipStream_t)stream);
+}
+
+fcs_kswr fcs_ksw_align2(int qlen, const uint8_t* query, int tlen, const uint8_t* target, int m, const int8_t* mat,
+                        int o_del, int e_del, int o_ins, int e_ins, int xtra, void** qry) {
+  fcs_kswr r{FCS_KSW_FAILED, -1, -1, -1, -1, -1, -1};
+  if (m != 5) return (void)fail(FCS_ERR_UNSUPPORTED, "[E::fcs_ksw_align2] only m == 5 (bwa's alphabet) is supported"), r;
+  if (!mat) return (void)fail(FCS_ERR_INVALID, "[E::fcs_ksw_align2] null matrix"), r;
+  if (qry && *qry) return (void)fail(FCS_ERR_UNSUPPORTED, "[E::fcs_ksw_align2] cached query profiles unsupported"), r;
+  fcs_bsw_params p;
+  std::memcpy(p.mat, mat, 25);
+  p.o_del = o_del;
+  p.e_del = e_del;
+  p.o_ins = o_ins;
+  p.e_ins = e_ins;
+  p.end_bonus = 0;
+  p.zdrop = 0;
+  fcs_bsw_task t{qlen, tlen, 0, 0, query, target};
+  fcs_kswr out;
+  if (fcs_bsw_align(&t, 1, &p, &xtra, &out, g_default_device)) return r;
+  return out;
+}
+
 int fcs_ksw_extend2(int qlen, const uint8_t* query, int tlen, const uint8_t* target, int m, const int8_t* mat,
                     int o_del, int e_del, int o_ins, int e_ins, int w, int end_bonus, int zdrop, int h0, int* qle,
                     int* tle, int* gtle, int* gscore, int* max_off) {
@@ -1462,6 +1548,6 @@ int fcs_ksw_global2(int qlen, const uint8_t* query, int tlen, const uint8_t* tar
   return score;
 }
 
-int fcs_abi_symbol_count(void) { return 38; }
+int fcs_abi_symbol_count(void) { return 41; }
 
 }  // extern "C"

@@ -221,12 +221,10 @@ constexpr int kBswKeyBits = 24;
 // next kPhmmClasses the grouped kernels (phmm2.h / phmm_kernel), each range
 // longest first.
 // PairHMM sort keys: 16 bits (two 8-bit radix passes; the in-class order keys
-// hap length only) or 24 (three passes; stream classes also order by read length).
-#ifndef FCS_PHMM_KEY16
-#define FCS_PHMM_KEY16 1
-#endif
-constexpr int kPhmmKeyClassShift = FCS_PHMM_KEY16 ? 12 : 20;
-constexpr int kPhmmKeyBits = FCS_PHMM_KEY16 ? 16 : 24;
+// hap length only: 24-bit keys that also ordered stream classes by read length
+// measured slower).
+constexpr int kPhmmKeyClassShift = 12;
+constexpr int kPhmmKeyBits = 16;
 constexpr int kStreamClasses = 4;
 constexpr int kPhmmClasses = 6;
 constexpr int kPhmmLaunchClasses = kStreamClasses + kPhmmClasses;
@@ -237,6 +235,8 @@ int launch_bsw_extend_sorted(const BswDevBatch& b, const BswParams& p, int max_q
 // Wave-per-task kernel over sorted positions [bounds[kBswWideBucket], bounds[kBswWideBucket + 1]).
 int launch_bsw_extend_wide(const BswDevBatch& b, const BswParams& p, int max_qlen, int max_tlen, int32_t* res,
                            int64_t* cells, const int32_t* order, const int64_t* bounds, hipStream_t s);
+int launch_bsw_align(const BswDevBatch& b, const BswParams& p, const int32_t* xtra, int max_qlen, int max_tlen,
+                     int32_t* out, hipStream_t s);
 int launch_bsw_global(const BswDevBatch& b, const BswParams& p, int max_qlen, int max_tlen, int32_t* scores,
                       uint8_t* zbuf, int64_t zbytes, const int64_t* zoff, uint32_t* cigar, const int64_t* cigar_off,
                       const int32_t* cigar_cap, int32_t* n_cigar, hipStream_t s);

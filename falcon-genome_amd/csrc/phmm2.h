@@ -27,15 +27,9 @@
 // t - 15 from the second block on (the first block's columns are negative).
 #pragma once
 
-#ifndef FCS_STREAM_DPPSEL
-#define FCS_STREAM_DPPSEL 0  // 1: row a's DPP inputs by v_cndmask_b32_dpp (A/B: slower)
-#endif
-
 // 3 waves per SIMD (<= 168 VGPRs; LDS allows ~3.5 at H ~ 225): capped at 128
 // VGPRs for 4 the kernel spills 33 VGPRs to scratch.
-#ifndef PHMM2_LB
-#define PHMM2_LB 3
-#endif
+constexpr int kPhmm2Waves = 3;
 
 namespace fcs {
 
@@ -108,24 +102,10 @@ __device__ __forceinline__ void phmm2_step(Lane2& L, PhRing<float> (&pf)[PFD], i
   // (lane 0: the ring), row b's half is this lane's own row a, already there;
   // the packed ops read them with op_sel swapped (no register moves).
   pf2 Xsw = L.Xn, Isw = L.In;
-#if FCS_STREAM_DPPSEL
-  // one VOP2-DPP select per value (see pstream_step in phmm_stream.h)
-  {
-    const unsigned long long smask = __ballot(lane0);
-    asm("s_mov_b64 vcc, %2\n\t"
-        "s_nop 0\n\t"
-        "v_cndmask_b32_dpp %0, %0, %3, vcc row_shr:1 row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
-        "v_cndmask_b32_dpp %1, %1, %4, vcc row_shr:1 row_mask:0xf bank_mask:0xf bound_ctrl:1"
-        : "+v"(Xsw.y), "+v"(Isw.y)
-        : "s"(smask), "v"(cur.X), "v"(cur.I)
-        : "vcc");
-  }
-#else
   Xsw.y = __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(L.Xn.y), kDppRowShr1, 0xF, 0xF, true));
   Isw.y = __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(L.In.y), kDppRowShr1, 0xF, 0xF, true));
   Xsw.y = lane0 ? cur.X : Xsw.y;
   Isw.y = lane0 ? cur.I : Isw.y;
-#endif
   const pf2 I = __builtin_shufflevector(Isw, Isw, 1, 0);
   pf2 prior;
   if constexpr (BC) {
@@ -229,21 +209,13 @@ __device__ __forceinline__ void phmm2_stripe(const RowP2& p, PhRing<float>* __re
   }
 }
 
-// LDS layout of one wave: four rings, then four hap-code arrays.  The strides
-// carry padding (FCS_PHMM2_RPAD / _HPAD bytes) so the four segments' same-slot
-// accesses fall in different banks.
-#ifndef FCS_PHMM2_RPAD
-#define FCS_PHMM2_RPAD 0
-#endif
-#ifndef FCS_PHMM2_HPAD
-#define FCS_PHMM2_HPAD 0
-#endif
-__host__ __device__ constexpr int ring2_stride(int nslot) { return nslot * 8 + FCS_PHMM2_RPAD; }
-__host__ __device__ constexpr int hap2_stride(int nslot) { return nslot + 16 + FCS_PHMM2_HPAD; }
+// LDS layout of one wave: four rings, then four hap-code arrays.
+__host__ __device__ constexpr int ring2_stride(int nslot) { return nslot * 8; }
+__host__ __device__ constexpr int hap2_stride(int nslot) { return nslot + 16; }
 __host__ __device__ constexpr int phmm2_lds(int nslot) { return 4 * (ring2_stride(nslot) + hap2_stride(nslot)); }
 
 // Forward pass (fp32, FMA order) of one hap-length class; nslot >= H + 66.
-__global__ __launch_bounds__(64, PHMM2_LB) void phmm2_kernel(const PhmmDevBatch b, const int32_t* __restrict__ order,
+__global__ __launch_bounds__(64, kPhmm2Waves) void phmm2_kernel(const PhmmDevBatch b, const int32_t* __restrict__ order,
                                                       const int64_t* __restrict__ bounds, const int cls,
                                                       const int nslot, const PhmmTables<float> tab,
                                                       double* __restrict__ out, int32_t* __restrict__ rescue_list,

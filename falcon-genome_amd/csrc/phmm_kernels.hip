@@ -44,10 +44,7 @@ namespace fcs {
 // not: -8%) and, as a shift register, let every ring read land in the register
 // its DPP `old` operand needs: the four-deep rotation cost two v_mov per step
 // and spilled 2 VGPRs; 2, 3 and 4 measured within 0.5% (gpurun_out/abp2).
-#ifndef FCS_PHMM_PFD
-#define FCS_PHMM_PFD 2
-#endif
-constexpr int PFD = FCS_PHMM_PFD;
+constexpr int PFD = 2;
 template <typename T> struct alignas(2 * sizeof(T)) PhRing {
   T X, I;
 };
@@ -442,7 +439,7 @@ __host__ __device__ inline int phmm_class(int H) {
   return c < 0 ? 0 : c > kPhmmClasses - 1 ? kPhmmClasses - 1 : c;
 }
 
-// Sort keys (16 bits, two 8-bit radix passes; 24 / three under FCS_PHMM_KEY16=0): a 4-bit launch class, then the
+// Sort keys (16 bits, two 8-bit radix passes): a 4-bit launch class, then the
 // in-class order, as ascending keys — each class is a contiguous range and the
 // longest work comes first.  Classes 0 .. kStreamClasses-1 are the row-streamed
 // kernel's (kStreamMinR <= R <= kStreamMaxR, longest hap-length class first), the rest the
@@ -468,20 +465,13 @@ __global__ void phmm_keys_kernel(const PhmmDevBatch b, uint32_t* __restrict__ ke
   int sc;
   const uint32_t cf = (uint32_t)phmm_launch_class(R, H, sc);
   const uint32_t hh = 0xFFFu - (uint32_t)min(max(H, 0), 0xFFF);
-  uint32_t low;
-#if FCS_PHMM_KEY16
   // streamed: hap length (H <= 3700 fits 12 bits); grouped: stripe count (R < 33:
   // at most 3), then hap length in steps of 4
+  uint32_t low;
   if (sc >= 0)
     low = hh;
   else
     low = ((3u - (uint32_t)min((max(R, 0) + 15) >> 4, 3)) << 10) | (0x3FFu - (uint32_t)min(max(H, 0) >> 2, 0x3FF));
-#else
-  if (sc >= 0)
-    low = (hh << 8) | (0xFFu - (uint32_t)min(R >> 4, 0xFF));
-  else
-    low = ((0xFFu - (uint32_t)min((max(R, 0) + 15) >> 4, 0xFF)) << 12) | hh;
-#endif
   keys[p] = (cf << kPhmmKeyClassShift) | low;
   idx[p] = (int32_t)p;
 }
@@ -584,22 +574,6 @@ int launch_phmm_forward(const PhmmDevBatch& b, const int32_t* order, int64_t cou
     const int sc = kStreamClasses - 1 - j;
     const int hmax = std::min(stream_class_hmax(sc), max_hap_len);
     hipStream_t st = fs[fork++ % kForkStreams];
-#ifdef FCS_PHMM_NOSTREAM
-    if (!exact) {  // A/B baseline: the grouped two-row kernel over the stream range
-      const int ns2 = nslot_for(hmax) + 16;
-      const size_t lds2 = (size_t)phmm2_lds(ns2);
-      if (lds2 <= kLdsBytes) {
-        if (lds2 > 64 * 1024)
-          FCS_HIP_CHECK(
-              hipFuncSetAttribute((const void*)phmm2_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds2));
-        hipLaunchKernelGGL(phmm2_kernel, dim3((unsigned)std::min<long long>(std::max<long long>(groups, 1), 65536)),
-                           dim3(64), lds2, st, b, order, bounds, j, ns2, t.tf, out, rescue_list, rescue_count, thr,
-                           use_rescue ? 1 : 0);
-        FCS_HIP_CHECK(hipGetLastError());
-        continue;
-      }
-    }
-#endif
     if (exact) {  // GKL operation order: the one-row kernel over the same range
       const int rc = launch_one<float, true, false>(b, order, nullptr, count, bounds, j, nslot_for(hmax), groups, t.tf,
                                                    out, rescue_list, rescue_count, thr, use_rescue, st);
@@ -624,11 +598,7 @@ int launch_phmm_forward(const PhmmDevBatch& b, const int32_t* order, int64_t cou
       FCS_HIP_CHECK(hipGetLastError());
       return FCS_OK;
     };
-#ifndef FCS_STREAM_LB4
-#define FCS_STREAM_LB4 1
-#endif
-    const int rc = (w >= 4 && FCS_STREAM_LB4) ? launch(phmm3_kernel<4>) : w >= 3 ? launch(phmm3_kernel<3>)
-                 : w == 2 ? launch(phmm3_kernel<2>) : launch(phmm3_kernel<1>);
+    const int rc = w >= 3 ? launch(phmm3_kernel<3>) : w == 2 ? launch(phmm3_kernel<2>) : launch(phmm3_kernel<1>);
     if (rc != FCS_OK) return rc;
   }
   // Grouped classes (reads shorter than kStreamMinR or longer than kStreamMaxR; empty in most batches):
@@ -638,22 +608,13 @@ int launch_phmm_forward(const PhmmDevBatch& b, const int32_t* order, int64_t cou
   // the chip's wave slots at 3 waves/SIMD), since the host does not know the
   // class sizes and each of 64K empty workgroups still takes a dispatch, a wave
   // slot and its LDS while it reads the bounds.
-#ifndef FCS_PHMM_GROUPED_GRID
-#define FCS_PHMM_GROUPED_GRID 8192
-#endif
-  constexpr long long kGroupedGrid = FCS_PHMM_GROUPED_GRID;
+  constexpr long long kGroupedGrid = 8192;
   int gfork = 0;
   for (int j = kPhmmClasses - 1 - c_max; j < kPhmmClasses; ++j) {
     const int c = kPhmmClasses - 1 - j;
     const int lc = kStreamClasses + j;  // launch class of grouped class c
     const int ns = (c == kPhmmClasses - 1) ? ns_max : std::min(224 + 32 * c, ns_max);
-#if FCS_PHMM_GROUPED_GRID >= 65536
-    hipStream_t st = fs[fork++ % kForkStreams];  // A/B: the round-1 placement and grid
-    (void)gfork;
-#else
     hipStream_t st = fs[1 + gfork++ % (kForkStreams - 1)];
-#endif
-#ifndef FCS_PHMM_ONEROW
     // the two-rows-per-lane kernel (phmm2.h) for the FMA-order pass when its
     // four rings fit (ring slots >= H + 65, hap bytes + 16)
     const int ns2 = ns + 16;
@@ -668,7 +629,6 @@ int launch_phmm_forward(const PhmmDevBatch& b, const int32_t* order, int64_t cou
       FCS_HIP_CHECK(hipGetLastError());
       continue;
     }
-#endif
     const int rc = exact ? launch_one<float, true, false>(b, order, nullptr, count, bounds, lc, ns, groups, t.tf, out,
                                                            rescue_list, rescue_count, thr, use_rescue, st)
                          : launch_one<float, false, false>(b, order, nullptr, count, bounds, lc, ns, groups, t.tf, out,

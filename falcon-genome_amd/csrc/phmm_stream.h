@@ -42,26 +42,22 @@
 
 namespace fcs {
 
-#ifndef FCS_STREAM_HALF
-#define FCS_STREAM_HALF 8
-#endif
-constexpr int kStreamHalf = FCS_STREAM_HALF;  // a stripe's last block runs 8 steps when that suffices (0: never)
-#ifndef FCS_STREAM_PFD
-#define FCS_STREAM_PFD 2
-#endif
-constexpr int kStreamPfd = FCS_STREAM_PFD;  // LDS read-ahead of the 3/2/1-wave stream classes
+constexpr int kStreamHalf = 8;   // a stripe's last block runs 8 steps when that suffices
+constexpr int kStreamPfd = 2;    // LDS read-ahead (steps) of the ring and hap-code reads
 constexpr int kStreamMinR = 33;  // a pair spans >= 17 units: at most two pairs per stripe and segment
 constexpr int kStreamMaxR = 0xFFFF;  // a segment packs R | H << 16 between stripes; longer reads take phmm2
 constexpr int kStreamMaxK = 8;   // pairs per segment stream
 constexpr uint64_t kTopLanes = 0x8000800080008000ull;  // lane 15 of each 16-lane segment
-// Hap-length bounds of the stream classes: LDS <= 10,240 B per wave (4 waves per
-// SIMD), <= 13,312 B (3, at the 512-byte allocation granularity), <= 20 KB (2),
-// and the 160 KB limit.
+// Hap-length bounds of the stream classes: LDS <= 13,312 B per wave (3 waves per
+// SIMD at the 512-byte allocation granularity), <= 20 KB (2), and the 160 KB
+// limit.  Classes 0 and 1 both run at 3 waves per SIMD: at 4 (10,240 B) the
+// kernel's 128-VGPR budget spilled 9 VGPRs and measured the same time as 3
+// (DESIGN §4.1); class 0 keeps its smaller LDS footprint.
 __host__ __device__ constexpr int stream_class_hmax(int c) {
   return c == 0 ? 224 : c == 1 ? 300 : c == 2 ? 472 : 3700;
 }
 // Waves per SIMD the class's launch bounds ask for (its LDS allows as many).
-__host__ __device__ constexpr int stream_class_waves(int c) { return c == 0 ? 4 : c == 1 ? 3 : c == 2 ? 2 : 1; }
+__host__ __device__ constexpr int stream_class_waves(int c) { return c <= 1 ? 3 : c == 2 ? 2 : 1; }
 __host__ __device__ inline int stream_class(int H) {
   for (int c = 0; c < kStreamClasses; ++c)
     if (H <= stream_class_hmax(c)) return c;
@@ -74,18 +70,8 @@ __host__ __device__ inline int stream_class(int H) {
 // converted in place) | 64 bytes of read-ahead tail.
 __host__ __device__ constexpr int stream_nslot(int hmax) { return hmax + 18; }
 __host__ __device__ constexpr int stream_hstride(int hmax) { return (hmax + 12) & ~3; }
-// Ring stride in slots: FCS_STREAM_RINGPAD extra slots put the four segments'
-// one-address ring reads on different LDS banks.
-#ifndef FCS_STREAM_RINGPAD
-#define FCS_STREAM_RINGPAD 0
-#endif
-__host__ __device__ constexpr int stream_rstride(int nslot) { return nslot + FCS_STREAM_RINGPAD; }
-#ifndef FCS_STREAM_WRITEALL
-#define FCS_STREAM_WRITEALL 0  // diagnostic: every lane writes (others to a dummy area), no EXEC changes
-#endif
 __host__ __device__ constexpr int stream_lds(int hmax) {
-  return 512 + 4 * 8 * stream_rstride(stream_nslot(hmax)) + 8 * stream_hstride(hmax) + 64 +
-         (FCS_STREAM_WRITEALL ? 640 : 0);
+  return 512 + 4 * 8 * stream_nslot(hmax) + 8 * stream_hstride(hmax) + 64;
 }
 
 // Per-row constants of one half (role: 0 idle, 1 pad, 2 row r < R, 3 row R, 4 V).
@@ -153,122 +139,35 @@ __device__ __forceinline__ int srole(int r, int R) { return r == 0 ? 1 : r < R ?
 // captures the V lanes' X at their column H + 1.
 // Start-lane select as one full-rate v_bitop3_b32 on a per-lane mask VGPR:
 // v_cndmask_b32 on an SGPR lane mask issues at half the rate (4 cycles per
-// wave64 instruction on gfx950 vs 2; tools/micro/valu_rate.hip, gpurun_out/r3m).
-#ifndef FCS_DIAG_NOREAD
-#define FCS_DIAG_NOREAD 0
-#endif
-#ifndef FCS_DIAG_NOWRITE
-#define FCS_DIAG_NOWRITE 0
-#endif
-#ifndef FCS_DIAG_NORING
-#define FCS_DIAG_NORING 0
-#endif
-#ifndef FCS_DIAG_NOHAP
-#define FCS_DIAG_NOHAP 0
-#endif
-#ifndef FCS_STREAM_SELV
-#define FCS_STREAM_SELV 1
-#endif
+// wave64 instruction on gfx950 vs 2; tools/micro/valu_rate.hip, profiles/r3/r3m).
 __device__ __forceinline__ float sel_v(uint32_t m, float a, float b) {
   float r;
   asm("v_bitop3_b32 %0, %1, %2, %3 bitop3:0xe4" : "=v"(r) : "v"(a), "v"(b), "v"(m));
   return r;
 }
 
-// Hap-code read-ahead in steps (FCS_STREAM_HPF; 0: the ring's PF).
-#ifndef FCS_STREAM_HPF
-#define FCS_STREAM_HPF 0
-#endif
-template <int PF> constexpr int stream_hpf() { return FCS_STREAM_HPF > 0 ? FCS_STREAM_HPF : PF; }
-
-// Hap codes by aligned dword pairs (FCS_STREAM_HAP4): one ds_read2_b32 per
-// four steps brings the eight code bytes around a lane's next four columns
-// (the lane's column sequence is contiguous bytes), and a v_perm_b32 per step
-// picks the step's byte.  A per-step ds_read_u8 at a lane-varying, unaligned
-// address cost ~19% of the kernel (the no-hap-read diagnostic build).
-#ifndef FCS_STREAM_HAP4
-#define FCS_STREAM_HAP4 0  // measured neutral (gpurun_out/r3s) and +9 spilled VGPRs in the 4-wave class
-#endif
-struct HapG {
-  uint32_t lo, hi;    // the current four steps' bytes: byte o + k is step k's code
-  uint32_t nlo, nhi;  // the next four steps', in flight
-  uint32_t sel;       // v_perm selector of step 0's byte: 0x0C0C0C00 | o
-};
-
-template <bool COND, bool WRITE, int S, int PF, int HPF = stream_hpf<PF>()>
-__device__ __forceinline__ void pstream_step(Lane2& L, PhRing<float> (&pf)[PF], int (&hq)[HPF], HapG& hg,
-                                             const uint32_t* __restrict__ hw,
+template <bool COND, bool WRITE, int S, int PF>
+__device__ __forceinline__ void pstream_step(Lane2& L, PhRing<float> (&pf)[PF], int (&hq)[PF],
                                              const unsigned char* __restrict__ hp, const PhRing<float>* __restrict__ rd,
-                                             const RowP2& p, const bool start, const uint32_t smask, const bool top,
-                                             const int t0, const int dl, float& acc, const uint32_t wbase) {
-  [[maybe_unused]] const int t = t0 + S;
+                                             const RowP2& p, const uint32_t smask, const int t0, const int dl,
+                                             float& acc, const uint32_t wbase) {
+  const int t = t0 + S;
   const PhRing<float> cur = pf[0];
-#if FCS_STREAM_HAP4
-  if constexpr (S % 4 == 0) {
-    hg.lo = hg.nlo;
-    hg.hi = hg.nhi;
-    hg.nlo = hw[S / 4 + 1];
-    hg.nhi = hw[S / 4 + 2];
-  }
-  const int hba = (int)__builtin_amdgcn_perm(hg.hi, hg.lo, hg.sel + (uint32_t)(S % 4));
-  (void)hq;
-  (void)hp;
-#else
   const int hba = hq[0];
-  (void)hg;
-  (void)hw;
-#endif
 #pragma unroll
-  for (int k = 0; k + 1 < PF; ++k) pf[k] = pf[k + 1];
-#pragma unroll
-  for (int k = 0; k + 1 < HPF; ++k) hq[k] = hq[k + 1];
-#if FCS_DIAG_NOREAD || FCS_DIAG_NORING  // diagnostic builds only (timing; results are wrong)
-  pf[PF - 1] = PhRing<float>{pf[0].I, pf[0].X};
-  (void)rd;
-#else
-  pf[PF - 1] = rd[S];     // boundary input for step t + PF
-#endif
-#if FCS_DIAG_NOHAP == 2  // constant code N: every cell matches
-  hq[HPF - 1] = 4;
-#elif FCS_DIAG_NOHAP == 3  // constant padding code: every cell mismatches
-  hq[HPF - 1] = 6;
-#elif FCS_DIAG_NOREAD || FCS_DIAG_NOHAP
-  hq[HPF - 1] = hq[0] ^ 1;
-#elif !FCS_STREAM_HAP4
-  hq[HPF - 1] = hp[t];    // row a's hap code for column t + HPF - 2l
-#endif
+  for (int k = 0; k + 1 < PF; ++k) {
+    pf[k] = pf[k + 1];
+    hq[k] = hq[k + 1];
+  }
+  pf[PF - 1] = rd[S];  // boundary input for step t + PF
+  hq[PF - 1] = hp[t];  // row a's hap code for column t + PF - 2l
   const int hbb = L.hbp;
   L.hbp = hba;
   pf2 Xsw = L.Xn, Isw = L.In;
-#if FCS_STREAM_DPPSEL
-  // row a's inputs in one VOP2-DPP select each: start lanes take the boundary
-  // source, the others row b of the lane below (row_shr:1 on src0).  The
-  // compiler's form is a DPP move plus a VOP3 select per value (the start mask
-  // lives in an SGPR pair, not VCC).  s_mov + s_nop 0 give the two wait states
-  // a DPP read needs after a VALU write of its source.
-  {
-    const unsigned long long smask = __ballot(start);
-    asm("s_mov_b64 vcc, %2\n\t"
-        "s_nop 0\n\t"
-        "v_cndmask_b32_dpp %0, %0, %3, vcc row_shr:1 row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
-        "v_cndmask_b32_dpp %1, %1, %4, vcc row_shr:1 row_mask:0xf bank_mask:0xf bound_ctrl:1"
-        : "+v"(Xsw.y), "+v"(Isw.y)
-        : "s"(smask), "v"(cur.X), "v"(cur.I)
-        : "vcc");
-  }
-#else
   Xsw.y = __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(L.Xn.y), kDppRowShr1, 0xF, 0xF, true));
   Isw.y = __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(L.In.y), kDppRowShr1, 0xF, 0xF, true));
-#if FCS_STREAM_SELV
   Xsw.y = sel_v(smask, cur.X, Xsw.y);
   Isw.y = sel_v(smask, cur.I, Isw.y);
-  (void)start;
-#else
-  Xsw.y = start ? cur.X : Xsw.y;
-  Isw.y = start ? cur.I : Isw.y;
-  (void)smask;
-#endif
-#endif
   const pf2 I = __builtin_shufflevector(Isw, Isw, 1, 0);
   pf2 prior;
   prior.x = prior_code(p.ma, hba, p.e1.x, p.e3.x);
@@ -277,17 +176,11 @@ __device__ __forceinline__ void pstream_step(Lane2& L, PhRing<float> (&pf)[PF], 
   const pf2 D = __builtin_elementwise_fma(L.Mo, p.my, L.Do * p.yy);
   const pf2 Xn = __builtin_elementwise_fma(M, p.mm, __builtin_elementwise_fma(I, p.gm, D));
   const pf2 In = __builtin_elementwise_fma(M, p.mx, I * p.xx);
-  if constexpr (WRITE && !FCS_DIAG_NOWRITE) {
+  if constexpr (WRITE) {
     // row b of lane 15, column t - 31 -> ring slot t - 31: EXEC narrowed to the
     // four lanes 15 inside the statement, so the step stays one basic block (a
     // branch per step cost six SALU, and values carried across the blocks were
     // re-zero-extended at each use)
-#if FCS_STREAM_WRITEALL
-    asm volatile("ds_write2_b32 %0, %1, %2 offset0:%3 offset1:%4"
-                 :
-                 : "v"(wbase), "v"(Xn.y), "v"(In.y), "i"(2 * S), "i"(2 * S + 1)
-                 : "memory");
-#else
     uint64_t keep;
     asm volatile(
         "s_mov_b64 %0, exec\n\t"
@@ -297,8 +190,6 @@ __device__ __forceinline__ void pstream_step(Lane2& L, PhRing<float> (&pf)[PF], 
         : "=&s"(keep)
         : "v"(wbase), "v"(Xn.y), "v"(In.y), "s"(kTopLanes), "i"(2 * S), "i"(2 * S + 1)
         : "memory");
-#endif
-    (void)top;
   }
   else
     asm volatile("" ::: "memory");  // keep each step's LDS reads in their step (hoisted, they cost registers)
@@ -318,14 +209,13 @@ __device__ __forceinline__ void pstream_step(Lane2& L, PhRing<float> (&pf)[PF], 
 }
 
 template <bool COND, bool WRITE, int PF, int NS = 16>
-__device__ __forceinline__ void pstream_block(Lane2& L, PhRing<float> (&pf)[PF], int (&hq)[stream_hpf<PF>()],
-                                              HapG& hg, const uint32_t* __restrict__ hw,
+__device__ __forceinline__ void pstream_block(Lane2& L, PhRing<float> (&pf)[PF], int (&hq)[PF],
                                               const unsigned char* __restrict__ hp,
-                                              const PhRing<float>* __restrict__ rd, const RowP2& p, const bool start,
-                                              const uint32_t smask, const bool top, const int t0, const int dl,
-                                              float& acc, const uint32_t wbase) {
+                                              const PhRing<float>* __restrict__ rd, const RowP2& p,
+                                              const uint32_t smask, const int t0, const int dl, float& acc,
+                                              const uint32_t wbase) {
   [&]<int... S>(std::integer_sequence<int, S...>) {
-    (pstream_step<COND, WRITE, S, PF>(L, pf, hq, hg, hw, hp, rd, p, start, smask, top, t0, dl, acc, wbase), ...);
+    (pstream_step<COND, WRITE, S, PF>(L, pf, hq, hp, rd, p, smask, t0, dl, acc, wbase), ...);
   }(std::make_integer_sequence<int, NS>{});
 }
 
@@ -352,13 +242,10 @@ __global__ __launch_bounds__(64, LB) void phmm3_kernel(
   const int sl = lane & 15;
   const int sbase = lane & 48;
   const int sl2 = 2 * sl;
-  const bool top = sl == 15;
-  // LDS read-ahead (steps): the 4-wave class has no VGPRs to spare beyond 2
-  constexpr int PF = LB >= 4 ? 2 : kStreamPfd;
+  constexpr int PF = kStreamPfd;
   PhRing<float>* const Z = reinterpret_cast<PhRing<float>*>(smem_raw);
-  PhRing<float>* const ring = reinterpret_cast<PhRing<float>*>(smem_raw + 512) + seg * stream_rstride(nslot);
-  unsigned char* const hbufs = smem_raw + 512 + 32 * stream_rstride(nslot) + 2 * seg * hstride;  // this segment's two buffers
-  const uint32_t wdummy = lds_addr(smem_raw + 512 + 32 * stream_rstride(nslot) + 8 * hstride + 64 + 8 * lane);
+  PhRing<float>* const ring = reinterpret_cast<PhRing<float>*>(smem_raw + 512) + seg * nslot;
+  unsigned char* const hbufs = smem_raw + 512 + 32 * nslot + 2 * seg * hstride;  // this segment's two buffers
   {
     PhRing<float> z;
     z.X = lane >= 32 ? 1.f : 0.f;
@@ -546,7 +433,7 @@ __global__ __launch_bounds__(64, LB) void phmm3_kernel(
       const bool half = (nmax & 15) != 0 && (nmax & 15) <= kStreamHalf;
       const int hoff = 3 + ((cur_pk.w >> 5) & 3);
       const unsigned char* const hp =
-          (cur.act ? hbufs + (cur.k & 1) * hstride + hoff : hbufs) + stream_hpf<PF>() - sl2;  // hp[t]: column t + HPF - 2l
+          (cur.act ? hbufs + (cur.k & 1) * hstride + hoff : hbufs) + PF - sl2;  // hp[t]: column t + PF - 2l
 
       // Next stripe: its lane state, raw rows and new haplotype, all in flight
       // during this stripe.
@@ -567,58 +454,60 @@ __global__ __launch_bounds__(64, LB) void phmm3_kernel(
       L.Xp.y = (is_z && zsh && sl == 0) ? 1.f : 0.f;
       L.hbp = 6;
       PhRing<float> pf[PF];
-      int hq[stream_hpf<PF>()];
+      int hq[PF];
 #pragma unroll
       for (int q = 0; q < PF; ++q) pf[q] = is_z ? Z[32 + q - sl2 + zsh] : ring[q];
 #pragma unroll
-      for (int q = 0; q < stream_hpf<PF>(); ++q) hq[q] = FCS_STREAM_HAP4 ? 0 : hp[q - stream_hpf<PF>()];
-      // HAP4: the lane's code bytes for steps t sit at A + t (A = hp - HPF);
-      // hw = the dword-aligned base, o = A & 3
-      HapG hg;
-      const uint32_t* hw;
-      {
-        const uint32_t A = lds_addr(hp) - (uint32_t)stream_hpf<PF>();
-        hw = reinterpret_cast<const uint32_t*>(hp - stream_hpf<PF>() - (A & 3u));
-        hg.sel = 0x0C0C0C00u | (A & 3u);
-        hg.nlo = FCS_STREAM_HAP4 ? hw[0] : 0u;
-        hg.nhi = FCS_STREAM_HAP4 ? hw[1] : 0u;
-        hg.lo = hg.hi = 0u;
-      }
+      for (int q = 0; q < PF; ++q) hq[q] = hp[q - PF];
       float acc = 0.f;
-      for (int blk = 0; blk < nblk; ++blk) {
+      // Per block: the boundary source (ring, or Z for a lane whose pair starts
+      // in this stripe: Z[32 + c] is X = 1 for c >= 0, so past column 0 every
+      // block reads Z[32 ..]), the ring-write base, and whether some V lane
+      // captures its sum in the block (a wave-uniform branch to the COND body).
+      const int lblk = lim >> 4;  // the block holding this lane's capture (-1: none)
+      const int zb = PF - sl2 + zsh;
+      auto rd_of = [&](int t0) { return is_z ? Z + 32 + min(t0 + zb, 0) : ring + t0 + PF; };
+      auto wbase_of = [&](int t0) { return lds_addr(ring + (t0 - 31)); };
+      int blk = 0;
+      for (; blk < nblk && blk < 2; ++blk) {  // lane 15 writes from block 2 on (its columns are negative before)
         const int t0 = 16 * blk;
-        const PhRing<float>* const rd = is_z ? Z + 32 + min(t0 + PF - sl2 + zsh, 16) : ring + t0 + PF;
-        const bool cond = __ballot(lim >= t0 && lim < t0 + 16) != 0ull;
-        const uint32_t wbase = (!FCS_STREAM_WRITEALL || top) ? lds_addr(ring + (t0 - 31)) : wdummy;
-        const int dl = lim - t0;
-        if (blk >= 2) {
-          if (cond)
-            pstream_block<true, true, PF>(L, pf, hq, hg, hw + t0 / 4, hp, rd, prm, start, smask, top, t0, dl, acc, wbase);
-          else
-            pstream_block<false, true, PF>(L, pf, hq, hg, hw + t0 / 4, hp, rd, prm, start, smask, top, t0, dl, acc, wbase);
+        if (__ballot(lblk == blk) != 0ull)
+          pstream_block<true, false, PF>(L, pf, hq, hp, rd_of(t0), prm, smask, t0, lim - t0, acc, 0u);
+        else
+          pstream_block<false, false, PF>(L, pf, hq, hp, rd_of(t0), prm, smask, t0, lim - t0, acc, 0u);
+      }
+      // two blocks per iteration when neither captures: half the per-block
+      // bookkeeping and loop-carried register copies per step
+      for (; blk + 1 < nblk; blk += 2) {
+        const int t0 = 16 * blk;
+        if (__ballot((unsigned)(lblk - blk) < 2u) != 0ull) {
+          pstream_block<true, true, PF>(L, pf, hq, hp, rd_of(t0), prm, smask, t0, lim - t0, acc, wbase_of(t0));
+          pstream_block<true, true, PF>(L, pf, hq, hp, rd_of(t0 + 16), prm, smask, t0 + 16, lim - t0 - 16, acc,
+                                        wbase_of(t0 + 16));
         } else {
-          if (cond)
-            pstream_block<true, false, PF>(L, pf, hq, hg, hw + t0 / 4, hp, rd, prm, start, smask, top, t0, dl, acc, wbase);
-          else
-            pstream_block<false, false, PF>(L, pf, hq, hg, hw + t0 / 4, hp, rd, prm, start, smask, top, t0, dl, acc, wbase);
+          pstream_block<false, true, PF, 32>(L, pf, hq, hp, rd_of(t0), prm, smask, t0, 0, acc, wbase_of(t0));
         }
+      }
+      if (blk < nblk) {
+        const int t0 = 16 * blk;
+        if (__ballot(lblk == blk) != 0ull)
+          pstream_block<true, true, PF>(L, pf, hq, hp, rd_of(t0), prm, smask, t0, lim - t0, acc, wbase_of(t0));
+        else
+          pstream_block<false, true, PF>(L, pf, hq, hp, rd_of(t0), prm, smask, t0, 0, acc, wbase_of(t0));
       }
       if (half) {
         const int t0 = 16 * nblk;
-        const PhRing<float>* const rd = is_z ? Z + 32 + min(t0 + PF - sl2 + zsh, 16) : ring + t0 + PF;
         const bool cond = __ballot(lim >= t0 && lim < t0 + 8) != 0ull;
-        const uint32_t wbase = (!FCS_STREAM_WRITEALL || top) ? lds_addr(ring + (t0 - 31)) : wdummy;
-        const int dl = lim - t0;
         if (nblk >= 2) {
           if (cond)
-            pstream_block<true, true, PF, 8>(L, pf, hq, hg, hw + t0 / 4, hp, rd, prm, start, smask, top, t0, dl, acc, wbase);
+            pstream_block<true, true, PF, 8>(L, pf, hq, hp, rd_of(t0), prm, smask, t0, lim - t0, acc, wbase_of(t0));
           else
-            pstream_block<false, true, PF, 8>(L, pf, hq, hg, hw + t0 / 4, hp, rd, prm, start, smask, top, t0, dl, acc, wbase);
+            pstream_block<false, true, PF, 8>(L, pf, hq, hp, rd_of(t0), prm, smask, t0, 0, acc, wbase_of(t0));
         } else {
           if (cond)
-            pstream_block<true, false, PF, 8>(L, pf, hq, hg, hw + t0 / 4, hp, rd, prm, start, smask, top, t0, dl, acc, wbase);
+            pstream_block<true, false, PF, 8>(L, pf, hq, hp, rd_of(t0), prm, smask, t0, lim - t0, acc, 0u);
           else
-            pstream_block<false, false, PF, 8>(L, pf, hq, hg, hw + t0 / 4, hp, rd, prm, start, smask, top, t0, dl, acc, wbase);
+            pstream_block<false, false, PF, 8>(L, pf, hq, hp, rd_of(t0), prm, smask, t0, 0, acc, 0u);
         }
       }
       if (lim >= 0) {
@@ -627,7 +516,7 @@ __global__ __launch_bounds__(64, LB) void phmm3_kernel(
           const unsigned long long k = atomicAdd(fb_count, 1ull);
           fb_list[k] = p;
           out[p] = __builtin_nan("");
-        } else if (use_rescue && acc < thr && !(FCS_DIAG_NOREAD || FCS_DIAG_NOWRITE || FCS_DIAG_NORING || FCS_DIAG_NOHAP)) {
+        } else if (use_rescue && acc < thr) {
           const unsigned long long k = atomicAdd(rescue_count, 1ull);
           rescue_list[k] = p;
           out[p] = __builtin_nan("");

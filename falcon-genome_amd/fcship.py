@@ -96,6 +96,14 @@ class BswResult(C.Structure):
                 ("gscore", C.c_int32), ("max_off", C.c_int32)]
 
 
+class Kswr(C.Structure):  # bwa's kswr_t
+    _fields_ = [("score", C.c_int32), ("te", C.c_int32), ("qe", C.c_int32), ("score2", C.c_int32),
+                ("te2", C.c_int32), ("tb", C.c_int32), ("qb", C.c_int32)]
+
+
+KSW_XBYTE, KSW_XSTOP, KSW_XSUBO, KSW_XSTART = 0x10000, 0x20000, 0x40000, 0x80000
+
+
 class BswBatch(C.Structure):
     _fields_ = [("qbuf", C.c_void_p), ("qoff", C.c_void_p), ("qlen", C.c_void_p), ("tbuf", C.c_void_p),
                 ("toff", C.c_void_p), ("tlen", C.c_void_p), ("h0", C.c_void_p), ("w", C.c_void_p),
@@ -150,6 +158,11 @@ _sig("fcs_bsw_extend_plan", C.c_int, [C.c_void_p, C.POINTER(BswBatch), C.POINTER
                                       C.c_void_p])
 _sig("fcs_bsw_global", C.c_int, [C.POINTER(BswTask), C.c_int32, C.POINTER(BswParams), i32p, u32p, i64p, i32p,
                                  i32p, C.c_int32])
+_sig("fcs_bsw_align", C.c_int, [C.POINTER(BswTask), C.c_int32, C.POINTER(BswParams), i32p, C.c_void_p, C.c_int32])
+_sig("fcs_bsw_align_dev", C.c_int, [C.POINTER(BswBatch), C.POINTER(BswParams), C.c_void_p, C.c_void_p, C.c_int32,
+                                    C.c_void_p])
+_sig("fcs_ksw_align2", Kswr, [C.c_int, u8p, C.c_int, u8p, C.c_int, i8p, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int,
+                              C.c_void_p])
 _sig("fcs_bsw_global_dev", C.c_int, [C.POINTER(BswBatch), C.POINTER(BswParams), C.c_void_p, C.c_void_p, C.c_int64,
                                      C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_int32,
                                      C.c_void_p])
@@ -457,6 +470,34 @@ def bsw_global(t: BswTasks, params: BswParams | None = None, device=0, with_ciga
                              off.ctypes.data_as(i64p), cap.ctypes.data_as(i32p), ncig.ctypes.data_as(i32p), device))
     cigars = [arena[off[k]:off[k] + ncig[k]].copy() for k in range(n)]
     return scores, cigars
+
+
+def bsw_align(t: BswTasks, xtra, params: BswParams | None = None, device=0) -> np.ndarray:
+    """Batched ksw_align2 (fcs_bsw_align): (n, 7) int32 rows = bwa's kswr_t
+    (score, te, qe, score2, te2, tb, qb)."""
+    params = params or bsw_params()
+    n = t.n
+    tasks = (BswTask * max(n, 1))()
+    for k in range(n):
+        q, tg, _, _ = t.task(k)
+        tasks[k] = BswTask(int(t.qlen[k]), int(t.tlen[k]), 0, 0, q.ctypes.data_as(u8p) if q.size else None,
+                           tg.ctypes.data_as(u8p) if tg.size else None)
+    x = np.ascontiguousarray(np.broadcast_to(np.asarray(xtra, np.int32), (n,)), np.int32)
+    out = np.zeros((max(n, 1), 7), np.int32)
+    check(lib.fcs_bsw_align(tasks, n, C.byref(params), x.ctypes.data_as(i32p), out.ctypes.data, device))
+    return out[:n]
+
+
+def ksw_align2(q, t, xtra, mat=None, o_del=6, e_del=1, o_ins=6, e_ins=1):
+    """bwa's ksw_align2 signature twin: (score, te, qe, score2, te2, tb, qb)."""
+    q = np.ascontiguousarray(q, np.uint8)
+    t = np.ascontiguousarray(t, np.uint8)
+    m = np.ascontiguousarray(default_mat() if mat is None else mat, np.int8)
+    r = lib.fcs_ksw_align2(len(q), q.ctypes.data_as(u8p), len(t), t.ctypes.data_as(u8p), 5, m.ctypes.data_as(i8p),
+                           o_del, e_del, o_ins, e_ins, xtra, None)
+    if r.score == -2147483648:
+        raise FcsError(FCS_ERR_DEVICE, lib.fcs_last_error().decode(errors="replace"))
+    return (r.score, r.te, r.qe, r.score2, r.te2, r.tb, r.qb)
 
 
 def ksw_extend2(q, t, h0, w, mat=None, o_del=6, e_del=1, o_ins=6, e_ins=1, end_bonus=5, zdrop=100):

@@ -83,6 +83,7 @@ struct Cand {
   int seedcov = 0;                   // query bases of the chain's seeds inside the region
   SeedAln aln;                       // qb, qe, rb, re, score, truesc, w (+ CIGAR for output regions)
   int sub = 0, sub_n = 0, secondary = -1;
+  int csub = 0;         // bwa's csub: ksw_align2's second-best score of a mate-rescue hit
   uint64_t hash = 0;
   double frac_rep = 0;  // the read's repetitive fraction (bwa's frac_rep; 0 for rescued hits)
   bool rescued = false; // a mate-rescue hit (seedcov = half the shorter span)
@@ -126,11 +127,12 @@ uint64_t hash64(uint64_t key) {  // bwa's hash_64 (Thomas Wang)
 // bwa raw_mapq.
 int raw_mapq(int diff, int a) { return (int)(6.02 * diff / a + .499); }
 
-// bwa mem_approx_mapq_se (MEM_MAPQ_COEF 30, mapQ_coef_len 0; csub is 0: no
-// sub-optimal score comes out of ksw_extend2).
+// bwa mem_approx_mapq_se (MEM_MAPQ_COEF 30, mapQ_coef_len 0); csub is
+// ksw_align2's second-best score for mate-rescue hits, 0 otherwise.
 int approx_mapq_se(const Cand& c, int min_seed_len, int match, int mismatch) {
   const SeedAln& a = c.aln;
   int sub = c.sub ? c.sub : min_seed_len * match;
+  sub = c.csub > sub ? c.csub : sub;
   if (sub >= a.score || a.score <= 0) return 0;
   const int l = std::max(a.qe - a.qb, (int)(a.re - a.rb));
   const double identity = 1. - (double)(l * match - a.score) / (match + mismatch) / l;
@@ -407,51 +409,6 @@ void extend_chains(const KmerIndex& idx, const fcs_bsw_params& P, const AlignOpt
         if (t.qbeg >= C.aln.qb && t.qbeg + t.len <= C.aln.qe && t.rbeg >= C.aln.rb && t.rbeg + t.len <= C.aln.re)
           C.seedcov += t.len;
     });
-  }
-}
-
-// Extension round for the mate-rescue hits (regions without a chain): each
-// extends inside its rescue window; bwa mem_matesw keeps a hit scoring >=
-// min_seed_len (x match) with seedcov = half the shorter span.
-void extend_loose(const KmerIndex& idx, const fcs_bsw_params& P, const AlignOptions& opt, std::vector<ReadAln*>& reads,
-                  AlignStats& st) {
-  std::vector<SeedJob> jobs;
-  std::vector<Cand*> who;
-  for (ReadAln* R : reads)
-    for (Cand& C : R->cands) {
-      if (C.done) continue;
-      const std::vector<uint8_t>& rc = idx.codes(C.contig);
-      SeedJob J;
-      J.q = R->code[C.rev].data();
-      J.qlen = (int)R->code[C.rev].size();
-      J.ref = rc.data();
-      J.rlen = (int64_t)rc.size();
-      J.seed_q = C.seed_q;
-      J.seed_r = C.seed_r;
-      J.seed_len = C.seed_len;
-      J.win_lo = C.win_lo;
-      J.win_hi = C.win_hi;
-      jobs.push_back(J);
-      who.push_back(&C);
-    }
-  if (jobs.empty()) return;
-  SeedExtOptions so;
-  so.w = opt.w;
-  so.pen_clip5 = so.pen_clip3 = P.end_bonus;
-  so.gpu = opt.gpu;
-  so.threads = opt.threads;
-  so.want_cigar = false;
-  std::vector<SeedAln> res;
-  SeedExtStats xs;
-  extend_seeds(jobs, P, so, res, xs);
-  st.ext_tasks += xs.ext_tasks;
-  st.gpu_seconds += xs.gpu_seconds;
-  for (size_t i = 0; i < who.size(); ++i) {
-    Cand& C = *who[i];
-    C.aln = std::move(res[i]);
-    C.done = true;
-    C.ok = C.aln.qe > C.aln.qb && C.aln.re > C.aln.rb && C.aln.score >= opt.k * P.mat[0];
-    C.seedcov = (int)(std::min<int64_t>(C.aln.re - C.aln.rb, C.aln.qe - C.aln.qb) >> 1);
   }
 }
 
@@ -787,17 +744,24 @@ std::array<PeStat, 4> pestat(const KmerIndex& idx, const std::vector<ReadAln>& m
   return pes;
 }
 
-// Mate rescue (bwa mem_matesw's windows): for each orientation whose
-// distribution holds and in which no region of the mate already pairs with
-// `anchor`, the window where the mate must lie (bwa's arithmetic in the
-// 2 x l space, then clipped to the strand half holding its middle).  bwa runs
-// a local Smith-Waterman (ksw_align2) over the window; here the window's
-// best-supported diagonal of 12-mer exact hits seeds an extension confined to
-// the window (extend_loose, one GPU round for the batch).  Appends the seeds
-// as regions to extend; returns how many.
-int rescue_seeds(const KmerIndex& idx, const std::array<PeStat, 4>& pes, const Cand& anchor, ReadAln& mate,
-                 const AlignOptions& opt) {
-  const int kk = 12;
+// Mate rescue (bwa mem_matesw): for each orientation whose distribution holds
+// and in which no region of the mate already pairs with `anchor`, the window
+// where the mate must lie (bwa's arithmetic in the 2 x l space, then clipped to
+// the strand half holding its middle, as bns_fetch_seq does), aligned by a
+// local Smith-Waterman with bwa's ksw_align2 semantics (the mate reverse-
+// complemented when the orientation says so; xtra = KSW_XSUBO | KSW_XSTART |
+// KSW_XBYTE for short mates | min_seed_len * a).  One job per window; the
+// jobs of the whole batch run as one fcs_bsw_align call.
+struct RescueJob {
+  ReadAln* mate = nullptr;
+  int contig = -1;
+  bool is_rev = false;   // the mate reverse-complemented
+  int64_t rb = 0, re = 0;  // the window in the contig's 2 x l space
+  std::vector<uint8_t> ref;  // its sequence (the reverse strand's is the reverse complement)
+};
+
+void rescue_windows(const KmerIndex& idx, const std::array<PeStat, 4>& pes, const Cand& anchor, ReadAln& mate,
+                    const AlignOptions& opt, std::vector<RescueJob>& jobs) {
   const std::vector<uint8_t>& rc = idx.codes(anchor.contig);
   const int64_t l = (int64_t)rc.size(), lms = (int64_t)mate.code[0].size();
   bool skip[4];
@@ -808,7 +772,6 @@ int rescue_seeds(const KmerIndex& idx, const std::array<PeStat, 4>& pes, const C
     const int r = infer_dir(l, rb2(idx, anchor), rb2(idx, m), dist);
     if (dist >= pes[r].low && dist <= pes[r].high) skip[r] = true;
   }
-  int added = 0;
   const int64_t a_rb = rb2(idx, anchor);
   for (int r = 0; r < 4; ++r) {
     if (skip[r]) continue;
@@ -828,62 +791,75 @@ int rescue_seeds(const KmerIndex& idx, const std::array<PeStat, 4>& pes, const C
     if (rhalf) rb = std::max(rb, l);
     else re = std::min(re, l);
     if (re - rb < opt.k || re - rb > 100000) continue;
-    const int64_t wb = rhalf ? 2 * l - re : rb, we = rhalf ? 2 * l - rb : re;  // forward coordinates
-    const bool rev = is_rev != rhalf;  // the mate's strand on the forward contig
-    std::unordered_multimap<uint32_t, int64_t> win;
-    win.reserve((size_t)(we - wb));
-    uint32_t key = 0;
-    int valid = 0;
-    const uint32_t mask = (1u << (2 * kk)) - 1;
-    for (int64_t p = wb; p < we; ++p) {
-      if (rc[p] > 3) {
-        valid = 0;
-        continue;
-      }
-      key = ((key << 2) | rc[p]) & mask;
-      if (++valid >= kk) win.emplace(key, p - kk + 1);
-    }
-    const std::vector<uint8_t>& q = mate.code[rev];
-    std::map<int64_t, std::pair<int, int>> diag;  // diagonal -> (hits, first query pos)
-    key = 0;
-    valid = 0;
-    for (int i = 0; i < (int)q.size(); ++i) {
-      if (q[i] > 3) {
-        valid = 0;
-        continue;
-      }
-      key = ((key << 2) | q[i]) & mask;
-      if (++valid < kk) continue;
-      const int qp = i - kk + 1;
-      auto range = win.equal_range(key);
-      for (auto it = range.first; it != range.second; ++it) {
-        auto& d = diag[it->second - qp];
-        if (d.first++ == 0) d.second = qp;
-      }
-    }
-    int best = 0;
-    int64_t bd = 0;
-    int bq = 0;
-    for (const auto& [d, h] : diag)
-      if (h.first > best) best = h.first, bd = d, bq = h.second;
-    if (best < 1) continue;
-    int qs = bq, qe = bq + kk;
-    int64_t rs = bd + bq;
-    while (qs > 0 && rs > wb && q[qs - 1] < 4 && q[qs - 1] == rc[rs - 1]) --qs, --rs;
-    while (qe < (int)q.size() && rs + (qe - qs) < we && q[qe] < 4 && q[qe] == rc[rs + (qe - qs)]) ++qe;
-    Cand C;
-    C.rev = rev;
-    C.contig = anchor.contig;
-    C.seed_q = qs;
-    C.seed_len = qe - qs;
-    C.seed_r = rs;
-    C.win_lo = wb;
-    C.win_hi = we;
-    C.rescued = true;
-    mate.cands.push_back(std::move(C));
-    ++added;
+    RescueJob J;
+    J.mate = &mate;
+    J.contig = anchor.contig;
+    J.is_rev = is_rev;
+    J.rb = rb;
+    J.re = re;
+    J.ref.resize((size_t)(re - rb));
+    for (int64_t x = rb; x < re; ++x)  // the 2 x l sequence: forward, then the reverse complement
+      J.ref[(size_t)(x - rb)] = x < l ? rc[x] : (rc[2 * l - 1 - x] < 4 ? (uint8_t)(3 - rc[2 * l - 1 - x]) : 4);
+    jobs.push_back(std::move(J));
   }
-  return added;
+}
+
+// The rescue jobs' local alignments (one batch) and bwa's region for each hit
+// scoring >= min_seed_len with a start: query / reference spans mapped back
+// from the oriented mate and the 2 x l window, score, csub = score2, seedcov =
+// half the shorter span.  Returns the reads that gained a region.
+std::vector<ReadAln*> rescue_align(const KmerIndex& idx, const fcs_bsw_params& P, const AlignOptions& opt,
+                                   std::vector<RescueJob>& jobs, AlignStats& st) {
+  std::vector<ReadAln*> out;
+  if (jobs.empty()) return out;
+  const int a = P.mat[0];
+  std::vector<fcs_bsw_task> tasks(jobs.size());
+  std::vector<int32_t> xtra(jobs.size());
+  for (size_t k = 0; k < jobs.size(); ++k) {
+    const RescueJob& J = jobs[k];
+    const std::vector<uint8_t>& q = J.mate->code[J.is_rev];
+    tasks[k] = fcs_bsw_task{(int32_t)q.size(), (int32_t)J.ref.size(), 0, 0, q.data(), J.ref.data()};
+    xtra[k] = FCS_KSW_XSUBO | FCS_KSW_XSTART | ((int)q.size() * a < 250 ? FCS_KSW_XBYTE : 0) | (opt.k * a);
+  }
+  std::vector<fcs_kswr> res(jobs.size());
+  const uint64_t t0 = now_us();
+  if (fcs_bsw_align(tasks.data(), (int32_t)tasks.size(), &P, xtra.data(), res.data(), opt.gpu) != FCS_OK)
+    throw internalError(std::string("[E::fcsg] fcs_bsw_align: ") + fcs_last_error());
+  st.gpu_seconds += (now_us() - t0) / 1e6;
+  st.ext_tasks += (int64_t)jobs.size();
+  for (size_t k = 0; k < jobs.size(); ++k) {
+    const RescueJob& J = jobs[k];
+    const fcs_kswr& x = res[k];
+    if (x.score < opt.k || x.qb < 0) continue;  // bwa: aln.score >= min_seed_len && aln.qb >= 0
+    const int64_t l = (int64_t)idx.codes(J.contig).size();
+    const int lms = (int)J.mate->code[0].size();
+    // bwa's region in the 2 x l space and on the original mate
+    const int qb = J.is_rev ? lms - (x.qe + 1) : x.qb, qe = J.is_rev ? lms - x.qb : x.qe + 1;
+    const int64_t rb = J.is_rev ? 2 * l - (J.rb + x.te + 1) : J.rb + x.tb;
+    const int64_t re = J.is_rev ? 2 * l - (J.rb + x.tb) : J.rb + x.te + 1;
+    Cand C;
+    C.contig = J.contig;
+    C.rev = rb >= l;
+    if (!C.rev) {
+      C.aln.rb = rb, C.aln.re = re, C.aln.qb = qb, C.aln.qe = qe;
+    } else {  // forward coordinates, query on the reverse-complemented mate
+      C.aln.rb = 2 * l - re, C.aln.re = 2 * l - rb, C.aln.qb = lms - qe, C.aln.qe = lms - qb;
+    }
+    C.aln.score = C.aln.truesc = x.score;
+    C.csub = x.score2 > 0 ? x.score2 : 0;
+    C.seedcov = (int)(std::min<int64_t>(C.aln.re - C.aln.rb, C.aln.qe - C.aln.qb) >> 1);
+    C.rescued = C.done = C.ok = true;
+    ReadAln& M = *J.mate;
+    // bwa inserts the region into the mate's score-sorted list (after the
+    // equal scores)
+    size_t at = 0;
+    while (at < M.cands.size() && M.cands[at].aln.score >= C.aln.score) ++at;
+    M.cands.insert(M.cands.begin() + (std::ptrdiff_t)at, std::move(C));
+    if (out.empty() || out.back() != &M) out.push_back(&M);
+  }
+  std::sort(out.begin(), out.end());
+  out.erase(std::unique(out.begin(), out.end()), out.end());
+  return out;
 }
 
 // bwa mem_pair: every (region of read 1, region of read 2) in a valid
@@ -1260,7 +1236,7 @@ AlignStats align_pairs(const Reference& ref, const KmerIndex& idx, const std::ve
   // mate rescue (bwa mem_sam_pe): every region of a read within pen_unpaired of
   // its best (at most max_matesw) searches the mate's windows
   if (!pes[0].failed || !pes[1].failed || !pes[2].failed || !pes[3].failed) {
-    std::vector<std::array<int, 2>> added(n);
+    std::vector<std::vector<RescueJob>> per(n);
     parallel_for(n, opt.threads, [&](size_t i) {
       ReadAln* r[2] = {&m1[i], &m2[i]};
       std::vector<Cand> anchors[2];
@@ -1268,18 +1244,14 @@ AlignStats align_pairs(const Reference& ref, const KmerIndex& idx, const std::ve
         for (const Cand& c : r[s]->cands)
           if (c.aln.score >= r[s]->cands[0].aln.score - opt.pen_unpaired && (int)anchors[s].size() < opt.max_matesw)
             anchors[s].push_back(c);
-      for (int s = 0; s < 2; ++s) {
-        added[i][!s] = 0;
-        for (const Cand& a : anchors[s]) added[i][!s] += rescue_seeds(idx, pes, a, *r[!s], opt);
-      }
+      for (int s = 0; s < 2; ++s)
+        for (const Cand& a : anchors[s]) rescue_windows(idx, pes, a, *r[!s], opt, per[i]);
     });
-    std::vector<ReadAln*> resc;
-    for (size_t i = 0; i < n; ++i) {
-      if (added[i][0]) resc.push_back(&m1[i]);
-      if (added[i][1]) resc.push_back(&m2[i]);
-    }
+    std::vector<RescueJob> jobs;
+    for (auto& v : per)
+      for (RescueJob& J : v) jobs.push_back(std::move(J));
     const uint64_t te = now_us();
-    extend_loose(idx, P, opt, resc, st);
+    std::vector<ReadAln*> resc = rescue_align(idx, P, opt, jobs, st);
     dedup_patch(idx, P, opt, resc, false, st);
     st.extend_seconds += (now_us() - te) / 1e6;
     st.pair_seconds -= (now_us() - te) / 1e6;
@@ -1311,7 +1283,7 @@ AlignStats align_pairs(const Reference& ref, const KmerIndex& idx, const std::ve
           if (c.secondary >= 0) c.sub = a[s]->cands[c.secondary].aln.score, c.secondary = -2;
           q_se[s] = approx_mapq_se(c, opt.k, P.mat[0], -P.mat[1]);
           q_se[s] = q_se[s] > q_pe ? q_se[s] : q_pe < q_se[s] + 40 ? q_pe : q_se[s] + 40;
-          q_se[s] = std::min(q_se[s], raw_mapq(c.aln.score, P.mat[0]));  // csub 0: bwa's tandem-repeat cap
+          q_se[s] = std::min(q_se[s], raw_mapq(c.aln.score - c.csub, P.mat[0]));  // bwa's tandem-repeat cap
         }
         proper[i] = 1;
       } else {

@@ -18,17 +18,19 @@
 //     (mem_approx_mapq_se with frac_rep); supplementary = further
 //     non-overlapping regions (split reads: flag 0x800, hard clips, SA tags);
 //   * paired ends (mem_sam_pe): mem_pestat per orientation, mate rescue in
-//     mem_matesw's windows, mem_pair's best pair by score + insert-size
+//     mem_matesw's windows by bwa's ksw_align2 (GPU, fcs_bsw_align: score,
+//     score2 as csub, start by the reverse pass), mem_pair's best pair by score + insert-size
 //     likelihood, secondary regions re-rooted when they make the pair, paired
 //     MAPQ; split reads and unpaired best hits go out single-end style;
 //   * CIGARs by mem_reg2aln / bwa_gen_cigar2 (GPU ksw_global2); NM / MD / AS /
 //     XS tags; sorted BAM + BAI.
 // [EXT] bwa is not vendored, so this is a restatement (parity unpinned against
-// bwa itself).  Known differences: the mate rescue finds its hit by 12-mer
-// seeds + a window-confined extension where bwa runs a local Smith-Waterman
-// (ksw_align2; no csub), reverse-strand regions are extended right-first
-// where bwa extends its reverse-complement space left-first (tie-breaking
-// only), and mem_flt_chained_seeds (long reads only) is not applied.
+// bwa itself).  Known differences: reverse-strand regions are extended
+// right-first where bwa extends its reverse-complement space left-first
+// (tie-breaking only), mem_flt_chained_seeds (long reads only) is not applied,
+// a rescued region's truesc is its score (bwa leaves it 0, which would give
+// its CIGAR a zero band), and the rescue list is deduplicated once after all
+// orientations rather than after each.
 #pragma once
 
 #include <cstdint>

@@ -284,6 +284,28 @@ int fcs_bsw_global_dev(const fcs_bsw_batch* dev_batch, const fcs_bsw_params* par
                        const int64_t* dev_cigar_off, const int32_t* dev_cigar_cap, int32_t* dev_n_cigar,
                        int32_t device, void* stream);
 
+/* Batched ksw_align2: bwa's local Smith-Waterman with the second-best score
+ * and the alignment start (bwa ksw.c ksw_align2 = ksw_u8 / ksw_i16 + the
+ * KSW_XSTART reverse pass), the kernel of bwa mem's mate rescue (mem_matesw:
+ * xtra = KSW_XSUBO | KSW_XSTART | (l_ms * a < 250 ? KSW_XBYTE : 0) |
+ * min_seed_len * a).  Replaces the call inside bwa-flow reached from
+ * /root/reference/src/workers/BWAWorker.cpp:134-166.  Task k: query / target
+ * codes 0..4 (qlen <= 1024), tasks[k].h0 / .w ignored, xtra[k] bwa's xtra word.
+ * out[k] = bwa's kswr_t (score, te, qe, score2, te2, tb, qb; -1 where bwa
+ * leaves -1). */
+#define FCS_KSW_XBYTE 0x10000
+#define FCS_KSW_XSTOP 0x20000
+#define FCS_KSW_XSUBO 0x40000
+#define FCS_KSW_XSTART 0x80000
+typedef struct {
+  int32_t score, te, qe, score2, te2, tb, qb;
+} fcs_kswr;
+int fcs_bsw_align(const fcs_bsw_task* tasks, int32_t n, const fcs_bsw_params* params, const int32_t* xtra,
+                  fcs_kswr* out, int32_t device);
+/* Device path (stream-ordered, no host sync): dev_xtra[k], dev_out[k] as above. */
+int fcs_bsw_align_dev(const fcs_bsw_batch* dev_batch, const fcs_bsw_params* params, const int32_t* dev_xtra,
+                      fcs_kswr* dev_out, int32_t device, void* stream);
+
 /* Signature twins of bwa's ksw.c entry points, running on GPU `device` 0 (or
  * the device set by fcs_set_default_device).  m must be 5.  They return the
  * score exactly as bwa does; because a global score can be negative, failure
@@ -298,6 +320,11 @@ int fcs_ksw_extend2(int qlen, const uint8_t* query, int tlen, const uint8_t* tar
 int fcs_ksw_global2(int qlen, const uint8_t* query, int tlen, const uint8_t* target, int m,
                     const int8_t* mat, int o_del, int e_del, int o_ins, int e_ins, int w,
                     int* n_cigar, uint32_t** cigar);
+/* bwa's kswr_t ksw_align2(qlen, query, tlen, target, m, mat, o_del, e_del,
+ * o_ins, e_ins, xtra, qry); qry must be NULL (no cached profile).  On failure
+ * the returned score is FCS_KSW_FAILED (fcs_last_error()). */
+fcs_kswr fcs_ksw_align2(int qlen, const uint8_t* query, int tlen, const uint8_t* target, int m, const int8_t* mat,
+                        int o_del, int e_del, int o_ins, int e_ins, int xtra, void** qry);
 int fcs_set_default_device(int32_t device);
 
 /* ---------------------------------------------- synthetic workload builders */

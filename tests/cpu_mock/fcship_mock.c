@@ -2,8 +2,9 @@
  * TEST INFRASTRUCTURE ONLY — never shipped, never on a product path.
  *
  * A CPU stand-in for libfcship.so's banded Smith-Waterman entry points
- * (fcs_bsw_extend, fcs_bsw_global), computed by the oracle's ksw_extend2 /
- * ksw_global2 restatement (oracle/ksw_oracle.c), so that the `-m "not gpu"`
+ * (fcs_bsw_extend, fcs_bsw_global, fcs_bsw_align), computed by the oracle's
+ * ksw_extend2 / ksw_global2 / ksw_align2 restatements (oracle/ksw_oracle.c,
+ * oracle/ksw_align_oracle.c), so that the `-m "not gpu"`
  * tests can drive the aligner's host logic (chains, dedup / patch, primary /
  * supplementary marking, pairing, SAM fields) in a container without a GPU.
  * tests/test_align_host_cpu.py compiles it into a temporary directory and
@@ -54,6 +55,9 @@ int oracle_ksw_global2(int qlen, const uint8_t* query, int tlen, const uint8_t* 
                        int o_del, int e_del, int o_ins, int e_ins, int w, int* n_cigar, uint32_t* cigar_out,
                        int cigar_cap);
 
+void oracle_ksw_align2(int qlen, const uint8_t* query, int tlen, const uint8_t* target, int m, const int8_t* mat,
+                       int o_del, int e_del, int o_ins, int e_ins, int xtra, int* out);
+
 static __thread const char* g_err = "";
 
 const char* fcs_last_error(void) { return g_err; }
@@ -101,6 +105,18 @@ int fcs_bsw_global(const fcs_bsw_task* t, int32_t n, const fcs_bsw_params* p, in
   }
   if (rc != FCS_OK) g_err = "fcs_bsw_global: CIGAR longer than its cap";
   return rc;
+}
+
+int fcs_bsw_align(const fcs_bsw_task* t, int32_t n, const fcs_bsw_params* p, const int32_t* xtra, fcs_kswr* out,
+                  int32_t device) {
+  (void)device;
+  for (int32_t k = 0; k < n; ++k) {
+    int r[7];
+    oracle_ksw_align2(t[k].qlen, t[k].query, t[k].tlen, t[k].target, 5, p->mat, p->o_del, p->e_del, p->o_ins,
+                      p->e_ins, xtra[k], r);
+    out[k] = (fcs_kswr){r[0], r[1], r[2], r[3], r[4], r[5], r[6]};
+  }
+  return FCS_OK;
 }
 
 void fcs_phmm_opts_default(fcs_phmm_opts* o) { memset(o, 0, sizeof *o); }

@@ -54,6 +54,8 @@ lib.oracle_ksw_extend2.restype = C.c_int
 lib.oracle_ksw_extend2.argtypes = [C.c_int, vp, C.c_int, vp, C.c_int, vp] + [C.c_int] * 8 + [vp] * 6
 lib.oracle_ksw_global2.restype = C.c_int
 lib.oracle_ksw_global2.argtypes = [C.c_int, vp, C.c_int, vp, C.c_int, vp] + [C.c_int] * 5 + [vp, vp, C.c_int]
+lib.oracle_ksw_align2.restype = None
+lib.oracle_ksw_align2.argtypes = [C.c_int, vp, C.c_int, vp, C.c_int, vp] + [C.c_int] * 5 + [vp]
 lib.oracle_ksw_extend2_batch.restype = None
 lib.oracle_ksw_extend2_batch.argtypes = [vp, vp, vp, vp, vp, vp, vp, vp, C.c_int64, vp] + [C.c_int] * 6 + \
     [vp, vp, C.c_int]
@@ -157,6 +159,20 @@ def ksw_global2(q, t, w, mat, o_del=6, e_del=1, o_ins=6, e_ins=1):
     sc = lib.oracle_ksw_global2(len(q), _p(q), len(t), _p(t), 5, _p(m), o_del, e_del, o_ins, e_ins, w,
                                 C.addressof(n), _p(cig), cap)
     return sc, cig[:n.value].copy()
+
+
+KSW_XBYTE, KSW_XSTOP, KSW_XSUBO, KSW_XSTART = 0x10000, 0x20000, 0x40000, 0x80000
+
+
+def ksw_align2(q, t, mat, xtra, o_del=6, e_del=1, o_ins=6, e_ins=1):
+    """bwa ksw_align2 restated (oracle/ksw_align_oracle.c): (score, te, qe,
+    score2, te2, tb, qb) as bwa's kswr_t."""
+    q = _a(q)
+    t = _a(t)
+    m = _a(mat, np.int8)
+    out = np.zeros(7, np.int32)
+    lib.oracle_ksw_align2(len(q), _p(q), len(t), _p(t), 5, _p(m), o_del, e_del, o_ins, e_ins, xtra, _p(out))
+    return tuple(int(x) for x in out)
 
 
 def ksw_extend2_batch(t, mat, o_del=6, e_del=1, o_ins=6, e_ins=1, end_bonus=5, zdrop=100, threads=1):

@@ -16,12 +16,9 @@ ROOT = __import__("os").path.dirname(__import__("os").path.dirname(__import__("o
 
 
 @pytest.fixture(scope="module")
-def mock_env(tmp_path_factory):
-    d = tmp_path_factory.mktemp("mock")
-    subprocess.run(["gcc", "-O2", "-shared", "-fPIC", "-I", f"{ROOT}/include", f"{ROOT}/tests/cpu_mock/fcship_mock.c",
-                    f"{ROOT}/oracle/ksw_oracle.c", f"{ROOT}/oracle/pairhmm_oracle.c", "-lm", "-o",
-                    str(d / "libfcship.so")], check=True)
-    return {"LD_LIBRARY_PATH": str(d), "FCS_GPU_DEVICES": "0"}
+def mock_env():
+    subprocess.run(["make", "-C", f"{ROOT}/tests/cpu_mock"], check=True, capture_output=True)
+    return {"LD_LIBRARY_PATH": f"{ROOT}/tests/cpu_mock/build", "FCS_GPU_DEVICES": "0"}
 
 
 @pytest.fixture(scope="module")

@@ -342,3 +342,64 @@ def test_global_dev_direction_layouts(gpu, gap):
         assert sc[k] == rs, f"task {k}: score {sc[k]} != {rs}"
         got = cg[coff[k]:coff[k] + nc[k]]
         assert np.array_equal(got, rc), f"task {k}: {fcship.cigar_str(got)} != {fcship.cigar_str(rc)}"
+
+
+def align_tasks(seed, n, qmin=20, qmax=200, tmin=40, tmax=700, related=0.7):
+    """Mate-rescue-shaped ksw_align2 tasks: a query that is (mostly) a mutated
+    piece of its target window, sometimes twice (score2), sometimes unrelated."""
+    rng = np.random.default_rng(seed)
+    items = []
+    for k in range(n):
+        ql = int(rng.integers(qmin, qmax + 1))
+        tl = int(rng.integers(tmin, tmax + 1))
+        t = rng.integers(0, 4, tl).astype(np.uint8)
+        if rng.random() < related and tl > 8:
+            a = int(rng.integers(0, max(1, tl - ql // 2)))
+            q, _ = related_pair(rng, ql, ql, sub=0.03, indel=0.01)
+            piece = t[a:a + ql]
+            q = piece.copy() if rng.random() < 0.5 else q
+            if len(q) > 4:
+                for j in range(len(q)):
+                    if rng.random() < 0.04:
+                        q[j] = (q[j] + 1) % 4
+            if rng.random() < 0.3 and tl > 2 * len(q) + 10:  # a second, weaker copy far away
+                b = int(rng.integers(0, tl - len(q)))
+                t[b:b + len(q)] = q
+                t[b + len(q) // 2] = (t[b + len(q) // 2] + 1) % 4
+        else:
+            q = rng.integers(0, 4, ql).astype(np.uint8)
+        if rng.random() < 0.05:
+            q[int(rng.integers(0, len(q)))] = 4  # N
+        items.append((np.asarray(q, np.uint8), t, 0, 0))
+    return fcship.make_tasks(items)
+
+
+@pytest.mark.parametrize("xbyte", [True, False])
+def test_ksw_align2_batch_bit_exact(gpu, xbyte):
+    """Batched ksw_align2 (mate rescue, row a5's family) against the striped
+    restatement: all seven kswr_t fields, with mem_matesw's xtra (XSUBO |
+    XSTART | min_seed_len 19), u8 (KSW_XBYTE, p = 16) and i16 (p = 8)."""
+    t = align_tasks(31 if xbyte else 32, 400, qmax=240 if xbyte else 400)
+    m = fcship.default_mat()
+    x = fcship.KSW_XSUBO | fcship.KSW_XSTART | (fcship.KSW_XBYTE if xbyte else 0) | 19
+    got = fcship.bsw_align(t, x)
+    for k in range(t.n):
+        q, tg, _, _ = t.task(k)
+        ref = oracle_lib.ksw_align2(q, tg, m, x)
+        assert tuple(got[k]) == ref, f"task {k} (qlen {len(q)}, tlen {len(tg)}): {tuple(got[k])} != {ref}"
+
+
+def test_ksw_align2_flags_and_twin(gpu):
+    """Without XSUBO every column counts and no b[] list; without XSTART no
+    start; XSTOP ends at a score; the signature twin equals the batch."""
+    t = align_tasks(33, 60, qmax=150)
+    m = fcship.default_mat()
+    for x in (fcship.KSW_XBYTE, fcship.KSW_XSTART, fcship.KSW_XSUBO | 30, fcship.KSW_XSTOP | 40,
+              fcship.KSW_XBYTE | fcship.KSW_XSUBO | fcship.KSW_XSTART | 25):
+        got = fcship.bsw_align(t, x)
+        for k in range(t.n):
+            q, tg, _, _ = t.task(k)
+            assert tuple(got[k]) == oracle_lib.ksw_align2(q, tg, m, x), (hex(x), k)
+    q, tg, _, _ = t.task(5)
+    x = fcship.KSW_XBYTE | fcship.KSW_XSUBO | fcship.KSW_XSTART | 19
+    assert fcship.ksw_align2(q, tg, x) == oracle_lib.ksw_align2(q, tg, m, x)

@@ -10,6 +10,7 @@ import json
 import os
 
 import numpy as np
+import pytest
 
 import oracle_lib
 
@@ -190,3 +191,78 @@ def test_golden_fixtures():
     for c in g["global"]:
         sc, cig = oracle_lib.ksw_global2(c["q"], c["t"], c["w"], mat)
         assert sc == c["score"] and list(map(int, cig)) == c["cigar"]
+
+
+# ------------------------------------------------------------ ksw_align2 (mate rescue)
+def _textbook_local(q, t, mat, o_del=6, e_del=1, o_ins=6, e_ins=1, stop=None):
+    """Gotoh local alignment, rows = target (bwa's i), columns = query (j):
+    best score, the first row reaching it, the smallest column holding it in
+    that row.  stop: end at the first row whose maximum reaches `stop`."""
+    n, m = len(t), len(q)
+    NEG = -10 ** 9
+    Hp = [0] * (m + 1)
+    E = [NEG] * (m + 1)
+    best, te, qe = 0, -1, -1
+    for i in range(n):
+        H = [0] * (m + 1)
+        F = NEG
+        for j in range(1, m + 1):
+            E[j] = max(Hp[j] - o_del - e_del, E[j] - e_del)
+            F = max(H[j - 1] - o_ins - e_ins, F - e_ins)
+            H[j] = max(0, Hp[j - 1] + int(mat[t[i] * 5 + q[j - 1]]), E[j], F)
+        rmax = max(H[1:]) if m else 0
+        if rmax > best:
+            best, te, qe = rmax, i, H.index(rmax, 1) - 1
+            if stop is not None and best >= stop:
+                break
+        Hp = H
+    return best, te, qe
+
+
+@pytest.mark.parametrize("xbyte", [True, False])
+def test_ksw_align2_matches_textbook_local(xbyte):
+    """Score, te and qe of the striped restatement equal a textbook local
+    alignment (no insertion directly followed by a deletion is ever optimal
+    with bwa's defaults, the only paths the striped E rule excludes); tb / qb
+    equal the textbook reverse alignment's first row and column reaching the
+    score."""
+    mat = np.asarray(MAT, np.int8)
+    rng = np.random.default_rng(5 if xbyte else 6)
+    x = oracle_lib.KSW_XSUBO | oracle_lib.KSW_XSTART | (oracle_lib.KSW_XBYTE if xbyte else 0) | 19
+    for _ in range(40):
+        tlen = int(rng.integers(60, 260))
+        t = rng.integers(0, 4, tlen).astype(np.uint8)
+        ql = int(rng.integers(20, 90))
+        a = int(rng.integers(0, tlen - ql // 2))
+        q = t[a:a + ql].copy()
+        for k in range(len(q)):  # substitutions and one indel
+            if rng.random() < 0.05:
+                q[k] = (q[k] + 1 + rng.integers(0, 3)) % 4
+        if rng.random() < 0.5 and len(q) > 10:
+            c = int(rng.integers(3, len(q) - 3))
+            q = np.concatenate([q[:c], q[c + 2:]]) if rng.random() < 0.5 else np.concatenate([q[:c], [1, 2], q[c:]])
+        q = np.concatenate([rng.integers(0, 4, 5), q, rng.integers(0, 4, 5)]).astype(np.uint8)
+        got = oracle_lib.ksw_align2(q, t, mat, x)
+        sc, te, qe = _textbook_local(list(q), list(t), mat)
+        assert got[:3] == (sc, te, qe), (got, sc, te, qe)
+        if sc >= 19:
+            rq, rt = list(q[:qe + 1][::-1]), list(t[:te + 1][::-1]) + list(t[te + 1:])
+            s2, te2, qe2 = _textbook_local(rq, rt, mat, stop=sc)
+            assert s2 == sc and (got[5], got[6]) == (te - te2, qe - qe2), (got, te2, qe2)
+        else:
+            assert got[5] == got[6] == -1  # XSUBO: below minsc no start is searched
+
+
+def test_ksw_align2_suboptimal_hit():
+    """score2 / te2 (mem_matesw's csub): a second copy of the query far from
+    the best hit is reported; a copy inside te +- score is not."""
+    mat = np.asarray(MAT, np.int8)
+    rng = np.random.default_rng(9)
+    q = rng.integers(0, 4, 60).astype(np.uint8)
+    q2 = q.copy()
+    q2[[10, 30, 50]] = (q2[[10, 30, 50]] + 1) % 4  # a weaker copy: 3 mismatches
+    t = np.concatenate([rng.integers(0, 4, 40), q2, rng.integers(0, 4, 200), q, rng.integers(0, 4, 30)]).astype(np.uint8)
+    x = oracle_lib.KSW_XSUBO | oracle_lib.KSW_XSTART | oracle_lib.KSW_XBYTE | 19
+    sc, te, qe, sc2, te2, tb, qb = oracle_lib.ksw_align2(q, t, mat, x)
+    assert (sc, qe, qb) == (60, 59, 0) and te == 40 + 60 + 200 + 59 and tb == 300
+    assert sc2 == 60 - 3 * 5 and te2 == 40 + 59
