@@ -87,6 +87,7 @@ struct Cand {
   uint64_t hash = 0;
   double frac_rep = 0;  // the read's repetitive fraction (bwa's frac_rep; 0 for rescued hits)
   bool rescued = false; // a mate-rescue hit (seedcov = half the shorter span)
+  std::vector<int> xa;  // output regions: the alternative hits of its XA tag (bwa mem_gen_alt)
   bool done = false;  // extended
   bool ok = false;    // has an alignment (qe > qb, re > rb)
 };
@@ -921,16 +922,39 @@ int mem_pair(const KmerIndex& idx, const std::array<PeStat, 4>& pes, const ReadA
   return ret;
 }
 
+// bwa mem_gen_alt: the XA hits of each output region k are the regions that
+// are secondary to k (get_pri_idx) and score >= XA_drop_ratio (0.80) x k's
+// score; a region with more than max_XA_hits (5) of them gets none.  No ALT
+// contigs here, so max_XA_hits_alt does not arise.
+void xa_hits(ReadAln& R) {
+  constexpr double kXaDropRatio = 0.80;
+  constexpr int kMaxXaHits = 5;
+  for (Cand& c : R.cands) c.xa.clear();
+  for (const auto& o : R.outs) {
+    Cand& k = R.cands[o.first];
+    for (int i = 0; i < (int)R.cands.size(); ++i)
+      if (R.cands[i].secondary == o.first && R.cands[i].aln.score >= k.aln.score * kXaDropRatio) k.xa.push_back(i);
+    if ((int)k.xa.size() > kMaxXaHits) k.xa.clear();
+  }
+}
+
 // The CIGARs (mem_reg2aln / bwa_gen_cigar2) of every output region of the
-// batch (R.outs of each read) in one round of GPU global alignments.
+// batch (R.outs of each read) and of their XA hits, in one round of GPU global
+// alignments.
 void output_cigars(const KmerIndex& idx, const fcs_bsw_params& P, const AlignOptions& opt,
                    const std::vector<ReadAln*>& reads, AlignStats& st) {
   std::vector<SeedJob> jobs;
   std::vector<SeedAln> alns;
   std::vector<Cand*> who;
-  for (ReadAln* R : reads)
+  for (ReadAln* R : reads) {
+    xa_hits(*R);
+    std::vector<int> need;
     for (const auto& o : R->outs) {
-      Cand& C = R->cands[o.first];
+      need.push_back(o.first);
+      for (int i : R->cands[o.first].xa) need.push_back(i);
+    }
+    for (int ci : need) {
+      Cand& C = R->cands[ci];
       const std::vector<uint8_t>& rc = idx.codes(C.contig);
       SeedJob J;
       J.q = R->code[C.rev].data();
@@ -941,6 +965,7 @@ void output_cigars(const KmerIndex& idx, const fcs_bsw_params& P, const AlignOpt
       alns.push_back(C.aln);
       who.push_back(&C);
     }
+  }
   if (jobs.empty()) return;
   SeedExtOptions so;
   so.w = opt.w;
@@ -1015,6 +1040,19 @@ OutAln out_aln(const Reference& ref, const ReadAln& R, int i, int mapq) {
   return o;
 }
 
+// XA:Z of an output region (bwa mem_gen_alt): "rname,[+-]pos,CIGAR,NM;" per
+// alternative hit, CIGAR with soft clips.
+std::string xa_tag(const Reference& ref, const ReadAln& R, const Cand& C) {
+  std::string s;
+  for (int i : C.xa) {
+    const OutAln o = out_aln(ref, R, i, 0);
+    s += ref.contigs[o.c->contig].name + "," + (o.c->rev ? "-" : "+") + std::to_string(o.c->aln.rb + 1) + ",";
+    for (uint32_t c : o.cig) s += std::to_string(cigar_len(c)) + "MIDNSHP=X"[cigar_op(c)];
+    s += "," + std::to_string(o.nm) + ";";
+  }
+  return s;
+}
+
 // SA:Z of output alignment `self`: the read's other primary / supplementary
 // alignments, "rname,pos,strand,CIGAR,mapQ,NM;" (bwa mem_aln2sam; soft clips).
 std::string sa_tag(const Reference& ref, const std::vector<OutAln>& v, size_t self) {
@@ -1080,6 +1118,7 @@ std::vector<BamRecord> make_records(const Reference& ref, const ReadAln& R, cons
     rec.set_aux_int("AS", C.aln.score);
     rec.set_aux_int("XS", C.sub);
     if (v.size() > 1) rec.set_aux_string("SA", sa_tag(ref, v, k));
+    if (!C.xa.empty()) rec.set_aux_string("XA", xa_tag(ref, R, C));
     out.push_back(std::move(rec));
   }
   return out;

@@ -95,3 +95,37 @@ def test_saved_index_rejected_after_same_length_edit(mock_env, tmp_path):
     ref.write_text("\n".join(lines))
     p = H.run_cli("align", "-f", "-r", ref, "-1", fq, "-o", tmp_path / "b.bam", env=mock_env, cwd=tmp_path)
     assert p.returncode == 0 and "built in memory" in p.stderr, p.stderr[-2000:]
+
+
+def test_xa_alternative_hits_cpu(mock_env, tmp_path):
+    """bwa's XA tag (mem_gen_alt): a read from a segment that exists twice
+    (an exact copy on chr21, a copy with one substitution on chr20) is placed
+    on the exact copy, and its record lists the other copy as
+    "chr20,[+-]pos,CIGAR,NM;" (secondary hits scoring >= 0.80 of the primary)."""
+    import numpy as np
+    d = tmp_path / "r"
+    p = H.run_cli("synth", "-o", d, "-c", "chr20:60000,chr21:30000", "-x", "1", "--seed", "21", "--no-fastq")
+    assert p.returncode == 0, p.stderr[-2000:]
+    contigs = A.read_fasta(d / "ref.fasta")
+    rng = np.random.default_rng(4)
+    seg = "".join(rng.choice(list("ACGT"), 400))
+    seg_b = seg[:200] + {"A": "C", "C": "G", "G": "T", "T": "A"}[seg[200]] + seg[201:]
+    c20 = contigs["chr20"][:20000] + seg_b + contigs["chr20"][20400:]
+    c21 = contigs["chr21"][:10000] + seg + contigs["chr21"][10400:]
+    ref = tmp_path / "ref.fasta"
+    ref.write_text(f">chr20\n{c20}\n>chr21\n{c21}\n")
+    fq = tmp_path / "r.fastq"
+    reads = [(f"x{k}", seg[a:a + 150]) for k, a in enumerate((60, 120, 180))]
+    fq.write_text("".join(f"@{n}\n{s}\n+\n{'I' * 150}\n" for n, s in reads))
+    out = tmp_path / "o.bam"
+    p = H.run_cli("align", "-r", ref, "-1", fq, "-o", out, env=mock_env, cwd=tmp_path)
+    assert p.returncode == 0, p.stderr[-2000:]
+    names, _, recs = H.read_bam(out)
+    assert len(recs) == 3
+    for r in recs:
+        assert names[r["ref_id"]] == "chr21", r
+        tags = H.parse_aux(r["aux"])
+        a = int(r["name"][1:])
+        start = 20000 + (60, 120, 180)[a] + 1
+        assert tags.get("XA") == f"chr20,+{start},150M,1;", tags
+        assert r["mapq"] < 10  # the near-identical copy makes the placement ambiguous
