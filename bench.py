@@ -247,6 +247,10 @@ def shard_stats(logs, dt):
     st["phmm_device_seconds"] = round(dev, 4)
     st["rescue_fp64_device_seconds"] = round(res, 4)
     st["gpu_busy_frac"] = round(dev / dt, 4)  # PairHMM device time (HIP events) / wall time, one GPU
+    # cells over the passes' summed HIP-event spans: with passes merged across
+    # shards (gpu.phmm.combine_ms) the spans no longer overlap, so this is the
+    # device-effective PairHMM rate
+    st["phmm_device_tcups"] = round(st["cells"] / dev / 1e12, 3) if dev > 0 else None
     st["effective_gcups"] = round(st["cells"] / dt / 1e9, 2)
     return st
 

@@ -6,11 +6,15 @@
 #include <algorithm>
 #include <array>
 #include <charconv>
+#include <chrono>
 #include <cmath>
+#include <condition_variable>
 #include <cstdio>
 #include <cstring>
+#include <deque>
 #include <map>
 #include <memory>
+#include <mutex>
 #include <string_view>
 #include <tuple>
 #include <type_traits>
@@ -404,6 +408,113 @@ void dump_region(std::FILE* f, const Region& g, int s) {
   std::fwrite(g.lik[s].data(), 8, g.lik[s].size(), f);
 }
 
+// Device passes of concurrent shard threads merged into one (group commit).
+// Each shard of `htc` / `mutect2` batches its own regions, so at the C4 shape
+// (31 Mbp per GPU in 32 shards) a pass is ~87K pairs, and the per-pass fixed
+// work (schedule sort, class launches, rescue) holds the device-effective rate
+// to about half of a 1M-pair pass.  Shard threads hand their region lists to
+// the combiner of their (device, rescue) slot; the oldest waiting request
+// leads: it gathers until every active shard thread of the slot is waiting,
+// its window (`gpu.phmm.combine_ms`) ends or the pass holds `max_pairs`, then
+// runs ONE fcs_phmm_compute_regions over the concatenated region list (each
+// region keeps its own output matrix, so results are bitwise those of separate
+// passes) while later requests queue for the next pass.  A waiting thread
+// yields its CPU to the shards still building regions.
+class PassCombiner {
+ public:
+  struct Req {
+    const std::vector<fcs_phmm_region>* regs = nullptr;
+    int64_t pairs = 0;
+    int rc = FCS_OK;
+    std::string err;
+    bool done = false, led = false;
+    double dev_ms = 0, res_ms = 0;
+    int64_t rescued = 0;
+  };
+  void enter() {
+    std::lock_guard<std::mutex> g(m_);
+    ++active_;
+  }
+  void leave() {
+    std::lock_guard<std::mutex> g(m_);
+    --active_;
+    cv_.notify_all();
+  }
+  void run(Req& r, const fcs_phmm_opts& o, int window_ms, int64_t max_pairs) {
+    std::unique_lock<std::mutex> lk(m_);
+    q_.push_back(&r);
+    cv_.notify_all();
+    const auto deadline = std::chrono::steady_clock::now() + std::chrono::milliseconds(window_ms);
+    while (!r.done) {
+      if (busy_ || q_.front() != &r) {
+        cv_.wait(lk);
+        continue;
+      }
+      auto ready = [&] {
+        int64_t pairs = 0;
+        for (const Req* x : q_) pairs += x->pairs;
+        return (int)q_.size() >= active_ || pairs >= max_pairs;
+      };
+      while (!ready() && cv_.wait_until(lk, deadline) != std::cv_status::timeout) {
+      }
+      std::vector<Req*> take;
+      int64_t tp = 0;
+      while (!q_.empty() && (take.empty() || tp + q_.front()->pairs <= max_pairs)) {
+        tp += q_.front()->pairs;
+        take.push_back(q_.front());
+        q_.pop_front();
+      }
+      busy_ = true;
+      lk.unlock();
+      std::vector<fcs_phmm_region> all;
+      for (const Req* x : take) all.insert(all.end(), x->regs->begin(), x->regs->end());
+      const int rc = fcs_phmm_compute_regions(all.data(), (int32_t)all.size(), &o);
+      const std::string err = rc != FCS_OK ? std::string(fcs_last_error()) : std::string();
+      double dev = 0, res = 0;
+      int64_t nres = 0;
+      if (rc == FCS_OK) {
+        if (fcs_phmm_last_rescued(&nres) != FCS_OK) nres = 0;
+        if (fcs_phmm_last_device_ms(&dev, &res) != FCS_OK) dev = res = 0;
+      }
+      lk.lock();
+      for (Req* x : take) x->rc = rc, x->err = err, x->done = true;
+      r.led = true, r.dev_ms = dev, r.res_ms = res, r.rescued = nres;
+      busy_ = false;
+      cv_.notify_all();
+    }
+  }
+
+ private:
+  std::mutex m_;
+  std::condition_variable cv_;
+  std::deque<Req*> q_;
+  bool busy_ = false;
+  int active_ = 0;
+};
+
+PassCombiner& pass_combiner(int gpu, bool rescue) {
+  static std::mutex m;
+  static std::map<std::pair<int, bool>, std::unique_ptr<PassCombiner>> slots;
+  std::lock_guard<std::mutex> g(m);
+  auto& c = slots[{gpu, rescue}];
+  if (!c) c = std::make_unique<PassCombiner>();
+  return *c;
+}
+
+// A shard thread counts as active on its slot's combiner while it calls.
+struct CombinerScope {
+  PassCombiner* c;
+  explicit CombinerScope(const CallerOptions& opt)
+      : c(opt.combine_ms > 0 ? &pass_combiner(opt.gpu, opt.fp64_rescue) : nullptr) {
+    if (c) c->enter();
+  }
+  ~CombinerScope() {
+    if (c) c->leave();
+  }
+  CombinerScope(const CombinerScope&) = delete;
+  CombinerScope& operator=(const CombinerScope&) = delete;
+};
+
 // One device pass over a batch of regions (both read sets in Mutect2 mode).
 void run_phmm(std::vector<std::unique_ptr<Region>>& batch, const CallerOptions& opt, CallerStats& st, std::FILE* dump) {
   std::vector<std::vector<fcs_phmm_read>> rv;
@@ -432,16 +543,31 @@ void run_phmm(std::vector<std::unique_ptr<Region>>& batch, const CallerOptions& 
   o.device = opt.gpu;
   o.use_fp64_rescue = opt.fp64_rescue ? 1 : 0;
   const uint64_t t0 = now_us();
-  const int rc = fcs_phmm_compute_regions(regs.data(), (int32_t)regs.size(), &o);
-  st.phmm_seconds += (now_us() - t0) / 1e6;
-  ++st.device_passes;
-  if (rc != FCS_OK) throw failedCommand(std::string(fcs_last_error()));
-  int64_t nres = 0;
-  if (fcs_phmm_last_rescued(&nres) == FCS_OK) st.rescued += nres;
-  double dev_ms = 0, res_ms = 0;
-  if (fcs_phmm_last_device_ms(&dev_ms, &res_ms) == FCS_OK) {
-    st.phmm_device_seconds += dev_ms / 1e3;
-    st.rescue_device_seconds += res_ms / 1e3;
+  if (opt.combine_ms > 0) {
+    PassCombiner::Req r;
+    r.regs = &regs;
+    for (const fcs_phmm_region& g : regs) r.pairs += (int64_t)g.n_reads * g.n_haps;
+    pass_combiner(opt.gpu, opt.fp64_rescue).run(r, o, opt.combine_ms, opt.combine_max_pairs);
+    st.phmm_seconds += (now_us() - t0) / 1e6;
+    if (r.rc != FCS_OK) throw failedCommand(r.err);
+    if (r.led) {  // the pass's device time and rescues count once, on the thread that ran it
+      ++st.device_passes;
+      st.rescued += r.rescued;
+      st.phmm_device_seconds += r.dev_ms / 1e3;
+      st.rescue_device_seconds += r.res_ms / 1e3;
+    }
+  } else {
+    const int rc = fcs_phmm_compute_regions(regs.data(), (int32_t)regs.size(), &o);
+    st.phmm_seconds += (now_us() - t0) / 1e6;
+    ++st.device_passes;
+    if (rc != FCS_OK) throw failedCommand(std::string(fcs_last_error()));
+    int64_t nres = 0;
+    if (fcs_phmm_last_rescued(&nres) == FCS_OK) st.rescued += nres;
+    double dev_ms = 0, res_ms = 0;
+    if (fcs_phmm_last_device_ms(&dev_ms, &res_ms) == FCS_OK) {
+      st.phmm_device_seconds += dev_ms / 1e3;
+      st.rescue_device_seconds += res_ms / 1e3;
+    }
   }
   if (dump)
     for (const auto& g : batch)
@@ -709,6 +835,7 @@ CallerStats call_intervals(const Reference& ref, const std::vector<std::string>&
                            const std::vector<std::string>& normal_bams, const std::vector<Interval>& intervals_in,
                            const CallerOptions& opt, VcfWriter& out) {
   CallerStats st;
+  const CombinerScope combiner(opt);
   const uint64_t t0 = now_us();
   const double cpu0 = thread_cpu();
   std::FILE* dump = opt.dump_path.empty() ? nullptr : std::fopen(opt.dump_path.c_str(), "ab");

@@ -39,6 +39,10 @@ struct CallerOptions {
   int max_region = 300;
   int max_reads_per_region = 250;
   int batch_regions = 4096;
+  // concurrent shards' passes merged per device (caller.cpp PassCombiner): the
+  // leader's wait window in ms (0: every flush is its own pass) and pass cap
+  int combine_ms = 20;
+  int64_t combine_max_pairs = 4000000;
   bool fp64_rescue = true;
   double min_qual = 30.0;  // stand_call_conf
   double tlod = 6.3, nlod = 2.2;

@@ -40,11 +40,13 @@ CallerOptions caller_options_from_config(int gpu) {
   o.max_region = c.get_int("htc.max_region");
   o.max_reads_per_region = c.get_int("htc.max_reads_per_region");
   o.batch_regions = c.get_int("gpu.phmm.batch_regions");
+  o.combine_ms = c.get_int("gpu.phmm.combine_ms");
   o.fp64_rescue = c.get_bool("gpu.phmm.rescue");
   o.tlod = std::stod(c.get_string("mutect2.tlod"));
   o.nlod = std::stod(c.get_string("mutect2.nlod"));
-  if (o.padding < 0 || o.max_region < 1 || o.batch_regions < 1 || o.max_reads_per_region < 1)
-    throw invalidParam("htc.padding / htc.max_region / gpu.phmm.batch_regions / htc.max_reads_per_region");
+  if (o.padding < 0 || o.max_region < 1 || o.batch_regions < 1 || o.max_reads_per_region < 1 || o.combine_ms < 0)
+    throw invalidParam(
+        "htc.padding / htc.max_region / gpu.phmm.batch_regions / htc.max_reads_per_region / gpu.phmm.combine_ms");
   return o;
 }
 
