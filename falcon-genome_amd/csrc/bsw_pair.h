@@ -284,7 +284,6 @@ struct PairTask {
   int qlen, tlen, h0, w;
   int beg, end;
   int mx, max_i, max_j, max_ie, gscore, max_off, ncell;
-  int tcur, tnext;
   bool done;
 };
 
@@ -313,8 +312,6 @@ __device__ __forceinline__ void task_load(PairTask& T, const BswDevBatch& b, con
   T.gscore = -1;
   T.max_off = 0;
   T.ncell = 0;
-  T.tcur = (T.tlen > 0) ? T.tg[0] : 0;
-  T.tnext = (T.tlen > 1) ? T.tg[1] : 0;
 }
 
 // ---------------------------------------------------------------- bookkeeping
@@ -424,13 +421,20 @@ __device__ __forceinline__ void pair_wave(const BswDevBatch& b, const BswParams&
   S.MOFF = 0;
   S.DONE = (A.done ? 0xFFFFu : 0u) | (B.done ? 0xFFFF0000u : 0u);
   S.NCA = S.NCB = 0;
-  const uint8_t* __restrict__ tgA = A.tg;
-  const uint8_t* __restrict__ tgB = B.tg;
-  const int tlenA = A.tlen, tlenB = B.tlen;
-  uint32_t TB = (uint32_t)A.tcur | ((uint32_t)A.tnext << 8) | ((uint32_t)B.tcur << 16) | ((uint32_t)B.tnext << 24);
-  // target bytes of row i + 2, loaded during row i - 1: a whole row of cells
-  // hides the load (loaded and used in the same row, it stalled every row: +4%)
-  uint32_t PND = (tlenA > 2 ? (uint32_t)tgA[2] : 0u) | ((tlenB > 2 ? (uint32_t)tgB[2] : 0u) << 8);
+  // Target bytes as the aligned dwords that cover each target, one load per
+  // task every four rows (wave-uniform rows), realigned by v_alignbyte: a byte
+  // load per task and row made every row touch 128 target lines per wave, and
+  // at 8 waves per CU those lines thrash the XCD's L2 (2.84 GB of DRAM reads
+  // per C3 batch for 0.28 GB of input).  The dword for rows
+  // 4k + 4 .. 4k + 7 is requested at row 4k: four rows of cells hide it.
+  const uint32_t* __restrict__ twA = reinterpret_cast<const uint32_t*>((uintptr_t)A.tg & ~(uintptr_t)3);
+  const uint32_t* __restrict__ twB = reinterpret_cast<const uint32_t*>((uintptr_t)B.tg & ~(uintptr_t)3);
+  const uint32_t toA = (uint32_t)((uintptr_t)A.tg & 3), toB = (uint32_t)((uintptr_t)B.tg & 3);
+  // aligned dwords holding some target byte (they lie inside the hipMalloc'd buffer)
+  const int nwA = ((int)toA + A.tlen + 3) >> 2, nwB = ((int)toB + B.tlen + 3) >> 2;
+  uint32_t LA = nwA > 0 ? twA[0] : 0u, LB = nwB > 0 ? twB[0] : 0u;  // low dword of the coming quad
+  uint32_t HA = nwA > 1 ? twA[1] : 0u, HB = nwB > 1 ? twB[1] : 0u;  // its high dword (in flight)
+  uint32_t QA = 0, QB = 0;  // this quad's target bytes, row i in the low byte
   const uint32_t ONE = k.one, ED1 = (uint32_t)p.e_del * 0x10001u, EI1 = (uint32_t)p.e_ins * 0x10001u;
   const uint32_t ZD2 = (uint32_t)min(p.zdrop, 32767) * 0x10001u;
 
@@ -439,13 +443,18 @@ __device__ __forceinline__ void pair_wave(const BswDevBatch& b, const BswParams&
     const uint32_t I2 = (uint32_t)i * 0x10001u;
     const uint32_t ALIVE = ~S.DONE & pk_lt(I2, S.TLEN);
     if (__ballot(ALIVE != 0u) == 0ull) break;
-    const uint32_t tA = TB & 0xFFu, tB = (TB >> 16) & 0xFFu;
-    TB = ((TB >> 8) & 0x00FF00FFu) | ((PND & 0xFFu) << 8) | ((PND >> 8) << 24);
-    {
-      const uint32_t nA = ((ALIVE & 0xFFFFu) && i + 3 < tlenA) ? tgA[i + 3] : 0u;
-      const uint32_t nB = ((ALIVE >> 16) && i + 3 < tlenB) ? tgB[i + 3] : 0u;
-      PND = nA | (nB << 8);
+    if ((i & 3) == 0) {
+      QA = __builtin_amdgcn_alignbyte(HA, LA, toA);
+      QB = __builtin_amdgcn_alignbyte(HB, LB, toB);
+      LA = HA;
+      LB = HB;
+      const int w = (i >> 2) + 2;
+      HA = w < nwA ? twA[w] : 0u;
+      HB = w < nwB ? twB[w] : 0u;
     }
+    const uint32_t tA = QA & 0xFFu, tB = QB & 0xFFu;
+    QA >>= 8;
+    QB >>= 8;
     // bwa's band: beg = max(beg, i - w), end = min(end, i + w + 1, qlen)
     S.BEG = s_max(S.BEG, s_sub(I2, S.W));
     S.END = s_min(S.END, s_min(s_add(s_add(I2, ONE), S.W), S.QLEN));

@@ -84,15 +84,17 @@ struct SRowC {
 // through a 36-byte stack copy, i.e. a scratch store + reload per stripe
 // (0.5-0.8 GB of scratch traffic per C2 pass, profiles/r2/r2d_*).
 __device__ __forceinline__ SRowC srow_params(const PhmmTables<float>& tab, const RawRow& raw, int role, bool first,
-                                             int H) {
+                                             float init_h) {
   const RowP<float> q = row_params<float, false>(tab, raw);
   const bool real = role == 2 || role == 3;  // rows 1..R
   const bool mid = role == 2;                // rows 1..R-1
   const bool last = role == 3;               // row R hands X = M + I, I = 0; D is never needed by anyone
   const bool v = role == 4;                  // V: D = running sum of M; X = M + D
   const bool pad = role == 1;                // pad: X = prior * Xp = Z one column on, I = 0, D = 0
-  // row 1: M(1, c) = prior * x0 (x0 = X(0, c - 1) for c - 1 >= 0); x * 1.f is exact elsewhere
-  const float x0 = first ? (tab.init_const / (float)H) * tab.dmatch[raw.gq & 127] : 1.f;
+  // row 1: M(1, c) = prior * x0 (x0 = X(0, c - 1) for c - 1 >= 0); x * 1.f is exact elsewhere.
+  // init_h = 2^120 / H, divided once per pair at batch start (two divisions per
+  // stripe here were ~54 VALU of the stripe's ~700)
+  const float x0 = first ? init_h * tab.dmatch[raw.gq & 127] : 1.f;
   const float one_vp = (v || pad) ? 1.f : 0.f;
   SRowC c;
   c.e1 = real ? q.e1 * x0 : one_vp;
@@ -127,6 +129,7 @@ __device__ __forceinline__ RowP2 srow_pack(const SRowC a, const SRowC b) {
 // p), unit u of the pair, its rows and their roles.
 struct SLane {
   int k, p, R, H, u;
+  float ih;  // 2^120 / H (GKL's initial D row value), computed once per pair
   int64_t ro;
   int role_a, role_b, ra, rb;  // rb = ra + 1; rows are 1-based, 0 = pad
   bool act;
@@ -277,6 +280,7 @@ __global__ __launch_bounds__(64, LB) void phmm3_kernel(
     const long long idx = bstart + 4LL * sl + seg;
     const int pm = (sl < Kb && idx < bend) ? order[idx] : -1;
     int Rm = 0, Hm = 0, Um = 0;
+    float Im = 0.f;
     int64_t rom = 0, hom = 0;
     if (pm >= 0) {
       const int ri = b.pair_read[pm], hi = b.pair_hap[pm];
@@ -285,6 +289,7 @@ __global__ __launch_bounds__(64, LB) void phmm3_kernel(
       rom = b.read_off[ri];
       hom = b.hap_off[hi];
       Um = (Rm + 2) >> 1;
+      Im = tab.init_const / (float)Hm;
     }
     int ube = Um;  // inclusive prefix sum of units over the segment
     ube += __builtin_amdgcn_update_dpp(0, ube, kDppRowShr1, 0xF, 0xF, false);
@@ -312,6 +317,7 @@ __global__ __launch_bounds__(64, LB) void phmm3_kernel(
       s.p = __shfl(pm, sbase + kk);
       s.R = __shfl(Rm, sbase + kk);
       s.H = __shfl(Hm, sbase + kk);
+      s.ih = __shfl(Im, sbase + kk);
       const int lo = __shfl((int)rom, sbase + kk), hi = __shfl((int)(rom >> 32), sbase + kk);
       s.ro = (int64_t)(((uint64_t)(uint32_t)hi << 32) | (uint32_t)lo);
       s.u = g - __shfl(ubb, sbase + kk);
@@ -329,11 +335,13 @@ __global__ __launch_bounds__(64, LB) void phmm3_kernel(
     // act | k << 1 | hap alignment << 5 | u << 7.
     struct SPack {
       int p, rh, w;
+      float ih;
     };
     auto pack = [&](const SLane& s) {
       SPack q;
       q.p = s.p;
       q.rh = s.R | (s.H << 16);
+      q.ih = s.ih;
       const uint8_t* const ha = b.hb + (int64_t)(uint32_t)__shfl((int)hom, sbase + min(s.k, 15));
       const int al = (int)((uintptr_t)ha & 3);  // only its address: a lane past the stream may point anywhere
       q.w = (s.act ? 1 : 0) | (s.k << 1) | (al << 5) | (s.u << 7);
@@ -344,6 +352,7 @@ __global__ __launch_bounds__(64, LB) void phmm3_kernel(
       s.p = q.p;
       s.R = q.rh & 0xFFFF;
       s.H = q.rh >> 16;
+      s.ih = q.ih;
       s.act = q.w & 1;
       s.k = (q.w >> 1) & 15;
       s.u = q.w >> 7;
@@ -356,7 +365,8 @@ __global__ __launch_bounds__(64, LB) void phmm3_kernel(
       return s;
     };
     auto params_of = [&](const SLane& s, const RawRow& a, const RawRow& bb) {
-      return srow_pack(srow_params(tab, a, s.role_a, s.ra == 1, s.H), srow_params(tab, bb, s.role_b, s.rb == 1, s.H));
+      return srow_pack(srow_params(tab, a, s.role_a, s.ra == 1, s.ih),
+                       srow_params(tab, bb, s.role_b, s.rb == 1, s.ih));
     };
 
     // Haplotype codes of the pair that starts in the coming stripe (at most one
