@@ -532,6 +532,64 @@ def phmm_parity(gpu, ref, used_d, tol=1e-5):
             "against": "oracle/pairhmm_simd.c (GKL-style AVX-512 restatement, bit-identical to the scalar oracle)"}
 
 
+def bench_bsw_align(args, dev, tasks, xtra, reps=3):
+    """ksw_align2 (bwa mem_matesw's local SW with score2 and, by KSW_XSTART, the
+    reversed start pass) on device-resident tasks.  Cells: the first pass's
+    qlen x tlen matrix plus the second pass's (qe + 1) x (te + 1) (it stops at
+    the score, at the latest at column te of the reversed target)."""
+    b, keep = bsw_dev_batch(tasks, dev)
+    n = tasks.n
+    params = fcship.bsw_params()
+    stream = torch.cuda.current_stream(dev)
+    xt = torch.from_numpy(np.ascontiguousarray(np.broadcast_to(np.int32(xtra), (n,)))).to(dev)
+    out = torch.empty((n, 7), dtype=torch.int32, device=dev)
+    B, P = fcship.C.byref(b), fcship.C.byref(params)
+
+    def run():
+        fcship.check(fcship.lib.fcs_bsw_align_dev(B, P, xt.data_ptr(), out.data_ptr(), dev.index,
+                                                  stream.cuda_stream))
+    run()
+    torch.cuda.synchronize(dev)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record(stream)
+    for _ in range(reps):
+        run()
+    e1.record(stream)
+    torch.cuda.synchronize(dev)
+    ms = e0.elapsed_time(e1) / reps
+    res = out.cpu().numpy()
+    first = int((tasks.qlen.astype(np.int64) * tasks.tlen).sum())
+    second = int(((res[:, 2].astype(np.int64) + 1) * (res[:, 1].astype(np.int64) + 1))[res[:, 5] >= 0].sum())
+    del keep
+    return dict(ms=ms, tasks=n, cells_first=first, cells=first + second, res=res,
+                gcups=(first + second) / (ms * 1e-3) / 1e9)
+
+
+def cpu_baseline_bsw_align(tasks, gpu, xtra, budget_s):
+    """The oracle's ksw_align2 (a literal restatement of bwa's striped SSE2
+    ksw_u8 / ksw_i16, scalar) on a leading sample of the timed tasks, one
+    thread; its outputs are compared with the GPU's for the same tasks."""
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import oracle_lib
+    mat = fcship.default_mat()
+    got, t0, n = [], time.perf_counter(), 0
+    while n < tasks.n and (n < 64 or time.perf_counter() - t0 < budget_s):
+        q, t, _, _ = tasks.task(n)
+        got.append(oracle_lib.ksw_align2(q, t, mat, xtra))
+        n += 1
+    dt = time.perf_counter() - t0
+    ref = np.array(got, np.int32).reshape(n, 7)
+    same = (ref == gpu["res"][:n]).all(axis=1)
+    cells = int((tasks.qlen[:n].astype(np.int64) * tasks.tlen[:n]).sum())
+    cells += int(((ref[:, 2].astype(np.int64) + 1) * (ref[:, 1].astype(np.int64) + 1))[ref[:, 5] >= 0].sum())
+    parity = {"n": n, "bit_exact": int(same.sum()), "mismatched": int(n - same.sum()), "pass": bool(same.all()),
+              "fields": "score, te, qe, score2, te2, tb, qb",
+              "against": "oracle/ksw_align_oracle.c (bwa ksw_align2 restatement, striped semantics)"}
+    return dict(value=cells / dt / 1e9, unit="GCUPS", cores=1, kind="port",
+                sample=f"first {n} of the {tasks.n} timed tasks, the oracle's scalar emulation of bwa's striped "
+                       f"SSE2 kernels (bwa itself runs 16 u8 lanes per instruction), one thread, {dt:.2f} s"), parity
+
+
 def bsw_roofline(r3, rf):
     """SW roofline: VALU issue.  achieved = cells/s x the lane-instructions per
     cell measured by rocprofv3 (SQ_INSTS_VALU, profiles/pmc_bsw.json, same
@@ -828,9 +886,25 @@ def main():
                 "achieved": round(ach / 1e12, 3), "frac": round(ach / VALU_LANE_INSTR_PEAK, 4),
                 "valu_instr_per_cell": vpc, "of": "scores-only pass (DP kernels)",
                 "valu_source": "profiles/pmc_bsw.json global (SQ_INSTS_VALU x 64 / band cells)"}
+        # mate rescue: 151 bp reads in 600 bp windows (mem_matesw's window for a
+        # ~350 +- 50 bp insert), bwa's xtra for it (XSUBO | XSTART | min_seed_len * a,
+        # XBYTE as l_ms * a < 250)
+        al = fcship.synth_bsw(args.seed + 3, args.bsw_reads // 4, read_len=151, ref_len=10_000_000, w=100,
+                              mode=1, fixed_q=151, fixed_t=600)
+        xa = 0x40000 | 0x80000 | 0x10000 | 19
+        ga = bench_bsw_align(args, dev, al, xa)
+        line["bsw"]["align"] = {
+            "workload": "ksw_align2 of 151 bp reads in 600 bp windows (bwa mem_matesw shape), xtra = XSUBO | "
+                        "XSTART | XBYTE | 19",
+            "tasks": ga["tasks"], "ms": round(ga["ms"], 3), "gcups": round(ga["gcups"], 3),
+            "cells": ga["cells"], "cells_first_pass": ga["cells_first"],
+            "kernel": "bsw_align_kernel<4> (one wave per task, lane l holds query positions l + 64k; striped-F "
+                      "semantics by segmented max-plus scans; both passes in one launch)"}
         if world == 1 and not args.no_cpu_baseline:
             line["bsw"]["cpu_baseline"], line["bsw"]["parity"] = cpu_baseline_bsw(c3, r3, args.cpu_budget,
                                                                                   cpu_threads())
+            line["bsw"]["align"]["cpu_baseline"], line["bsw"]["align"]["parity"] = cpu_baseline_bsw_align(
+                al, ga, xa, min(args.cpu_budget, 5.0))
 
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         line["cpu_baseline"], ref, used_d = cpu_baseline_phmm(p, args.cpu_budget, cpu_threads())
