@@ -159,7 +159,6 @@ __device__ __forceinline__ uint32_t pack2(int a, int b) { return ((uint32_t)a & 
 // ---------------------------------------------------------------- layout
 constexpr int kPW = 8;  // columns per chunk (skip / fast / masked unit)
 template <int NC> constexpr int PCH = (NC + kPW - 1) / kPW;  // chunks
-template <int NC> constexpr int PNZ = (NC + 15) / 16;        // bitmap words
 
 // Wave-uniform constants of the cell body (x256 domain, both halves).
 struct PairK {
@@ -177,7 +176,6 @@ struct PairRow {
   uint32_t BEGM1, END;       // per half: beg - 1, end
   uint32_t O;                // scores of the current column pair
   uint4 sel[2];              // selector dwords, double-buffered by chunk parity
-  uint32_t nz[PNZ<NC>];
 };
 
 // bwa's inner-loop body for column J of both tasks, the same code for every
@@ -208,9 +206,7 @@ __device__ __forceinline__ void pair_cell(uint32_t (&eh)[NC], PairRow<NC>& r, co
   // in place (tied operand), so no chunk path moves eh[] between registers;
   // edge chunks copy the entries they must restore in their pre-pass
   asm("v_perm_b32 %0, %1, %2, %3" : "+v"(eh[J]) : "v"(r.H1), "v"(EN), "s"(0x07030501u));
-  const uint32_t wst = eh[J];
   r.KEY = pk_max(r.KEY, H | JJ);
-  r.nz[J / 16] |= pk_nz(wst, k.one) << (J % 16);
   r.H1 = H;
   r.F = Fn;
 }
@@ -255,15 +251,6 @@ __device__ __forceinline__ void pair_chunk(uint32_t (&eh)[NC], const uint4* __re
   }(std::make_integer_sequence<int, L>{});
   if (edge) {
     const uint32_t endv = launder(r.END);
-    // bitmap bits of this chunk beyond end (restored stale entries) cleared
-    {
-      constexpr int o = j0 % 16;
-      const int endA = (int)(endv & 0xFFFFu), endB = (int)(endv >> 16);
-      const uint32_t ka = __builtin_amdgcn_ubfe(~0u, 0, (uint32_t)min(max(endA + 1 - j0, 0), L));
-      const uint32_t kb = __builtin_amdgcn_ubfe(~0u, 0, (uint32_t)min(max(endB + 1 - j0, 0), L));
-      constexpr uint32_t cm = ((1u << L) - 1u) * 0x10001u << o;
-      r.nz[j0 / 16] &= ~cm | (ka << o) | (kb << (16 + o));
-    }
     uint32_t mx = pk_lt((uint32_t)(j0 - 1) * 0x10001u, endv);  // column j0 <= end
     [&]<int... S>(std::integer_sequence<int, S...>) __attribute__((always_inline)) {
       (([&] __attribute__((always_inline)) {
@@ -275,6 +262,29 @@ __device__ __forceinline__ void pair_chunk(uint32_t (&eh)[NC], const uint4* __re
        ...);
     }(std::make_integer_sequence<int, L>{});
   }
+}
+
+// Non-zero map of chunk C's stored entries: bit S of each half set when column
+// j0 + S of that task has h or e != 0; columns beyond the task's end (stale
+// entries bwa leaves in place) masked out.
+template <int C, int NC>
+__device__ __forceinline__ uint32_t chunk_nz(const uint32_t (&eh)[NC], uint32_t one, int endA, int endB) {
+  constexpr int j0 = kPW * C, L = (NC - j0) < kPW ? (NC - j0) : kPW;
+  uint32_t b = 0;
+  [&]<int... S>(std::integer_sequence<int, S...>) __attribute__((always_inline)) {
+    ((b |= pk_nz(eh[j0 + S], one) << S), ...);
+  }(std::make_integer_sequence<int, L>{});
+  const uint32_t ka = __builtin_amdgcn_ubfe(~0u, 0, (uint32_t)min(max(endA + 1 - j0, 0), L));
+  const uint32_t kb = __builtin_amdgcn_ubfe(~0u, 0, (uint32_t)min(max(endB + 1 - j0, 0), L));
+  return b & (ka | (kb << 16));
+}
+// ~(last set column) of chunk c's map w (one task's half), ~0u when w == 0:
+// a v_min_u32 chain over chunks then keeps the highest column.
+__device__ __forceinline__ uint32_t last_col(uint32_t w, int c) {
+  uint32_t h;
+  asm("v_ffbh_u32 %0, %1" : "=v"(h) : "v"(w));
+  const uint32_t none = (uint32_t)((int)h >> 31);
+  return bsel(none, ~0u, ~((uint32_t)(kPW * c + 31) - h));
 }
 
 // bwa's per-task scalar state.
@@ -489,8 +499,6 @@ __device__ __forceinline__ void pair_wave(const BswDevBatch& b, const BswParams&
     r.CAP = 0;
     r.BEGM1 = s_sub(S.BEG, ONE);
     r.END = S.END;
-#pragma unroll
-    for (int q = 0; q < PNZ<NC>; ++q) r.nz[q] = 0;
     if (cmax >= 0) r.sel[0] = r.sel[1] = qs[64 * (min(max(cmin, 0), NC - 1) / kPW)];
     // chunk classes of this row as wave-uniform bit masks (bit C = chunk C):
     // processed = overlaps [cmin, cmax]; edge = reaches some end (>= emin) or
@@ -542,28 +550,46 @@ __device__ __forceinline__ void pair_wave(const BswDevBatch& b, const BswParams&
     S.DONE |= EMPTY | ZERO | DROP;
     const uint32_t TRIM = WORK & ~S.DONE;
     if (__ballot(TRIM != 0u)) {
-      // bwa's trims: beg = first non-zero entry, end = last non-zero entry + 2.
-      // The bitmap holds no bit left of beg (those entries are zero) and none
-      // beyond end (edge chunks clear them), so these are the lowest and highest
-      // set bits: v_ffbl over 32-column words, the highest via bit reverse.
-      constexpr int NM = (PNZ<NC> + 1) / 2;
-      uint32_t fa = ~0u, la = ~0u, fb = ~0u, lb = ~0u;
-#pragma unroll
-      for (int m = 0; m < NM; ++m) {
-        if (32 * m + 31 < cmin || 32 * m > cmax) continue;  // wave-uniform: outside every band
-        const uint32_t lo = r.nz[2 * m], hi = (2 * m + 1 < PNZ<NC>) ? r.nz[2 * m + 1] : 0u;
-        const uint32_t wa = __builtin_amdgcn_perm(hi, lo, 0x05040100u), wb = __builtin_amdgcn_perm(hi, lo, 0x07060302u);
-        fa = min(fa, ffbl_or(wa, (uint32_t)(m << 5)));
-        la = min(la, ffbh_or(wa, (uint32_t)((NM - 1 - m) << 5)));
-        fb = min(fb, ffbl_or(wb, (uint32_t)(m << 5)));
-        lb = min(lb, ffbh_or(wb, (uint32_t)((NM - 1 - m) << 5)));
-      }
-      // f and l are ~0u together (no bit set: bwa's beg = end, end = end + 1);
-      // the sign bit of f is that mask (a found position is < 32 * NM)
+      // bwa's trims: beg = first entry in [beg, end] with h or e != 0, end = the
+      // last one + 2.  Entries left of beg are zero (kept so), so the first one
+      // is found by scanning chunks of the stored entries upward from the band's
+      // first chunk until every trimming task has one, and the last one downward
+      // from the band's last chunk: one chunk each in most rows (the live band
+      // moves about a column per row), where a per-cell bitmap cost two VALU in
+      // every cell of the row.
+      const int cf = max(cmin, 0) / kPW, cl = min(cmax, NC - 1) / kPW;
+      const bool ta = (TRIM & 0xFFFFu) != 0u, tb = (TRIM >> 16) != 0u;
+      uint32_t fa = ~0u, fb = ~0u;  // first non-zero column, ~0u: none
+      uint32_t la = ~0u, lb = ~0u;  // last non-zero column, ~0u: none
+      bool go = true;
+      [&]<int... C>(std::integer_sequence<int, C...>) __attribute__((always_inline)) {
+        (([&] __attribute__((always_inline)) {
+           if (!go || C < cf || C > cl) return;
+           const uint32_t bits = chunk_nz<C, NC>(eh, ONE, endA, endB);
+           fa = min(fa, ffbl_or(bits & 0xFFFFu, (uint32_t)(kPW * C)));
+           fb = min(fb, ffbl_or(bits >> 16, (uint32_t)(kPW * C)));
+           go = __ballot((ta && fa == ~0u) || (tb && fb == ~0u)) != 0ull;
+         }()),
+         ...);
+      }(std::make_integer_sequence<int, PCH<NC>>{});
+      go = true;
+      [&]<int... C>(std::integer_sequence<int, C...>) __attribute__((always_inline)) {
+        (([&] __attribute__((always_inline)) {
+           constexpr int D = PCH<NC> - 1 - C;  // descending
+           if (!go || D < cf || D > cl) return;
+           const uint32_t bits = chunk_nz<D, NC>(eh, ONE, endA, endB);
+           la = min(la, last_col(bits & 0xFFFFu, D));
+           lb = min(lb, last_col(bits >> 16, D));
+           go = __ballot((ta && la == ~0u) || (tb && lb == ~0u)) != 0ull;
+         }()),
+         ...);
+      }(std::make_integer_sequence<int, PCH<NC>>{});
+      // f is ~0u (sign bit set) when the task has no non-zero entry: bwa's
+      // beg = end, end = end + 1; l is then ~0u too
       auto trim = [&](uint32_t f, uint32_t l, int endv, int qlen, int& nb, int& ne) __attribute__((always_inline)) {
         const uint32_t none = (uint32_t)((int)f >> 31);
         nb = (int)bsel(none, (uint32_t)endv, f);
-        const int last = bsel(none, (uint32_t)(endv - 1), (uint32_t)(32 * (NM - 1) + 31) - ((l >> 5) << 5) - (l & 31u));
+        const int last = (int)bsel(none, (uint32_t)(endv - 1), ~l);
         ne = min(last + 2, qlen);
       };
       int nba, nea, nbb, neb;
