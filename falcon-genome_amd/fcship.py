@@ -112,7 +112,11 @@ class BswBatch(C.Structure):
 
 
 def _sig(name, res, args):
-    f = getattr(lib, name)
+    f = getattr(lib, name, None)
+    if f is None:
+        if os.environ.get("FCSHIP_LIB"):  # an older A/B variant (tools/ab.sh) may predate an entry point
+            return None
+        raise AttributeError(f"libfcship.so lacks {name}")
     f.restype = res
     f.argtypes = args
     return f

@@ -23,7 +23,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--reads", type=int, default=500_000)
     ap.add_argument("--seed", type=int, default=20261015)
-    ap.add_argument("--which", default="both", choices=["c3", "fixed", "both", "global"])
+    ap.add_argument("--which", default="both", choices=["c3", "fixed", "both", "global", "align"])
     ap.add_argument("--reps", type=int, default=3)
     args = ap.parse_args()
     dev = torch.device("cuda", 0)
@@ -32,16 +32,21 @@ def main():
     if args.which in ("c3", "both"):
         t = fcship.synth_bsw(args.seed, args.reads, read_len=151, ref_len=10_000_000, w=100)
         r = bench.bench_bsw(args, dev, t, reps=args.reps)
-        out["c3"] = {k: (round(v, 3) if isinstance(v, float) else v) for k, v in r.items()}
+        out["c3"] = {k: (round(v, 3) if isinstance(v, float) else v) for k, v in r.items() if not hasattr(v, "shape")}
     if args.which in ("fixed", "both"):
         t = fcship.synth_bsw(args.seed, 2 * args.reads, read_len=151, ref_len=10_000_000, w=100, mode=1,
                              fixed_q=151, fixed_t=251)
         r = bench.bench_bsw(args, dev, t, reps=args.reps)
-        out["fixed"] = {k: (round(v, 3) if isinstance(v, float) else v) for k, v in r.items()}
+        out["fixed"] = {k: (round(v, 3) if isinstance(v, float) else v) for k, v in r.items() if not hasattr(v, "shape")}
     if args.which == "global":  # bench.py's ksw_global2 workload, scores + CIGARs (reps + 1 runs each)
         t = fcship.synth_bsw(args.seed + 2, args.reads // 2, read_len=151, ref_len=10_000_000, w=16, mode=1,
                              fixed_q=151, fixed_t=151)
         out["global"] = bench.bench_bsw_global(args, dev, t, reps=args.reps)
+    if args.which == "align":  # bench.py's ksw_align2 (mate rescue) workload
+        t = fcship.synth_bsw(args.seed + 3, args.reads // 4, read_len=151, ref_len=10_000_000, w=100, mode=1,
+                             fixed_q=151, fixed_t=600)
+        r = bench.bench_bsw_align(args, dev, t, 0x40000 | 0x80000 | 0x10000 | 19, reps=args.reps)
+        out["align"] = {k: (round(v, 3) if isinstance(v, float) else v) for k, v in r.items() if not hasattr(v, "shape")}
     print(json.dumps(out))
 
 
