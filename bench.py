@@ -259,12 +259,15 @@ def cpu_mock_env(env):
     """Environment of an fcs-genome child that runs the reference's CPU
     PairHMM path: tests/cpu_mock/build/libfcship.so (test infrastructure: the
     oracle's Java-semantics or GKL-style AVX-512 PairHMM behind the same
-    C-ABI) first on its LD_LIBRARY_PATH.  Only that child sees it."""
+    C-ABI) first on its LD_LIBRARY_PATH.  Only that child sees it.  Shard
+    passes are not merged (gpu.phmm.combine_ms = 0): on the CPU path each
+    shard thread computes its own PairHMM batches, as GATK's per-shard
+    HaplotypeCaller processes do; a merged pass would run on one thread."""
     import subprocess
     mock = os.path.join(ROOT, "tests", "cpu_mock", "build")
     if not os.path.exists(os.path.join(mock, "libfcship.so")):
         subprocess.run(["make", "-C", os.path.join(ROOT, "tests", "cpu_mock")], check=True, capture_output=True)
-    return dict(env, LD_LIBRARY_PATH=mock + os.pathsep + env.get("LD_LIBRARY_PATH", ""))
+    return dict(env, LD_LIBRARY_PATH=mock + os.pathsep + env.get("LD_LIBRARY_PATH", ""), FCS_GPU_PHMM_COMBINE_MS="0")
 
 
 def vcf_calls(path):
