@@ -962,12 +962,46 @@ int fcs_phmm_compute(const fcs_phmm_read* reads, int32_t n_reads, const fcs_phmm
 // are concatenated (straight into the pinned staging) into one SoA batch whose
 // pair list is region-major and read-major within a region, so the flat
 // result splits back into each region's read-major matrix by a running offset.
+}  // extern "C"
+
+namespace {
+// Runs f(k0, k1) over contiguous region ranges: on the calling thread for a
+// small batch, on up to 8 threads for a large one (a pass merged from many
+// shards' batches, host/caller.cpp, stages ~100 MB through per-read memcpys;
+// on one thread that serialised the shards waiting for it).
+template <class F>
+void for_region_ranges(int32_t n, int64_t bytes, F&& f) {
+  const unsigned hw = std::max(1u, std::thread::hardware_concurrency());
+  const int nt = (int)std::min<int64_t>({8, (int64_t)hw, n, bytes / (4 << 20)});
+  if (nt <= 1) {
+    f(0, n);
+    return;
+  }
+  std::vector<std::thread> th;
+  th.reserve(nt - 1);
+  const int32_t chunk = (n + nt - 1) / nt;
+  for (int t = 1; t < nt; ++t) {
+    const int32_t a = t * chunk, b = std::min(n, a + chunk);
+    if (a < b) th.emplace_back([&f, a, b] { f(a, b); });
+  }
+  f(0, std::min(n, chunk));
+  for (auto& x : th) x.join();
+}
+}  // namespace
+
+extern "C" {
+
 int fcs_phmm_compute_regions(const fcs_phmm_region* regions, int32_t n_regions, const fcs_phmm_opts* opts_in) {
   if (n_regions < 0 || (n_regions > 0 && !regions))
     return fail(FCS_ERR_INVALID, "[E::fcs_phmm_compute_regions] bad arguments");
   PhmmStage g;
+  // per-region starts in the packed batch (reads, haplotypes, pairs, read and
+  // hap bytes): regions are staged independently, in parallel when large
+  std::vector<int64_t> r_at(n_regions + 1), h_at(n_regions + 1), p_at(n_regions + 1), rb_at(n_regions + 1),
+      hb_at(n_regions + 1);
   for (int32_t k = 0; k < n_regions; ++k) {
     const fcs_phmm_region& R = regions[k];
+    r_at[k] = g.n_reads, h_at[k] = g.n_haps, p_at[k] = g.n_pairs, rb_at[k] = g.read_bytes, hb_at[k] = g.hap_bytes;
     if (R.n_reads < 0 || R.n_haps < 0 || (R.n_reads > 0 && !R.reads) || (R.n_haps > 0 && !R.haps))
       return fail(FCS_ERR_INVALID, "[E::fcs_phmm_compute_regions] malformed region");
     const int64_t pairs = (int64_t)R.n_reads * R.n_haps;
@@ -1003,43 +1037,45 @@ int fcs_phmm_compute_regions(const fcs_phmm_region* regions, int32_t n_regions, 
     int64_t *roff = S->h<int64_t>(off[kRo]), *hoff = S->h<int64_t>(off[kHo]);
     int32_t *rlen = S->h<int32_t>(off[kRl]), *hlen = S->h<int32_t>(off[kHl]), *pr = S->h<int32_t>(off[kPr]),
             *ph = S->h<int32_t>(off[kPh]);
-    int64_t ri = 0, hi = 0, pi = 0, ro = 0, ho = 0;
-    for (int32_t k = 0; k < n_regions; ++k) {
-      const fcs_phmm_region& R = regions[k];
-      const int64_t r0 = ri, h0 = hi;
-      for (int32_t r = 0; r < R.n_reads; ++r, ++ri) {
-        const fcs_phmm_read& x = R.reads[r];
-        roff[ri] = ro;
-        rlen[ri] = x.len;
-        if (x.len) {
-          std::memcpy(rb + ro, x.bases, x.len);
-          std::memcpy(bq + ro, x.base_q, x.len);
-          std::memcpy(iq + ro, x.ins_q, x.len);
-          std::memcpy(dq + ro, x.del_q, x.len);
-          std::memcpy(gq + ro, x.gcp, x.len);
+    for_region_ranges(n_regions, g.read_bytes + 8 * g.n_pairs, [&](int32_t k0, int32_t k1) {
+      for (int32_t k = k0; k < k1; ++k) {
+        const fcs_phmm_region& R = regions[k];
+        int64_t ri = r_at[k], hi = h_at[k], pi = p_at[k], ro = rb_at[k], ho = hb_at[k];
+        const int64_t r0 = ri, h0 = hi;
+        for (int32_t r = 0; r < R.n_reads; ++r, ++ri) {
+          const fcs_phmm_read& x = R.reads[r];
+          roff[ri] = ro;
+          rlen[ri] = x.len;
+          if (x.len) {
+            std::memcpy(rb + ro, x.bases, x.len);
+            std::memcpy(bq + ro, x.base_q, x.len);
+            std::memcpy(iq + ro, x.ins_q, x.len);
+            std::memcpy(dq + ro, x.del_q, x.len);
+            std::memcpy(gq + ro, x.gcp, x.len);
+          }
+          ro += x.len;
         }
-        ro += x.len;
-      }
-      for (int32_t h = 0; h < R.n_haps; ++h, ++hi) {
-        hoff[hi] = ho;
-        hlen[hi] = R.haps[h].len;
-        if (R.haps[h].len) std::memcpy(hb + ho, R.haps[h].bases, R.haps[h].len);
-        ho += R.haps[h].len;
-      }
-      for (int32_t r = 0; r < R.n_reads; ++r)
-        for (int32_t h = 0; h < R.n_haps; ++h, ++pi) {
-          pr[pi] = (int32_t)(r0 + r);
-          ph[pi] = (int32_t)(h0 + h);
+        for (int32_t h = 0; h < R.n_haps; ++h, ++hi) {
+          hoff[hi] = ho;
+          hlen[hi] = R.haps[h].len;
+          if (R.haps[h].len) std::memcpy(hb + ho, R.haps[h].bases, R.haps[h].len);
+          ho += R.haps[h].len;
         }
-    }
+        for (int32_t r = 0; r < R.n_reads; ++r)
+          for (int32_t h = 0; h < R.n_haps; ++h, ++pi) {
+            pr[pi] = (int32_t)(r0 + r);
+            ph[pi] = (int32_t)(h0 + h);
+          }
+      }
+    });
   }, &res);
   if (rc) return rc;
-  int64_t o = 0;
-  for (int32_t k = 0; k < n_regions; ++k) {
-    const int64_t pairs = (int64_t)regions[k].n_reads * regions[k].n_haps;
-    if (pairs) std::memcpy(regions[k].out_log10, res + o, 8 * (size_t)pairs);
-    o += pairs;
-  }
+  for_region_ranges(n_regions, 8 * g.n_pairs, [&](int32_t k0, int32_t k1) {
+    for (int32_t k = k0; k < k1; ++k) {
+      const int64_t pairs = (int64_t)regions[k].n_reads * regions[k].n_haps;
+      if (pairs) std::memcpy(regions[k].out_log10, res + p_at[k], 8 * (size_t)pairs);
+    }
+  });
   return FCS_OK;
 }
 
