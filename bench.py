@@ -413,6 +413,22 @@ def bench_e2e(args, rank, local):
         hs = stage_s(err, "Haplotype Caller")
         out["htc"]["caller_stage_seconds"] = hs  # the 32-shard stage alone: no process start, GPU init, concat
         out["htc"]["caller_stage_regions_per_s"] = round(out["htc"]["regions"] / hs, 1) if hs else None
+        # the same command with concurrent shards' PairHMM passes merged per
+        # device (gpu.phmm.combine_ms, off by default): fewer, larger device
+        # passes, reported for their device-effective rate and wall time
+        env_m = dict(env, FCS_GPU_PHMM_COMBINE_MS="20")
+        shutil.rmtree(env["FCS_LOG_DIR"], ignore_errors=True)
+        t0 = time.perf_counter()
+        r = subprocess.run([exe, "htc", "-f", "-r", d + "/ref.fasta", "-i", d + "/sample.bam", "-o",
+                            work + "/htc_m.g.vcf"], env=env_m, capture_output=True, text=True, cwd=work)
+        dtm = time.perf_counter() - t0
+        if r.returncode == 0:
+            logs_m = "".join(open(os.path.join(env["FCS_LOG_DIR"], f)).read() for f in os.listdir(env["FCS_LOG_DIR"])
+                             if ".part-" not in f)
+            sm = shard_stats(logs_m, dtm)
+            out["htc"]["merged_passes"] = {k: sm[k] for k in ("seconds", "device_passes", "phmm_device_seconds",
+                                                                 "phmm_device_tcups")}
+            out["htc"]["merged_passes"]["setting"] = "gpu.phmm.combine_ms = 20"
         if cpu_htc:  # the reference's CPU path beside it, on the same genome (rank 0, N=1 only)
             out["htc"]["cpu_baseline"] = htc_cpu_baseline(exe, env, work, d + "/ref.fasta", d + "/sample.bam",
                                                           work + "/htc.g.vcf")

@@ -46,7 +46,7 @@ void Config::init(const std::string& root_dir) {
   // accelerator (replaces bwa.use_fpga / bwa.fpga.bit_path / blaze.nam_path)
   declare("gpu.devices", "all", "GPU ordinals for shard tasks: all | comma list");
   declare("gpu.phmm.batch_regions", "4096", "active regions per PairHMM device pass");
-  declare("gpu.phmm.combine_ms", "20", "ms a shard's PairHMM pass waits to merge with other shards' (0: no merging)");
+  declare("gpu.phmm.combine_ms", "0", "ms a shard's PairHMM pass waits to merge with other shards' (0: no merging)");
   declare("gpu.phmm.rescue", "true", "fp64 rescue of pairs whose fp32 likelihood underflows (GKL)");
   // caller knobs (GATK HaplotypeCaller / Mutect2 argument defaults)
   declare("htc.min_base_quality", "10", "min base quality counted as evidence of activity");
