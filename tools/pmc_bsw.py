@@ -49,7 +49,7 @@ def main():
     fe = totals(os.path.join(src, "bswpmc_c3_fetch")).get("FETCH_SIZE")
     wr = totals(os.path.join(src, "bswpmc_c3_write")).get("WRITE_SIZE")
     if fe is not None and wr is not None:
-        out["c3"]["hbm_bytes_per_batch"] = int(round((fe + wr) * 1024))
+        out["c3"]["hbm_bytes_per_batch"] = int(round((2 * fe + wr) * 1024))  # 2 x FETCH_SIZE: gfx950 calibration
         out["c3"]["fetch_kib"], out["c3"]["write_kib"] = fe, wr
     gdir = os.path.join(src, "bswpmc_global")
     if os.path.isdir(gdir):  # ksw_global2: scores-only and scores + CIGAR runs, 2 each (warm-up + timed)
@@ -71,8 +71,9 @@ def main():
     out["_note"] = ("rocprofv3 --pmc of tools/bsw_bench.py --which <w> --reps 1 (separate passes: SQ issue/stall "
                     "counters, FETCH_SIZE, WRITE_SIZE), every bsw_* kernel of one ksw_extend2 batch (keys, bounds, "
                     "extension launch), halved for the warm-up batch; VALU per cell = SQ_INSTS_VALU x 64 / evaluated "
-                    "cells; SQ_*_CYCLES / WAIT / ACTIVE in quad-cycles; FETCH_SIZE uncorrected (1-4 B per-lane loads, "
-                    "the gfx950 1/2 calibration of MI355X_MICROARCH.md is for 16 B/lane streams)")
+                    "cells; SQ_*_CYCLES / WAIT / ACTIVE in quad-cycles; fetch_kib / write_kib as rocprofv3 reports them, "
+                    "hbm_bytes_per_batch = 2 x FETCH_SIZE + WRITE_SIZE (the gfx950 FETCH_SIZE calibration, "
+                    "profiles/fetch_calibration.json)")
     out["source"] = tag
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     json.dump(out, open(os.path.join(root, "profiles", "pmc_bsw.json"), "w"), indent=1)

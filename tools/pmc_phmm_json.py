@@ -48,10 +48,16 @@ if "FETCH_SIZE" in q and "WRITE_SIZE" in q:
     t["_note"] = ("HBM bytes per fp32 forward pass (all hap-length class launches) on the default C2 workload = "
                   "(FETCH_SIZE + WRITE_SIZE) KiB * 1024 from separate rocprofv3 --pmc passes "
                   f"(gpurun_out/{tag}, summary in profiles/r4/{tag}_pmc_phmm.txt), divided by the passes profiled.  "
-                  "FETCH_SIZE is uncorrected: the gfx950 1/2 correction in MI355X_MICROARCH.md applies to 16-B/lane "
-                  "streaming loads; this kernel's reads are 1- and 4-byte per-lane loads (see fetch_calibration).")
+                  "FETCH_SIZE as reported: bench.py prices HBM reads as 2 x FETCH_SIZE (the gfx950 calibration of "
+                  "profiles/fetch_calibration.json, measured for 1, 4 and 16 B per-lane loads).")
     json.dump(t, open(tp, "w"), indent=1)
 os.makedirs(dst, exist_ok=True)
 if os.path.exists(os.path.join(src, "summary.txt")):
     shutil.copy(os.path.join(src, "summary.txt"), os.path.join(dst, f"{tag}_pmc_phmm.txt"))
+else:  # the per-pass counters themselves
+    with open(os.path.join(dst, f"{tag}_pmc_phmm.txt"), "w") as f:
+        f.write(f"fp32 forward kernels {', '.join(FWD)}: counters per C2 pass ({passes:g} passes profiled)\n")
+        for k, v in q.items():
+            f.write(f"{k:28s} {v:18.1f}\n")
+        f.write(json.dumps(d) + "\n")
 print(json.dumps(d))
