@@ -11,8 +11,11 @@
 //     consecutive positions), so E(i + 1, x) opens from that first-pass H1;
 //   * the lazy-F loop then carries F across the blocks; it only raises H
 //     (never E), and bwa's column maximum is taken from H1.
-// Here one 64-lane wave runs one task; lane l owns positions x = l + 64 k
-// (k < NK slots), padded to slen * p as bwa's profile is (padding scores 0).
+// Here a group of W lanes (a 16-lane DPP row, four tasks per wave, for
+// qlen <= 160; the whole 64-lane wave for longer queries) runs one task; lane
+// l of the group owns the NK consecutive positions x = l NK + k, padded to
+// slen * p as bwa's profile is (padding scores 0), so the max-plus scans are a
+// running max along the lane's registers plus one group scan of lane totals.
 // Per target base (one column):
 //   M  = sat(Hprev(x - 1) + s)            (u8: biased, saturating; i16: saturating)
 //   M' = max(M, E)
@@ -23,7 +26,9 @@
 // M'; a block-id term in the scan value keeps the first one inside its block).
 // Column maxima, bwa's b[] list (LDS), te / qe / score2 / te2, and the
 // KSW_XSTART second pass over the reversed query and target prefixes run in
-// the same wave, all control flow wave-uniform.
+// the same group.  With W = 16 the four tasks of a wave run their columns in
+// lock-step (the wave loops to its longest target; a group past its own end or
+// early exit computes masked columns).
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -35,157 +40,244 @@ namespace fcs {
 
 constexpr int kKswXByte = 0x10000, kKswXStop = 0x20000, kKswXSubo = 0x40000, kKswXStart = 0x80000;
 constexpr int kBlockBig = 1 << 20;  // > the range of one block's scan values; block ids < 16
+constexpr int kAlignSegQ = 160;      // longest query of the 16-lane groups (NK = 10 slots)
+
+// Group-level primitives: W = 16 (a DPP row) or 64 (the wave).
+template <int W>
+__device__ __forceinline__ int grp_lane() {
+  return W == 64 ? lane_id() : (lane_id() & 15);
+}
+// Inclusive max scan inside the group (lanes without a source see `neg`).
+template <int W>
+__device__ __forceinline__ int grp_incl_max(int v, int neg) {
+  if constexpr (W == 64) {
+    return wave_incl_max(v, neg);
+  } else {
+    v = max(v, __builtin_amdgcn_update_dpp(neg, v, kDppRowShr1, 0xF, 0xF, false));
+    v = max(v, __builtin_amdgcn_update_dpp(neg, v, kDppRowShr2, 0xF, 0xF, false));
+    v = max(v, __builtin_amdgcn_update_dpp(neg, v, kDppRowShr4, 0xF, 0xF, false));
+    v = max(v, __builtin_amdgcn_update_dpp(neg, v, kDppRowShr8, 0xF, 0xF, false));
+    return v;
+  }
+}
+// The group's last lane's value, in every lane of the group.
+template <int W>
+__device__ __forceinline__ int grp_last(int v) {
+  if constexpr (W == 64) {
+    return read_lane(v, 63);
+  } else {
+    // ds_swizzle bit mode inside 32-lane halves: lane -> (lane & 0x10) | 0x0F
+    return __builtin_amdgcn_ds_swizzle(v, 0x10 | (0x0F << 5));
+  }
+}
+template <int W>
+__device__ __forceinline__ int grp_max(int v) {
+  return grp_last<W>(grp_incl_max<W>(v, INT32_MIN));
+}
+// Lane l <- lane l - 1 of the group's value; the group's lane 0 <- `first`.
+template <int W>
+__device__ __forceinline__ int grp_shr1(int first, int v) {
+  if constexpr (W == 64) return dpp_wave_shr1_i(first, v);
+  else return __builtin_amdgcn_update_dpp(first, v, kDppRowShr1, 0xF, 0xF, false);
+}
+// Exclusive prefix max over the group's positions x = lane * NS + k (each
+// lane holds NS consecutive positions), seeded with kScanNeg: a running max
+// along the lane's own slots, and one group scan of the lanes' totals.
+template <int W, int NS>
+__device__ __forceinline__ void grp_excl_scan(const int (&u)[NS], int (&ex)[NS]) {
+  int run[NS];
+  run[0] = u[0];
+#pragma unroll
+  for (int k = 1; k < NS; ++k) run[k] = max(run[k - 1], u[k]);
+  const int cin = grp_shr1<W>(kScanNeg, grp_incl_max<W>(run[NS - 1], kScanNeg));  // lanes below
+  ex[0] = cin;
+#pragma unroll
+  for (int k = 1; k < NS; ++k) ex[k] = max(cin, run[k - 1]);
+}
 
 struct AlignRun {
   int score, te, qe, score2, te2;
 };
 
-// One ksw_u8 / ksw_i16 run of query q[x] (x < qlen, read through qidx) against
-// target t[j] (j < tlen, LDS, read through tidx).  minsc / endsc as bwa's.
-template <int NK, class QAt, class TAt>
-__device__ AlignRun align_run(const BswParams& p, int qlen, QAt q_at, int tlen, TAt t_at, bool u8, int shift,
-                              int max_mat, int minsc, int endsc, uint64_t* __restrict__ blist) {
-  const int lane = lane_id();
+// One ksw_u8 / ksw_i16 run of query q[x] (x < qlen, read through q_at) against
+// target t[j] (j < tlen, LDS, read through t_at) in this lane's group.  minsc /
+// endsc as bwa's.  live: the group runs this task (group-uniform).  Every lane
+// of the wave calls it (the column loop is wave-uniform); blist is the
+// group's b[] area.
+template <int W, int NK, class QAt, class TAt>
+__device__ AlignRun align_run(const BswParams& p, bool live, int qlen, QAt q_at, int tlen, TAt t_at, bool u8,
+                              int shift, int max_mat, int minsc, int endsc, uint64_t* __restrict__ blist) {
+  const int gl = grp_lane<W>();
   const int pl = u8 ? 16 : 8;
   const int slen = (qlen + pl - 1) / pl;
-  const int nlen = slen * pl;
+  const int nlen = live ? slen * pl : 0;
   const int oe_del = p.o_del + p.e_del, oe_ins = p.o_ins + p.e_ins, e_del = p.e_del, e_ins = p.e_ins;
-  int Hp[NK], E[NK], Hm[NK], plo[NK], phi[NK], blk[NK];
+  // Per slot: the biased profile bytes (mat[a][q] + shift, a = 0..3 in plo;
+  // a = 4 (N) in byte k % 4 of phi[k / 4]: v_perm picks the score by the
+  // target code), and the scan
+  // offsets c1 = x e_ins - oe_ins + block * kBlockBig, c2 = x e_ins - oe_ins
+  // (u = M' + c turns both max-plus scans into plain max scans).
+  constexpr int NP = (NK + 3) / 4;
+  int Hp[NK], E[NK], plo[NK], phi[NP], c1[NK], c2[NK];
+#pragma unroll
+  for (int k = 0; k < NP; ++k) phi[k] = 0;
 #pragma unroll
   for (int k = 0; k < NK; ++k) {
-    const int x = lane + 64 * k;
-    const int qb = x < qlen ? q_at(x) : -1;  // padding: score 0 against every base
-    auto sc = [&](int a) { return qb < 0 ? 0 : (int)p.mat[a * 5 + qb]; };
-    plo[k] = (sc(0) & 0xFF) | ((sc(1) & 0xFF) << 8) | ((sc(2) & 0xFF) << 16) | ((sc(3) & 0xFF) << 24);
-    phi[k] = sc(4);
-    blk[k] = slen > 0 ? x / slen : 0;
-    Hp[k] = E[k] = Hm[k] = 0;
+    const int x = gl * NK + k;
+    const int qb = (live && x < qlen) ? q_at(x) : -1;  // padding: score 0 against every base
+    auto sc = [&](int a) { return ((qb < 0 ? 0 : (int)p.mat[a * 5 + qb]) + shift) & 0xFF; };
+    plo[k] = sc(0) | (sc(1) << 8) | (sc(2) << 16) | (sc(3) << 24);
+    phi[k / 4] |= sc(4) << (8 * (k % 4));
+    c2[k] = x * e_ins - oe_ins;
+    c1[k] = c2[k] + (slen > 0 ? x / slen : 0) * kBlockBig;
+    Hp[k] = E[k] = 0;
   }
-  int gmax = 0, te = -1, n_b = 0, last_i = -2, last_v = 0;  // b[]'s last entry (column, score): wave-uniform
-  for (int i = 0; i < tlen; ++i) {
-    const int tb = first_lane(t_at(i));
+  // M = sat(H + s): u8 max(min(H + s', 255) - shift, 0), i16 clamp to 16 bits;
+  // with s' = s + shift both are one med3 of H + s' - shift
+  const int mlo = u8 ? 0 : -32768, mhi = u8 ? 255 - shift : 32767;
+  // group-uniform state: best score / column / position, b[]'s size and last entry
+  int gmax = 0, te = -1, qe_best = 0, n_b = 0, last_i = -2, last_v = 0;
+  // column maximum and its smallest position in one max: key = H1 << (5 + LB)
+  // | (W - 1 - lane) << 5 | (31 - slot) (bwa's qe: the first position in memory
+  // order holding the maximum of the column the best score is first seen in;
+  // positions holding it there hold it in H1, as the lazy F stays below it)
+  constexpr int LB = W == 64 ? 6 : 4;
+  static_assert(NK <= 32, "slot index in 5 bits");
+  bool run = live && tlen > 0;
+  const int ncol = W == 64 ? tlen : wave_max(run ? tlen : 0);
+  for (int i = 0; i < ncol; ++i) {
+    if (__ballot(run) == 0ull) break;
+    const bool act = run && i < tlen;
+    const int tb = act ? t_at(i) : 4;
+    // byte 0 selects the score (plo byte tb, or phi byte 4 + k % 4 for N), the rest 0
+    uint32_t sel[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) sel[r] = 0x0C0C0C00u | (uint32_t)(tb + (tb == 4 ? r : 0));
     int Mp[NK], u1[NK], u2[NK];
-    int carry = 0;  // H(i - 1, x - 1) for lane 0 of slot k: lane 63 of slot k - 1
+    // H(i - 1, x - 1): the previous slot of this lane, for slot 0 the last slot
+    // of the lane below (position -1: 0)
+    const int hd0 = grp_shr1<W>(0, Hp[NK - 1]);
 #pragma unroll
     for (int k = 0; k < NK; ++k) {
-      const int x = lane + 64 * k;
-      const int hd = dpp_wave_shr1_i(carry, Hp[k]);
-      carry = read_lane(Hp[k], 63);
-      const int s = prof_score(plo[k], phi[k], tb);
-      int m = u8 ? max(min(hd + s + shift, 255) - shift, 0) : max(min(hd + s, 32767), -32768);
-      m = max(m, E[k]);
+      const int hd = k == 0 ? hd0 : Hp[k - 1];
+      const int sb = (int)__builtin_amdgcn_perm((uint32_t)phi[k / 4], (uint32_t)plo[k], sel[k % 4]);
+      const int m = max(min(max(hd + sb - shift, mlo), mhi), E[k]);
       Mp[k] = m;
-      const bool in = x < nlen;
-      u1[k] = in ? m - oe_ins + x * e_ins + blk[k] * kBlockBig : kScanNeg;
-      u2[k] = in ? m - oe_ins + x * e_ins : kScanNeg;
+      u1[k] = m + c1[k];
+      u2[k] = m + c2[k];
     }
     int ex1[NK], ex2[NK];
-    excl_scan<NK>(u1, kScanNeg, ex1);
-    excl_scan<NK>(u2, kScanNeg, ex2);
-    int imax = 0;
+    grp_excl_scan<W, NK>(u1, ex1);
+    grp_excl_scan<W, NK>(u2, ex2);
+    // Positions past nlen (the group's last lanes) compute values that feed
+    // only later positions; they are kept out of the column maximum.  A block's
+    // first position sees only earlier blocks in ex1, whose smaller block term
+    // makes f1 negative, and position 0 sees kScanNeg: no tests needed.
+    int key = 0;
 #pragma unroll
     for (int k = 0; k < NK; ++k) {
-      const int x = lane + 64 * k;
-      const bool in = x < nlen;
-      const bool first = slen == 0 || x % slen == 0;
-      const int f1 = first ? 0 : max(0, ex1[k] - blk[k] * kBlockBig - (x - 1) * e_ins);
-      const int h1 = max(Mp[k], f1);
-      const int f2 = x == 0 ? 0 : max(0, ex2[k] - (x - 1) * e_ins);
-      E[k] = in ? max(max(E[k] - e_del, 0), max(h1 - oe_del, 0)) : 0;
-      Hp[k] = in ? max(h1, f2) : 0;
-      imax = max(imax, in ? h1 : 0);
+      const int x = gl * NK + k;
+      const int h1 = max(Mp[k], ex1[k] - c1[k] - p.o_ins);  // max(M', F1): F1 >= 0 is implied by M' >= 0
+      E[k] = max(max(E[k] - e_del, h1 - oe_del), 0);
+      Hp[k] = max(h1, ex2[k] - c2[k] - p.o_ins);
+      key = max(key, ((x < nlen ? h1 : 0) << 5) | (31 - k));
     }
-    imax = wave_max(imax);
-    if (imax >= minsc) {  // bwa's b[]: append, or raise the last entry when it holds the previous column
+    // value, then lane (lane-major positions), then slot
+    const int gkey = grp_max<W>(((key >> 5) << (5 + LB)) | ((W - 1 - gl) << 5) | (key & 31));
+    const int imax = gkey >> (5 + LB);
+    if (act && imax >= minsc) {  // bwa's b[]: append, or raise the last entry when it holds the previous column
       if (n_b == 0 || last_i + 1 != i) {
-        if (lane == 0) blist[n_b] = (uint64_t)(uint32_t)imax << 32 | (uint32_t)i;
+        if (gl == 0) blist[n_b] = (uint64_t)(uint32_t)imax << 32 | (uint32_t)i;
         ++n_b;
         last_i = i, last_v = imax;
       } else if (last_v < imax) {
-        if (lane == 0) blist[n_b - 1] = (uint64_t)(uint32_t)imax << 32 | (uint32_t)i;
+        if (gl == 0) blist[n_b - 1] = (uint64_t)(uint32_t)imax << 32 | (uint32_t)i;
         last_i = i, last_v = imax;
       }
     }
-    if (imax > gmax) {
+    if (act && imax > gmax) {
       gmax = imax;
       te = i;
-#pragma unroll
-      for (int k = 0; k < NK; ++k) Hm[k] = Hp[k];
-      if ((u8 && gmax + shift >= 255) || gmax >= endsc) break;
+      qe_best = (W - 1 - ((gkey >> 5) & (W - 1))) * NK + (31 - (gkey & 31));
+      if ((u8 && gmax + shift >= 255) || gmax >= endsc) run = false;
     }
+    if (!(i + 1 < tlen)) run = false;
   }
   AlignRun r{u8 ? (gmax + shift < 255 ? gmax : 255) : gmax, te, -1, -1, -1};
-  if (!u8 || r.score != 255) {
-    int mx = -1;
-#pragma unroll
-    for (int k = 0; k < NK; ++k)
-      if (lane + 64 * k < nlen) mx = max(mx, Hm[k]);
-    mx = wave_max(mx);
-    int qe = 0x7FFFFFFF;  // the smallest position holding the column maximum (bwa's scan keeps it)
-#pragma unroll
-    for (int k = 0; k < NK; ++k)
-      if (lane + 64 * k < nlen && Hm[k] == mx) qe = min(qe, lane + 64 * k);
-    r.qe = -wave_max(-qe);
-    if (n_b > 0) {
-      __syncthreads();  // lane 0's b[] stores before every lane reads them
-      const int w = (r.score + max_mat - 1) / max_mat;
-      const int low = te - w, high = te + w;
-      int best = -1, bte = -1;
-      for (int j = lane; j < n_b; j += 64) {  // the first entry (column order) of the largest score outside the window
-        const uint64_t e = blist[j];
-        const int c = (int)(uint32_t)e, v = (int)(e >> 32);
-        if ((c < low || c > high) && v > best) best = v, bte = c;
-      }
-      const int vmax = wave_max(best);
-      if (vmax > -1) {
-        const int c = bte >= 0 && best == vmax ? bte : 0x7FFFFFFF;
-        r.score2 = vmax;
-        r.te2 = -wave_max(-c);
-      }
+  // the b[] stores of lane 0 before other lanes of its group read them (one
+  // wave per workgroup: LDS ops complete in order; this orders the compiler)
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+  const bool tail = live && (!u8 || r.score != 255);
+  const int w = max_mat > 0 ? (r.score + max_mat - 1) / max_mat : 0;
+  const int low = te - w, high = te + w;
+  int best = -1, bte = -1;
+  const int nbl = tail ? n_b : 0;
+  const int nbmax = W == 64 ? nbl : wave_max(nbl);
+  for (int j0 = 0; j0 < nbmax; j0 += W) {  // the first entry (column order) of the largest score outside the window
+    const int j = j0 + gl;
+    if (j < nbl) {
+      const uint64_t e = blist[j];
+      const int c = (int)(uint32_t)e, v = (int)(e >> 32);
+      if ((c < low || c > high) && v > best) best = v, bte = c;
     }
+  }
+  const int vmax = grp_max<W>(best);
+  const int te2 = -grp_max<W>(-(bte >= 0 && best == vmax ? bte : 0x7FFFFFFF));
+  if (tail) {
+    r.qe = qe_best;
+    if (vmax > -1) r.score2 = vmax, r.te2 = te2;
   }
   return r;
 }
 
-template <int NK>
+// Groups of W lanes run tasks: W = 64, one task per workgroup iteration; W =
+// 16, four consecutive tasks, each group skipping tasks the other launch runs
+// (qlen > kAlignSegQ).  LDS per group: b[] (8 B per target base) and the target.
+template <int W, int NK>
 __global__ __launch_bounds__(64) void bsw_align_kernel(const BswDevBatch b, const BswParams p,
                                                        const int32_t* __restrict__ xtra, int32_t* __restrict__ out,
                                                        int max_tlen) {
   extern __shared__ __align__(16) unsigned char smem[];
-  uint64_t* const blist = reinterpret_cast<uint64_t*>(smem);
-  uint8_t* const tl = smem + 8 * (size_t)max_tlen;
-  const int lane = lane_id();
+  constexpr int G = 64 / W;  // groups per wave
+  const int grp = lane_id() / W, gl = grp_lane<W>();
+  uint64_t* const blist = reinterpret_cast<uint64_t*>(smem) + (size_t)grp * max_tlen;
+  uint8_t* const tl = smem + 8 * (size_t)G * max_tlen + (size_t)grp * max_tlen;
   // bwa's shift (u8 bias) and max_mat from the 5 x 5 matrix, as ksw_qinit
   int mn = 127, mxm = 0;
   for (int a = 0; a < 25; ++a) mn = min(mn, (int)p.mat[a]), mxm = max(mxm, (int)p.mat[a]);
   const int shift = (256 - (int)(uint8_t)(int8_t)mn) & 0xFF;
-  for (long long task = blockIdx.x; task < b.n; task += gridDim.x) {
-    const int qlen = b.qlen[task], tlen = b.tlen[task], xt = xtra[task];
-    const uint8_t* __restrict__ q = b.qbuf + b.qoff[task];
-    const uint8_t* __restrict__ tg = b.tbuf + b.toff[task];
-    for (int i = lane; i < tlen; i += 64) tl[i] = tg[i];
+  const long long ngroups = (b.n + G - 1) / G;
+  for (long long g = blockIdx.x; g < ngroups; g += gridDim.x) {
+    const long long task = g * G + grp;
+    int qlen = 0, tlen = 0, xt = 0;
+    if (task < b.n) qlen = b.qlen[task], tlen = b.tlen[task], xt = xtra[task];
+    const bool mine = task < b.n && (W == 64 ? qlen > kAlignSegQ : qlen <= kAlignSegQ);
+    const uint8_t* __restrict__ q = b.qbuf + (mine ? b.qoff[task] : 0);
+    const uint8_t* __restrict__ tg = b.tbuf + (mine ? b.toff[task] : 0);
+    if (mine)
+      for (int i = gl; i < tlen; i += W) tl[i] = tg[i];
     __syncthreads();
     const bool u8 = (xt & kKswXByte) != 0;
     const int minsc = (xt & kKswXSubo) ? xt & 0xffff : 0x10000;
     const int endsc = (xt & kKswXStop) ? xt & 0xffff : 0x10000;
-    AlignRun r = align_run<NK>(
-        p, qlen, [&](int x) { return (int)q[x]; }, tlen, [&](int j) { return (int)tl[j]; }, u8, shift, mxm, minsc,
-        endsc, blist);
+    AlignRun r = align_run<W, NK>(
+        p, mine, qlen, [&](int x) { return (int)q[x]; }, tlen, [&](int j) { return (int)tl[j]; }, u8, shift, mxm,
+        minsc, endsc, blist);
+    __syncthreads();  // the first pass's b[] reads before the second pass (which appends nothing)
+    // bwa: reverse query[0, qe] and target[0, te] in place (the rest of the
+    // target unchanged, full tlen), stop at the first score, no b[] list
+    const bool second = mine && (xt & kKswXStart) && !((xt & kKswXSubo) && r.score < (xt & 0xffff));
+    const int qe = r.qe, te = r.te;
+    const AlignRun rr = align_run<W, NK>(
+        p, second, qe + 1, [&](int x) { return (int)q[qe - x]; }, tlen,
+        [&](int j) { return (int)tl[j <= te ? te - j : j]; }, u8, shift, mxm, 0x10000, r.score, blist);
     int tb = -1, qb = -1;
-    if ((xt & kKswXStart) && !((xt & kKswXSubo) && r.score < (xt & 0xffff))) {
-      // bwa: reverse query[0, qe] and target[0, te] in place (the rest of the
-      // target unchanged, full tlen), stop at the first score, no b[] list
-      const int qe = r.qe, te = r.te;
-      const AlignRun rr = align_run<NK>(
-          p, qe + 1, [&](int x) { return (int)q[qe - x]; }, tlen,
-          [&](int j) { return (int)tl[j <= te ? te - j : j]; }, u8, shift, mxm, 0x10000, r.score, blist);
-      if (rr.score == r.score) tb = r.te - rr.te, qb = r.qe - rr.qe;
-    }
-    if (lane == 0) {
+    if (second && rr.score == r.score) tb = r.te - rr.te, qb = r.qe - rr.qe;
+    if (mine && gl == 0) {
       int32_t* o = out + 7 * task;
       o[0] = r.score, o[1] = r.te, o[2] = r.qe, o[3] = r.score2, o[4] = r.te2, o[5] = tb, o[6] = qb;
     }
-    __syncthreads();  // the next task rewrites the target and the b[] list
+    __syncthreads();  // the next tasks rewrite the targets and the b[] lists
   }
 }
 
@@ -193,16 +285,25 @@ int launch_bsw_align(const BswDevBatch& b, const BswParams& p, const int32_t* xt
                      int32_t* out, hipStream_t s) {
   if (b.n <= 0) return FCS_OK;
   if (max_qlen > 1024) return fail(FCS_ERR_UNSUPPORTED, "[E::fcship] ksw_align2: qlen > 1024 unsupported");
-  const size_t lds = 8 * (size_t)max(max_tlen, 1) + (size_t)((max_tlen + 15) / 16) * 16;
-  if (lds > 64 * 1024) return fail(FCS_ERR_UNSUPPORTED, "[E::fcship] ksw_align2: tlen too large");
-  const unsigned grid = (unsigned)std::min<long long>(b.n, 4096);
-  // slots of 64 positions for slen * p (p = 16 u8 / 8 i16: at most qlen + 15)
-  const int nlen = max_qlen + 15;
-  if (nlen <= 256)
-    hipLaunchKernelGGL(bsw_align_kernel<4>, dim3(grid), dim3(64), lds, s, b, p, xtra, out, max_tlen);
-  else
-    hipLaunchKernelGGL(bsw_align_kernel<17>, dim3(grid), dim3(64), lds, s, b, p, xtra, out, max_tlen);
-  FCS_HIP_CHECK(hipGetLastError());
+  const int mt = std::max(max_tlen, 1);
+  // queries <= kAlignSegQ: four tasks per wave in 16-lane groups (NK = 10:
+  // slen * p <= 160); longer ones: one task per wave
+  const size_t lds16 = 4 * (8 * (size_t)mt + (size_t)mt) + 16, lds64 = 8 * (size_t)mt + (size_t)mt + 16;
+  if (lds16 > 64 * 1024) return fail(FCS_ERR_UNSUPPORTED, "[E::fcship] ksw_align2: tlen too large");
+  {
+    const unsigned grid = (unsigned)std::min<long long>((b.n + 3) / 4, 4096);
+    hipLaunchKernelGGL((bsw_align_kernel<16, 10>), dim3(grid), dim3(64), lds16, s, b, p, xtra, out, mt);
+    FCS_HIP_CHECK(hipGetLastError());
+  }
+  if (max_qlen > kAlignSegQ) {
+    const unsigned grid = (unsigned)std::min<long long>(b.n, 4096);
+    // slots of 64 positions for slen * p (p = 16 u8 / 8 i16: at most qlen + 15)
+    if (max_qlen + 15 <= 256)
+      hipLaunchKernelGGL((bsw_align_kernel<64, 4>), dim3(grid), dim3(64), lds64, s, b, p, xtra, out, mt);
+    else
+      hipLaunchKernelGGL((bsw_align_kernel<64, 17>), dim3(grid), dim3(64), lds64, s, b, p, xtra, out, mt);
+    FCS_HIP_CHECK(hipGetLastError());
+  }
   return FCS_OK;
 }
 

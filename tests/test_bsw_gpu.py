@@ -389,6 +389,34 @@ def test_ksw_align2_batch_bit_exact(gpu, xbyte):
         assert tuple(got[k]) == ref, f"task {k} (qlen {len(q)}, tlen {len(tg)}): {tuple(got[k])} != {ref}"
 
 
+@pytest.mark.parametrize("xbyte", [True, False])
+def test_ksw_align2_low_complexity_ties(gpu, xbyte):
+    """Tandem repeats and homopolymers: many positions share a column's
+    maximum and many columns share the best score, so qe (smallest position
+    holding the maximum), te (first column reaching it), te2 and the b[] list
+    rules all meet ties; queries across the 16-lane / 64-lane kernels' split."""
+    rng = np.random.default_rng(41 if xbyte else 42)
+    items = []
+    for k in range(240):
+        unit = rng.integers(0, 4, int(rng.integers(1, 5))).astype(np.uint8)
+        ql = int(rng.choice([16, 17, 33, 100, 151, 160, 161, 200]))
+        q = np.resize(unit, ql)
+        flank = rng.integers(0, 4, int(rng.integers(0, 60))).astype(np.uint8)
+        t = np.concatenate([flank, np.resize(unit, int(rng.integers(ql // 2, 2 * ql + 1))),
+                            rng.integers(0, 4, int(rng.integers(0, 60))).astype(np.uint8)])
+        if rng.random() < 0.3:
+            q = q.copy()
+            q[int(rng.integers(0, ql))] = (q[0] + 1) % 4
+        items.append((q.astype(np.uint8), t.astype(np.uint8), 0, 0))
+    t = fcship.make_tasks(items)
+    m = fcship.default_mat()
+    x = fcship.KSW_XSUBO | fcship.KSW_XSTART | (fcship.KSW_XBYTE if xbyte else 0) | 19
+    got = fcship.bsw_align(t, x)
+    for k in range(t.n):
+        q, tg, _, _ = t.task(k)
+        assert tuple(got[k]) == oracle_lib.ksw_align2(q, tg, m, x), (k, len(q), len(tg))
+
+
 def test_ksw_align2_flags_and_twin(gpu):
     """Without XSUBO every column counts and no b[] list; without XSTART no
     start; XSTOP ends at a score; the signature twin equals the batch."""
