@@ -118,7 +118,7 @@ __device__ AlignRun align_run(const BswParams& p, bool live, int qlen, QAt q_at,
   // offsets c1 = x e_ins - oe_ins + block * kBlockBig, c2 = x e_ins - oe_ins
   // (u = M' + c turns both max-plus scans into plain max scans).
   constexpr int NP = (NK + 3) / 4;
-  int Hp[NK], E[NK], plo[NK], phi[NP], c1[NK], c2[NK];
+  int Hp[NK], E[NK], Hm[NK], plo[NK], phi[NP], c1[NK], c2[NK];
 #pragma unroll
   for (int k = 0; k < NP; ++k) phi[k] = 0;
 #pragma unroll
@@ -130,19 +130,16 @@ __device__ AlignRun align_run(const BswParams& p, bool live, int qlen, QAt q_at,
     phi[k / 4] |= sc(4) << (8 * (k % 4));
     c2[k] = x * e_ins - oe_ins;
     c1[k] = c2[k] + (slen > 0 ? x / slen : 0) * kBlockBig;
-    Hp[k] = E[k] = 0;
+    Hp[k] = E[k] = Hm[k] = 0;
   }
   // M = sat(H + s): u8 max(min(H + s', 255) - shift, 0), i16 clamp to 16 bits;
   // with s' = s + shift both are one med3 of H + s' - shift
   const int mlo = u8 ? 0 : -32768, mhi = u8 ? 255 - shift : 32767;
-  // group-uniform state: best score / column / position, b[]'s size and last entry
-  int gmax = 0, te = -1, qe_best = 0, n_b = 0, last_i = -2, last_v = 0;
-  // column maximum and its smallest position in one max: key = H1 << (5 + LB)
-  // | (W - 1 - lane) << 5 | (31 - slot) (bwa's qe: the first position in memory
-  // order holding the maximum of the column the best score is first seen in;
-  // positions holding it there hold it in H1, as the lazy F stays below it)
-  constexpr int LB = W == 64 ? 6 : 4;
-  static_assert(NK <= 32, "slot index in 5 bits");
+  // group-uniform state: best score / column, b[]'s size and last entry; Hm:
+  // the H column of the best score (bwa's Hmax, for qe).  (A packed
+  // max-and-position key per cell instead of the copy saves the 10 VGPRs that
+  // give 3 waves per SIMD, and measured 12% slower: profiles/r4/r4k_*.)
+  int gmax = 0, te = -1, n_b = 0, last_i = -2, last_v = 0;
   bool run = live && tlen > 0;
   const int ncol = W == 64 ? tlen : wave_max(run ? tlen : 0);
   for (int i = 0; i < ncol; ++i) {
@@ -173,18 +170,17 @@ __device__ AlignRun align_run(const BswParams& p, bool live, int qlen, QAt q_at,
     // only later positions; they are kept out of the column maximum.  A block's
     // first position sees only earlier blocks in ex1, whose smaller block term
     // makes f1 negative, and position 0 sees kScanNeg: no tests needed.
-    int key = 0;
+    int imax = 0, Hn[NK];
 #pragma unroll
     for (int k = 0; k < NK; ++k) {
       const int x = gl * NK + k;
       const int h1 = max(Mp[k], ex1[k] - c1[k] - p.o_ins);  // max(M', F1): F1 >= 0 is implied by M' >= 0
       E[k] = max(max(E[k] - e_del, h1 - oe_del), 0);
-      Hp[k] = max(h1, ex2[k] - c2[k] - p.o_ins);
-      key = max(key, ((x < nlen ? h1 : 0) << 5) | (31 - k));
+      Hn[k] = max(h1, ex2[k] - c2[k] - p.o_ins);
+      Hp[k] = Hn[k];
+      imax = max(imax, x < nlen ? h1 : 0);
     }
-    // value, then lane (lane-major positions), then slot
-    const int gkey = grp_max<W>(((key >> 5) << (5 + LB)) | ((W - 1 - gl) << 5) | (key & 31));
-    const int imax = gkey >> (5 + LB);
+    imax = grp_max<W>(imax);
     if (act && imax >= minsc) {  // bwa's b[]: append, or raise the last entry when it holds the previous column
       if (n_b == 0 || last_i + 1 != i) {
         if (gl == 0) blist[n_b] = (uint64_t)(uint32_t)imax << 32 | (uint32_t)i;
@@ -198,7 +194,8 @@ __device__ AlignRun align_run(const BswParams& p, bool live, int qlen, QAt q_at,
     if (act && imax > gmax) {
       gmax = imax;
       te = i;
-      qe_best = (W - 1 - ((gkey >> 5) & (W - 1))) * NK + (31 - (gkey & 31));
+#pragma unroll
+      for (int k = 0; k < NK; ++k) Hm[k] = Hn[k];
       if ((u8 && gmax + shift >= 255) || gmax >= endsc) run = false;
     }
     if (!(i + 1 < tlen)) run = false;
@@ -208,6 +205,16 @@ __device__ AlignRun align_run(const BswParams& p, bool live, int qlen, QAt q_at,
   // wave per workgroup: LDS ops complete in order; this orders the compiler)
   __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
   const bool tail = live && (!u8 || r.score != 255);
+  int mx = -1;
+#pragma unroll
+  for (int k = 0; k < NK; ++k)
+    if (gl * NK + k < nlen) mx = max(mx, Hm[k]);
+  mx = grp_max<W>(mx);
+  int qx = 0x7FFFFFFF;  // the smallest position holding the column maximum (bwa's memory-order scan)
+#pragma unroll
+  for (int k = 0; k < NK; ++k)
+    if (gl * NK + k < nlen && Hm[k] == mx) qx = min(qx, gl * NK + k);
+  const int qe_best = -grp_max<W>(-qx);
   const int w = max_mat > 0 ? (r.score + max_mat - 1) / max_mat : 0;
   const int low = te - w, high = te + w;
   int best = -1, bte = -1;
