@@ -917,8 +917,9 @@ def main():
                         "XSTART | XBYTE | 19",
             "tasks": ga["tasks"], "ms": round(ga["ms"], 3), "gcups": round(ga["gcups"], 3),
             "cells": ga["cells"], "cells_first_pass": ga["cells_first"],
-            "kernel": "bsw_align_kernel<4> (one wave per task, lane l holds query positions l + 64k; striped-F "
-                      "semantics by segmented max-plus scans; both passes in one launch)"}
+            "kernel": "bsw_align_kernel<16, 10> (four tasks per wave in 16-lane groups, lane l holding query "
+                      "positions 10 l .. 10 l + 9; bwa's striped-F semantics by register running-max scans plus one "
+                      "row scan; both passes in one launch)"}
         if world == 1 and not args.no_cpu_baseline:
             line["bsw"]["cpu_baseline"], line["bsw"]["parity"] = cpu_baseline_bsw(c3, r3, args.cpu_budget,
                                                                                   cpu_threads())
