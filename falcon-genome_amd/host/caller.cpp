@@ -444,7 +444,10 @@ class PassCombiner {
     std::unique_lock<std::mutex> lk(m_);
     q_.push_back(&r);
     cv_.notify_all();
-    const auto deadline = std::chrono::steady_clock::now() + std::chrono::milliseconds(window_ms);
+    // system_clock: waits on it are pthread_cond_timedwait, which ThreadSanitizer
+    // follows (a steady_clock wait_until is pthread_cond_clockwait in this
+    // libstdc++, which GCC 11's TSAN does not intercept: false double locks)
+    const auto deadline = std::chrono::system_clock::now() + std::chrono::milliseconds(window_ms);
     while (!r.done) {
       if (busy_ || q_.front() != &r) {
         cv_.wait(lk);

@@ -44,6 +44,13 @@ rc=0
   FCS_TEMP_DIR=$W/tmp2 FCS_LOG_DIR=$W/log $SANBIN synth -o $W/syn2 -c chr1:40000000 -x 30 >/dev/null 2>$W/int.err &
   pid=$!; sleep 3; kill -INT $pid; wait $pid; st=$?
   [ $st -eq 130 ] && [ ! -e $W/tmp2 ] && echo "synth + SIGINT: exit 130, temp dir removed" || { rc=1; echo "SIGINT: exit $st"; }
+  # htc with concurrent shards' PairHMM passes merged (host/caller.cpp
+  # PassCombiner: shard threads, one leader per pass) against the CPU mock
+  make -C tests/cpu_mock >/dev/null || rc=1
+  LD_LIBRARY_PATH=$PWD/tests/cpu_mock/build FCS_GPU_DEVICES=0 FCS_MOCK_PHMM=gkl FCS_GATK_NCONTIGS=8 \
+    FCS_GATK_NPROCS=4 FCS_GPU_PHMM_COMBINE_MS=500 FCS_TEMP_DIR=$W/tmp3 FCS_LOG_DIR=$W/log3 \
+    timeout 600 $SANBIN htc -f -r $W/syn/ref.fasta -i $W/syn/sample.bam -o $W/m.vcf -v >/dev/null 2>$W/htc.err \
+    && echo "htc with merged passes (8 shards, 4 threads): ok" || { rc=1; tail -5 $W/htc.err; }
   if ls $W/tsan.* >/dev/null 2>&1; then cat $W/tsan.*; rc=1; else echo "TSAN reports: none"; fi
   echo "sanitize rc=$rc"
 } 2>&1 | tee "$LOG"
