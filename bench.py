@@ -920,6 +920,19 @@ def main():
             "kernel": "bsw_align_kernel<16, 10> (four tasks per wave in 16-lane groups, lane l holding query "
                       "positions 10 l .. 10 l + 9; bwa's striped-F semantics by register running-max scans plus one "
                       "row scan; both passes in one launch)"}
+        am = {}
+        try:
+            am = json.load(open(os.path.join(ROOT, "profiles", "pmc_bsw.json"))).get("align", {})
+        except (OSError, ValueError):
+            pass
+        if am.get("valu_lane_instr_per_cell"):
+            vpc = am["valu_lane_instr_per_cell"]
+            ach = ga["gcups"] * 1e9 * vpc
+            line["bsw"]["align"]["roofline"] = {
+                "bound": "valu", "unit": "T lane-instr/s", "peak": round(VALU_LANE_INSTR_PEAK / 1e12, 3),
+                "achieved": round(ach / 1e12, 3), "frac": round(ach / VALU_LANE_INSTR_PEAK, 4),
+                "valu_instr_per_cell": vpc,
+                "valu_source": f"profiles/pmc_bsw.json align ({am.get('source', '')}: SQ_INSTS_VALU x 64 / cells)"}
         if world == 1 and not args.no_cpu_baseline:
             line["bsw"]["cpu_baseline"], line["bsw"]["parity"] = cpu_baseline_bsw(c3, r3, args.cpu_budget,
                                                                                   cpu_threads())

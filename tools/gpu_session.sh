@@ -43,7 +43,13 @@ for step in "$@"; do
       run bswpmc_c3_write 300 rocprofv3 --pmc WRITE_SIZE -d "$OUT/bswpmc_c3_write" -o run --output-format csv -- \
             python3 "$ROOT/tools/bsw_bench.py" --which c3 --reps 1 &&
       run bswpmc_global 300 rocprofv3 --pmc $SQ -d "$OUT/bswpmc_global" -o run --output-format csv -- \
-            python3 "$ROOT/tools/bsw_bench.py" --which global --reps 1 ;;
+            python3 "$ROOT/tools/bsw_bench.py" --which global --reps 1 &&
+      run bswpmc_align 300 rocprofv3 --pmc $SQ -d "$OUT/bswpmc_align" -o run --output-format csv -- \
+            python3 "$ROOT/tools/bsw_bench.py" --which align --reps 1 ;;
+    alignpmc)  # ksw_align2 only: SQ issue counters of one batch
+      SQ="SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY"
+      run bswpmc_align 300 rocprofv3 --pmc $SQ -d "$OUT/bswpmc_align" -o run --output-format csv -- \
+            python3 "$ROOT/tools/bsw_bench.py" --which align --reps 1 ;;
     phmmpmc)  # PairHMM C2 forward pass: SQ issue/stall counters, then HBM bytes (separate passes)
       run phmmpmc_sq 300 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_BUSY_CYCLES \
             SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY -d "$OUT/phmmpmc_sq" -o run --output-format csv -- \
