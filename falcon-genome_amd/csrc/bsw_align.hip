@@ -214,7 +214,8 @@ __device__ AlignRun align_run(const BswParams& p, bool live, int qlen, QAt q_at,
 #pragma unroll
   for (int k = 0; k < NK; ++k)
     if (gl * NK + k < nlen && Hm[k] == mx) qx = min(qx, gl * NK + k);
-  const int qe_best = -grp_max<W>(-qx);
+  const int qe_min = -grp_max<W>(-qx);
+  const int qe_best = nlen > 0 ? qe_min : -1;  // an empty query: bwa's scan finds nothing
   const int w = max_mat > 0 ? (r.score + max_mat - 1) / max_mat : 0;
   const int low = te - w, high = te + w;
   int best = -1, bte = -1;

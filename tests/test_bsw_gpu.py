@@ -417,6 +417,23 @@ def test_ksw_align2_low_complexity_ties(gpu, xbyte):
         assert tuple(got[k]) == oracle_lib.ksw_align2(q, tg, m, x), (k, len(q), len(tg))
 
 
+def test_ksw_align2_empty_and_tiny(gpu):
+    """Empty and one-base queries and targets, alone and mixed into one batch
+    (the four tasks of a wave run in lock-step), against the restatement."""
+    rng = np.random.default_rng(43)
+    shapes = [(0, 0), (0, 5), (5, 0), (1, 1), (1, 30), (30, 1), (2, 2), (0, 300), (160, 0), (161, 3)]
+    items = []
+    for ql, tl in shapes * 3:
+        items.append((rng.integers(0, 4, ql).astype(np.uint8), rng.integers(0, 4, tl).astype(np.uint8), 0, 0))
+    t = fcship.make_tasks(items)
+    m = fcship.default_mat()
+    for x in (fcship.KSW_XSUBO | fcship.KSW_XSTART | fcship.KSW_XBYTE | 19, fcship.KSW_XSTART, 0):
+        got = fcship.bsw_align(t, x)
+        for k in range(t.n):
+            q, tg, _, _ = t.task(k)
+            assert tuple(got[k]) == oracle_lib.ksw_align2(q, tg, m, x), (hex(x), k, len(q), len(tg))
+
+
 def test_ksw_align2_flags_and_twin(gpu):
     """Without XSUBO every column counts and no b[] list; without XSTART no
     start; XSTOP ends at a score; the signature twin equals the batch."""
