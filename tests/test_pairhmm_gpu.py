@@ -474,7 +474,7 @@ def test_session_pool_concurrent_calls(gpu):
 def test_grouped_class_grid_stride(gpu):
     """40,000 short-read pairs (R < 33: the grouped two-row kernel) in one launch
     class: 10,000 four-pair groups, more than the grouped launch's workgroup cap
-    (FCS_PHMM_GROUPED_GRID = 8192), so workgroups stride over the class."""
+    (kGroupedGrid = 8192), so workgroups stride over the class."""
     reads, haps = random_batch(23, 200, 200, 5, 32, 20, 60)
     p = fcship.make_pairs(reads, haps)
     assert p.n_pairs == 40_000
