@@ -621,7 +621,7 @@ def bsw_roofline(r3, rf):
     perf = meas.get("fixed", {}).get("valu_lane_instr_per_cell")
     out = {"bound": "valu", "unit": "T lane-instr/s", "peak": round(VALU_LANE_INSTR_PEAK / 1e12, 3),
            "kernel": "bsw_ext_kernel (pair waves: two ksw_extend2 tasks per lane, packed 16-bit VOP3P; one LPT-ordered launch)",
-           "body_instr_per_cell": 9.75,
+           "body_instr_per_cell": 8.75,
            "hbm_GBs": round(r3["bytes"] / (r3["ms"] * 1e-3) / 1e9, 2),
            "hbm_frac": round(r3["bytes"] / (r3["ms"] * 1e-3) / 1e9 / HBM_PEAK_GBS, 5)}
     c3m = meas.get("c3", {})
