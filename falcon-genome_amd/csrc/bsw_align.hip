@@ -32,6 +32,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <string>
 
 #include "bsw_scan.h"
 #include "fcship_internal.h"
@@ -239,12 +240,13 @@ __device__ AlignRun align_run(const BswParams& p, bool live, int qlen, QAt q_at,
 }
 
 // Groups of W lanes run tasks: W = 64, one task per workgroup iteration; W =
-// 16, four consecutive tasks, each group skipping tasks the other launch runs
-// (qlen > kAlignSegQ).  LDS per group: b[] (8 B per target base) and the target.
+// 16, four consecutive tasks.  The 16-lane launch takes the queries up to
+// seg_q, the 64-lane launch the longer ones.  LDS per group: b[] (8 B per
+// target base) and the target.
 template <int W, int NK>
 __global__ __launch_bounds__(64) void bsw_align_kernel(const BswDevBatch b, const BswParams p,
                                                        const int32_t* __restrict__ xtra, int32_t* __restrict__ out,
-                                                       int max_tlen) {
+                                                       int max_tlen, int seg_q) {
   extern __shared__ __align__(16) unsigned char smem[];
   constexpr int G = 64 / W;  // groups per wave
   const int grp = lane_id() / W, gl = grp_lane<W>();
@@ -259,7 +261,7 @@ __global__ __launch_bounds__(64) void bsw_align_kernel(const BswDevBatch b, cons
     const long long task = g * G + grp;
     int qlen = 0, tlen = 0, xt = 0;
     if (task < b.n) qlen = b.qlen[task], tlen = b.tlen[task], xt = xtra[task];
-    const bool mine = task < b.n && (W == 64 ? qlen > kAlignSegQ : qlen <= kAlignSegQ);
+    const bool mine = task < b.n && (W == 64 ? qlen > seg_q : qlen <= seg_q);
     const uint8_t* __restrict__ q = b.qbuf + (mine ? b.qoff[task] : 0);
     const uint8_t* __restrict__ tg = b.tbuf + (mine ? b.toff[task] : 0);
     if (mine)
@@ -294,25 +296,44 @@ int launch_bsw_align(const BswDevBatch& b, const BswParams& p, const int32_t* xt
   if (b.n <= 0) return FCS_OK;
   if (max_qlen > 1024) return fail(FCS_ERR_UNSUPPORTED, "[E::fcship] ksw_align2: qlen > 1024 unsupported");
   const int mt = std::max(max_tlen, 1);
-  // queries <= kAlignSegQ: four tasks per wave in 16-lane groups (NK = 10:
-  // slen * p <= 160); longer ones: one task per wave
-  const size_t lds16 = 4 * (8 * (size_t)mt + (size_t)mt) + 16, lds64 = 8 * (size_t)mt + (size_t)mt + 16;
-  if (lds16 > 64 * 1024) return fail(FCS_ERR_UNSUPPORTED, "[E::fcship] ksw_align2: tlen too large");
-  {
-    const unsigned grid = (unsigned)std::min<long long>((b.n + 3) / 4, 4096);
-    hipLaunchKernelGGL((bsw_align_kernel<16, 10>), dim3(grid), dim3(64), lds16, s, b, p, xtra, out, mt);
+  // LDS per group: b[] + target = 9 B per target base.  Queries <= kAlignSegQ
+  // run four tasks per wave in 16-lane groups (NK = 10: slen * p <= 160) while
+  // four groups' areas fit the CU's 160 KB; longer queries, and every query
+  // when the target windows are longer (mate rescue with wide insert-size
+  // distributions), run one task per wave.
+  constexpr size_t kLdsMax = 160 * 1024;
+  const size_t lds16 = 4 * 9 * (size_t)mt + 16, lds64 = 9 * (size_t)mt + 16;
+  if (lds64 > kLdsMax)
+    return fail(FCS_ERR_UNSUPPORTED, "[E::fcship] ksw_align2: target longer than " +
+                                         std::to_string((kLdsMax - 16) / 9) + " bases unsupported");
+  const bool seg = lds16 <= kLdsMax;
+  const int seg_q = seg ? kAlignSegQ : -1;
+  auto go = [&](const void* kern, unsigned grid, size_t lds, auto launch) -> int {
+    if (lds > 64 * 1024)
+      FCS_HIP_CHECK(hipFuncSetAttribute(kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+    launch(grid, lds);
     FCS_HIP_CHECK(hipGetLastError());
-  }
-  if (max_qlen > kAlignSegQ) {
+    return FCS_OK;
+  };
+  int rc = FCS_OK;
+  if (seg)
+    rc = go((const void*)bsw_align_kernel<16, 10>, (unsigned)std::min<long long>((b.n + 3) / 4, 4096), lds16,
+            [&](unsigned grid, size_t lds) {
+              hipLaunchKernelGGL((bsw_align_kernel<16, 10>), dim3(grid), dim3(64), lds, s, b, p, xtra, out, mt, seg_q);
+            });
+  if (rc == FCS_OK && max_qlen > seg_q) {
     const unsigned grid = (unsigned)std::min<long long>(b.n, 4096);
     // slots of 64 positions for slen * p (p = 16 u8 / 8 i16: at most qlen + 15)
     if (max_qlen + 15 <= 256)
-      hipLaunchKernelGGL((bsw_align_kernel<64, 4>), dim3(grid), dim3(64), lds64, s, b, p, xtra, out, mt);
+      rc = go((const void*)bsw_align_kernel<64, 4>, grid, lds64, [&](unsigned g, size_t lds) {
+        hipLaunchKernelGGL((bsw_align_kernel<64, 4>), dim3(g), dim3(64), lds, s, b, p, xtra, out, mt, seg_q);
+      });
     else
-      hipLaunchKernelGGL((bsw_align_kernel<64, 17>), dim3(grid), dim3(64), lds64, s, b, p, xtra, out, mt);
-    FCS_HIP_CHECK(hipGetLastError());
+      rc = go((const void*)bsw_align_kernel<64, 17>, grid, lds64, [&](unsigned g, size_t lds) {
+        hipLaunchKernelGGL((bsw_align_kernel<64, 17>), dim3(g), dim3(64), lds, s, b, p, xtra, out, mt, seg_q);
+      });
   }
-  return FCS_OK;
+  return rc;
 }
 
 }  // namespace fcs
