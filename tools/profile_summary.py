@@ -76,8 +76,8 @@ def main():
              "_note": "HBM bytes per fp32 forward pass (all hap-length class launches) on the default C2 workload = "
                       "(FETCH_SIZE + WRITE_SIZE) KiB * 1024 from separate rocprofv3 --pmc passes "
                       f"(profiles/{os.path.basename(dst)}/{tag}_*.csv), divided by the passes profiled.  FETCH_SIZE "
-                      "is uncorrected: the gfx950 1/2 correction in MI355X_MICROARCH.md applies to 16-B/lane "
-                      "streaming loads; this kernel's reads are 1-byte per-lane loads whose calibration is unmeasured.",
+                      "as reported: bench.py prices HBM reads as 2 x FETCH_SIZE (the gfx950 calibration of "
+                      "profiles/fetch_calibration.json, measured for 1, 4 and 16 B per-lane loads).",
              "fetch_kib": pmc["FETCH_SIZE"], "write_kib": pmc["WRITE_SIZE"], "source": tag}
         json.dump(t, open(os.path.join(root, "pmc_traffic.json"), "w"), indent=1)
     if "SQ_INSTS_VALU" in pmc:
