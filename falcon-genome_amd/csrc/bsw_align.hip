@@ -295,6 +295,13 @@ int launch_bsw_align(const BswDevBatch& b, const BswParams& p, const int32_t* xt
                      int32_t* out, hipStream_t s) {
   if (b.n <= 0) return FCS_OK;
   if (max_qlen > 1024) return fail(FCS_ERR_UNSUPPORTED, "[E::fcship] ksw_align2: qlen > 1024 unsupported");
+  {  // the profile holds mat + shift as bytes (shift = -min, as bwa's u8 bias)
+    int mn = 127, mx = -128;
+    for (int a = 0; a < 25; ++a) mn = std::min(mn, (int)p.mat[a]), mx = std::max(mx, (int)p.mat[a]);
+    const int shift = (256 - (int)(uint8_t)(int8_t)mn) & 0xFF;
+    if (mx + shift > 255)
+      return fail(FCS_ERR_UNSUPPORTED, "[E::fcship] ksw_align2: a scoring matrix without a negative entry is unsupported");
+  }
   const int mt = std::max(max_tlen, 1);
   // LDS per group: b[] + target = 9 B per target base.  Queries <= kAlignSegQ
   // run four tasks per wave in 16-lane groups (NK = 10: slen * p <= 160) while
