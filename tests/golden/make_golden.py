@@ -80,6 +80,32 @@ def ksw_cases():
     return dict(mat=m.tolist(), extend=ext, global_=glo)
 
 
+def align_cases():
+    """bwa ksw_align2 (mate rescue): related and unrelated query / window pairs,
+    second copies for score2, both widths and the flag mixes bwa uses."""
+    rng = np.random.default_rng(20261017)
+    m = mat()
+    flags = [0x40000 | 0x80000 | 0x10000 | 19, 0x40000 | 0x80000 | 19, 0x80000, 0x10000, 0x20000 | 30, 0]
+    out = []
+    for k in range(48):
+        ql, tl = int(rng.integers(0, 170)), int(rng.integers(0, 400))
+        t = rng.integers(0, 4, tl)
+        if k % 3 and tl > 10 and ql > 0:
+            a = int(rng.integers(0, max(1, tl - ql)))
+            q = np.resize(t[a:a + ql] if tl - a >= 1 else t, ql).copy()
+            mut = rng.random(ql) < 0.05
+            q[mut] = rng.integers(0, 5, int(mut.sum()))
+            if k % 4 == 1 and tl > 2 * ql + 4:
+                b = int(rng.integers(0, tl - ql))
+                t[b:b + ql] = q
+        else:
+            q = rng.integers(0, 5, ql)
+        x = flags[k % len(flags)]
+        r = oracle_lib.ksw_align2(q.astype(np.uint8), t.astype(np.uint8), m, x)
+        out.append(dict(q=q.tolist(), t=t.tolist(), xtra=x, out=list(r)))
+    return out
+
+
 def main():
     with open(os.path.join(HERE, "phmm_golden.json"), "w") as f:
         json.dump({"generator": "tests/golden/make_golden.py", "semantics": "GKL float + double rescue",
@@ -88,6 +114,9 @@ def main():
     with open(os.path.join(HERE, "ksw_golden.json"), "w") as f:
         json.dump({"generator": "tests/golden/make_golden.py", "semantics": "bwa ksw_extend2 / ksw_global2",
                    "mat": k["mat"], "extend": k["extend"], "global": k["global_"]}, f, separators=(",", ":"))
+    with open(os.path.join(HERE, "ksw_align_golden.json"), "w") as f:
+        json.dump({"generator": "tests/golden/make_golden.py", "semantics": "bwa ksw_align2 (striped u8 / i16)",
+                   "mat": mat().tolist(), "cases": align_cases()}, f, separators=(",", ":"))
 
 
 if __name__ == "__main__":

@@ -449,6 +449,20 @@ def test_ksw_align2_long_windows(gpu, tlen):
         assert tuple(got[k]) == oracle_lib.ksw_align2(q, tg, m, x), (k, len(q), len(tg))
 
 
+def test_ksw_align2_golden_fixtures_gpu(gpu):
+    """The committed ksw_align2 vectors (tests/golden/ksw_align_golden.json),
+    each through the batch entry point with its own xtra."""
+    import json
+    import os
+    with open(os.path.join(os.path.dirname(__file__), "golden", "ksw_align_golden.json")) as f:
+        g = json.load(f)
+    items = [(np.array(c["q"], np.uint8), np.array(c["t"], np.uint8), 0, 0) for c in g["cases"]]
+    t = fcship.make_tasks(items)
+    got = fcship.bsw_align(t, np.array([c["xtra"] for c in g["cases"]], np.int32))
+    for k, c in enumerate(g["cases"]):
+        assert list(got[k]) == c["out"], k
+
+
 def test_ksw_align2_flags_and_twin(gpu):
     """Without XSUBO every column counts and no b[] list; without XSTART no
     start; XSTOP ends at a score; the signature twin equals the batch."""

@@ -266,3 +266,14 @@ def test_ksw_align2_suboptimal_hit():
     sc, te, qe, sc2, te2, tb, qb = oracle_lib.ksw_align2(q, t, mat, x)
     assert (sc, qe, qb) == (60, 59, 0) and te == 40 + 60 + 200 + 59 and tb == 300
     assert sc2 == 60 - 3 * 5 and te2 == 40 + 59
+
+
+def test_ksw_align2_golden_fixtures():
+    """The restatement reproduces the committed ksw_align2 vectors
+    (tests/golden/ksw_align_golden.json, generated by make_golden.py)."""
+    with open(os.path.join(HERE, "golden", "ksw_align_golden.json")) as f:
+        g = json.load(f)
+    m = np.array(g["mat"], np.int8)
+    for k, c in enumerate(g["cases"]):
+        got = oracle_lib.ksw_align2(np.array(c["q"], np.uint8), np.array(c["t"], np.uint8), m, c["xtra"])
+        assert list(got) == c["out"], k
