@@ -41,7 +41,10 @@ namespace fcs {
 
 constexpr int kKswXByte = 0x10000, kKswXStop = 0x20000, kKswXSubo = 0x40000, kKswXStart = 0x80000;
 constexpr int kBlockBig = 1 << 20;  // > the range of one block's scan values; block ids < 16
-constexpr int kAlignSegQ = 160;      // longest query of the 16-lane groups (NK = 10 slots)
+constexpr int kAlignSegQ = 160;
+#ifndef FCS_ALIGN_PK_WAVES
+#define FCS_ALIGN_PK_WAVES 1  // the packed kernel's occupancy target (A/B: tools/build_alt.sh)
+#endif      // longest query of the 16-lane groups (NK = 10 slots)
 
 // Group-level primitives: W = 16 (a DPP row) or 64 (the wave).
 template <int W>
@@ -71,9 +74,19 @@ __device__ __forceinline__ int grp_last(int v) {
     return __builtin_amdgcn_ds_swizzle(v, 0x10 | (0x0F << 5));
   }
 }
+// The group's maximum in every lane: W = 16, a butterfly of row rotations
+// (no LDS round trip on the column loop's critical path).
 template <int W>
 __device__ __forceinline__ int grp_max(int v) {
-  return grp_last<W>(grp_incl_max<W>(v, INT32_MIN));
+  if constexpr (W == 64) {
+    return grp_last<W>(grp_incl_max<W>(v, INT32_MIN));
+  } else {
+    v = max(v, __builtin_amdgcn_update_dpp(v, v, kDppRowRor8, 0xF, 0xF, false));
+    v = max(v, __builtin_amdgcn_update_dpp(v, v, kDppRowRor4, 0xF, 0xF, false));
+    v = max(v, __builtin_amdgcn_update_dpp(v, v, kDppRowRor2, 0xF, 0xF, false));
+    v = max(v, __builtin_amdgcn_update_dpp(v, v, kDppRowRor1, 0xF, 0xF, false));
+    return v;
+  }
 }
 // Lane l <- lane l - 1 of the group's value; the group's lane 0 <- `first`.
 template <int W>
@@ -107,7 +120,7 @@ struct AlignRun {
 // group's b[] area.
 template <int W, int NK, class QAt, class TAt>
 __device__ AlignRun align_run(const BswParams& p, bool live, int qlen, QAt q_at, int tlen, TAt t_at, bool u8,
-                              int shift, int max_mat, int minsc, int endsc, uint64_t* __restrict__ blist) {
+                              int shift, int max_mat, int minsc, int endsc, uint32_t* __restrict__ blist) {
   const int gl = grp_lane<W>();
   const int pl = u8 ? 16 : 8;
   const int slen = (qlen + pl - 1) / pl;
@@ -184,11 +197,11 @@ __device__ AlignRun align_run(const BswParams& p, bool live, int qlen, QAt q_at,
     imax = grp_max<W>(imax);
     if (act && imax >= minsc) {  // bwa's b[]: append, or raise the last entry when it holds the previous column
       if (n_b == 0 || last_i + 1 != i) {
-        if (gl == 0) blist[n_b] = (uint64_t)(uint32_t)imax << 32 | (uint32_t)i;
+        if (gl == 0) blist[n_b] = (uint32_t)imax << 16 | (uint32_t)i;
         ++n_b;
         last_i = i, last_v = imax;
       } else if (last_v < imax) {
-        if (gl == 0) blist[n_b - 1] = (uint64_t)(uint32_t)imax << 32 | (uint32_t)i;
+        if (gl == 0) blist[n_b - 1] = (uint32_t)imax << 16 | (uint32_t)i;
         last_i = i, last_v = imax;
       }
     }
@@ -225,8 +238,195 @@ __device__ AlignRun align_run(const BswParams& p, bool live, int qlen, QAt q_at,
   for (int j0 = 0; j0 < nbmax; j0 += W) {  // the first entry (column order) of the largest score outside the window
     const int j = j0 + gl;
     if (j < nbl) {
-      const uint64_t e = blist[j];
-      const int c = (int)(uint32_t)e, v = (int)(e >> 32);
+      const uint32_t e = blist[j];
+      const int c = (int)(e & 0xFFFF), v = (int)(e >> 16);
+      if ((c < low || c > high) && v > best) best = v, bte = c;
+    }
+  }
+  const int vmax = grp_max<W>(best);
+  const int te2 = -grp_max<W>(-(bte >= 0 && best == vmax ? bte : 0x7FFFFFFF));
+  if (tail) {
+    r.qe = qe_best;
+    if (vmax > -1) r.score2 = vmax, r.te2 = te2;
+  }
+  return r;
+}
+
+// ---------------------------------------------------------------- packed u8
+// bwa's ksw_u8 tasks (XBYTE: every H, E, M' in [0, 255]) in 16-lane groups, on
+// pairs of positions in packed 16-bit halves: lane l's ten positions
+// x = 10 l + k sit in five registers, lo half k = j, hi half k = j + 5, so one
+// VOP3P instruction does two cells.  The scan values are biased to stay
+// non-negative (c2 = x e_ins + 1, c1 = c2 + block * big with big = 257 + 159
+// e_ins > the spread of one block's values), so 0 is the scan's empty value
+// and the signed differences ex - c fit in 16 bits while
+// 16 big + o_ins < 32768 (align_packed_ok).  Same recurrence, same results as
+// align_run<16, 10> (tests/test_bsw_gpu.py).
+typedef uint16_t au16x2 __attribute__((ext_vector_type(2)));
+typedef int16_t ai16x2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ au16x2 AV(uint32_t x) { return __builtin_bit_cast(au16x2, x); }
+__device__ __forceinline__ ai16x2 AS(uint32_t x) { return __builtin_bit_cast(ai16x2, x); }
+__device__ __forceinline__ uint32_t AU(au16x2 x) { return __builtin_bit_cast(uint32_t, x); }
+__device__ __forceinline__ uint32_t AI(ai16x2 x) { return __builtin_bit_cast(uint32_t, x); }
+__device__ __forceinline__ uint32_t ap_maxu(uint32_t a, uint32_t b) {
+  return AU(__builtin_elementwise_max(AV(a), AV(b)));
+}
+__device__ __forceinline__ uint32_t ap_minu(uint32_t a, uint32_t b) {
+  return AU(__builtin_elementwise_min(AV(a), AV(b)));
+}
+__device__ __forceinline__ uint32_t ap_maxi(uint32_t a, uint32_t b) {
+  return AI(__builtin_elementwise_max(AS(a), AS(b)));
+}
+__device__ __forceinline__ uint32_t ap_add(uint32_t a, uint32_t b) { return AU(AV(a) + AV(b)); }
+__device__ __forceinline__ uint32_t ap_sub(uint32_t a, uint32_t b) { return AU(AV(a) - AV(b)); }
+__device__ __forceinline__ uint32_t ap_subs(uint32_t a, uint32_t b) {
+  return AU(__builtin_elementwise_sub_sat(AV(a), AV(b)));
+}
+
+__host__ __device__ inline int align_packed_big(int e_ins) { return 257 + 159 * e_ins; }
+__host__ __device__ inline bool align_packed_ok(int o_ins, int e_ins) {
+  return o_ins >= 0 && e_ins >= 0 && e_ins <= 200 && 16 * align_packed_big(e_ins) + o_ins + 1 < 32768;
+}
+
+template <class QAt, class TAt>
+__device__ AlignRun align_run_u8p(const BswParams& p, bool live, int qlen, QAt q_at, int tlen, TAt t_at, int shift,
+                                  int max_mat, int minsc, int endsc, uint32_t* __restrict__ blist) {
+  constexpr int W = 16, NK = 10, NP = 5;
+  const int gl = grp_lane<W>();
+  const int slen = (qlen + 15) / 16;
+  const int nlen = live ? slen * 16 : 0;
+  const int big = align_packed_big(p.e_ins);
+  // c1 / c2: the scan offsets; o1 / o2 = c + o_ins (f = ex - c - o_ins)
+  uint32_t H[NP], E[NP], Hm[NP], plo[NK], phi[NP], c1[NP], c2[NP], o1[NP], o2[NP], inm[NP];
+#pragma unroll
+  for (int j = 0; j < NP; ++j) {
+    uint32_t n2 = 0, a1 = 0, a2 = 0, b1 = 0, b2 = 0, im = 0;
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int k = j + 5 * h, x = gl * NK + k;
+      const int qb = (live && x < qlen) ? q_at(x) : -1;  // padding: score 0 against every base
+      auto sc = [&](int a) { return (uint32_t)(((qb < 0 ? 0 : (int)p.mat[a * 5 + qb]) + shift) & 0xFF); };
+      plo[k] = sc(0) | (sc(1) << 8) | (sc(2) << 16) | (sc(3) << 24);
+      const int cc2 = x * p.e_ins + 1;
+      const int cc1 = cc2 + (slen > 0 ? x / slen : 0) * big;
+      n2 |= sc(4) << (16 * h);
+      a1 |= (uint32_t)cc1 << (16 * h);
+      a2 |= (uint32_t)cc2 << (16 * h);
+      b1 |= (uint32_t)(cc1 + p.o_ins) << (16 * h);
+      b2 |= (uint32_t)(cc2 + p.o_ins) << (16 * h);
+      im |= (x < nlen ? 0xFFFFu : 0u) << (16 * h);
+    }
+    phi[j] = n2, c1[j] = a1, c2[j] = a2, o1[j] = b1, o2[j] = b2, inm[j] = im;
+    H[j] = E[j] = Hm[j] = 0;
+  }
+  const uint32_t SH = (uint32_t)shift * 0x10001u, MH = (uint32_t)(255 - shift) * 0x10001u;
+  const uint32_t ED = (uint32_t)p.e_del * 0x10001u, OED = (uint32_t)(p.o_del + p.e_del) * 0x10001u;
+#ifdef FCS_ALIGN_PK_NOO
+  const uint32_t OI = (uint32_t)p.o_ins * 0x10001u;
+#endif
+  int gmax = 0, te = -1, n_b = 0, last_i = -2, last_v = 0;
+  bool run = live && tlen > 0;
+  const int ncol = wave_max(run ? tlen : 0);
+  for (int i = 0; i < ncol; ++i) {
+    if (__ballot(run) == 0ull) break;
+    const bool act = run && i < tlen;
+    const int tb = act ? t_at(i) : 0;
+    // lo half: byte tb of plo[j]; hi half: byte tb of plo[j + 5]; zero-extended
+    const uint32_t sel = 0x0C000C00u | (uint32_t)tb | ((uint32_t)(tb + 4) << 16);
+    uint32_t sb[NP];
+#pragma unroll
+    for (int j = 0; j < NP; ++j) sb[j] = __builtin_amdgcn_perm(plo[j + 5], plo[j], sel);
+    if (__ballot(tb == 4) != 0ull) {  // an N in some group's target column: the per-position N scores
+      const bool isn = tb == 4;
+#pragma unroll
+      for (int j = 0; j < NP; ++j) sb[j] = isn ? phi[j] : sb[j];
+    }
+    // H(i - 1, x - 1): lo of pair 0 is the lane below's position 9 (hi of its
+    // pair 4; group lane 0: position -1, 0), hi of pair 0 this lane's position 4
+    const uint32_t hb = (uint32_t)grp_shr1<W>(0, (int)H[NP - 1]);
+    const uint32_t hd0 = __builtin_amdgcn_perm(H[NP - 1], hb, 0x05040302u);
+    uint32_t Mp[NP], r1[NP], r2[NP];
+#pragma unroll
+    for (int j = 0; j < NP; ++j) {
+      const uint32_t hd = j == 0 ? hd0 : H[j - 1];
+      const uint32_t m = ap_maxu(ap_minu(ap_subs(ap_add(hd, sb[j]), SH), MH), E[j]);
+      Mp[j] = m;
+      const uint32_t u1 = ap_add(m, c1[j]), u2 = ap_add(m, c2[j]);
+      r1[j] = j == 0 ? u1 : ap_maxu(r1[j - 1], u1);
+      r2[j] = j == 0 ? u2 : ap_maxu(r2[j - 1], u2);
+    }
+    // lane totals (lo: positions 0..4, hi: 5..9), group scan, carries per half
+    const int lo1 = (int)(r1[NP - 1] & 0xFFFF), lo2 = (int)(r2[NP - 1] & 0xFFFF);
+    const int t1 = max(lo1, (int)(r1[NP - 1] >> 16)), t2 = max(lo2, (int)(r2[NP - 1] >> 16));
+    const int ci1 = grp_shr1<W>(0, grp_incl_max<W>(t1, 0)), ci2 = grp_shr1<W>(0, grp_incl_max<W>(t2, 0));
+    const uint32_t C1 = (uint32_t)ci1 | ((uint32_t)max(ci1, lo1) << 16);
+    const uint32_t C2 = (uint32_t)ci2 | ((uint32_t)max(ci2, lo2) << 16);
+    uint32_t imp = 0, Hn[NP];
+#pragma unroll
+    for (int j = 0; j < NP; ++j) {
+      const uint32_t ex1 = j == 0 ? C1 : ap_maxu(C1, r1[j - 1]);
+      const uint32_t ex2 = j == 0 ? C2 : ap_maxu(C2, r2[j - 1]);
+#ifdef FCS_ALIGN_PK_NOO
+      const uint32_t h1 = ap_maxi(Mp[j], ap_sub(ap_sub(ex1, c1[j]), OI));
+      E[j] = ap_maxu(ap_subs(E[j], ED), ap_subs(h1, OED));
+      Hn[j] = ap_maxi(h1, ap_sub(ap_sub(ex2, c2[j]), OI));
+#else
+      const uint32_t h1 = ap_maxi(Mp[j], ap_sub(ex1, o1[j]));  // signed: ex1 - c1 - o_ins may be negative
+      E[j] = ap_maxu(ap_subs(E[j], ED), ap_subs(h1, OED));
+      Hn[j] = ap_maxi(h1, ap_sub(ex2, o2[j]));
+#endif
+      H[j] = Hn[j];
+      imp = ap_maxu(imp, h1 & inm[j]);
+    }
+    const int imax = grp_max<W>(max((int)(imp & 0xFFFF), (int)(imp >> 16)));
+    if (act && imax >= minsc) {
+      if (n_b == 0 || last_i + 1 != i) {
+        if (gl == 0) blist[n_b] = (uint32_t)imax << 16 | (uint32_t)i;
+        ++n_b;
+        last_i = i, last_v = imax;
+      } else if (last_v < imax) {
+        if (gl == 0) blist[n_b - 1] = (uint32_t)imax << 16 | (uint32_t)i;
+        last_i = i, last_v = imax;
+      }
+    }
+    if (act && imax > gmax) {
+      gmax = imax;
+      te = i;
+#pragma unroll
+      for (int j = 0; j < NP; ++j) Hm[j] = Hn[j];
+      if (gmax + shift >= 255 || gmax >= endsc) run = false;
+    }
+    if (!(i + 1 < tlen)) run = false;
+  }
+  AlignRun r{gmax + shift < 255 ? gmax : 255, te, -1, -1, -1};
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+  const bool tail = live && r.score != 255;
+  int mx = -1, qx = 0x7FFFFFFF;
+#pragma unroll
+  for (int j = 0; j < NP; ++j)
+#pragma unroll
+    for (int h = 0; h < 2; ++h)
+      if (gl * NK + j + 5 * h < nlen) mx = max(mx, (int)((Hm[j] >> (16 * h)) & 0xFFFF));
+  mx = grp_max<W>(mx);
+#pragma unroll
+  for (int j = 0; j < NP; ++j)
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int x = gl * NK + j + 5 * h;
+      if (x < nlen && (int)((Hm[j] >> (16 * h)) & 0xFFFF) == mx) qx = min(qx, x);
+    }
+  const int qe_min = -grp_max<W>(-qx);
+  const int qe_best = nlen > 0 ? qe_min : -1;
+  const int w = max_mat > 0 ? (r.score + max_mat - 1) / max_mat : 0;
+  const int low = te - w, high = te + w;
+  int best = -1, bte = -1;
+  const int nbl = tail ? n_b : 0;
+  const int nbmax = wave_max(nbl);
+  for (int j0 = 0; j0 < nbmax; j0 += W) {
+    const int j = j0 + gl;
+    if (j < nbl) {
+      const uint32_t e = blist[j];
+      const int c = (int)(e & 0xFFFF), v = (int)(e >> 16);
       if ((c < low || c > high) && v > best) best = v, bte = c;
     }
   }
@@ -241,17 +441,20 @@ __device__ AlignRun align_run(const BswParams& p, bool live, int qlen, QAt q_at,
 
 // Groups of W lanes run tasks: W = 64, one task per workgroup iteration; W =
 // 16, four consecutive tasks.  The 16-lane launch takes the queries up to
-// seg_q, the 64-lane launch the longer ones.  LDS per group: b[] (8 B per
-// target base) and the target.
-template <int W, int NK>
-__global__ __launch_bounds__(64) void bsw_align_kernel(const BswDevBatch b, const BswParams p,
+// seg_q, the 64-lane launch the longer ones.  LDS per group: b[] (2 B per
+// target base) and the target.  pk: 0 every task of the launch, 1 (the PK
+// kernel) the waves whose 16-lane tasks are all u8, 2 the other waves; both
+// launches see the same per-wave test.
+template <int W, int NK, bool PK>
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(PK ? FCS_ALIGN_PK_WAVES : 1))) void bsw_align_kernel(const BswDevBatch b, const BswParams p,
                                                        const int32_t* __restrict__ xtra, int32_t* __restrict__ out,
-                                                       int max_tlen, int seg_q) {
+                                                       int max_tlen, int seg_q, int pk) {
   extern __shared__ __align__(16) unsigned char smem[];
   constexpr int G = 64 / W;  // groups per wave
   const int grp = lane_id() / W, gl = grp_lane<W>();
-  uint64_t* const blist = reinterpret_cast<uint64_t*>(smem) + (size_t)grp * max_tlen;
-  uint8_t* const tl = smem + 8 * (size_t)G * max_tlen + (size_t)grp * max_tlen;
+  const size_t bcap = ((size_t)max_tlen + 1) / 2;  // b[] appends are >= 2 columns apart
+  uint32_t* const blist = reinterpret_cast<uint32_t*>(smem) + (size_t)grp * bcap;
+  uint8_t* const tl = smem + 4 * (size_t)G * bcap + (size_t)grp * max_tlen;
   // bwa's shift (u8 bias) and max_mat from the 5 x 5 matrix, as ksw_qinit
   int mn = 127, mxm = 0;
   for (int a = 0; a < 25; ++a) mn = min(mn, (int)p.mat[a]), mxm = max(mxm, (int)p.mat[a]);
@@ -261,7 +464,11 @@ __global__ __launch_bounds__(64) void bsw_align_kernel(const BswDevBatch b, cons
     const long long task = g * G + grp;
     int qlen = 0, tlen = 0, xt = 0;
     if (task < b.n) qlen = b.qlen[task], tlen = b.tlen[task], xt = xtra[task];
-    const bool mine = task < b.n && (W == 64 ? qlen > seg_q : qlen <= seg_q);
+    bool mine = task < b.n && (W == 64 ? qlen > seg_q : qlen <= seg_q);
+    if (pk != 0) {
+      const bool u8w = __ballot(mine && !(xt & kKswXByte)) == 0ull;
+      mine = mine && u8w == (pk == 1);
+    }
     const uint8_t* __restrict__ q = b.qbuf + (mine ? b.qoff[task] : 0);
     const uint8_t* __restrict__ tg = b.tbuf + (mine ? b.toff[task] : 0);
     if (mine)
@@ -270,17 +477,21 @@ __global__ __launch_bounds__(64) void bsw_align_kernel(const BswDevBatch b, cons
     const bool u8 = (xt & kKswXByte) != 0;
     const int minsc = (xt & kKswXSubo) ? xt & 0xffff : 0x10000;
     const int endsc = (xt & kKswXStop) ? xt & 0xffff : 0x10000;
-    AlignRun r = align_run<W, NK>(
-        p, mine, qlen, [&](int x) { return (int)q[x]; }, tlen, [&](int j) { return (int)tl[j]; }, u8, shift, mxm,
-        minsc, endsc, blist);
+    auto qf = [&](int x) { return (int)q[x]; };
+    auto tf = [&](int j) { return (int)tl[j]; };
+    AlignRun r;
+    if constexpr (PK) r = align_run_u8p(p, mine, qlen, qf, tlen, tf, shift, mxm, minsc, endsc, blist);
+    else r = align_run<W, NK>(p, mine, qlen, qf, tlen, tf, u8, shift, mxm, minsc, endsc, blist);
     __syncthreads();  // the first pass's b[] reads before the second pass (which appends nothing)
     // bwa: reverse query[0, qe] and target[0, te] in place (the rest of the
     // target unchanged, full tlen), stop at the first score, no b[] list
     const bool second = mine && (xt & kKswXStart) && !((xt & kKswXSubo) && r.score < (xt & 0xffff));
     const int qe = r.qe, te = r.te;
-    const AlignRun rr = align_run<W, NK>(
-        p, second, qe + 1, [&](int x) { return (int)q[qe - x]; }, tlen,
-        [&](int j) { return (int)tl[j <= te ? te - j : j]; }, u8, shift, mxm, 0x10000, r.score, blist);
+    auto qr = [&](int x) { return (int)q[qe - x]; };
+    auto tr = [&](int j) { return (int)tl[j <= te ? te - j : j]; };
+    AlignRun rr;
+    if constexpr (PK) rr = align_run_u8p(p, second, qe + 1, qr, tlen, tr, shift, mxm, 0x10000, r.score, blist);
+    else rr = align_run<W, NK>(p, second, qe + 1, qr, tlen, tr, u8, shift, mxm, 0x10000, r.score, blist);
     int tb = -1, qb = -1;
     if (second && rr.score == r.score) tb = r.te - rr.te, qb = r.qe - rr.qe;
     if (mine && gl == 0) {
@@ -292,7 +503,7 @@ __global__ __launch_bounds__(64) void bsw_align_kernel(const BswDevBatch b, cons
 }
 
 int launch_bsw_align(const BswDevBatch& b, const BswParams& p, const int32_t* xtra, int max_qlen, int max_tlen,
-                     int32_t* out, hipStream_t s) {
+                     int32_t* out, hipStream_t s, bool all_u8) {
   if (b.n <= 0) return FCS_OK;
   if (max_qlen > 1024) return fail(FCS_ERR_UNSUPPORTED, "[E::fcship] ksw_align2: qlen > 1024 unsupported");
   {  // the profile holds mat + shift as bytes (shift = -min, as bwa's u8 bias)
@@ -303,16 +514,20 @@ int launch_bsw_align(const BswDevBatch& b, const BswParams& p, const int32_t* xt
       return fail(FCS_ERR_UNSUPPORTED, "[E::fcship] ksw_align2: a scoring matrix without a negative entry is unsupported");
   }
   const int mt = std::max(max_tlen, 1);
-  // LDS per group: b[] + target = 9 B per target base.  Queries <= kAlignSegQ
+  // LDS per group: b[] + target = 3 B per target base (b[] entries: score << 16
+  // | column, 4 B; an append needs the last entry's column != i - 1, so at most
+  // ceil(tlen / 2) entries; scores <= 32767 and columns < 65536 fit 16 bits
+  // each).  Queries <= kAlignSegQ
   // run four tasks per wave in 16-lane groups (NK = 10: slen * p <= 160) while
   // four groups' areas fit the CU's 160 KB; longer queries, and every query
   // when the target windows are longer (mate rescue with wide insert-size
   // distributions), run one task per wave.
   constexpr size_t kLdsMax = 160 * 1024;
-  const size_t lds16 = 4 * 9 * (size_t)mt + 16, lds64 = 9 * (size_t)mt + 16;
+  const size_t per_group = 4 * (((size_t)mt + 1) / 2) + (size_t)mt;
+  const size_t lds16 = 4 * per_group + 16, lds64 = per_group + 16;
   if (lds64 > kLdsMax)
     return fail(FCS_ERR_UNSUPPORTED, "[E::fcship] ksw_align2: target longer than " +
-                                         std::to_string((kLdsMax - 16) / 9) + " bases unsupported");
+                                         std::to_string((kLdsMax - 18) / 3) + " bases unsupported");
   const bool seg = lds16 <= kLdsMax;
   const int seg_q = seg ? kAlignSegQ : -1;
   auto go = [&](const void* kern, unsigned grid, size_t lds, auto launch) -> int {
@@ -323,21 +538,35 @@ int launch_bsw_align(const BswDevBatch& b, const BswParams& p, const int32_t* xt
     return FCS_OK;
   };
   int rc = FCS_OK;
-  if (seg)
-    rc = go((const void*)bsw_align_kernel<16, 10>, (unsigned)std::min<long long>((b.n + 3) / 4, 4096), lds16,
-            [&](unsigned grid, size_t lds) {
-              hipLaunchKernelGGL((bsw_align_kernel<16, 10>), dim3(grid), dim3(64), lds, s, b, p, xtra, out, mt, seg_q);
-            });
+  // 16-lane tasks: the packed kernel takes the waves of u8 tasks (when the gap
+  // costs keep its 16-bit scan values in range), the 32-bit kernel the rest
+  // (skipped when the caller knows every task is u8)
+#ifdef FCS_ALIGN_NO_PK
+  const bool packed = false;
+#else
+  const bool packed = seg && align_packed_ok(p.o_ins, p.e_ins);
+#endif
+  const unsigned grid16 = (unsigned)std::min<long long>((b.n + 3) / 4, 4096);
+  if (packed)
+    rc = go((const void*)bsw_align_kernel<16, 10, true>, grid16, lds16, [&](unsigned grid, size_t lds) {
+      hipLaunchKernelGGL((bsw_align_kernel<16, 10, true>), dim3(grid), dim3(64), lds, s, b, p, xtra, out, mt, seg_q, 1);
+    });
+  if (rc == FCS_OK && seg && !(packed && all_u8))
+    rc = go((const void*)bsw_align_kernel<16, 10, false>, grid16, lds16, [&](unsigned grid, size_t lds) {
+      hipLaunchKernelGGL((bsw_align_kernel<16, 10, false>), dim3(grid), dim3(64), lds, s, b, p, xtra, out, mt, seg_q,
+                         packed ? 2 : 0);
+    });
   if (rc == FCS_OK && max_qlen > seg_q) {
     const unsigned grid = (unsigned)std::min<long long>(b.n, 4096);
     // slots of 64 positions for slen * p (p = 16 u8 / 8 i16: at most qlen + 15)
     if (max_qlen + 15 <= 256)
-      rc = go((const void*)bsw_align_kernel<64, 4>, grid, lds64, [&](unsigned g, size_t lds) {
-        hipLaunchKernelGGL((bsw_align_kernel<64, 4>), dim3(g), dim3(64), lds, s, b, p, xtra, out, mt, seg_q);
+      rc = go((const void*)bsw_align_kernel<64, 4, false>, grid, lds64, [&](unsigned g, size_t lds) {
+        hipLaunchKernelGGL((bsw_align_kernel<64, 4, false>), dim3(g), dim3(64), lds, s, b, p, xtra, out, mt, seg_q, 0);
       });
     else
-      rc = go((const void*)bsw_align_kernel<64, 17>, grid, lds64, [&](unsigned g, size_t lds) {
-        hipLaunchKernelGGL((bsw_align_kernel<64, 17>), dim3(g), dim3(64), lds, s, b, p, xtra, out, mt, seg_q);
+      rc = go((const void*)bsw_align_kernel<64, 17, false>, grid, lds64, [&](unsigned g, size_t lds) {
+        hipLaunchKernelGGL((bsw_align_kernel<64, 17, false>), dim3(g), dim3(64), lds, s, b, p, xtra, out, mt, seg_q,
+                           0);
       });
   }
   return rc;

@@ -1477,7 +1477,10 @@ int fcs_bsw_align(const fcs_bsw_task* tasks, int32_t n, const fcs_bsw_params* pa
   d.toff = S->d<int64_t>(oto);
   d.tlen = S->d<int32_t>(otl);
   d.n = n;
-  if ((rc = launch_bsw_align(d, to_params(params), S->d<int32_t>(ox), mq, mt, S->d<int32_t>(oo), s))) return rc;
+  bool all_u8 = true;
+  for (int32_t k = 0; k < n; ++k) all_u8 = all_u8 && (xtra[k] & FCS_KSW_XBYTE);
+  if ((rc = launch_bsw_align(d, to_params(params), S->d<int32_t>(ox), mq, mt, S->d<int32_t>(oo), s, all_u8)))
+    return rc;
   FCS_HIP_CHECK(hipMemcpyAsync(S->h<void>(oo), S->d<void>(oo), sizeof(fcs_kswr) * nn, hipMemcpyDeviceToHost, s));
   FCS_HIP_CHECK(hipStreamSynchronize(s));
   std::memcpy(out, S->h<void>(oo), sizeof(fcs_kswr) * nn);
@@ -1505,7 +1508,7 @@ int fcs_bsw_align_dev(const fcs_bsw_batch* b, const fcs_bsw_params* params, cons
   d.w = b->w;
   d.n = b->n;
   return launch_bsw_align(d, to_params(params), dev_xtra, std::max(b->max_qlen, 1), std::max(b->max_tlen, 1),
-                          reinterpret_cast<int32_t*>(dev_out), (hipStream_t)stream);
+                          reinterpret_cast<int32_t*>(dev_out), (hipStream_t)stream, false);
 }
 
 fcs_kswr fcs_ksw_align2(int qlen, const uint8_t* query, int tlen, const uint8_t* target, int m, const int8_t* mat,

@@ -45,6 +45,10 @@ enum : int {
   kDppRowShr2 = 0x112,
   kDppRowShr4 = 0x114,
   kDppRowShr8 = 0x118,
+  kDppRowRor1 = 0x121,
+  kDppRowRor2 = 0x122,
+  kDppRowRor4 = 0x124,
+  kDppRowRor8 = 0x128,
   kDppWaveShr1 = 0x138,
   kDppRowBcast15 = 0x142,
   kDppRowBcast31 = 0x143,
@@ -235,8 +239,9 @@ int launch_bsw_extend_sorted(const BswDevBatch& b, const BswParams& p, int max_q
 // Wave-per-task kernel over sorted positions [bounds[kBswWideBucket], bounds[kBswWideBucket + 1]).
 int launch_bsw_extend_wide(const BswDevBatch& b, const BswParams& p, int max_qlen, int max_tlen, int32_t* res,
                            int64_t* cells, const int32_t* order, const int64_t* bounds, hipStream_t s);
+// all_u8: the caller knows every xtra has KSW_XBYTE (skips the 32-bit 16-lane launch)
 int launch_bsw_align(const BswDevBatch& b, const BswParams& p, const int32_t* xtra, int max_qlen, int max_tlen,
-                     int32_t* out, hipStream_t s);
+                     int32_t* out, hipStream_t s, bool all_u8);
 int launch_bsw_global(const BswDevBatch& b, const BswParams& p, int max_qlen, int max_tlen, int32_t* scores,
                       uint8_t* zbuf, int64_t zbytes, const int64_t* zoff, uint32_t* cigar, const int64_t* cigar_off,
                       const int32_t* cigar_cap, int32_t* n_cigar, hipStream_t s);

@@ -434,12 +434,13 @@ def test_ksw_align2_empty_and_tiny(gpu):
             assert tuple(got[k]) == oracle_lib.ksw_align2(q, tg, m, x), (hex(x), k, len(q), len(tg))
 
 
-@pytest.mark.parametrize("tlen", [2000, 5000])
+@pytest.mark.parametrize("tlen", [2000, 5000, 16000])
 def test_ksw_align2_long_windows(gpu, tlen):
-    """Mate-rescue windows of wide insert-size distributions: at 2,000 bases
-    the four 16-lane groups' LDS (b[] + target) exceeds the 64 KB default and
-    the launch raises the limit; at 5,000 it exceeds the CU's 160 KB and every
-    task runs one per wave.  Both against the restatement."""
+    """Mate-rescue windows of wide insert-size distributions: at 2,000 and
+    5,000 bases the four 16-lane groups' LDS (b[] + target, 3 B per base)
+    exceeds the 64 KB default and the launch raises the limit; at 16,000 it
+    exceeds the CU's 160 KB and every task runs one per wave.  All against the
+    restatement."""
     t = align_tasks(44 + tlen, 24, qmin=60, qmax=200, tmin=tlen // 2, tmax=tlen)
     m = fcship.default_mat()
     x = fcship.KSW_XSUBO | fcship.KSW_XSTART | fcship.KSW_XBYTE | 19
