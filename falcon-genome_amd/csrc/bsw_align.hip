@@ -42,6 +42,9 @@ namespace fcs {
 constexpr int kKswXByte = 0x10000, kKswXStop = 0x20000, kKswXSubo = 0x40000, kKswXStart = 0x80000;
 constexpr int kBlockBig = 1 << 20;  // > the range of one block's scan values; block ids < 16
 constexpr int kAlignSegQ = 160;
+#ifndef FCS_ALIGN_GRID_CAP
+#define FCS_ALIGN_GRID_CAP (1 << 20)
+#endif
 #ifndef FCS_ALIGN_PK_WAVES
 #define FCS_ALIGN_PK_WAVES 1  // the packed kernel's occupancy target (A/B: tools/build_alt.sh)
 #endif      // longest query of the 16-lane groups (NK = 10 slots)
@@ -546,7 +549,9 @@ int launch_bsw_align(const BswDevBatch& b, const BswParams& p, const int32_t* xt
 #else
   const bool packed = seg && align_packed_ok(p.o_ins, p.e_ins);
 #endif
-  const unsigned grid16 = (unsigned)std::min<long long>((b.n + 3) / 4, 4096);
+  // one workgroup per four tasks (per task for W = 64): the dispatcher
+  // balances the uneven task lengths and early exits
+  const unsigned grid16 = (unsigned)std::min<long long>((b.n + 3) / 4, FCS_ALIGN_GRID_CAP);
   if (packed)
     rc = go((const void*)bsw_align_kernel<16, 10, true>, grid16, lds16, [&](unsigned grid, size_t lds) {
       hipLaunchKernelGGL((bsw_align_kernel<16, 10, true>), dim3(grid), dim3(64), lds, s, b, p, xtra, out, mt, seg_q, 1);
@@ -557,7 +562,7 @@ int launch_bsw_align(const BswDevBatch& b, const BswParams& p, const int32_t* xt
                          packed ? 2 : 0);
     });
   if (rc == FCS_OK && max_qlen > seg_q) {
-    const unsigned grid = (unsigned)std::min<long long>(b.n, 4096);
+    const unsigned grid = (unsigned)std::min<long long>(b.n, FCS_ALIGN_GRID_CAP);
     // slots of 64 positions for slen * p (p = 16 u8 / 8 i16: at most qlen + 15)
     if (max_qlen + 15 <= 256)
       rc = go((const void*)bsw_align_kernel<64, 4, false>, grid, lds64, [&](unsigned g, size_t lds) {
