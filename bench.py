@@ -917,9 +917,10 @@ def main():
                         "XSTART | XBYTE | 19",
             "tasks": ga["tasks"], "ms": round(ga["ms"], 3), "gcups": round(ga["gcups"], 3),
             "cells": ga["cells"], "cells_first_pass": ga["cells_first"],
-            "kernel": "bsw_align_kernel<16, 10> (four tasks per wave in 16-lane groups, lane l holding query "
-                      "positions 10 l .. 10 l + 9; bwa's striped-F semantics by register running-max scans plus one "
-                      "row scan; both passes in one launch)"}
+            "kernel": "bsw_align_kernel<16, 10, true> (u8 tasks: four per wave in 16-lane groups, lane l holding "
+                      "query positions 10 l .. 10 l + 9 as five packed 16-bit pairs; bwa's striped-F semantics by "
+                      "register running-max scans plus one row scan; both passes in one launch; the 32-bit "
+                      "<16, 10, false> launch of the device entry point finds no i16 wave and exits)"}
         am = {}
         try:
             am = json.load(open(os.path.join(ROOT, "profiles", "pmc_bsw.json"))).get("align", {})
