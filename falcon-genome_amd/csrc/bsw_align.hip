@@ -41,13 +41,8 @@ namespace fcs {
 
 constexpr int kKswXByte = 0x10000, kKswXStop = 0x20000, kKswXSubo = 0x40000, kKswXStart = 0x80000;
 constexpr int kBlockBig = 1 << 20;  // > the range of one block's scan values; block ids < 16
-constexpr int kAlignSegQ = 160;
-#ifndef FCS_ALIGN_GRID_CAP
-#define FCS_ALIGN_GRID_CAP (1 << 20)
-#endif
-#ifndef FCS_ALIGN_PK_WAVES
-#define FCS_ALIGN_PK_WAVES 1  // the packed kernel's occupancy target (A/B: tools/build_alt.sh)
-#endif      // longest query of the 16-lane groups (NK = 10 slots)
+constexpr int kAlignSegQ = 160;                // longest query of the 16-lane groups (NK = 10 slots)
+constexpr long long kAlignGridCap = 1 << 20;  // workgroups per launch (they stride beyond)
 
 // Group-level primitives: W = 16 (a DPP row) or 64 (the wave).
 template <int W>
@@ -324,9 +319,6 @@ __device__ AlignRun align_run_u8p(const BswParams& p, bool live, int qlen, QAt q
   }
   const uint32_t SH = (uint32_t)shift * 0x10001u, MH = (uint32_t)(255 - shift) * 0x10001u;
   const uint32_t ED = (uint32_t)p.e_del * 0x10001u, OED = (uint32_t)(p.o_del + p.e_del) * 0x10001u;
-#ifdef FCS_ALIGN_PK_NOO
-  const uint32_t OI = (uint32_t)p.o_ins * 0x10001u;
-#endif
   int gmax = 0, te = -1, n_b = 0, last_i = -2, last_v = 0;
   bool run = live && tlen > 0;
   const int ncol = wave_max(run ? tlen : 0);
@@ -369,15 +361,9 @@ __device__ AlignRun align_run_u8p(const BswParams& p, bool live, int qlen, QAt q
     for (int j = 0; j < NP; ++j) {
       const uint32_t ex1 = j == 0 ? C1 : ap_maxu(C1, r1[j - 1]);
       const uint32_t ex2 = j == 0 ? C2 : ap_maxu(C2, r2[j - 1]);
-#ifdef FCS_ALIGN_PK_NOO
-      const uint32_t h1 = ap_maxi(Mp[j], ap_sub(ap_sub(ex1, c1[j]), OI));
-      E[j] = ap_maxu(ap_subs(E[j], ED), ap_subs(h1, OED));
-      Hn[j] = ap_maxi(h1, ap_sub(ap_sub(ex2, c2[j]), OI));
-#else
       const uint32_t h1 = ap_maxi(Mp[j], ap_sub(ex1, o1[j]));  // signed: ex1 - c1 - o_ins may be negative
       E[j] = ap_maxu(ap_subs(E[j], ED), ap_subs(h1, OED));
       Hn[j] = ap_maxi(h1, ap_sub(ex2, o2[j]));
-#endif
       H[j] = Hn[j];
       imp = ap_maxu(imp, h1 & inm[j]);
     }
@@ -449,7 +435,7 @@ __device__ AlignRun align_run_u8p(const BswParams& p, bool live, int qlen, QAt q
 // kernel) the waves whose 16-lane tasks are all u8, 2 the other waves; both
 // launches see the same per-wave test.
 template <int W, int NK, bool PK>
-__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(PK ? FCS_ALIGN_PK_WAVES : 1))) void bsw_align_kernel(const BswDevBatch b, const BswParams p,
+__global__ __launch_bounds__(64) void bsw_align_kernel(const BswDevBatch b, const BswParams p,
                                                        const int32_t* __restrict__ xtra, int32_t* __restrict__ out,
                                                        int max_tlen, int seg_q, int pk) {
   extern __shared__ __align__(16) unsigned char smem[];
@@ -544,14 +530,10 @@ int launch_bsw_align(const BswDevBatch& b, const BswParams& p, const int32_t* xt
   // 16-lane tasks: the packed kernel takes the waves of u8 tasks (when the gap
   // costs keep its 16-bit scan values in range), the 32-bit kernel the rest
   // (skipped when the caller knows every task is u8)
-#ifdef FCS_ALIGN_NO_PK
-  const bool packed = false;
-#else
   const bool packed = seg && align_packed_ok(p.o_ins, p.e_ins);
-#endif
   // one workgroup per four tasks (per task for W = 64): the dispatcher
   // balances the uneven task lengths and early exits
-  const unsigned grid16 = (unsigned)std::min<long long>((b.n + 3) / 4, FCS_ALIGN_GRID_CAP);
+  const unsigned grid16 = (unsigned)std::min<long long>((b.n + 3) / 4, kAlignGridCap);
   if (packed)
     rc = go((const void*)bsw_align_kernel<16, 10, true>, grid16, lds16, [&](unsigned grid, size_t lds) {
       hipLaunchKernelGGL((bsw_align_kernel<16, 10, true>), dim3(grid), dim3(64), lds, s, b, p, xtra, out, mt, seg_q, 1);
@@ -562,7 +544,7 @@ int launch_bsw_align(const BswDevBatch& b, const BswParams& p, const int32_t* xt
                          packed ? 2 : 0);
     });
   if (rc == FCS_OK && max_qlen > seg_q) {
-    const unsigned grid = (unsigned)std::min<long long>(b.n, FCS_ALIGN_GRID_CAP);
+    const unsigned grid = (unsigned)std::min<long long>(b.n, kAlignGridCap);
     // slots of 64 positions for slen * p (p = 16 u8 / 8 i16: at most qlen + 15)
     if (max_qlen + 15 <= 256)
       rc = go((const void*)bsw_align_kernel<64, 4, false>, grid, lds64, [&](unsigned g, size_t lds) {
