@@ -228,7 +228,9 @@ int fcs_bsw_extend_multi(const fcs_bsw_task* tasks, int32_t n, const fcs_bsw_par
 
 /* Packed structure-of-arrays extension batch (device or host pointers
  * depending on the entry point).  Task k: query bytes
- * qbuf[qoff[k] .. +qlen[k]), target bytes tbuf[toff[k] .. +tlen[k]). */
+ * qbuf[qoff[k] .. +qlen[k]), target bytes tbuf[toff[k] .. +tlen[k]).
+ * max_qlen / max_tlen must bound every qlen / tlen (they size on-chip and
+ * scratch buffers). */
 typedef struct {
   const uint8_t* qbuf;
   const int64_t* qoff;
