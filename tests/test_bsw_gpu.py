@@ -389,6 +389,24 @@ def test_ksw_align2_batch_bit_exact(gpu, xbyte):
         assert tuple(got[k]) == ref, f"task {k} (qlen {len(q)}, tlen {len(tg)}): {tuple(got[k])} != {ref}"
 
 
+@pytest.mark.parametrize("gaps", [(6, 1, 6, 1), (4, 2, 9, 3), (1, 3, 0, 11), (5, 1, 2, 12), (12, 4, 16, 7)])
+def test_ksw_align2_gap_costs(gpu, gaps):
+    """Gap costs across the packed u8 kernel's range (its 16-bit scan values
+    need 16 (257 + 159 e_ins) + o_ins < 32768: e_ins <= 11) and past it
+    (e_ins = 12 takes the 32-bit kernel), in one batch mixing u8 and i16
+    tasks, so both 16-lane launches run, each on its own waves."""
+    o_del, e_del, o_ins, e_ins = gaps
+    t = align_tasks(90 + e_ins, 160, qmax=160)
+    m = fcship.default_mat()
+    xs = np.array([fcship.KSW_XSUBO | fcship.KSW_XSTART | (fcship.KSW_XBYTE if k % 3 else 0) | 19
+                   for k in range(t.n)], np.int32)
+    got = fcship.bsw_align(t, xs, fcship.bsw_params(o_del=o_del, e_del=e_del, o_ins=o_ins, e_ins=e_ins))
+    for k in range(t.n):
+        q, tg, _, _ = t.task(k)
+        ref = oracle_lib.ksw_align2(q, tg, m, int(xs[k]), o_del, e_del, o_ins, e_ins)
+        assert tuple(got[k]) == ref, f"task {k} (qlen {len(q)}, tlen {len(tg)}): {tuple(got[k])} != {ref}"
+
+
 @pytest.mark.parametrize("xbyte", [True, False])
 def test_ksw_align2_low_complexity_ties(gpu, xbyte):
     """Tandem repeats and homopolymers: many positions share a column's
