@@ -79,10 +79,12 @@ __device__ __forceinline__ int grp_max(int v) {
   if constexpr (W == 64) {
     return grp_last<W>(grp_incl_max<W>(v, INT32_MIN));
   } else {
-    v = max(v, __builtin_amdgcn_update_dpp(v, v, kDppRowRor8, 0xF, 0xF, false));
-    v = max(v, __builtin_amdgcn_update_dpp(v, v, kDppRowRor4, 0xF, 0xF, false));
-    v = max(v, __builtin_amdgcn_update_dpp(v, v, kDppRowRor2, 0xF, 0xF, false));
-    v = max(v, __builtin_amdgcn_update_dpp(v, v, kDppRowRor1, 0xF, 0xF, false));
+    // (every lane has a source, so old = 0 with bound_ctrl is never used; that
+    // form folds into v_max_i32_dpp)
+    v = max(v, __builtin_amdgcn_update_dpp(0, v, kDppRowRor8, 0xF, 0xF, true));
+    v = max(v, __builtin_amdgcn_update_dpp(0, v, kDppRowRor4, 0xF, 0xF, true));
+    v = max(v, __builtin_amdgcn_update_dpp(0, v, kDppRowRor2, 0xF, 0xF, true));
+    v = max(v, __builtin_amdgcn_update_dpp(0, v, kDppRowRor1, 0xF, 0xF, true));
     return v;
   }
 }
@@ -294,30 +296,35 @@ __device__ AlignRun align_run_u8p(const BswParams& p, bool live, int qlen, QAt q
   const int slen = (qlen + 15) / 16;
   const int nlen = live ? slen * 16 : 0;
   const int big = align_packed_big(p.e_ins);
-  // c1 / c2: the scan offsets; o1 / o2 = c + o_ins (f = ex - c - o_ins)
-  uint32_t H[NP], E[NP], Hm[NP], plo[NK], phi[NP], c1[NP], c2[NP], o1[NP], o2[NP], inm[NP];
+  // c1 / c2: the scan offsets; o1 / o2 = c + o_ins (f = ex - c - o_ins).
+  // Positions past nlen (the group's last lanes, when slen < 10) feed only
+  // later such positions; mh = 0 there (M = 0), no block term in c1 (so every
+  // scan value stays below 2^15) and o1 = o2 = 0x7FFF (both F's <= 0) keep
+  // their H and E at 0, so they drop out of the column maximum without a mask.
+  uint32_t H[NP], E[NP], Hm[NP], plo[NK], phi[NP], c1[NP], c2[NP], o1[NP], o2[NP], mh[NP];
 #pragma unroll
   for (int j = 0; j < NP; ++j) {
-    uint32_t n2 = 0, a1 = 0, a2 = 0, b1 = 0, b2 = 0, im = 0;
+    uint32_t n2 = 0, a1 = 0, a2 = 0, b1 = 0, b2 = 0, m2 = 0;
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
       const int k = j + 5 * h, x = gl * NK + k;
       const int qb = (live && x < qlen) ? q_at(x) : -1;  // padding: score 0 against every base
       auto sc = [&](int a) { return (uint32_t)(((qb < 0 ? 0 : (int)p.mat[a * 5 + qb]) + shift) & 0xFF); };
       plo[k] = sc(0) | (sc(1) << 8) | (sc(2) << 16) | (sc(3) << 24);
+      const bool in = x < nlen;
       const int cc2 = x * p.e_ins + 1;
-      const int cc1 = cc2 + (slen > 0 ? x / slen : 0) * big;
+      const int cc1 = in ? cc2 + (x / slen) * big : cc2;  // block ids < 16 inside nlen only
       n2 |= sc(4) << (16 * h);
       a1 |= (uint32_t)cc1 << (16 * h);
       a2 |= (uint32_t)cc2 << (16 * h);
-      b1 |= (uint32_t)(cc1 + p.o_ins) << (16 * h);
-      b2 |= (uint32_t)(cc2 + p.o_ins) << (16 * h);
-      im |= (x < nlen ? 0xFFFFu : 0u) << (16 * h);
+      b1 |= (uint32_t)(in ? cc1 + p.o_ins : 0x7FFF) << (16 * h);
+      b2 |= (uint32_t)(in ? cc2 + p.o_ins : 0x7FFF) << (16 * h);
+      m2 |= (uint32_t)(in ? 255 - shift : 0) << (16 * h);
     }
-    phi[j] = n2, c1[j] = a1, c2[j] = a2, o1[j] = b1, o2[j] = b2, inm[j] = im;
+    phi[j] = n2, c1[j] = a1, c2[j] = a2, o1[j] = b1, o2[j] = b2, mh[j] = m2;
     H[j] = E[j] = Hm[j] = 0;
   }
-  const uint32_t SH = (uint32_t)shift * 0x10001u, MH = (uint32_t)(255 - shift) * 0x10001u;
+  const uint32_t SH = (uint32_t)shift * 0x10001u;
   const uint32_t ED = (uint32_t)p.e_del * 0x10001u, OED = (uint32_t)(p.o_del + p.e_del) * 0x10001u;
   int gmax = 0, te = -1, n_b = 0, last_i = -2, last_v = 0;
   bool run = live && tlen > 0;
@@ -344,7 +351,7 @@ __device__ AlignRun align_run_u8p(const BswParams& p, bool live, int qlen, QAt q
 #pragma unroll
     for (int j = 0; j < NP; ++j) {
       const uint32_t hd = j == 0 ? hd0 : H[j - 1];
-      const uint32_t m = ap_maxu(ap_minu(ap_subs(ap_add(hd, sb[j]), SH), MH), E[j]);
+      const uint32_t m = ap_maxu(ap_minu(ap_subs(ap_add(hd, sb[j]), SH), mh[j]), E[j]);
       Mp[j] = m;
       const uint32_t u1 = ap_add(m, c1[j]), u2 = ap_add(m, c2[j]);
       r1[j] = j == 0 ? u1 : ap_maxu(r1[j - 1], u1);
@@ -365,7 +372,7 @@ __device__ AlignRun align_run_u8p(const BswParams& p, bool live, int qlen, QAt q
       E[j] = ap_maxu(ap_subs(E[j], ED), ap_subs(h1, OED));
       Hn[j] = ap_maxi(h1, ap_sub(ex2, o2[j]));
       H[j] = Hn[j];
-      imp = ap_maxu(imp, h1 & inm[j]);
+      imp = ap_maxu(imp, h1);
     }
     const int imax = grp_max<W>(max((int)(imp & 0xFFFF), (int)(imp >> 16)));
     if (act && imax >= minsc) {
