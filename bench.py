@@ -284,32 +284,33 @@ def vcf_calls(path):
     return out
 
 
-def htc_cpu_baseline(exe, env, work, ref, bam, gpu_out, modes=("gkl", "java"), vcf=False, tag="c4"):
-    """`fcs-genome htc` with the PairHMM on the host CPU (BASELINE.json
-    configs[0]'s path: GATK HaplotypeCaller with --native-pair-hmm-threads,
-    /root/reference/src/workers/HTCWorker.cpp:85,105), same command, genome and
-    shard threads as the GPU run: gkl = GKL's AVX-512 float PairHMM with the
-    double rescue restated, java = GATK's Java LoglessPairHMM (double).  Calls
-    compared with the GPU run's output."""
+def caller_cpu_baseline(exe, env, work, cmd, gpu_out, modes=("gkl", "java"), tag="c4", ext=".g.vcf"):
+    """An `fcs-genome htc` / `mutect2` command with the PairHMM on the host
+    CPU: the reference's CPU path (GATK HaplotypeCaller / Mutect2 with
+    --native-pair-hmm-threads, /root/reference/src/workers/HTCWorker.cpp:85,105,
+    Mutect2Worker.cpp:109-192), same command, genome and shard threads as the
+    GPU run: gkl = GKL's AVX-512 float PairHMM with the double rescue restated,
+    java = GATK's Java LoglessPairHMM (double).  cmd(out_path) gives the
+    arguments.  Calls compared with the GPU run's output."""
+    import shutil
     import subprocess
     cenv = cpu_mock_env(env)
     gpu_calls = vcf_calls(gpu_out)
     res = {}
     for m in modes:
-        import shutil
-        o = os.path.join(work, f"htc_cpu_{tag}_{m}" + (".vcf" if vcf else ".g.vcf"))
+        o = os.path.join(work, f"cpu_{tag}_{m}{ext}")
         logd = os.path.join(work, f"log_cpu_{tag}_{m}")
         shutil.rmtree(logd, ignore_errors=True)
         e = dict(cenv, FCS_MOCK_PHMM=m, FCS_LOG_DIR=logd)
         t0 = time.perf_counter()
-        r = subprocess.run([exe, "htc", "-f", "-r", ref, "-i", bam, "-o", o] + (["-v"] if vcf else []),
-                           env=e, capture_output=True, text=True, cwd=work)
+        r = subprocess.run([exe, *cmd(o)], env=e, capture_output=True, text=True, cwd=work)
         dt = time.perf_counter() - t0
         if r.returncode != 0:
-            raise RuntimeError(f"CPU-path htc ({m}) failed ({r.returncode}): {r.stderr[-2000:]}")
+            raise RuntimeError(f"CPU-path {tag} ({m}) failed ({r.returncode}): {r.stderr[-2000:]}")
         logs = "".join(open(os.path.join(logd, f)).read() for f in os.listdir(logd) if ".part-" not in f)
         st = shard_stats(logs, dt)
-        for k in ("phmm_device_seconds", "rescue_fp64_device_seconds", "gpu_busy_frac", "device_passes"):
+        for k in ("phmm_device_seconds", "rescue_fp64_device_seconds", "gpu_busy_frac", "device_passes",
+                  "phmm_device_tcups"):
             st.pop(k, None)
         c = vcf_calls(o)
         st.update(kind="port", cores=int(env.get("FCS_GATK_NPROCS", "16")),
@@ -321,6 +322,130 @@ def htc_cpu_baseline(exe, env, work, ref, bam, gpu_out, modes=("gkl", "java"), v
                   calls_only_gpu=len(gpu_calls - c), calls_only_cpu=len(c - gpu_calls))
         res[m] = st
     return res
+
+
+def htc_cpu_baseline(exe, env, work, ref, bam, gpu_out, modes=("gkl", "java"), vcf=False, tag="c4"):
+    """`fcs-genome htc` on the reference's CPU PairHMM path (caller_cpu_baseline)."""
+    return caller_cpu_baseline(exe, env, work, lambda o: ["htc", "-f", "-r", ref, "-i", bam, "-o", o] +
+                               (["-v"] if vcf else []), gpu_out, modes, tag, ".vcf" if vcf else ".g.vcf")
+
+
+def damage_mates(fastq, every=25, offset=7):
+    """A mismatch every 16 bases in every `every`-th read of `fastq` (4% at
+    25): no 19-mer seed survives in them, so only the mate rescue (bwa
+    mem_matesw, the GPU ksw_align2) can place them.  Returns how many."""
+    flip = {"A": "C", "C": "G", "G": "T", "T": "A", "N": "A"}
+    lines = open(fastq).read().split("\n")
+    n = 0
+    for i in range(0, len(lines) - 3, 4):
+        if (i // 4) % every == offset:
+            seq = list(lines[i + 1])
+            for j in range(5, len(seq), 16):
+                seq[j] = flip[seq[j]]
+            lines[i + 1] = "".join(seq)
+            n += 1
+    open(fastq, "w").write("\n".join(lines))
+    return n
+
+
+def bam_payload(path):
+    """The decompressed bytes of a BAM (BGZF blocks are gzip members): equal
+    payloads mean the same header and the same records in the same order."""
+    import gzip
+    return gzip.decompress(open(path, "rb").read())
+
+
+def align_cpu_baseline(exe, env, work, cmd, gpu_bam, threads):
+    """`fcs-genome align` with the banded Smith-Waterman on the host CPU: the
+    reference's `bwa-flow mem` without --use_fpga
+    (/root/reference/src/workers/BWAWorker.cpp:134-166), i.e. bwa's scalar
+    ksw_extend2 / ksw_global2 and its SSE2 striped ksw_align2 (restated in
+    oracle/ksw_oracle.c, oracle/ksw_align_sse.c) on `threads` OpenMP threads
+    per batch, the same binary, seeding, pairing and output around them.  The
+    BAM must equal the GPU run's."""
+    import subprocess
+    out = os.path.join(work, "aln_cpu.bam")
+    e = dict(cpu_mock_env(env), FCS_MOCK_BSW_THREADS=str(threads))
+    t0 = time.perf_counter()
+    r = subprocess.run([exe, *cmd(out)], env=e, capture_output=True, text=True, cwd=work)
+    dt = time.perf_counter() - t0
+    if r.returncode != 0:
+        raise RuntimeError(f"CPU-path align failed ({r.returncode}): {r.stderr[-2000:]}")
+    rep = align_report(r.stderr)
+    return {"seconds": round(dt, 3), "reads_per_s": round(rep["reads"] / dt, 1), "kind": "port", "cores": threads,
+            "sw": "bwa's ksw_extend2 / ksw_global2 (scalar C, as bwa's) and ksw_align2 (SSE2 striped, 16 x u8 / "
+                  "8 x i16 lanes, as bwa's) restated, OpenMP over each batch's tasks",
+            "sw_call_seconds": rep["gpu_call_seconds"], "thread_seconds": rep["thread_seconds"],
+            "mates_rescued": rep["mates_rescued"],
+            "bam_equal_to_gpu": bam_payload(out) == bam_payload(gpu_bam)}
+
+
+def align_report(err):
+    """The counters and phase times `fcs-genome align` prints."""
+    import re
+    m = re.search(r"(\d+) reads, (\d+) mapped, (\d+) supplementary, (\d+) extension tasks, (\d+) global "
+                  r"alignments, ([\d.]+) s \(GPU calls ([\d.]+) s\)", err)
+    pm = re.search(r"(\d+) reads properly paired, (\d+) mates rescued, insert ([\d.]+) \+- ([\d.]+)", err)
+    ph = re.search(r"alignment thread-seconds ([\d.]+): seeding ([\d.]+), extension ([\d.]+), pairing ([\d.]+), "
+                   r"records ([\d.]+)", err)
+    wp = re.search(r"phases: reference ([\d.e-]+) s, FMD index ([\d.e-]+) s .*FASTQ \+ alignment ([\d.e-]+) s .*"
+                   r"sort \+ BAM \+ index ([\d.e-]+) s", err)
+    if not (m and pm and ph and wp):
+        raise RuntimeError("fcs-genome align report not understood: " + err[-2000:])
+    return {"reads": int(m.group(1)), "mapped": int(m.group(2)), "supplementary": int(m.group(3)),
+            "ext_tasks": int(m.group(4)), "global_tasks": int(m.group(5)), "gpu_call_seconds": float(m.group(7)),
+            "thread_seconds": {k: float(ph.group(i + 1)) for i, k in
+                               enumerate(("total", "seeding", "extension", "pairing", "records"))},
+            "wall_phases_seconds": {k: float(wp.group(i + 1)) for i, k in
+                                    enumerate(("reference", "fmd_index", "fastq_and_alignment", "sort_bam_index"))},
+            "proper_pair_reads": int(pm.group(1)), "mates_rescued": int(pm.group(2))}
+
+
+def bench_c4(exe, env, work, mbp, n_dev, seed, nprocs, reps=1):
+    """BASELINE.json configs[3] (C4) as the reference runs it: ONE
+    `fcs-genome htc` job over a 30x chr1-like genome (mbp Mbp; 248 is chr1),
+    its gatk.ncontigs = 32 interval shards in one stage
+    (/root/reference/src/worker-htc.cpp:113-145, the shard unit of
+    src/config.cpp:470-509) dealt round-robin to the GPU slots 0..n_dev-1
+    (gpu.devices[job_id % n], the host round-robin of src/Executor.cpp:262),
+    nprocs shard threads.  Returns the shard statistics, wall time and the
+    per-device pass counts."""
+    import re
+    import shutil
+    import subprocess
+    d = os.path.join(work, "c4")
+    t0 = time.perf_counter()
+    subprocess.run([exe, "synth", "-o", d, "-c", f"chr1:{int(mbp * 1e6)}", "-x", "30", "--no-fastq", "--noisy-frac",
+                    "0.01", "--seed", str(seed)], env=env, check=True, capture_output=True)
+    synth_s = time.perf_counter() - t0
+    logd = os.path.join(work, "log_c4")
+    e = dict(env, FCS_GPU_DEVICES=",".join(str(i) for i in range(n_dev)), FCS_LOG_DIR=logd,
+             FCS_GATK_NPROCS=str(nprocs))
+    runs = []
+    for _ in range(max(1, reps)):
+        shutil.rmtree(logd, ignore_errors=True)
+        t0 = time.perf_counter()
+        r = subprocess.run([exe, "htc", "-f", "-r", d + "/ref.fasta", "-i", d + "/sample.bam", "-o",
+                            work + "/c4.g.vcf"], env=e, capture_output=True, text=True, cwd=work)
+        dt = time.perf_counter() - t0
+        if r.returncode != 0:
+            raise RuntimeError(f"C4 htc failed ({r.returncode}): {r.stderr[-2000:]}")
+        logs = "".join(open(os.path.join(logd, f)).read() for f in os.listdir(logd) if ".part-" not in f)
+        runs.append((dt, logs, r.stderr))
+    dt, logs, err = min(runs, key=lambda x: x[0])
+    st = shard_stats(logs, dt)
+    st["runs_seconds"] = [round(x[0], 3) for x in runs]
+    st["devices"] = n_dev
+    st["shard_threads"] = nprocs
+    st["genome_mbp"] = mbp
+    st["synth_seconds"] = round(synth_s, 1)
+    st["shards_per_device"] = {str(k): len(re.findall(rf"gpu {k}\b", logs)) for k in range(n_dev)}
+    m = re.search(r"Haplotype Caller finishes in ([\d.]+) seconds", err)
+    st["caller_stage_seconds"] = float(m.group(1)) if m else None
+    st["workload"] = (f"C4: one fcs-genome htc (GVCF) over a {mbp:g} Mbp chr1-like genome at 30x, 32 interval "
+                      f"shards dealt to {n_dev} GPU slot(s), {nprocs} shard threads")
+    shutil.rmtree(d, ignore_errors=True)
+    return st
 
 
 def bench_c1(exe, env, work, seed):
@@ -432,13 +557,17 @@ def bench_e2e(args, rank, local):
         if cpu_htc:  # the reference's CPU path beside it, on the same genome (rank 0, N=1 only)
             out["htc"]["cpu_baseline"] = htc_cpu_baseline(exe, env, work, d + "/ref.fasta", d + "/sample.bam",
                                                           work + "/htc.g.vcf")
-        (dt, logs, err), runs = best("mutect2", ["mutect2", "-f", "-r", d + "/ref.fasta", "-t", d + "/tumor.bam", "-n",
-                                                 d + "/sample.bam", "-o", work + "/m2.vcf"])
+        m2_cmd = lambda o: ["mutect2", "-f", "-r", d + "/ref.fasta", "-t", d + "/tumor.bam", "-n",  # noqa: E731
+                            d + "/sample.bam", "-o", o]
+        (dt, logs, err), runs = best("mutect2", m2_cmd(work + "/m2.vcf"))
         out["mutect2"] = shard_stats(logs, dt)
         out["mutect2"]["runs_seconds"] = runs
         ms = stage_s(err, "Mutect2")
         out["mutect2"]["caller_stage_seconds"] = ms
         out["mutect2"]["caller_stage_regions_per_s"] = round(out["mutect2"]["regions"] / ms, 1) if ms else None
+        if cpu_htc:  # C5's CPU path: GATK Mutect2 with the CPU PairHMM, same command and genome
+            out["mutect2"]["cpu_baseline"] = caller_cpu_baseline(exe, env, work, m2_cmd, work + "/m2.vcf",
+                                                                 tag="c5", ext=".vcf")
         shutil.rmtree(d, ignore_errors=True)
         if cpu_htc:
             out["c1"] = bench_c1(exe, env, work, args.seed + rank)
@@ -446,36 +575,42 @@ def bench_e2e(args, rank, local):
         subprocess.run([exe, "synth", "-o", work + "/a", "-c", f"chr1:{La}", "-x", "30", "--no-fastq", "--paired",
                         "350", "--seed", str(args.seed + rank)], env=env, check=True, capture_output=True)
         a = work + "/a"
+        # 4% of the read-2 mates damaged past seeding: only the mate rescue
+        # (bwa mem_matesw on the GPU ksw_align2) can place them
+        n_damaged = damage_mates(a + "/sample_2.fastq")
         # bwa-flow maps a prebuilt index (bwa index): built once here, outside the timed runs
         ti = time.perf_counter()
         subprocess.run([exe, "index", "-r", a + "/ref.fasta", "--sa-intv", "32"], env=env, check=True,
                        capture_output=True)
         index_s = time.perf_counter() - ti
-        (dt, _, err), runs = best("align", ["align", "-f", "-r", a + "/ref.fasta", "-1", a + "/sample_1.fastq", "-2",
-                                            a + "/sample_2.fastq", "-o", work + "/aln.bam"])
-        m = re.search(r"(\d+) reads, (\d+) mapped, (\d+) supplementary, (\d+) extension tasks, (\d+) global "
-                      r"alignments, ([\d.]+) s \(GPU calls ([\d.]+) s\)", err)
-        pm = re.search(r"(\d+) reads properly paired, (\d+) mates rescued, insert ([\d.]+) \+- ([\d.]+)", err)
-        ph = re.search(r"alignment thread-seconds ([\d.]+): seeding ([\d.]+), extension ([\d.]+), pairing ([\d.]+), "
-                       r"records ([\d.]+)", err)
-        wp = re.search(r"phases: reference ([\d.e-]+) s, FMD index ([\d.e-]+) s .*FASTQ \+ alignment ([\d.e-]+) s .*"
-                       r"sort \+ BAM \+ index ([\d.e-]+) s", err)
-        if not (m and pm and ph and wp):
-            raise RuntimeError("fcs-genome align report not understood: " + err[-2000:])
-        n = int(m.group(1))
-        out["align"] = {"mode": f"paired-end 2x151, fragments N(350, 50), {args.e2e_align_mbp:g} Mbp genome, 30x "
-                                "of pairs", "reads": n, "mapped": int(m.group(2)), "supplementary": int(m.group(3)),
-                        "ext_tasks": int(m.group(4)), "global_tasks": int(m.group(5)),
-                        "gpu_call_seconds": float(m.group(7)),
-                        "thread_seconds": {k: float(ph.group(i + 1)) for i, k in
-                                           enumerate(("total", "seeding", "extension", "pairing", "records"))},
-                        "wall_phases_seconds": {k: float(wp.group(i + 1)) for i, k in
-                                                enumerate(("reference", "fmd_index", "fastq_and_alignment",
-                                                           "sort_bam_index"))},
-                        "proper_pair_reads": int(pm.group(1)), "mates_rescued": int(pm.group(2)),
-                        "index": "prebuilt by fcs-genome index --sa-intv 32 (untimed, %.1f s), mapped by align" % index_s,
-                        "seconds": round(dt, 3), "runs_seconds": runs, "reads_per_s": round(n / dt, 1)}
+        al_cmd = lambda o: ["align", "-f", "-r", a + "/ref.fasta", "-1", a + "/sample_1.fastq", "-2",  # noqa: E731
+                            a + "/sample_2.fastq", "-o", o]
+        (dt, _, err), runs = best("align", al_cmd(work + "/aln.bam"))
+        rep = align_report(err)
+        n = rep["reads"]
+        out["align"] = dict(mode=f"paired-end 2x151, fragments N(350, 50), {args.e2e_align_mbp:g} Mbp genome, 30x "
+                                 f"of pairs; {n_damaged} read-2 mates (4%) carry a mismatch every 16 bases, so only "
+                                 "the mate rescue places them", damaged_mates=n_damaged, **rep)
+        out["align"].update(index="prebuilt by fcs-genome index --sa-intv 32 (untimed, %.1f s), mapped by align"
+                                  % index_s, seconds=round(dt, 3), runs_seconds=runs, reads_per_s=round(n / dt, 1))
+        if cpu_htc:  # bwa-flow mem without --use_fpga: the SW on the host cores, same binary and threads
+            out["align"]["cpu_baseline"] = align_cpu_baseline(exe, env, work, al_cmd, work + "/aln.bam", per_rank)
         return out
+    finally:
+        shutil.rmtree(work, ignore_errors=True)
+
+
+def run_c4(args, n_dev):
+    """bench_c4 on this node's n_dev GPUs, in a scratch directory (rank 0)."""
+    import shutil
+    import tempfile
+    exe = os.path.join(ROOT, "falcon-genome_amd", "bin", "fcs-genome")
+    work = tempfile.mkdtemp(prefix="fcs-c4-")
+    quota = host_cpu_quota()
+    env = dict(os.environ, FCS_TEMP_DIR=work, FCS_HOST_THREADS=str(quota))
+    try:
+        return bench_c4(exe, env, work, min(args.e2e_mbp * n_dev, 248.0), n_dev, args.seed + 4242, min(32, quota),
+                        reps=args.e2e_reps)
     finally:
         shutil.rmtree(work, ignore_errors=True)
 
@@ -702,7 +837,10 @@ class Ranks:
             if dry:
                 torch.distributed.init_process_group("gloo")
             else:
-                torch.distributed.init_process_group("nccl", device_id=self.dev)
+                # the C4 leg holds ranks > 0 in a barrier while rank 0's job runs (minutes at 8 GPUs)
+                import datetime
+                torch.distributed.init_process_group("nccl", device_id=self.dev,
+                                                     timeout=datetime.timedelta(minutes=30))
 
     def barrier(self):
         if self.world > 1:
@@ -799,6 +937,8 @@ def main():
                     help="per-GPU genome of the htc / mutect2 runs (31 Mbp = chr1 / 8 GPUs, the C4 share)")
     ap.add_argument("--e2e-align-mbp", type=float, default=4.0, help="genome of the align run")
     ap.add_argument("--e2e-reps", type=int, default=2, help="runs of each e2e command; the fastest is reported")
+    ap.add_argument("--no-c4", action="store_true",
+                    help="N > 1: skip the C4 leg (one htc job over N x --e2e-mbp, dealt to all N GPUs)")
     args = ap.parse_args()
 
     if "WORLD_SIZE" not in os.environ and (args.gpus or 1) > 1:
@@ -955,6 +1095,15 @@ def main():
                 e2e[k]["seconds"] = round(slow, 3)
                 e2e[k][unit + "_per_s"] = round(tot / slow, 1)
             e2e["n_gpus"] = world
+        if world > 1 and not args.no_c4:
+            # C4 as the reference runs it: ONE htc job over a genome of N x the
+            # per-GPU share (248 Mbp = chr1 at 8 GPUs), its 32 shards dealt to
+            # all N GPUs of the node by the job's own Executor.  Rank 0 runs it
+            # while the other ranks wait; their GPUs serve the job's slots.
+            rk.barrier()
+            if rank == 0:
+                e2e["c4"] = run_c4(args, int(os.environ.get("LOCAL_WORLD_SIZE", str(world))))
+            rk.barrier()
         line["e2e"] = e2e
 
     if rank == 0:

@@ -501,7 +501,8 @@ __global__ __launch_bounds__(64) void bsw_align_kernel(const BswDevBatch b, cons
 int launch_bsw_align(const BswDevBatch& b, const BswParams& p, const int32_t* xtra, int max_qlen, int max_tlen,
                      int32_t* out, hipStream_t s, bool all_u8) {
   if (b.n <= 0) return FCS_OK;
-  if (max_qlen > 1024) return fail(FCS_ERR_UNSUPPORTED, "[E::fcship] ksw_align2: qlen > 1024 unsupported");
+  static_assert(3 * FCS_ALIGN_MAX_TLEN + 18 <= 160 * 1024, "FCS_ALIGN_MAX_TLEN must fit one wave's LDS");
+  if (max_qlen > FCS_ALIGN_MAX_QLEN) return fail(FCS_ERR_UNSUPPORTED, "[E::fcship] ksw_align2: qlen > 1024 unsupported");
   {  // the profile holds mat + shift as bytes (shift = -min, as bwa's u8 bias)
     int mn = 127, mx = -128;
     for (int a = 0; a < 25; ++a) mn = std::min(mn, (int)p.mat[a]), mx = std::max(mx, (int)p.mat[a]);

@@ -24,7 +24,10 @@
 //    saturating packed ops; every later max / saturating subtract is exactly
 //    bwa's max(., 0) arithmetic.
 //  * Row max and arg-max: packed max of (h << 8 | j); ties go to the larger j
-//    as in bwa.  Trims: a 16-column bitmap per task half (v_pk_min + lshl_or).
+//    as in bwa.  Trims: at row end, scans of the stored entries chunk by
+//    chunk from the band's edges (first / last non-zero entry per task half;
+//    chunk_nz / last_col), usually one chunk each since the band moves about
+//    a column per row.
 //
 // Band edges without per-cell predicates:
 //  * left: every eh[] entry left of a task's `beg` is kept at zero (bwa's

@@ -791,7 +791,9 @@ void rescue_windows(const KmerIndex& idx, const std::array<PeStat, 4>& pes, cons
     const bool rhalf = ((rb + re) >> 1) >= l;  // bns_fetch_seq: the half holding the middle
     if (rhalf) rb = std::max(rb, l);
     else re = std::min(re, l);
-    if (re - rb < opt.k || re - rb > 100000) continue;
+    // bwa's own cap is 100000; windows or mates past fcs_bsw_align's limits are
+    // skipped here so that one long read cannot fail the batch's call
+    if (re - rb < opt.k || re - rb > FCS_ALIGN_MAX_TLEN || lms > FCS_ALIGN_MAX_QLEN) continue;
     RescueJob J;
     J.mate = &mate;
     J.contig = anchor.contig;
@@ -1275,22 +1277,44 @@ AlignStats align_pairs(const Reference& ref, const KmerIndex& idx, const std::ve
   // mate rescue (bwa mem_sam_pe): every region of a read within pen_unpaired of
   // its best (at most max_matesw) searches the mate's windows
   if (!pes[0].failed || !pes[1].failed || !pes[2].failed || !pes[3].failed) {
-    std::vector<std::vector<RescueJob>> per(n);
+    // the anchors are copies taken before any rescue (bwa's b[] lists); bwa
+    // runs mem_matesw anchor by anchor, and each call's skip[] sees the
+    // regions the earlier anchors of the same read added to the mate.  Here
+    // round k runs the k-th anchor of every read as one device batch, so the
+    // k-th anchor's windows are chosen after rounds 0 .. k - 1 have landed.
+    // (The two ends are independent: end s's anchors only add to end !s,
+    // whose own anchors were copied before.)
+    std::vector<std::array<std::vector<Cand>, 2>> anchors(n);
     parallel_for(n, opt.threads, [&](size_t i) {
       ReadAln* r[2] = {&m1[i], &m2[i]};
-      std::vector<Cand> anchors[2];
       for (int s = 0; s < 2; ++s)
         for (const Cand& c : r[s]->cands)
-          if (c.aln.score >= r[s]->cands[0].aln.score - opt.pen_unpaired && (int)anchors[s].size() < opt.max_matesw)
-            anchors[s].push_back(c);
-      for (int s = 0; s < 2; ++s)
-        for (const Cand& a : anchors[s]) rescue_windows(idx, pes, a, *r[!s], opt, per[i]);
+          if (c.aln.score >= r[s]->cands[0].aln.score - opt.pen_unpaired && (int)anchors[i][s].size() < opt.max_matesw)
+            anchors[i][s].push_back(c);
     });
-    std::vector<RescueJob> jobs;
-    for (auto& v : per)
-      for (RescueJob& J : v) jobs.push_back(std::move(J));
+    size_t rounds = 0;
+    for (const auto& a : anchors) rounds = std::max({rounds, a[0].size(), a[1].size()});
+    std::vector<ReadAln*> resc;
+    for (size_t k = 0; k < rounds; ++k) {
+      std::vector<std::vector<RescueJob>> per(n);
+      parallel_for(n, opt.threads, [&](size_t i) {
+        ReadAln* r[2] = {&m1[i], &m2[i]};
+        for (int s = 0; s < 2; ++s)
+          if (k < anchors[i][s].size()) rescue_windows(idx, pes, anchors[i][s][k], *r[!s], opt, per[i]);
+      });
+      std::vector<RescueJob> jobs;
+      for (auto& v : per)
+        for (RescueJob& J : v) jobs.push_back(std::move(J));
+      if (jobs.empty()) continue;
+      const uint64_t te = now_us();
+      std::vector<ReadAln*> got = rescue_align(idx, P, opt, jobs, st);
+      resc.insert(resc.end(), got.begin(), got.end());
+      st.extend_seconds += (now_us() - te) / 1e6;
+      st.pair_seconds -= (now_us() - te) / 1e6;
+    }
+    std::sort(resc.begin(), resc.end());
+    resc.erase(std::unique(resc.begin(), resc.end()), resc.end());
     const uint64_t te = now_us();
-    std::vector<ReadAln*> resc = rescue_align(idx, P, opt, jobs, st);
     dedup_patch(idx, P, opt, resc, false, st);
     st.extend_seconds += (now_us() - te) / 1e6;
     st.pair_seconds -= (now_us() - te) / 1e6;

@@ -30,7 +30,9 @@
 // (tie-breaking only), mem_flt_chained_seeds (long reads only) is not applied,
 // a rescued region's truesc is its score (bwa leaves it 0, which would give
 // its CIGAR a zero band), and the rescue list is deduplicated once after all
-// orientations rather than after each.
+// anchors rather than after each.  Rescue windows follow bwa's anchor order:
+// anchor k of every read runs in device round k, after the regions that
+// anchors 0 .. k - 1 added to the mate (mem_matesw's skip[] sees them).
 #pragma once
 
 #include <cstdint>

@@ -469,15 +469,27 @@ class PassCombiner {
       }
       busy_ = true;
       lk.unlock();
-      std::vector<fcs_phmm_region> all;
-      for (const Req* x : take) all.insert(all.end(), x->regs->begin(), x->regs->end());
-      const int rc = fcs_phmm_compute_regions(all.data(), (int32_t)all.size(), &o);
-      const std::string err = rc != FCS_OK ? std::string(fcs_last_error()) : std::string();
+      // nothing may leave this section by exception: the taken requests must be
+      // marked done and busy_ cleared, or every waiter of the slot blocks forever
+      int rc = FCS_OK;
+      std::string err;
       double dev = 0, res = 0;
       int64_t nres = 0;
-      if (rc == FCS_OK) {
-        if (fcs_phmm_last_rescued(&nres) != FCS_OK) nres = 0;
-        if (fcs_phmm_last_device_ms(&dev, &res) != FCS_OK) dev = res = 0;
+      try {
+        std::vector<fcs_phmm_region> all;
+        for (const Req* x : take) all.insert(all.end(), x->regs->begin(), x->regs->end());
+        rc = fcs_phmm_compute_regions(all.data(), (int32_t)all.size(), &o);
+        if (rc != FCS_OK) err = fcs_last_error();
+        if (rc == FCS_OK) {
+          if (fcs_phmm_last_rescued(&nres) != FCS_OK) nres = 0;
+          if (fcs_phmm_last_device_ms(&dev, &res) != FCS_OK) dev = res = 0;
+        }
+      } catch (const std::exception& e) {
+        rc = FCS_ERR_INVALID;
+        err = std::string("[E::fcsg] merged PairHMM pass: ") + e.what();
+      } catch (...) {
+        rc = FCS_ERR_INVALID;
+        err = "[E::fcsg] merged PairHMM pass: unknown exception";
       }
       lk.lock();
       for (Req* x : take) x->rc = rc, x->err = err, x->done = true;

@@ -295,6 +295,10 @@ int fcs_bsw_global_dev(const fcs_bsw_batch* dev_batch, const fcs_bsw_params* par
  * codes 0..4 (qlen <= 1024), tasks[k].h0 / .w ignored, xtra[k] bwa's xtra word.
  * out[k] = bwa's kswr_t (score, te, qe, score2, te2, tb, qb; -1 where bwa
  * leaves -1). */
+/* Task limits of fcs_bsw_align: longer queries or targets make the whole
+ * call fail with FCS_ERR_UNSUPPORTED (callers filter them first). */
+#define FCS_ALIGN_MAX_QLEN 1024
+#define FCS_ALIGN_MAX_TLEN 54000
 #define FCS_KSW_XBYTE 0x10000
 #define FCS_KSW_XSTOP 0x20000
 #define FCS_KSW_XSUBO 0x40000

@@ -9,7 +9,8 @@
  * supplementary marking, pairing, SAM fields) in a container without a GPU.
  * tests/test_align_host_cpu.py compiles it into a temporary directory and
  * puts that directory first on LD_LIBRARY_PATH of the fcs-genome child it
- * starts; the PairHMM entry points fail (FCS_ERR_DEVICE), unless
+ * starts (ksw_align2 by the SSE2 striped form, oracle/ksw_align_sse.c, which
+ * tests/test_oracle_ksw.py holds equal to the element-wise emulation); the PairHMM entry points fail (FCS_ERR_DEVICE), unless
  * FCS_MOCK_PHMM=1 (2) — then every haplotype but the first (last) scores -10
  * (placeholder likelihoods, no PairHMM at all), or FCS_MOCK_PHMM=3 — then
  * the oracle's PairHMM (oracle/pairhmm_oracle.c, slow) computes them, which lets a developer time the caller's
@@ -55,8 +56,16 @@ int oracle_ksw_global2(int qlen, const uint8_t* query, int tlen, const uint8_t* 
                        int o_del, int e_del, int o_ins, int e_ins, int w, int* n_cigar, uint32_t* cigar_out,
                        int cigar_cap);
 
-void oracle_ksw_align2(int qlen, const uint8_t* query, int tlen, const uint8_t* target, int m, const int8_t* mat,
-                       int o_del, int e_del, int o_ins, int e_ins, int xtra, int* out);
+void oracle_ksw_align2_sse(int qlen, const uint8_t* query, int tlen, const uint8_t* target, int m, const int8_t* mat,
+                           int o_del, int e_del, int o_ins, int e_ins, int xtra, int* out);
+
+/* FCS_MOCK_BSW_THREADS: OpenMP threads of the banded-SW entry points (default
+ * 1).  bench.py's align CPU baseline sets it to the command's host threads, so
+ * bwa's per-thread extension work runs on as many cores as the GPU run uses. */
+static int bsw_threads(void) {
+  const char* t = getenv("FCS_MOCK_BSW_THREADS");
+  return t && atoi(t) > 0 ? atoi(t) : 1;
+}
 
 static __thread const char* g_err = "";
 
@@ -80,6 +89,7 @@ void fcs_bsw_params_default(fcs_bsw_params* p) {
 
 int fcs_bsw_extend(const fcs_bsw_task* t, int32_t n, const fcs_bsw_params* p, fcs_bsw_result* r, int32_t device) {
   (void)device;
+#pragma omp parallel for schedule(dynamic, 32) num_threads(bsw_threads())
   for (int32_t k = 0; k < n; ++k) {
     fcs_bsw_result* o = &r[k];
     o->score = oracle_ksw_extend2(t[k].qlen, t[k].query, t[k].tlen, t[k].target, 5, p->mat, p->o_del, p->e_del,
@@ -93,6 +103,7 @@ int fcs_bsw_global(const fcs_bsw_task* t, int32_t n, const fcs_bsw_params* p, in
                    const int64_t* off, const int32_t* cap, int32_t* n_cigar, int32_t device) {
   (void)device;
   int rc = FCS_OK;
+#pragma omp parallel for schedule(dynamic, 32) num_threads(bsw_threads()) reduction(min : rc)
   for (int32_t k = 0; k < n; ++k) {
     int nc = 0;
     scores[k] = oracle_ksw_global2(t[k].qlen, t[k].query, t[k].tlen, t[k].target, 5, p->mat, p->o_del, p->e_del,
@@ -100,7 +111,7 @@ int fcs_bsw_global(const fcs_bsw_task* t, int32_t n, const fcs_bsw_params* p, in
                                    arena ? cap[k] : 0);
     if (arena) {
       n_cigar[k] = nc;
-      if (nc > cap[k]) rc = FCS_ERR_INVALID;
+      if (nc > cap[k]) rc = FCS_ERR_INVALID; /* negative: the min-reduction keeps it */
     }
   }
   if (rc != FCS_OK) g_err = "fcs_bsw_global: CIGAR longer than its cap";
@@ -110,9 +121,10 @@ int fcs_bsw_global(const fcs_bsw_task* t, int32_t n, const fcs_bsw_params* p, in
 int fcs_bsw_align(const fcs_bsw_task* t, int32_t n, const fcs_bsw_params* p, const int32_t* xtra, fcs_kswr* out,
                   int32_t device) {
   (void)device;
+#pragma omp parallel for schedule(dynamic, 8) num_threads(bsw_threads())
   for (int32_t k = 0; k < n; ++k) {
     int r[7];
-    oracle_ksw_align2(t[k].qlen, t[k].query, t[k].tlen, t[k].target, 5, p->mat, p->o_del, p->e_del, p->o_ins,
+    oracle_ksw_align2_sse(t[k].qlen, t[k].query, t[k].tlen, t[k].target, 5, p->mat, p->o_del, p->e_del, p->o_ins,
                       p->e_ins, xtra[k], r);
     out[k] = (fcs_kswr){r[0], r[1], r[2], r[3], r[4], r[5], r[6]};
   }

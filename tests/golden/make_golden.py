@@ -108,14 +108,14 @@ def align_cases():
 
 def main():
     with open(os.path.join(HERE, "phmm_golden.json"), "w") as f:
-        json.dump({"generator": "tests/golden/make_golden.py", "semantics": "GKL float + double rescue",
+        json.dump({"generator": "tests/golden/make_golden.py", "semantics": "GKL float + double rescue — outputs of this repo's oracle restatement (oracle/), not of GKL/GATK: parity unpinned",
                    "cases": phmm_cases()}, f, separators=(",", ":"))
     k = ksw_cases()
     with open(os.path.join(HERE, "ksw_golden.json"), "w") as f:
-        json.dump({"generator": "tests/golden/make_golden.py", "semantics": "bwa ksw_extend2 / ksw_global2",
+        json.dump({"generator": "tests/golden/make_golden.py", "semantics": "bwa ksw_extend2 / ksw_global2 — outputs of this repo's oracle restatement (oracle/), not of bwa: parity unpinned",
                    "mat": k["mat"], "extend": k["extend"], "global": k["global_"]}, f, separators=(",", ":"))
     with open(os.path.join(HERE, "ksw_align_golden.json"), "w") as f:
-        json.dump({"generator": "tests/golden/make_golden.py", "semantics": "bwa ksw_align2 (striped u8 / i16)",
+        json.dump({"generator": "tests/golden/make_golden.py", "semantics": "bwa ksw_align2 (striped u8 / i16) — outputs of this repo's oracle restatement (oracle/), not of bwa: parity unpinned (score2 / te2 / tb / qb and the b[] rules are checked only against the restatement)",
                    "mat": mat().tolist(), "cases": align_cases()}, f, separators=(",", ":"))
 
 

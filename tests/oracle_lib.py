@@ -56,6 +56,10 @@ lib.oracle_ksw_global2.restype = C.c_int
 lib.oracle_ksw_global2.argtypes = [C.c_int, vp, C.c_int, vp, C.c_int, vp] + [C.c_int] * 5 + [vp, vp, C.c_int]
 lib.oracle_ksw_align2.restype = None
 lib.oracle_ksw_align2.argtypes = [C.c_int, vp, C.c_int, vp, C.c_int, vp] + [C.c_int] * 5 + [vp]
+lib.oracle_ksw_align2_sse.restype = None
+lib.oracle_ksw_align2_sse.argtypes = lib.oracle_ksw_align2.argtypes
+lib.oracle_ksw_align2_sse_batch.restype = None
+lib.oracle_ksw_align2_sse_batch.argtypes = [vp] * 7 + [C.c_int64, vp] + [C.c_int] * 4 + [vp, C.c_int]
 lib.oracle_ksw_extend2_batch.restype = None
 lib.oracle_ksw_extend2_batch.argtypes = [vp, vp, vp, vp, vp, vp, vp, vp, C.c_int64, vp] + [C.c_int] * 6 + \
     [vp, vp, C.c_int]
@@ -173,6 +177,29 @@ def ksw_align2(q, t, mat, xtra, o_del=6, e_del=1, o_ins=6, e_ins=1):
     out = np.zeros(7, np.int32)
     lib.oracle_ksw_align2(len(q), _p(q), len(t), _p(t), 5, _p(m), o_del, e_del, o_ins, e_ins, xtra, _p(out))
     return tuple(int(x) for x in out)
+
+
+def ksw_align2_sse(q, t, mat, xtra, o_del=6, e_del=1, o_ins=6, e_ins=1):
+    """The SSE2 striped form of ksw_align2 (oracle/ksw_align_sse.c, the CPU
+    baseline): the same seven outputs as ksw_align2."""
+    q = _a(q)
+    t = _a(t)
+    m = _a(mat, np.int8)
+    out = np.zeros(7, np.int32)
+    lib.oracle_ksw_align2_sse(len(q), _p(q), len(t), _p(t), 5, _p(m), o_del, e_del, o_ins, e_ins, xtra, _p(out))
+    return tuple(int(x) for x in out)
+
+
+def ksw_align2_sse_batch(t, mat, xtra, o_del=6, e_del=1, o_ins=6, e_ins=1, threads=1):
+    """ksw_align2 (SSE2 striped restatement) over a BswTasks batch on OpenMP
+    threads; xtra: one int or one per task.  Returns an (n, 7) int32 array."""
+    n = t.n
+    out = np.zeros((n, 7), np.int32)
+    m = _a(mat, np.int8)
+    xt = np.ascontiguousarray(np.broadcast_to(np.asarray(xtra, np.int32), (n,)))
+    lib.oracle_ksw_align2_sse_batch(_p(t.qbuf), _p(t.qoff), _p(t.qlen), _p(t.tbuf), _p(t.toff), _p(t.tlen), _p(xt), n,
+                                    _p(m), o_del, e_del, o_ins, e_ins, _p(out), threads)
+    return out
 
 
 def ksw_extend2_batch(t, mat, o_del=6, e_del=1, o_ins=6, e_ins=1, end_bonus=5, zdrop=100, threads=1):

@@ -161,8 +161,9 @@ def test_align_split_reads_supplementary(gpu, data, tmp_path):
 def test_align_paired_end(gpu, tmp_path):
     """Paired-end align (row f4): FR pairs of N(350, 50) fragments; 4% of the
     read-2 mates carry a mismatch every 16 bases, so no 19-mer seeds them and
-    only the mate rescue (12-mer window search opposite the read-1 alignment)
-    places them.  Checks placement against the generator's truth, proper-pair
+    only the mate rescue (bwa's mem_matesw: a GPU ksw_align2 local alignment
+    of the mate in the window the insert-size statistics predict opposite
+    the read-1 alignment) places them.  Checks placement against the generator's truth, proper-pair
     flags, mate fields, signed TLEN and the insert-size estimate."""
     import re
     d = tmp_path / "pe"

@@ -277,3 +277,38 @@ def test_ksw_align2_golden_fixtures():
     for k, c in enumerate(g["cases"]):
         got = oracle_lib.ksw_align2(np.array(c["q"], np.uint8), np.array(c["t"], np.uint8), m, c["xtra"])
         assert list(got) == c["out"], k
+
+
+def test_ksw_align2_sse_equals_emulation():
+    """The SSE2 striped ksw_align2 (oracle/ksw_align_sse.c: the CPU baseline,
+    bwa's 16 x u8 / 8 x i16 lanes as real vectors) gives the element-wise
+    emulation's seven outputs on the golden vectors and on random tasks of
+    both widths: related, unrelated, tie-heavy (2-letter alphabets), empty,
+    saturating u8 (long exact matches) and every flag mix bwa uses, plus
+    gap costs other than bwa's defaults."""
+    with open(os.path.join(HERE, "golden", "ksw_align_golden.json")) as f:
+        g = json.load(f)
+    m = np.array(g["mat"], np.int8)
+    for k, c in enumerate(g["cases"]):
+        q, t = np.array(c["q"], np.uint8), np.array(c["t"], np.uint8)
+        assert oracle_lib.ksw_align2_sse(q, t, m, c["xtra"]) == oracle_lib.ksw_align2(q, t, m, c["xtra"]), k
+    rng = np.random.default_rng(20261018)
+    flags = [0x40000 | 0x80000 | 0x10000 | 19, 0x40000 | 0x80000 | 19, 0x80000, 0x10000, 0x20000 | 30, 0,
+             0x80000 | 0x10000, 0x40000 | 0x10000 | 25]
+    gaps = [(6, 1, 6, 1), (6, 1, 6, 1), (5, 2, 4, 1), (1, 1, 1, 1), (11, 3, 9, 2)]
+    for k in range(600):
+        ql, tl = int(rng.integers(0, 300)), int(rng.integers(0, 700))
+        alpha = 2 if k % 5 == 0 else 4
+        t = rng.integers(0, alpha, tl).astype(np.uint8)
+        if k % 3 and tl > 10 and ql > 0:
+            a = int(rng.integers(0, max(1, tl - ql)))
+            q = np.resize(t[a:a + ql] if tl - a >= 1 else t, ql).copy()
+            mut = rng.random(ql) < (0.0 if k % 7 == 0 else 0.05)
+            q[mut] = rng.integers(0, 5, int(mut.sum()))
+        else:
+            q = rng.integers(0, alpha + 1 if k % 4 else alpha, ql).astype(np.uint8)
+        x = flags[k % len(flags)]
+        od, ed, oi, ei = gaps[k % len(gaps)]
+        a = oracle_lib.ksw_align2(q, t, m, x, od, ed, oi, ei)
+        b = oracle_lib.ksw_align2_sse(q, t, m, x, od, ed, oi, ei)
+        assert a == b, (k, ql, tl, hex(x), a, b)
