@@ -220,10 +220,11 @@ hipError_t sort_pairs_u32(void* tmp, size_t& bytes, const uint32_t* kin, uint32_
 // SW schedule keys: bucket in bits [20, 24), below it the in-bucket order.
 constexpr int kBswKeyBucketShift = 20;
 constexpr int kBswKeyBits = 24;
-// PairHMM schedule keys: launch class in bits [20, 24).  Launch classes
-// 0 .. kStreamClasses-1 run the row-streamed fp32 kernel (phmm_stream.h), the
-// next kPhmmClasses the grouped kernels (phmm2.h / phmm_kernel), each range
-// longest first.
+// PairHMM schedule keys: launch class in bits [12, 16).  Launch classes
+// 0 .. kLongClasses-1 run the row-streamed fp32 kernel (phmm_stream.h) on
+// haplotypes longer than the column-blocked kernel takes, the next
+// kColsLaunch the column-blocked kernel (phmm_cols.h), the last kPhmmClasses
+// the grouped kernels (phmm2.h / phmm_kernel), each range longest first.
 // PairHMM sort keys: 16 bits (two 8-bit radix passes; the in-class order keys
 // hap length only: 24-bit keys that also ordered stream classes by read length
 // measured slower).
@@ -231,7 +232,9 @@ constexpr int kPhmmKeyClassShift = 12;
 constexpr int kPhmmKeyBits = 16;
 constexpr int kStreamClasses = 4;
 constexpr int kPhmmClasses = 6;
-constexpr int kPhmmLaunchClasses = kStreamClasses + kPhmmClasses;
+constexpr int kLongClasses = 2;  // phmm3 stream classes 3 and 2 (H <= 3700, <= 472)
+constexpr int kColsLaunch = 4;   // phmm_cols.h classes (H <= 303 .. <= 191)
+constexpr int kPhmmLaunchClasses = kLongClasses + kColsLaunch + kPhmmClasses;
 // Sorted schedule: one launch over the lane (0..9) and pair (kBswPairBucket0..+4)
 // buckets, then the wave-per-task kernel over kBswWideBucket.
 int launch_bsw_extend_sorted(const BswDevBatch& b, const BswParams& p, int max_qlen, int max_tlen, int32_t* res,

@@ -416,6 +416,7 @@ __global__ __launch_bounds__(64, (sizeof(T) == 4 && !EXACT) ? 4 : 1) void phmm_k
 
 #include "phmm2.h"
 #include "phmm_stream.h"
+#include "phmm_cols.h"
 
 namespace fcs {
 
@@ -441,15 +442,25 @@ __host__ __device__ inline int phmm_class(int H) {
 
 // Sort keys (16 bits, two 8-bit radix passes): a 4-bit launch class, then the
 // in-class order, as ascending keys — each class is a contiguous range and the
-// longest work comes first.  Classes 0 .. kStreamClasses-1 are the row-streamed
-// kernel's (kStreamMinR <= R <= kStreamMaxR, longest hap-length class first), the rest the
-// grouped kernels' hap-length classes (longest first).  In-class order:
-// streamed, hap length (24-bit keys: then read length) descending; grouped, stripe
-// count then hap length descending.  The clamps only change the order, never results.
+// longest work comes first.  For kStreamMinR <= R <= kStreamMaxR: haplotypes
+// longer than the column-blocked kernel's 303 columns take the row-streamed
+// kernel's classes 3 and 2 (launch classes 0, 1), the others the column-
+// blocked kernel's classes (launch classes kLongClasses .., widest first);
+// everything else the grouped kernels' hap-length classes (longest first).
+// In-class order: streamed and column-blocked, hap length descending;
+// grouped, stripe count then hap length descending.  The clamps only change
+// the order, never results.
 __host__ __device__ inline int phmm_launch_class(int R, int H, int& stream_cls) {
-  stream_cls = (R >= kStreamMinR && R <= kStreamMaxR && H >= 1) ? stream_class(H) : -1;
-  if (stream_cls >= 0) return kStreamClasses - 1 - stream_cls;
-  return kStreamClasses + kPhmmClasses - 1 - phmm_class(max(H, 0));
+  stream_cls = -1;
+  if (R >= kStreamMinR && R <= kStreamMaxR && H >= 1) {
+    static_assert(kColsMinR <= kStreamMinR, "column-blocked streams take every streamed read");
+    const int cc = cols_class(H);
+    stream_cls = cc >= 0 ? 0 : stream_class(H);
+    if (cc >= 0) return kLongClasses + cc;
+    if (stream_cls >= 2) return kStreamClasses - 1 - stream_cls;
+    stream_cls = -1;
+  }
+  return kLongClasses + kColsLaunch + kPhmmClasses - 1 - phmm_class(max(H, 0));
 }
 
 __global__ void phmm_keys_kernel(const PhmmDevBatch b, uint32_t* __restrict__ keys, int32_t* __restrict__ idx,
@@ -555,6 +566,19 @@ static int stream_pairs_per_segment(int64_t n) {
   return (int)std::max<int64_t>(1, std::min<int64_t>(kStreamMaxK, k));
 }
 
+// Pairs per half-stream of the column-blocked kernel: as many as keep >= ~24K
+// waves in flight for the batch (8 half-streams per wave), at most 8.
+// FCSHIP_STREAM_K=k (tests) forces k here too.
+static int cols_pairs_per_half(int64_t n) {
+  static const int forced = [] {
+    const char* e = std::getenv("FCSHIP_STREAM_K");
+    return e ? std::atoi(e) : 0;
+  }();
+  if (forced > 0) return std::min(forced, 8);
+  const int64_t k = n / (8 * 24576);
+  return (int)std::max<int64_t>(1, std::min<int64_t>(8, k));
+}
+
 int launch_phmm_forward(const PhmmDevBatch& b, const int32_t* order, int64_t count, int max_hap_len,
                         const int64_t* bounds, const DeviceTables& t, bool exact, double* out, int32_t* rescue_list,
                         unsigned long long* rescue_count, float thr, bool use_rescue, int32_t* fb_list,
@@ -563,15 +587,18 @@ int launch_phmm_forward(const PhmmDevBatch& b, const int32_t* order, int64_t cou
   const long long groups = (count + 3) / 4;
   const int ns_max = nslot_for(max_hap_len);
   const int c_max = phmm_class(max_hap_len);
-  const int sc_max = stream_class(max_hap_len) < 0 ? kStreamClasses - 1 : stream_class(max_hap_len);
   // One launch per launch class (ranges from the device-side bounds), forked
   // over streams so a class's tail overlaps the next class; classes above the
   // batch's longest haplotype are empty and not launched.
   hipStream_t fs[kForkStreams];
   if (const int rc = fork_streams(s, fs); rc != FCS_OK) return rc;
   int fork = 0;
-  for (int j = kStreamClasses - 1 - sc_max; j < kStreamClasses; ++j) {
+  // Haplotypes longer than the column-blocked kernel takes: row-streamed
+  // classes 3 and 2 (launch classes 0, 1: H in (472, 3700], (303, 472]).
+  for (int j = 0; j < kLongClasses; ++j) {
     const int sc = kStreamClasses - 1 - j;
+    const int lo = j == 0 ? stream_class_hmax(sc - 1) : cols_hmax(0);
+    if (max_hap_len <= lo) continue;
     const int hmax = std::min(stream_class_hmax(sc), max_hap_len);
     hipStream_t st = fs[fork++ % kForkStreams];
     if (exact) {  // GKL operation order: the one-row kernel over the same range
@@ -601,6 +628,40 @@ int launch_phmm_forward(const PhmmDevBatch& b, const int32_t* order, int64_t cou
     const int rc = w >= 3 ? launch(phmm3_kernel<3>) : w == 2 ? launch(phmm3_kernel<2>) : launch(phmm3_kernel<1>);
     if (rc != FCS_OK) return rc;
   }
+  // The column-blocked kernel (phmm_cols.h): every other streamed pair, by
+  // columns per lane (launch classes kLongClasses .., widest first).
+  for (int c = 0; c < kColsLaunch; ++c) {
+    const int lo = c + 1 < kColsLaunch ? cols_hmax(c + 1) : 0;
+    if (max_hap_len <= lo) continue;
+    const int j = kLongClasses + c;
+    hipStream_t st = fs[fork++ % kForkStreams];
+    if (exact) {
+      const int rc = launch_one<float, true, false>(b, order, nullptr, count, bounds, j,
+                                                   nslot_for(std::min(cols_hmax(c), max_hap_len)), groups, t.tf, out,
+                                                   rescue_list, rescue_count, thr, use_rescue, st);
+      if (rc != FCS_OK) return rc;
+      continue;
+    }
+    const int K = cols_pairs_per_half(count);
+    // the range's last pairs run one per half-stream: about one round of the
+    // chip's wave slots (256 CUs x 4 SIMDs x 3 waves x 8 half-streams)
+    const int tail = 1024 * 3 * 8;
+    const unsigned grid = (unsigned)std::min<long long>(
+        std::max<long long>((count + 8 * K - 1) / (8 * K) + (tail + 7) / 8, 1), 65536);
+    auto launch = [&](auto kern) -> int {
+      hipLaunchKernelGGL(kern, dim3(grid), dim3(64), (size_t)kColsLds, st, b, order, bounds, j, K, tail, t.tf, out,
+                         rescue_list, rescue_count, thr, use_rescue ? 1 : 0, fb_list, fb_count);
+      FCS_HIP_CHECK(hipGetLastError());
+      return FCS_OK;
+    };
+    static_assert(cols_C(0) == 19 && cols_C(1) == 16 && cols_C(2) == 14 && cols_C(3) == 12 && kColsClasses == 4,
+                  "launch table below");
+    const int rc = c == 0   ? launch(phmm4_kernel<19>)
+                   : c == 1 ? launch(phmm4_kernel<16>)
+                   : c == 2 ? launch(phmm4_kernel<14>)
+                            : launch(phmm4_kernel<12>);
+    if (rc != FCS_OK) return rc;
+  }
   // Grouped classes (reads shorter than kStreamMinR or longer than kStreamMaxR; empty in most batches):
   // kept off fs[0], which carries the longest-haplotype stream class, so an
   // empty grouped launch does not extend the pass after it; and launched with
@@ -612,7 +673,7 @@ int launch_phmm_forward(const PhmmDevBatch& b, const int32_t* order, int64_t cou
   int gfork = 0;
   for (int j = kPhmmClasses - 1 - c_max; j < kPhmmClasses; ++j) {
     const int c = kPhmmClasses - 1 - j;
-    const int lc = kStreamClasses + j;  // launch class of grouped class c
+    const int lc = kLongClasses + kColsLaunch + j;  // launch class of grouped class c
     const int ns = (c == kPhmmClasses - 1) ? ns_max : std::min(224 + 32 * c, ns_max);
     hipStream_t st = fs[1 + gfork++ % (kForkStreams - 1)];
     // the two-rows-per-lane kernel (phmm2.h) for the FMA-order pass when its

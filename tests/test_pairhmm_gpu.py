@@ -517,3 +517,54 @@ def test_dev_path_forward_twice_after_one_schedule(gpu):
     assert counts[0] > 0 and counts[0] == counts[1]
     np.testing.assert_array_equal(results[0], results[1])
     check_parity(p, results[0], False)
+
+
+@pytest.mark.parametrize("k", [1, 5])
+def test_column_kernel_class_edges(gpu, tmp_path, k):
+    """The column-blocked kernel (phmm_cols.h): lane l owns columns l*C + 1 ..
+    l*C + C and a class holds H <= 16 C - 1, so the haplotype lengths at and
+    around every class edge (191/192, 223/224, 255/256, 303/304 -> the
+    row-streamed kernel) put column H + 1 (the V row's last summed column) in
+    lane 15's last column or the next class.  Reads R = 33 (the minimum) to
+    160, N bases on both sides, some reads unrelated so that the fp64 rescue
+    fires inside streams, and a haplotype with bytes outside ACGTN (handed
+    back to the byte-compare kernel); K pairs per half-stream forced."""
+    import subprocess
+    import sys
+    rng = np.random.default_rng(777 + k)
+    hl = [150, 191, 192, 223, 224, 255, 256, 300, 303, 304, 310]
+    haps = []
+    for H in hl:
+        h = rng.choice(np.frombuffer(b"ACGT", np.uint8), H)
+        h[rng.random(H) < 0.01] = ord("N")
+        haps.append(h)
+    haps[3] = haps[3].copy()
+    haps[3][::11] = ord("Y")
+    reads = []
+    for i in range(180):
+        R = int(rng.choice([33, 34, 60, 101, 151, 160]))
+        rd = list(rand_read(rng, R, n_frac=0.01))
+        if i % 7:
+            rd[0] = mutate(rng, haps[i % len(haps)], R)
+        else:
+            rd[1][:] = 40
+            rd[2][:] = rd[3][:] = 60
+        reads.append(tuple(rd))
+    p = fcship.make_pairs(reads, haps)
+    path = tmp_path / "edges.npz"
+    np.savez(path, **{f: getattr(p, f) for f in p.__dataclass_fields__})
+    code = (
+        "import sys; sys.path.insert(0, %r)\n"
+        "import numpy as np, fcship\n"
+        "d = np.load(sys.argv[1])\n"
+        "p = fcship.PhmmPairs(**{f: d[f] for f in d.files})\n"
+        "np.save(sys.argv[2], fcship.phmm_compute_pairs(p))\n"
+        "print('DONE')\n"
+    ) % fcship.__file__.rsplit("/", 1)[0]
+    env = dict(__import__("os").environ, FCSHIP_STREAM_K=str(k))
+    out = tmp_path / "edges_out.npy"
+    r = subprocess.run([sys.executable, "-c", code, str(path), str(out)], env=env, capture_output=True, text=True,
+                       timeout=120)
+    assert "DONE" in r.stdout, r.stderr[-3000:]
+    used = check_parity(p, np.load(out), False)
+    assert used.sum() > 0, "the fp64 rescue must run on some streamed pairs"
