@@ -56,7 +56,8 @@ constexpr int kColsRing = 32;
 constexpr int kColsChunks = 6;
 constexpr int kColsChunkBytes = kColsRing * 4 * 16;  // one chunk of every (slot, segment)
 constexpr int kColsCapOff = kColsChunks * kColsChunkBytes;  // lane 15's D per step of a block
-constexpr int kColsLds = kColsCapOff + 4 * 8 * 8;
+constexpr int kColsTabOff = kColsCapOff + 4 * 8 * 8;  // ph2pr | dmatch | dmis (3 x 128 floats) for the ring items
+constexpr int kColsLds = kColsTabOff + 3 * 128 * 4;
 
 // A constant materialised where it is used: left to the compiler, the
 // constants of the code conversion and the item builder are hoisted out of
@@ -172,7 +173,7 @@ __device__ __forceinline__ void cols_load(const uint8_t* __restrict__ hb, int64_
 template <int C>
 __global__ __launch_bounds__(64, 2) void phmm4_kernel(
     const PhmmDevBatch b, const int32_t* __restrict__ order, const int64_t* __restrict__ bounds, const int cls,
-    const int K, const int tail_pairs, const PhmmTables<float> tab, double* __restrict__ out,
+    const int K, const int tail_pairs, const PhmmTables<float> gtab, double* __restrict__ out,
     int32_t* __restrict__ rescue_list, unsigned long long* __restrict__ rescue_count, const float thr,
     const int use_rescue, int32_t* __restrict__ fb_list, unsigned long long* __restrict__ fb_count) {
   constexpr int NW = (C + 3) / 4;  // code dwords per half
@@ -186,6 +187,20 @@ __global__ __launch_bounds__(64, 2) void phmm4_kernel(
   const int64_t cbeg = bounds[cls];
   const long long count = bounds[cls + 1] - cbeg;
   order += cbeg;
+  // the ring items' small tables in LDS (matchToMatch stays in global
+  // memory): their lookups wait on LDS instead of the L2 (+1%)
+  PhmmTables<float> tab = gtab;
+  {
+    float* const t = reinterpret_cast<float*>(smem_raw + kColsTabOff);
+    for (int i = lane; i < 128; i += 64) {
+      t[i] = gtab.ph2pr[i];
+      t[128 + i] = gtab.dmatch[i];
+      t[256 + i] = gtab.dmis[i];
+    }
+    tab.ph2pr = t;
+    tab.dmatch = t + 128;
+    tab.dmis = t + 256;
+  }
   // Batches: 8 half-streams per wave, K pairs each, except the range's last
   // tail_pairs (shortest haplotypes), one pair per half-stream.
   const long long tailn = count < (long long)tail_pairs ? count : (long long)tail_pairs;
@@ -275,8 +290,18 @@ __global__ __launch_bounds__(64, 2) void phmm4_kernel(
       nk[h] = 0;
       swr[h] = valid(h, 0) ? tG(h, 0) : 0x3FFFFFFF;
     }
-    // Captures: lane 15 takes half h's sum at the V row of pair kc[h].
+    // Captures: lane 15 takes half h's sum at the V row of pair kc[h]
+    // (stream row cap[h], pair index capp[h], fallback flag from other[h]).
     int kc[2] = {0, 0};
+    int cap[2], capp[2];
+    auto load_cap = [&](int h) {
+      const bool ok = valid(h, kc[h]);
+      const int v = tG(h, kc[h]) + tR(h, kc[h]);
+      cap[h] = ok ? v : -0x3FFFFFFF;  // stream row of the V row
+      capp[h] = tP(h, kc[h]);
+    };
+    load_cap(0);
+    load_cap(1);
 
     // The ring's items (row g of half th per lane) in two stages one block
     // apart, so the read bytes' HBM latency is not paid inside a block:
@@ -286,18 +311,33 @@ __global__ __launch_bounds__(64, 2) void phmm4_kernel(
     RawRow praw{-1, 0, 0, 0, 0, 0, 0};
     int prole = 0;  // role | first << 4
     float pih = 0.f;
+    // the cursor pair's table entries, cached: the shuffles run only in the
+    // blocks where some lane's cursor moves (about one block in 13 on C2)
+    bool kok = false, nok = false;
+    int kG = 0, kR = 0, nG = 0;
+    float kI = 0.f;
+    int64_t kro = 0;
+    auto load_cursor = [&] {
+      kok = valid(th, kp);
+      kG = tG(th, kp);
+      kR = tR(th, kp);
+      kI = tI(th, kp);
+      kro = t64(rom, th, kp);
+      nok = valid(th, kp + 1);
+      nG = tG(th, kp + 1);
+    };
+    load_cursor();
     auto stage_a = [&](int base) {
       const int g = base + tk;
-#pragma unroll
-      for (int it = 0; it < 2; ++it) {  // pairs span >= 35 rows: at most one advance per 8 rows
-        const int gn = tG(th, kp + 1);
-        const bool vn = valid(th, kp + 1);
-        if (vn && g >= gn) ++kp;
+      const bool adv = nok && g >= nG;  // pairs span >= 35 rows: at most one advance per 8 rows
+      if (__ballot(adv) != 0ull) {
+        if (adv) ++kp;
+        load_cursor();
       }
-      const bool ok = valid(th, kp);
-      const int G = tG(th, kp), R = tR(th, kp);
-      pih = tI(th, kp);
-      const int64_t ro = t64(rom, th, kp);
+      const bool ok = kok;
+      const int G = kG, R = kR;
+      pih = kI;
+      const int64_t ro = kro;
       const int r = g - G;
       int role = 0;
       if (ok && r >= 0 && r < R) role = r == R - 1 ? 3 : 2;
@@ -356,22 +396,17 @@ __global__ __launch_bounds__(64, 2) void phmm4_kernel(
       stage_b(t0 + 8);
       stage_a(t0 + 16);
       // This block's captures (lane 15 at the V row of pair kc[h]) and switches.
-      int cap[2];
-      int capp[2];
-      bool capo[2];
 #pragma unroll
       for (int h = 0; h < 2; ++h) {
-        {
-          const bool ok = valid(h, kc[h]);
-          const int v = tG(h, kc[h]) + tR(h, kc[h]);
-          if (ok && v + 15 < t0) ++kc[h];
+        const bool adv = cap[h] >= 0 && cap[h] + 15 < t0;  // lane 15 passed the V row in an earlier block
+        if (__ballot(adv) != 0ull) {
+          if (adv) ++kc[h];
+          load_cap(h);
         }
-        const bool ok = valid(h, kc[h]);
-        const int v = tG(h, kc[h]) + tR(h, kc[h]);
-        cap[h] = ok ? v : -0x3FFFFFFF;  // stream row of the V row
-        capp[h] = tP(h, kc[h]);
-        capo[h] = (other[h] >> kc[h]) & 1u;
       }
+      bool capo[2];
+#pragma unroll
+      for (int h = 0; h < 2; ++h) capo[h] = (other[h] >> kc[h]) & 1u;
       const int g0 = t0 - sl;  // this lane's row at the block's first step
       const bool any_cap = __ballot(sl == 15 && ((unsigned)(cap[0] - g0) < 8u || (unsigned)(cap[1] - g0) < 8u)) != 0ull;
       // steps of this block at which some lane takes its next haplotype codes
