@@ -305,30 +305,31 @@ void finish_support(Pileup& pu) {
 // Query slice [qs, qe) of the read whose bases align inside [rb, re) (inserted
 // bases go with their left anchor); soft clips excluded.  false if empty.
 bool clip_to_window(const Read& rd, int64_t rb, int64_t re, size_t& qs, size_t& qe) {
+  // per CIGAR op: the query span whose anchors (the reference base of an M
+  // base; an inserted base's left neighbour) fall inside [rb, re); anchors
+  // never decrease along the read, so the taken bases form one slice
   int64_t rp = rd.pos, anchor = rd.pos - 1;
   size_t q = 0;
   bool started = false;
   qs = qe = 0;
-  auto take = [&](int64_t a, size_t qi) {
-    if (a >= rb && a < re) {
-      if (!started) {
-        qs = qi;
-        started = true;
-      }
-      qe = qi + 1;
-    }
+  auto take = [&](size_t a, size_t b) {  // query [a, b) taken
+    if (!started) qs = a, started = true;
+    qe = b;
   };
   for (uint32_t c : rd.cigar) {
     const uint32_t len = cigar_len(c);
     switch (cigar_op(c)) {
-      case kM: case kEq: case kX:
-        for (uint32_t k = 0; k < len; ++k, ++rp, ++q) {
-          anchor = rp;
-          take(rp, q);
-        }
+      case kM: case kEq: case kX: {
+        const int64_t lo = std::max<int64_t>(rp, rb), hi = std::min<int64_t>(rp + len, re);
+        if (lo < hi) take(q + (size_t)(lo - rp), q + (size_t)(hi - rp));
+        if (len) anchor = rp + len - 1;
+        rp += len;
+        q += len;
         break;
+      }
       case kI:
-        for (uint32_t k = 0; k < len; ++k, ++q) take(anchor, q);
+        if (len && anchor >= rb && anchor < re) take(q, q + len);
+        q += len;
         break;
       case kD: case kN: rp += len; anchor = rp - 1; break;
       case kS: q += len; break;
@@ -338,12 +339,29 @@ bool clip_to_window(const Read& rd, int64_t rb, int64_t re, size_t& qs, size_t& 
   return started && qe > qs;
 }
 
+// A region's prepared reads in one arena: per read the five rows gatk_prep
+// writes (bases, base_q, ins_q, del_q, gcp; n bytes each) back to back, so
+// preparing a read costs no allocation.
+struct PreparedSet {
+  std::vector<uint8_t> buf;
+  std::vector<std::pair<size_t, int32_t>> at;  // per read: offset in buf, length
+  size_t size() const { return at.size(); }
+  bool empty() const { return at.empty(); }
+  uint8_t* add(int32_t n) {
+    at.emplace_back(buf.size(), n);
+    buf.resize(buf.size() + 5 * (size_t)n);
+    return buf.data() + at.back().first;
+  }
+  int32_t len(size_t i) const { return at[i].second; }
+  const uint8_t* row(size_t i, int k) const { return buf.data() + at[i].first + (size_t)k * (size_t)at[i].second; }
+};
+
 struct Region {
   int64_t beg = 0, end = 0;  // reference window [beg, end)
   std::vector<Allele> cands;
   std::vector<std::string> haps;
   std::vector<uint32_t> hap_mask;  // bit c: haplotype carries candidate c
-  std::vector<PreparedRead> reads[2];  // [0] sample / tumor, [1] normal
+  PreparedSet reads[2];                // [0] sample / tumor, [1] normal
   std::vector<double> lik[2];          // read-major log10 likelihoods
 };
 
@@ -395,10 +413,10 @@ void dump_region(std::FILE* f, const Region& g, int s) {
   std::fwrite("RGN1", 1, 4, f);
   std::fwrite(&nr, 4, 1, f);
   std::fwrite(&nh, 4, 1, f);
-  for (const PreparedRead& r : g.reads[s]) {
-    const int32_t L = (int32_t)r.bases.size();
+  for (size_t i = 0; i < g.reads[s].size(); ++i) {
+    const int32_t L = g.reads[s].len(i);
     std::fwrite(&L, 4, 1, f);
-    for (const auto* v : {&r.bases, &r.base_q, &r.ins_q, &r.del_q, &r.gcp}) std::fwrite(v->data(), 1, L, f);
+    std::fwrite(g.reads[s].row(i, 0), 1, 5 * (size_t)L, f);  // the five rows, in dump order
   }
   for (const std::string& h : g.haps) {
     const int32_t L = (int32_t)h.size();
@@ -543,10 +561,12 @@ void run_phmm(std::vector<std::unique_ptr<Region>>& batch, const CallerOptions& 
       g.lik[s].assign(g.reads[s].size() * g.haps.size(), 0.0);
       if (g.reads[s].empty()) continue;
       rv.emplace_back();
-      for (const PreparedRead& r : g.reads[s]) {
-        rv.back().push_back({r.bases.data(), r.base_q.data(), r.ins_q.data(), r.del_q.data(), r.gcp.data(),
-                             (int32_t)r.bases.size()});
-        for (const std::string& h : g.haps) st.cells += (int64_t)r.bases.size() * (int64_t)h.size();
+      const PreparedSet& ps = g.reads[s];
+      int64_t hap_bases = 0;
+      for (const std::string& h : g.haps) hap_bases += (int64_t)h.size();
+      for (size_t r = 0; r < ps.size(); ++r) {
+        rv.back().push_back({ps.row(r, 0), ps.row(r, 1), ps.row(r, 2), ps.row(r, 3), ps.row(r, 4), ps.len(r)});
+        st.cells += (int64_t)ps.len(r) * hap_bases;
       }
       regs.push_back({rv.back().data(), (int32_t)rv.back().size(), hv[i].data(), (int32_t)hv[i].size(),
                       g.lik[s].data()});
@@ -1000,13 +1020,12 @@ CallerStats call_intervals(const Reference& ref, const std::vector<std::string>&
             const Read& rd = *ov[(size_t)x];
             size_t qs, qe;
             if (!clip_to_window(rd, g->beg, g->end, qs, qe) || qe - qs < 20) continue;
-            std::vector<uint8_t> q(rd.qual.begin() + qs, rd.qual.begin() + qe);
-            PreparedRead pr;
-            gatk_prepare_read(std::string(rd.seq.substr(qs, qe - qs)), q,
-                              rd.bi.empty() ? std::string() : std::string(rd.bi.substr(qs, qe - qs)),
-                              rd.bd.empty() ? std::string() : std::string(rd.bd.substr(qs, qe - qs)), rd.mapq, pr,
+            const size_t n = qe - qs;
+            if ((!rd.bi.empty() && rd.bi.size() != rd.seq.size()) || (!rd.bd.empty() && rd.bd.size() != rd.seq.size()))
+              throw invalidParam("BI/BD tag length differs from the read length");
+            gatk_prepare_read(rd.seq.data() + qs, rd.qual.p + qs, rd.bi.empty() ? nullptr : rd.bi.data() + qs,
+                              rd.bd.empty() ? nullptr : rd.bd.data() + qs, n, rd.mapq, g->reads[s].add((int32_t)n),
                               opt.base_quality_threshold, (PcrIndelModel)opt.pcr_indel_model);
-            g->reads[s].push_back(std::move(pr));
           }
         }
         if (g->reads[0].empty()) continue;

@@ -169,42 +169,61 @@ int pcr_indel_cap(int repeat_len, PcrIndelModel m) {
   return std::max(10, r);
 }
 
+void gatk_prepare_read(const char* bases, const uint8_t* quals, const char* bi, const char* bd, size_t n, int mapq,
+                       uint8_t* out, int thr, PcrIndelModel pcr) {
+  // the model's cap per repeat run length, one table per model
+  static const auto kCaps = [] {
+    std::array<std::array<uint8_t, kMaxRepeatLen + 1>, 4> t{};
+    for (int m = 0; m < 4; ++m)
+      for (int r = 0; r <= kMaxRepeatLen; ++r) t[m][r] = (uint8_t)std::min(255, pcr_indel_cap(r, (PcrIndelModel)m));
+    return t;
+  }();
+  uint8_t* const ob = out;
+  uint8_t* const oq = out + n;
+  uint8_t* const oi = out + 2 * n;
+  uint8_t* const od = out + 3 * n;
+  std::memcpy(ob, bases, n);
+  std::memset(out + 4 * n, kGatkGcp, n);
+  const int cap = std::max(0, std::min(mapq, 255));
+  // gap-open quals: the tag (phred+33) or 45, capped by the PCR model at
+  // positions 0 .. n - 2, then floored at 6 (as the vector form above did:
+  // the cap applies to the tag value's low byte)
+  const uint8_t* runs = nullptr;
+  if (pcr != PcrIndelModel::NONE && n > 1) {
+    thread_local std::vector<uint8_t> tl_runs;
+    tl_runs.resize(n);
+    tandem_repeat_runs(bases, (int)n, tl_runs.data());
+    runs = tl_runs.data();
+  }
+  const uint8_t* caps = kCaps[(int)pcr].data();
+  for (size_t i = 0; i < n; ++i) {
+    int ins = bi ? (int)(uint8_t)bi[i] - 33 : kGatkDefaultGop;
+    int del = bd ? (int)(uint8_t)bd[i] - 33 : kGatkDefaultGop;
+    if (runs && i + 1 < n) {
+      const int c = caps[runs[i]];
+      ins = std::min(ins & 0xFF, c);
+      del = std::min(del & 0xFF, c);
+    }
+    int q = std::min<int>(quals[i], cap);
+    if (q < thr) q = kGatkMinUsableQ;
+    oq[i] = (uint8_t)q;
+    oi[i] = (uint8_t)std::max(ins, kGatkMinUsableQ);
+    od[i] = (uint8_t)std::max(del, kGatkMinUsableQ);
+  }
+}
+
 void gatk_prepare_read(const std::string& bases, const std::vector<uint8_t>& quals, const std::string& bi,
                        const std::string& bd, int mapq, PreparedRead& out, int thr, PcrIndelModel pcr) {
   const size_t n = bases.size();
   if (quals.size() != n) throw invalidParam("read quals and bases differ in length");
   if ((!bi.empty() && bi.size() != n) || (!bd.empty() && bd.size() != n))
     throw invalidParam("BI/BD tag length differs from the read length");
-  out.bases.assign(bases.begin(), bases.end());
-  out.base_q.resize(n);
-  out.ins_q.resize(n);
-  out.del_q.resize(n);
-  out.gcp.assign(n, (uint8_t)kGatkGcp);
-  const int cap = std::max(0, std::min(mapq, 255));
-  std::vector<int> ins(n), del(n);
-  for (size_t i = 0; i < n; ++i) {
-    ins[i] = bi.empty() ? kGatkDefaultGop : (int)(uint8_t)bi[i] - 33;
-    del[i] = bd.empty() ? kGatkDefaultGop : (int)(uint8_t)bd[i] - 33;
-  }
-  if (pcr != PcrIndelModel::NONE) {
-    int cache[kMaxRepeatLen + 1];
-    for (int r = 0; r <= kMaxRepeatLen; ++r) cache[r] = pcr_indel_cap(r, pcr);
-    thread_local std::vector<uint8_t> tl_runs;
-    std::vector<uint8_t>& runs = tl_runs;
-    runs.resize(n);
-    tandem_repeat_runs(bases.data(), (int)n, runs.data());
-    for (size_t i = 1; i < n; ++i) {  // applyPCRErrorModel: positions 0 .. n - 2
-      const int c = cache[runs[i - 1]];
-      ins[i - 1] = std::min(ins[i - 1] & 0xFF, c);
-      del[i - 1] = std::min(del[i - 1] & 0xFF, c);
-    }
-  }
-  for (size_t i = 0; i < n; ++i) {
-    int q = std::min<int>(quals[i], cap);
-    if (q < thr) q = kGatkMinUsableQ;
-    out.base_q[i] = (uint8_t)q;
-    out.ins_q[i] = (uint8_t)std::max(ins[i], kGatkMinUsableQ);
-    out.del_q[i] = (uint8_t)std::max(del[i], kGatkMinUsableQ);
+  std::vector<uint8_t> rows(5 * n);
+  gatk_prepare_read(bases.data(), quals.data(), bi.empty() ? nullptr : bi.data(), bd.empty() ? nullptr : bd.data(), n,
+                    mapq, rows.data(), thr, pcr);
+  for (int k = 0; k < 5; ++k) {
+    std::vector<uint8_t>& v = k == 0 ? out.bases : k == 1 ? out.base_q : k == 2 ? out.ins_q : k == 3 ? out.del_q : out.gcp;
+    v.assign(rows.begin() + (std::ptrdiff_t)(k * n), rows.begin() + (std::ptrdiff_t)((k + 1) * n));
   }
 }
 

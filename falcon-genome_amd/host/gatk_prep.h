@@ -45,6 +45,13 @@ struct PreparedRead {
   std::vector<uint8_t> bases, base_q, ins_q, del_q, gcp;
 };
 
+// The five prepared rows of one read, n bytes each, back to back at out:
+// bases, base_q, ins_q, del_q, gcp (the caller's arena form; no allocation).
+// bi / bd: n phred+33 bytes, or null when the tag is absent.
+void gatk_prepare_read(const char* bases, const uint8_t* quals, const char* bi, const char* bd, size_t n, int mapq,
+                       uint8_t* out, int base_qual_threshold = kGatkBaseQualThreshold,
+                       PcrIndelModel pcr = PcrIndelModel::CONSERVATIVE);
+
 // bases: read bases (ASCII); quals: phred (no offset); bi / bd: BI / BD tag
 // strings (phred+33) or empty when absent; mapq: mapping quality.
 void gatk_prepare_read(const std::string& bases, const std::vector<uint8_t>& quals, const std::string& bi,
