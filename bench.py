@@ -757,8 +757,10 @@ def cpu_baseline_bsw_align(tasks, gpu, xtra, budget_s, threads):
               "against": "oracle/ksw_align_sse.c (bwa's striped SSE2 ksw_align2 restated) on the whole sample, and "
                          "oracle/ksw_align_oracle.c (its element-wise emulation) on the leading tasks"}
     return dict(value=cells / min(times) / 1e9, unit="GCUPS", cores=threads, kind="port",
-                sample=f"first {n} of the {tasks.n} timed tasks, bwa's striped SSE2 ksw_align2 restated (16 x u8 "
-                       f"lanes per instruction for these XBYTE tasks), OpenMP {threads} threads (nproc "
+                sample=f"first {n} of the {tasks.n} timed tasks, bwa's striped SSE2 ksw_align2 restated ("
+                       + ("16 x u8 lanes per instruction for these XBYTE tasks" if xtra & 0x10000 else
+                          "8 x i16 lanes per instruction for these tasks without XBYTE")
+                       + f"), OpenMP {threads} threads (nproc "
                        f"{os.cpu_count()}), best of 3 ({', '.join(f'{t:.2f}' for t in times)} s)"), parity
 
 
@@ -1092,11 +1094,22 @@ def main():
                 "achieved": round(ach / 1e12, 3), "frac": round(ach / VALU_LANE_INSTR_PEAK, 4),
                 "valu_instr_per_cell": vpc,
                 "valu_source": f"profiles/pmc_bsw.json align ({am.get('source', '')}: SQ_INSTS_VALU x 64 / cells)"}
+        # the same windows as bwa's i16 tasks (no KSW_XBYTE: mem_matesw's case for
+        # l_ms * a >= 250, here forced on 151 bp reads to time the 16-bit path)
+        x16 = 0x40000 | 0x80000 | 19
+        g16 = bench_bsw_align(args, dev, al, x16)
+        line["bsw"]["align"]["i16"] = {
+            "workload": "the same tasks with xtra = XSUBO | XSTART | 19 (bwa's ksw_i16: 8 lanes, 16-bit saturation)",
+            "ms": round(g16["ms"], 3), "gcups": round(g16["gcups"], 3), "cells": g16["cells"],
+            "kernel": "bsw_align_kernel<16, 10, true> (i16 tasks on the packed path: scores of a <= 160-base query "
+                      "stay below 160 x max_mat, so the biased scan values of bwa's 8 blocks fit 16-bit halves)"}
         if world == 1 and not args.no_cpu_baseline:
             line["bsw"]["cpu_baseline"], line["bsw"]["parity"] = cpu_baseline_bsw(c3, r3, args.cpu_budget,
                                                                                   cpu_threads())
             line["bsw"]["align"]["cpu_baseline"], line["bsw"]["align"]["parity"] = cpu_baseline_bsw_align(
                 al, ga, xa, min(args.cpu_budget, 6.0), cpu_threads())
+            line["bsw"]["align"]["i16"]["cpu_baseline"], line["bsw"]["align"]["i16"]["parity"] = \
+                cpu_baseline_bsw_align(al, g16, x16, min(args.cpu_budget, 4.0), cpu_threads())
 
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         line["cpu_baseline"], ref, used_d = cpu_baseline_phmm(p, args.cpu_budget, cpu_threads())

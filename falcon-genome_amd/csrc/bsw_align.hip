@@ -252,16 +252,20 @@ __device__ AlignRun align_run(const BswParams& p, bool live, int qlen, QAt q_at,
   return r;
 }
 
-// ---------------------------------------------------------------- packed u8
-// bwa's ksw_u8 tasks (XBYTE: every H, E, M' in [0, 255]) in 16-lane groups, on
-// pairs of positions in packed 16-bit halves: lane l's ten positions
-// x = 10 l + k sit in five registers, lo half k = j, hi half k = j + 5, so one
-// VOP3P instruction does two cells.  The scan values are biased to stay
-// non-negative (c2 = x e_ins + 1, c1 = c2 + block * big with big = 257 + 159
-// e_ins > the spread of one block's values), so 0 is the scan's empty value
-// and the signed differences ex - c fit in 16 bits while
-// 16 big + o_ins < 32768 (align_packed_ok).  Same recurrence, same results as
-// align_run<16, 10> (tests/test_bsw_gpu.py).
+// ---------------------------------------------------------------- packed
+// bwa's ksw_u8 tasks (XBYTE: every H, E, M' in [0, 255]) and ksw_i16 tasks in
+// 16-lane groups, on pairs of positions in packed 16-bit halves: lane l's ten
+// positions x = 10 l + k sit in five registers, lo half k = j, hi half
+// k = j + 5, so one VOP3P instruction does two cells.  The scan values are
+// biased to stay non-negative (c2 = x e_ins + 1, c1 = c2 + block * big with
+// big = Mmax + 2 + 159 e_ins > the spread of one block's values, Mmax the
+// largest H / E / M'), so 0 is the scan's empty value and the signed
+// differences ex - c fit in 16 bits while blocks * big + o_ins < 32768
+// (align_packed_ok; 16 blocks for u8, 8 for i16).  u8: Mmax = 255.  i16: a
+// local score never exceeds qlen * max_mat (each query base adds at most
+// max_mat), so Mmax = 160 max_mat for the queries of the 16-lane groups, far
+// below bwa's 16-bit saturation, which therefore never acts.  Same recurrence,
+// same results as align_run<16, 10> (tests/test_bsw_gpu.py).
 typedef uint16_t au16x2 __attribute__((ext_vector_type(2)));
 typedef int16_t ai16x2 __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ au16x2 AV(uint32_t x) { return __builtin_bit_cast(au16x2, x); }
@@ -283,19 +287,24 @@ __device__ __forceinline__ uint32_t ap_subs(uint32_t a, uint32_t b) {
   return AU(__builtin_elementwise_sub_sat(AV(a), AV(b)));
 }
 
-__host__ __device__ inline int align_packed_big(int e_ins) { return 257 + 159 * e_ins; }
-__host__ __device__ inline bool align_packed_ok(int o_ins, int e_ins) {
-  return o_ins >= 0 && e_ins >= 0 && e_ins <= 200 && 16 * align_packed_big(e_ins) + o_ins + 1 < 32768;
+// Mmax: 255 (u8) or kAlignSegQ * max_mat (i16); blocks: 16 (u8) or 8 (i16)
+__host__ __device__ inline int align_packed_big(int mmax, int e_ins) { return mmax + 2 + 159 * e_ins; }
+__host__ __device__ inline int align_i16_mmax(int max_mat) { return kAlignSegQ * (max_mat > 0 ? max_mat : 0); }
+__host__ __device__ inline bool align_packed_ok(int mmax, int blocks, int o_ins, int e_ins) {
+  return o_ins >= 0 && e_ins >= 0 && e_ins <= 200 && mmax <= 8192 &&
+         blocks * align_packed_big(mmax, e_ins) + o_ins + 1 < 32768;
 }
 
 template <class QAt, class TAt>
-__device__ AlignRun align_run_u8p(const BswParams& p, bool live, int qlen, QAt q_at, int tlen, TAt t_at, int shift,
-                                  int max_mat, int minsc, int endsc, uint32_t* __restrict__ blist) {
+__device__ AlignRun align_run_pk(const BswParams& p, bool live, int qlen, QAt q_at, int tlen, TAt t_at, bool u8,
+                                 int shift, int max_mat, int minsc, int endsc, uint32_t* __restrict__ blist) {
   constexpr int W = 16, NK = 10, NP = 5;
   const int gl = grp_lane<W>();
-  const int slen = (qlen + 15) / 16;
-  const int nlen = live ? slen * 16 : 0;
-  const int big = align_packed_big(p.e_ins);
+  const int pl = u8 ? 16 : 8;
+  const int slen = (qlen + pl - 1) / pl;
+  const int nlen = live ? slen * pl : 0;
+  const int big = align_packed_big(u8 ? 255 : align_i16_mmax(max_mat), p.e_ins);
+  const int mtop = u8 ? 255 - shift : 0x7FFF;  // u8: bwa's saturation at 255 (biased); i16: never reached
   // c1 / c2: the scan offsets; o1 / o2 = c + o_ins (f = ex - c - o_ins).
   // Positions past nlen (the group's last lanes, when slen < 10) feed only
   // later such positions; mh = 0 there (M = 0), no block term in c1 (so every
@@ -313,13 +322,13 @@ __device__ AlignRun align_run_u8p(const BswParams& p, bool live, int qlen, QAt q
       plo[k] = sc(0) | (sc(1) << 8) | (sc(2) << 16) | (sc(3) << 24);
       const bool in = x < nlen;
       const int cc2 = x * p.e_ins + 1;
-      const int cc1 = in ? cc2 + (x / slen) * big : cc2;  // block ids < 16 inside nlen only
+      const int cc1 = in ? cc2 + (x / slen) * big : cc2;  // block ids < pl inside nlen only
       n2 |= sc(4) << (16 * h);
       a1 |= (uint32_t)cc1 << (16 * h);
       a2 |= (uint32_t)cc2 << (16 * h);
       b1 |= (uint32_t)(in ? cc1 + p.o_ins : 0x7FFF) << (16 * h);
       b2 |= (uint32_t)(in ? cc2 + p.o_ins : 0x7FFF) << (16 * h);
-      m2 |= (uint32_t)(in ? 255 - shift : 0) << (16 * h);
+      m2 |= (uint32_t)(in ? mtop : 0) << (16 * h);
     }
     phi[j] = n2, c1[j] = a1, c2[j] = a2, o1[j] = b1, o2[j] = b2, mh[j] = m2;
     H[j] = E[j] = Hm[j] = 0;
@@ -390,13 +399,13 @@ __device__ AlignRun align_run_u8p(const BswParams& p, bool live, int qlen, QAt q
       te = i;
 #pragma unroll
       for (int j = 0; j < NP; ++j) Hm[j] = Hn[j];
-      if (gmax + shift >= 255 || gmax >= endsc) run = false;
+      if ((u8 && gmax + shift >= 255) || gmax >= endsc) run = false;
     }
     if (!(i + 1 < tlen)) run = false;
   }
-  AlignRun r{gmax + shift < 255 ? gmax : 255, te, -1, -1, -1};
+  AlignRun r{!u8 || gmax + shift < 255 ? gmax : 255, te, -1, -1, -1};
   __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
-  const bool tail = live && r.score != 255;
+  const bool tail = live && (!u8 || r.score != 255);
   int mx = -1, qx = 0x7FFFFFFF;
 #pragma unroll
   for (int j = 0; j < NP; ++j)
@@ -440,7 +449,9 @@ __device__ AlignRun align_run_u8p(const BswParams& p, bool live, int qlen, QAt q
 // seg_q, the 64-lane launch the longer ones.  LDS per group: b[] (2 B per
 // target base) and the target.  pk: 0 every task of the launch, 1 (the PK
 // kernel) the waves whose 16-lane tasks are all u8, 2 the other waves; both
-// launches see the same per-wave test.
+// launches see the same per-wave test.  (When the gap costs and matrix keep
+// the i16 tasks' scan values in 16 bits, the PK kernel takes every 16-lane
+// task with pk = 0 and the 32-bit 16-lane launch is not made.)
 template <int W, int NK, bool PK>
 __global__ __launch_bounds__(64) void bsw_align_kernel(const BswDevBatch b, const BswParams p,
                                                        const int32_t* __restrict__ xtra, int32_t* __restrict__ out,
@@ -476,7 +487,7 @@ __global__ __launch_bounds__(64) void bsw_align_kernel(const BswDevBatch b, cons
     auto qf = [&](int x) { return (int)q[x]; };
     auto tf = [&](int j) { return (int)tl[j]; };
     AlignRun r;
-    if constexpr (PK) r = align_run_u8p(p, mine, qlen, qf, tlen, tf, shift, mxm, minsc, endsc, blist);
+    if constexpr (PK) r = align_run_pk(p, mine, qlen, qf, tlen, tf, u8, shift, mxm, minsc, endsc, blist);
     else r = align_run<W, NK>(p, mine, qlen, qf, tlen, tf, u8, shift, mxm, minsc, endsc, blist);
     __syncthreads();  // the first pass's b[] reads before the second pass (which appends nothing)
     // bwa: reverse query[0, qe] and target[0, te] in place (the rest of the
@@ -486,7 +497,7 @@ __global__ __launch_bounds__(64) void bsw_align_kernel(const BswDevBatch b, cons
     auto qr = [&](int x) { return (int)q[qe - x]; };
     auto tr = [&](int j) { return (int)tl[j <= te ? te - j : j]; };
     AlignRun rr;
-    if constexpr (PK) rr = align_run_u8p(p, second, qe + 1, qr, tlen, tr, shift, mxm, 0x10000, r.score, blist);
+    if constexpr (PK) rr = align_run_pk(p, second, qe + 1, qr, tlen, tr, u8, shift, mxm, 0x10000, r.score, blist);
     else rr = align_run<W, NK>(p, second, qe + 1, qr, tlen, tr, u8, shift, mxm, 0x10000, r.score, blist);
     int tb = -1, qb = -1;
     if (second && rr.score == r.score) tb = r.te - rr.te, qb = r.qe - rr.qe;
@@ -536,17 +547,22 @@ int launch_bsw_align(const BswDevBatch& b, const BswParams& p, const int32_t* xt
   };
   int rc = FCS_OK;
   // 16-lane tasks: the packed kernel takes the waves of u8 tasks (when the gap
-  // costs keep its 16-bit scan values in range), the 32-bit kernel the rest
+  // costs keep its 16-bit scan values in range) and, when the i16 tasks' range
+  // fits as well, every wave; otherwise the 32-bit kernel takes the rest
   // (skipped when the caller knows every task is u8)
-  const bool packed = seg && align_packed_ok(p.o_ins, p.e_ins);
+  int max_mat = 0;
+  for (int a = 0; a < 25; ++a) max_mat = std::max(max_mat, (int)p.mat[a]);
+  const bool packed = seg && align_packed_ok(255, 16, p.o_ins, p.e_ins);
+  const bool packed16 = packed && align_packed_ok(align_i16_mmax(max_mat), 8, p.o_ins, p.e_ins);
   // one workgroup per four tasks (per task for W = 64): the dispatcher
   // balances the uneven task lengths and early exits
   const unsigned grid16 = (unsigned)std::min<long long>((b.n + 3) / 4, kAlignGridCap);
   if (packed)
     rc = go((const void*)bsw_align_kernel<16, 10, true>, grid16, lds16, [&](unsigned grid, size_t lds) {
-      hipLaunchKernelGGL((bsw_align_kernel<16, 10, true>), dim3(grid), dim3(64), lds, s, b, p, xtra, out, mt, seg_q, 1);
+      hipLaunchKernelGGL((bsw_align_kernel<16, 10, true>), dim3(grid), dim3(64), lds, s, b, p, xtra, out, mt, seg_q,
+                         packed16 ? 0 : 1);
     });
-  if (rc == FCS_OK && seg && !(packed && all_u8))
+  if (rc == FCS_OK && seg && !(packed && (all_u8 || packed16)))
     rc = go((const void*)bsw_align_kernel<16, 10, false>, grid16, lds16, [&](unsigned grid, size_t lds) {
       hipLaunchKernelGGL((bsw_align_kernel<16, 10, false>), dim3(grid), dim3(64), lds, s, b, p, xtra, out, mt, seg_q,
                          packed ? 2 : 0);

@@ -233,7 +233,7 @@ constexpr int kPhmmKeyBits = 16;
 constexpr int kStreamClasses = 4;
 constexpr int kPhmmClasses = 6;
 constexpr int kLongClasses = 2;  // phmm3 stream classes 3 and 2 (H <= 3700, <= 472)
-constexpr int kColsLaunch = 4;   // phmm_cols.h classes (H <= 303 .. <= 191)
+constexpr int kColsLaunch = 8;   // phmm_cols.h classes (H <= 303, <= 271, .., <= 175)
 constexpr int kPhmmLaunchClasses = kLongClasses + kColsLaunch + kPhmmClasses;
 // Sorted schedule: one launch over the lane (0..9) and pair (kBswPairBucket0..+4)
 // buckets, then the wave-per-task kernel over kBswWideBucket.

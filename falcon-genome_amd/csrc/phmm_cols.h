@@ -34,10 +34,10 @@
 
 namespace fcs {
 
-constexpr int kColsClasses = 4;
+constexpr int kColsClasses = 8;
 constexpr int kColsMinR = 33;  // the next pair's haplotype codes are converted >= 16 rows after a switch
 // Columns per lane of launch class c (longest haplotypes first): H <= 16 C - 1.
-__host__ __device__ constexpr int cols_C(int c) { return c == 0 ? 19 : c == 1 ? 16 : c == 2 ? 14 : 12; }
+__host__ __device__ constexpr int cols_C(int c) { return c == 0 ? 19 : 18 - c; }  // 19, 17, 16, .., 11
 __host__ __device__ constexpr int cols_hmax(int c) { return 16 * cols_C(c) - 1; }
 // The smallest class that holds H (-1: none).
 __host__ __device__ inline int cols_class(int H) {

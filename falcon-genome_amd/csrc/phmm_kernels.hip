@@ -654,12 +654,18 @@ int launch_phmm_forward(const PhmmDevBatch& b, const int32_t* order, int64_t cou
       FCS_HIP_CHECK(hipGetLastError());
       return FCS_OK;
     };
-    static_assert(cols_C(0) == 19 && cols_C(1) == 16 && cols_C(2) == 14 && cols_C(3) == 12 && kColsClasses == 4,
-                  "launch table below");
-    const int rc = c == 0   ? launch(phmm4_kernel<19>)
-                   : c == 1 ? launch(phmm4_kernel<16>)
-                   : c == 2 ? launch(phmm4_kernel<14>)
-                            : launch(phmm4_kernel<12>);
+    static_assert(cols_C(0) == 19 && cols_C(1) == 17 && cols_C(7) == 11 && kColsClasses == 8, "launch table below");
+    int rc;
+    switch (cols_C(c)) {
+      case 19: rc = launch(phmm4_kernel<19>); break;
+      case 17: rc = launch(phmm4_kernel<17>); break;
+      case 16: rc = launch(phmm4_kernel<16>); break;
+      case 15: rc = launch(phmm4_kernel<15>); break;
+      case 14: rc = launch(phmm4_kernel<14>); break;
+      case 13: rc = launch(phmm4_kernel<13>); break;
+      case 12: rc = launch(phmm4_kernel<12>); break;
+      default: rc = launch(phmm4_kernel<11>); break;
+    }
     if (rc != FCS_OK) return rc;
   }
   // Grouped classes (reads shorter than kStreamMinR or longer than kStreamMaxR; empty in most batches):

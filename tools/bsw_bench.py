@@ -23,7 +23,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--reads", type=int, default=500_000)
     ap.add_argument("--seed", type=int, default=20261015)
-    ap.add_argument("--which", default="both", choices=["c3", "fixed", "both", "global", "align"])
+    ap.add_argument("--which", default="both", choices=["c3", "fixed", "both", "global", "align", "align16"])
     ap.add_argument("--reps", type=int, default=3)
     args = ap.parse_args()
     dev = torch.device("cuda", 0)
@@ -42,11 +42,13 @@ def main():
         t = fcship.synth_bsw(args.seed + 2, args.reads // 2, read_len=151, ref_len=10_000_000, w=16, mode=1,
                              fixed_q=151, fixed_t=151)
         out["global"] = bench.bench_bsw_global(args, dev, t, reps=args.reps)
-    if args.which == "align":  # bench.py's ksw_align2 (mate rescue) workload
+    if args.which in ("align", "align16"):  # bench.py's ksw_align2 (mate rescue) workload, u8 or i16 tasks
         t = fcship.synth_bsw(args.seed + 3, args.reads // 4, read_len=151, ref_len=10_000_000, w=100, mode=1,
                              fixed_q=151, fixed_t=600)
-        r = bench.bench_bsw_align(args, dev, t, 0x40000 | 0x80000 | 0x10000 | 19, reps=args.reps)
-        out["align"] = {k: (round(v, 3) if isinstance(v, float) else v) for k, v in r.items() if not hasattr(v, "shape")}
+        xt = 0x40000 | 0x80000 | (0x10000 if args.which == "align" else 0) | 19
+        r = bench.bench_bsw_align(args, dev, t, xt, reps=args.reps)
+        out[args.which] = {k: (round(v, 3) if isinstance(v, float) else v) for k, v in r.items()
+                           if not hasattr(v, "shape")}
     print(json.dumps(out))
 
 
