@@ -237,11 +237,27 @@ int launch_bsw_extend_wide(const BswDevBatch& b, const BswParams& p, int max_qle
 // keeps bwa's boundary values (H(i, -1) = -(o_del + e_del (i + 1)), E = -inf
 // past the band end, F = -inf entering it).  Query codes ride through the band
 // as bytes (5 * code, the bit offset of the score in the target's packed
-// matrix row) shifted one byte per row.  Directions are stored as nibbles
-// (h source | E-continue << 2 | F-continue << 3), one row of the task's band
-// in ceil((2w + 1) / 8) dwords, inside the task's own min(qlen, 2w + 1) * tlen
+// matrix row) shifted one byte per row.  Directions are stored as nibbles of
+// raw compare bits (M < E, max(M, E) < F, E-continue, F-continue), cell c of a
+// dword in bits 28 - 4c .. 31 - 4c (each bit is the sign of a difference,
+// shifted in by one v_alignbit_b32), one row of the task's band in
+// ceil((2w + 1) / 8) dwords, inside the task's own min(qlen, 2w + 1) * tlen
 // bytes of the direction matrix; the traceback maps bwa's byte index onto
 // them.  Tasks outside these bounds take the wave-per-task kernel below.
+//
+// Every row runs the same unmasked cell sequence over all NB slots.  Slots
+// outside a lane's band compute values no band cell reads, except three, set
+// up so the unmasked recurrence reproduces bwa's boundaries:
+//   * column -1 (left of the band in the first w rows): its E entering row 0
+//     is -(o_del + e_del) and the columns left of it hold -inf, so E, and with
+//     it H, run down column -1 as bwa's H(i, -1) = -(o_del + e_del (i + 1)),
+//     and the F entering column 0 from it is -inf plus a few gap costs, which
+//     no compare against a band cell can tell from bwa's -inf;
+//   * slot 2w + 1 of a lane whose band is narrower than NB: its E is reset to
+//     -inf after each row (bwa's eh[end].e), the only value it passes back;
+//   * columns >= qlen pass nothing back (F runs right, E down its own column,
+//     the diagonal right), and the score, bwa's eh[qlen].h, is read from the
+//     last row's slot qlen - 1 - i + w.
 constexpr int kGLaneMaxNB = 65;
 __host__ __device__ __forceinline__ bool glane_ok(int qlen, int tlen, int w, bool mat_ok) {
   const int nb = 2 * w + 1;
@@ -330,8 +346,9 @@ __device__ __forceinline__ void glane_traceback(const GLayout& L, int qlen, int 
       crow = r, cdw = dw;
       cval = L.base[(long long)r * L.rs + dw * L.ds];
     }
-    const int nbl = (int)((cval >> (4 * (kb & 7))) & 15u);
-    return (nbl & 3) | ((nbl >> 2) & 1) << 2 | ((nbl >> 3) & 1) << 5;
+    const int nbl = (int)((cval >> (28 - 4 * (kb & 7))) & 15u);
+    // bits: M < E, max(M, E) < F, E-continue, F-continue -> bwa's direction byte
+    return ((nbl & 2) ? 2 : (nbl & 1)) | ((nbl >> 2) & 1) << 2 | ((nbl >> 3) & 1) << 5;
   };
   int n = 0, which = 0, curop = -1;
   uint32_t curlen = 0;
@@ -370,66 +387,46 @@ __device__ __forceinline__ void glane_traceback(const GLayout& L, int qlen, int 
   *n_out = n;
 }
 
-// The row's direction bits and the masked row's band selects as sign-bit
-// arithmetic and v_bitop3_b32 selects (full rate) instead of compares feeding
-// v_cndmask (the compiler's VOP2 form costs ~7 extra cycles each in a mix,
-// profiles/r3/gfx950_sq_counters.txt) and per-cell branches.  Every score stays
-// within +-2^30 + 2^10, so the differences never overflow: (uint32)(a - b) >> 31
-// is exactly a < b.
-
-__device__ __forceinline__ int gsel(int mask, int a, int b) {  // mask ? a : b, mask all-ones or zero
-  int r;
-  asm("v_bitop3_b32 %0, %1, %2, %3 bitop3:0xe4" : "=v"(r) : "v"(a), "v"(b), "v"(mask));  // as phmm's sel_v
+// The row's direction bits are signs of differences (every score stays within
+// +-2^30 + 2^10, so a difference never overflows: (uint32)(a - b) >> 31 is
+// exactly a < b), shifted into the row's dwords by v_alignbit_b32 (acc << 1 |
+// x >> 31, one full-rate instruction per bit; the compiler's compare +
+// v_cndmask for the same shift costs two).
+__device__ __forceinline__ uint32_t gbit(uint32_t acc, int x) {
+  uint32_t r;
+  asm("v_alignbit_b32 %0, %1, %2, 31" : "=v"(r) : "v"(acc), "v"(x));
   return r;
 }
 
-template <int NB, bool CIG, bool MASKED>
+template <int NB, bool CIG>
 __device__ __forceinline__ void glane_row(int (&Hd)[NB], int (&Ed)[NB + 1], const uint32_t (&Qb)[(NB + 4) / 4],
-                                          uint32_t (&nib)[(NB + 7) / 8], const int rowpack, const int lo,
-                                          const int hi, const int hb, const int oe_del, const int oe_ins,
-                                          const int e_del, const int e_ins, int& h1) {
+                                          uint32_t (&nib)[(NB + 7) / 8], const int rowpack, const int oe_del,
+                                          const int oe_ins, const int e_del, const int e_ins) {
   int f = kMinusInf;
-  const int minf = kMinusInf;
+  uint32_t acc = 0;
 #pragma unroll
   for (int k = 0; k < NB; ++k) {
     const int qoff = (int)((Qb[k >> 2] >> (8 * (k & 3))) & 0xFFu);
     const int s = __builtin_amdgcn_sbfe(rowpack, qoff, 5);
     const int m = Hd[k] + s;
-    int e = Ed[k + 1];
-    uint32_t d = 0;
-    if constexpr (CIG) d = (uint32_t)(m - e) >> 31;  // m < e: H from E
-    int h = max(m, e);
+    const int e0 = Ed[k + 1];
+    const int h1 = max(m, e0);
+    const int h = max(h1, f);
+    const int td = m - oe_del, ti = m - oe_ins;
+    const int e = e0 - e_del;
+    const int fn = f - e_ins;
     if constexpr (CIG) {
-      const int ltf = (h - f) >> 31;  // h < f: H from F
-      d = (uint32_t)gsel(ltf, 2, (int)d);
+      acc = gbit(acc, ti - fn);  // F-continue: f - e_ins > M - oe_ins
+      acc = gbit(acc, td - e);   // E-continue: e - e_del > M - oe_del
+      acc = gbit(acc, h1 - f);   // max(M, E) < F: H from F
+      acc = gbit(acc, m - e0);   // M < E: H from E
+      if ((k & 7) == 7) nib[k >> 3] = acc;
     }
-    h = max(h, f);
-    int t = m - oe_del;
-    e -= e_del;
-    if constexpr (CIG) d |= ((uint32_t)(t - e) >> 31) << 2;  // e > t
-    e = max(e, t);
-    t = m - oe_ins;
-    int fn = f - e_ins;
-    if constexpr (CIG) d |= ((uint32_t)(t - fn) >> 31) << 3;  // fn > t
-    fn = max(fn, t);
-    if constexpr (MASKED) {
-      const int below = (k - lo) >> 31;                  // k < lo
-      const int vm = ~((k - lo) | (hi - 1 - k)) >> 31;   // lo <= k < hi
-      Hd[k] = gsel(vm, h, gsel(below, hb, Hd[k]));
-      Ed[k] = gsel(vm, e, minf);
-      f = gsel(vm, fn, minf);
-      h1 = gsel(vm, h, h1);
-    } else {
-      Hd[k] = h;
-      Ed[k] = e;
-      f = fn;
-      if (k == NB - 1) h1 = h;
-    }
-    if constexpr (CIG) {
-      if ((k & 7) == 0) nib[k >> 3] = (uint32_t)d;
-      else nib[k >> 3] |= (uint32_t)d << (4 * (k & 7));
-    }
+    Hd[k] = h;
+    Ed[k] = max(e, td);
+    f = max(fn, ti);
   }
+  if constexpr (CIG && (NB & 7) != 0) nib[NB >> 3] = acc << (4 * (8 - (NB & 7)));  // the row's last cells to the top
 }
 
 template <int NB, bool CIG>
@@ -455,7 +452,16 @@ __device__ void glane_run(const BswDevBatch& b, const BswParams& p, long long ta
   if constexpr (CIG) zl = glane_layout(b, p, zbuf, zoff, task, ok);
   int Hd[NB], Ed[NB + 1];
   uint32_t Qb[NQ], nib[NW];
-  auto qbyte = [&](int j) -> uint32_t { return (ok && j >= 0 && j < qlen) ? 5u * (uint32_t)q[j] : 0u; };
+  // every lane loads every row (a clamped index into a valid buffer) and
+  // selects afterwards: a load under a branch makes the compiler wait for all
+  // outstanding loads at the next use, which serialised the row-ahead reads
+  const uint8_t* __restrict__ qp = ok ? q : b.qbuf;
+  const uint8_t* __restrict__ tp = ok ? tg : b.tbuf;
+  const int qlast = max(qlen - 1, 0);
+  auto qbyte = [&](int j) -> uint32_t {
+    const uint32_t v = qp[min(max(j, 0), qlast)];
+    return (ok && j >= 0 && j < qlen) ? 5u * v : 0u;
+  };
 #pragma unroll
   for (int k = 0; k < NB; ++k) {
     const int j = k - w;  // column of slot k in row 0; Hd holds "H(-1, j - 1)" = bwa's first-row eh[j].h
@@ -473,44 +479,101 @@ __device__ void glane_run(const BswDevBatch& b, const BswParams& p, long long ta
   }
 #pragma unroll
   for (int d = 0; d < NW; ++d) nib[d] = 0;
-  int h1 = kMinusInf;
-  int tb_next = (ok && tlen > 0) ? (int)tg[0] : 4;
-  uint32_t qn_next = qbyte(NB + 1 - w);  // byte NB of row 1
-  for (int i = 0; i < tmax; ++i) {
-    const int tb = tb_next;
-    const uint32_t qn = qn_next;
-    tb_next = (ok && i + 1 < tlen) ? (int)tg[i + 1] : 4;  // next row's inputs in flight during this row
-    qn_next = qbyte(i + NB + 2 - w);
-    const int rowpack = tb == 0 ? p.matpack[0] : tb == 1 ? p.matpack[1] : tb == 2 ? p.matpack[2]
-                      : tb == 3 ? p.matpack[3] : p.matpack[4];
-    const bool live = ok && i < tlen;
-    const int lo = live ? w - i : NB;
-    const int hi = live ? min(nb, qlen - i + w) : 0;
-    const int hb = -(p.o_del + e_del * (i + 1));
-    // bwa's h1 at the row start: H(i, -1) when the band starts at column 0,
-    // else -inf; an empty band leaves it in eh[end].h (lanes past their last
-    // row keep their final value)
-    if (live) h1 = lo >= 0 ? hb : kMinusInf;
-    const bool full = __ballot(!(lo <= 0 && hi >= NB)) == 0ull;
-    if (full)
-      glane_row<NB, CIG, false>(Hd, Ed, Qb, nib, rowpack, lo, hi, hb, oe_del, oe_ins, e_del, e_ins, h1);
-    else
-      glane_row<NB, CIG, true>(Hd, Ed, Qb, nib, rowpack, lo, hi, hb, oe_del, oe_ins, e_del, e_ins, h1);
-    if constexpr (CIG) {
-      if (live) {
-        uint32_t* const zr = zl.base + (long long)i * zl.rs;
+  // column -1's E entering row 0 (slot w - 1 reads Ed[w]): bwa's H(i, -1)
+  // chain, -(o_del + e_del (i + 1)), runs down it from here
 #pragma unroll
-        for (int d = 0; d < NW; ++d)
-          if (d < nd) zr[d * zl.ds] = nib[d];
-      }
+  for (int k = 1; k <= NB; ++k)
+    if (k == w) Ed[k] = -(p.o_del + e_del);
+  // lanes whose band is narrower than the class: E of slot nb back to -inf
+  // after every row (a wave-uniform test; the class's widest lanes need none)
+  const bool narrow = __ballot(ok && nb < NB) != 0ull;
+  int score = kMinusInf;
+  const int kfin = qlen - tlen + w;  // the last row's slot of column qlen - 1
+  // Row inputs as byte streams read by aligned dwords, four rows per group
+  // (the target byte of row i and the query byte entering the band for row
+  // i + 1, position i + NB + 1 - w).  The two dwords a group needs are loaded
+  // during the group before and only read (realigned) at its start, so no
+  // register holding a load in flight is copied and the loads get a group's
+  // compute to land.  (A byte load per lane and row kept the lines of a
+  // wave's 64 tasks live, overflowing the XCD's L2 at 4 waves per SIMD, and
+  // every row waited on memory.)
+  struct Stream {
+    const uint32_t* __restrict__ w;
+    uint32_t off;
+    int last;  // last dword holding a byte of the stream (clamped loads stay inside it)
+    uint32_t lo, hi, cur;
+    __device__ __forceinline__ void init(const uint8_t* base, int len) {
+      off = (uint32_t)((uintptr_t)base & 3);
+      w = reinterpret_cast<const uint32_t*>(base - off);  // pointer arithmetic keeps the global address space
+      last = max(((int)off + len + 3) / 4 - 1, 0);
+      lo = w[0];
+      hi = w[min(1, last)];
     }
-    // next row's query bytes: the band moves one column right
+    // at row 4k: bytes 4k .. 4k + 3 into cur; then group k + 1's dwords requested
+    __device__ __forceinline__ void realign() { cur = __builtin_amdgcn_alignbyte(hi, lo, off); }
+    __device__ __forceinline__ void fetch(int k) {
+      lo = w[min(k + 1, last)];
+      hi = w[min(k + 2, last)];
+    }
+  };
+  Stream ts, qs;
+  const int qc = NB + 1 - w;  // row i's entering query position is i + qc
+  ts.init(tp, ok ? tlen : 1);
+  // (a lane whose band never takes a new query byte reads its first byte)
+  const bool qin = ok && qc < qlen;
+  qs.init(qin ? qp + qc : qp, qin ? qlen - qc : 1);
+  // the row's packed score table by the lane's target base: lanes 0..4 hold
+  // the five tables, one ds_bpermute fetches lane tb's
+  const int ln = lane_id();
+  const int tabv = ln == 0 ? p.matpack[0] : ln == 1 ? p.matpack[1] : ln == 2 ? p.matpack[2]
+                 : ln == 3 ? p.matpack[3] : ln == 4 ? p.matpack[4] : 0;
+  for (int i0 = 0; i0 < tmax; i0 += 4) {
+    // both streams realigned before either requests more (with the CIG pass's
+    // stores counted in vmcnt, a wait after a new request would wait for it)
+    ts.realign();
+    qs.realign();
+    asm volatile("" ::: "memory");
+    ts.fetch(i0 >> 2);
+    qs.fetch(i0 >> 2);
 #pragma unroll
-    for (int d = 0; d < NQ; ++d) Qb[d] = (Qb[d] >> 8) | (d + 1 < NQ ? Qb[d + 1] << 24 : 0u);
-    Qb[NB >> 2] = (Qb[NB >> 2] & ~(0xFFu << (8 * (NB & 3)))) | (qn << (8 * (NB & 3)));
+    for (int r = 0; r < 4; ++r) {
+      const int i = i0 + r;
+      if (i >= tmax) break;
+      const int tb = (ok && i < tlen) ? (int)((ts.cur >> (8 * r)) & 0xFFu) : 4;
+      const uint32_t qn = (ok && i + qc < qlen) ? 5u * ((qs.cur >> (8 * r)) & 0xFFu) : 0u;
+      const int rowpack = __builtin_amdgcn_ds_bpermute(4 * min(tb, 4), tabv);
+      glane_row<NB, CIG>(Hd, Ed, Qb, nib, rowpack, oe_del, oe_ins, e_del, e_ins);
+      // (the slot tests are built where they are used: hoisted out of the row
+      // loop they would hold one SGPR pair per slot)
+      if (narrow) {
+        int nbv = nb;
+        asm volatile("" : "+v"(nbv));
+#pragma unroll
+        for (int k = 5; k < NB; k += 2)
+          if (k == nbv) Ed[k] = kMinusInf;
+      }
+      if (ok && i == tlen - 1) {  // bwa's score eh[qlen].h: H(tlen - 1, qlen - 1) when the band reaches it
+        int kf = kfin < nb ? kfin : -1;
+        asm volatile("" : "+v"(kf));
+#pragma unroll
+        for (int k = 0; k < NB; ++k)
+          if (k == kf) score = Hd[k];
+      }
+      if constexpr (CIG) {
+        if (ok && i < tlen) {
+          uint32_t* const zr = zl.base + (long long)i * zl.rs;
+#pragma unroll
+          for (int d = 0; d < NW; ++d)
+            if (d < nd) zr[d * zl.ds] = nib[d];
+        }
+      }
+      // next row's query bytes: the band moves one column right
+#pragma unroll
+      for (int d = 0; d < NQ; ++d) Qb[d] = (Qb[d] >> 8) | (d + 1 < NQ ? Qb[d + 1] << 24 : 0u);
+      Qb[NB >> 2] = (Qb[NB >> 2] & ~(0xFFu << (8 * (NB & 3)))) | (qn << (8 * (NB & 3)));
+    }
   }
-  // bwa: score = eh[qlen].h, written by the last row when its band reaches qlen
-  if (ok) scores[task] = qlen <= tlen + w ? h1 : kMinusInf;
+  if (ok) scores[task] = score;
   if constexpr (CIG) {
     // the traceback of the task's own rows, read back by the lane that wrote
     // them (stores complete before the loads)

@@ -46,6 +46,10 @@ for step in "$@"; do
             python3 "$ROOT/tools/bsw_bench.py" --which global --reps 1 &&
       run bswpmc_align 300 rocprofv3 --pmc $SQ -d "$OUT/bswpmc_align" -o run --output-format csv -- \
             python3 "$ROOT/tools/bsw_bench.py" --which align --reps 1 ;;
+    globalpmc)  # ksw_global2 only (scores + CIGAR passes): SQ issue counters
+      SQ="SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY"
+      run bswpmc_global 300 rocprofv3 --pmc $SQ -d "$OUT/bswpmc_global" -o run --output-format csv -- \
+            python3 "$ROOT/tools/bsw_bench.py" --which global --reps 1 ;;
     alignpmc)  # ksw_align2 only: SQ issue counters of one batch
       SQ="SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY"
       run bswpmc_align 300 rocprofv3 --pmc $SQ -d "$OUT/bswpmc_align" -o run --output-format csv -- \
