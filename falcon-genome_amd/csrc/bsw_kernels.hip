@@ -450,6 +450,8 @@ __device__ void glane_run(const BswDevBatch& b, const BswParams& p, long long ta
   const int nb = 2 * w + 1, nd = (nb + 7) >> 3;
   GLayout zl{nullptr, 0, 0};
   if constexpr (CIG) zl = glane_layout(b, p, zbuf, zoff, task, ok);
+  uint32_t* zrow = zl.base;
+  const bool zil = zl.ds == 64;
   int Hd[NB], Ed[NB + 1];
   uint32_t Qb[NQ], nib[NW];
   // every lane loads every row (a clamped index into a valid buffer) and
@@ -560,27 +562,30 @@ __device__ void glane_run(const BswDevBatch& b, const BswParams& p, long long ta
           if (k == kf) score = Hd[k];
       }
       if constexpr (CIG) {
+        // a running row pointer and compile-time dword offsets (the layout's
+        // dword stride is 64 or 1, wave-uniform)
         if (ok && i < tlen) {
-          uint32_t* const zr = zl.base + (long long)i * zl.rs;
+          if (zil) {
 #pragma unroll
-          for (int d = 0; d < NW; ++d)
-            if (d < nd) zr[d * zl.ds] = nib[d];
+            for (int d = 0; d < NW; ++d)
+              if (d < nd) zrow[64 * d] = nib[d];
+          } else {
+#pragma unroll
+            for (int d = 0; d < NW; ++d)
+              if (d < nd) zrow[d] = nib[d];
+          }
         }
+        zrow += zl.rs;
       }
       // next row's query bytes: the band moves one column right
 #pragma unroll
-      for (int d = 0; d < NQ; ++d) Qb[d] = (Qb[d] >> 8) | (d + 1 < NQ ? Qb[d + 1] << 24 : 0u);
+      for (int d = 0; d < NQ; ++d) Qb[d] = d + 1 < NQ ? __builtin_amdgcn_alignbyte(Qb[d + 1], Qb[d], 1) : Qb[d] >> 8;
       Qb[NB >> 2] = (Qb[NB >> 2] & ~(0xFFu << (8 * (NB & 3)))) | (qn << (8 * (NB & 3)));
     }
   }
   if (ok) scores[task] = score;
-  if constexpr (CIG) {
-    // the traceback of the task's own rows, read back by the lane that wrote
-    // them (stores complete before the loads)
-    __builtin_amdgcn_s_waitcnt(0);
-    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-    if (ok) glane_traceback(zl, qlen, tlen, w, cigar + cigar_off[task], cigar_cap[task], n_cigar + task);
-  }
+  // (the traceback runs in bsw_traceback_kernel: a chain of dependent loads per
+  // lane, it wants the occupancy this kernel's registers do not leave)
 }
 
 // One launch per band class (each with its own register budget): a wave runs
@@ -722,15 +727,23 @@ __global__ __launch_bounds__(64) void bsw_global_kernel(const BswDevBatch b, con
 }
 
 // One lane per task walks the direction bytes back from (tlen-1, last column).
-__global__ void bsw_traceback_kernel(const BswDevBatch b, const BswParams p, uint8_t* __restrict__ zbuf,
+__global__ __launch_bounds__(64) void bsw_traceback_kernel(const BswDevBatch b, const BswParams p, uint8_t* __restrict__ zbuf,
                                      const int64_t* __restrict__ zoff, uint32_t* __restrict__ cigar,
                                      const int64_t* __restrict__ cigar_off, const int32_t* __restrict__ cigar_cap,
                                      int32_t* __restrict__ n_cigar) {
   const long long task = (long long)blockIdx.x * blockDim.x + threadIdx.x;
-  if (task >= b.n) return;
-  const int qlen = b.qlen[task], tlen = b.tlen[task], w = b.w[task];
-  // lane-path tasks were traced back by bsw_global_lane_kernel itself
-  if (glane_ok(qlen, tlen, w, p.lane_ok != 0)) return;
+  const bool exists = task < b.n;
+  const int qlen = exists ? b.qlen[task] : 0, tlen = exists ? b.tlen[task] : 0, w = exists ? b.w[task] : 0;
+  // lane-path tasks: their nibble rows, located as bsw_global_lane_kernel
+  // wrote them (the same 64-task waves: every lane takes part in the layout's
+  // wave votes)
+  const bool lane = exists && glane_ok(qlen, tlen, w, p.lane_ok != 0);
+  const GLayout zl = glane_layout(b, p, zbuf, zoff, task, lane);
+  if (!exists) return;
+  if (lane) {
+    glane_traceback(zl, qlen, tlen, w, cigar + cigar_off[task], cigar_cap[task], n_cigar + task);
+    return;
+  }
   const int n_col = qlen < 2 * w + 1 ? qlen : 2 * w + 1;
   const uint8_t* z = zbuf + zoff[task];
   const long long zsize = (long long)n_col * (tlen > 0 ? tlen : 0);
