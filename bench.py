@@ -1049,9 +1049,11 @@ def main():
             "tasks": g["tasks"], "w": g["w"], "band_cells": g["cells"],
             "scores_gcups": g["scores"]["gcups"], "scores_ms": g["scores"]["ms"],
             "cigar_gcups": g["cigar"]["gcups"], "cigar_ms": g["cigar"]["ms"],
-            "kernel": "bsw_global_lane_kernel<33> (one task per lane, band in registers, nibble direction rows "
-                      "interleaved across the wave's 64 tasks, bwa's traceback fused at the end of the same launch); "
-                      "wider bands go to bsw_global_kernel (one wave per task) + bsw_traceback_kernel"}
+            "kernel": "bsw_global_lane_kernel<33> (one task per lane, band in registers, one unmasked row form "
+                      "with bwa's boundaries carried by column -1, direction nibbles of raw compare signs shifted in "
+                      "by v_alignbit, rows interleaved across the wave's 64 tasks, row inputs as dword streams), then "
+                      "bsw_traceback_kernel (bwa's traceback, one lane per task, 8 waves per SIMD); wider bands go "
+                      "to bsw_global_kernel (one wave per task)"}
         gm = {}
         try:
             gm = json.load(open(os.path.join(ROOT, "profiles", "pmc_bsw.json"))).get("global", {})
@@ -1065,6 +1067,9 @@ def main():
                 "achieved": round(ach / 1e12, 3), "frac": round(ach / VALU_LANE_INSTR_PEAK, 4),
                 "valu_instr_per_cell": vpc, "of": "scores-only pass (DP kernels)",
                 "valu_source": "profiles/pmc_bsw.json global (SQ_INSTS_VALU x 64 / band cells)"}
+            if gm.get("cigar_pass_valu_lane_instr_per_cell"):
+                line["bsw"]["global"]["roofline"]["cigar_pass_valu_instr_per_cell"] = \
+                    gm["cigar_pass_valu_lane_instr_per_cell"]
         # mate rescue: 151 bp reads in 600 bp windows (mem_matesw's window for a
         # ~350 +- 50 bp insert), bwa's xtra for it (XSUBO | XSTART | min_seed_len * a,
         # XBYTE as l_ms * a < 250)

@@ -77,6 +77,9 @@ def main():
                          "dp_valu_lane_instr_per_cell": round(64 * tot.get("scores", 0) / 2 / g["cells"], 3),
                          "dp_cigar_valu_lane_instr_per_cell": round(64 * tot.get("cigar", 0) / 2 / g["cells"], 3),
                          "traceback_valu_wave_instr": tot.get("traceback", 0) / 2}
+        # the CIGAR pass as a whole: direction-row DP plus the traceback launch
+        out["global"]["cigar_pass_valu_lane_instr_per_cell"] = round(
+            64 * (tot.get("cigar", 0) + tot.get("traceback", 0)) / 2 / g["cells"], 3)
     adir = os.path.join(src, "bswpmc_align")
     if os.path.isdir(adir):  # ksw_align2: warm-up + timed batch
         tot = {}
