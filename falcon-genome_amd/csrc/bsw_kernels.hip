@@ -324,34 +324,75 @@ __device__ __forceinline__ GLayout glane_layout(const BswDevBatch& b, const BswP
 // of nibble row i; c past the row's band end reads 0, as bwa's zeroed bytes
 // there do; a column left of the row's band start indexes bwa's flat matrix
 // backwards into the rows above (row-major, n_col bytes a row), as bwa does.
+// Next traceback state from (state, nibble), 2 bits per entry: from M the
+// source (max(M, E) < F ? F : M < E ? E : M), from E / F its continue bit.
+// A zero nibble (bwa's zeroed bytes) goes to M from every state, as bwa's 0.
+__host__ __device__ constexpr uint64_t glane_next01() {
+  uint64_t t = 0;
+  for (int nb = 0; nb < 16; ++nb) {
+    t |= (uint64_t)((nb & 2) ? 2 : (nb & 1)) << (2 * nb);
+    t |= (uint64_t)((nb & 4) ? 1 : 0) << (32 + 2 * nb);
+  }
+  return t;
+}
+__host__ __device__ constexpr uint32_t glane_next2() {
+  uint32_t t = 0;
+  for (int nb = 0; nb < 16; ++nb) t |= (uint32_t)((nb & 8) ? 2 : 0) << (2 * nb);
+  return t;
+}
+
 __device__ __forceinline__ void glane_traceback(const GLayout& L, int qlen, int tlen, int w,
                                                 uint32_t* __restrict__ cg, int cap, int32_t* __restrict__ n_out) {
   const int n_col = min(qlen, 2 * w + 1);
   const long long zsize = (long long)n_col * tlen;
+  constexpr uint64_t T01 = glane_next01();
+  constexpr uint32_t T2 = glane_next2();
   int crow = -1, cdw = -1;
   uint32_t cval = 0;
-  auto byte_at = [&](int i, int k) -> int {
-    int r = i, c = k - (i > w ? i - w : 0);
-    if (c < 0 || c >= n_col) {  // bwa's flat index left of the band: an earlier row's bytes
-      const long long zi = (long long)i * n_col + c;
-      if (zi < 0 || zi >= zsize) return 0;
-      r = (int)(zi / n_col);
-      c = (int)(zi - (long long)r * n_col);
-    }
-    const int beg = r > w ? r - w : 0, end = r + w + 1 < qlen ? r + w + 1 : qlen;
-    if (beg + c >= end) return 0;
-    const int kb = beg + c - r + w;
-    const int dw = kb >> 3;
-    if (r != crow || dw != cdw) {
-      crow = r, cdw = dw;
-      cval = L.base[(long long)r * L.rs + dw * L.ds];
-    }
-    const int nbl = (int)((cval >> (28 - 4 * (kb & 7))) & 15u);
-    // bits: M < E, max(M, E) < F, E-continue, F-continue -> bwa's direction byte
-    return ((nbl & 2) ? 2 : (nbl & 1)) | ((nbl >> 2) & 1) << 2 | ((nbl >> 3) & 1) << 5;
-  };
   int n = 0, which = 0, curop = -1;
   uint32_t curlen = 0;
+  int i = tlen - 1;
+  int k = (i + w + 1 < qlen ? i + w + 1 : qlen) - 1;
+  while (i >= 0 && k >= 0) {
+    // bwa's byte (row i, band offset c = k - beg_i) is cell k - i + w of
+    // nibble row i; c past the row's band end reads 0, as bwa's zeroed bytes
+    // there do; a column left of the row's band start indexes bwa's flat
+    // matrix backwards into the rows above (row-major, n_col bytes a row)
+    int r = i, c = k - (i > w ? i - w : 0);
+    if (c < 0 || c >= n_col) {
+      const long long zi = (long long)i * n_col + c;
+      r = (zi < 0 || zi >= zsize) ? -1 : (int)(zi / n_col);
+      c = r < 0 ? 0 : (int)(zi - (long long)r * n_col);
+    }
+    uint32_t nb = 0;
+    if (r >= 0) {
+      const int beg = r > w ? r - w : 0, end = r + w + 1 < qlen ? r + w + 1 : qlen;
+      if (beg + c < end) {
+        const int kb = beg + c - r + w;
+        const int dw = kb >> 3;
+        if (r != crow || dw != cdw) {
+          crow = r, cdw = dw;
+          cval = L.base[(long long)r * L.rs + dw * L.ds];
+        }
+        nb = (cval >> (28 - 4 * (kb & 7))) & 15u;
+      }
+    }
+    which = which == 2 ? (int)((T2 >> (2 * nb)) & 3u) : (int)((T01 >> (32 * which + 2 * nb)) & 3u);
+    // state M: diagonal (CIGAR M), E: up (D), F: left (I)
+    const int op = (int)((0x18u >> (2 * which)) & 3u);
+    i -= which != 2;
+    k -= which != 1;
+    if (op == curop) {
+      ++curlen;
+    } else {
+      if (curop >= 0) {
+        if (n < cap) cg[n] = curlen << 4 | (uint32_t)curop;
+        ++n;
+      }
+      curop = op;
+      curlen = 1;
+    }
+  }
   auto push = [&](int op, int len) {
     if (op == curop) {
       curlen += (uint32_t)len;
@@ -364,14 +405,6 @@ __device__ __forceinline__ void glane_traceback(const GLayout& L, int qlen, int 
       curlen = (uint32_t)len;
     }
   };
-  int i = tlen - 1;
-  int k = (i + w + 1 < qlen ? i + w + 1 : qlen) - 1;
-  while (i >= 0 && k >= 0) {
-    which = byte_at(i, k) >> (which << 1) & 3;
-    if (which == 0) push(0, 1), --i, --k;
-    else if (which == 1) push(2, 1), --i;
-    else push(1, 1), --k;
-  }
   if (i >= 0) push(2, i + 1);
   if (k >= 0) push(1, k + 1);
   if (curop >= 0) {

@@ -50,6 +50,11 @@ for step in "$@"; do
       SQ="SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY"
       run bswpmc_global 300 rocprofv3 --pmc $SQ -d "$OUT/bswpmc_global" -o run --output-format csv -- \
             python3 "$ROOT/tools/bsw_bench.py" --which global --reps 1 ;;
+    globalprof)  # ksw_global2 only: per-kernel durations (scores pass, direction-row DP, traceback)
+      run globalprof 300 rocprofv3 --kernel-trace --stats -d "$OUT/globalprof" -o run --output-format csv -- \
+            python3 "$ROOT/tools/bsw_bench.py" --which global ;;
+    e2eprobe)  # htc timeline at the bench's 31 Mbp (tools/e2e_probe.sh, htc only)
+      run e2eprobe 900 env MBP=31 HTC_ONLY=1 bash "$ROOT/tools/e2e_probe.sh" ;;
     alignpmc)  # ksw_align2 only: SQ issue counters of one batch
       SQ="SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY"
       run bswpmc_align 300 rocprofv3 --pmc $SQ -d "$OUT/bswpmc_align" -o run --output-format csv -- \
