@@ -1012,10 +1012,13 @@ def main():
                      "traffic_note": "HBM bytes per forward pass: 2 x FETCH_SIZE + WRITE_SIZE from separate rocprofv3 "
                                      "--pmc passes (profiles/pmc_traffic.json; the x2 is the gfx950 FETCH_SIZE "
                                      "calibration, profiles/fetch_calibration.json)",
-                     "kernel": "phmm3_kernel (row-streamed segments, two read rows per lane, packed FP32): fp32 forward pass = one launch "
-                               "per launch class, overlapped on 4 streams; achieved = algorithmic FLOPs / pass "
-                               "time (HIP events on the launch stream; rocprofv3 kernel stats of this bench in "
-                               "profiles/r4/)",
+                     "kernel": "phmm4_kernel<C> (column-blocked: lane = one of 16 haplotype columns of a block, "
+                               "two packed half-streams of read rows per wave, rows streamed through an LDS ring; "
+                               "eight column classes C = 19, 17..11 for reads of 33..160 bases) plus phmm3_kernel "
+                               "(row-streamed stripes) for longer haplotypes: fp32 forward pass = one launch per "
+                               "launch class, overlapped on 4 streams; achieved = algorithmic FLOPs / pass time "
+                               "(HIP events on the launch stream; rocprofv3 kernel stats of this bench in "
+                               "profiles/r5/)",
                      "valu_instr_per_cell": vipc,
                      "valu_issue_frac": (round(ph["cells"] / fwd_s * vipc / VALU_LANE_INSTR_PEAK, 4) if vipc
                                          else None),

@@ -377,8 +377,14 @@ bool BamReader::next(BamRecord& r) {
 
 bool BamReader::next_raw(const uint8_t*& body, size_t& n) {
   int32_t bs = 0;
-  if (!bgzf_.read_exact(&bs, 4)) return false;
+  if (const uint8_t* p = bgzf_.view(4)) std::memcpy(&bs, p, 4);
+  else if (!bgzf_.read_exact(&bs, 4)) return false;
   if (bs < 32) throw formatError("bad BAM block_size");
+  if (const uint8_t* p = bgzf_.view((size_t)bs)) {  // inside one block: no copy
+    body = p;
+    n = (size_t)bs;
+    return true;
+  }
   buf_.resize(bs);
   bgzf_.read_exact(buf_.data(), bs);
   body = buf_.data();

@@ -59,7 +59,7 @@ uint16_t reg2bin(int64_t beg, int64_t end);
 
 class BamWriter {
  public:
-  BamWriter(const std::string& path, const BamHeader& h, int level = 6);
+  BamWriter(const std::string& path, const BamHeader& h, int level = kBgzfLevel);
   void write(const BamRecord& r);
   // write(r) with the record body already encoded by encode_bam_record(r, body)
   // (callers encode many records on worker threads and write them in order).

@@ -290,6 +290,7 @@ uint64_t BgzfWriter::voffset(uint64_t u) const {
 BgzfReader::BgzfReader(const std::string& path) {
   f_ = std::fopen(path.c_str(), "rb");
   if (!f_) throw fileNotFound(path);
+  std::setvbuf(f_, nullptr, _IOFBF, 1 << 20);  // about 30 blocks per read(2)
 }
 
 BgzfReader::~BgzfReader() {
@@ -299,7 +300,8 @@ BgzfReader::~BgzfReader() {
 bool BgzfReader::load_block() {
   for (;;) {
     block_coff_ = next_coff_;
-    if (std::fseek(f_, (long)block_coff_, SEEK_SET) != 0) return false;
+    // sequential blocks need no seek (a seek drops the stdio buffer)
+    if (std::ftell(f_) != (long)block_coff_ && std::fseek(f_, (long)block_coff_, SEEK_SET) != 0) return false;
     uint8_t h[18];
     const size_t got = std::fread(h, 1, 18, f_);
     if (got == 0) return false;
@@ -317,10 +319,14 @@ bool BgzfReader::load_block() {
       k += 4 + slen;
     }
     if (bsize == 0) throw formatError("gzip member without BGZF BC field");
-    std::vector<uint8_t> comp(bsize);
-    std::fseek(f_, (long)block_coff_, SEEK_SET);
-    if (std::fread(comp.data(), 1, bsize, f_) != bsize) throw formatError("truncated BGZF block");
     const size_t hdr = 12 + xlen;
+    if (bsize < hdr + 8) throw formatError("corrupt BGZF block header");
+    // the header is read; the rest of the member follows it in the file
+    std::vector<uint8_t>& comp = comp_;
+    comp.resize(bsize);
+    std::memcpy(comp.data(), h, 12);
+    std::memcpy(comp.data() + 12, extra.data(), xlen);
+    if (std::fread(comp.data() + hdr, 1, bsize - hdr, f_) != bsize - hdr) throw formatError("truncated BGZF block");
     const uint32_t isize = get32(&comp[bsize - 4]);
     const uint32_t crc = get32(&comp[bsize - 8]);
     if (isize > kBgzfMaxBlock || bsize < hdr + 8) throw formatError("corrupt BGZF block header");

@@ -1,6 +1,9 @@
 #include "fasta.h"
 
+#include <array>
 #include <cctype>
+#include <cstdio>
+#include <cstring>
 #include <fstream>
 #include <sstream>
 
@@ -21,26 +24,56 @@ int64_t Reference::total_length() const {
 }
 
 Reference load_fasta(const std::string& path) {
-  std::ifstream in(path);
-  if (!in) throw fileNotFound(path);
+  // the whole file in one read, then one pass over its lines: bases through a
+  // 256-entry table (upper case ACGT kept, anything else N), a line's bases
+  // appended in one copy
+  std::FILE* f = std::fopen(path.c_str(), "rb");
+  if (!f) throw fileNotFound(path);
+  std::string buf;
+  {
+    char chunk[1 << 16];
+    size_t got;
+    if (std::fseek(f, 0, SEEK_END) == 0) {
+      const long n = std::ftell(f);
+      if (n > 0) buf.reserve((size_t)n);
+      std::fseek(f, 0, SEEK_SET);
+    }
+    while ((got = std::fread(chunk, 1, sizeof chunk, f)) > 0) buf.append(chunk, got);
+    std::fclose(f);
+  }
+  static const auto kBase = [] {
+    std::array<char, 256> t{};
+    for (int c = 0; c < 256; ++c) {
+      const int u = std::toupper(c);
+      t[c] = (u == 'A' || u == 'C' || u == 'G' || u == 'T') ? (char)u : 'N';
+    }
+    return t;
+  }();
   Reference ref;
-  std::string line;
-  while (std::getline(in, line)) {
-    if (!line.empty() && line.back() == '\r') line.pop_back();
-    if (line.empty()) continue;
-    if (line[0] == '>') {
-      std::string name = line.substr(1);
-      const size_t ws = name.find_first_of(" \t");
-      if (ws != std::string::npos) name.resize(ws);
-      ref.contigs.push_back({name, ""});
-      continue;
+  std::string* s = nullptr;
+  const char* p = buf.data();
+  const char* const e = p + buf.size();
+  while (p < e) {
+    const char* nl = static_cast<const char*>(std::memchr(p, '\n', (size_t)(e - p)));
+    const char* le = nl ? nl : e;
+    const char* q = le;
+    if (q > p && q[-1] == '\r') --q;
+    if (q > p) {
+      if (*p == '>') {
+        std::string name(p + 1, q);
+        const size_t ws = name.find_first_of(" \t");
+        if (ws != std::string::npos) name.resize(ws);
+        ref.contigs.push_back({name, ""});
+        s = &ref.contigs.back().seq;
+      } else {
+        if (!s) throw formatError(path + ": sequence before the first '>' header");
+        const size_t at = s->size();
+        s->resize(at + (size_t)(q - p));
+        char* o = &(*s)[at];
+        for (const char* c = p; c < q; ++c) *o++ = kBase[(unsigned char)*c];
+      }
     }
-    if (ref.contigs.empty()) throw formatError(path + ": sequence before the first '>' header");
-    std::string& s = ref.contigs.back().seq;
-    for (char c : line) {
-      const char u = (char)std::toupper((unsigned char)c);
-      s += (u == 'A' || u == 'C' || u == 'G' || u == 'T') ? u : 'N';
-    }
+    p = nl ? nl + 1 : e;
   }
   return ref;
 }

@@ -458,7 +458,8 @@ void bgzip_tabix_file(const std::string& input, const std::string& output) {
   bx.finish();
 }
 
-void vcf_concat_bgzip_tabix(const std::vector<std::string>& inputs, const std::string& plain, const std::string& gz) {
+void vcf_concat_bgzip_tabix(const std::vector<std::string>& inputs, const std::string& plain, const std::string& gz,
+                            bool consume_inputs) {
   // vcf_concat's text (every line of the first part, the others without
   // their '#' lines, a last line without '\n' gets one) written to `plain`
   // and, in the same pass, bgzipped + indexed as bgzip_tabix_file(plain, gz)
@@ -478,8 +479,8 @@ void vcf_concat_bgzip_tabix(const std::vector<std::string>& inputs, const std::s
   } po{fd, {}};
   BgzipIndexer bx(gz);
   // the next part loads on the pool while this one is written
-  auto load = [](const std::string& path) {
-    return host_pool_async([path] {
+  auto load = [consume_inputs](const std::string& path) {
+    return host_pool_async([path, consume_inputs] {
       std::FILE* in = std::fopen(path.c_str(), "rb");
       if (!in) throw fileNotFound(path);
       std::fseek(in, 0, SEEK_END);
@@ -489,6 +490,7 @@ void vcf_concat_bgzip_tabix(const std::vector<std::string>& inputs, const std::s
       const size_t got = n > 0 ? std::fread(buf->data(), 1, (size_t)n, in) : 0;
       std::fclose(in);
       buf->resize(got);
+      if (consume_inputs) std::remove(path.c_str());
       return buf;
     });
   };

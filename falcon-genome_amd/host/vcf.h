@@ -59,6 +59,10 @@ void tabix_index_vcf(const std::string& vcf_gz);
 void bgzip_tabix_file(const std::string& input, const std::string& output);
 // vcf_concat(inputs, plain) + bgzip_tabix_file(plain, gz) in one pass over
 // the parts (HTC's concat → bgzip → tabix tail as one stage).
-void vcf_concat_bgzip_tabix(const std::vector<std::string>& inputs, const std::string& plain, const std::string& gz);
+// consume_inputs: each input file is removed once it has been read (temporary
+// shard parts; their pages leave the page cache inside this pass instead of in
+// a separate removal afterwards).
+void vcf_concat_bgzip_tabix(const std::vector<std::string>& inputs, const std::string& plain, const std::string& gz,
+                            bool consume_inputs = false);
 
 }  // namespace fcsg

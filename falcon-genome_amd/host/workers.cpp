@@ -172,11 +172,12 @@ int Mutect2Worker::run(TaskContext& ctx) {
 }
 
 // ------------------------------------------------------------------ VCF tail
-VCFConcatWorker::VCFConcatWorker(std::vector<std::string> inputs, std::string output, std::string gz)
+VCFConcatWorker::VCFConcatWorker(std::vector<std::string> inputs, std::string output, std::string gz, bool consume)
     : Worker(1, 1, {}, gz.empty() ? "VCF concat" : "VCF concat + bgzip + tabix"),
       inputs_(std::move(inputs)),
       output_(std::move(output)),
-      gz_(std::move(gz)) {}
+      gz_(std::move(gz)),
+      consume_(consume) {}
 
 void VCFConcatWorker::check() {
   if (inputs_.empty()) throw invalidParam("no VCF to concatenate");
@@ -184,7 +185,7 @@ void VCFConcatWorker::check() {
 
 int VCFConcatWorker::run(TaskContext&) {
   if (gz_.empty()) vcf_concat(inputs_, output_);
-  else vcf_concat_bgzip_tabix(inputs_, output_, gz_);
+  else vcf_concat_bgzip_tabix(inputs_, output_, gz_, consume_);
   return 0;
 }
 

@@ -63,14 +63,16 @@ class Mutect2Worker : public Worker {
 
 class VCFConcatWorker : public Worker {
  public:
-  // gz non-empty: also gz + gz.tbi from the same pass (concat + bgzip + tabix as one stage)
-  VCFConcatWorker(std::vector<std::string> inputs, std::string output, std::string gz = "");
+  // gz non-empty: also gz + gz.tbi from the same pass (concat + bgzip + tabix as one stage);
+  // consume: the inputs are temporary parts, removed as soon as they are read
+  VCFConcatWorker(std::vector<std::string> inputs, std::string output, std::string gz = "", bool consume = false);
   void check() override;
   int run(TaskContext& ctx) override;
 
  private:
   std::vector<std::string> inputs_;
   std::string output_, gz_;
+  bool consume_;
 };
 
 class ZIPWorker : public Worker {

@@ -14,7 +14,7 @@ import sys
 src, dst, tag = sys.argv[1:4]
 passes = float(sys.argv[4]) if len(sys.argv) > 4 else 2.0
 cells = float(sys.argv[5]) if len(sys.argv) > 5 else 22721383941.0
-FWD = ("phmm3_kernel", "phmm2_kernel", "phmm_kernel<float, false, false>")
+FWD = ("phmm4_kernel", "phmm3_kernel", "phmm2_kernel", "phmm_kernel<float, false, false>")
 tot = {}
 for f in glob.glob(os.path.join(src, "**", "*counter_collection.csv"), recursive=True):
     for r in csv.DictReader(open(f)):

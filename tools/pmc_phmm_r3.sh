@@ -23,5 +23,5 @@ pass sq4 SQ_LDS_ADDR_CONFLICT SQ_LDS_UNALIGNED_STALL SQ_LDS_DATA_FIFO_FULL SQ_LD
   SQ_INST_CYCLES_VMEM_RD SQ_LEVEL_WAVES SQ_IFETCH
 pass fetch FETCH_SIZE
 pass write WRITE_SIZE
-for d in sq1 sq2 sq3 sq4 fetch write; do python3 tools/pmc_kernels.py "$OUT/$d" phmm3; done > "$OUT/summary.txt"
+for d in sq1 sq2 sq3 sq4 fetch write; do python3 tools/pmc_kernels.py "$OUT/$d" phmm; done > "$OUT/summary.txt"
 cat "$OUT/summary.txt"
