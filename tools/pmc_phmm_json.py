@@ -47,7 +47,7 @@ if "FETCH_SIZE" in q and "WRITE_SIZE" in q:
     t.pop("phmm_fwd_fp32_source", None)
     t["_note"] = ("HBM bytes per fp32 forward pass (all hap-length class launches) on the default C2 workload = "
                   "(FETCH_SIZE + WRITE_SIZE) KiB * 1024 from separate rocprofv3 --pmc passes "
-                  f"(gpurun_out/{tag}, summary in profiles/r4/{tag}_pmc_phmm.txt), divided by the passes profiled.  "
+                  f"(gpurun_out/{tag}, summary in {os.path.relpath(dst, os.path.dirname(root))}/{tag}_pmc_phmm.txt), divided by the passes profiled.  "
                   "FETCH_SIZE as reported: bench.py prices HBM reads as 2 x FETCH_SIZE (the gfx950 calibration of "
                   "profiles/fetch_calibration.json, measured for 1, 4 and 16 B per-lane loads).")
     json.dump(t, open(tp, "w"), indent=1)
