@@ -1587,6 +1587,108 @@ int fcs_ksw_global2(int qlen, const uint8_t* query, int tlen, const uint8_t* tar
   return score;
 }
 
-int fcs_abi_symbol_count(void) { return 41; }
+int fcs_bgzf_index(const uint8_t* comp, int64_t comp_bytes, int64_t* coff, int64_t* uoff, int32_t cap,
+                   int32_t* n_members, int64_t* comp_used) {
+  if (!n_members || !comp_used || comp_bytes < 0 || cap < 0 || (comp_bytes > 0 && !comp) || !coff || !uoff)
+    return fail(FCS_ERR_INVALID, "[E::fcs_bgzf_index] bad arguments");
+  auto le16 = [&](int64_t at) { return (uint32_t)comp[at] | (uint32_t)comp[at + 1] << 8; };
+  int64_t at = 0, u = 0;
+  int32_t k = 0;
+  while (k < cap && comp_bytes - at >= 18) {
+    // gzip member with FEXTRA (RFC 1952) carrying the BGZF "BC" subfield
+    if (comp[at] != 31 || comp[at + 1] != 139 || comp[at + 2] != 8 || !(comp[at + 3] & 4))
+      return fail(FCS_ERR_INVALID, "[E::fcs_bgzf_index] no BGZF header at byte " + std::to_string(at));
+    const int64_t xlen = le16(at + 10);
+    if (comp_bytes - at < 12 + xlen) break;
+    int64_t bsize = -1;
+    for (int64_t x = at + 12; x + 4 <= at + 12 + xlen;) {
+      const int64_t slen = le16(x + 2);
+      if (comp[x] == 'B' && comp[x + 1] == 'C' && slen == 2 && x + 6 <= at + 12 + xlen) bsize = le16(x + 4);
+      x += 4 + slen;
+    }
+    if (bsize < 0 || bsize + 1 < 12 + xlen + 8)
+      return fail(FCS_ERR_INVALID, "[E::fcs_bgzf_index] no BGZF block size at byte " + std::to_string(at));
+    const int64_t len = bsize + 1;
+    if (comp_bytes - at < len) break;  // incomplete: left for the next call
+    const int64_t isize = (int64_t)(le16(at + len - 4) | le16(at + len - 2) << 16);
+    if (isize > 65536)
+      return fail(FCS_ERR_INVALID, "[E::fcs_bgzf_index] member at byte " + std::to_string(at) + " inflates past 64 KiB");
+    coff[k] = at;
+    uoff[k] = u;
+    at += len;
+    u += isize;
+    ++k;
+  }
+  coff[k] = at;
+  uoff[k] = u;
+  *n_members = k;
+  *comp_used = at;
+  return FCS_OK;
+}
+
+int fcs_bgzf_inflate_dev(const uint8_t* dev_comp, const int64_t* dev_coff, const int64_t* dev_uoff, int32_t n,
+                         uint8_t* dev_out, int32_t* dev_status, int32_t device, void* stream) {
+  if (n < 0 || (n > 0 && (!dev_comp || !dev_coff || !dev_uoff || !dev_out || !dev_status)))
+    return fail(FCS_ERR_INVALID, "[E::fcs_bgzf_inflate_dev] bad arguments");
+  if (n == 0) return FCS_OK;
+  int rc = check_device(device);
+  if (rc) return rc;
+  FCS_SET_DEVICE((device));
+  return launch_bgzf_inflate(dev_comp, dev_coff, dev_uoff, n, dev_out, dev_status, static_cast<hipStream_t>(stream));
+}
+
+int fcs_bgzf_inflate(const uint8_t* comp, int64_t comp_bytes, uint8_t* out, int64_t out_cap, int64_t* comp_used,
+                     int64_t* out_bytes, int32_t device) {
+  if (!comp_used || !out_bytes || comp_bytes < 0 || (comp_bytes > 0 && !comp) || out_cap < 0 || (out_cap > 0 && !out))
+    return fail(FCS_ERR_INVALID, "[E::fcs_bgzf_inflate] bad arguments");
+  *comp_used = 0;
+  *out_bytes = 0;
+  // a member is at least 28 bytes (18 of header / trailer, 2 of DEFLATE)
+  const int64_t most = std::min<int64_t>(comp_bytes / 20 + 1, 0x7FFFFFFE);
+  std::vector<int64_t> coff((size_t)most + 1), uoff((size_t)most + 1);
+  int32_t n = 0;
+  int64_t used = 0;
+  int rc = fcs_bgzf_index(comp, comp_bytes, coff.data(), uoff.data(), (int32_t)most, &n, &used);
+  if (rc) return rc;
+  const int64_t total = uoff[(size_t)n];
+  if (total > out_cap)
+    return fail(FCS_ERR_INVALID, "[E::fcs_bgzf_inflate] output needs " + std::to_string(total) + " bytes, capacity " +
+                                     std::to_string(out_cap));
+  *comp_used = used;
+  if (n == 0) return FCS_OK;
+  if ((rc = check_device(device))) return rc;
+  FCS_SET_DEVICE((device));
+  SessionLease lease;
+  if ((rc = lease.acquire(device))) return rc;
+  Session* S = lease.get();
+  const size_t nn = (size_t)n;
+  Layout L;
+  const size_t oco = L.add(8 * (nn + 1)), ouo = L.add(8 * (nn + 1)), ocp = L.add((size_t)used + 16);
+  const size_t in_bytes = L.total, ost = L.add(4 * nn), oout = L.add((size_t)total);
+  if ((rc = S->ensure_host(L.total)) || (rc = S->ensure_dev(L.total))) return rc;
+  std::memcpy(S->h<void>(oco), coff.data(), 8 * (nn + 1));
+  std::memcpy(S->h<void>(ouo), uoff.data(), 8 * (nn + 1));
+  std::memcpy(S->h<void>(ocp), comp, (size_t)used);
+  hipStream_t s = S->s;
+  const StreamDrain drain{s};
+  FCS_HIP_CHECK(hipMemcpyAsync(S->dev, S->host, in_bytes, hipMemcpyHostToDevice, s));
+  if ((rc = launch_bgzf_inflate(S->d<uint8_t>(ocp), S->d<int64_t>(oco), S->d<int64_t>(ouo), n, S->d<uint8_t>(oout),
+                                S->d<int32_t>(ost), s)))
+    return rc;
+  FCS_HIP_CHECK(hipMemcpyAsync(S->h<void>(ost), S->d<void>(ost), L.total - ost, hipMemcpyDeviceToHost, s));
+  FCS_HIP_CHECK(hipStreamSynchronize(s));
+  const int32_t* st = S->h<int32_t>(ost);
+  for (size_t k = 0; k < nn; ++k)
+    if (st[k] != FCS_BGZF_OK) {
+      static const char* what[4] = {"ok", "corrupt DEFLATE stream", "inflates past its ISIZE", "CRC-32 mismatch"};
+      return fail(FCS_ERR_INVALID, "[E::fcs_bgzf_inflate] member " + std::to_string(k) + " at byte " +
+                                       std::to_string(coff[k]) + ": " + what[st[k] & 3]);
+    }
+  std::memcpy(out, S->h<void>(oout), (size_t)total);
+  *out_bytes = total;
+  return FCS_OK;
+}
+
+int fcs_abi_symbol_count(void) { return 44; }
 
 }  // extern "C"

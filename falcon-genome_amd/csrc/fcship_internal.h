@@ -248,5 +248,8 @@ int launch_bsw_align(const BswDevBatch& b, const BswParams& p, const int32_t* xt
 int launch_bsw_global(const BswDevBatch& b, const BswParams& p, int max_qlen, int max_tlen, int32_t* scores,
                       uint8_t* zbuf, int64_t zbytes, const int64_t* zoff, uint32_t* cigar, const int64_t* cigar_off,
                       const int32_t* cigar_cap, int32_t* n_cigar, hipStream_t s);
+// One wave per BGZF member (bgzf_kernels.hip); coff / uoff have n + 1 entries.
+int launch_bgzf_inflate(const uint8_t* comp, const int64_t* coff, const int64_t* uoff, int32_t n, uint8_t* out,
+                        int32_t* status, hipStream_t s);
 
 }  // namespace fcs

@@ -176,6 +176,10 @@ _sig("fcs_ksw_extend2", C.c_int, [C.c_int, u8p, C.c_int, u8p, C.c_int, i8p, C.c_
 _sig("fcs_ksw_global2", C.c_int, [C.c_int, u8p, C.c_int, u8p, C.c_int, i8p, C.c_int, C.c_int, C.c_int, C.c_int,
                                   C.c_int, C.POINTER(C.c_int), C.POINTER(u32p)])
 _sig("fcs_set_default_device", C.c_int, [C.c_int32])
+_sig("fcs_bgzf_index", C.c_int, [C.c_void_p, C.c_int64, C.c_void_p, C.c_void_p, C.c_int32, i32p, i64p])
+_sig("fcs_bgzf_inflate", C.c_int, [C.c_void_p, C.c_int64, C.c_void_p, C.c_int64, i64p, i64p, C.c_int32])
+_sig("fcs_bgzf_inflate_dev", C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_int32, C.c_void_p, C.c_void_p,
+                                       C.c_int32, C.c_void_p])
 _sig("fcs_synth_phmm_sizes", C.c_int, [C.c_uint64, C.c_int64, C.c_int32, C.c_int32, C.c_int32, i64p, i64p])
 _sig("fcs_synth_phmm", C.c_int, [C.c_uint64, C.c_int64, C.c_int32, C.c_int32, C.c_int32] + [C.c_void_p] * 10)
 _sig("fcs_synth_bsw_sizes", C.c_int, [C.c_uint64, C.c_int64, C.c_int32, C.c_int64, C.c_int32, C.c_int32,
@@ -551,3 +555,28 @@ def synth_bsw(seed: int, n_reads: int, read_len: int = 151, ref_len: int = 10_00
 
 def cigar_str(ops) -> str:
     return "".join(f"{int(c) >> 4}{'MID'[int(c) & 0xf]}" for c in ops)
+
+
+FCS_BGZF_OK, FCS_BGZF_CORRUPT, FCS_BGZF_OVERFLOW, FCS_BGZF_CRC = 0, 1, 2, 3
+
+
+def bgzf_index(comp, cap: int | None = None):
+    """fcs_bgzf_index: (coff, uoff, comp_used) of the whole BGZF members in
+    `comp` (bytes / uint8 array); coff / uoff have n + 1 entries."""
+    c = np.frombuffer(bytes(comp), np.uint8) if not isinstance(comp, np.ndarray) else np.ascontiguousarray(comp, np.uint8)
+    cap = len(c) // 20 + 1 if cap is None else cap
+    coff = np.zeros(cap + 1, np.int64)
+    uoff = np.zeros(cap + 1, np.int64)
+    n, used = C.c_int32(), C.c_int64()
+    check(lib.fcs_bgzf_index(_ptr(c), len(c), coff.ctypes.data, uoff.ctypes.data, cap, C.byref(n), C.byref(used)))
+    return coff[:n.value + 1].copy(), uoff[:n.value + 1].copy(), used.value
+
+
+def bgzf_inflate(comp, out_cap: int | None = None, device: int = 0):
+    """fcs_bgzf_inflate: (inflated bytes of the whole members, comp_used)."""
+    c = np.frombuffer(bytes(comp), np.uint8) if not isinstance(comp, np.ndarray) else np.ascontiguousarray(comp, np.uint8)
+    cap = int(bgzf_index(c)[1][-1]) if out_cap is None else out_cap
+    out = np.zeros(max(cap, 1), np.uint8)
+    used, got = C.c_int64(), C.c_int64()
+    check(lib.fcs_bgzf_inflate(_ptr(c), len(c), out.ctypes.data, cap, C.byref(used), C.byref(got), device))
+    return out[:got.value].tobytes(), used.value

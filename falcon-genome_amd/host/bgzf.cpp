@@ -12,6 +12,7 @@
 #include <thread>
 
 #include "common.h"
+#include "fcship.h"
 
 namespace fcsg {
 
@@ -298,6 +299,7 @@ BgzfReader::~BgzfReader() {
 }
 
 bool BgzfReader::load_block() {
+  if (device_ >= 0) return load_chunk();
   for (;;) {
     block_coff_ = next_coff_;
     // sequential blocks need no seek (a seek drops the stdio buffer)
@@ -385,9 +387,62 @@ bool BgzfReader::getline(std::string& line) {
   }
 }
 
+uint64_t BgzfReader::tell() const {
+  if (mcoff_.size() < 2) return (block_coff_ << 16) | (uint64_t)pos_;
+  // the chunk's member holding pos_; a member boundary reached by reading is
+  // the end of the earlier member, as for single blocks
+  size_t k = (size_t)(std::upper_bound(muoff_.begin(), muoff_.end() - 1, (int64_t)pos_) - muoff_.begin()) - 1;
+  if (k > 0 && (int64_t)pos_ == muoff_[k]) --k;
+  return ((uint64_t)mcoff_[k] << 16) | (uint64_t)(pos_ - (size_t)muoff_[k]);
+}
+
+void BgzfReader::use_device(int device, size_t first, size_t next) {
+  constexpr size_t kMinChunk = 1 << 17;  // two whole members at least
+  device_ = device;
+  // FCS_BGZF_DEVICE_CHUNK (tests): every load reads this many bytes
+  if (const char* e = std::getenv("FCS_BGZF_DEVICE_CHUNK"); e && std::atoll(e) > 0) first = next = (size_t)std::atoll(e);
+  chunk_first_ = std::max(first, kMinChunk);
+  chunk_next_ = std::max(next, kMinChunk);
+  want_ = chunk_first_;
+}
+
+bool BgzfReader::load_chunk() {
+  for (;;) {
+    block_coff_ = next_coff_;
+    if (std::ftell(f_) != (long)block_coff_ && std::fseek(f_, (long)block_coff_, SEEK_SET) != 0) return false;
+    comp_.resize(want_);
+    const size_t got = std::fread(comp_.data(), 1, want_, f_);
+    want_ = chunk_next_;
+    if (got == 0) return false;
+    const size_t cap = got / 20 + 2;
+    mcoff_.resize(cap + 1);
+    muoff_.resize(cap + 1);
+    int32_t n = 0;
+    int64_t used = 0;
+    if (fcs_bgzf_index(comp_.data(), (int64_t)got, mcoff_.data(), muoff_.data(), (int32_t)cap, &n, &used) != FCS_OK)
+      throw formatError(std::string("BGZF at offset ") + std::to_string(block_coff_) + ": " + fcs_last_error());
+    if (n == 0) throw formatError("truncated BGZF block at offset " + std::to_string(block_coff_));
+    mcoff_.resize((size_t)n + 1);
+    muoff_.resize((size_t)n + 1);
+    block_.resize((size_t)muoff_[(size_t)n]);
+    int64_t used2 = 0, out = 0;
+    if (fcs_bgzf_inflate(comp_.data(), used, block_.data(), (int64_t)block_.size(), &used2, &out, device_) != FCS_OK)
+      throw formatError(std::string("BGZF at offset ") + std::to_string(block_coff_) + ": " + fcs_last_error());
+    for (int32_t k = 0; k <= n; ++k) mcoff_[(size_t)k] += (int64_t)block_coff_;
+    for (int32_t k = 0; k < n; ++k)
+      if (muoff_[(size_t)k + 1] == muoff_[(size_t)k]) saw_eof_ = true;  // empty member (the EOF marker)
+    next_coff_ = block_coff_ + (uint64_t)used;
+    pos_ = 0;
+    if (!block_.empty()) return true;
+  }
+}
+
 void BgzfReader::seek(uint64_t voff) {
   next_coff_ = voff >> 16;
   block_.clear();
+  mcoff_.clear();
+  muoff_.clear();
+  if (device_ >= 0) want_ = chunk_first_;
   pos_ = 0;
   if (!load_block()) throw formatError("seek past end of BGZF file");
   pos_ = (size_t)(voff & 0xffff);

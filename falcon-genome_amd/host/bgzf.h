@@ -113,17 +113,29 @@ class BgzfReader {
     pos_ += n;
     return p;
   }
-  uint64_t tell() const { return (block_coff_ << 16) | (uint64_t)pos_; }
+  uint64_t tell() const;
   void seek(uint64_t voff);
   bool saw_eof_marker() const { return saw_eof_; }
+  // Device mode: from the next load on, members are inflated on GPU `device`
+  // many at a time (fcs_bgzf_inflate): a load reads
+  // `first` compressed bytes (then `next` per further load), inflates every
+  // whole member in them in one call and serves their concatenated output as
+  // one block, so records spanning members are viewed in place too.  `first`
+  // is the caller's estimate of its range (a BAI span), rounded up.
+  void use_device(int device, size_t first, size_t next = 1 << 20);
 
  private:
   bool load_block();  // false at end of file
+  bool load_chunk();  // device mode's load_block
   FILE* f_ = nullptr;
   std::vector<uint8_t> block_, comp_;
   size_t pos_ = 0;
   uint64_t block_coff_ = 0, next_coff_ = 0;
   bool saw_eof_ = false;
+  // device mode: the chunk's members (file offsets, output offsets; n + 1)
+  int device_ = -1;
+  size_t chunk_first_ = 0, chunk_next_ = 0, want_ = 0;
+  std::vector<int64_t> mcoff_, muoff_;
 };
 
 // Whole-buffer helpers (tests, small files).

@@ -46,6 +46,7 @@ struct CallerOptions {
   int combine_ms = 0;
   int64_t combine_max_pairs = 4000000;
   bool fp64_rescue = true;
+  bool gpu_inflate = true;  // window BAM blocks through fcs_bgzf_inflate (BgzfReader::use_device)
   double min_qual = 30.0;  // stand_call_conf
   double tlod = 6.3, nlod = 2.2;
   std::string dump_path;  // if set: append every region's PairHMM inputs/outputs here (tests)

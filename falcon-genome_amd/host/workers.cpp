@@ -42,6 +42,7 @@ CallerOptions caller_options_from_config(int gpu) {
   o.batch_regions = c.get_int("gpu.phmm.batch_regions");
   o.combine_ms = c.get_int("gpu.phmm.combine_ms");
   o.fp64_rescue = c.get_bool("gpu.phmm.rescue");
+  o.gpu_inflate = c.get_bool("gpu.bam_inflate");
   o.tlod = std::stod(c.get_string("mutect2.tlod"));
   o.nlod = std::stod(c.get_string("mutect2.nlod"));
   if (o.padding < 0 || o.max_region < 1 || o.batch_regions < 1 || o.max_reads_per_region < 1 || o.combine_ms < 0)

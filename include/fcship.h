@@ -333,6 +333,39 @@ fcs_kswr fcs_ksw_align2(int qlen, const uint8_t* query, int tlen, const uint8_t*
                         int o_del, int e_del, int o_ins, int e_ins, int xtra, void** qry);
 int fcs_set_default_device(int32_t device);
 
+/* ------------------------------------------------------ BGZF inflate (§8 f3) */
+/* The BAM / BGZF container in front of the PairHMM path:
+ * the reference's `htc` reads its window through htslib's bgzf_read
+ * (htslib bgzf.c inflate_block: one raw-DEFLATE member at a time, CRC-32
+ * checked); these entry points inflate a run of whole members on the GPU.
+ *
+ * fcs_bgzf_index walks the members of comp[0, comp_bytes) (gzip header with
+ * the BC extra field, payload, CRC32, ISIZE), stopping before an incomplete
+ * member or after cap members: coff[0..n] = member starts (coff[n] = bytes of
+ * whole members = *comp_used), uoff[0..n] = their inflated starts (prefix sums
+ * of ISIZE).  FCS_ERR_INVALID when the bytes at a member start are not a
+ * BGZF header.
+ *
+ * fcs_bgzf_inflate: host buffers; inflates the whole members of comp into
+ * out (concatenated), *out_bytes = their inflated size (FCS_ERR_INVALID when it
+ * exceeds out_cap, or when a member is corrupt / fails its CRC: the message
+ * names the member).  A trailing incomplete member is left for the next call
+ * (*comp_used tells where it starts).
+ *
+ * fcs_bgzf_inflate_dev: device buffers, stream-ordered; dev_coff / dev_uoff
+ * as fcs_bgzf_index returns them, dev_status[k] = FCS_BGZF_* of member k
+ * (member k's output is written only when it is FCS_BGZF_OK). */
+#define FCS_BGZF_OK 0
+#define FCS_BGZF_CORRUPT 1  /* bad DEFLATE stream, header or ISIZE */
+#define FCS_BGZF_OVERFLOW 2 /* the stream inflates past ISIZE */
+#define FCS_BGZF_CRC 3      /* CRC-32 mismatch */
+int fcs_bgzf_index(const uint8_t* comp, int64_t comp_bytes, int64_t* coff, int64_t* uoff, int32_t cap,
+                   int32_t* n_members, int64_t* comp_used);
+int fcs_bgzf_inflate(const uint8_t* comp, int64_t comp_bytes, uint8_t* out, int64_t out_cap, int64_t* comp_used,
+                     int64_t* out_bytes, int32_t device);
+int fcs_bgzf_inflate_dev(const uint8_t* dev_comp, const int64_t* dev_coff, const int64_t* dev_uoff, int32_t n,
+                         uint8_t* dev_out, int32_t* dev_status, int32_t device, void* stream);
+
 /* ---------------------------------------------- synthetic workload builders */
 /* Seeded generators for the benchmark configurations (BASELINE.json C2/C3).
  * Deterministic for a given seed.  Callers size the buffers with the *_sizes

@@ -232,3 +232,101 @@ int fcs_phmm_last_device_ms(double* device_ms, double* rescue_ms) {
   *device_ms = *rescue_ms = 0;
   return FCS_OK;
 }
+
+/* BGZF inflate: the member walk restated and zlib's raw inflate per member
+ * (the GPU path is checked against this mock and against zlib in the tests). */
+#include <zlib.h>
+
+static uint32_t mock_le16(const uint8_t* p) { return (uint32_t)p[0] | (uint32_t)p[1] << 8; }
+
+int fcs_bgzf_index(const uint8_t* comp, int64_t comp_bytes, int64_t* coff, int64_t* uoff, int32_t cap,
+                   int32_t* n_members, int64_t* comp_used) {
+  if (!n_members || !comp_used || comp_bytes < 0 || cap < 0 || (comp_bytes > 0 && !comp) || !coff || !uoff) {
+    g_err = "[E::fcs_bgzf_index] bad arguments";
+    return FCS_ERR_INVALID;
+  }
+  int64_t at = 0, u = 0;
+  int32_t k = 0;
+  while (k < cap && comp_bytes - at >= 18) {
+    const uint8_t* h = comp + at;
+    if (h[0] != 31 || h[1] != 139 || h[2] != 8 || !(h[3] & 4)) {
+      g_err = "[E::fcs_bgzf_index] no BGZF header";
+      return FCS_ERR_INVALID;
+    }
+    const int64_t xlen = mock_le16(h + 10);
+    if (comp_bytes - at < 12 + xlen) break;
+    int64_t bsize = -1;
+    for (int64_t x = 12; x + 4 <= 12 + xlen;) {
+      const int64_t slen = mock_le16(h + x + 2);
+      if (h[x] == 'B' && h[x + 1] == 'C' && slen == 2 && x + 6 <= 12 + xlen) bsize = mock_le16(h + x + 4);
+      x += 4 + slen;
+    }
+    if (bsize < 0 || bsize + 1 < 12 + xlen + 8) {
+      g_err = "[E::fcs_bgzf_index] no BGZF block size";
+      return FCS_ERR_INVALID;
+    }
+    const int64_t len = bsize + 1;
+    if (comp_bytes - at < len) break;
+    const int64_t isize = (int64_t)(mock_le16(h + len - 4) | mock_le16(h + len - 2) << 16);
+    if (isize > 65536) {
+      g_err = "[E::fcs_bgzf_index] member inflates past 64 KiB";
+      return FCS_ERR_INVALID;
+    }
+    coff[k] = at;
+    uoff[k] = u;
+    at += len;
+    u += isize;
+    ++k;
+  }
+  coff[k] = at;
+  uoff[k] = u;
+  *n_members = k;
+  *comp_used = at;
+  return FCS_OK;
+}
+
+int fcs_bgzf_inflate(const uint8_t* comp, int64_t comp_bytes, uint8_t* out, int64_t out_cap, int64_t* comp_used,
+                     int64_t* out_bytes, int32_t device) {
+  (void)device;
+  if (!comp_used || !out_bytes || comp_bytes < 0 || (comp_bytes > 0 && !comp) || out_cap < 0 || (out_cap > 0 && !out)) {
+    g_err = "[E::fcs_bgzf_inflate] bad arguments";
+    return FCS_ERR_INVALID;
+  }
+  *comp_used = *out_bytes = 0;
+  const int64_t most = comp_bytes / 20 + 1;
+  int64_t* coff = malloc(sizeof(int64_t) * (size_t)(most + 1));
+  int64_t* uoff = malloc(sizeof(int64_t) * (size_t)(most + 1));
+  int32_t n = 0;
+  int64_t used = 0;
+  int rc = coff && uoff ? fcs_bgzf_index(comp, comp_bytes, coff, uoff, (int32_t)most, &n, &used) : FCS_ERR_NOMEM;
+  if (rc == FCS_OK && uoff[n] > out_cap) {
+    g_err = "[E::fcs_bgzf_inflate] output larger than its capacity";
+    rc = FCS_ERR_INVALID;
+  }
+  for (int32_t k = 0; rc == FCS_OK && k < n; ++k) {
+    const uint8_t* h = comp + coff[k];
+    const int64_t xlen = mock_le16(h + 10), len = coff[k + 1] - coff[k], isize = uoff[k + 1] - uoff[k];
+    z_stream zs;
+    memset(&zs, 0, sizeof zs);
+    inflateInit2(&zs, -15);
+    zs.next_in = (Bytef*)(h + 12 + xlen);
+    zs.avail_in = (uInt)(len - 12 - xlen - 8);
+    zs.next_out = out + uoff[k];
+    zs.avail_out = (uInt)isize;
+    const int z = inflate(&zs, Z_FINISH);
+    const int64_t got = (int64_t)zs.total_out;
+    inflateEnd(&zs);
+    const uint32_t want = mock_le16(h + len - 8) | mock_le16(h + len - 6) << 16;
+    if (z != Z_STREAM_END || got != isize || (uint32_t)crc32(0, out + uoff[k], (uInt)isize) != want) {
+      g_err = "[E::fcs_bgzf_inflate] corrupt member";
+      rc = FCS_ERR_INVALID;
+    }
+  }
+  if (rc == FCS_OK) {
+    *comp_used = used;
+    *out_bytes = uoff[n];
+  }
+  free(coff);
+  free(uoff);
+  return rc;
+}

@@ -1,0 +1,110 @@
+"""GPU parity: BGZF member inflation (fcs_bgzf_inflate / _dev, SURVEY.md §8
+row f3) against zlib.
+
+Bar: bit-exact — every inflated byte equals zlib's, for members written by
+zlib at every level and strategy, by libdeflate (the host's BAM / GVCF codec),
+stored blocks, empty and EOF members, and a whole BAM from `fcs-genome
+synth`; corrupt streams, CRC mismatches and lying ISIZEs are reported per
+member, never written out.
+"""
+import struct
+import zlib
+
+import numpy as np
+import pytest
+
+import bgzf_cases
+import fcship
+
+pytestmark = pytest.mark.gpu
+
+
+def test_inflate_members_one_by_one(gpu):
+    for label, m, p in bgzf_cases.suite(seed=11, count=60):
+        out, used = fcship.bgzf_inflate(m, device=gpu)
+        assert used == len(m), label
+        assert out == p, label
+
+
+def test_inflate_concatenated_batch(gpu):
+    cases = bgzf_cases.suite(seed=12, count=400)
+    blob = b"".join(m for _, m, _ in cases)
+    out, used = fcship.bgzf_inflate(blob, device=gpu)
+    assert used == len(blob)
+    assert out == b"".join(p for _, _, p in cases)
+
+
+def test_inflate_whole_bam(gpu, tmp_path):
+    import host_lib as H
+    p = H.run_cli("synth", "-o", tmp_path, "-c", "chrA:200000", "-x", "10", "--seed", "4")
+    assert p.returncode == 0, p.stderr
+    blob = (tmp_path / "sample.bam").read_bytes()
+    coff, _, _ = fcship.bgzf_index(blob)
+    want = b"".join(zlib.decompress(blob[coff[k] + 18:coff[k + 1] - 8], -15) for k in range(len(coff) - 1))
+    out, used = fcship.bgzf_inflate(blob, device=gpu)
+    assert used == len(blob) and out == want
+
+
+def test_trailing_partial_member_is_left(gpu):
+    cases = bgzf_cases.suite(seed=13, count=8)
+    blob = b"".join(m for _, m, _ in cases)
+    out, used = fcship.bgzf_inflate(blob[:-5], device=gpu)
+    assert used == len(blob) - len(cases[-1][1])
+    assert out == b"".join(p for _, _, p in cases[:-1])
+
+
+def _with_bad(cases, k, bad):
+    return b"".join(bad if i == k else m for i, (_, m, _) in enumerate(cases))
+
+
+def test_corruption_is_reported_per_member(gpu):
+    rng = np.random.default_rng(14)
+    cases = [c for c in bgzf_cases.suite(seed=14, count=40) if len(c[2]) > 1000]
+    k = 3
+    m = bytearray(cases[k][1])
+    # a wrong CRC-32
+    crc = bytearray(m)
+    crc[-8] ^= 1
+    with pytest.raises(fcship.FcsError, match=f"member {k} .*CRC-32 mismatch"):
+        fcship.bgzf_inflate(_with_bad(cases, k, bytes(crc)), device=gpu)
+    # an ISIZE smaller than the stream
+    short = bytearray(m)
+    short[-4:] = struct.pack("<I", len(cases[k][2]) - 1)
+    with pytest.raises(fcship.FcsError, match=f"member {k} "):
+        fcship.bgzf_inflate(_with_bad(cases, k, bytes(short)), device=gpu)
+    # flipped bits in the DEFLATE stream: an error (corrupt, overflow or CRC),
+    # never a fault; the other members are unaffected
+    for trial in range(40):
+        bad = bytearray(m)
+        at = 18 + int(rng.integers(0, len(m) - 26))
+        bad[at] ^= 1 << int(rng.integers(0, 8))
+        with pytest.raises(fcship.FcsError, match=f"member {k} "):
+            fcship.bgzf_inflate(_with_bad(cases, k, bytes(bad)), device=gpu)
+    out, _ = fcship.bgzf_inflate(b"".join(c[1] for c in cases), device=gpu)
+    assert out == b"".join(c[2] for c in cases)
+
+
+def test_inflate_dev_statuses(gpu):
+    import torch
+    cases = bgzf_cases.suite(seed=15, count=30)
+    bad_k = 5
+    ms = [bytearray(m) for _, m, _ in cases]
+    ms[bad_k][-8] ^= 0x80  # CRC
+    blob = b"".join(bytes(m) for m in ms)
+    coff, uoff, used = fcship.bgzf_index(blob)
+    dev = torch.device("cuda", 0)
+    comp = torch.from_numpy(np.frombuffer(blob, np.uint8).copy()).to(dev)
+    dco = torch.from_numpy(coff).to(dev)
+    duo = torch.from_numpy(uoff).to(dev)
+    out = torch.zeros(int(uoff[-1]) + 1, dtype=torch.uint8, device=dev)
+    st = torch.full((len(coff) - 1,), -1, dtype=torch.int32, device=dev)
+    fcship.check(fcship.lib.fcs_bgzf_inflate_dev(comp.data_ptr(), dco.data_ptr(), duo.data_ptr(), len(coff) - 1,
+                                                 out.data_ptr(), st.data_ptr(), 0, None))
+    torch.cuda.synchronize()
+    s = st.cpu().numpy()
+    assert s[bad_k] == fcship.FCS_BGZF_CRC
+    assert (np.delete(s, bad_k) == fcship.FCS_BGZF_OK).all()
+    o = out.cpu().numpy().tobytes()
+    for k, (_, _, p) in enumerate(cases):
+        if k != bad_k:
+            assert o[uoff[k]:uoff[k + 1]] == p

@@ -55,10 +55,10 @@ def covered_truth(d):
     return out, len(recs), (lo, hi)
 
 
-def run_cpu(mode, c1, mock_dir, tmp_path, name):
+def run_cpu(mode, c1, mock_dir, tmp_path, name, extra_env=None):
     out = tmp_path / f"{name}.vcf"
     env = {"LD_LIBRARY_PATH": mock_dir, "FCS_GPU_DEVICES": "0", "FCS_MOCK_PHMM": mode,
-           "FCS_LOG_DIR": str(tmp_path / f"log_{name}")}
+           "FCS_LOG_DIR": str(tmp_path / f"log_{name}"), **(extra_env or {})}
     p = H.run_cli("htc", "-f", "-r", c1 / "ref.fasta", "-i", c1 / "sample.bam", "-o", out, "-v", env=env,
                   cwd=tmp_path)
     assert p.returncode == 0, p.stderr[-3000:]
@@ -88,3 +88,35 @@ def test_c1_java_and_gkl_semantics_agree(c1, mock_dir, tmp_path):
     strip = lambda f: [ln for ln in open(f) if not ln.startswith("##")]  # noqa: E731
     assert calls(a) == calls(b)
     assert strip(a) == strip(b)
+
+
+def test_c1_window_inflate_paths_agree(c1, mock_dir, tmp_path):
+    """The window's BAM blocks read member by member with the host's
+    libdeflate (gpu.bam_inflate=false) and in multi-member chunks through
+    fcs_bgzf_inflate (the default; here the mock's zlib behind the same
+    C-ABI) give byte-identical VCFs: the chunk reader's seeks, record
+    boundaries across members and window ends are the same."""
+    a = run_cpu("gkl", c1, mock_dir, tmp_path, "chunked")
+    b = run_cpu("gkl", c1, mock_dir, tmp_path, "host", {"FCS_GPU_BAM_INFLATE": "false"})
+    strip = lambda f: [ln for ln in open(f) if not ln.startswith("##")]  # noqa: E731
+    assert strip(a) == strip(b)
+
+
+def test_window_inflate_chunks_cross_members(mock_dir, tmp_path):
+    """Many 128 KiB chunks per window (FCS_BGZF_DEVICE_CHUNK), several
+    windows and shards: records split across chunk ends, chunks ending
+    mid-member and BAI seeks into a chunk give the same VCF as the host's
+    member-by-member reader."""
+    d = tmp_path / "in"
+    p = H.run_cli("synth", "-o", d, "-c", "chrA:400000,chrB:150000", "-x", "12", "--no-fastq", "--seed", "9")
+    assert p.returncode == 0, p.stderr[-2000:]
+    outs = []
+    for name, env in (("chunked", {"FCS_BGZF_DEVICE_CHUNK": str(128 << 10)}), ("host", {"FCS_GPU_BAM_INFLATE": "false"})):
+        out = tmp_path / f"{name}.vcf"
+        e = {"LD_LIBRARY_PATH": mock_dir, "FCS_GPU_DEVICES": "0", "FCS_MOCK_PHMM": "gkl",
+             "FCS_LOG_DIR": str(tmp_path / f"log_{name}"), **env}
+        p = H.run_cli("htc", "-f", "-r", d / "ref.fasta", "-i", d / "sample.bam", "-o", out, "-v", env=e, cwd=tmp_path)
+        assert p.returncode == 0, p.stderr[-3000:]
+        outs.append([ln for ln in open(out) if not ln.startswith("##")])
+    assert len(outs[0]) > 20
+    assert outs[0] == outs[1]
