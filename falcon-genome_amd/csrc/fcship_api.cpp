@@ -140,6 +140,7 @@ struct Session {
   void* host = nullptr;
   size_t host_cap = 0;
   hipEvent_t ev[3] = {nullptr, nullptr, nullptr};  // PairHMM call: start, after forward, after rescue
+  hipEvent_t done = nullptr;                        // inflate sessions: a blocking-sync event (no host spin)
   int ensure_dev(size_t bytes);
   int ensure_host(size_t bytes);
   int ensure_phmm(int64_t pairs);
@@ -152,13 +153,24 @@ namespace {
 
 size_t grown(size_t need, size_t cap) { return std::max(need + need / 4, std::min<size_t>(2 * cap, need + (1u << 30))); }
 
-int sessions_per_device() {
-  static const int n = [] {
-    const char* e = std::getenv("FCS_SESSIONS_PER_DEVICE");
-    const int v = e && *e ? std::atoi(e) : 4;
-    return std::max(1, std::min(v, 64));
-  }();
-  return n;
+// Pool kinds: the compute sessions (PairHMM / SW entry points) and the BGZF
+// inflate sessions, a pool of their own so the htc shards' many small inflate
+// calls (one per 4 MiB of compressed BAM) neither wait behind PairHMM passes
+// nor pay for fork streams they never use.
+enum SessionKind : int { kComputeSession = 0, kInflateSession = 1 };
+
+int sessions_per_device(int kind = kComputeSession) {
+  static const int n[2] = {[] {
+                             const char* e = std::getenv("FCS_SESSIONS_PER_DEVICE");
+                             const int v = e && *e ? std::atoi(e) : 4;
+                             return std::max(1, std::min(v, 64));
+                           }(),
+                           [] {
+                             const char* e = std::getenv("FCS_BGZF_SESSIONS_PER_DEVICE");
+                             const int v = e && *e ? std::atoi(e) : 16;
+                             return std::max(1, std::min(v, 64));
+                           }()};
+  return n[kind];
 }
 
 struct SessionPool {
@@ -168,20 +180,21 @@ struct SessionPool {
   int creating = 0;
 };
 
-SessionPool& session_pool(int device) {
+SessionPool& session_pool(int device, int kind = kComputeSession) {
   static std::mutex mu;
-  static auto* pools = new std::map<int, SessionPool*>();
+  static auto* pools = new std::map<std::pair<int, int>, SessionPool*>();
   std::lock_guard<std::mutex> lk(mu);
-  SessionPool*& p = (*pools)[device];
+  SessionPool*& p = (*pools)[{device, kind}];
   if (!p) p = new SessionPool();
   return *p;
 }
 
 // A new session on `device` (the current device), or null.
-Session* create_session(int device) {
+Session* create_session(int device, int kind = kComputeSession) {
   auto* S = new Session();
   S->device = device;
-  if (hipStreamCreateWithFlags(&S->s, hipStreamNonBlocking) != hipSuccess || !fork_set(S->s)) {
+  if (hipStreamCreateWithFlags(&S->s, hipStreamNonBlocking) != hipSuccess ||
+      (kind == kComputeSession && !fork_set(S->s))) {
     delete S;  // a failed stream is not reused; nothing else was created
     return nullptr;
   }
@@ -225,9 +238,9 @@ class SessionLease {
   SessionLease(const SessionLease&) = delete;
   SessionLease& operator=(const SessionLease&) = delete;
   ~SessionLease() { release(); }
-  int acquire(int device) {
+  int acquire(int device, int kind = kComputeSession) {
     release();
-    SessionPool& P = session_pool(device);
+    SessionPool& P = session_pool(device, kind);
     std::unique_lock<std::mutex> lk(P.mu);
     for (;;) {
       if (!P.idle.empty()) {
@@ -236,12 +249,12 @@ class SessionLease {
         pool_ = &P;
         return FCS_OK;
       }
-      if ((int)P.all.size() + P.creating < sessions_per_device()) break;
+      if ((int)P.all.size() + P.creating < sessions_per_device(kind)) break;
       P.cv.wait(lk);
     }
     ++P.creating;
     lk.unlock();
-    Session* S = create_session(device);
+    Session* S = create_session(device, kind);
     lk.lock();
     --P.creating;
     if (!S) {
@@ -1659,7 +1672,7 @@ int fcs_bgzf_inflate(const uint8_t* comp, int64_t comp_bytes, uint8_t* out, int6
   if ((rc = check_device(device))) return rc;
   FCS_SET_DEVICE((device));
   SessionLease lease;
-  if ((rc = lease.acquire(device))) return rc;
+  if ((rc = lease.acquire(device, kInflateSession))) return rc;
   Session* S = lease.get();
   const size_t nn = (size_t)n;
   Layout L;
@@ -1676,7 +1689,11 @@ int fcs_bgzf_inflate(const uint8_t* comp, int64_t comp_bytes, uint8_t* out, int6
                                 S->d<int32_t>(ost), s)))
     return rc;
   FCS_HIP_CHECK(hipMemcpyAsync(S->h<void>(ost), S->d<void>(ost), L.total - ost, hipMemcpyDeviceToHost, s));
-  FCS_HIP_CHECK(hipStreamSynchronize(s));
+  // the calling shard thread sleeps until the copy lands: a spinning wait of
+  // 16 shard threads costs more host time than the inflate saves
+  if (!S->done) FCS_HIP_CHECK(hipEventCreateWithFlags(&S->done, hipEventBlockingSync | hipEventDisableTiming));
+  FCS_HIP_CHECK(hipEventRecord(S->done, s));
+  FCS_HIP_CHECK(hipEventSynchronize(S->done));
   const int32_t* st = S->h<int32_t>(ost);
   for (size_t k = 0; k < nn; ++k)
     if (st[k] != FCS_BGZF_OK) {

@@ -97,9 +97,9 @@ class BamReader {
   bool next_raw(const uint8_t*& body, size_t& n);
   uint64_t tell() const { return bgzf_.tell(); }
   void seek(uint64_t voff) { bgzf_.seek(voff); }
-  // BgzfReader::use_device: later blocks inflated on GPU `device`, `first`
-  // compressed bytes at the first load
-  void use_device(int device, size_t first) { bgzf_.use_device(device, first); }
+  // BgzfReader::use_device: later blocks inflated on GPU `device`; `span` =
+  // the estimated compressed bytes of the range read from the next seek
+  void use_device(int device, size_t span) { bgzf_.use_device(device, span); }
 
  private:
   BgzfReader bgzf_;

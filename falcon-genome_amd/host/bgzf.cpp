@@ -295,6 +295,7 @@ BgzfReader::BgzfReader(const std::string& path) {
 }
 
 BgzfReader::~BgzfReader() {
+  drop_ahead();  // the helper thread reads f_
   if (f_) std::fclose(f_);
 }
 
@@ -396,53 +397,97 @@ uint64_t BgzfReader::tell() const {
   return ((uint64_t)mcoff_[k] << 16) | (uint64_t)(pos_ - (size_t)muoff_[k]);
 }
 
-void BgzfReader::use_device(int device, size_t first, size_t next) {
-  constexpr size_t kMinChunk = 1 << 17;  // two whole members at least
+void BgzfReader::use_device(int device, size_t span) {
   device_ = device;
-  // FCS_BGZF_DEVICE_CHUNK (tests): every load reads this many bytes
-  if (const char* e = std::getenv("FCS_BGZF_DEVICE_CHUNK"); e && std::atoll(e) > 0) first = next = (size_t)std::atoll(e);
-  chunk_first_ = std::max(first, kMinChunk);
-  chunk_next_ = std::max(next, kMinChunk);
-  want_ = chunk_first_;
+  chunk_ = 16u << 20;
+  if (const char* e = std::getenv("FCS_BGZF_DEVICE_CHUNK"); e && std::atoll(e) > 0) chunk_ = (size_t)std::atoll(e);
+  chunk_ = std::max<size_t>(chunk_, 1 << 17);  // two whole members at least
+  span_ = span;
+  range_start_ = next_coff_;
+  want_ = first_want();
+}
+
+// The first load after a seek covers the caller's whole estimated range in
+// one call (the kernel's rate comes from many members in flight: a shard's
+// range is a few hundred members, a chunk of it a few dozen), at most 256 MiB.
+size_t BgzfReader::first_want() const {
+  if (std::getenv("FCS_BGZF_DEVICE_CHUNK")) return chunk_;
+  return span_ ? std::min<size_t>(std::max<size_t>(span_, 1 << 17), 256u << 20) : chunk_;
+}
+
+// Reads `want` bytes at `at` and inflates their whole members into c.
+void BgzfReader::fetch(uint64_t at, size_t want, Chunk& c) {
+  c.start = at;
+  c.used = 0;
+  c.out.clear();
+  c.empty_member = false;
+  if (std::ftell(f_) != (long)at && std::fseek(f_, (long)at, SEEK_SET) != 0) return;
+  c.comp.resize(want);
+  const size_t got = std::fread(c.comp.data(), 1, want, f_);
+  if (got == 0) return;
+  const size_t cap = got / 20 + 2;
+  c.coff.resize(cap + 1);
+  c.uoff.resize(cap + 1);
+  int32_t n = 0;
+  int64_t used = 0;
+  if (fcs_bgzf_index(c.comp.data(), (int64_t)got, c.coff.data(), c.uoff.data(), (int32_t)cap, &n, &used) != FCS_OK)
+    throw formatError(std::string("BGZF at offset ") + std::to_string(at) + ": " + fcs_last_error());
+  if (n == 0) throw formatError("truncated BGZF block at offset " + std::to_string(at));
+  c.coff.resize((size_t)n + 1);
+  c.uoff.resize((size_t)n + 1);
+  c.out.resize((size_t)c.uoff[(size_t)n]);
+  int64_t used2 = 0, out = 0;
+  if (fcs_bgzf_inflate(c.comp.data(), used, c.out.data(), (int64_t)c.out.size(), &used2, &out, device_) != FCS_OK)
+    throw formatError(std::string("BGZF at offset ") + std::to_string(at) + ": " + fcs_last_error());
+  for (int32_t k = 0; k <= n; ++k) c.coff[(size_t)k] += (int64_t)at;
+  for (int32_t k = 0; k < n; ++k)
+    if (c.uoff[(size_t)k + 1] == c.uoff[(size_t)k]) c.empty_member = true;  // the EOF marker
+  c.used = (uint64_t)used;
+}
+
+void BgzfReader::drop_ahead() {
+  if (!ahead_job_.valid()) return;
+  try {
+    ahead_job_.get();
+  } catch (...) {  // a prefetch past the caller's range may fail; it is not used
+  }
 }
 
 bool BgzfReader::load_chunk() {
   for (;;) {
-    block_coff_ = next_coff_;
-    if (std::ftell(f_) != (long)block_coff_ && std::fseek(f_, (long)block_coff_, SEEK_SET) != 0) return false;
-    comp_.resize(want_);
-    const size_t got = std::fread(comp_.data(), 1, want_, f_);
-    want_ = chunk_next_;
-    if (got == 0) return false;
-    const size_t cap = got / 20 + 2;
-    mcoff_.resize(cap + 1);
-    muoff_.resize(cap + 1);
-    int32_t n = 0;
-    int64_t used = 0;
-    if (fcs_bgzf_index(comp_.data(), (int64_t)got, mcoff_.data(), muoff_.data(), (int32_t)cap, &n, &used) != FCS_OK)
-      throw formatError(std::string("BGZF at offset ") + std::to_string(block_coff_) + ": " + fcs_last_error());
-    if (n == 0) throw formatError("truncated BGZF block at offset " + std::to_string(block_coff_));
-    mcoff_.resize((size_t)n + 1);
-    muoff_.resize((size_t)n + 1);
-    block_.resize((size_t)muoff_[(size_t)n]);
-    int64_t used2 = 0, out = 0;
-    if (fcs_bgzf_inflate(comp_.data(), used, block_.data(), (int64_t)block_.size(), &used2, &out, device_) != FCS_OK)
-      throw formatError(std::string("BGZF at offset ") + std::to_string(block_coff_) + ": " + fcs_last_error());
-    for (int32_t k = 0; k <= n; ++k) mcoff_[(size_t)k] += (int64_t)block_coff_;
-    for (int32_t k = 0; k < n; ++k)
-      if (muoff_[(size_t)k + 1] == muoff_[(size_t)k]) saw_eof_ = true;  // empty member (the EOF marker)
-    next_coff_ = block_coff_ + (uint64_t)used;
+    if (ahead_job_.valid()) {
+      ahead_job_.get();  // a failure of the chunk the caller needs is reported here
+      std::swap(cur_, ahead_);
+    } else {
+      fetch(next_coff_, want_, cur_);
+    }
+    want_ = chunk_;
+    if (cur_.used == 0) return false;
+    block_.swap(cur_.out);
+    mcoff_.swap(cur_.coff);
+    muoff_.swap(cur_.uoff);
+    block_coff_ = cur_.start;
+    next_coff_ = cur_.start + cur_.used;
+    saw_eof_ = saw_eof_ || cur_.empty_member;
     pos_ = 0;
+    // the next chunk on a helper thread while the caller parses this one,
+    // inside the caller's estimated range only
+    if (!span_ || next_coff_ - range_start_ < span_)
+      ahead_job_ = std::async(std::launch::async, [this, at = next_coff_, w = want_] { fetch(at, w, ahead_); });
     if (!block_.empty()) return true;
   }
 }
 
 void BgzfReader::seek(uint64_t voff) {
+  drop_ahead();
   next_coff_ = voff >> 16;
   block_.clear();
   mcoff_.clear();
   muoff_.clear();
-  if (device_ >= 0) want_ = chunk_first_;
+  if (device_ >= 0) {
+    range_start_ = next_coff_;
+    want_ = first_want();
+  }
   pos_ = 0;
   if (!load_block()) throw formatError("seek past end of BGZF file");
   pos_ = (size_t)(voff & 0xffff);

@@ -117,25 +117,40 @@ class BgzfReader {
   void seek(uint64_t voff);
   bool saw_eof_marker() const { return saw_eof_; }
   // Device mode: from the next load on, members are inflated on GPU `device`
-  // many at a time (fcs_bgzf_inflate): a load reads
-  // `first` compressed bytes (then `next` per further load), inflates every
-  // whole member in them in one call and serves their concatenated output as
-  // one block, so records spanning members are viewed in place too.  `first`
-  // is the caller's estimate of its range (a BAI span), rounded up.
-  void use_device(int device, size_t first, size_t next = 1 << 20);
+  // many at a time (fcs_bgzf_inflate): a load reads a
+  // chunk of compressed bytes, inflates every whole member in it in one call
+  // and serves their concatenated output as one block, so records spanning
+  // members are viewed in place too.  `span` is the caller's estimate of its
+  // compressed range from the next seek (a BAI span; 0: unknown): the first
+  // load covers it whole, later loads read 16 MiB (FCS_BGZF_DEVICE_CHUNK sets
+  // every load's size), and while inside the range the next chunk is read and
+  // inflated on a helper thread while the caller parses the current one.
+  void use_device(int device, size_t span);
 
  private:
+  struct Chunk {
+    uint64_t start = 0, used = 0;  // file offset, bytes of whole members
+    std::vector<uint8_t> comp, out;
+    std::vector<int64_t> coff, uoff;  // absolute member offsets, output offsets (n + 1)
+    bool empty_member = false;
+  };
   bool load_block();  // false at end of file
   bool load_chunk();  // device mode's load_block
+  void fetch(uint64_t at, size_t want, Chunk& c);
+  size_t first_want() const;
+  void drop_ahead();
   FILE* f_ = nullptr;
   std::vector<uint8_t> block_, comp_;
   size_t pos_ = 0;
   uint64_t block_coff_ = 0, next_coff_ = 0;
   bool saw_eof_ = false;
-  // device mode: the chunk's members (file offsets, output offsets; n + 1)
+  // device mode
   int device_ = -1;
-  size_t chunk_first_ = 0, chunk_next_ = 0, want_ = 0;
-  std::vector<int64_t> mcoff_, muoff_;
+  size_t chunk_ = 0, span_ = 0, want_ = 0;
+  uint64_t range_start_ = 0;
+  std::vector<int64_t> mcoff_, muoff_;  // the current chunk's members
+  Chunk cur_, ahead_;
+  std::future<void> ahead_job_;
 };
 
 // Whole-buffer helpers (tests, small files).

@@ -88,12 +88,11 @@ void load_reads_one(const std::string& bam, const std::string& chrom, int64_t be
       // the window's compressed span by the BAI's linear index at its end,
       // plus the reads that start in that last 16 kb window
       const uint64_t e = ix.seek_offset(tid, end);
-      const size_t span = e > off ? (size_t)((e >> 16) - (off >> 16)) : (size_t)8 << 20;
-      rd.use_device(opt.gpu, span + (256 << 10));
+      rd.use_device(opt.gpu, e > off ? (size_t)((e >> 16) - (off >> 16)) + (256 << 10) : 0);
     }
     if (off) rd.seek(off);
   } else if (opt.gpu_inflate) {
-    rd.use_device(opt.gpu, (size_t)8 << 20);
+    rd.use_device(opt.gpu, 0);
   }
   // fields read straight from the raw record (decode_bam_record's layout),
   // filters applied before SEQ / QUAL are decoded

@@ -46,7 +46,9 @@ struct CallerOptions {
   int combine_ms = 0;
   int64_t combine_max_pairs = 4000000;
   bool fp64_rescue = true;
-  bool gpu_inflate = true;  // window BAM blocks through fcs_bgzf_inflate (BgzfReader::use_device)
+  // window BAM blocks through fcs_bgzf_inflate (BgzfReader::use_device); off by
+  // default: at the htc shard shape the host's libdeflate is faster
+  bool gpu_inflate = false;
   double min_qual = 30.0;  // stand_call_conf
   double tlod = 6.3, nlod = 2.2;
   std::string dump_path;  // if set: append every region's PairHMM inputs/outputs here (tests)

@@ -48,7 +48,8 @@ void Config::init(const std::string& root_dir) {
   declare("gpu.phmm.batch_regions", "4096", "active regions per PairHMM device pass");
   declare("gpu.phmm.combine_ms", "0", "ms a shard's PairHMM pass waits to merge with other shards' (0: no merging)");
   declare("gpu.phmm.rescue", "true", "fp64 rescue of pairs whose fp32 likelihood underflows (GKL)");
-  declare("gpu.bam_inflate", "true", "inflate a calling window's BAM blocks on the GPU (false: host libdeflate)");
+  declare("gpu.bam_inflate", "false",
+          "inflate a calling window's BAM blocks on the GPU (fcs_bgzf_inflate) instead of host libdeflate");
   // caller knobs (GATK HaplotypeCaller / Mutect2 argument defaults)
   declare("htc.min_base_quality", "10", "min base quality counted as evidence of activity");
   declare("htc.base_quality_threshold", "18", "PairHMM: base quals below this become 6");

@@ -92,11 +92,11 @@ def test_c1_java_and_gkl_semantics_agree(c1, mock_dir, tmp_path):
 
 def test_c1_window_inflate_paths_agree(c1, mock_dir, tmp_path):
     """The window's BAM blocks read member by member with the host's
-    libdeflate (gpu.bam_inflate=false) and in multi-member chunks through
-    fcs_bgzf_inflate (the default; here the mock's zlib behind the same
-    C-ABI) give byte-identical VCFs: the chunk reader's seeks, record
+    libdeflate (the default) and in multi-member chunks through
+    fcs_bgzf_inflate (gpu.bam_inflate=true; here the mock's zlib behind the
+    same C-ABI) give byte-identical VCFs: the chunk reader's seeks, record
     boundaries across members and window ends are the same."""
-    a = run_cpu("gkl", c1, mock_dir, tmp_path, "chunked")
+    a = run_cpu("gkl", c1, mock_dir, tmp_path, "chunked", {"FCS_GPU_BAM_INFLATE": "true"})
     b = run_cpu("gkl", c1, mock_dir, tmp_path, "host", {"FCS_GPU_BAM_INFLATE": "false"})
     strip = lambda f: [ln for ln in open(f) if not ln.startswith("##")]  # noqa: E731
     assert strip(a) == strip(b)
@@ -111,7 +111,8 @@ def test_window_inflate_chunks_cross_members(mock_dir, tmp_path):
     p = H.run_cli("synth", "-o", d, "-c", "chrA:400000,chrB:150000", "-x", "12", "--no-fastq", "--seed", "9")
     assert p.returncode == 0, p.stderr[-2000:]
     outs = []
-    for name, env in (("chunked", {"FCS_BGZF_DEVICE_CHUNK": str(128 << 10)}), ("host", {"FCS_GPU_BAM_INFLATE": "false"})):
+    for name, env in (("chunked", {"FCS_GPU_BAM_INFLATE": "true", "FCS_BGZF_DEVICE_CHUNK": str(128 << 10)}),
+                      ("host", {"FCS_GPU_BAM_INFLATE": "false"})):
         out = tmp_path / f"{name}.vcf"
         e = {"LD_LIBRARY_PATH": mock_dir, "FCS_GPU_DEVICES": "0", "FCS_MOCK_PHMM": "gkl",
              "FCS_LOG_DIR": str(tmp_path / f"log_{name}"), **env}
