@@ -48,49 +48,46 @@ struct InfTables {
 
 enum : int { kInfOk = 0, kInfCorrupt = 1, kInfOverflow = 2 };
 
+// Offsets are 32-bit (a member is at most 64 KiB in and out), so the device
+// keeps them in scalar registers with 32-bit compares.  A read past the input
+// leaves `cnt` negative (checked at block ends): zero bits decode to some
+// symbols, but every symbol either advances the output or ends the block, so a
+// corrupt stream still ends (overflow or a negative count).
 template <class L>
 struct InfBits {
-  const uint8_t* p;
-  const uint8_t* end;
+  const uint8_t* in;
+  uint32_t at, n;
   uint64_t buf;
   int cnt;
-  bool over;  // a read past the input
   __host__ __device__ __forceinline__ void refill() {
-    if (end - p >= 8) {
+    if (n - at >= 8) {
       // 7 or 8 whole bytes: the buffer ends up holding 56..63 bits
-      buf |= L::load64(p) << cnt;  // uniform (L::load64 says so)
-      p += (63 - cnt) >> 3;
+      buf |= L::load64(in + at) << cnt;  // uniform (L::load64 says so)
+      at += (uint32_t)(63 - cnt) >> 3;
       cnt |= 56;
       return;
     }
-    while (cnt <= 56) {
-      if (p < end) {
-        buf |= (uint64_t)L::uni(*p++) << cnt;
-      } else {
-        if (cnt == 0) over = true;  // only zeros left: a further read is corrupt
-        return;
-      }
+    if (cnt < 0) return;
+    while (cnt <= 56 && at < n) {
+      buf |= (uint64_t)L::uni(in[at++]) << cnt;
       cnt += 8;
     }
   }
-  __host__ __device__ __forceinline__ uint32_t peek(int n) {
-    if (cnt < n) refill();
-    return (uint32_t)(buf & ((1ull << n) - 1));
+  __host__ __device__ __forceinline__ uint32_t peek(int k) {
+    if (cnt < k) refill();
+    return (uint32_t)(buf & ((1ull << k) - 1));
   }
-  __host__ __device__ __forceinline__ void drop(int n) {
-    if (n > cnt) {
-      over = true;
-      n = cnt;
-    }
-    buf >>= n;
-    cnt -= n;
+  __host__ __device__ __forceinline__ void drop(int k) {
+    buf >>= k;
+    cnt -= k;
   }
-  __host__ __device__ __forceinline__ uint32_t get(int n) {
-    if (n == 0) return 0;
-    const uint32_t v = peek(n);
-    drop(n);
+  __host__ __device__ __forceinline__ uint32_t get(int k) {
+    if (k == 0) return 0;
+    const uint32_t v = peek(k);
+    drop(k);
     return v;
   }
+  __host__ __device__ __forceinline__ bool over() const { return cnt < 0; }
 };
 
 // Canonical Huffman table from code lengths (len[0..n)); false when the
@@ -157,15 +154,15 @@ __host__ __device__ inline bool inf_build(InfHuff& h, const uint8_t* len, int n)
   return true;
 }
 
-// One symbol; -1 on an invalid code.
+// One symbol; kInfBadSym (above every valid literal/length and distance
+// symbol, so the callers' range checks catch it) on an invalid code.
+constexpr int kInfBadSym = 0x7FFF;
+
+// Codes longer than the fast table, bit by bit (rare: kept rolled).
 template <class L>
-__host__ __device__ __forceinline__ int inf_decode(InfBits<L>& b, const InfHuff& h) {
-  const uint32_t e = L::uni(h.fast[b.peek(kInfFastBits)]);
-  if (e) {
-    b.drop((int)(e >> 9));
-    return (int)(e & 511u);
-  }
+__host__ __device__ inline int inf_decode_slow(InfBits<L>& b, const InfHuff& h) {
   int code = 0, first = 0, index = 0;
+#pragma unroll 1
   for (int l = 1; l < 16; ++l) {
     code |= (int)b.get(1);
     const int count = L::uni(h.count[l]);
@@ -175,7 +172,17 @@ __host__ __device__ __forceinline__ int inf_decode(InfBits<L>& b, const InfHuff&
     first <<= 1;
     code <<= 1;
   }
-  return -1;
+  return kInfBadSym;
+}
+
+template <class L>
+__host__ __device__ __forceinline__ int inf_decode(InfBits<L>& b, const InfHuff& h) {
+  const uint32_t e = L::uni(h.fast[b.peek(kInfFastBits)]);
+  if (e) {
+    b.drop((int)(e >> 9));
+    return (int)(e & 511u);
+  }
+  return inf_decode_slow(b, h);
 }
 
 __host__ __device__ __forceinline__ void inf_len_base(int i, int& base, int& extra) {
@@ -188,22 +195,90 @@ __host__ __device__ __forceinline__ void inf_dist_base(int i, int& base, int& ex
   else extra = (i - 2) >> 1, base = ((2 + (i & 1)) << extra) + 1;
 }
 
+// The literal/length and distance codes of one block up to its end-of-block
+// symbol.  One refill per symbol: a refill leaves 56+ bits unless the input is
+// nearly used up, and a literal/length code (15), its extra bits (5), a
+// distance code (15) and its extra bits (13) take at most 48.
+template <class L>
+__host__ __device__ __forceinline__ int inf_codes(InfBits<L>& b, const InfTables& t, uint8_t* out, uint32_t cap,
+                                                  uint32_t& pos) {
+  for (;;) {
+    if (b.cnt < 48) b.refill();
+    int sym;
+    {
+      const uint32_t e = L::uni(t.lit.fast[(uint32_t)b.buf & ((1u << kInfFastBits) - 1)]);
+      if (e) {
+        b.drop((int)(e >> 9));
+        sym = (int)(e & 511u);
+      } else {
+        sym = inf_decode_slow(b, t.lit);
+      }
+    }
+    if (sym < 256) {
+      if (pos >= cap) return kInfOverflow;
+      L::put(out, pos++, (uint8_t)sym);
+      continue;
+    }
+    if (sym == 256) return b.over() ? kInfCorrupt : kInfOk;
+    if (sym > 285) return kInfCorrupt;
+    int lbase, lextra, dbase, dextra;
+    inf_len_base(sym - 257, lbase, lextra);
+    const int len = lbase + (int)((uint32_t)b.buf & ((1u << lextra) - 1));
+    b.drop(lextra);
+    int dsym;
+    {
+      const uint32_t e = L::uni(t.dist.fast[(uint32_t)b.buf & ((1u << kInfFastBits) - 1)]);
+      if (e) {
+        b.drop((int)(e >> 9));
+        dsym = (int)(e & 511u);
+      } else {
+        dsym = inf_decode_slow(b, t.dist);
+      }
+    }
+    if (dsym > 29) return kInfCorrupt;
+    inf_dist_base(dsym, dbase, dextra);
+    const uint32_t dist = (uint32_t)dbase + ((uint32_t)b.buf & ((1u << dextra) - 1));
+    b.drop(dextra);
+    if (dist > pos) return kInfCorrupt;
+    if ((uint32_t)len > cap - pos) return kInfOverflow;
+    // the match repeats the last `dist` bytes: byte k of it is source byte
+    // k mod dist (overlapping copies, as DEFLATE means)
+    L::sync();
+    const uint32_t src = pos - dist;
+    const int d = (int)dist;
+    for (int k = L::id(); k < len; k += L::n()) L::copy(out, pos + k, src + (k < d ? k : k % d));
+    L::sync();
+    pos += (uint32_t)len;
+  }
+}
+
 // Raw DEFLATE in[0, n) -> out[0, cap); *produced = bytes written.
 template <class L>
-__host__ __device__ inline int inflate_raw(const uint8_t* in, size_t n, uint8_t* out, size_t cap, size_t* produced,
-                                           InfTables& t) {
-  InfBits<L> b{in, in + n, 0, 0, false};
-  size_t pos = 0;
+__host__ __device__ inline int inflate_raw(const uint8_t* in, uint32_t n, uint8_t* out, uint32_t cap,
+                                           uint32_t* produced, InfTables& t) {
+  InfBits<L> b{in, 0, n, 0, 0};
+  uint32_t pos = 0;
   int rc = kInfOk;
   for (;;) {
     const uint32_t bfinal = b.get(1), btype = b.get(2);
     if (btype == 0) {  // stored: to a byte boundary, LEN, NLEN, LEN raw bytes
+      if (b.over()) { rc = kInfCorrupt; break; }
       b.drop(b.cnt & 7);
       const uint32_t len = b.get(16), nlen = b.get(16);
-      if ((len ^ 0xFFFFu) != nlen) { rc = kInfCorrupt; break; }
+      if ((len ^ 0xFFFFu) != nlen || b.over()) { rc = kInfCorrupt; break; }
       if (len > cap - pos) { rc = kInfOverflow; break; }
-      for (uint32_t k = 0; k < len; ++k) L::put(out, pos++, (uint8_t)b.get(8));
+      // whole bytes still in the bit buffer, then the rest straight from the
+      // input, split over the lanes
+      uint32_t k = 0;
+      for (; k < len && b.cnt >= 8; ++k) L::put(out, pos + k, (uint8_t)b.get(8));
+      const uint32_t rest = len - k;
+      if (rest > b.n - b.at) { rc = kInfCorrupt; break; }
       L::sync();
+      for (uint32_t j = (uint32_t)L::id(); j < rest; j += (uint32_t)L::n()) out[pos + k + j] = b.in[b.at + j];
+      L::sync();
+      b.at += rest;
+      if (rest) b.buf = 0, b.cnt = 0;
+      pos += len;
     } else if (btype == 1 || btype == 2) {
       uint8_t* const lens = t.lens;
       int nlit = 288, ndist = 30;
@@ -230,7 +305,7 @@ __host__ __device__ inline int inflate_raw(const uint8_t* in, size_t n, uint8_t*
         int s = 0;
         while (s < nlit + ndist) {
           const int sym = inf_decode(b, t.dist);
-          if (sym < 0) { rc = kInfCorrupt; break; }
+          if (sym > 18) { rc = kInfCorrupt; break; }
           if (sym < 16) {
             if (L::id() == 0) lens[s] = (uint8_t)sym;
             ++s;
@@ -269,40 +344,12 @@ __host__ __device__ inline int inflate_raw(const uint8_t* in, size_t n, uint8_t*
         L::sync();
       }
       if (!inf_build<L>(t.lit, lens, 288) || !inf_build<L>(t.dist, lens + 288, 30)) { rc = kInfCorrupt; break; }
-      for (;;) {
-        const int sym = inf_decode(b, t.lit);
-        if (sym < 0 || b.over) { rc = kInfCorrupt; break; }
-        if (sym < 256) {
-          if (pos >= cap) { rc = kInfOverflow; break; }
-          L::put(out, pos++, (uint8_t)sym);
-          continue;
-        }
-        if (sym == 256) break;
-        if (sym > 285) { rc = kInfCorrupt; break; }
-        int lbase, lextra, dbase, dextra;
-        inf_len_base(sym - 257, lbase, lextra);
-        const int len = lbase + (int)b.get(lextra);
-        const int dsym = inf_decode(b, t.dist);
-        if (dsym < 0 || dsym > 29) { rc = kInfCorrupt; break; }
-        inf_dist_base(dsym, dbase, dextra);
-        const size_t dist = (size_t)dbase + b.get(dextra);
-        if (dist > pos) { rc = kInfCorrupt; break; }
-        if ((size_t)len > cap - pos) { rc = kInfOverflow; break; }
-        // the match repeats the last `dist` bytes: byte k of it is source
-        // byte k mod dist (overlapping copies, as DEFLATE means)
-        L::sync();
-        const size_t src = pos - dist;
-        const int d = (int)dist;
-        for (int k = L::id(); k < len; k += L::n()) L::copy(out, pos + k, src + (k < d ? k : k % d));
-        L::sync();
-        pos += (size_t)len;
-      }
-      if (rc != kInfOk) break;
+      if ((rc = inf_codes<L>(b, t, out, cap, pos)) != kInfOk) break;
     } else {
       rc = kInfCorrupt;
       break;
     }
-    if (b.over) { rc = kInfCorrupt; break; }
+    if (b.over()) { rc = kInfCorrupt; break; }
     if (bfinal) break;
   }
   L::sync();

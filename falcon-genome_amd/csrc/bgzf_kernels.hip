@@ -49,10 +49,10 @@ struct WaveLanes {
     const uint64_t v = (lo >> sh) | ((hi << 1) << (63 - sh));
     return (uint64_t)rfl((uint32_t)v) | (uint64_t)rfl((uint32_t)(v >> 32)) << 32;
   }
-  __device__ static void put(uint8_t* out, size_t pos, uint8_t v) {
-    if (threadIdx.x == 0) out[pos] = v;
-  }
-  __device__ static void copy(uint8_t* out, size_t to, size_t from) {
+  // every lane stores the same byte to the same address: one write, and no
+  // exec-mask switch around it
+  __device__ static void put(uint8_t* out, uint32_t pos, uint8_t v) { out[pos] = v; }
+  __device__ static void copy(uint8_t* out, uint32_t to, uint32_t from) {
     out[to] = __hip_atomic_load(out + from, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
   // one wave: its memory operations are performed in order, so the lanes only
@@ -91,8 +91,8 @@ __global__ __launch_bounds__(64) void bgzf_inflate_kernel(const uint8_t* __restr
   }
   uint8_t* dst = out + u0;
   __syncthreads();
-  size_t got = 0;
-  int rc = inflate_raw<WaveLanes>(mem + 12 + xlen, (size_t)plen, dst, (size_t)ulen, &got, S.t);
+  uint32_t got = 0;
+  int rc = inflate_raw<WaveLanes>(mem + 12 + xlen, (uint32_t)plen, dst, (uint32_t)ulen, &got, S.t);
   const uint32_t want_crc = le32(mem + clen - 8), isize = le32(mem + clen - 4);
   if (rc == kInfOk && ((int64_t)got != ulen || (int64_t)isize != ulen)) rc = kInfCorrupt;
   // CRC-32 of the output: contiguous lane chunks read back past the L1, each

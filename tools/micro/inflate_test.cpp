@@ -25,13 +25,13 @@ struct HostLanes {
   static constexpr int n() { return 1; }
   template <class T>
   static T uni(T v) { return v; }
-  static void copy(uint8_t* out, size_t to, size_t from) { out[to] = out[from]; }
+  static void copy(uint8_t* out, uint32_t to, uint32_t from) { out[to] = out[from]; }
   static uint64_t load64(const uint8_t* p) {
     uint64_t v;
     std::memcpy(&v, p, 8);
     return v;
   }
-  static void put(uint8_t* out, size_t pos, uint8_t v) { out[pos] = v; }
+  static void put(uint8_t* out, uint32_t pos, uint8_t v) { out[pos] = v; }
   static void sync() {}
 };
 
@@ -75,10 +75,10 @@ int main(int argc, char** argv) {
     const int level = (int)(rng() % 10), strategy = strategies[rng() % 5];
     const std::vector<uint8_t> c = deflate_raw(d, level, strategy);
     std::vector<uint8_t> o(n + 16, 0xAA);
-    size_t got = 0;
-    const int rc = inflate_raw<HostLanes>(c.data(), c.size(), o.data(), n, &got, *t);
+    uint32_t got = 0;
+    const int rc = inflate_raw<HostLanes>(c.data(), (uint32_t)c.size(), o.data(), (uint32_t)n, &got, *t);
     if (rc != kInfOk || got != n || (n && std::memcmp(o.data(), d.data(), n) != 0)) {
-      if (++bad < 5) std::printf("FAIL it %d n %zu level %d strategy %d rc %d got %zu\n", it, n, level, strategy, rc, got);
+      if (++bad < 5) std::printf("FAIL it %d n %zu level %d strategy %d rc %d got %u\n", it, n, level, strategy, rc, got);
     }
     // the CRC split over 64 chunks and recombined, as the device does
     const uint32_t want = (uint32_t)crc32(0, d.data(), (uInt)n);
@@ -93,11 +93,11 @@ int main(int argc, char** argv) {
     if (!c.empty()) {  // a flipped bit: any status, in bounds
       std::vector<uint8_t> cc = c;
       cc[rng() % cc.size()] ^= (uint8_t)(1u << (rng() % 8));
-      inflate_raw<HostLanes>(cc.data(), cc.size(), o.data(), n, &got, *t);
+      inflate_raw<HostLanes>(cc.data(), (uint32_t)cc.size(), o.data(), (uint32_t)n, &got, *t);
     }
-    if (c.size() > 2) inflate_raw<HostLanes>(c.data(), c.size() / 2, o.data(), n, &got, *t);
+    if (c.size() > 2) inflate_raw<HostLanes>(c.data(), (uint32_t)c.size() / 2, o.data(), (uint32_t)n, &got, *t);
     if (n > 1) {  // too small an output
-      const int r2 = inflate_raw<HostLanes>(c.data(), c.size(), o.data(), n - 1, &got, *t);
+      const int r2 = inflate_raw<HostLanes>(c.data(), (uint32_t)c.size(), o.data(), (uint32_t)n - 1, &got, *t);
       if (r2 != kInfOverflow && ++bad < 5) std::printf("FAIL it %d: short output gave %d\n", it, r2);
     }
   }
