@@ -26,6 +26,8 @@ def main():
     ap.add_argument("--members", type=int, default=4096)
     ap.add_argument("--reps", type=int, default=5)
     ap.add_argument("--kind", default="bam")
+    ap.add_argument("--stress", type=int, default=0,
+                    help="extra launches, each checked: every status OK and the output equal to the first launch's")
     a = ap.parse_args()
     import torch
     rng = np.random.default_rng(1)
@@ -56,6 +58,18 @@ def main():
     o = out.cpu().numpy()
     for k in range(min(n, 64)):
         assert o[uoff[k]:uoff[k + 1]].tobytes() == members[k][1]
+    if a.stress:
+        first = out.clone()
+        bad = 0
+        for r in range(a.stress):
+            out.fill_(0x5A)
+            st.fill_(-1)
+            run()
+            torch.cuda.synchronize()
+            ok = bool((st == 0).all().item()) and bool(torch.equal(out, first))
+            bad += not ok
+        print(json.dumps({"stress_launches": a.stress, "bad_launches": bad}), flush=True)
+        assert bad == 0
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     e0.record(s)
     for _ in range(a.reps):
