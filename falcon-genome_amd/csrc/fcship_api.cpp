@@ -360,7 +360,23 @@ int check_params(const fcs_bsw_params* p) {
 // The onesweep kernels' default tile (1024 threads x ~16 items) gives a 1M-key
 // sort 62 workgroups on a 256-CU chip; 256 x 8 tiles give it ~490 but measured
 // slower (C2 2.86 vs 2.93 TCUPS, C3 1.95 vs 2.05, profiles/r2/abt_*).
+#ifndef FCS_SORT_BITS
+#define FCS_SORT_BITS 0  // 0: rocPRIM's default onesweep config for the target
+#endif
+#ifndef FCS_SORT_BLOCK
+#define FCS_SORT_BLOCK 1024
+#endif
+#ifndef FCS_SORT_ITEMS
+#define FCS_SORT_ITEMS 8
+#endif
+#if FCS_SORT_BITS
+using OnesweepConfig = rocprim::radix_sort_onesweep_config<rocprim::kernel_config<256, 12>,
+                                                           rocprim::kernel_config<FCS_SORT_BLOCK, FCS_SORT_ITEMS>,
+                                                           FCS_SORT_BITS, rocprim::block_radix_rank_algorithm::match>;
+using SortConfig = rocprim::radix_sort_config<rocprim::default_config, rocprim::default_config, OnesweepConfig, 0>;
+#else
 using SortConfig = rocprim::radix_sort_config<rocprim::default_config, rocprim::default_config, rocprim::default_config, 0>;
+#endif
 hipError_t sort_pairs_u32(void* tmp, size_t& bytes, const uint32_t* kin, uint32_t* kout, const int32_t* vin,
                           int32_t* vout, int n, hipStream_t s, int end_bit) {
   return rocprim::radix_sort_pairs<SortConfig>(tmp, bytes, kin, kout, vin, vout, (size_t)n, 0, (unsigned)end_bit, s);
