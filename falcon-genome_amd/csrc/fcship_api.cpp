@@ -1746,6 +1746,42 @@ int fcs_bgzf_inflate(const uint8_t* comp, int64_t comp_bytes, uint8_t* out, int6
   return FCS_OK;
 }
 
-int fcs_abi_symbol_count(void) { return 44; }
+int fcs_device_release(int32_t device) {
+  int rc = check_device(device);
+  if (rc) return rc;
+  for (int kind : {kComputeSession, kInflateSession}) {
+    SessionPool& P = session_pool(device, kind);
+    std::lock_guard<std::mutex> lk(P.mu);
+    if (P.creating || P.idle.size() != P.all.size())
+      return fail(FCS_ERR_INVALID, "[E::fcs_device_release] a call on this device is still running");
+  }
+  // the handles die with the reset below: the pools, fork sets and tables are
+  // dropped (not destroyed one by one) and made again on the next call
+  for (int kind : {kComputeSession, kInflateSession}) {
+    SessionPool& P = session_pool(device, kind);
+    std::lock_guard<std::mutex> lk(P.mu);
+    P.all.clear();
+    P.idle.clear();
+  }
+  {
+    std::lock_guard<std::mutex> lk(g_fork_mu);
+    for (auto it = g_fork_sets->begin(); it != g_fork_sets->end();)
+      it = it->first.first == device ? g_fork_sets->erase(it) : std::next(it);
+  }
+  {
+    std::lock_guard<std::mutex> lk(g_dev_mu);
+    auto it = g_tables.find(device);
+    if (it != g_tables.end()) {
+      (void)it->second.release();
+      g_tables.erase(it);
+    }
+  }
+  FCS_SET_DEVICE((device));
+  FCS_HIP_CHECK(hipDeviceSynchronize());
+  FCS_HIP_CHECK(hipDeviceReset());
+  return FCS_OK;
+}
+
+int fcs_abi_symbol_count(void) { return 45; }
 
 }  // extern "C"

@@ -145,6 +145,7 @@ _sig("fcs_phmm_last_rescued", C.c_int, [i64p])
 _sig("fcs_phmm_last_device_ms", C.c_int, [C.POINTER(C.c_double), C.POINTER(C.c_double)])
 _sig("fcs_device_warmup", C.c_int, [C.c_int32, C.c_int32])
 _sig("fcs_stream_release", C.c_int, [C.c_int32, C.c_void_p])
+_sig("fcs_device_release", C.c_int, [C.c_int32])
 _sig("fcs_phmm_partition", C.c_int, [C.POINTER(PhmmBatch), C.c_int32, C.c_void_p])
 _sig("fcs_phmm_compute_pairs_multi", C.c_int, [C.POINTER(PhmmBatch), C.c_void_p, C.POINTER(PhmmOpts), C.c_void_p,
                                                C.c_int32])

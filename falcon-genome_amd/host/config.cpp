@@ -48,6 +48,8 @@ void Config::init(const std::string& root_dir) {
   declare("gpu.phmm.batch_regions", "4096", "active regions per PairHMM device pass");
   declare("gpu.phmm.combine_ms", "0", "ms a shard's PairHMM pass waits to merge with other shards' (0: no merging)");
   declare("gpu.phmm.rescue", "true", "fp64 rescue of pairs whose fp32 likelihood underflows (GKL)");
+  declare("gpu.release_early", "true",
+          "release the GPUs beside the VCF tail once the callers are done (their teardown off the critical path)");
   declare("gpu.bam_inflate", "false",
           "inflate a calling window's BAM blocks on the GPU (fcs_bgzf_inflate) instead of host libdeflate");
   // caller knobs (GATK HaplotypeCaller / Mutect2 argument defaults)

@@ -238,6 +238,7 @@ int htc_main(int argc, char** argv) {
   } else {
     ex.addTask(std::make_shared<VCFConcatWorker>(parts, plain), sample_id, true);
   }
+  if (conf().get_bool("gpu.release_early")) ex.addTask(std::make_shared<GpuReleaseWorker>(gpus, &warm), sample_id);
   timeline("stages queued");
   ex.run();
   timeline("stages done");
@@ -289,6 +290,7 @@ int mutect2_main(int argc, char** argv) {
                sample_id);
   }
   ex.addTask(std::make_shared<VCFConcatWorker>(parts, output, output + ".gz", /*consume=*/true), sample_id, true);
+  if (conf().get_bool("gpu.release_early")) ex.addTask(std::make_shared<GpuReleaseWorker>(gpus, &warm), sample_id);
   ex.run();
   warm.wait();
   if (warm.status() != 0) throw failedCommand(std::string("[E::fcs-genome] GPU warm-up failed: ") + fcs_last_error());

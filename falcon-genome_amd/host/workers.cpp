@@ -1,5 +1,7 @@
 #include "workers.h"
 
+#include <algorithm>
+#include <cstdio>
 #include <iostream>
 #include <map>
 #include <mutex>
@@ -291,6 +293,20 @@ int DeviceWarmupWorker::run(TaskContext&) {
   // device, while the shards decode their first reads
   for (int d : gpus_)
     if (fcs_device_warmup(d, 0) != FCS_OK) return 1;
+  return 0;
+}
+
+GpuReleaseWorker::GpuReleaseWorker(std::vector<int> gpus, BackgroundExecutor* warm)
+    : Worker(1, 1, {}, "GPU release"), gpus_(std::move(gpus)), warm_(warm) {
+  std::sort(gpus_.begin(), gpus_.end());
+  gpus_.erase(std::unique(gpus_.begin(), gpus_.end()), gpus_.end());
+}
+
+int GpuReleaseWorker::run(TaskContext&) {
+  if (warm_) warm_->wait();
+  // a failure only means the teardown happens at exit as before
+  for (int d : gpus_)
+    if (d >= 0 && fcs_device_release(d) != FCS_OK) std::fprintf(stderr, "[W::fcs-genome] %s\n", fcs_last_error());
   return 0;
 }
 

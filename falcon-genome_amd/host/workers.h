@@ -145,6 +145,20 @@ class DeviceWarmupWorker : public Worker {
   std::vector<int> gpus_;
 };
 
+// Releases the devices the job's callers used (fcs_device_release) once the
+// caller stage is done, beside the VCF tail, so the GPU context's teardown
+// does not follow the last output (gpu.release_early).  Waits for the warm-up
+// first: nothing else uses the devices by then.
+class GpuReleaseWorker : public Worker {
+ public:
+  GpuReleaseWorker(std::vector<int> gpus, BackgroundExecutor* warm);
+  int run(TaskContext& ctx) override;
+
+ private:
+  std::vector<int> gpus_;
+  BackgroundExecutor* warm_;
+};
+
 // Applies the caller's config keys (htc.*, mutect2.*, gpu.*) to options.
 CallerOptions caller_options_from_config(int gpu);
 

@@ -79,6 +79,14 @@ int fcs_device_warmup(int32_t device, int32_t sessions);
  * stream's work has finished and before destroying the stream; a later *_dev
  * call on the same stream recreates them. */
 int fcs_stream_release(int32_t device, void* stream);
+/* Releases everything the library holds on `device` (session streams, pinned
+ * and device arenas, plans, tables) and resets the device, so the process's
+ * GPU teardown happens now instead of after its last output: `fcs-genome`
+ * calls it beside the VCF tail.  FCS_ERR_INVALID while a call on the device
+ * is still running.  A later call on the device sets everything up again.
+ * The reset frees every allocation of the process on the device, other
+ * libraries' included: call it only when nothing else holds device memory. */
+int fcs_device_release(int32_t device);
 
 /* ----------------------------------------------------------------- PairHMM */
 /* One read: bases + the four per-base quality arrays GATK hands to the PairHMM

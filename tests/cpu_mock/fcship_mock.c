@@ -72,6 +72,10 @@ static __thread const char* g_err = "";
 const char* fcs_last_error(void) { return g_err; }
 const char* fcs_version(void) { return "cpu-mock"; }
 int fcs_device_count(void) { return 1; }
+int fcs_device_release(int32_t device) {
+  (void)device;
+  return FCS_OK;
+}
 int fcs_device_warmup(int32_t device, int32_t sessions) {
   (void)device;
   (void)sessions;

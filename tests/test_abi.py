@@ -5,6 +5,7 @@ seeded workload generators are deterministic and match SURVEY.md §8(d)."""
 import ctypes as C
 import os
 import subprocess
+import sys
 
 import numpy as np
 import pytest
@@ -128,3 +129,30 @@ def test_dense_compute_validates_reads():
         fcship.lib.fcs_phmm_compute(None, 1, None, 1, None, None) and None
         fcship.check(fcship.lib.fcs_phmm_compute(None, 1, None, 1, None, None))
     assert e.value.code == fcship.FCS_ERR_INVALID
+
+
+@pytest.mark.gpu
+def test_device_release_then_reuse(gpu, tmp_path):
+    """fcs_device_release resets the device; the next calls set everything up
+    again and give the same results.  In a child process: the reset frees every
+    allocation of the process (torch's included)."""
+    script = tmp_path / "rel.py"
+    script.write_text(f"""
+import sys
+sys.path[:0] = [{os.path.join(ROOT, 'falcon-genome_amd')!r}, {os.path.join(ROOT, 'tests')!r}]
+import numpy as np
+import fcship
+import bgzf_cases
+p = fcship.synth_phmm(7, 2000)
+a = fcship.phmm_compute_pairs(p)
+blob = b"".join(m for _, m, _ in bgzf_cases.suite(seed=3, count=20))
+x, _ = fcship.bgzf_inflate(blob)
+fcship.check(fcship.lib.fcs_device_release(0))
+fcship.check(fcship.lib.fcs_device_release(0))  # twice: nothing left to drop
+b = fcship.phmm_compute_pairs(p)
+y, _ = fcship.bgzf_inflate(blob)
+assert np.array_equal(a, b) and x == y
+print("release ok")
+""")
+    r = subprocess.run([sys.executable, str(script)], capture_output=True, text=True, timeout=110)
+    assert r.returncode == 0 and "release ok" in r.stdout, r.stdout[-2000:] + r.stderr[-2000:]
