@@ -19,7 +19,8 @@
 // bytes, little-endian, from p with p + 8 <= end and 8 more readable),
 // `L::put(out, pos, byte)` (one lane writes a literal), `L::copy(out, to,
 // from)` (a lane copies one byte written earlier: back-references), `L::uni(v)` (a value every
-// lane holds alike: the device keeps the decode state in scalar registers)
+// lane holds alike: the device keeps the decode state in scalar registers),
+// `L::lane(v, l)` (lane l's value of v; device only)
 // and `L::sync()` (the lanes' writes visible to each other).  Every lane
 // decodes the same symbols; the lanes split the table fills and the match
 // copies.
@@ -95,12 +96,21 @@ struct InfBits {
 // are built by every lane alike; the fast table's entries are split.
 template <class L>
 __host__ __device__ inline bool inf_build(InfHuff& h, const uint8_t* len, int n) {
+  // per-length code counts: on the device lane l holds the count of length l
+  // in one register (read back with L::lane), on the host an array
+  uint32_t mine = 0, cnt_host[16];
+  if constexpr (L::n() > 1) {
+#pragma unroll 1
+    for (int s = 0; s < n; ++s) mine += (uint32_t)(L::uni(len[s]) == L::id());
+  } else {
+    for (int l = 0; l < 16; ++l) cnt_host[l] = 0;
+    for (int s = 0; s < n; ++s) cnt_host[len[s]]++;
+  }
   uint32_t cnt[16];
-  for (int l = 0; l < 16; ++l) cnt[l] = 0;
-  for (int s = 0; s < n; ++s) {
-    const int l = L::uni(len[s]);
 #pragma unroll
-    for (int k = 1; k < 16; ++k) cnt[k] += l == k;  // register counts, no indexed array
+  for (int l = 0; l < 16; ++l) {
+    if constexpr (L::n() > 1) cnt[l] = l ? L::lane(mine, l) : 0;
+    else cnt[l] = l ? cnt_host[l] : 0;
   }
   int left = 1;
 #pragma unroll
@@ -112,13 +122,14 @@ __host__ __device__ inline bool inf_build(InfHuff& h, const uint8_t* len, int n)
   uint32_t o = 0, my_off = 0;
 #pragma unroll
   for (int l = 0; l < 16; ++l) {
-    if (L::id() == 0) h.count[l] = (uint16_t)(l ? cnt[l] : 0);
+    if (L::id() == 0) h.count[l] = (uint16_t)cnt[l];
     if (l == L::id()) my_off = o;  // the device lane of length l
-    if (l) o += cnt[l];
+    o += cnt[l];
   }
   // symbols in (length, symbol) order: on the device lane l (1..15) places
   // the length-l ones; the host's single lane all of them
   if constexpr (L::n() > 1) {
+#pragma unroll 1  // unrolled, the symbol numbers became 29 hoisted VGPR constants
     for (int s = 0; s < n; ++s) {
       const int l = L::uni(len[s]);
       if (l && l == L::id()) h.sorted[my_off++] = (uint16_t)s;
@@ -330,16 +341,19 @@ __host__ __device__ inline int inflate_raw(const uint8_t* in, uint32_t n, uint8_
         L::sync();
         if (L::uni(lens[256]) == 0) { rc = kInfCorrupt; break; }  // no end-of-block code
         // the distance lengths follow the literal / length ones: moved up to
-        // 288 (through registers: the ranges overlap when nlit + ndist > 288),
-        // the unused entries of both codes zeroed
-        uint8_t dl[30];
-#pragma unroll
-        for (int k = 0; k < 30; ++k) dl[k] = k < ndist ? L::uni(lens[nlit + k]) : 0;
-        L::sync();
-        if (L::id() == 0) {
-#pragma unroll
-          for (int k = 0; k < 30; ++k) lens[288 + k] = dl[k];
+        // 288 (the ranges overlap when nlit + ndist > 288: the device reads
+        // them into lane registers first, the host copies backwards), the
+        // unused entries of both codes zeroed
+        if constexpr (L::n() > 1) {
+          const int k = L::id();
+          const uint8_t v = k < ndist ? lens[nlit + k] : 0;
+          L::sync();
+          if (k < 30) lens[288 + k] = v;
+        } else {
+          for (int k = ndist - 1; k >= 0; --k) lens[288 + k] = lens[nlit + k];
+          for (int k = ndist; k < 30; ++k) lens[288 + k] = 0;
         }
+        L::sync();
         for (int k = nlit + L::id(); k < 288; k += L::n()) lens[k] = 0;
         L::sync();
       }

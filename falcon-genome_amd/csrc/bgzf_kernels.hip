@@ -9,8 +9,8 @@
 // - the decode state is wave-uniform and kept in scalar registers (every
 //   value the chain reads goes through readfirstlane), so the symbol step is
 //   SALU work plus one LDS table read, with scalar branches;
-// - a member holds only its Huffman tables and the CRC table in LDS
-//   (≈ 6.6 KiB): the compressed payload is read from global memory 8 bytes
+// - a member holds only its Huffman tables in LDS (5.6 KiB, 54 VGPRs: 7
+//   members per SIMD): the compressed payload is read from global memory 8 bytes
 //   at a time, the output is written straight to its place in global memory
 //   and back-references read it back past the vector L1 (agent-scope loads:
 //   the bytes were written by this wave moments before);
@@ -39,6 +39,7 @@ struct WaveLanes {
   __device__ static T uni(T v) {
     return (T)rfl((uint32_t)v);
   }
+  __device__ static uint32_t lane(uint32_t v, int l) { return (uint32_t)__builtin_amdgcn_readlane((int)v, l); }
   // 8 bytes at p (global, any alignment; 8 more bytes readable): two aligned
   // 8-byte reads and a funnel shift, all uniform
   __device__ static uint64_t load64(const uint8_t* p) {
@@ -66,7 +67,6 @@ struct WaveLanes {
 
 struct MemberLds {
   InfTables t;
-  uint32_t crc[256];
 };
 
 __device__ __forceinline__ uint32_t le32(const uint8_t* p) {
@@ -80,7 +80,6 @@ __global__ __launch_bounds__(64) void bgzf_inflate_kernel(const uint8_t* __restr
   __shared__ MemberLds S;
   const int m = (int)blockIdx.x, lane = (int)threadIdx.x;
   if (m >= n) return;
-  for (int i = lane; i < 256; i += 64) S.crc[i] = crc32_entry((uint32_t)i);
   const int64_t c0 = coff[m], clen = coff[m + 1] - c0, u0 = uoff[m], ulen = uoff[m + 1] - u0;
   const uint8_t* mem = comp + c0;
   const int xlen = (int)rfl((uint32_t)mem[10] | (uint32_t)mem[11] << 8);
@@ -99,10 +98,13 @@ __global__ __launch_bounds__(64) void bgzf_inflate_kernel(const uint8_t* __restr
   // shifted past the bytes after it
   const int ng = (int)got, chunk = (ng + 63) / 64;
   const int b = min(ng, lane * chunk), e = min(ng, b + chunk);
+  // bitwise (no table: its 1 KiB of LDS would cost members in flight, and this
+  // pass is ≈ 2% of a member's time)
   uint32_t c = 0xFFFFFFFFu;
   for (int q = b; q < e; ++q) {
-    const uint32_t v = __hip_atomic_load(dst + q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    c = S.crc[(c ^ v) & 255u] ^ (c >> 8);
+    c ^= __hip_atomic_load(dst + q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) c = (c >> 1) ^ (kCrcPoly & (0u - (c & 1u)));
   }
   uint32_t part = e > b ? crc_shift(~c, (uint64_t)(ng - e)) : 0u;
   for (int off = 32; off > 0; off >>= 1) part ^= (uint32_t)__shfl_xor((int)part, off, 64);
