@@ -1697,52 +1697,47 @@ int fcs_bgzf_inflate(const uint8_t* comp, int64_t comp_bytes, uint8_t* out, int6
   if ((rc = lease.acquire(device, kInflateSession))) return rc;
   Session* S = lease.get();
   const size_t nn = (size_t)n;
-  // No pinned staging: a shard's range is tens of MiB, and growing a pinned
-  // arena per session (hipHostMalloc) cost up to 0.5 s per call while 16 shard
-  // threads started at once; the copies go from and to the caller's pageable
-  // buffers, the device scratch comes from the stream-ordered pool.
+  // Through the session's pinned staging arena.  Copies straight from and to
+  // the caller's pageable buffers with device scratch from the stream-ordered
+  // pool were tried: with 16 shard threads calling at once, member 0 of a
+  // call came out corrupt in about one htc run in four (r5ae, r5al, r5am),
+  // never with the pinned arena.
   Layout L;
-  const size_t oco = L.add(8 * (nn + 1)), ouo = L.add(8 * (nn + 1)), ocp = L.add((size_t)used + 16),
-               ost = L.add(4 * nn), oout = L.add((size_t)total);
+  const size_t oco = L.add(8 * (nn + 1)), ouo = L.add(8 * (nn + 1)), ocp = L.add((size_t)used + 16);
+  const size_t in_bytes = L.total, ost = L.add(4 * nn), oout = L.add((size_t)total);
   const double t_lease = ms(t0);
+  if ((rc = S->ensure_host(L.total)) || (rc = S->ensure_dev(L.total))) return rc;
+  const double t_alloc = ms(t0);
+  std::memcpy(S->h<void>(oco), coff.data(), 8 * (nn + 1));
+  std::memcpy(S->h<void>(ouo), uoff.data(), 8 * (nn + 1));
+  std::memcpy(S->h<void>(ocp), comp, (size_t)used);
+  const double t_in = ms(t0);
   hipStream_t s = S->s;
   const StreamDrain drain{s};
-  void* dv = nullptr;
-  FCS_HIP_CHECK(hipMallocAsync(&dv, L.total, s));
-  struct PoolFree {
-    void* p;
-    hipStream_t s;
-    ~PoolFree() { (void)hipFreeAsync(p, s); }
-  } pool_free{dv, s};
-  auto dptr = [&](size_t off) { return static_cast<char*>(dv) + off; };
-  const double t_alloc = ms(t0);
-  FCS_HIP_CHECK(hipMemcpyAsync(dptr(oco), coff.data(), 8 * (nn + 1), hipMemcpyHostToDevice, s));
-  FCS_HIP_CHECK(hipMemcpyAsync(dptr(ouo), uoff.data(), 8 * (nn + 1), hipMemcpyHostToDevice, s));
-  FCS_HIP_CHECK(hipMemcpyAsync(dptr(ocp), comp, (size_t)used, hipMemcpyHostToDevice, s));
-  const double t_in = ms(t0);
-  if ((rc = launch_bgzf_inflate(reinterpret_cast<const uint8_t*>(dptr(ocp)), reinterpret_cast<const int64_t*>(dptr(oco)),
-                                reinterpret_cast<const int64_t*>(dptr(ouo)), n, reinterpret_cast<uint8_t*>(dptr(oout)),
-                                reinterpret_cast<int32_t*>(dptr(ost)), s)))
+  FCS_HIP_CHECK(hipMemcpyAsync(S->dev, S->host, in_bytes, hipMemcpyHostToDevice, s));
+  if ((rc = launch_bgzf_inflate(S->d<uint8_t>(ocp), S->d<int64_t>(oco), S->d<int64_t>(ouo), n, S->d<uint8_t>(oout),
+                                S->d<int32_t>(ost), s)))
     return rc;
-  std::vector<int32_t> st(nn);
-  FCS_HIP_CHECK(hipMemcpyAsync(st.data(), dptr(ost), 4 * nn, hipMemcpyDeviceToHost, s));
-  FCS_HIP_CHECK(hipMemcpyAsync(out, dptr(oout), (size_t)total, hipMemcpyDeviceToHost, s));
+  FCS_HIP_CHECK(hipMemcpyAsync(S->h<void>(ost), S->d<void>(ost), L.total - ost, hipMemcpyDeviceToHost, s));
   // the calling shard thread sleeps until the copy lands: a spinning wait of
   // 16 shard threads costs more host time than the inflate saves
   if (!S->done) FCS_HIP_CHECK(hipEventCreateWithFlags(&S->done, hipEventBlockingSync | hipEventDisableTiming));
   FCS_HIP_CHECK(hipEventRecord(S->done, s));
   FCS_HIP_CHECK(hipEventSynchronize(S->done));
   const double t_gpu = ms(t0);
+  const int32_t* st = S->h<int32_t>(ost);
   for (size_t k = 0; k < nn; ++k)
     if (st[k] != FCS_BGZF_OK) {
       static const char* what[4] = {"ok", "corrupt DEFLATE stream", "inflates past its ISIZE", "CRC-32 mismatch"};
       return fail(FCS_ERR_INVALID, "[E::fcs_bgzf_inflate] member " + std::to_string(k) + " at byte " +
                                        std::to_string(coff[k]) + ": " + what[st[k] & 3]);
     }
+  std::memcpy(out, S->h<void>(oout), (size_t)total);
   *out_bytes = total;
   if (trace)
-    std::fprintf(stderr, "[fcs_bgzf_inflate] %d members, %lld -> %lld bytes: lease %.2f alloc %.2f in %.2f gpu+out %.2f ms\n",
-                 n, (long long)used, (long long)total, t_lease, t_alloc - t_lease, t_in - t_alloc, t_gpu - t_in);
+    std::fprintf(stderr, "[fcs_bgzf_inflate] %d members, %lld -> %lld bytes: lease %.2f alloc %.2f in %.2f gpu %.2f out %.2f ms\n",
+                 n, (long long)used, (long long)total, t_lease, t_alloc - t_lease, t_in - t_alloc, t_gpu - t_in,
+                 ms(t0) - t_gpu);
   return FCS_OK;
 }
 

@@ -294,9 +294,28 @@ BgzfReader::BgzfReader(const std::string& path) {
   std::setvbuf(f_, nullptr, _IOFBF, 1 << 20);  // about 30 blocks per read(2)
 }
 
+namespace {
+// Device mode's chunk buffers outlive a reader on its thread: a window's
+// chunk is tens of MiB, and fresh buffers for every window cost a page fault
+// per 4 KiB of it.
+struct ChunkCache {
+  std::vector<uint8_t> comp, out, block;
+};
+ChunkCache& chunk_cache() {
+  static thread_local ChunkCache c;
+  return c;
+}
+}  // namespace
+
 BgzfReader::~BgzfReader() {
   drop_ahead();  // the helper thread reads f_
   if (f_) std::fclose(f_);
+  if (device_ >= 0) {
+    ChunkCache& c = chunk_cache();
+    c.comp.swap(cur_.comp);
+    c.out.swap(cur_.out);
+    c.block.swap(block_);
+  }
 }
 
 bool BgzfReader::load_block() {
@@ -398,8 +417,20 @@ uint64_t BgzfReader::tell() const {
 }
 
 void BgzfReader::use_device(int device, size_t span) {
+  if (device_ < 0) {  // reuse this thread's buffers of an earlier reader
+    ChunkCache& c = chunk_cache();
+    cur_.comp.swap(c.comp);
+    cur_.out.swap(c.out);
+    if (block_.empty()) {  // (a block still being read stays)
+      block_.swap(c.block);
+      block_.clear();
+      pos_ = 0;
+    }
+  }
   device_ = device;
-  chunk_ = 16u << 20;
+  // later loads (past the caller's estimate) are small: they only finish the
+  // reads that start inside the range
+  chunk_ = 1u << 20;
   if (const char* e = std::getenv("FCS_BGZF_DEVICE_CHUNK"); e && std::atoll(e) > 0) chunk_ = (size_t)std::atoll(e);
   chunk_ = std::max<size_t>(chunk_, 1 << 17);  // two whole members at least
   span_ = span;
@@ -419,8 +450,7 @@ size_t BgzfReader::first_want() const {
 void BgzfReader::fetch(uint64_t at, size_t want, Chunk& c) {
   c.start = at;
   c.used = 0;
-  c.out.clear();
-  c.empty_member = false;
+  c.empty_member = false;  // (c.out keeps its size: a resize below fills only what it adds)
   if (std::ftell(f_) != (long)at && std::fseek(f_, (long)at, SEEK_SET) != 0) return;
   c.comp.resize(want);
   const size_t got = std::fread(c.comp.data(), 1, want, f_);

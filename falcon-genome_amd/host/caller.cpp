@@ -86,9 +86,10 @@ void load_reads_one(const std::string& bam, const std::string& chrom, int64_t be
     const uint64_t off = ix.seek_offset(tid, beg);
     if (opt.gpu_inflate) {
       // the window's compressed span by the BAI's linear index at its end,
-      // plus the reads that start in that last 16 kb window
+      // plus the reads that start in that last 16 kb window (at 30x about 0.4
+      // MiB compressed; 1 MiB of margin)
       const uint64_t e = ix.seek_offset(tid, end);
-      rd.use_device(opt.gpu, e > off ? (size_t)((e >> 16) - (off >> 16)) + (256 << 10) : 0);
+      rd.use_device(opt.gpu, e > off ? (size_t)((e >> 16) - (off >> 16)) + (1 << 20) : 0);
     }
     if (off) rd.seek(off);
   } else if (opt.gpu_inflate) {

@@ -9,11 +9,11 @@ MBP=${MBP:-31}
 B=$GRAFT_REPO_ROOT/falcon-genome_amd/bin/fcs-genome
 timeout 300 $B synth -o $W/d -c chr1:$((MBP * 1000000)) -x 30 --tumor --noisy-frac 0.01 --paired 350 > /dev/null || exit 1
 ls -la $W/d/sample.bam
-for i in 1 2; do
+for i in 1 2 3 4; do
   for mode in true false; do
     rm -rf $W/log
     export FCS_LOG_DIR=$W/log FCS_GPU_BAM_INFLATE=$mode
-    { time timeout 300 $B htc -f -r $W/d/ref.fasta -i $W/d/sample.bam -o $W/h_$mode.g.vcf 2> $W/htc.err; } 2> $W/htc.time || { tail $W/htc.err; exit 1; }
+    { time timeout 300 $B htc -f -r $W/d/ref.fasta -i $W/d/sample.bam -o $W/h_$mode.g.vcf 2> $W/htc.err; } 2> $W/htc.time || { tail -3 $W/htc.err; grep -rh "E::\|rror\|what" $W/log | head -10; exit 1; }
     echo "== gpu_inflate=$mode run $i: $(grep -E '^(real|user)' $W/htc.time | tr '\n' ' ')"
     grep -E "timeline" $W/htc.err | tail -2
     grep -h "htc\] shard" $W/log/*.log | awk '{for(i=1;i<=NF;i++){if($i=="(decode"||$i=="decode"){d+=$(i+1)}}} END{print "  decode thread-s", d, "shards", NR}'
