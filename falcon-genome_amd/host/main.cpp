@@ -608,6 +608,7 @@ int main(int argc, char** argv) {
 #if defined(__SANITIZE_ADDRESS__) || defined(__SANITIZE_THREAD__)
   return ret;  // sanitizer builds keep the normal exit (leak and race reports run at exit)
 #else
+  if (std::getenv("FCS_NORMAL_EXIT")) return ret;  // profilers that report from atexit handlers
   std::_Exit(ret);
 #endif
 }
