@@ -34,7 +34,7 @@ namespace fcs {
 constexpr int kInfFastBits = 10;
 
 struct InfHuff {
-  uint16_t fast[1 << kInfFastBits];  // len << 9 | sym, 0: longer code (or none)
+  uint16_t fast[1 << kInfFastBits];  // len << 9 | sym (| 0x8000 for a literal in the lit table), 0: longer code
   uint16_t count[16];                // codes per length
   uint16_t sorted[288];              // symbols ordered by (length, symbol)
 };
@@ -94,7 +94,7 @@ struct InfBits {
 // Canonical Huffman table from code lengths (len[0..n)); false when the
 // lengths over-subscribe the code space.  Counts and the sorted symbol list
 // are built by every lane alike; the fast table's entries are split.
-template <class L>
+template <class L, bool kLitFlag = false>
 __host__ __device__ inline bool inf_build(InfHuff& h, const uint8_t* len, int n) {
   // per-length code counts: on the device lane l holds the count of length l
   // in one register (read back with L::lane), on the host an array
@@ -153,7 +153,10 @@ __host__ __device__ inline bool inf_build(InfHuff& h, const uint8_t* len, int n)
       const int code = r >> (kInfFastBits - l);
       const int c = (int)cnt[l];
       if (code - first < c) {
-        e = (uint16_t)(l << 9 | h.sorted[index + code - first]);
+        const int sym = h.sorted[index + code - first];
+        // the literal/length table marks literals (bit 15): the literal-run
+        // loop's exit test is one bit and the output room
+        e = (uint16_t)(l << 9 | sym | (kLitFlag && sym < 256 ? 0x8000 : 0));
         break;
       }
       index += c;
@@ -215,11 +218,21 @@ __host__ __device__ __forceinline__ int inf_codes(InfBits<L>& b, const InfTables
                                                   uint32_t& pos) {
   for (;;) {
     if (b.cnt < 48) b.refill();
+    // literal runs in a loop of their own with one combined exit test (a
+    // literal from the fast table and room for it): its step is a table read,
+    // a shift, a store and a refill test, with no per-exit flow flags
+    uint32_t e = L::uni(t.lit.fast[(uint32_t)b.buf & ((1u << kInfFastBits) - 1)]);
+    while ((e >> 15) && pos < cap) {
+      b.drop((int)((e >> 9) & 15u));
+      L::put(out, pos++, (uint8_t)e);
+      if (b.cnt < kInfFastBits) b.refill();
+      e = L::uni(t.lit.fast[(uint32_t)b.buf & ((1u << kInfFastBits) - 1)]);
+    }
+    if (b.cnt < 48) b.refill();
     int sym;
     {
-      const uint32_t e = L::uni(t.lit.fast[(uint32_t)b.buf & ((1u << kInfFastBits) - 1)]);
       if (e) {
-        b.drop((int)(e >> 9));
+        b.drop((int)((e >> 9) & 15u));
         sym = (int)(e & 511u);
       } else {
         sym = inf_decode_slow(b, t.lit);
@@ -357,7 +370,7 @@ __host__ __device__ inline int inflate_raw(const uint8_t* in, uint32_t n, uint8_
         for (int k = nlit + L::id(); k < 288; k += L::n()) lens[k] = 0;
         L::sync();
       }
-      if (!inf_build<L>(t.lit, lens, 288) || !inf_build<L>(t.dist, lens + 288, 30)) { rc = kInfCorrupt; break; }
+      if (!inf_build<L, true>(t.lit, lens, 288) || !inf_build<L>(t.dist, lens + 288, 30)) { rc = kInfCorrupt; break; }
       if ((rc = inf_codes<L>(b, t, out, cap, pos)) != kInfOk) break;
     } else {
       rc = kInfCorrupt;
