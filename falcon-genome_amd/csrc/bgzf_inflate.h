@@ -270,7 +270,11 @@ __host__ __device__ __forceinline__ int inf_codes(InfBits<L>& b, const InfTables
     L::sync();
     const uint32_t src = pos - dist;
     const int d = (int)dist;
-    for (int k = L::id(); k < len; k += L::n()) L::copy(out, pos + k, src + (k < d ? k : k % d));
+    if (d >= len) {  // no overlap: a straight copy (the modulo below is ≈ 20 VALU ops)
+      for (int k = L::id(); k < len; k += L::n()) L::copy(out, pos + k, src + k);
+    } else {
+      for (int k = L::id(); k < len; k += L::n()) L::copy(out, pos + k, src + (uint32_t)(k % d));
+    }
     L::sync();
     pos += (uint32_t)len;
   }
