@@ -53,6 +53,11 @@ for step in "$@"; do
     globalprof)  # ksw_global2 only: per-kernel durations (scores pass, direction-row DP, traceback)
       run globalprof 300 rocprofv3 --kernel-trace --stats -d "$OUT/globalprof" -o run --output-format csv -- \
             python3 "$ROOT/tools/bsw_bench.py" --which global ;;
+    bgzfprof)  # BGZF inflate kernel: kernel trace + stats of the microbench (4,096 BAM-like members)
+      run bgzfprof 300 rocprofv3 --kernel-trace --stats -d "$OUT/bgzfprof" -o run --output-format csv -- \
+            python3 "$ROOT/tools/bgzf_bench.py" --reps 5 ;;
+    bgzfpmc)  # BGZF inflate kernel: SQ counters (tools/pmc_bgzf.sh)
+      run bgzfpmc 600 bash "$ROOT/tools/pmc_bgzf.sh" "$OUT/bgzfpmc" ;;
     e2eprobe)  # htc timeline at the bench's 31 Mbp (tools/e2e_probe.sh, htc only)
       run e2eprobe 900 env MBP=31 HTC_ONLY=1 bash "$ROOT/tools/e2e_probe.sh" ;;
     alignpmc)  # ksw_align2 only: SQ issue counters of one batch
