@@ -267,6 +267,23 @@ class SessionLease {
     pool_ = &P;
     return FCS_OK;
   }
+  // An idle session whose arenas already hold `bytes` (host and device), or
+  // false at once: no waiting, no session created, no arena grown.
+  bool try_acquire(int device, int kind, size_t bytes) {
+    release();
+    SessionPool& P = session_pool(device, kind);
+    std::lock_guard<std::mutex> lk(P.mu);
+    for (size_t i = 0; i < P.idle.size(); ++i) {
+      Session* S = P.idle[i];
+      if (S->host_cap >= bytes && S->dev_cap >= bytes) {
+        P.idle.erase(P.idle.begin() + (long)i);
+        s_ = S;
+        pool_ = &P;
+        return true;
+      }
+    }
+    return false;
+  }
   Session* operator->() const { return s_; }
   Session* get() const { return s_; }
 
@@ -1667,8 +1684,12 @@ int fcs_bgzf_inflate_dev(const uint8_t* dev_comp, const int64_t* dev_coff, const
   return launch_bgzf_inflate(dev_comp, dev_coff, dev_uoff, n, dev_out, dev_status, static_cast<hipStream_t>(stream));
 }
 
-int fcs_bgzf_inflate(const uint8_t* comp, int64_t comp_bytes, uint8_t* out, int64_t out_cap, int64_t* comp_used,
-                     int64_t* out_bytes, int32_t device) {
+namespace {
+
+// fcs_bgzf_inflate / fcs_bgzf_inflate_try: `try_only` takes an idle inflate
+// session whose arenas already fit the call, or returns FCS_BGZF_BUSY.
+int bgzf_inflate_host(const uint8_t* comp, int64_t comp_bytes, uint8_t* out, int64_t out_cap, int64_t* comp_used,
+                      int64_t* out_bytes, int32_t device, bool try_only) {
   if (!comp_used || !out_bytes || comp_bytes < 0 || (comp_bytes > 0 && !comp) || out_cap < 0 || (out_cap > 0 && !out))
     return fail(FCS_ERR_INVALID, "[E::fcs_bgzf_inflate] bad arguments");
   *comp_used = 0;
@@ -1693,18 +1714,25 @@ int fcs_bgzf_inflate(const uint8_t* comp, int64_t comp_bytes, uint8_t* out, int6
   using clk = std::chrono::steady_clock;
   const auto t0 = clk::now();
   auto ms = [&](clk::time_point a) { return std::chrono::duration<double, std::milli>(clk::now() - a).count(); };
-  SessionLease lease;
-  if ((rc = lease.acquire(device, kInflateSession))) return rc;
-  Session* S = lease.get();
   const size_t nn = (size_t)n;
+  Layout L;
+  const size_t oco = L.add(8 * (nn + 1)), ouo = L.add(8 * (nn + 1)), ocp = L.add((size_t)used + 16);
+  const size_t in_bytes = L.total, ost = L.add(4 * nn), oout = L.add((size_t)total);
+  SessionLease lease;
+  if (try_only) {
+    if (!lease.try_acquire(device, kInflateSession, L.total)) {
+      *comp_used = 0;
+      return FCS_BGZF_BUSY;
+    }
+  } else if ((rc = lease.acquire(device, kInflateSession))) {
+    return rc;
+  }
+  Session* S = lease.get();
   // Through the session's pinned staging arena.  Copies straight from and to
   // the caller's pageable buffers with device scratch from the stream-ordered
   // pool were tried: with 16 shard threads calling at once, member 0 of a
   // call came out corrupt in about one htc run in four (r5ae, r5al, r5am),
   // never with the pinned arena.
-  Layout L;
-  const size_t oco = L.add(8 * (nn + 1)), ouo = L.add(8 * (nn + 1)), ocp = L.add((size_t)used + 16);
-  const size_t in_bytes = L.total, ost = L.add(4 * nn), oout = L.add((size_t)total);
   const double t_lease = ms(t0);
   if ((rc = S->ensure_host(L.total)) || (rc = S->ensure_dev(L.total))) return rc;
   const double t_alloc = ms(t0);
@@ -1738,6 +1766,35 @@ int fcs_bgzf_inflate(const uint8_t* comp, int64_t comp_bytes, uint8_t* out, int6
     std::fprintf(stderr, "[fcs_bgzf_inflate] %d members, %lld -> %lld bytes: lease %.2f alloc %.2f in %.2f gpu %.2f out %.2f ms\n",
                  n, (long long)used, (long long)total, t_lease, t_alloc - t_lease, t_in - t_alloc, t_gpu - t_in,
                  ms(t0) - t_gpu);
+  return FCS_OK;
+}
+
+}  // namespace
+
+int fcs_bgzf_inflate(const uint8_t* comp, int64_t comp_bytes, uint8_t* out, int64_t out_cap, int64_t* comp_used,
+                     int64_t* out_bytes, int32_t device) {
+  return bgzf_inflate_host(comp, comp_bytes, out, out_cap, comp_used, out_bytes, device, false);
+}
+
+int fcs_bgzf_inflate_try(const uint8_t* comp, int64_t comp_bytes, uint8_t* out, int64_t out_cap, int64_t* comp_used,
+                         int64_t* out_bytes, int32_t device) {
+  return bgzf_inflate_host(comp, comp_bytes, out, out_cap, comp_used, out_bytes, device, true);
+}
+
+int fcs_bgzf_warmup(int32_t device, int32_t sessions, int64_t arena_bytes) {
+  if (sessions < 0 || arena_bytes < 0) return fail(FCS_ERR_INVALID, "[E::fcs_bgzf_warmup] bad arguments");
+  int rc = check_device(device);
+  if (rc) return rc;
+  FCS_SET_DEVICE((device));
+  sessions = std::min(sessions, sessions_per_device(kInflateSession));
+  // lease them all at once (so each is a different session), size, return
+  std::vector<std::unique_ptr<SessionLease>> held;
+  for (int k = 0; k < sessions; ++k) {
+    auto L = std::make_unique<SessionLease>();
+    if ((rc = L->acquire(device, kInflateSession))) return rc;
+    if ((rc = (*L)->ensure_host((size_t)arena_bytes)) || (rc = (*L)->ensure_dev((size_t)arena_bytes))) return rc;
+    held.push_back(std::move(L));
+  }
   return FCS_OK;
 }
 
@@ -1777,6 +1834,6 @@ int fcs_device_release(int32_t device) {
   return FCS_OK;
 }
 
-int fcs_abi_symbol_count(void) { return 45; }
+int fcs_abi_symbol_count(void) { return 47; }
 
 }  // extern "C"

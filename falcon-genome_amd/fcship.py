@@ -179,6 +179,8 @@ _sig("fcs_ksw_global2", C.c_int, [C.c_int, u8p, C.c_int, u8p, C.c_int, i8p, C.c_
 _sig("fcs_set_default_device", C.c_int, [C.c_int32])
 _sig("fcs_bgzf_index", C.c_int, [C.c_void_p, C.c_int64, C.c_void_p, C.c_void_p, C.c_int32, i32p, i64p])
 _sig("fcs_bgzf_inflate", C.c_int, [C.c_void_p, C.c_int64, C.c_void_p, C.c_int64, i64p, i64p, C.c_int32])
+_sig("fcs_bgzf_inflate_try", C.c_int, [C.c_void_p, C.c_int64, C.c_void_p, C.c_int64, i64p, i64p, C.c_int32])
+_sig("fcs_bgzf_warmup", C.c_int, [C.c_int32, C.c_int32, C.c_int64])
 _sig("fcs_bgzf_inflate_dev", C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_int32, C.c_void_p, C.c_void_p,
                                        C.c_int32, C.c_void_p])
 _sig("fcs_synth_phmm_sizes", C.c_int, [C.c_uint64, C.c_int64, C.c_int32, C.c_int32, C.c_int32, i64p, i64p])

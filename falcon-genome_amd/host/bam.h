@@ -100,6 +100,8 @@ class BamReader {
   // BgzfReader::use_device: later blocks inflated on GPU `device`; `span` =
   // the estimated compressed bytes of the range read from the next seek
   void use_device(int device, size_t span) { bgzf_.use_device(device, span); }
+  int device_chunks() const { return bgzf_.device_chunks(); }
+  int host_chunks() const { return bgzf_.host_chunks(); }
 
  private:
   BgzfReader bgzf_;

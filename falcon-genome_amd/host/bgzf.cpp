@@ -428,9 +428,7 @@ void BgzfReader::use_device(int device, size_t span) {
     }
   }
   device_ = device;
-  // later loads (past the caller's estimate) are small: they only finish the
-  // reads that start inside the range
-  chunk_ = 1u << 20;
+  chunk_ = 24u << 20;
   if (const char* e = std::getenv("FCS_BGZF_DEVICE_CHUNK"); e && std::atoll(e) > 0) chunk_ = (size_t)std::atoll(e);
   chunk_ = std::max<size_t>(chunk_, 1 << 17);  // two whole members at least
   span_ = span;
@@ -441,9 +439,17 @@ void BgzfReader::use_device(int device, size_t span) {
 // The first load after a seek covers the caller's whole estimated range in
 // one call (the kernel's rate comes from many members in flight: a shard's
 // range is a few hundred members, a chunk of it a few dozen), at most 256 MiB.
-size_t BgzfReader::first_want() const {
+size_t BgzfReader::first_want() const { return next_want(); }
+
+// Inside the caller's range: the rest of it, at most chunk_ (24 MiB: the
+// inflate sessions' staging holds such a chunk with its output); past it
+// 1 MiB loads finish the reads that start inside the range.
+size_t BgzfReader::next_want() const {
   if (std::getenv("FCS_BGZF_DEVICE_CHUNK")) return chunk_;
-  return span_ ? std::min<size_t>(std::max<size_t>(span_, 1 << 17), 256u << 20) : chunk_;
+  const uint64_t done = next_coff_ - range_start_;
+  if (!span_) return chunk_;
+  if (done < span_) return std::min<size_t>(std::max<size_t>(span_ - (size_t)done, 1 << 17), chunk_);
+  return 1 << 20;
 }
 
 // Reads `want` bytes at `at` and inflates their whole members into c.
@@ -467,8 +473,24 @@ void BgzfReader::fetch(uint64_t at, size_t want, Chunk& c) {
   c.uoff.resize((size_t)n + 1);
   c.out.resize((size_t)c.uoff[(size_t)n]);
   int64_t used2 = 0, out = 0;
-  if (fcs_bgzf_inflate(c.comp.data(), used, c.out.data(), (int64_t)c.out.size(), &used2, &out, device_) != FCS_OK)
+  // the GPU when one of its inflate sessions is idle and warm, else this
+  // thread's libdeflate: a reader never queues behind other shards' calls
+  const int rc = fcs_bgzf_inflate_try(c.comp.data(), used, c.out.data(), (int64_t)c.out.size(), &used2, &out, device_);
+  if (rc == FCS_BGZF_BUSY) {
+    ++host_chunks_;
+    for (int32_t k = 0; k < n; ++k) {
+      const uint8_t* m = c.comp.data() + c.coff[(size_t)k];
+      const size_t len = (size_t)(c.coff[(size_t)k + 1] - c.coff[(size_t)k]), hdr = 12 + get16(m + 10);
+      const size_t isize = (size_t)(c.uoff[(size_t)k + 1] - c.uoff[(size_t)k]);
+      uint8_t* o = c.out.data() + c.uoff[(size_t)k];
+      if (isize && (!inflate_block(m + hdr, len - hdr - 8, o, isize) || block_crc(o, isize) != get32(m + len - 8)))
+        throw formatError("corrupt BGZF block at offset " + std::to_string(at + (uint64_t)c.coff[(size_t)k]));
+    }
+  } else if (rc != FCS_OK) {
     throw formatError(std::string("BGZF at offset ") + std::to_string(at) + ": " + fcs_last_error());
+  } else {
+    ++device_chunks_;
+  }
   for (int32_t k = 0; k <= n; ++k) c.coff[(size_t)k] += (int64_t)at;
   for (int32_t k = 0; k < n; ++k)
     if (c.uoff[(size_t)k + 1] == c.uoff[(size_t)k]) c.empty_member = true;  // the EOF marker
@@ -491,13 +513,14 @@ bool BgzfReader::load_chunk() {
     } else {
       fetch(next_coff_, want_, cur_);
     }
-    want_ = chunk_;
+    want_ = 0;  // (set from the new position below)
     if (cur_.used == 0) return false;
     block_.swap(cur_.out);
     mcoff_.swap(cur_.coff);
     muoff_.swap(cur_.uoff);
     block_coff_ = cur_.start;
     next_coff_ = cur_.start + cur_.used;
+    want_ = next_want();
     saw_eof_ = saw_eof_ || cur_.empty_member;
     pos_ = 0;
     // the next chunk on a helper thread while the caller parses this one,

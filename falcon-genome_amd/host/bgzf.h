@@ -8,6 +8,7 @@
 // offset is (compressed block start << 16) | offset inside the block.
 #pragma once
 
+#include <atomic>
 #include <cstdint>
 #include <cstdio>
 #include <deque>
@@ -121,10 +122,11 @@ class BgzfReader {
   // chunk of compressed bytes, inflates every whole member in it in one call
   // and serves their concatenated output as one block, so records spanning
   // members are viewed in place too.  `span` is the caller's estimate of its
-  // compressed range from the next seek (a BAI span; 0: unknown): the first
-  // load covers it whole, later loads read 16 MiB (FCS_BGZF_DEVICE_CHUNK sets
-  // every load's size), and while inside the range the next chunk is read and
-  // inflated on a helper thread while the caller parses the current one.
+  // compressed range from the next seek (a BAI span; 0: unknown): loads cover
+  // it in chunks of at most 24 MiB (FCS_BGZF_DEVICE_CHUNK sets every load's
+  // size), the next one read and inflated on a helper thread while the caller
+  // parses the current one; a chunk goes to the host codec when no warm GPU
+  // inflate session is idle (fcs_bgzf_inflate_try).
   void use_device(int device, size_t span);
 
  private:
@@ -138,6 +140,7 @@ class BgzfReader {
   bool load_chunk();  // device mode's load_block
   void fetch(uint64_t at, size_t want, Chunk& c);
   size_t first_want() const;
+  size_t next_want() const;
   void drop_ahead();
   FILE* f_ = nullptr;
   std::vector<uint8_t> block_, comp_;
@@ -151,6 +154,14 @@ class BgzfReader {
   std::vector<int64_t> mcoff_, muoff_;  // the current chunk's members
   Chunk cur_, ahead_;
   std::future<void> ahead_job_;
+
+ public:
+  // device mode: chunks inflated on the GPU / on this host (sessions busy)
+  int device_chunks() const { return device_chunks_; }
+  int host_chunks() const { return host_chunks_; }
+
+ private:
+  std::atomic<int> device_chunks_{0}, host_chunks_{0};
 };
 
 // Whole-buffer helpers (tests, small files).

@@ -10,6 +10,7 @@
 #include <cmath>
 #include <condition_variable>
 #include <cstdio>
+#include <utility>
 #include <cstring>
 #include <deque>
 #include <map>
@@ -36,6 +37,8 @@ void CallerStats::add(const CallerStats& o) {
   calls += o.calls;
   device_passes += o.device_passes;
   decode_passes += o.decode_passes;
+  inflate_gpu_chunks += o.inflate_gpu_chunks;
+  inflate_host_chunks += o.inflate_host_chunks;
   cpu_seconds += o.cpu_seconds;
   for (int k = 0; k < 4; ++k) faults[k] += o.faults[k];
   rescued += o.rescued;
@@ -75,9 +78,19 @@ struct Read {
 };
 static_assert(std::is_trivially_copyable_v<Read>, "Read lives in a HugeVec");
 
+// window chunks of this thread inflated on the GPU / on the host (gpu.bam_inflate)
+thread_local int64_t tl_inflate_gpu = 0, tl_inflate_host = 0;
+
 void load_reads_one(const std::string& bam, const std::string& chrom, int64_t beg, int64_t end,
                     const CallerOptions& opt, HugeSlab& slab, HugeVec<Read>& out) {
   BamReader rd(bam);
+  struct Count {
+    const BamReader& r;
+    ~Count() {
+      tl_inflate_gpu += r.device_chunks();
+      tl_inflate_host += r.host_chunks();
+    }
+  } count{rd};
   const int tid = rd.header().ref_index(chrom);
   if (tid < 0) return;
   const std::string bai = bam_index_path(bam);
@@ -942,6 +955,8 @@ CallerStats call_intervals(const Reference& ref, const std::vector<std::string>&
       const uint64_t tp = now_us();
       st.decode_seconds += (tp - td) / 1e6;
       ++st.decode_passes;
+      st.inflate_gpu_chunks += std::exchange(tl_inflate_gpu, 0);
+      st.inflate_host_chunks += std::exchange(tl_inflate_host, 0);
       const int64_t f1 = thread_faults();
       st.faults[0] += f1 - f0;
       pu = Pileup();

@@ -57,6 +57,7 @@ struct CallerOptions {
 
 struct CallerStats {
   int64_t reads = 0, regions = 0, pairs = 0, cells = 0, calls = 0, device_passes = 0, decode_passes = 0;
+  int64_t inflate_gpu_chunks = 0, inflate_host_chunks = 0;  // gpu.bam_inflate: window chunks by where they inflated
   int64_t rescued = 0;  // pairs the fp64 rescue recomputed (fp32 sum < 1e-28)
   double seconds = 0, phmm_seconds = 0;
   // wall-time breakdown of `seconds`: BAM decode, pileup + active sites,

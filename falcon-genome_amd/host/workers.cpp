@@ -109,12 +109,13 @@ int HTCWorker::run(TaskContext& ctx) {
     std::fprintf(ctx.log,
                  "[fcs-genome htc] shard %d gpu %d: %lld reads, %lld regions, %lld pairs, %lld cells, %lld rescued, "
                  "%lld calls, %.3f s (PairHMM %.3f s, device %.4f s, rescue %.4f s, %lld device passes; decode %.3f s "
-                 "(%lld passes), pileup %.3f s, regions %.3f s, genotype %.3f s, output %.3f s; thread cpu %.3f s, "
+                 "(%lld passes, inflate %lld gpu / %lld host chunks), pileup %.3f s, regions %.3f s, genotype %.3f s, output %.3f s; thread cpu %.3f s, "
                  "minor faults %lld/%lld/%lld/%lld)\n",
                  contig_, ctx.gpu, (long long)stats_.reads, (long long)stats_.regions, (long long)stats_.pairs,
                  (long long)stats_.cells, (long long)stats_.rescued, (long long)stats_.calls, stats_.seconds,
                  stats_.phmm_seconds, stats_.phmm_device_seconds, stats_.rescue_device_seconds,
-                 (long long)stats_.device_passes, stats_.decode_seconds, (long long)stats_.decode_passes, stats_.pileup_seconds,
+                 (long long)stats_.device_passes, stats_.decode_seconds, (long long)stats_.decode_passes,
+                 (long long)stats_.inflate_gpu_chunks, (long long)stats_.inflate_host_chunks, stats_.pileup_seconds,
                  stats_.region_seconds, stats_.genotype_seconds, stats_.output_seconds, stats_.cpu_seconds,
                  (long long)stats_.faults[0], (long long)stats_.faults[1], (long long)stats_.faults[2],
                  (long long)stats_.faults[3]);
@@ -162,12 +163,13 @@ int Mutect2Worker::run(TaskContext& ctx) {
     std::fprintf(ctx.log,
                  "[fcs-genome mutect2] shard %d gpu %d: %lld reads, %lld regions, %lld pairs, %lld cells, %lld rescued, "
                  "%lld calls, %.3f s (PairHMM %.3f s, device %.4f s, rescue %.4f s, %lld device passes; decode %.3f s "
-                 "(%lld passes), pileup %.3f s, regions %.3f s, genotype %.3f s, output %.3f s; thread cpu %.3f s, "
+                 "(%lld passes, inflate %lld gpu / %lld host chunks), pileup %.3f s, regions %.3f s, genotype %.3f s, output %.3f s; thread cpu %.3f s, "
                  "minor faults %lld/%lld/%lld/%lld)\n",
                  contig_, ctx.gpu, (long long)stats_.reads, (long long)stats_.regions, (long long)stats_.pairs,
                  (long long)stats_.cells, (long long)stats_.rescued, (long long)stats_.calls, stats_.seconds,
                  stats_.phmm_seconds, stats_.phmm_device_seconds, stats_.rescue_device_seconds,
-                 (long long)stats_.device_passes, stats_.decode_seconds, (long long)stats_.decode_passes, stats_.pileup_seconds,
+                 (long long)stats_.device_passes, stats_.decode_seconds, (long long)stats_.decode_passes,
+                 (long long)stats_.inflate_gpu_chunks, (long long)stats_.inflate_host_chunks, stats_.pileup_seconds,
                  stats_.region_seconds, stats_.genotype_seconds, stats_.output_seconds, stats_.cpu_seconds,
                  (long long)stats_.faults[0], (long long)stats_.faults[1], (long long)stats_.faults[2],
                  (long long)stats_.faults[3]);
@@ -290,9 +292,14 @@ DeviceWarmupWorker::DeviceWarmupWorker(std::vector<int> gpus) : Worker(1, 1, {},
 
 int DeviceWarmupWorker::run(TaskContext&) {
   // runtime, code objects, GKL tables and the pooled call sessions of each
-  // device, while the shards decode their first reads
+  // device, while the shards decode their first reads; then, with
+  // gpu.bam_inflate, warm inflate sessions (the windows decoded before they
+  // are ready inflate on their own threads)
   for (int d : gpus_)
     if (fcs_device_warmup(d, 0) != FCS_OK) return 1;
+  if (conf().get_bool("gpu.bam_inflate"))
+    for (int d : gpus_)
+      if (fcs_bgzf_warmup(d, 8, (int64_t)112 << 20) != FCS_OK) return 1;
   return 0;
 }
 

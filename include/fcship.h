@@ -373,6 +373,15 @@ int fcs_bgzf_inflate(const uint8_t* comp, int64_t comp_bytes, uint8_t* out, int6
                      int64_t* out_bytes, int32_t device);
 int fcs_bgzf_inflate_dev(const uint8_t* dev_comp, const int64_t* dev_coff, const int64_t* dev_uoff, int32_t n,
                          uint8_t* dev_out, int32_t* dev_status, int32_t device, void* stream);
+/* fcs_bgzf_inflate without waiting: FCS_BGZF_BUSY (nothing done, *comp_used =
+ * 0) unless an inflate session is idle whose staging arenas already hold the
+ * call, so a reader can inflate on its own cores instead of queueing.
+ * fcs_bgzf_warmup creates `sessions` inflate sessions with `arena_bytes` of
+ * pinned host and device staging each (the growth a first call would pay). */
+#define FCS_BGZF_BUSY 1
+int fcs_bgzf_inflate_try(const uint8_t* comp, int64_t comp_bytes, uint8_t* out, int64_t out_cap, int64_t* comp_used,
+                         int64_t* out_bytes, int32_t device);
+int fcs_bgzf_warmup(int32_t device, int32_t sessions, int64_t arena_bytes);
 
 /* ---------------------------------------------- synthetic workload builders */
 /* Seeded generators for the benchmark configurations (BASELINE.json C2/C3).

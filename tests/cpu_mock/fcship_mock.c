@@ -334,3 +334,24 @@ int fcs_bgzf_inflate(const uint8_t* comp, int64_t comp_bytes, uint8_t* out, int6
   free(uoff);
   return rc;
 }
+
+/* fcs_bgzf_inflate_try: FCS_MOCK_BGZF_BUSY=all makes every call busy,
+ * =alternate every other one, so CPU tests cover the reader's host fallback. */
+int fcs_bgzf_inflate_try(const uint8_t* comp, int64_t comp_bytes, uint8_t* out, int64_t out_cap, int64_t* comp_used,
+                         int64_t* out_bytes, int32_t device) {
+  static int calls = 0;
+  const char* m = getenv("FCS_MOCK_BGZF_BUSY");
+  const int k = __atomic_fetch_add(&calls, 1, __ATOMIC_RELAXED);
+  if (m && (!strcmp(m, "all") || (!strcmp(m, "alternate") && (k & 1)))) {
+    if (comp_used) *comp_used = 0;
+    return FCS_BGZF_BUSY;
+  }
+  return fcs_bgzf_inflate(comp, comp_bytes, out, out_cap, comp_used, out_bytes, device);
+}
+
+int fcs_bgzf_warmup(int32_t device, int32_t sessions, int64_t arena_bytes) {
+  (void)device;
+  (void)sessions;
+  (void)arena_bytes;
+  return FCS_OK;
+}

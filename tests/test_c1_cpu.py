@@ -106,12 +106,16 @@ def test_window_inflate_chunks_cross_members(mock_dir, tmp_path):
     """Many 128 KiB chunks per window (FCS_BGZF_DEVICE_CHUNK), several
     windows and shards: records split across chunk ends, chunks ending
     mid-member and BAI seeks into a chunk give the same VCF as the host's
-    member-by-member reader."""
+    member-by-member reader — with every chunk through fcs_bgzf_inflate_try,
+    and with every other one "busy" so the reader inflates it on its own
+    thread."""
     d = tmp_path / "in"
     p = H.run_cli("synth", "-o", d, "-c", "chrA:400000,chrB:150000", "-x", "12", "--no-fastq", "--seed", "9")
     assert p.returncode == 0, p.stderr[-2000:]
     outs = []
     for name, env in (("chunked", {"FCS_GPU_BAM_INFLATE": "true", "FCS_BGZF_DEVICE_CHUNK": str(128 << 10)}),
+                      ("mixed", {"FCS_GPU_BAM_INFLATE": "true", "FCS_BGZF_DEVICE_CHUNK": str(128 << 10),
+                                 "FCS_MOCK_BGZF_BUSY": "alternate"}),
                       ("host", {"FCS_GPU_BAM_INFLATE": "false"})):
         out = tmp_path / f"{name}.vcf"
         e = {"LD_LIBRARY_PATH": mock_dir, "FCS_GPU_DEVICES": "0", "FCS_MOCK_PHMM": "gkl",
@@ -120,4 +124,4 @@ def test_window_inflate_chunks_cross_members(mock_dir, tmp_path):
         assert p.returncode == 0, p.stderr[-3000:]
         outs.append([ln for ln in open(out) if not ln.startswith("##")])
     assert len(outs[0]) > 20
-    assert outs[0] == outs[1]
+    assert outs[0] == outs[1] == outs[2]

@@ -16,7 +16,7 @@ for i in 1 2 3 4; do
     { time timeout 300 $B htc -f -r $W/d/ref.fasta -i $W/d/sample.bam -o $W/h_$mode.g.vcf 2> $W/htc.err; } 2> $W/htc.time || { tail -3 $W/htc.err; grep -rh "E::\|rror\|what" $W/log | head -10; exit 1; }
     echo "== gpu_inflate=$mode run $i: $(grep -E '^(real|user)' $W/htc.time | tr '\n' ' ')"
     grep -E "timeline" $W/htc.err | tail -2
-    grep -h "htc\] shard" $W/log/*.log | awk '{for(i=1;i<=NF;i++){if($i=="(decode"||$i=="decode"){d+=$(i+1)}}} END{print "  decode thread-s", d, "shards", NR}'
+    grep -h "htc\] shard" $W/log/*.log | awk '{for(i=1;i<=NF;i++){if($i=="(decode"||$i=="decode"){d+=$(i+1)} if($i=="inflate"){g+=$(i+1); h+=$(i+4)}}} END{print "  decode thread-s", d, "shards", NR, "inflate chunks gpu", g, "host", h}'
   done
 done
 grep -h "htc\] shard" $W/log/*.log | head -2
