@@ -1032,7 +1032,8 @@ def main():
     ap.add_argument("--e2e-mbp", type=float, default=31.0,
                     help="per-GPU genome of the htc / mutect2 runs (31 Mbp = chr1 / 8 GPUs, the C4 share)")
     ap.add_argument("--e2e-align-mbp", type=float, default=4.0, help="genome of the align run")
-    ap.add_argument("--e2e-reps", type=int, default=2, help="runs of each e2e command; the fastest is reported")
+    ap.add_argument("--e2e-reps", type=int, default=3,
+                    help="runs of each e2e command; the fastest is reported, every run's wall time listed")
     ap.add_argument("--no-c4", action="store_true",
                     help="N > 1: skip the C4 leg (one htc job over N x --e2e-mbp, dealt to all N GPUs)")
     args = ap.parse_args()
