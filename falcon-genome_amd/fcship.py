@@ -561,6 +561,7 @@ def cigar_str(ops) -> str:
 
 
 FCS_BGZF_OK, FCS_BGZF_CORRUPT, FCS_BGZF_OVERFLOW, FCS_BGZF_CRC = 0, 1, 2, 3
+FCS_BGZF_BUSY = 1  # fcs_bgzf_inflate_try's return when no warm inflate session is idle
 
 
 def bgzf_index(comp, cap: int | None = None):

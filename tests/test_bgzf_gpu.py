@@ -108,3 +108,25 @@ def test_inflate_dev_statuses(gpu):
     for k, (_, _, p) in enumerate(cases):
         if k != bad_k:
             assert o[uoff[k]:uoff[k + 1]] == p
+
+
+def test_try_uses_only_warm_idle_sessions(gpu):
+    """fcs_bgzf_inflate_try inflates when a warm inflate session's arenas fit
+    the call, and answers FCS_BGZF_BUSY (nothing done) when none does."""
+    import ctypes as C
+    cases = bgzf_cases.suite(seed=16, count=12)
+    blob = np.frombuffer(b"".join(m for _, m, _ in cases), np.uint8).copy()
+    want = b"".join(p for _, _, p in cases)
+    fcship.check(fcship.lib.fcs_bgzf_warmup(0, 2, 64 << 20))
+    out = np.zeros(len(want) + 1, np.uint8)
+    used, got = C.c_int64(), C.c_int64()
+    rc = fcship.lib.fcs_bgzf_inflate_try(blob.ctypes.data, len(blob), out.ctypes.data, len(want), C.byref(used),
+                                         C.byref(got), 0)
+    assert rc == fcship.FCS_OK and used.value == len(blob) and out[:got.value].tobytes() == want
+    # a call larger than every warm arena: busy, nothing written
+    big = np.frombuffer(b"".join(bgzf_cases.member(bytes(60000), 1) for _ in range(2000)), np.uint8).copy()
+    cap = 2000 * 60000
+    obig = np.zeros(cap, np.uint8)
+    rc = fcship.lib.fcs_bgzf_inflate_try(big.ctypes.data, len(big), obig.ctypes.data, cap, C.byref(used),
+                                         C.byref(got), 0)
+    assert rc == fcship.FCS_BGZF_BUSY and used.value == 0
