@@ -53,6 +53,19 @@ def member_libdeflate(payload: bytes, level: int) -> bytes:
     return member(payload, raw=buf.raw[:n])
 
 
+def flushed_member(payload: bytes, pieces: int, level: int = 6, flush: int = zlib.Z_SYNC_FLUSH) -> bytes:
+    """One member of several DEFLATE blocks: the payload compressed in pieces
+    with a flush after each (a sync flush adds an empty stored block, a full
+    flush also resets the window)."""
+    c = zlib.compressobj(level, zlib.DEFLATED, -15, 8, zlib.Z_DEFAULT_STRATEGY)
+    step = max(1, len(payload) // pieces)
+    raw = b""
+    for k in range(0, len(payload), step):
+        raw += c.compress(payload[k:k + step]) + c.flush(flush)
+    raw += c.flush()
+    return member(payload, raw=raw)
+
+
 def stored_member(payload: bytes) -> bytes:
     """One stored (type 0) block: LEN, NLEN, the bytes."""
     assert len(payload) < 65536 - 64
@@ -97,6 +110,9 @@ def suite(seed: int = 3, count: int = 120) -> list[tuple[str, bytes, bytes]]:
     raw = payload(rng, "random", 60000)
     cases = [("eof", EOF_MEMBER, b""), ("empty-l6", member(b""), b""), ("one-byte", member(b"x"), b"x"),
              ("stored", stored_member(raw), raw)]
+    for kind, pieces, fl in (("bam", 7, zlib.Z_SYNC_FLUSH), ("gvcf", 13, zlib.Z_FULL_FLUSH), ("runs", 3, zlib.Z_SYNC_FLUSH)):
+        p = payload(rng, kind, 50000)
+        cases.append((f"{kind}-{pieces}-blocks", flushed_member(p, pieces, 6, fl), p))
     kinds = ["random", "runs", "gvcf", "bam"]
     strategies = [zlib.Z_DEFAULT_STRATEGY, zlib.Z_FIXED, zlib.Z_HUFFMAN_ONLY, zlib.Z_RLE, zlib.Z_FILTERED]
     for i in range(count):
