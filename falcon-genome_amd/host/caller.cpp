@@ -829,23 +829,18 @@ void emit_gvcf(const Pileup& pu, int64_t beg, int64_t end, int contig, const std
 // {chrom, b + 1, ".", REF, "<NON_REF>", ".", ".", "END=e + 1",
 //  "GT:DP:GQ:MIN_DP:PL", "0/0:DP:GQ:MIN_DP:PL0,PL1,PL2"}.
 void append_block_line(const std::string& chrom, char ref, const GvcfBlock& k, std::string& s) {
-  char b[256];  // 2 x 20 + 6 x 11 digits + 60 literal bytes at most
+  char b[256 + 64];  // a short contig name + 2 x 20 + 6 x 11 digits + 60 literal bytes at most
   char* p = b;
-  auto num = [&](int64_t v) {  // decimal, as std::to_chars
-    uint64_t u = v < 0 ? (*p++ = '-', 0 - (uint64_t)v) : (uint64_t)v;
-    char d[20];
-    int k = 0;
-    do {
-      d[k++] = (char)('0' + u % 10);
-      u /= 10;
-    } while (u);
-    while (k) *p++ = d[--k];
-  };
+  auto num = [&](int64_t v) { p = std::to_chars(p, b + sizeof b, v).ptr; };  // (gcc's: 2 digits a step)
   auto lit = [&](std::string_view t) {
     std::memcpy(p, t.data(), t.size());
     p += t.size();
   };
-  s += chrom;
+  if (chrom.size() <= 64) {
+    lit(chrom);
+  } else {
+    s += chrom;
+  }
   *p++ = '\t';
   num(k.b + 1);
   lit("\t.\t");
