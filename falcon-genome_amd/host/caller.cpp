@@ -828,6 +828,10 @@ void emit_gvcf(const Pileup& pu, int64_t beg, int64_t end, int contig, const std
 // One GVCF block line, as VcfRecord::append_line writes the record
 // {chrom, b + 1, ".", REF, "<NON_REF>", ".", ".", "END=e + 1",
 //  "GT:DP:GQ:MIN_DP:PL", "0/0:DP:GQ:MIN_DP:PL0,PL1,PL2"}.
+// (GCC's -Wstringop-overflow cannot bound to_chars' result pointer here; the
+// buffer holds the longest line, see its size)
+#pragma GCC diagnostic push
+#pragma GCC diagnostic ignored "-Wstringop-overflow"
 void append_block_line(const std::string& chrom, char ref, const GvcfBlock& k, std::string& s) {
   char b[256 + 64];  // a short contig name + 2 x 20 + 6 x 11 digits + 60 literal bytes at most
   char* p = b;
@@ -862,6 +866,7 @@ void append_block_line(const std::string& chrom, char ref, const GvcfBlock& k, s
   *p++ = '\n';
   s.append(b, (size_t)(p - b));
 }
+#pragma GCC diagnostic pop
 
 }  // namespace
 
