@@ -832,6 +832,7 @@ void emit_gvcf(const Pileup& pu, int64_t beg, int64_t end, int contig, const std
 // buffer holds the longest line, see its size)
 #pragma GCC diagnostic push
 #pragma GCC diagnostic ignored "-Wstringop-overflow"
+#pragma GCC diagnostic ignored "-Warray-bounds"
 void append_block_line(const std::string& chrom, char ref, const GvcfBlock& k, std::string& s) {
   char b[256 + 64];  // a short contig name + 2 x 20 + 6 x 11 digits + 60 literal bytes at most
   char* p = b;
