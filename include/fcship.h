@@ -362,7 +362,8 @@ int fcs_set_default_device(int32_t device);
  *
  * fcs_bgzf_inflate_dev: device buffers, stream-ordered; dev_coff / dev_uoff
  * as fcs_bgzf_index returns them, dev_status[k] = FCS_BGZF_* of member k
- * (member k's output is written only when it is FCS_BGZF_OK). */
+ * (member k's output range holds its bytes when it is FCS_BGZF_OK; a failing
+ * member may leave partial bytes there, never outside its range). */
 #define FCS_BGZF_OK 0
 #define FCS_BGZF_CORRUPT 1  /* bad DEFLATE stream, header or ISIZE */
 #define FCS_BGZF_OVERFLOW 2 /* the stream inflates past ISIZE */
