@@ -82,6 +82,10 @@ __global__ __launch_bounds__(64) void bgzf_inflate_kernel(const uint8_t* __restr
   if (m >= n) return;
   const int64_t c0 = coff[m], clen = coff[m + 1] - c0, u0 = uoff[m], ulen = uoff[m + 1] - u0;
   const uint8_t* mem = comp + c0;
+  if (clen < 20) {  // shorter than a gzip header and trailer: read nothing of it
+    if (lane == 0) status[m] = FCS_BGZF_CORRUPT;
+    return;
+  }
   const int xlen = (int)rfl((uint32_t)mem[10] | (uint32_t)mem[11] << 8);
   const int64_t plen = clen - 12 - xlen - 8;
   if (plen < 0 || plen > kBgzfMax || ulen < 0 || ulen > kBgzfMax) {
