@@ -654,6 +654,12 @@ def bench_bgzf(bam, dev_index, cpu, reps=3):
                       "frac": round((tot_in + tot_out) / ms / 1e6 / HBM_PEAK_GBS, 5),
                       "algorithmic_bytes_per_launch": tot_in + tot_out,
                       "kernel": "bgzf_inflate_kernel (bgzf_kernels.hip)"}}
+    try:  # the kernel's issue counters (SALU-bound: one SALU per cycle per CU)
+        pm = json.load(open(os.path.join(ROOT, "profiles", "pmc_bgzf.json")))
+        r["roofline"]["counters_per_member"] = pm["per_member"]
+        r["roofline"]["counters_source"] = pm["source"]
+    except (OSError, ValueError, KeyError):
+        pass
     if cpu:
         L = ctypes.CDLL("libdeflate.so.0")
         L.libdeflate_alloc_decompressor.restype = ctypes.c_void_p
