@@ -72,14 +72,24 @@ def test_corruption_is_reported_per_member(gpu):
     short[-4:] = struct.pack("<I", len(cases[k][2]) - 1)
     with pytest.raises(fcship.FcsError, match=f"member {k} "):
         fcship.bgzf_inflate(_with_bad(cases, k, bytes(short)), device=gpu)
-    # flipped bits in the DEFLATE stream: an error (corrupt, overflow or CRC),
-    # never a fault; the other members are unaffected
+    # flipped bits in the DEFLATE stream: an error naming the member (corrupt,
+    # overflow or CRC), never a fault — or, for the bits DEFLATE ignores (the
+    # padding of a stored block's header, the bits after the final block),
+    # the right bytes
+    want = b"".join(c[2] for c in cases)
+    errors = 0
     for trial in range(40):
         bad = bytearray(m)
         at = 18 + int(rng.integers(0, len(m) - 26))
         bad[at] ^= 1 << int(rng.integers(0, 8))
-        with pytest.raises(fcship.FcsError, match=f"member {k} "):
-            fcship.bgzf_inflate(_with_bad(cases, k, bytes(bad)), device=gpu)
+        try:
+            out, _ = fcship.bgzf_inflate(_with_bad(cases, k, bytes(bad)), device=gpu)
+        except fcship.FcsError as e:
+            assert f"member {k} " in str(e), str(e)
+            errors += 1
+        else:
+            assert out == want
+    assert errors >= 30
     out, _ = fcship.bgzf_inflate(b"".join(c[1] for c in cases), device=gpu)
     assert out == b"".join(c[2] for c in cases)
 
