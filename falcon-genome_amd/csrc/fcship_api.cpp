@@ -449,6 +449,8 @@ struct fcs_phmm_plan {
   unsigned long long* rescue_count = nullptr;  // [0] rescue count, [1] fallback count, then int64 class bounds
   unsigned long long* fb_count = nullptr;
   int64_t* bounds = nullptr;
+  uint32_t* bin_hist = nullptr;    // the bin schedule's histogram (kept zero between schedules)
+  uint32_t* bin_cursor = nullptr;  // and its running bin starts
   int64_t scheduled = -1;  // n_pairs of the last schedule
   bool counters_zeroed = false;  // the last schedule's keys kernel zeroed rescue_count[0..1]
 };
@@ -618,6 +620,10 @@ int fcs_phmm_plan_create(int32_t device, int64_t max_pairs, fcs_phmm_plan** plan
   FCS_HIP_CHECK(sort_pairs_u32(nullptr, tmp, p->keys_in, p->keys_out, p->idx_in, p->idx_out, (int)n, nullptr));
   p->sort_tmp_bytes = std::max<size_t>(tmp, 16);
   FCS_HIP_CHECK(hipMalloc(&p->sort_tmp, p->sort_tmp_bytes));
+  constexpr size_t kBins = (size_t)1 << (kPhmmKeyBits - 4);
+  FCS_HIP_CHECK(hipMalloc(&p->bin_hist, 2 * kBins * sizeof(uint32_t)));
+  p->bin_cursor = p->bin_hist + kBins;
+  FCS_HIP_CHECK(hipMemset(p->bin_hist, 0, kBins * sizeof(uint32_t)));  // before any stream uses the plan
   *plan = p.release();
   return FCS_OK;
 }
@@ -634,6 +640,7 @@ int fcs_phmm_plan_destroy(fcs_phmm_plan* p) {
   (void)hipFree(p->rescue_list);
   (void)hipFree(p->fb_list);
   (void)hipFree(p->rescue_count);
+  (void)hipFree(p->bin_hist);
   delete p;
   return FCS_OK;
 }
@@ -646,15 +653,30 @@ int fcs_phmm_dev_schedule(fcs_phmm_plan* plan, const fcs_phmm_batch* b, void* st
   FCS_SET_DEVICE((plan->device));
   hipStream_t s = (hipStream_t)stream;
   const PhmmDevBatch d = to_dev(b);
-  rc = launch_phmm_keys(d, plan->keys_in, plan->idx_in, plan->rescue_count, s);
-  if (rc) return rc;
-  plan->counters_zeroed = b->n_pairs > 0;
-  if (b->n_pairs > 0) {
-    size_t tmp = plan->sort_tmp_bytes;
-    FCS_HIP_CHECK(sort_pairs_u32(plan->sort_tmp, tmp, plan->keys_in, plan->keys_out, plan->idx_in, plan->idx_out,
-                                 (int)b->n_pairs, s, kPhmmKeyBits));
+  // The bin schedule (a counting sort on the key's top 12 bits, three
+  // kernels) unless FCS_PHMM_SCHEDULE=radix asks for the full 16-bit radix
+  // sort (rocPRIM onesweep: eight launches and look-back state fills, ≈ 0.15 ms
+  // of a 1M-pair C2 step).
+  static const bool radix = [] {
+    const char* e = std::getenv("FCS_PHMM_SCHEDULE");
+    return e && std::string(e) == "radix";
+  }();
+  if (!radix) {
+    if ((rc = launch_phmm_bin_schedule(d, plan->idx_out, plan->bounds, plan->rescue_count, plan->bin_hist,
+                                       plan->bin_cursor, s)))
+      return rc;
+    plan->counters_zeroed = true;
+  } else {
+    rc = launch_phmm_keys(d, plan->keys_in, plan->idx_in, plan->rescue_count, s);
+    if (rc) return rc;
+    plan->counters_zeroed = b->n_pairs > 0;
+    if (b->n_pairs > 0) {
+      size_t tmp = plan->sort_tmp_bytes;
+      FCS_HIP_CHECK(sort_pairs_u32(plan->sort_tmp, tmp, plan->keys_in, plan->keys_out, plan->idx_in, plan->idx_out,
+                                   (int)b->n_pairs, s, kPhmmKeyBits));
+    }
+    if ((rc = launch_phmm_bounds(plan->keys_out, b->n_pairs, plan->bounds, s))) return rc;
   }
-  if ((rc = launch_phmm_bounds(plan->keys_out, b->n_pairs, plan->bounds, s))) return rc;
   if (fault_drop_schedule()) FCS_HIP_CHECK(hipMemsetAsync(plan->bounds, 0, (kPhmmLaunchClasses + 1) * sizeof(int64_t), s));
   plan->scheduled = b->n_pairs;
   return FCS_OK;

@@ -463,14 +463,7 @@ __host__ __device__ inline int phmm_launch_class(int R, int H, int& stream_cls) 
   return kLongClasses + kColsLaunch + kPhmmClasses - 1 - phmm_class(max(H, 0));
 }
 
-__global__ void phmm_keys_kernel(const PhmmDevBatch b, uint32_t* __restrict__ keys, int32_t* __restrict__ idx,
-                                 unsigned long long* __restrict__ counters) {
-  const long long p = (long long)blockIdx.x * blockDim.x + threadIdx.x;
-  if (p == 0) {
-    counters[0] = 0ull;
-    counters[1] = 0ull;
-  }
-  if (p >= b.n_pairs) return;
+__device__ __forceinline__ uint32_t phmm_key(const PhmmDevBatch& b, long long p) {
   const int R = b.read_len[b.pair_read[p]];
   const int H = b.hap_len[b.pair_hap[p]];
   int sc;
@@ -483,8 +476,101 @@ __global__ void phmm_keys_kernel(const PhmmDevBatch b, uint32_t* __restrict__ ke
     low = hh;
   else
     low = ((3u - (uint32_t)min((max(R, 0) + 15) >> 4, 3)) << 10) | (0x3FFu - (uint32_t)min(max(H, 0) >> 2, 0x3FF));
-  keys[p] = (cf << kPhmmKeyClassShift) | low;
+  return (cf << kPhmmKeyClassShift) | low;
+}
+
+__global__ void phmm_keys_kernel(const PhmmDevBatch b, uint32_t* __restrict__ keys, int32_t* __restrict__ idx,
+                                 unsigned long long* __restrict__ counters) {
+  const long long p = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (p == 0) {
+    counters[0] = 0ull;
+    counters[1] = 0ull;
+  }
+  if (p >= b.n_pairs) return;
+  keys[p] = phmm_key(b, p);
   idx[p] = (int32_t)p;
+}
+
+// ---- bin schedule: a counting sort on the key's top 12 bits (class, then the
+// in-class order in steps of 16), three small kernels instead of the radix
+// sort's eight launches and state fills.  Order inside a bin is arbitrary
+// (results never depend on the order; the bins keep the longest work first
+// to 16 haplotype bases).
+constexpr int kPhmmBins = 1 << (kPhmmKeyBits - 4);
+constexpr int kBinBlock = 1024, kBinItems = 4;
+__device__ __forceinline__ int phmm_bin(const PhmmDevBatch& b, long long p) { return (int)(phmm_key(b, p) >> 4); }
+
+__global__ __launch_bounds__(kBinBlock) void phmm_bin_count_kernel(const PhmmDevBatch b, uint32_t* __restrict__ hist,
+                                                                    unsigned long long* __restrict__ counters) {
+  __shared__ uint32_t h[kPhmmBins];
+  for (int i = threadIdx.x; i < kPhmmBins; i += kBinBlock) h[i] = 0;
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    counters[0] = 0ull;
+    counters[1] = 0ull;
+  }
+  __syncthreads();
+  const long long base = (long long)blockIdx.x * (kBinBlock * kBinItems);
+  for (int k = 0; k < kBinItems; ++k) {
+    const long long p = base + (long long)k * kBinBlock + threadIdx.x;
+    if (p < b.n_pairs) atomicAdd(&h[phmm_bin(b, p)], 1u);
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < kPhmmBins; i += kBinBlock)
+    if (h[i]) atomicAdd(&hist[i], h[i]);
+}
+
+// One block: cursor = exclusive prefix of hist, bounds per launch class, hist
+// zeroed again for the next schedule.
+__global__ __launch_bounds__(kBinBlock) void phmm_bin_scan_kernel(uint32_t* __restrict__ hist,
+                                                                   uint32_t* __restrict__ cursor, long long n,
+                                                                   int64_t* __restrict__ bounds) {
+  constexpr int kPer = kPhmmBins / kBinBlock;
+  __shared__ uint32_t part[kBinBlock];
+  const int t = threadIdx.x;
+  uint32_t v[kPer], sum = 0;
+  for (int j = 0; j < kPer; ++j) {
+    v[j] = hist[t * kPer + j];
+    sum += v[j];
+  }
+  part[t] = sum;
+  __syncthreads();
+  for (int off = 1; off < kBinBlock; off <<= 1) {  // inclusive scan of the per-thread sums
+    const uint32_t x = t >= off ? part[t - off] : 0u;
+    __syncthreads();
+    part[t] += x;
+    __syncthreads();
+  }
+  uint32_t run = part[t] - sum;
+  for (int j = 0; j < kPer; ++j) {
+    const int bin = t * kPer + j;
+    cursor[bin] = run;
+    if ((bin & 255) == 0 && (bin >> 8) < kPhmmLaunchClasses) bounds[bin >> 8] = run;
+    run += v[j];
+    hist[bin] = 0u;
+  }
+  if (t == 0) bounds[kPhmmLaunchClasses] = n;
+}
+
+__global__ __launch_bounds__(kBinBlock) void phmm_bin_scatter_kernel(const PhmmDevBatch b,
+                                                                      uint32_t* __restrict__ cursor,
+                                                                      int32_t* __restrict__ idx) {
+  __shared__ uint32_t cnt[kPhmmBins], at[kPhmmBins];
+  for (int i = threadIdx.x; i < kPhmmBins; i += kBinBlock) cnt[i] = 0;
+  __syncthreads();
+  const long long base = (long long)blockIdx.x * (kBinBlock * kBinItems);
+  int bin[kBinItems];
+  uint32_t rank[kBinItems];
+  for (int k = 0; k < kBinItems; ++k) {
+    const long long p = base + (long long)k * kBinBlock + threadIdx.x;
+    bin[k] = p < b.n_pairs ? phmm_bin(b, p) : -1;
+    rank[k] = bin[k] >= 0 ? atomicAdd(&cnt[bin[k]], 1u) : 0u;
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < kPhmmBins; i += kBinBlock)
+    if (cnt[i]) at[i] = atomicAdd(&cursor[i], cnt[i]);  // this block's range of bin i
+  __syncthreads();
+  for (int k = 0; k < kBinItems; ++k)
+    if (bin[k] >= 0) idx[at[bin[k]] + rank[k]] = (int32_t)(base + (long long)k * kBinBlock + threadIdx.x);
 }
 
 // bounds[j] = first sorted position of launch class j; bounds[kPhmmLaunchClasses] = n.
@@ -503,6 +589,22 @@ int launch_phmm_keys(const PhmmDevBatch& b, uint32_t* keys, int32_t* idx, unsign
   const long long nb = (b.n_pairs + bs - 1) / bs;
   hipLaunchKernelGGL(phmm_keys_kernel, dim3((unsigned)nb), dim3(bs), 0, s, b, keys, idx, counters);
   FCS_HIP_CHECK(hipGetLastError());
+  return FCS_OK;
+}
+
+int launch_phmm_bin_schedule(const PhmmDevBatch& b, int32_t* idx_out, int64_t* bounds, unsigned long long* counters,
+                             uint32_t* hist, uint32_t* cursor, hipStream_t s) {
+  static_assert(kPhmmBins % kBinBlock == 0 && (kPhmmLaunchClasses << 8) <= kPhmmBins, "bins");
+  const long long n = b.n_pairs > 0 ? b.n_pairs : 0;
+  const unsigned nb = (unsigned)std::max<long long>((n + kBinBlock * kBinItems - 1) / (kBinBlock * kBinItems), 1);
+  hipLaunchKernelGGL(phmm_bin_count_kernel, dim3(nb), dim3(kBinBlock), 0, s, b, hist, counters);
+  FCS_HIP_CHECK(hipGetLastError());
+  hipLaunchKernelGGL(phmm_bin_scan_kernel, dim3(1), dim3(kBinBlock), 0, s, hist, cursor, n, bounds);
+  FCS_HIP_CHECK(hipGetLastError());
+  if (n > 0) {
+    hipLaunchKernelGGL(phmm_bin_scatter_kernel, dim3(nb), dim3(kBinBlock), 0, s, b, cursor, idx_out);
+    FCS_HIP_CHECK(hipGetLastError());
+  }
   return FCS_OK;
 }
 
