@@ -451,6 +451,7 @@ struct fcs_phmm_plan {
   int64_t* bounds = nullptr;
   uint32_t* bin_hist = nullptr;    // the bin schedule's histogram (kept zero between schedules)
   uint32_t* bin_cursor = nullptr;  // and its running bin starts
+  bool bin_zeroed = false;         // bin_hist zeroed on a schedule stream (then kept zero by the scan)
   int64_t scheduled = -1;  // n_pairs of the last schedule
   bool counters_zeroed = false;  // the last schedule's keys kernel zeroed rescue_count[0..1]
 };
@@ -623,8 +624,7 @@ int fcs_phmm_plan_create(int32_t device, int64_t max_pairs, fcs_phmm_plan** plan
   constexpr size_t kBins = (size_t)1 << (kPhmmKeyBits - 4);
   FCS_HIP_CHECK(hipMalloc(&p->bin_hist, 2 * kBins * sizeof(uint32_t)));
   p->bin_cursor = p->bin_hist + kBins;
-  FCS_HIP_CHECK(hipMemset(p->bin_hist, 0, kBins * sizeof(uint32_t)));  // before any stream uses the plan
-  *plan = p.release();
+  *plan = p.release();  // (the bin histogram is zeroed on the first schedule's stream)
   return FCS_OK;
 }
 
@@ -662,6 +662,13 @@ int fcs_phmm_dev_schedule(fcs_phmm_plan* plan, const fcs_phmm_batch* b, void* st
     return e && std::string(e) == "radix";
   }();
   if (!radix) {
+    // stream-ordered, once per plan: a synchronous hipMemset at plan creation
+    // waited behind other shards' kernels on the device (htc PairHMM call time
+    // 0.45 -> 2.2 thread-s in r5aw)
+    if (!plan->bin_zeroed) {
+      FCS_HIP_CHECK(hipMemsetAsync(plan->bin_hist, 0, ((size_t)1 << (kPhmmKeyBits - 4)) * sizeof(uint32_t), s));
+      plan->bin_zeroed = true;
+    }
     if ((rc = launch_phmm_bin_schedule(d, plan->idx_out, plan->bounds, plan->rescue_count, plan->bin_hist,
                                        plan->bin_cursor, s)))
       return rc;
