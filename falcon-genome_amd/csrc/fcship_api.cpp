@@ -191,6 +191,11 @@ SessionPool& session_pool(int device, int kind = kComputeSession) {
 }
 
 // A new session on `device` (the current device), or null.
+int64_t env_int(const char* name, int64_t dflt) {
+  const char* e = std::getenv(name);
+  return e && *e ? std::max<int64_t>(0, std::atoll(e)) : dflt;
+}
+
 Session* create_session(int device, int kind = kComputeSession) {
   auto* S = new Session();
   S->device = device;
@@ -198,6 +203,18 @@ Session* create_session(int device, int kind = kComputeSession) {
       (kind == kComputeSession && !fork_set(S->s))) {
     delete S;  // a failed stream is not reused; nothing else was created
     return nullptr;
+  }
+  // FCS_SESSION_PRESIZE_MB (default 24, 0 = off): a compute session starts
+  // with staging of that size and a PairHMM plan for FCS_SESSION_PRESIZE_PAIRS
+  // (default 120000), so the first passes of a run (an htc shard's pass is
+  // ~17 MB and ~90K pairs on the 30x panel) do not allocate pinned and device
+  // memory while other threads' passes are in flight; sessions are created by
+  // the warm-up, off the callers' path.  A failed presize only leaves the
+  // session to grow on demand.
+  static const size_t presize = (size_t)env_int("FCS_SESSION_PRESIZE_MB", 24) << 20;
+  static const int64_t presize_pairs = env_int("FCS_SESSION_PRESIZE_PAIRS", 120000);
+  if (kind == kComputeSession && presize > 0) {
+    (void)(S->ensure_host(presize) || S->ensure_dev(presize) || (presize_pairs > 0 && S->ensure_phmm(presize_pairs)));
   }
   return S;
 }
@@ -827,7 +844,14 @@ int phmm_staged(const PhmmStage& g, const fcs_phmm_opts& opts, SessionLease& lea
   int rc = check_device(opts.device);
   if (rc) return rc;
   FCS_SET_DEVICE((opts.device));
+  // FCS_PHMM_TRACE=1: one stderr line per call with its host-side phases (ms)
+  static const bool trace = std::getenv("FCS_PHMM_TRACE") != nullptr;
+  using clk = std::chrono::steady_clock;
+  const auto t0 = clk::now();
+  static const auto t_load = t0;  // the first call
+  auto ms = [](clk::time_point a, clk::time_point b) { return std::chrono::duration<double, std::milli>(b - a).count(); };
   if ((rc = lease.acquire(opts.device))) return rc;
+  const auto t_lease = clk::now();
   Session* S = lease.get();
   const size_t RB = (size_t)g.read_bytes, HB = (size_t)g.hap_bytes, nr = (size_t)g.n_reads, nh = (size_t)g.n_haps,
                np = (size_t)g.n_pairs;
@@ -842,8 +866,11 @@ int phmm_staged(const PhmmStage& g, const fcs_phmm_opts& opts, SessionLease& lea
   off[kPr] = L.add(4 * np);
   off[kPh] = L.add(4 * np);
   const size_t in_bytes = L.total, out_off = L.add(8 * np);
+  const bool grew = L.total > S->host_cap || L.total > S->dev_cap || !S->phmm || S->phmm->max_pairs < g.n_pairs;
   if ((rc = S->ensure_host(L.total)) || (rc = S->ensure_dev(L.total)) || (rc = S->ensure_phmm(g.n_pairs))) return rc;
+  const auto t_ensure = clk::now();
   fill(S, off);
+  const auto t_fill = clk::now();
   hipStream_t s = S->s;
   const StreamDrain drain{s};
   FCS_HIP_CHECK(hipMemcpyAsync(S->dev, S->host, in_bytes, hipMemcpyHostToDevice, s));
@@ -884,13 +911,21 @@ int phmm_staged(const PhmmStage& g, const fcs_phmm_opts& opts, SessionLease& lea
   g_last_rescued = 0;
   if (opts.use_fp64_rescue)
     FCS_HIP_CHECK(hipMemcpyAsync(hres, S->phmm->rescue_count, sizeof(*hres), hipMemcpyDeviceToHost, s));
+  const auto t_issue = clk::now();
   FCS_HIP_CHECK(hipStreamSynchronize(s));
+  const auto t_sync = clk::now();
   if (opts.use_fp64_rescue) g_last_rescued = (int64_t)*hres;
   float ms_all = 0.f, ms_res = 0.f;
   FCS_HIP_CHECK(hipEventElapsedTime(&ms_all, S->ev[0], S->ev[2]));
   FCS_HIP_CHECK(hipEventElapsedTime(&ms_res, S->ev[1], S->ev[2]));
   g_last_device_ms = ms_all;
   g_last_rescue_ms = ms_res;
+  if (trace)
+    std::fprintf(stderr,
+                 "[fcs_phmm_trace] at %.1f pairs %lld bytes %zu lease %.3f ensure %.3f%s fill %.3f issue %.3f sync %.3f "
+                 "device %.3f total %.3f\n",
+                 ms(t_load, t0), (long long)np, in_bytes, ms(t0, t_lease), ms(t_lease, t_ensure), grew ? " (grew)" : "",
+                 ms(t_ensure, t_fill), ms(t_fill, t_issue), ms(t_issue, t_sync), (double)ms_all, ms(t0, t_sync));
   int64_t missing = 0;
   for (size_t k = 0; k < np; ++k) missing += std::isnan(hout[k]);
   if (missing)
