@@ -358,24 +358,32 @@ __device__ __forceinline__ void glane_traceback(const GLayout& L, int qlen, int 
     // nibble row i; c past the row's band end reads 0, as bwa's zeroed bytes
     // there do; a column left of the row's band start indexes bwa's flat
     // matrix backwards into the rows above (row-major, n_col bytes a row)
-    int r = i, c = k - (i > w ? i - w : 0);
-    if (c < 0 || c >= n_col) {
-      const long long zi = (long long)i * n_col + c;
-      r = (zi < 0 || zi >= zsize) ? -1 : (int)(zi / n_col);
-      c = r < 0 ? 0 : (int)(zi - (long long)r * n_col);
+    // In band (|k - i| <= w; k < qlen always holds) the cell is slot
+    // k - i + w of nibble row i; only a path that left the band takes the
+    // general mapping below.
+    int r = i, kb = k - i + w;
+    bool have = (unsigned)kb <= (unsigned)(2 * w);
+    if (!have) {
+      int c = k - (i > w ? i - w : 0);
+      if (c < 0 || c >= n_col) {
+        const long long zi = (long long)i * n_col + c;
+        r = (zi < 0 || zi >= zsize) ? -1 : (int)(zi / n_col);
+        c = r < 0 ? 0 : (int)(zi - (long long)r * n_col);
+      }
+      if (r >= 0) {
+        const int beg = r > w ? r - w : 0, end = r + w + 1 < qlen ? r + w + 1 : qlen;
+        have = beg + c < end;
+        kb = beg + c - r + w;
+      }
     }
     uint32_t nb = 0;
-    if (r >= 0) {
-      const int beg = r > w ? r - w : 0, end = r + w + 1 < qlen ? r + w + 1 : qlen;
-      if (beg + c < end) {
-        const int kb = beg + c - r + w;
-        const int dw = kb >> 3;
-        if (r != crow || dw != cdw) {
-          crow = r, cdw = dw;
-          cval = L.base[(long long)r * L.rs + dw * L.ds];
-        }
-        nb = (cval >> (28 - 4 * (kb & 7))) & 15u;
+    if (have) {
+      const int dw = kb >> 3;
+      if (r != crow || dw != cdw) {
+        crow = r, cdw = dw;
+        cval = L.base[(long long)r * L.rs + dw * L.ds];
       }
+      nb = (cval >> (28 - 4 * (kb & 7))) & 15u;
     }
     which = which == 2 ? (int)((T2 >> (2 * nb)) & 3u) : (int)((T01 >> (32 * which + 2 * nb)) & 3u);
     // state M: diagonal (CIGAR M), E: up (D), F: left (I)
@@ -431,12 +439,20 @@ __device__ __forceinline__ uint32_t gbit(uint32_t acc, int x) {
   return r;
 }
 
+// a + b + c in one VALU instruction (the compiler splits a - b + c into two)
+__device__ __forceinline__ int add3(int a, int b, int c) {
+  int r;
+  asm("v_add3_u32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+  return r;
+}
+
 template <int NB, bool CIG>
 __device__ __forceinline__ void glane_row(int (&Hd)[NB], int (&Ed)[NB + 1], const uint32_t (&Qb)[(NB + 4) / 4],
                                           uint32_t (&nib)[(NB + 7) / 8], const int rowpack, const int oe_del,
                                           const int oe_ins, const int e_del, const int e_ins) {
   int f = kMinusInf;
   uint32_t acc = 0;
+  const int o_del = oe_del - e_del, neg_e_del = -e_del;
 #pragma unroll
   for (int k = 0; k < NB; ++k) {
     const int qoff = (int)((Qb[k >> 2] >> (8 * (k & 3))) & 0xFFu);
@@ -445,18 +461,24 @@ __device__ __forceinline__ void glane_row(int (&Hd)[NB], int (&Ed)[NB + 1], cons
     const int e0 = Ed[k + 1];
     const int h1 = max(m, e0);
     const int h = max(h1, f);
-    const int td = m - oe_del, ti = m - oe_ins;
-    const int e = e0 - e_del;
+    const int ti = m - oe_ins;
     const int fn = f - e_ins;
     if constexpr (CIG) {
+      // E from the two differences the direction bits need anyway:
+      // max(e0 - e_del, M - oe_del) = e0 - e_del + max(x, 0) with
+      // x = M - e0 - o_del, one instruction fewer than forming both terms
+      const int dme = m - e0;
+      const int x = dme - o_del;
       acc = gbit(acc, ti - fn);  // F-continue: f - e_ins > M - oe_ins
-      acc = gbit(acc, td - e);   // E-continue: e - e_del > M - oe_del
+      acc = gbit(acc, x);        // E-continue: e0 - e_del > M - oe_del
       acc = gbit(acc, h1 - f);   // max(M, E) < F: H from F
-      acc = gbit(acc, m - e0);   // M < E: H from E
+      acc = gbit(acc, dme);      // M < E: H from E
       if ((k & 7) == 7) nib[k >> 3] = acc;
+      Ed[k] = add3(e0, max(x, 0), neg_e_del);
+    } else {
+      Ed[k] = max(e0 - e_del, m - oe_del);
     }
     Hd[k] = h;
-    Ed[k] = max(e, td);
     f = max(fn, ti);
   }
   if constexpr (CIG && (NB & 7) != 0) nib[NB >> 3] = acc << (4 * (8 - (NB & 7)));  // the row's last cells to the top
