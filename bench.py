@@ -236,6 +236,7 @@ def shard_stats(logs, dt):
     st = {"regions": tot(r"(\d+) regions", int), "pairs": tot(r"(\d+) pairs", int),
           "cells": tot(r"(\d+) cells", int), "rescued_pairs": tot(r"(\d+) rescued", int),
           "device_passes": tot(r"(\d+) device passes", int),
+          "shards_run_while_device_came_up": tot(r"ran (\d+) queued shards", int),
           "seconds": round(dt, 3)}
     st["regions_per_s"] = round(st["regions"] / dt, 1)
     brk = {k: round(tot(pat), 3) for k, pat in (

@@ -51,6 +51,9 @@ void CallerStats::add(const CallerStats& o) {
   region_seconds += o.region_seconds;
   genotype_seconds += o.genotype_seconds;
   output_seconds += o.output_seconds;
+  helped_tasks += o.helped_tasks;
+  helped_seconds += o.helped_seconds;
+  helped_cpu_seconds += o.helped_cpu_seconds;
 }
 
 namespace {
@@ -912,9 +915,19 @@ CallerStats call_intervals(const Reference& ref, const std::vector<std::string>&
   const std::vector<Interval>& intervals = intervals_in;
   std::vector<std::unique_ptr<Region>> pending;
   std::vector<std::tuple<int64_t, int64_t, std::string>> own;  // per pending region: owned range + chrom
+  int64_t helped_faults = 0;
   auto flush = [&] {
     if (pending.empty()) return;
     if (interrupted()) throw interruptedError();
+    if (opt.help_while_cold) {
+      const uint64_t th = now_us();
+      const double ch = thread_cpu();
+      const int64_t fh = thread_faults();
+      while (opt.help_while_cold()) ++st.helped_tasks;
+      st.helped_seconds += (now_us() - th) / 1e6;
+      st.helped_cpu_seconds += thread_cpu() - ch;
+      helped_faults += thread_faults() - fh;
+    }
     run_phmm(pending, opt, st, dump);
     const uint64_t tg = now_us();
     for (size_t i = 0; i < pending.size(); ++i) {
@@ -1010,7 +1023,8 @@ CallerStats call_intervals(const Reference& ref, const std::vector<std::string>&
       for (const Read& rd : reads[s]) max_span[s] = std::max<int64_t>(max_span[s], rd.end - rd.pos);
     const uint64_t tr = now_us();
     const int64_t fr = thread_faults();
-    const double in_flush0 = st.phmm_seconds + st.genotype_seconds;
+    const double in_flush0 = st.phmm_seconds + st.genotype_seconds + st.helped_seconds;
+    const int64_t hf0 = helped_faults;
     for (const auto& [first, last] : clusters) {
       for (int64_t rb = std::max<int64_t>(0, first - opt.padding); rb < std::min<int64_t>(L, last + opt.padding + 1);
            rb += opt.max_region) {
@@ -1069,9 +1083,10 @@ CallerStats call_intervals(const Reference& ref, const std::vector<std::string>&
         if ((int)pending.size() >= opt.batch_regions) flush();
       }
     }
-    st.region_seconds += (now_us() - tr) / 1e6 - (st.phmm_seconds + st.genotype_seconds - in_flush0);
+    st.region_seconds +=
+        (now_us() - tr) / 1e6 - (st.phmm_seconds + st.genotype_seconds + st.helped_seconds - in_flush0);
     flush();
-    st.faults[2] += thread_faults() - fr;
+    st.faults[2] += thread_faults() - fr - (helped_faults - hf0);
     if (opt.gvcf && !opt.somatic) {
       const uint64_t tv = now_us();
       const int64_t fv = thread_faults();
@@ -1125,8 +1140,8 @@ CallerStats call_intervals(const Reference& ref, const std::vector<std::string>&
   }
   st.output_seconds += (now_us() - tw) / 1e6;
   st.faults[3] += thread_faults() - fw;
-  st.seconds = (now_us() - t0) / 1e6;
-  st.cpu_seconds = thread_cpu() - cpu0;
+  st.seconds = (now_us() - t0) / 1e6 - st.helped_seconds;
+  st.cpu_seconds = thread_cpu() - cpu0 - st.helped_cpu_seconds;
   return st;
 }
 

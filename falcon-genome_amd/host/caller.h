@@ -15,6 +15,7 @@
 #pragma once
 
 #include <cstdint>
+#include <functional>
 #include <string>
 #include <vector>
 
@@ -49,6 +50,10 @@ struct CallerOptions {
   // window BAM blocks through fcs_bgzf_inflate (BgzfReader::use_device); off by
   // default: at the htc shard shape the host's libdeflate is faster
   bool gpu_inflate = false;
+  // called before each PairHMM pass until it returns false: while the device
+  // is still coming up it runs another queued shard on this thread
+  // (gpu.warmup_help; set by the shard workers, empty elsewhere)
+  std::function<bool()> help_while_cold;
   double min_qual = 30.0;  // stand_call_conf
   double tlod = 6.3, nlod = 2.2;
   std::string dump_path;  // if set: append every region's PairHMM inputs/outputs here (tests)
@@ -70,6 +75,10 @@ struct CallerStats {
   int64_t faults[4] = {0, 0, 0, 0};
   // device time of the PairHMM calls (HIP events: schedule + forward + rescue) and of the fp64 rescue alone
   double phmm_device_seconds = 0, rescue_device_seconds = 0;
+  // other shards run on this thread while the device came up (help_while_cold):
+  // their wall and CPU time, left out of this shard's figures above
+  int64_t helped_tasks = 0;
+  double helped_seconds = 0, helped_cpu_seconds = 0;
   void add(const CallerStats& o);
 };
 

@@ -124,6 +124,30 @@ void Executor::stop() {
   pool_.clear();
 }
 
+namespace {
+std::atomic<Executor*> g_running{nullptr};
+std::atomic<bool> g_devices_warm{false};
+}  // namespace
+
+bool executor_help_once() {
+  Executor* ex = g_running.load();
+  return ex && ex->try_run_one();
+}
+void set_devices_warm(bool warm) { g_devices_warm.store(warm); }
+bool devices_warm() { return g_devices_warm.load(); }
+
+bool Executor::try_run_one() {
+  std::function<void()> fn;
+  {
+    std::lock_guard<std::mutex> g(mu_);
+    if (stopping_ || q_.empty()) return false;
+    fn = std::move(q_.front());
+    q_.pop();
+  }
+  fn();
+  return true;
+}
+
 void Executor::post(std::function<void()> fn) {
   {
     std::lock_guard<std::mutex> g(mu_);
@@ -142,6 +166,14 @@ void Executor::addTask(Worker_ptr w, const std::string& sample_id, bool wait_for
 }
 
 void Executor::run() {
+  struct Running {
+    Executor* self;
+    explicit Running(Executor* e) : self(e) { g_running.store(e); }
+    ~Running() {
+      Executor* e = self;
+      g_running.compare_exchange_strong(e, nullptr);
+    }
+  } running(this);
   while (!stages_.empty()) {
     stages_.front()->run();
     stages_.pop();

@@ -74,6 +74,14 @@ class Stage {
 };
 typedef std::shared_ptr<Stage> Stage_ptr;
 
+// Runs one task still queued on the running Executor on the calling thread;
+// false when none is queued (or no Executor runs).  A shard that would block
+// for a device still coming up does other shards' host work meanwhile.
+bool executor_help_once();
+// Set by the device warm-up once the GPU runtime and sessions are up.
+void set_devices_warm(bool warm);
+bool devices_warm();
+
 class Executor {
  public:
   Executor(std::string job_name, int num_executors = 1, std::vector<int> gpus = {});
@@ -82,6 +90,7 @@ class Executor {
   void run();
   int execute(Worker_ptr w, const std::string& log);
   void post(std::function<void()> fn);
+  bool try_run_one();
   std::string get_log_name(const std::string& label, int idx = -1);
   const std::string& job_name() const { return job_name_; }
   int num_executors() const { return num_executors_; }

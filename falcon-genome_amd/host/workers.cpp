@@ -2,6 +2,7 @@
 
 #include <algorithm>
 #include <cstdio>
+#include <cstdlib>
 #include <iostream>
 #include <map>
 #include <mutex>
@@ -45,6 +46,10 @@ CallerOptions caller_options_from_config(int gpu) {
   o.combine_ms = c.get_int("gpu.phmm.combine_ms");
   o.fp64_rescue = c.get_bool("gpu.phmm.rescue");
   o.gpu_inflate = c.get_bool("gpu.bam_inflate");
+  // (merged passes wait for every active shard's pass: a shard run inside
+  // another's flush would hold that pass back, so no help then)
+  if (c.get_bool("gpu.warmup_help") && o.combine_ms == 0)
+    o.help_while_cold = [] { return !devices_warm() && executor_help_once(); };
   o.tlod = std::stod(c.get_string("mutect2.tlod"));
   o.nlod = std::stod(c.get_string("mutect2.nlod"));
   if (o.padding < 0 || o.max_region < 1 || o.batch_regions < 1 || o.max_reads_per_region < 1 || o.combine_ms < 0)
@@ -110,7 +115,7 @@ int HTCWorker::run(TaskContext& ctx) {
                  "[fcs-genome htc] shard %d gpu %d: %lld reads, %lld regions, %lld pairs, %lld cells, %lld rescued, "
                  "%lld calls, %.3f s (PairHMM %.3f s, device %.4f s, rescue %.4f s, %lld device passes; decode %.3f s "
                  "(%lld passes, inflate %lld gpu / %lld host chunks), pileup %.3f s, regions %.3f s, genotype %.3f s, output %.3f s; thread cpu %.3f s, "
-                 "minor faults %lld/%lld/%lld/%lld)\n",
+                 "minor faults %lld/%lld/%lld/%lld; ran %lld queued shards in %.3f s while the device came up)\n",
                  contig_, ctx.gpu, (long long)stats_.reads, (long long)stats_.regions, (long long)stats_.pairs,
                  (long long)stats_.cells, (long long)stats_.rescued, (long long)stats_.calls, stats_.seconds,
                  stats_.phmm_seconds, stats_.phmm_device_seconds, stats_.rescue_device_seconds,
@@ -118,7 +123,7 @@ int HTCWorker::run(TaskContext& ctx) {
                  (long long)stats_.inflate_gpu_chunks, (long long)stats_.inflate_host_chunks, stats_.pileup_seconds,
                  stats_.region_seconds, stats_.genotype_seconds, stats_.output_seconds, stats_.cpu_seconds,
                  (long long)stats_.faults[0], (long long)stats_.faults[1], (long long)stats_.faults[2],
-                 (long long)stats_.faults[3]);
+                 (long long)stats_.faults[3], (long long)stats_.helped_tasks, stats_.helped_seconds);
   return 0;
 }
 
@@ -297,6 +302,9 @@ int DeviceWarmupWorker::run(TaskContext&) {
   // are ready inflate on their own threads)
   for (int d : gpus_)
     if (fcs_device_warmup(d, 0) != FCS_OK) return 1;
+  // FCS_TEST_COLD_DEVICE=1 (tests): the devices never count as warm, so every
+  // shard's pass first runs the queued shards (tests/test_c1_cpu.py)
+  if (!std::getenv("FCS_TEST_COLD_DEVICE")) set_devices_warm(true);
   if (conf().get_bool("gpu.bam_inflate"))
     for (int d : gpus_)
       if (fcs_bgzf_warmup(d, 8, (int64_t)112 << 20) != FCS_OK) return 1;

@@ -125,3 +125,37 @@ def test_window_inflate_chunks_cross_members(mock_dir, tmp_path):
         outs.append([ln for ln in open(out) if not ln.startswith("##")])
     assert len(outs[0]) > 20
     assert outs[0] == outs[1] == outs[2]
+
+
+def test_shards_run_while_device_comes_up(mock_dir, tmp_path):
+    """gpu.warmup_help: a shard whose PairHMM pass finds the device not yet
+    warm runs queued shards on its own thread first.  With the device held
+    cold for the whole run (FCS_TEST_COLD_DEVICE) every pass nests the queued
+    shards; the GVCF and the somatic VCF are byte-identical to the plain
+    schedule's, and the shard logs count the nested shards."""
+    import glob
+    import re
+    d = tmp_path / "in"
+    p = H.run_cli("synth", "-o", d, "-c", "chrA:300000,chrB:120000", "-x", "12", "--tumor", "--no-fastq",
+                  "--seed", "11")
+    assert p.returncode == 0, p.stderr[-2000:]
+    res = {}
+    for name, env in (("cold", {"FCS_TEST_COLD_DEVICE": "1"}), ("plain", {"FCS_GPU_WARMUP_HELP": "false"})):
+        e = {"LD_LIBRARY_PATH": mock_dir, "FCS_GPU_DEVICES": "0", "FCS_MOCK_PHMM": "gkl", "FCS_GATK_NPROCS": "2",
+             "FCS_LOG_DIR": str(tmp_path / f"log_{name}"), **env}
+        h = tmp_path / f"{name}.g.vcf"
+        p = H.run_cli("htc", "-f", "-r", d / "ref.fasta", "-i", d / "sample.bam", "-o", h, env=e, cwd=tmp_path)
+        assert p.returncode == 0, p.stderr[-3000:]
+        m = tmp_path / f"{name}.m2.vcf"
+        p = H.run_cli("mutect2", "-f", "-r", d / "ref.fasta", "-n", d / "sample.bam", "-t", d / "tumor.bam",
+                      "-o", m, env=e, cwd=tmp_path)
+        assert p.returncode == 0, p.stderr[-3000:]
+        logs = "".join(open(f).read() for f in glob.glob(str(tmp_path / f"log_{name}" / "*.log")))
+        nested = sum(int(x) for x in re.findall(r"ran (\d+) queued shards", logs))
+        body = lambda f: [ln for ln in open(f) if not ln.startswith("##")]  # noqa: E731
+        res[name] = (body(h), body(m), nested)
+    assert len(res["plain"][0]) > 100 and len(res["plain"][1]) > 1
+    assert res["cold"][0] == res["plain"][0]
+    assert res["cold"][1] == res["plain"][1]
+    assert res["plain"][2] == 0
+    assert res["cold"][2] > 0
