@@ -50,7 +50,7 @@ void Config::init(const std::string& root_dir) {
   declare("gpu.phmm.rescue", "true", "fp64 rescue of pairs whose fp32 likelihood underflows (GKL)");
   declare("gpu.release_early", "true",
           "release the GPUs beside the VCF tail once the callers are done (their teardown off the critical path)");
-  declare("gpu.warmup_help", "true",
+  declare("gpu.warmup_help", "false",
           "a shard whose PairHMM pass finds the GPU runtime still coming up runs a queued shard meanwhile");
   declare("gpu.bam_inflate", "false",
           "inflate a calling window's BAM blocks on the GPU (fcs_bgzf_inflate) instead of host libdeflate");

@@ -140,7 +140,8 @@ def test_shards_run_while_device_comes_up(mock_dir, tmp_path):
                   "--seed", "11")
     assert p.returncode == 0, p.stderr[-2000:]
     res = {}
-    for name, env in (("cold", {"FCS_TEST_COLD_DEVICE": "1"}), ("plain", {"FCS_GPU_WARMUP_HELP": "false"})):
+    for name, env in (("cold", {"FCS_TEST_COLD_DEVICE": "1", "FCS_GPU_WARMUP_HELP": "true"}),
+                      ("plain", {"FCS_GPU_WARMUP_HELP": "false"})):
         e = {"LD_LIBRARY_PATH": mock_dir, "FCS_GPU_DEVICES": "0", "FCS_MOCK_PHMM": "gkl", "FCS_GATK_NPROCS": "2",
              "FCS_LOG_DIR": str(tmp_path / f"log_{name}"), **env}
         h = tmp_path / f"{name}.g.vcf"
