@@ -18,6 +18,12 @@ torch.distributed carries only the barrier and the max-over-ranks timing
 reduction.  `--dry-run` runs the same rank/launcher/reduction path on CPU
 (gloo) with a stand-in workload, for the CPU tests.
 
+C4 / C5 (configs[3], configs[4]) as the reference runs them: ONE `fcs-genome
+htc` job and ONE `fcs-genome mutect2` job over a chr1-sized genome (--c4-mbp,
+248 Mbp, the same at every N), their 32 interval shards dealt over all N GPUs
+of the node; at N = 1 beside each job's CPU PairHMM path.  The line ends with
+`summary`, every headline figure in one short block.
+
 Also reported (not the headline): banded-SW ksw_extend2 GCUPS on C3-shaped
 synthetic extension tasks (2x151 bp reads, bwa defaults) and on the fixed
 qlen=151/tlen=251 variant, cells counted by the kernel exactly as ksw_extend2
@@ -43,6 +49,12 @@ VALU_LANE_INSTR_PEAK = 256 * 4 * 32 * 2.4e9  # lane-instructions/s: one wave64 V
 FP32_VECTOR_PEAK_TF = 157.3  # MI355X_MICROARCH.md chip table (spec)
 HBM_PEAK_GBS = 8000.0
 SW_OPS_PER_CELL = 12         # BASELINE.md §3 / SURVEY §8d: ~12 int ops per ksw_extend2 cell
+
+
+def progress(msg):
+    """A progress line on stderr (a long bench run keeps showing signs of life;
+    stdout carries only the JSON line)."""
+    print(f"[bench {time.strftime('%H:%M:%S')}] {msg}", file=sys.stderr, flush=True)
 
 
 def phmm_dev_batch(p: "fcship.PhmmPairs", dev):
@@ -402,35 +414,59 @@ def align_report(err):
             "proper_pair_reads": int(pm.group(1)), "mates_rescued": int(pm.group(2))}
 
 
-def bench_c4(exe, env, work, mbp, n_dev, seed, nprocs, reps=1):
-    """BASELINE.json configs[3] (C4) as the reference runs it: ONE
-    `fcs-genome htc` job over a 30x chr1-like genome (mbp Mbp; 248 is chr1),
-    its gatk.ncontigs = 32 interval shards in one stage
-    (/root/reference/src/worker-htc.cpp:113-145, the shard unit of
+def synth_job_genome(exe, env, d, mbp, seed, tumor=True):
+    """The C4/C5 input: a chr1-like genome of mbp Mbp (248 is chr1), a 30x
+    sample BAM and, with tumor, a 40x tumor BAM (+1e-4 somatic); 1% of the
+    reads mis-mapped-like, so the fp64 rescue fires.  Returns seconds."""
+    import subprocess
+    t0 = time.perf_counter()
+    subprocess.run([exe, "synth", "-o", d, "-c", f"chr1:{int(mbp * 1e6)}", "-x", "30", "--no-fastq", "--noisy-frac",
+                    "0.01", "--seed", str(seed)] + (["--tumor"] if tumor else []), env=env, check=True,
+                   capture_output=True)
+    return time.perf_counter() - t0
+
+
+JOB_TOOLS = {
+    # tool -> (config, Stage name, reference driver)
+    "htc": ("C4", "Haplotype Caller", "/root/reference/src/worker-htc.cpp:113-145"),
+    "mutect2": ("C5", "Mutect2", "/root/reference/src/worker-mutect2.cpp:167-201"),
+}
+
+
+def job_cmd(tool, d, out):
+    """The fcs-genome command line of one C4 (htc, GVCF) or C5 (mutect2
+    tumor/normal) job over the genome directory d."""
+    if tool == "htc":
+        return ["htc", "-f", "-r", d + "/ref.fasta", "-i", d + "/sample.bam", "-o", out]
+    return ["mutect2", "-f", "-r", d + "/ref.fasta", "-t", d + "/tumor.bam", "-n", d + "/sample.bam", "-o", out]
+
+
+def bench_job(exe, env, work, d, tool, mbp, n_dev, nprocs, reps=1):
+    """BASELINE.json configs[3] (C4: htc) or configs[4] (C5: mutect2) as the
+    reference runs them: ONE fcs-genome job over the genome in d, its
+    gatk.ncontigs = 32 interval shards in one stage (the reference's one
+    Executor per job, JOB_TOOLS[tool][2]; the shard unit of
     src/config.cpp:470-509) dealt round-robin to the GPU slots 0..n_dev-1
     (gpu.devices[job_id % n], the host round-robin of src/Executor.cpp:262),
     nprocs shard threads.  Returns the shard statistics, wall time and the
-    per-device pass counts."""
+    per-device shard counts; the job's output is work/<c4|c5>.<ext>."""
     import re
     import shutil
     import subprocess
-    d = os.path.join(work, "c4")
-    t0 = time.perf_counter()
-    subprocess.run([exe, "synth", "-o", d, "-c", f"chr1:{int(mbp * 1e6)}", "-x", "30", "--no-fastq", "--noisy-frac",
-                    "0.01", "--seed", str(seed)], env=env, check=True, capture_output=True)
-    synth_s = time.perf_counter() - t0
-    logd = os.path.join(work, "log_c4")
+    cfg, stage, _ = JOB_TOOLS[tool]
+    tag = cfg.lower()
+    logd = os.path.join(work, "log_" + tag)
     e = dict(env, FCS_GPU_DEVICES=",".join(str(i) for i in range(n_dev)), FCS_LOG_DIR=logd,
              FCS_GATK_NPROCS=str(nprocs))
+    out = os.path.join(work, tag + (".g.vcf" if tool == "htc" else ".vcf"))
     runs = []
     for _ in range(max(1, reps)):
         shutil.rmtree(logd, ignore_errors=True)
         t0 = time.perf_counter()
-        r = subprocess.run([exe, "htc", "-f", "-r", d + "/ref.fasta", "-i", d + "/sample.bam", "-o",
-                            work + "/c4.g.vcf"], env=e, capture_output=True, text=True, cwd=work)
+        r = subprocess.run([exe, *job_cmd(tool, d, out)], env=e, capture_output=True, text=True, cwd=work)
         dt = time.perf_counter() - t0
         if r.returncode != 0:
-            raise RuntimeError(f"C4 htc failed ({r.returncode}): {r.stderr[-2000:]}")
+            raise RuntimeError(f"{cfg} {tool} failed ({r.returncode}): {r.stderr[-2000:]}")
         logs = "".join(open(os.path.join(logd, f)).read() for f in os.listdir(logd) if ".part-" not in f)
         runs.append((dt, logs, r.stderr))
     dt, logs, err = min(runs, key=lambda x: x[0])
@@ -439,14 +475,31 @@ def bench_c4(exe, env, work, mbp, n_dev, seed, nprocs, reps=1):
     st["devices"] = n_dev
     st["shard_threads"] = nprocs
     st["genome_mbp"] = mbp
-    st["synth_seconds"] = round(synth_s, 1)
-    st["shards_per_device"] = {str(k): len(re.findall(rf"gpu {k}\b", logs)) for k in range(n_dev)}
-    m = re.search(r"Haplotype Caller finishes in ([\d.]+) seconds", err)
+    st["shards_per_device"] = {str(k): len(re.findall(rf"\] shard \d+ gpu {k}\b", logs)) for k in range(n_dev)}
+    m = re.search(stage + r" finishes in ([\d.]+) seconds", err)
     st["caller_stage_seconds"] = float(m.group(1)) if m else None
-    st["workload"] = (f"C4: one fcs-genome htc (GVCF) over a {mbp:g} Mbp chr1-like genome at 30x, 32 interval "
-                      f"shards dealt to {n_dev} GPU slot(s), {nprocs} shard threads")
-    shutil.rmtree(d, ignore_errors=True)
+    st["calls"] = len(vcf_calls(out))
+    st["output"] = out
+    st["workload"] = (f"{cfg}: one fcs-genome {tool} " + ("(GVCF) over a " if tool == "htc" else "(tumor 40x / normal "
+                      "30x) over a ") + f"{mbp:g} Mbp chr1-like genome, 32 interval shards dealt to {n_dev} GPU "
+                      f"slot(s), {nprocs} shard threads")
     return st
+
+
+def bench_c4(exe, env, work, mbp, n_dev, seed, nprocs, reps=1, tools=("htc",)):
+    """One genome synthesised (tumor BAM too when mutect2 is asked for), then
+    one bench_job per tool on it; {tool: stats}.  The genome is removed."""
+    import shutil
+    d = os.path.join(work, "c4")
+    synth_s = synth_job_genome(exe, env, d, mbp, seed, tumor="mutect2" in tools)
+    try:
+        out = {}
+        for t in tools:
+            out[t] = bench_job(exe, env, work, d, t, mbp, n_dev, nprocs, reps)
+            out[t]["synth_seconds"] = round(synth_s, 1)
+        return out
+    finally:
+        shutil.rmtree(d, ignore_errors=True)
 
 
 def bench_c1(exe, env, work, seed):
@@ -558,6 +611,7 @@ def bench_e2e(args, rank, local):
         if cpu_htc:  # the reference's CPU path beside it, on the same genome (rank 0, N=1 only)
             out["htc"]["cpu_baseline"] = htc_cpu_baseline(exe, env, work, d + "/ref.fasta", d + "/sample.bam",
                                                           work + "/htc.g.vcf")
+        progress("e2e: mutect2")
         m2_cmd = lambda o: ["mutect2", "-f", "-r", d + "/ref.fasta", "-t", d + "/tumor.bam", "-n",  # noqa: E731
                             d + "/sample.bam", "-o", o]
         (dt, logs, err), runs = best("mutect2", m2_cmd(work + "/m2.vcf"))
@@ -569,13 +623,16 @@ def bench_e2e(args, rank, local):
         if cpu_htc:  # C5's CPU path: GATK Mutect2 with the CPU PairHMM, same command and genome
             out["mutect2"]["cpu_baseline"] = caller_cpu_baseline(exe, env, work, m2_cmd, work + "/m2.vcf",
                                                                  tag="c5", ext=".vcf")
+        progress("e2e: BGZF inflate")
         try:
             out["bgzf"] = bench_bgzf(d + "/sample.bam", local, cpu_htc)
         except Exception as e:  # reported, not fatal to the e2e line
             out["bgzf"] = {"error": repr(e)[:300]}
         shutil.rmtree(d, ignore_errors=True)
         if cpu_htc:
+            progress("e2e: C1")
             out["c1"] = bench_c1(exe, env, work, args.seed + rank)
+        progress("e2e: align")
         La = int(args.e2e_align_mbp * 1e6)
         subprocess.run([exe, "synth", "-o", work + "/a", "-c", f"chr1:{La}", "-x", "30", "--no-fastq", "--paired",
                         "350", "--seed", str(args.seed + rank)], env=env, check=True, capture_output=True)
@@ -683,19 +740,58 @@ def bench_bgzf(bam, dev_index, cpu, reps=3):
     return r
 
 
-def run_c4(args, n_dev):
-    """bench_c4 on this node's n_dev GPUs, in a scratch directory (rank 0)."""
+def run_jobs(args, n_dev, cpu):
+    """C4 (one htc job) and C5 (one mutect2 job) over ONE genome of
+    --c4-mbp (248 = chr1) on this node's n_dev GPUs, in a scratch directory
+    (rank 0).  The genome does not depend on N, so the N = 1 run is the anchor
+    of the same job at 2/4/8 GPUs (strong scaling of the job).  With cpu (N = 1
+    only) each job also runs on the reference's CPU PairHMM path (GKL-style
+    AVX-512 through tests/cpu_mock, the same command, shards and threads) and
+    the calls are compared."""
     import shutil
     import tempfile
     exe = os.path.join(ROOT, "falcon-genome_amd", "bin", "fcs-genome")
     work = tempfile.mkdtemp(prefix="fcs-c4-")
     quota = host_cpu_quota()
     env = dict(os.environ, FCS_TEMP_DIR=work, FCS_HOST_THREADS=str(quota))
+    nprocs = min(32, quota)
+    d = os.path.join(work, "g")
     try:
-        return bench_c4(exe, env, work, min(args.e2e_mbp * n_dev, 248.0), n_dev, args.seed + 4242, min(32, quota),
-                        reps=args.e2e_reps)
+        progress(f"C4/C5: synthesising a {args.c4_mbp:g} Mbp genome (30x sample, 40x tumor)")
+        synth_s = synth_job_genome(exe, env, d, args.c4_mbp, args.seed + 4242, tumor=True)
+        progress(f"C4/C5: genome ready in {synth_s:.1f} s")
+        out = {}
+        for tool in ("htc", "mutect2"):
+            cfg = JOB_TOOLS[tool][0].lower()
+            st = bench_job(exe, env, work, d, tool, args.c4_mbp, n_dev, nprocs, reps=args.c4_reps)
+            st["synth_seconds"] = round(synth_s, 1)
+            progress(f"{cfg}: {tool} on {n_dev} GPU(s) {st['seconds']:.2f} s")
+            if cpu:
+                cb = caller_cpu_baseline(exe, dict(env, FCS_GATK_NPROCS=str(nprocs)), work,
+                                         lambda o, t=tool: job_cmd(t, d, o), st["output"], modes=("gkl",), tag=cfg,
+                                         ext=".g.vcf" if tool == "htc" else ".vcf")["gkl"]
+                st["cpu_baseline"] = cb
+                st["speedup_vs_cpu_path"] = round(cb["seconds"] / st["seconds"], 3)
+                progress(f"{cfg}: {tool} on the CPU path {cb['seconds']:.2f} s")
+            st.pop("output")
+            out[cfg] = st
+        return out
     finally:
         shutil.rmtree(work, ignore_errors=True)
+
+
+def job_summary(st):
+    """The compact figures of a C4/C5 block for the line's summary."""
+    s = {k: st.get(k) for k in ("genome_mbp", "devices", "seconds", "runs_seconds", "regions", "regions_per_s",
+                                "caller_stage_seconds", "shards_per_device", "calls", "rescued_pairs",
+                                "gpu_busy_frac")}
+    cb = st.get("cpu_baseline")
+    if cb:
+        s["cpu_baseline"] = {"seconds": cb["seconds"], "regions_per_s": cb["regions_per_s"], "cores": cb["cores"],
+                             "kind": cb["kind"], "pairhmm": "GKL-style AVX-512", "calls_equal_to_gpu":
+                             cb["calls_equal_to_gpu"]}
+        s["speedup_vs_cpu_path"] = st.get("speedup_vs_cpu_path")
+    return s
 
 
 def host_cpu_quota():
@@ -1042,7 +1138,10 @@ def main():
     ap.add_argument("--e2e-reps", type=int, default=3,
                     help="runs of each e2e command; the fastest is reported, every run's wall time listed")
     ap.add_argument("--no-c4", action="store_true",
-                    help="N > 1: skip the C4 leg (one htc job over N x --e2e-mbp, dealt to all N GPUs)")
+                    help="skip the C4 / C5 legs (one htc and one mutect2 job over --c4-mbp, dealt to all N GPUs)")
+    ap.add_argument("--c4-mbp", type=float, default=248.0,
+                    help="genome of the C4 / C5 jobs (248 Mbp = chr1), the same at every N")
+    ap.add_argument("--c4-reps", type=int, default=1, help="runs of each C4 / C5 job; the fastest is reported")
     args = ap.parse_args()
 
     if "WORLD_SIZE" not in os.environ and (args.gpus or 1) > 1:
@@ -1056,6 +1155,7 @@ def main():
         return dry_main(args, rk)
     load_fcship()
 
+    progress("C2 PairHMM")
     ph = bench_phmm(args, dev, rk)
     total_cells = ph["cells"] * world * args.steps
     value = total_cells / ph["elapsed"] / 1e9
@@ -1118,6 +1218,7 @@ def main():
     }
 
     if not args.no_bsw and rank == 0:
+        progress("C3 / ksw_global2 / ksw_align2")
         c3 = fcship.synth_bsw(args.seed, args.bsw_reads, read_len=151, ref_len=10_000_000, w=100)
         fx = fcship.synth_bsw(args.seed, max(1, args.bsw_reads * 2), read_len=151, ref_len=10_000_000, w=100,
                               mode=1, fixed_q=151, fixed_t=251)
@@ -1204,10 +1305,12 @@ def main():
                 cpu_baseline_bsw_align(al, g16, x16, min(args.cpu_budget, 4.0), cpu_threads())
 
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        progress("C2 CPU baseline and parity")
         line["cpu_baseline"], ref, used_d = cpu_baseline_phmm(p, args.cpu_budget, cpu_threads())
         line["parity"] = phmm_parity(ph["out"], ref, used_d)
 
     if not args.no_e2e:
+        progress("e2e htc / mutect2 / align")
         e2e = bench_e2e(args, rank, local)
         if world > 1:  # whole-job rates: units of all ranks over the slowest rank's time
             for k, unit in (("htc", "regions"), ("mutect2", "regions"), ("align", "reads")):
@@ -1218,20 +1321,71 @@ def main():
                 e2e[k]["seconds"] = round(slow, 3)
                 e2e[k][unit + "_per_s"] = round(tot / slow, 1)
             e2e["n_gpus"] = world
-        if world > 1 and not args.no_c4:
-            # C4 as the reference runs it: ONE htc job over a genome of N x the
-            # per-GPU share (248 Mbp = chr1 at 8 GPUs), its 32 shards dealt to
-            # all N GPUs of the node by the job's own Executor.  Rank 0 runs it
-            # while the other ranks wait; their GPUs serve the job's slots.
-            rk.barrier()
-            if rank == 0:
-                e2e["c4"] = run_c4(args, int(os.environ.get("LOCAL_WORLD_SIZE", str(world))))
-            rk.barrier()
         line["e2e"] = e2e
 
+    if not args.no_c4:
+        # C4 / C5 as the reference runs them: ONE htc and ONE mutect2 job over
+        # a --c4-mbp genome (chr1's 248 Mbp by default, the same at every N),
+        # their 32 shards dealt to all N GPUs of the node by the job's own
+        # Executor.  Rank 0 runs them while the other ranks wait; their GPUs
+        # serve the jobs' slots.  At N = 1 each job's CPU path runs beside it.
+        rk.barrier()
+        if rank == 0:
+            jobs = run_jobs(args, int(os.environ.get("LOCAL_WORLD_SIZE", str(world))),
+                            cpu=world == 1 and not args.no_cpu_baseline)
+            line.update(jobs)
+        rk.barrier()
+
     if rank == 0:
+        # the driver keeps only the tail of stdout: the long e2e block first,
+        # then the SW and parity blocks, then one compact summary of every figure
+        for k in ("bsw", "parity", "c4", "c5"):
+            if k in line:
+                line[k] = line.pop(k)
+        line["summary"] = summary(line)
         print(json.dumps(line), flush=True)
     rk.close()
+
+
+def summary(line):
+    """Every headline figure of the line in one short block (the end of the
+    line is what the driver's record keeps)."""
+    s = {"c2_gcups": line["value"], "c2_roofline_frac": line["roofline"]["frac"]}
+    if "parity" in line:
+        p = line["parity"]
+        s["c2_parity"] = {"n": p["n"], "max_rel_err": p["max_rel_err"], "pass": p["pass"]}
+    b = line.get("bsw")
+    if b:
+        s["c3_gcups"] = b["c3_gcups"]
+        s["c3_fixed_gcups"] = b["fixed_151x251_gcups"]
+        s["global_scores_gcups"] = b["global"]["scores_gcups"]
+        s["global_cigar_gcups"] = b["global"]["cigar_gcups"]
+        s["align_u8_gcups"] = b["align"]["gcups"]
+        s["align_i16_gcups"] = b["align"]["i16"]["gcups"]
+        if "parity" in b:
+            s["c3_parity"] = {k: b["parity"][k] for k in ("n", "bit_exact", "pass")}
+            s["align_parity"] = {k: b["align"]["parity"][k] for k in ("n", "bit_exact", "pass")}
+            s["align_i16_parity"] = {k: b["align"]["i16"]["parity"][k] for k in ("n", "bit_exact", "pass")}
+    e = line.get("e2e", {})
+    for k in ("htc", "mutect2"):
+        if k in e:
+            x = {"seconds": e[k]["seconds"], "runs_seconds": e[k]["runs_seconds"],
+                 "regions_per_s": e[k]["regions_per_s"]}
+            cb = e[k].get("cpu_baseline", {}).get("gkl")
+            if cb:
+                x["cpu_gkl_seconds"] = cb["seconds"]
+                x["calls_equal"] = cb["calls_equal_to_gpu"]
+            s["e2e_" + k] = x
+    if "align" in e:
+        s["e2e_align"] = {"seconds": e["align"]["seconds"], "reads_per_s": e["align"]["reads_per_s"],
+                          "mates_rescued": e["align"]["mates_rescued"]}
+        if "cpu_baseline" in e["align"]:
+            s["e2e_align"]["cpu_seconds"] = e["align"]["cpu_baseline"]["seconds"]
+            s["e2e_align"]["bam_equal"] = e["align"]["cpu_baseline"]["bam_equal_to_gpu"]
+    for k in ("c4", "c5"):
+        if k in line:
+            s[k] = job_summary(line[k])
+    return s
 
 
 def dry_main(args, rk):

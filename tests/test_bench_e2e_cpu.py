@@ -29,17 +29,33 @@ def mock_env():
     return env
 
 
-def test_c4_leg_deals_32_shards_over_slots(mock_env, tmp_path):
-    w1, w2 = tmp_path / "one", tmp_path / "two"
-    w1.mkdir()
-    w2.mkdir()
-    one = bench.bench_c4(H.BIN, dict(mock_env, FCS_TEMP_DIR=str(w1)), str(w1), 1.2, 1, 7, 4)
-    two = bench.bench_c4(H.BIN, dict(mock_env, FCS_TEMP_DIR=str(w2)), str(w2), 1.2, 2, 7, 4)
+@pytest.fixture(scope="module")
+def job_runs(mock_env, tmp_path_factory):
+    """The C4 (htc) and C5 (mutect2) jobs on one slot and dealt over two."""
+    runs = {}
+    for n in (1, 2):
+        w = tmp_path_factory.mktemp(f"slots{n}")
+        runs[n] = (w, bench.bench_c4(H.BIN, dict(mock_env, FCS_TEMP_DIR=str(w)), str(w), 1.2, n, 7, 4,
+                                     tools=("htc", "mutect2")))
+    return runs
+
+
+@pytest.mark.parametrize("tool,out", [("htc", "c4.g.vcf"), ("mutect2", "c5.vcf")])
+def test_job_deals_32_shards_over_slots(job_runs, tool, out):
+    (w1, one), (w2, two) = job_runs[1], job_runs[2]
+    one, two = one[tool], two[tool]
     assert one["shards_per_device"] == {"0": 32}
     assert two["shards_per_device"] == {"0": 16, "1": 16}  # gpu.devices[job_id % n]
     assert two["devices"] == 2 and two["genome_mbp"] == 1.2 and two["regions"] > 0
     assert two["regions"] == one["regions"] and two["cells"] == one["cells"]
-    assert bench.vcf_calls(str(w1 / "c4.g.vcf")) == bench.vcf_calls(str(w2 / "c4.g.vcf"))
+    assert two["calls"] == one["calls"] > 0
+    assert bench.vcf_calls(str(w1 / out)) == bench.vcf_calls(str(w2 / out))
+
+
+def test_summary_keeps_job_figures_at_the_end(job_runs):
+    line = {"value": 1.0, "roofline": {"frac": 0.5}, "c4": job_runs[2][1]["htc"], "c5": job_runs[2][1]["mutect2"]}
+    s = bench.summary(line)
+    assert s["c4"]["shards_per_device"] == {"0": 16, "1": 16} and s["c5"]["calls"] == line["c5"]["calls"]
 
 
 def test_align_cpu_baseline_rescues_damaged_mates(mock_env, tmp_path):
@@ -59,3 +75,18 @@ def test_align_cpu_baseline_rescues_damaged_mates(mock_env, tmp_path):
     assert rep["mates_rescued"] >= 0.8 * n_damaged, (rep["mates_rescued"], n_damaged)
     cb = bench.align_cpu_baseline(H.BIN, env, str(tmp_path), cmd, ref_bam, 4)
     assert cb["bam_equal_to_gpu"] and cb["mates_rescued"] == rep["mates_rescued"] and cb["cores"] == 4
+
+
+def test_run_jobs_n1_with_cpu_path(mock_env, monkeypatch):
+    """bench.py's N = 1 C4/C5 leg end to end (both jobs, then each job's CPU
+    path beside it), here with the mock standing in for the GPU library too."""
+    import argparse
+    for k, v in mock_env.items():
+        monkeypatch.setenv(k, v)
+    args = argparse.Namespace(c4_mbp=1.0, seed=11, c4_reps=1)
+    out = bench.run_jobs(args, 1, cpu=True)
+    for k in ("c4", "c5"):
+        st = out[k]
+        assert st["shards_per_device"] == {"0": 32} and st["regions"] > 0
+        assert st["cpu_baseline"]["calls_equal_to_gpu"] and st["speedup_vs_cpu_path"] > 0
+        assert "output" not in st
