@@ -179,6 +179,7 @@ struct SessionPool {
   std::condition_variable cv;
   std::vector<Session*> all, idle;  // never freed: the pools outlive static teardown and the HIP runtime
   int creating = 0;
+  bool releasing = false;  // fcs_device_release is resetting the device: leases are refused
 };
 
 SessionPool& session_pool(int device, int kind = kComputeSession) {
@@ -226,6 +227,7 @@ int prefill_sessions(int device, int n) {
   for (;;) {
     {
       std::lock_guard<std::mutex> lk(P.mu);
+      if (P.releasing) return fail(FCS_ERR_INVALID, "[E::fcship] the device is being released");
       if ((int)P.all.size() + P.creating >= n) return FCS_OK;
       ++P.creating;
     }
@@ -261,6 +263,7 @@ class SessionLease {
     SessionPool& P = session_pool(device, kind);
     std::unique_lock<std::mutex> lk(P.mu);
     for (;;) {
+      if (P.releasing) return fail(FCS_ERR_INVALID, "[E::fcship] the device is being released");
       if (!P.idle.empty()) {
         s_ = P.idle.back();
         P.idle.pop_back();
@@ -290,6 +293,7 @@ class SessionLease {
     release();
     SessionPool& P = session_pool(device, kind);
     std::lock_guard<std::mutex> lk(P.mu);
+    if (P.releasing) return false;
     for (size_t i = 0; i < P.idle.size(); ++i) {
       Session* S = P.idle[i];
       if (S->host_cap >= bytes && S->dev_cap >= bytes) {
@@ -353,29 +357,59 @@ BswParams to_params(const fcs_bsw_params* p) {
   return q;
 }
 
-// Workspace for one SW schedule of up to cap tasks.  Stream-ordered
-// allocation when `stream_alloc`, so the *_dev entry point stays asynchronous.
-int ws_alloc(BswWorkspace& ws, int64_t cap, hipStream_t s, bool stream_alloc) {
+// Workspace for one SW schedule of up to cap tasks (plain hipMalloc: the
+// library never uses the stream-ordered pool, see stream_workspace).
+int ws_alloc(BswWorkspace& ws, int64_t cap) {
   ws.cap = cap;
   const size_t n = (size_t)std::max<int64_t>(cap, 1);
   size_t tmp = 0;
-  FCS_HIP_CHECK(sort_pairs_u32(nullptr, tmp, nullptr, nullptr, nullptr, nullptr, (int)n, s));
+  FCS_HIP_CHECK(sort_pairs_u32(nullptr, tmp, nullptr, nullptr, nullptr, nullptr, (int)n, nullptr));
   ws.tmp_bytes = std::max<size_t>(tmp, 16);
   void** bufs[6] = {(void**)&ws.keys_in, (void**)&ws.keys_out, (void**)&ws.idx_in, (void**)&ws.idx_out,
                     (void**)&ws.bounds, &ws.tmp};
   const size_t sz[6] = {4 * n, 4 * n, 4 * n, 4 * n, (kBswWideBucket + 2) * sizeof(int64_t), ws.tmp_bytes};
-  for (int i = 0; i < 6; ++i) {
-    if (stream_alloc) FCS_HIP_CHECK(hipMallocAsync(bufs[i], sz[i], s));
-    else FCS_HIP_CHECK(hipMalloc(bufs[i], sz[i]));
-  }
+  for (int i = 0; i < 6; ++i) FCS_HIP_CHECK(hipMalloc(bufs[i], sz[i]));
   return FCS_OK;
 }
 
-void ws_free(BswWorkspace& ws, hipStream_t s, bool stream_alloc) {
+void ws_free(BswWorkspace& ws) {
   void* bufs[6] = {ws.keys_in, ws.keys_out, ws.idx_in, ws.idx_out, ws.bounds, ws.tmp};
   for (void* b : bufs)
-    if (b) (void)(stream_alloc ? hipFreeAsync(b, s) : hipFree(b));
+    if (b) (void)hipFree(b);
   ws = BswWorkspace();
+}
+
+// The SW workspace of a caller's launch stream (fcs_bsw_extend_dev), kept per
+// (device, stream) like the fork sets and grown with plain hipMalloc.  Round 5
+// took it from the stream-ordered pool (hipMallocAsync / hipFreeAsync), as
+// fcs_bgzf_inflate once took its scratch: on this runtime that pool hands
+// memory still in use on one stream to an allocation on another.
+// tools/micro/pin_reuse.hip (profiles/r6/r6b_pin_reuse.log) finds overlapping
+// live allocations with 16 threads x 16 streams in every configuration tried
+// (default attributes, the stream synchronised before each free, reuse
+// attributes off, every pool call under one mutex) and from one thread over 16
+// streams; hipMalloc / hipFree and pageable copies never.  That is the cause of
+// the round-5 inflate corruption (member 0 of a call: the start of its input
+// scratch, overwritten by another call).  The caller uses a stream for one call
+// at a time, so one workspace per stream is enough.
+std::map<std::pair<int, hipStream_t>, BswWorkspace>* g_stream_ws = new std::map<std::pair<int, hipStream_t>, BswWorkspace>();
+
+int stream_workspace(int device, hipStream_t s, int64_t n, BswWorkspace** out) {
+  std::lock_guard<std::mutex> lk(g_fork_mu);
+  BswWorkspace& ws = (*g_stream_ws)[{device, s}];
+  if (ws.cap < n || !ws.keys_in) {
+    if (ws.keys_in) {
+      FCS_HIP_CHECK(hipStreamSynchronize(s));  // the stream's last call may still read the old one
+      ws_free(ws);
+    }
+    const int rc = ws_alloc(ws, std::max<int64_t>(n + n / 4, 4096));
+    if (rc) {
+      ws_free(ws);
+      return rc;
+    }
+  }
+  *out = &ws;
+  return FCS_OK;
 }
 
 int check_params(const fcs_bsw_params* p) {
@@ -455,12 +489,7 @@ struct fcs_bsw_plan {
 struct fcs_phmm_plan {
   int device = 0;
   int64_t max_pairs = 0;
-  uint32_t* keys_in = nullptr;
-  uint32_t* keys_out = nullptr;
-  int32_t* idx_in = nullptr;
-  int32_t* idx_out = nullptr;
-  void* sort_tmp = nullptr;
-  size_t sort_tmp_bytes = 0;
+  int32_t* idx_out = nullptr;  // the schedule: pair indices, launch class by class
   int32_t* rescue_list = nullptr;
   int32_t* fb_list = nullptr;                  // pairs the streamed kernel hands back (bytes outside ACGTN)
   unsigned long long* rescue_count = nullptr;  // [0] rescue count, [1] fallback count, then int64 class bounds
@@ -470,7 +499,7 @@ struct fcs_phmm_plan {
   uint32_t* bin_cursor = nullptr;  // and its running bin starts
   bool bin_zeroed = false;         // bin_hist zeroed on a schedule stream (then kept zero by the scan)
   int64_t scheduled = -1;  // n_pairs of the last schedule
-  bool counters_zeroed = false;  // the last schedule's keys kernel zeroed rescue_count[0..1]
+  bool counters_zeroed = false;  // the last schedule's count kernel zeroed rescue_count[0..1]
 };
 
 namespace fcs {
@@ -620,9 +649,6 @@ int fcs_phmm_plan_create(int32_t device, int64_t max_pairs, fcs_phmm_plan** plan
   p->device = device;
   p->max_pairs = max_pairs;
   const size_t n = (size_t)std::max<int64_t>(max_pairs, 1);
-  FCS_HIP_CHECK(hipMalloc(&p->keys_in, n * 4));
-  FCS_HIP_CHECK(hipMalloc(&p->keys_out, n * 4));
-  FCS_HIP_CHECK(hipMalloc(&p->idx_in, n * 4));
   FCS_HIP_CHECK(hipMalloc(&p->idx_out, n * 4));
   FCS_HIP_CHECK(hipMalloc(&p->rescue_list, n * 4));
   FCS_HIP_CHECK(hipMalloc(&p->fb_list, n * 4));
@@ -634,10 +660,6 @@ int fcs_phmm_plan_create(int32_t device, int64_t max_pairs, fcs_phmm_plan** plan
   // once landed after a schedule, so class launches computed nothing.)
   p->fb_count = p->rescue_count + 1;
   p->bounds = reinterpret_cast<int64_t*>(p->rescue_count + 2);
-  size_t tmp = 0;
-  FCS_HIP_CHECK(sort_pairs_u32(nullptr, tmp, p->keys_in, p->keys_out, p->idx_in, p->idx_out, (int)n, nullptr));
-  p->sort_tmp_bytes = std::max<size_t>(tmp, 16);
-  FCS_HIP_CHECK(hipMalloc(&p->sort_tmp, p->sort_tmp_bytes));
   constexpr size_t kBins = (size_t)1 << (kPhmmKeyBits - 4);
   FCS_HIP_CHECK(hipMalloc(&p->bin_hist, 2 * kBins * sizeof(uint32_t)));
   p->bin_cursor = p->bin_hist + kBins;
@@ -649,11 +671,7 @@ int fcs_phmm_plan_destroy(fcs_phmm_plan* p) {
   if (!p) return FCS_OK;
   ::fcs::DeviceScope dev_scope;
   (void)hipSetDevice(p->device);
-  (void)hipFree(p->keys_in);
-  (void)hipFree(p->keys_out);
-  (void)hipFree(p->idx_in);
   (void)hipFree(p->idx_out);
-  (void)hipFree(p->sort_tmp);
   (void)hipFree(p->rescue_list);
   (void)hipFree(p->fb_list);
   (void)hipFree(p->rescue_count);
@@ -670,37 +688,24 @@ int fcs_phmm_dev_schedule(fcs_phmm_plan* plan, const fcs_phmm_batch* b, void* st
   FCS_SET_DEVICE((plan->device));
   hipStream_t s = (hipStream_t)stream;
   const PhmmDevBatch d = to_dev(b);
-  // The bin schedule (a counting sort on the key's top 12 bits, three
-  // kernels) unless FCS_PHMM_SCHEDULE=radix asks for the full 16-bit radix
-  // sort (rocPRIM onesweep: eight launches and look-back state fills, ≈ 0.15 ms
-  // of a 1M-pair C2 step).
-  static const bool radix = [] {
-    const char* e = std::getenv("FCS_PHMM_SCHEDULE");
-    return e && std::string(e) == "radix";
-  }();
-  if (!radix) {
-    // stream-ordered, once per plan: a synchronous hipMemset at plan creation
-    // waited behind other shards' kernels on the device (htc PairHMM call time
-    // 0.45 -> 2.2 thread-s in r5aw)
-    if (!plan->bin_zeroed) {
-      FCS_HIP_CHECK(hipMemsetAsync(plan->bin_hist, 0, ((size_t)1 << (kPhmmKeyBits - 4)) * sizeof(uint32_t), s));
-      plan->bin_zeroed = true;
-    }
-    if ((rc = launch_phmm_bin_schedule(d, plan->idx_out, plan->bounds, plan->rescue_count, plan->bin_hist,
-                                       plan->bin_cursor, s)))
-      return rc;
-    plan->counters_zeroed = true;
-  } else {
-    rc = launch_phmm_keys(d, plan->keys_in, plan->idx_in, plan->rescue_count, s);
-    if (rc) return rc;
-    plan->counters_zeroed = b->n_pairs > 0;
-    if (b->n_pairs > 0) {
-      size_t tmp = plan->sort_tmp_bytes;
-      FCS_HIP_CHECK(sort_pairs_u32(plan->sort_tmp, tmp, plan->keys_in, plan->keys_out, plan->idx_in, plan->idx_out,
-                                   (int)b->n_pairs, s, kPhmmKeyBits));
-    }
-    if ((rc = launch_phmm_bounds(plan->keys_out, b->n_pairs, plan->bounds, s))) return rc;
-  }
+  // The bin schedule: a counting sort on the key's top 12 bits in three
+  // kernels (count, scan, scatter).  It replaced a 16-bit rocPRIM radix sort
+  // (eight launches and look-back state fills, ≈ 0.15 ms of a 1M-pair C2 step;
+  // A/B in profiles/r5/r5av_phmm_schedule_ab.log).  The histogram is zeroed
+  // stream-ordered, once per plan (a synchronous hipMemset at plan creation
+  // waited behind other shards' kernels on the device: htc PairHMM call time
+  // 0.45 -> 2.2 thread-s in r5aw), and the scan kernel leaves it zero.  Any
+  // failure before the scan ran may leave it dirty: the next schedule zeroes
+  // it again.
+  plan->scheduled = -1;
+  if (!plan->bin_zeroed)
+    FCS_HIP_CHECK(hipMemsetAsync(plan->bin_hist, 0, ((size_t)1 << (kPhmmKeyBits - 4)) * sizeof(uint32_t), s));
+  plan->bin_zeroed = false;  // until the scan has been launched
+  if ((rc = launch_phmm_bin_schedule(d, plan->idx_out, plan->bounds, plan->rescue_count, plan->bin_hist,
+                                     plan->bin_cursor, s)))
+    return rc;
+  plan->bin_zeroed = true;
+  plan->counters_zeroed = true;
   if (fault_drop_schedule()) FCS_HIP_CHECK(hipMemsetAsync(plan->bounds, 0, (kPhmmLaunchClasses + 1) * sizeof(int64_t), s));
   plan->scheduled = b->n_pairs;
   return FCS_OK;
@@ -757,13 +762,27 @@ int fcs_stream_release(int32_t device, void* stream) {
   if (rc) return rc;
   FCS_SET_DEVICE((device));
   ForkSet f;
+  BswWorkspace ws;
+  bool have_fork = false;
   {
     std::lock_guard<std::mutex> lk(g_fork_mu);
+    auto wi = g_stream_ws->find({device, (hipStream_t)stream});
+    if (wi != g_stream_ws->end()) {
+      ws = wi->second;
+      g_stream_ws->erase(wi);
+    }
     auto it = g_fork_sets->find({device, (hipStream_t)stream});
-    if (it == g_fork_sets->end()) return FCS_OK;
-    f = it->second;
-    g_fork_sets->erase(it);
+    if (it != g_fork_sets->end()) {
+      f = it->second;
+      g_fork_sets->erase(it);
+      have_fork = true;
+    }
   }
+  if (ws.keys_in) {
+    (void)hipStreamSynchronize((hipStream_t)stream);
+    ws_free(ws);
+  }
+  if (!have_fork) return FCS_OK;
   // tear down every side stream and event (best effort), then report the
   // first failure: an early return would leak the rest unreachably
   hipError_t first = hipSuccess;
@@ -1226,15 +1245,10 @@ int fcs_bsw_extend_dev(const fcs_bsw_batch* b, const fcs_bsw_params* params, int
   if (b->n == 0) return FCS_OK;
   FCS_SET_DEVICE((device));
   hipStream_t s = (hipStream_t)stream;
-  BswWorkspace ws;
-  if ((rc = ws_alloc(ws, b->n, s, true))) {
-    ws_free(ws, s, true);
-    return rc;
-  }
-  rc = launch_bsw_extend_sorted(bsw_dev(b), to_params(params), std::max(b->max_qlen, 0), std::max(b->max_tlen, 0),
-                                res, cells, ws, s);
-  ws_free(ws, s, true);
-  return rc;
+  BswWorkspace* ws = nullptr;
+  if ((rc = stream_workspace(device, s, b->n, &ws))) return rc;
+  return launch_bsw_extend_sorted(bsw_dev(b), to_params(params), std::max(b->max_qlen, 0), std::max(b->max_tlen, 0),
+                                  res, cells, *ws, s);
 }
 
 int fcs_bsw_plan_create(int32_t device, int64_t max_tasks, fcs_bsw_plan** plan) {
@@ -1244,8 +1258,8 @@ int fcs_bsw_plan_create(int32_t device, int64_t max_tasks, fcs_bsw_plan** plan) 
   FCS_SET_DEVICE((device));
   std::unique_ptr<fcs_bsw_plan> p(new fcs_bsw_plan());
   p->device = device;
-  if ((rc = ws_alloc(p->ws, max_tasks, nullptr, false))) {
-    ws_free(p->ws, nullptr, false);
+  if ((rc = ws_alloc(p->ws, max_tasks))) {
+    ws_free(p->ws);
     return rc;
   }
   *plan = p.release();
@@ -1256,7 +1270,7 @@ int fcs_bsw_plan_destroy(fcs_bsw_plan* plan) {
   if (!plan) return FCS_OK;
   ::fcs::DeviceScope dev_scope;
   (void)hipSetDevice(plan->device);
-  ws_free(plan->ws, nullptr, false);
+  ws_free(plan->ws);
   delete plan;
   return FCS_OK;
 }
@@ -1865,24 +1879,37 @@ int fcs_bgzf_warmup(int32_t device, int32_t sessions, int64_t arena_bytes) {
 int fcs_device_release(int32_t device) {
   int rc = check_device(device);
   if (rc) return rc;
-  for (int kind : {kComputeSession, kInflateSession}) {
-    SessionPool& P = session_pool(device, kind);
-    std::lock_guard<std::mutex> lk(P.mu);
-    if (P.creating || P.idle.size() != P.all.size())
-      return fail(FCS_ERR_INVALID, "[E::fcs_device_release] a call on this device is still running");
+  SessionPool& C = session_pool(device, kComputeSession);
+  SessionPool& I = session_pool(device, kInflateSession);
+  {
+    // one critical section from the idle check to the drop: a lease between
+    // them would hold a session the reset destroys.  `releasing` then refuses
+    // every lease (FCS_ERR_INVALID, or busy for a try) until the reset is done.
+    std::scoped_lock lk(C.mu, I.mu);
+    for (SessionPool* P : {&C, &I})
+      if (P->releasing || P->creating || P->idle.size() != P->all.size())
+        return fail(FCS_ERR_INVALID, "[E::fcs_device_release] a call on this device is still running");
+    // the handles die with the reset below: the pools, fork sets and tables
+    // are dropped (not destroyed one by one) and made again on the next call
+    for (SessionPool* P : {&C, &I}) {
+      P->all.clear();
+      P->idle.clear();
+      P->releasing = true;
+    }
   }
-  // the handles die with the reset below: the pools, fork sets and tables are
-  // dropped (not destroyed one by one) and made again on the next call
-  for (int kind : {kComputeSession, kInflateSession}) {
-    SessionPool& P = session_pool(device, kind);
-    std::lock_guard<std::mutex> lk(P.mu);
-    P.all.clear();
-    P.idle.clear();
-  }
+  struct Reopen {  // leases are accepted again once the reset has returned (or failed)
+    SessionPool *c, *i;
+    ~Reopen() {
+      std::scoped_lock lk(c->mu, i->mu);
+      c->releasing = i->releasing = false;
+    }
+  } reopen{&C, &I};
   {
     std::lock_guard<std::mutex> lk(g_fork_mu);
     for (auto it = g_fork_sets->begin(); it != g_fork_sets->end();)
       it = it->first.first == device ? g_fork_sets->erase(it) : std::next(it);
+    for (auto it = g_stream_ws->begin(); it != g_stream_ws->end();)
+      it = it->first.first == device ? g_stream_ws->erase(it) : std::next(it);
   }
   {
     std::lock_guard<std::mutex> lk(g_dev_mu);

@@ -161,16 +161,13 @@ int fork_streams(hipStream_t s, hipStream_t (&fs)[kForkStreams]);
 int join_streams(hipStream_t s, const hipStream_t (&fs)[kForkStreams]);
 
 // ------------------------------------------------------------ kernel launchers
-// Also zeroes counters[0..1] (the forward pass's rescue and fallback counts)
-// when it launches (n_pairs > 0), which saves the forward pass a memset.
-int launch_phmm_keys(const PhmmDevBatch& b, uint32_t* keys, int32_t* idx, unsigned long long* counters, hipStream_t s);
 // The bin schedule (counting sort on the key's top 12 bits): idx_out = the
-// pairs in bin order, bounds as below, counters zeroed; hist / cursor are
+// pairs in bin order, bounds = device int64[kPhmmLaunchClasses + 1] (the first
+// position of each launch class, then n), counters[0..1] (the forward pass's
+// rescue and fallback counts) zeroed; hist / cursor are
 // uint32[1 << (kPhmmKeyBits - 4)], hist all zero on entry (left zero).
 int launch_phmm_bin_schedule(const PhmmDevBatch& b, int32_t* idx_out, int64_t* bounds, unsigned long long* counters,
                              uint32_t* hist, uint32_t* cursor, hipStream_t s);
-// bounds: device int64[kPhmmLaunchClasses + 1] from launch_phmm_bounds over the sorted keys.
-int launch_phmm_bounds(const uint32_t* sorted_keys, int64_t n, int64_t* bounds, hipStream_t s);
 // fb_list / fb_count: pairs the streamed kernel hands back (haplotype bytes
 // outside A/C/G/T/N), recomputed by the one-row kernel within this call.
 int launch_phmm_forward(const PhmmDevBatch& b, const int32_t* order, int64_t count, int max_hap_len,

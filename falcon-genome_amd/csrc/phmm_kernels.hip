@@ -440,7 +440,7 @@ __host__ __device__ inline int phmm_class(int H) {
   return c < 0 ? 0 : c > kPhmmClasses - 1 ? kPhmmClasses - 1 : c;
 }
 
-// Sort keys (16 bits, two 8-bit radix passes): a 4-bit launch class, then the
+// Schedule keys (16 bits; the bin schedule sorts on the top 12): a 4-bit launch class, then the
 // in-class order, as ascending keys — each class is a contiguous range and the
 // longest work comes first.  For kStreamMinR <= R <= kStreamMaxR: haplotypes
 // longer than the column-blocked kernel's 303 columns take the row-streamed
@@ -477,18 +477,6 @@ __device__ __forceinline__ uint32_t phmm_key(const PhmmDevBatch& b, long long p)
   else
     low = ((3u - (uint32_t)min((max(R, 0) + 15) >> 4, 3)) << 10) | (0x3FFu - (uint32_t)min(max(H, 0) >> 2, 0x3FF));
   return (cf << kPhmmKeyClassShift) | low;
-}
-
-__global__ void phmm_keys_kernel(const PhmmDevBatch b, uint32_t* __restrict__ keys, int32_t* __restrict__ idx,
-                                 unsigned long long* __restrict__ counters) {
-  const long long p = (long long)blockIdx.x * blockDim.x + threadIdx.x;
-  if (p == 0) {
-    counters[0] = 0ull;
-    counters[1] = 0ull;
-  }
-  if (p >= b.n_pairs) return;
-  keys[p] = phmm_key(b, p);
-  idx[p] = (int32_t)p;
 }
 
 // ---- bin schedule: a counting sort on the key's top 12 bits (class, then the
@@ -573,25 +561,6 @@ __global__ __launch_bounds__(kBinBlock) void phmm_bin_scatter_kernel(const PhmmD
     if (bin[k] >= 0) idx[at[bin[k]] + rank[k]] = (int32_t)(base + (long long)k * kBinBlock + threadIdx.x);
 }
 
-// bounds[j] = first sorted position of launch class j; bounds[kPhmmLaunchClasses] = n.
-__global__ void phmm_bounds_kernel(const uint32_t* __restrict__ keys, long long n, int64_t* __restrict__ bounds) {
-  const long long k = (long long)blockIdx.x * blockDim.x + threadIdx.x;
-  if (k > n) return;
-  const int cur = (k < n) ? (int)(keys[k] >> kPhmmKeyClassShift) : kPhmmLaunchClasses;
-  const int prev = (k > 0) ? (int)(keys[k - 1] >> kPhmmKeyClassShift) : -1;
-  for (int j = prev + 1; j <= cur; ++j) bounds[j] = k;
-}
-
-int launch_phmm_keys(const PhmmDevBatch& b, uint32_t* keys, int32_t* idx, unsigned long long* counters,
-                     hipStream_t s) {
-  if (b.n_pairs <= 0) return FCS_OK;
-  const int bs = 256;
-  const long long nb = (b.n_pairs + bs - 1) / bs;
-  hipLaunchKernelGGL(phmm_keys_kernel, dim3((unsigned)nb), dim3(bs), 0, s, b, keys, idx, counters);
-  FCS_HIP_CHECK(hipGetLastError());
-  return FCS_OK;
-}
-
 int launch_phmm_bin_schedule(const PhmmDevBatch& b, int32_t* idx_out, int64_t* bounds, unsigned long long* counters,
                              uint32_t* hist, uint32_t* cursor, hipStream_t s) {
   static_assert(kPhmmBins % kBinBlock == 0 && (kPhmmLaunchClasses << 8) <= kPhmmBins, "bins");
@@ -605,14 +574,6 @@ int launch_phmm_bin_schedule(const PhmmDevBatch& b, int32_t* idx_out, int64_t* b
     hipLaunchKernelGGL(phmm_bin_scatter_kernel, dim3(nb), dim3(kBinBlock), 0, s, b, cursor, idx_out);
     FCS_HIP_CHECK(hipGetLastError());
   }
-  return FCS_OK;
-}
-
-int launch_phmm_bounds(const uint32_t* sorted_keys, int64_t n, int64_t* bounds, hipStream_t s) {
-  const int bs = 256;
-  hipLaunchKernelGGL(phmm_bounds_kernel, dim3((unsigned)((n + 1 + bs - 1) / bs)), dim3(bs), 0, s, sorted_keys,
-                     (long long)n, bounds);
-  FCS_HIP_CHECK(hipGetLastError());
   return FCS_OK;
 }
 

@@ -479,8 +479,8 @@ void vcf_concat_bgzip_tabix(const std::vector<std::string>& inputs, const std::s
   } po{fd, {}};
   BgzipIndexer bx(gz);
   // the next part loads on the pool while this one is written
-  auto load = [consume_inputs](const std::string& path) {
-    return host_pool_async([path, consume_inputs] {
+  auto load = [](const std::string& path) {
+    return host_pool_async([path] {
       std::FILE* in = std::fopen(path.c_str(), "rb");
       if (!in) throw fileNotFound(path);
       std::fseek(in, 0, SEEK_END);
@@ -490,7 +490,6 @@ void vcf_concat_bgzip_tabix(const std::vector<std::string>& inputs, const std::s
       const size_t got = n > 0 ? std::fread(buf->data(), 1, (size_t)n, in) : 0;
       std::fclose(in);
       buf->resize(got);
-      if (consume_inputs) std::remove(path.c_str());
       return buf;
     });
   };
@@ -531,6 +530,14 @@ void vcf_concat_bgzip_tabix(const std::vector<std::string>& inputs, const std::s
   for (auto& w : po.writes) ok = w.get() && ok;
   if (!ok) throw internalError("[E::vcf] write to " + plain + " failed");
   bx.finish();
+  // the parts go only once the VCF, its .gz and .tbi are complete (a failed
+  // concat leaves them for a rerun of this stage alone); removed on the pool,
+  // so their page-cache pages are released in parallel
+  if (consume_inputs) {
+    std::vector<std::future<int>> rm;
+    for (const std::string& path : inputs) rm.push_back(host_pool_async([path] { return std::remove(path.c_str()); }));
+    for (auto& r : rm) r.wait();
+  }
 }
 
 }  // namespace fcsg

@@ -74,16 +74,20 @@ int fcs_abi_symbol_count(void);
  * decode their reads (the reference's BackgroundExecutor role,
  * /root/reference/include/fcs-genome/BackgroundExecutor.h:12). */
 int fcs_device_warmup(int32_t device, int32_t sessions);
-/* Drops the side streams and events the library keeps for launch stream
- * `stream` on `device` (created at its first *_dev call).  Call it after the
- * stream's work has finished and before destroying the stream; a later *_dev
- * call on the same stream recreates them. */
+/* Drops the side streams, events and SW schedule workspace the library keeps
+ * for launch stream `stream` on `device` (created at its first *_dev call).
+ * Call it after the stream's work has finished and before destroying the
+ * stream; a later *_dev call on the same stream recreates them. */
 int fcs_stream_release(int32_t device, void* stream);
 /* Releases everything the library holds on `device` (session streams, pinned
  * and device arenas, plans, tables) and resets the device, so the process's
  * GPU teardown happens now instead of after its last output: `fcs-genome`
- * calls it beside the VCF tail.  FCS_ERR_INVALID while a call on the device
- * is still running.  A later call on the device sets everything up again.
+ * calls it beside the VCF tail.  FCS_ERR_INVALID while a synchronous
+ * (host-pointer) call on the device is still running; while the reset runs,
+ * such calls on the device fail with FCS_ERR_INVALID (fcs_bgzf_inflate_try
+ * answers FCS_BGZF_BUSY).  The *_dev entry points on caller streams and plans
+ * the caller owns are not tracked: the caller finishes them first.  A later
+ * call on the device sets everything up again.
  * The reset frees every allocation of the process on the device, other
  * libraries' included: call it only when nothing else holds device memory. */
 int fcs_device_release(int32_t device);
@@ -261,8 +265,11 @@ int fcs_bsw_extend_dev(const fcs_bsw_batch* dev_batch, const fcs_bsw_params* par
                        int64_t* dev_cells, int32_t device, void* stream);
 
 /* Reusable device scratch for fcs_bsw_extend_plan (schedule sort buffers for
- * batches of up to max_tasks tasks); fcs_bsw_extend_dev allocates the same
- * scratch stream-ordered on every call instead. */
+ * batches of up to max_tasks tasks); fcs_bsw_extend_dev keeps the same scratch
+ * per launch stream (grown with hipMalloc when a batch outgrows it, dropped by
+ * fcs_stream_release).  No entry point uses the stream-ordered pool
+ * (hipMallocAsync): on this runtime it hands memory live on one stream to
+ * another (tools/micro/pin_reuse.hip). */
 typedef struct fcs_bsw_plan fcs_bsw_plan;
 int fcs_bsw_plan_create(int32_t device, int64_t max_tasks, fcs_bsw_plan** plan);
 int fcs_bsw_plan_destroy(fcs_bsw_plan* plan);

@@ -496,3 +496,52 @@ def test_ksw_align2_flags_and_twin(gpu):
     q, tg, _, _ = t.task(5)
     x = fcship.KSW_XBYTE | fcship.KSW_XSUBO | fcship.KSW_XSTART | 19
     assert fcship.ksw_align2(q, tg, x) == oracle_lib.ksw_align2(q, tg, m, x)
+
+
+def test_extend_dev_concurrent_streams(gpu):
+    """fcs_bsw_extend_dev from 8 threads, each on its own launch stream, with
+    batches that grow and shrink (the per-stream schedule workspace is grown
+    with hipMalloc, never taken from the stream-ordered pool, which on this
+    runtime hands memory live on one stream to another: tools/micro/
+    pin_reuse.hip), then fcs_stream_release; every batch bit-exact against the
+    oracle."""
+    import threading
+    import torch
+    dev = torch.device("cuda", gpu)
+    m = fcship.default_mat()
+    sets = [random_tasks(500 + k, n) for k, n in enumerate((300, 2500, 900, 4000))]
+    refs = [oracle_lib.ksw_extend2_batch(t, m) for t in sets]
+    params = fcship.bsw_params()
+    errors = []
+
+    def worker(k):
+        try:
+            s = torch.cuda.Stream(dev)
+            with torch.cuda.stream(s):
+                for rep in range(3):
+                    for j in ((k + rep) % 4, (k + rep + 1) % 4, (k + rep + 2) % 4):
+                        t = sets[j]
+                        keep = {n: torch.from_numpy(np.ascontiguousarray(getattr(t, n))).to(dev)
+                                for n in ("qbuf", "qoff", "qlen", "tbuf", "toff", "tlen", "h0", "w")}
+                        b = t.to_struct()
+                        for n, x in keep.items():
+                            setattr(b, n, x.data_ptr())
+                        res = torch.empty((t.n, 6), dtype=torch.int32, device=dev)
+                        cells = torch.empty(t.n, dtype=torch.int64, device=dev)
+                        fcship.check(fcship.lib.fcs_bsw_extend_dev(fcship.C.byref(b), fcship.C.byref(params),
+                                                                   res.data_ptr(), cells.data_ptr(), gpu,
+                                                                   s.cuda_stream))
+                        s.synchronize()
+                        ref, rcells = refs[j]
+                        if not (np.array_equal(res.cpu().numpy(), ref) and np.array_equal(cells.cpu().numpy(), rcells)):
+                            errors.append(f"thread {k} set {j}: differs from the oracle")
+                s.synchronize()
+                fcship.check(fcship.lib.fcs_stream_release(gpu, s.cuda_stream))
+        except Exception as e:  # noqa: BLE001
+            errors.append(f"thread {k}: {e}")
+    th = [threading.Thread(target=worker, args=(k,)) for k in range(8)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join()
+    assert not errors, errors[:4]
