@@ -52,18 +52,6 @@ __host__ __device__ inline int cols_class(int H) {
 // of a segment read 16 consecutive slots of a chunk, 256 contiguous bytes
 // (row-major records 256 B apart per slot put all 16 lanes on the same banks:
 // 7.4 conflict cycles per LDS cycle; segment-minor entries, 64 B apart, 4.5).
-// FCS_COLS_SDWA: the match tables hold 0xFF bytes and a column's select mask
-// is one full-rate SDWA byte move with sign extension (v_bfe_i32 issues at
-// half rate on gfx950, profiles/r3/r3m_valu_rate.txt).  FCS_COLS_DCHAIN: the
-// deletion chain as D' = fma(D, yy, M * my), one dependent op per column
-// instead of two (M * my is computed a column ahead).
-#ifndef FCS_COLS_SDWA
-#define FCS_COLS_SDWA 0
-#endif
-#ifndef FCS_COLS_DCHAIN
-#define FCS_COLS_DCHAIN 0
-#endif
-constexpr uint32_t kColsMatch = FCS_COLS_SDWA ? 0xFFu : 0x01u;  // a match byte of the tables
 constexpr int kColsRing = 32;
 constexpr int kColsChunks = 6;
 constexpr int kColsChunkBytes = kColsRing * 4 * 16;  // one chunk of every (slot, segment)
@@ -107,16 +95,16 @@ __device__ __forceinline__ ColsItem cols_item(const PhmmTables<float>& tab, cons
     c.mx = last ? 0.f : q.mx;
     c.xx = last ? 0.f : q.xx;
     const int bc = base_code((unsigned char)raw.rb);
-    c.tlo = bc < 4 ? kColsMatch << (8 * bc) : bc == 4 ? vconst(kColsMatch * 0x01010101u) : 0u;
-    c.thi = kColsMatch;
+    c.tlo = bc < 4 ? 1u << (8 * bc) : bc == 4 ? vconst(0x01010101u) : 0u;
+    c.thi = 0x00000001u;
     c.z = 0.f;
   } else if (role == 4) {  // V: prior 1 on codes 0..5, 0 past column H + 1; D = running sum of M
     c.e1 = 1.f;
     c.e3 = 0.f;
     c.my = c.yy = c.mm = c.gm = 1.f;
     c.mx = c.xx = 0.f;
-    c.tlo = vconst(kColsMatch * 0x01010101u);
-    c.thi = vconst(kColsMatch * 0x00000101u);
+    c.tlo = vconst(0x01010101u);
+    c.thi = vconst(0x00000101u);
     c.z = 0.f;
   } else {  // Z: M = 0, D = 1 (from lane 0's boundary), X = D = 1, I = 0
     c.e1 = c.e3 = c.my = c.mm = c.gm = c.mx = c.xx = 0.f;
@@ -182,11 +170,8 @@ __device__ __forceinline__ void cols_load(const uint8_t* __restrict__ hb, int64_
   for (int d = 0; d <= NW; ++d) raw[d] = (base + 4 * d < ho + H && H > 0) ? src[d] : 0u;
 }
 
-#ifndef FCS_COLS_WAVES
-#define FCS_COLS_WAVES 2
-#endif
 template <int C>
-__global__ __launch_bounds__(64, FCS_COLS_WAVES) void phmm4_kernel(
+__global__ __launch_bounds__(64, 2) void phmm4_kernel(
     const PhmmDevBatch b, const int32_t* __restrict__ order, const int64_t* __restrict__ bounds, const int cls,
     const int K, const int tail_pairs, const PhmmTables<float> gtab, double* __restrict__ out,
     int32_t* __restrict__ rescue_list, unsigned long long* __restrict__ rescue_count, const float thr,
@@ -492,17 +477,9 @@ __global__ __launch_bounds__(64, FCS_COLS_WAVES) void phmm4_kernel(
             mB = __builtin_amdgcn_perm(cr.w, cr.y, cur[1][j >> 2]);
           }
           int a, c;
-#if FCS_COLS_SDWA
-          asm volatile(
-              "v_mov_b32_sdwa %0, sext(%2) dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:BYTE_%3\n\t"
-              "v_mov_b32_sdwa %1, sext(%4) dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:BYTE_%3"
-              : "=&v"(a), "=&v"(c)
-              : "v"(mA), "i"(j & 3), "v"(mB), "v"(dep));
-#else
           asm volatile("v_bfe_i32 %0, %2, %3, 1\n\tv_bfe_i32 %1, %4, %3, 1"
                        : "=&v"(a), "=&v"(c)
                        : "v"(mA), "i"(8 * (j & 3)), "v"(mB), "v"(dep));
-#endif
           return pf2{sel_v((uint32_t)a, e1.x, e3.x), sel_v((uint32_t)c, e1.y, e3.y)};
         };
         pf2 Mn = xcur * prior(0, xcur);
@@ -510,11 +487,7 @@ __global__ __launch_bounds__(64, FCS_COLS_WAVES) void phmm4_kernel(
 #pragma unroll
         for (int j = 0; j < C; ++j) {
           const pf2 M = Mn;
-#if FCS_COLS_DCHAIN
-          if (j > 0) D = __builtin_elementwise_fma(Dp, yy, Mp);  // Mp holds M(j - 1) * my here
-#else
           if (j > 0) D = __builtin_elementwise_fma(Mp, my, Dp * yy);
-#endif
           pf2 I = In[j], Xo = Xn[j];
           asm volatile("" : "+v"(I), "+v"(Xo) : "v"(D));
           if (j + 1 < C) Mn = Xo * prior(j + 1, D);
@@ -523,18 +496,10 @@ __global__ __launch_bounds__(64, FCS_COLS_WAVES) void phmm4_kernel(
           asm volatile("" : "+v"(xn), "+v"(in));  // and its outputs leave it in order
           Xn[j] = xn;
           In[j] = in;
-#if FCS_COLS_DCHAIN
-          Mp = M * my;
-#else
           Mp = M;
-#endif
           Dp = D;
         }
-#if FCS_COLS_DCHAIN
-        dn = __builtin_elementwise_fma(Dp, yy, Mp);
-#else
         dn = __builtin_elementwise_fma(Mp, my, Dp * yy);
-#endif
         xo = Xn[C - 1];
         // lane 15's D entering column 16 C + 1, kept per step in LDS (EXEC
         // narrowed to the lanes 15 inside the statement, no branch): at a V row
