@@ -446,18 +446,47 @@ __device__ __forceinline__ int add3(int a, int b, int c) {
   return r;
 }
 
+// FCS_GLANE_PERM: the row's scores of four band cells in one v_perm_b32 (the
+// row's five scores as table bytes, indexed by the cells' query codes), each
+// added to H by one SDWA add of its sign-extended byte; otherwise a bit-field
+// extract of the query offset and of its 5-bit score per cell.
+#ifndef FCS_GLANE_PERM
+#define FCS_GLANE_PERM 1
+#endif
+template <int B>
+__device__ __forceinline__ int add_sbyte_c(int h, uint32_t s4) {
+  int r;
+  asm("v_add_u32_sdwa %0, %1, sext(%2) dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:BYTE_%3"
+      : "=v"(r)
+      : "v"(h), "v"(s4), "i"(B));
+  return r;
+}
+
 template <int NB, bool CIG>
 __device__ __forceinline__ void glane_row(int (&Hd)[NB], int (&Ed)[NB + 1], const uint32_t (&Qb)[(NB + 4) / 4],
-                                          uint32_t (&nib)[(NB + 7) / 8], const int rowpack, const int oe_del,
-                                          const int oe_ins, const int e_del, const int e_ins) {
+                                          uint32_t (&nib)[(NB + 7) / 8], const uint32_t rowlo, const uint32_t rowhi,
+                                          const int oe_del, const int oe_ins, const int e_del, const int e_ins) {
   int f = kMinusInf;
   uint32_t acc = 0;
   const int o_del = oe_del - e_del, neg_e_del = -e_del;
+  uint32_t s4 = 0;
 #pragma unroll
   for (int k = 0; k < NB; ++k) {
-    const int qoff = (int)((Qb[k >> 2] >> (8 * (k & 3))) & 0xFFu);
-    const int s = __builtin_amdgcn_sbfe(rowpack, qoff, 5);
+#if FCS_GLANE_PERM
+    if ((k & 3) == 0) s4 = __builtin_amdgcn_perm(rowhi, rowlo, Qb[k >> 2]);  // bytes: scores of cells k .. k + 3
+    int m;
+    switch (k & 3) {
+      case 0: m = add_sbyte_c<0>(Hd[k], s4); break;
+      case 1: m = add_sbyte_c<1>(Hd[k], s4); break;
+      case 2: m = add_sbyte_c<2>(Hd[k], s4); break;
+      default: m = add_sbyte_c<3>(Hd[k], s4); break;
+    }
+#else
+    (void)s4;
+    const int qoff = 5 * (int)((Qb[k >> 2] >> (8 * (k & 3))) & 0xFFu);
+    const int s = __builtin_amdgcn_sbfe((int)rowlo, qoff, 5);
     const int m = Hd[k] + s;
+#endif
     const int e0 = Ed[k + 1];
     const int h1 = max(m, e0);
     const int h = max(h1, f);
@@ -517,7 +546,7 @@ __device__ void glane_run(const BswDevBatch& b, const BswParams& p, long long ta
   const int qlast = max(qlen - 1, 0);
   auto qbyte = [&](int j) -> uint32_t {
     const uint32_t v = qp[min(max(j, 0), qlast)];
-    return (ok && j >= 0 && j < qlen) ? 5u * v : 0u;
+    return (ok && j >= 0 && j < qlen) ? v : 0u;
   };
 #pragma unroll
   for (int k = 0; k < NB; ++k) {
@@ -582,8 +611,18 @@ __device__ void glane_run(const BswDevBatch& b, const BswParams& p, long long ta
   // the row's packed score table by the lane's target base: lanes 0..4 hold
   // the five tables, one ds_bpermute fetches lane tb's
   const int ln = lane_id();
+#if FCS_GLANE_PERM
+  // lane t < 5: target base t's scores of query codes 0..3 (bytes of tabv)
+  // and of code 4 (byte 0 of tabh)
+  const int tabv = ln < 5 ? (int)((uint32_t)(uint8_t)p.mat[5 * ln] | (uint32_t)(uint8_t)p.mat[5 * ln + 1] << 8 |
+                                  (uint32_t)(uint8_t)p.mat[5 * ln + 2] << 16 | (uint32_t)(uint8_t)p.mat[5 * ln + 3] << 24)
+                         : 0;
+  const int tabh = ln < 5 ? (int)(uint32_t)(uint8_t)p.mat[5 * ln + 4] : 0;
+#else
   const int tabv = ln == 0 ? p.matpack[0] : ln == 1 ? p.matpack[1] : ln == 2 ? p.matpack[2]
                  : ln == 3 ? p.matpack[3] : ln == 4 ? p.matpack[4] : 0;
+  const int tabh = 0;
+#endif
   for (int i0 = 0; i0 < tmax; i0 += 4) {
     // both streams realigned before either requests more (with the CIG pass's
     // stores counted in vmcnt, a wait after a new request would wait for it)
@@ -597,9 +636,10 @@ __device__ void glane_run(const BswDevBatch& b, const BswParams& p, long long ta
       const int i = i0 + r;
       if (i >= tmax) break;
       const int tb = (ok && i < tlen) ? (int)((ts.cur >> (8 * r)) & 0xFFu) : 4;
-      const uint32_t qn = (ok && i + qc < qlen) ? 5u * ((qs.cur >> (8 * r)) & 0xFFu) : 0u;
-      const int rowpack = __builtin_amdgcn_ds_bpermute(4 * min(tb, 4), tabv);
-      glane_row<NB, CIG>(Hd, Ed, Qb, nib, rowpack, oe_del, oe_ins, e_del, e_ins);
+      const uint32_t qn = (ok && i + qc < qlen) ? ((qs.cur >> (8 * r)) & 0xFFu) : 0u;
+      const uint32_t rowlo = (uint32_t)__builtin_amdgcn_ds_bpermute(4 * min(tb, 4), tabv);
+      const uint32_t rowhi = FCS_GLANE_PERM ? (uint32_t)__builtin_amdgcn_ds_bpermute(4 * min(tb, 4), tabh) : 0u;
+      glane_row<NB, CIG>(Hd, Ed, Qb, nib, rowlo, rowhi, oe_del, oe_ins, e_del, e_ins);
       // (the slot tests are built where they are used: hoisted out of the row
       // loop they would hold one SGPR pair per slot)
       if (narrow) {
