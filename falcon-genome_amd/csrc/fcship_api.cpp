@@ -1772,9 +1772,15 @@ int bgzf_inflate_host(const uint8_t* comp, int64_t comp_bytes, uint8_t* out, int
     return fail(FCS_ERR_INVALID, "[E::fcs_bgzf_inflate] bad arguments");
   *comp_used = 0;
   *out_bytes = 0;
-  // a member is at least 28 bytes (18 of header / trailer, 2 of DEFLATE)
+  // a member is at least 28 bytes (18 of header / trailer, 2 of DEFLATE); the
+  // offset tables are this thread's, kept between calls (no fresh zeroed
+  // pages per call)
   const int64_t most = std::min<int64_t>(comp_bytes / 20 + 1, 0x7FFFFFFE);
-  std::vector<int64_t> coff((size_t)most + 1), uoff((size_t)most + 1);
+  static thread_local std::vector<int64_t> coff, uoff;
+  if (coff.size() < (size_t)most + 1) {
+    coff.resize((size_t)most + 1);
+    uoff.resize((size_t)most + 1);
+  }
   int32_t n = 0;
   int64_t used = 0;
   int rc = fcs_bgzf_index(comp, comp_bytes, coff.data(), uoff.data(), (int32_t)most, &n, &used);

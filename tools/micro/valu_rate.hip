@@ -303,6 +303,30 @@ __global__ __launch_bounds__(256) void kern(float* out, unsigned long long* stam
 #define I(j) asm volatile("v_min3_i32 %0, %1, %2, %0" : "+v"(a[j]) : "v"(b[j]), "v"(b[(j + 1) & 7]));
         BODY8(I)
 #undef I
+      } else if constexpr (K == 68) {  // byte -> float (VOP1)
+#define I(j) asm volatile("v_cvt_f32_ubyte1 %0, %1" : "=v"(a[j]) : "v"(b[j]));
+        BODY8(I)
+#undef I
+      } else if constexpr (K == 69) {  // prior as fma(m, e1 - e3, e3) on both halves
+#define I(j) asm volatile("v_pk_fma_f32 %0, %1, %2, %0" : "+v"(c[j]) : "v"(d[j]), "v"(d[(j + 1) & 7]));
+        BODY8(I)
+#undef I
+      } else if constexpr (K == 70) {  // v_bfe_i32 mask + v_bitop3 select (the column kernel's prior, per half)
+#define I(j) asm volatile("v_bfe_i32 %0, %1, 8, 1\n\tv_bitop3_b32 %0, %1, %2, %0 bitop3:0xe4" : "=&v"(a[j]) : "v"(b[j]), "v"(b[(j + 1) & 7]));
+        BODY8(I)
+#undef I
+      } else if constexpr (K == 71) {  // v_cvt_f32_ubyte mask (the alternative, per half)
+#define I(j) asm volatile("v_cvt_f32_ubyte2 %0, %1" : "=v"(a[j]) : "v"(b[j]));
+        BODY8(I)
+#undef I
+      } else if constexpr (K == 72) {  // v_mov_b32_sdwa sext byte
+#define I(j) asm volatile("v_mov_b32_sdwa %0, sext(%1) dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:BYTE_1" : "=v"(a[j]) : "v"(b[j]));
+        BODY8(I)
+#undef I
+      } else if constexpr (K == 73) {
+#define I(j) asm volatile("v_lshrrev_b32 %0, 31, %1" : "=v"(a[j]) : "v"(b[j]));
+        BODY8(I)
+#undef I
       } else if constexpr (K == 67) {
 #define I(j) asm volatile("v_sub_u32 %0, %1, %0\n\tv_alignbit_b32 %0, %0, %1, 31" : "+v"(a[j]) : "v"(b[j]));
         BODY8(I)
@@ -353,6 +377,14 @@ int main(int argc, char** argv) {
   CHECK(hipMalloc(&out, sizeof(float) * ncu * 4 * waves * 64 * 2));
   CHECK(hipMalloc(&st, 16));
   run<0>("v_fma_f32", waves, out, st, ncu);
+  run<68>("v_cvt_f32_ubyte1", waves, out, st, ncu);
+  run<71>("v_cvt_f32_ubyte2", waves, out, st, ncu);
+  run<69>("v_pk_fma_f32", waves, out, st, ncu);
+  run<70>("bfe_i32 + bitop3 (2 instr)", waves, out, st, ncu);
+  run<72>("v_mov_b32_sdwa sext byte", waves, out, st, ncu);
+  run<73>("v_lshrrev_b32", waves, out, st, ncu);
+  run<3>("v_bfe_i32", waves, out, st, ncu);
+  run<4>("v_bitop3_b32", waves, out, st, ncu);
   run<60>("v_alignbit_b32", waves, out, st, ncu);
   run<61>("v_lshl_or_b32", waves, out, st, ncu);
   run<62>("v_or3_b32", waves, out, st, ncu);
