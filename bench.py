@@ -782,6 +782,8 @@ def run_jobs(args, n_dev, cpu):
 
 def job_summary(st):
     """The compact figures of a C4/C5 block for the line's summary."""
+    if "error" in st:
+        return {"error": st["error"]}
     s = {k: st.get(k) for k in ("genome_mbp", "devices", "seconds", "runs_seconds", "regions", "regions_per_s",
                                 "caller_stage_seconds", "shards_per_device", "calls", "rescued_pairs",
                                 "gpu_busy_frac")}
@@ -1040,10 +1042,29 @@ class Ranks:
                 import datetime
                 torch.distributed.init_process_group("nccl", device_id=self.dev,
                                                      timeout=datetime.timedelta(minutes=30))
+        # a CPU-side group for the long waits (ranks > 0 while rank 0 runs the
+        # C4 / C5 jobs): a gloo barrier blocks in a socket read, where an RCCL
+        # barrier's stream wait may spin a host core the jobs need
+        self.cpu_group = None
+        if self.world > 1:
+            import datetime
+            self.cpu_group = torch.distributed.new_group(backend="gloo", timeout=datetime.timedelta(minutes=30))
 
     def barrier(self):
         if self.world > 1:
             torch.distributed.barrier()
+
+    def cpu_barrier(self):
+        if self.world > 1:
+            torch.distributed.barrier(group=self.cpu_group)
+
+    def cpu_sum(self, v):
+        """Sum of one float over the ranks through the gloo group (a blocking
+        wait, no spinning host core while slower ranks finish)."""
+        t = torch.tensor([float(v)], dtype=torch.float64)
+        if self.world > 1:
+            torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.SUM, group=self.cpu_group)
+        return float(t.item())
 
     def _reduce(self, vals, op):
         t = torch.tensor(vals, dtype=torch.float64, device=self.dev)
@@ -1311,8 +1332,15 @@ def main():
 
     if not args.no_e2e:
         progress("e2e htc / mutect2 / align")
-        e2e = bench_e2e(args, rank, local)
-        if world > 1:  # whole-job rates: units of all ranks over the slowest rank's time
+        try:
+            e2e, ok = bench_e2e(args, rank, local), 1.0
+        except Exception as e:  # reported in the line; the headline stands
+            progress(f"e2e failed: {e!r}"[:400])
+            e2e, ok = {"error": repr(e)[:400]}, 0.0
+        n_ok = rk.cpu_sum(ok)
+        if world > 1 and n_ok < world:
+            e2e["ranks_failed"] = int(world - n_ok)
+        elif world > 1:  # whole-job rates: units of all ranks over the slowest rank's time
             for k, unit in (("htc", "regions"), ("mutect2", "regions"), ("align", "reads")):
                 tot, = rk.sum(e2e[k][unit])
                 slow, = rk.max(e2e[k]["seconds"])
@@ -1329,12 +1357,16 @@ def main():
         # their 32 shards dealt to all N GPUs of the node by the job's own
         # Executor.  Rank 0 runs them while the other ranks wait; their GPUs
         # serve the jobs' slots.  At N = 1 each job's CPU path runs beside it.
-        rk.barrier()
+        rk.cpu_barrier()
         if rank == 0:
-            jobs = run_jobs(args, int(os.environ.get("LOCAL_WORLD_SIZE", str(world))),
-                            cpu=world == 1 and not args.no_cpu_baseline)
+            try:
+                jobs = run_jobs(args, int(os.environ.get("LOCAL_WORLD_SIZE", str(world))),
+                                cpu=world == 1 and not args.no_cpu_baseline)
+            except Exception as e:  # reported in the line; the headline stands
+                progress(f"C4/C5 legs failed: {e!r}"[:400])
+                jobs = {"c4": {"error": repr(e)[:400]}}
             line.update(jobs)
-        rk.barrier()
+        rk.cpu_barrier()
 
     if rank == 0:
         # the driver keeps only the tail of stdout: the long e2e block first,
@@ -1367,6 +1399,8 @@ def summary(line):
             s["align_parity"] = {k: b["align"]["parity"][k] for k in ("n", "bit_exact", "pass")}
             s["align_i16_parity"] = {k: b["align"]["i16"]["parity"][k] for k in ("n", "bit_exact", "pass")}
     e = line.get("e2e", {})
+    if "error" in e:
+        s["e2e_error"] = e["error"]
     for k in ("htc", "mutect2"):
         if k in e:
             x = {"seconds": e[k]["seconds"], "runs_seconds": e[k]["runs_seconds"],
@@ -1403,6 +1437,9 @@ def dry_main(args, rk):
     elapsed, = rk.max(time.perf_counter() - t0)
     units, = rk.sum(float(args.steps))
     ranks_seen, = rk.sum(1.0)
+    rk.cpu_barrier()  # the gloo wait group of the C4 / C5 legs
+    if rk.cpu_sum(1.0) != ranks_seen:
+        sys.exit("bench.py: the CPU wait group disagrees with the rank count")
     if rk.rank == 0:
         print(json.dumps({"metric": METRIC, "value": round(units / elapsed, 3), "unit": "dry steps/s",
                           "n_gpus": rk.world, "steps": args.steps, "warmup": args.warmup,
