@@ -446,13 +446,9 @@ __device__ __forceinline__ int add3(int a, int b, int c) {
   return r;
 }
 
-// FCS_GLANE_PERM: the row's scores of four band cells in one v_perm_b32 (the
-// row's five scores as table bytes, indexed by the cells' query codes), each
-// added to H by one SDWA add of its sign-extended byte; otherwise a bit-field
-// extract of the query offset and of its 5-bit score per cell.
-#ifndef FCS_GLANE_PERM
-#define FCS_GLANE_PERM 1
-#endif
+// The row's scores of four band cells in one v_perm_b32 (the row's five
+// scores as table bytes, indexed by the cells' query codes), each added to H by
+// one SDWA add of its sign-extended byte.
 template <int B>
 __device__ __forceinline__ int add_sbyte_c(int h, uint32_t s4) {
   int r;
@@ -462,17 +458,51 @@ __device__ __forceinline__ int add_sbyte_c(int h, uint32_t s4) {
   return r;
 }
 
-template <int NB, bool CIG>
+// The 16-bit form of a row (U): every H / E / F value is held as value +
+// kGU16Bias, zero-extended in its 32-bit register, with bwa's MINUS_INF
+// standing in as kGU16NegInf.  Its maxes are v_max_u16 (full rate on gfx950;
+// v_max_i32 issues at half rate), adds and subtracts stay 32-bit
+// (a biased value never leaves [0, 65535], so they are exact and stay
+// zero-extended), and the difference of two biased values is the true
+// difference, so the direction bits are unchanged.  Taken by a wave whose
+// tasks all satisfy glane_u16_ok: every real value and every MINUS_INF-derived
+// one then keeps its 32-bit path's value up to the bias (|real| <= 8000,
+// MINUS_INF-derived within 8000 of kGU16NegInf), so every compare and every
+// output is the same.
+constexpr int kGU16Bias = 32768;
+constexpr int kGU16NegInf = -24576;
+__host__ __device__ __forceinline__ bool glane_u16_ok(int qlen, int tlen, int e_del, int e_ins, int o_del,
+                                                      int o_ins) {
+  // a path's score moves by at most max(e) + 16 (|mat| <= 16 on the lane path)
+  // per row or column, plus the two gap opens
+  const long long span = (long long)(qlen + tlen + 2) * ((e_del > e_ins ? e_del : e_ins) + 16) + o_del + o_ins;
+  return span <= 8000;
+}
+template <bool U>
+__device__ __forceinline__ int gmax(int a, int b) {
+  if constexpr (U) {
+    int r;
+    asm("v_max_u16 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+    return r;
+  } else {
+    return max(a, b);
+  }
+}
+template <bool U>
+__host__ __device__ constexpr int gval(int v) {  // a boundary value as the row form holds it
+  return U ? (v == kMinusInf ? kGU16NegInf : v) + kGU16Bias : v;
+}
+
+template <int NB, bool CIG, bool U>
 __device__ __forceinline__ void glane_row(int (&Hd)[NB], int (&Ed)[NB + 1], const uint32_t (&Qb)[(NB + 4) / 4],
                                           uint32_t (&nib)[(NB + 7) / 8], const uint32_t rowlo, const uint32_t rowhi,
                                           const int oe_del, const int oe_ins, const int e_del, const int e_ins) {
-  int f = kMinusInf;
+  int f = gval<U>(kMinusInf);
   uint32_t acc = 0;
   const int o_del = oe_del - e_del, neg_e_del = -e_del;
   uint32_t s4 = 0;
 #pragma unroll
   for (int k = 0; k < NB; ++k) {
-#if FCS_GLANE_PERM
     if ((k & 3) == 0) s4 = __builtin_amdgcn_perm(rowhi, rowlo, Qb[k >> 2]);  // bytes: scores of cells k .. k + 3
     int m;
     switch (k & 3) {
@@ -481,21 +511,16 @@ __device__ __forceinline__ void glane_row(int (&Hd)[NB], int (&Ed)[NB + 1], cons
       case 2: m = add_sbyte_c<2>(Hd[k], s4); break;
       default: m = add_sbyte_c<3>(Hd[k], s4); break;
     }
-#else
-    (void)s4;
-    const int qoff = 5 * (int)((Qb[k >> 2] >> (8 * (k & 3))) & 0xFFu);
-    const int s = __builtin_amdgcn_sbfe((int)rowlo, qoff, 5);
-    const int m = Hd[k] + s;
-#endif
     const int e0 = Ed[k + 1];
-    const int h1 = max(m, e0);
-    const int h = max(h1, f);
+    const int h1 = gmax<U>(m, e0);
+    const int h = gmax<U>(h1, f);
     const int ti = m - oe_ins;
     const int fn = f - e_ins;
     if constexpr (CIG) {
       // E from the two differences the direction bits need anyway:
       // max(e0 - e_del, M - oe_del) = e0 - e_del + max(x, 0) with
       // x = M - e0 - o_del, one instruction fewer than forming both terms
+      // (the 16-bit form takes the full-rate max of both terms instead)
       const int dme = m - e0;
       const int x = dme - o_del;
       acc = gbit(acc, ti - fn);  // F-continue: f - e_ins > M - oe_ins
@@ -503,17 +528,19 @@ __device__ __forceinline__ void glane_row(int (&Hd)[NB], int (&Ed)[NB + 1], cons
       acc = gbit(acc, h1 - f);   // max(M, E) < F: H from F
       acc = gbit(acc, dme);      // M < E: H from E
       if ((k & 7) == 7) nib[k >> 3] = acc;
-      Ed[k] = add3(e0, max(x, 0), neg_e_del);
+      if constexpr (U) Ed[k] = gmax<U>(e0 - e_del, m - oe_del);
+      else Ed[k] = add3(e0, max(x, 0), neg_e_del);
     } else {
-      Ed[k] = max(e0 - e_del, m - oe_del);
+      (void)neg_e_del;
+      Ed[k] = gmax<U>(e0 - e_del, m - oe_del);
     }
     Hd[k] = h;
-    f = max(fn, ti);
+    f = gmax<U>(fn, ti);
   }
   if constexpr (CIG && (NB & 7) != 0) nib[NB >> 3] = acc << (4 * (8 - (NB & 7)));  // the row's last cells to the top
 }
 
-template <int NB, bool CIG>
+template <int NB, bool CIG, bool U>
 __device__ void glane_run(const BswDevBatch& b, const BswParams& p, long long task, bool ok,
                           int32_t* __restrict__ scores, uint8_t* __restrict__ zbuf, const int64_t* __restrict__ zoff,
                           uint32_t* __restrict__ cigar, const int64_t* __restrict__ cigar_off,
@@ -551,10 +578,10 @@ __device__ void glane_run(const BswDevBatch& b, const BswParams& p, long long ta
 #pragma unroll
   for (int k = 0; k < NB; ++k) {
     const int j = k - w;  // column of slot k in row 0; Hd holds "H(-1, j - 1)" = bwa's first-row eh[j].h
-    Hd[k] = j == 0 ? 0 : (j >= 1 && j <= w) ? -(p.o_ins + e_ins * j) : kMinusInf;
-    Ed[k] = kMinusInf;
+    Hd[k] = gval<U>(j == 0 ? 0 : (j >= 1 && j <= w) ? -(p.o_ins + e_ins * j) : kMinusInf);
+    Ed[k] = gval<U>(kMinusInf);
   }
-  Ed[NB] = kMinusInf;
+  Ed[NB] = gval<U>(kMinusInf);
 #pragma unroll
   for (int d = 0; d < NQ; ++d) {
     uint32_t v = 0;
@@ -569,7 +596,7 @@ __device__ void glane_run(const BswDevBatch& b, const BswParams& p, long long ta
   // chain, -(o_del + e_del (i + 1)), runs down it from here
 #pragma unroll
   for (int k = 1; k <= NB; ++k)
-    if (k == w) Ed[k] = -(p.o_del + e_del);
+    if (k == w) Ed[k] = gval<U>(-(p.o_del + e_del));
   // lanes whose band is narrower than the class: E of slot nb back to -inf
   // after every row (a wave-uniform test; the class's widest lanes need none)
   const bool narrow = __ballot(ok && nb < NB) != 0ull;
@@ -611,18 +638,12 @@ __device__ void glane_run(const BswDevBatch& b, const BswParams& p, long long ta
   // the row's packed score table by the lane's target base: lanes 0..4 hold
   // the five tables, one ds_bpermute fetches lane tb's
   const int ln = lane_id();
-#if FCS_GLANE_PERM
   // lane t < 5: target base t's scores of query codes 0..3 (bytes of tabv)
   // and of code 4 (byte 0 of tabh)
   const int tabv = ln < 5 ? (int)((uint32_t)(uint8_t)p.mat[5 * ln] | (uint32_t)(uint8_t)p.mat[5 * ln + 1] << 8 |
                                   (uint32_t)(uint8_t)p.mat[5 * ln + 2] << 16 | (uint32_t)(uint8_t)p.mat[5 * ln + 3] << 24)
                          : 0;
   const int tabh = ln < 5 ? (int)(uint32_t)(uint8_t)p.mat[5 * ln + 4] : 0;
-#else
-  const int tabv = ln == 0 ? p.matpack[0] : ln == 1 ? p.matpack[1] : ln == 2 ? p.matpack[2]
-                 : ln == 3 ? p.matpack[3] : ln == 4 ? p.matpack[4] : 0;
-  const int tabh = 0;
-#endif
   for (int i0 = 0; i0 < tmax; i0 += 4) {
     // both streams realigned before either requests more (with the CIG pass's
     // stores counted in vmcnt, a wait after a new request would wait for it)
@@ -638,8 +659,8 @@ __device__ void glane_run(const BswDevBatch& b, const BswParams& p, long long ta
       const int tb = (ok && i < tlen) ? (int)((ts.cur >> (8 * r)) & 0xFFu) : 4;
       const uint32_t qn = (ok && i + qc < qlen) ? ((qs.cur >> (8 * r)) & 0xFFu) : 0u;
       const uint32_t rowlo = (uint32_t)__builtin_amdgcn_ds_bpermute(4 * min(tb, 4), tabv);
-      const uint32_t rowhi = FCS_GLANE_PERM ? (uint32_t)__builtin_amdgcn_ds_bpermute(4 * min(tb, 4), tabh) : 0u;
-      glane_row<NB, CIG>(Hd, Ed, Qb, nib, rowlo, rowhi, oe_del, oe_ins, e_del, e_ins);
+      const uint32_t rowhi = (uint32_t)__builtin_amdgcn_ds_bpermute(4 * min(tb, 4), tabh);
+      glane_row<NB, CIG, U>(Hd, Ed, Qb, nib, rowlo, rowhi, oe_del, oe_ins, e_del, e_ins);
       // (the slot tests are built where they are used: hoisted out of the row
       // loop they would hold one SGPR pair per slot)
       if (narrow) {
@@ -647,7 +668,7 @@ __device__ void glane_run(const BswDevBatch& b, const BswParams& p, long long ta
         asm volatile("" : "+v"(nbv));
 #pragma unroll
         for (int k = 5; k < NB; k += 2)
-          if (k == nbv) Ed[k] = kMinusInf;
+          if (k == nbv) Ed[k] = gval<U>(kMinusInf);
       }
       if (ok && i == tlen - 1) {  // bwa's score eh[qlen].h: H(tlen - 1, qlen - 1) when the band reaches it
         int kf = kfin < nb ? kfin : -1;
@@ -678,6 +699,12 @@ __device__ void glane_run(const BswDevBatch& b, const BswParams& p, long long ta
       Qb[NB >> 2] = (Qb[NB >> 2] & ~(0xFFu << (8 * (NB & 3)))) | (qn << (8 * (NB & 3)));
     }
   }
+  if constexpr (U) {  // back to the 32-bit form: MINUS_INF-derived values keep their offset from it
+    if (score != kMinusInf) {
+      score -= kGU16Bias;
+      if (score < -16384) score = score - kGU16NegInf + kMinusInf;
+    }
+  }
   if (ok) scores[task] = score;
   // (the traceback runs in bsw_traceback_kernel: a chain of dependent loads per
   // lane, it wants the occupancy this kernel's registers do not leave)
@@ -703,7 +730,10 @@ __global__ __launch_bounds__(64) void bsw_global_lane_kernel(const BswDevBatch b
   const int nbw = 2 * wave_max(ok ? w : -1) + 1;
   constexpr int lo = NB == 17 ? 0 : NB == 33 ? 17 : 33;
   if (nbw <= lo || nbw > NB) return;
-  glane_run<NB, CIG>(b, p, task, ok, scores, zbuf, zoff, cigar, cigar_off, cigar_cap, n_cigar);
+  // the 16-bit row form when every task of the wave keeps its values in range
+  const bool u16 = __ballot(ok && !glane_u16_ok(b.qlen[task], b.tlen[task], p.e_del, p.e_ins, p.o_del, p.o_ins)) == 0ull;
+  if (u16) glane_run<NB, CIG, true>(b, p, task, ok, scores, zbuf, zoff, cigar, cigar_off, cigar_cap, n_cigar);
+  else glane_run<NB, CIG, false>(b, p, task, ok, scores, zbuf, zoff, cigar, cigar_off, cigar_cap, n_cigar);
 }
 
 template <int NS>

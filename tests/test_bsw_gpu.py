@@ -545,3 +545,36 @@ def test_extend_dev_concurrent_streams(gpu):
     for t in th:
         t.join()
     assert not errors, errors[:4]
+
+
+@pytest.mark.parametrize("shape", ["long", "heavy_gaps", "mixed_wave"])
+def test_global_lane_kernel_32bit_form(gpu, shape):
+    """The lane kernel's 32-bit row form: a wave whose tasks could leave the
+    16-bit form's range (glane_u16_ok: long tasks, heavy gap costs, or one
+    such task among short ones) runs the 32-bit rows; scores and CIGARs
+    bit-exact against the oracle either way."""
+    kw = {}
+    if shape == "long":  # qlen + tlen ~ 1,400 at w = 16
+        t = fcship.synth_bsw(71, 300, read_len=700, ref_len=1_000_000, w=16, mode=1, fixed_q=700, fixed_t=700)
+    elif shape == "heavy_gaps":  # 151 bp reads with o = 30, e = 12 per gap
+        t = fcship.synth_bsw(72, 600, read_len=151, ref_len=1_000_000, w=16, mode=1, fixed_q=151, fixed_t=151)
+        kw = dict(o_del=30, e_del=12, o_ins=30, e_ins=12)
+    else:  # one long task in every 64-task wave of short ones
+        s = fcship.synth_bsw(73, 640, read_len=151, ref_len=1_000_000, w=16, mode=1, fixed_q=151, fixed_t=151)
+        lng = fcship.synth_bsw(74, 10, read_len=600, ref_len=1_000_000, w=16, mode=1, fixed_q=600, fixed_t=600)
+        items = []
+        for k in range(s.n):
+            items.append(s.task(k))
+            if k % 64 == 17:
+                items.append(lng.task(k // 64))
+        t = fcship.make_tasks(items)
+    params = fcship.bsw_params(**kw)
+    scores, cigars = fcship.bsw_global(t, params)
+    m = fcship.default_mat()
+    for k in range(t.n):
+        q, tg, _, ww = t.task(k)
+        rs, rc = oracle_lib.ksw_global2(q, tg, ww, m, **kw)
+        assert scores[k] == rs, f"task {k}: score {scores[k]} != {rs}"
+        assert np.array_equal(cigars[k], rc), f"task {k}: {fcship.cigar_str(cigars[k])} != {fcship.cigar_str(rc)}"
+    s2, _ = fcship.bsw_global(t, params, with_cigar=False)
+    assert np.array_equal(s2, scores)
