@@ -12,7 +12,8 @@ for i in 1 2 3; do
     [ $tag = A ] && E=$A || E=$B
     rm -rf $W/log
     { time env $E FCS_LOG_DIR=$W/log timeout 300 $X htc -f -r $W/d/ref.fasta -i $W/d/sample.bam -o $W/h_$tag.g.vcf 2> $W/err; } 2> $W/time || { tail -3 $W/err; exit 1; }
-    echo "== $tag ($E) run $i: $(grep real $W/time)"
+    echo "== $tag ($E) run $i: $(grep real $W/time) $(grep user $W/time) $(grep sys $W/time)"
+    grep -h "timeline\] exit" $W/err | sed 's/^/  /' 
     grep -h "htc\] shard" $W/log/*.log | awk '{for(i=1;i<=NF;i++){if($i=="decode"){d+=$(i+1)} if($i=="(PairHMM"){p+=$(i+1)} if($i=="regions"&&$(i+1)~/^[0-9.]+$/&&$(i+2)=="s,"){r+=$(i+1)} if($i=="ran"){n+=$(i+1)}}} END{print "  decode", d, "phmm", p, "regions", r, "nested", n+0}'
   done
 done
