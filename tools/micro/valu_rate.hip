@@ -327,6 +327,34 @@ __global__ __launch_bounds__(256) void kern(float* out, unsigned long long* stam
 #define I(j) asm volatile("v_lshrrev_b32 %0, 31, %1" : "=v"(a[j]) : "v"(b[j]));
         BODY8(I)
 #undef I
+      } else if constexpr (K == 74) {
+#define I(j) asm volatile("v_pk_sub_u16 %0, %1, %0 clamp" : "+v"(a[j]) : "v"(b[j]));
+        BODY8(I)
+#undef I
+      } else if constexpr (K == 75) {
+#define I(j) asm volatile("v_pk_min_u16 %0, %1, %0" : "+v"(a[j]) : "v"(b[j]));
+        BODY8(I)
+#undef I
+      } else if constexpr (K == 76) {
+#define I(j) asm volatile("v_pk_mad_u16 %0, %1, %2, %0" : "+v"(a[j]) : "v"(b[j]), "v"(b[(j + 1) & 7]));
+        BODY8(I)
+#undef I
+      } else if constexpr (K == 77) {
+#define I(j) asm volatile("v_pk_mad_u16 %0, %1, %2, 0 op_sel_hi:[1,1,0] clamp" : "=v"(a[j]) : "v"(b[j]), "v"(b[(j + 1) & 7]));
+        BODY8(I)
+#undef I
+      } else if constexpr (K == 78) {
+#define I(j) asm volatile("v_pk_ashrrev_i16 %0, 15, %1 op_sel_hi:[0,1]" : "=v"(a[j]) : "v"(b[j]));
+        BODY8(I)
+#undef I
+      } else if constexpr (K == 79) {
+#define I(j) asm volatile("v_pk_lshlrev_b16 %0, 8, %1 op_sel_hi:[0,1]" : "=v"(a[j]) : "v"(b[j]));
+        BODY8(I)
+#undef I
+      } else if constexpr (K == 80) {
+#define I(j) asm volatile("v_sub_u16 %0, %1, %0 clamp" : "+v"(a[j]) : "v"(b[j]));
+        BODY8(I)
+#undef I
       } else if constexpr (K == 67) {
 #define I(j) asm volatile("v_sub_u32 %0, %1, %0\n\tv_alignbit_b32 %0, %0, %1, 31" : "+v"(a[j]) : "v"(b[j]));
         BODY8(I)
@@ -377,6 +405,18 @@ int main(int argc, char** argv) {
   CHECK(hipMalloc(&out, sizeof(float) * ncu * 4 * waves * 64 * 2));
   CHECK(hipMalloc(&st, 16));
   run<0>("v_fma_f32", waves, out, st, ncu);
+  run<35>("v_pk_max_i16", waves, out, st, ncu);
+  run<41>("v_pk_max_u16", waves, out, st, ncu);
+  run<75>("v_pk_min_u16", waves, out, st, ncu);
+  run<36>("v_pk_add_u16", waves, out, st, ncu);
+  run<40>("v_pk_sub_u16", waves, out, st, ncu);
+  run<74>("v_pk_sub_u16 clamp", waves, out, st, ncu);
+  run<76>("v_pk_mad_u16", waves, out, st, ncu);
+  run<77>("v_pk_mad_u16 clamp", waves, out, st, ncu);
+  run<78>("v_pk_ashrrev_i16", waves, out, st, ncu);
+  run<79>("v_pk_lshlrev_b16", waves, out, st, ncu);
+  run<80>("v_sub_u16 clamp", waves, out, st, ncu);
+  run<14>("v_and_b32", waves, out, st, ncu);
   run<68>("v_cvt_f32_ubyte1", waves, out, st, ncu);
   run<71>("v_cvt_f32_ubyte2", waves, out, st, ncu);
   run<69>("v_pk_fma_f32", waves, out, st, ncu);
