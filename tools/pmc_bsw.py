@@ -9,6 +9,7 @@ profiles/pmc_bsw.json for bench.py's SW roofline:
 
 usage: python tools/pmc_bsw.py gpurun_out/<tag> <tag>"""
 import csv
+import re
 import glob
 import json
 import os
@@ -67,7 +68,7 @@ def main():
             for r in csv.DictReader(open(f)):
                 n = r["Kernel_Name"]
                 if "bsw_global" in n and r["Counter_Name"] == "SQ_INSTS_VALU":
-                    k = "cigar" if ", true>" in n else "scores"  # bsw_global_lane_kernel<NB, CIG>
+                    k = "cigar" if re.search(r"<\d+, true", n) else "scores"  # bsw_global_lane_kernel<NB, CIG, U>
                     tot[k] = tot.get(k, 0.0) + float(r["Counter_Value"])
                 elif "traceback" in n and r["Counter_Name"] == "SQ_INSTS_VALU":
                     tot["traceback"] = tot.get("traceback", 0.0) + float(r["Counter_Value"])
