@@ -341,10 +341,25 @@ __host__ __device__ constexpr uint32_t glane_next2() {
   return t;
 }
 
-__device__ __forceinline__ void glane_traceback(const GLayout& L, int qlen, int tlen, int w,
-                                                uint32_t* __restrict__ cg, int cap, int32_t* __restrict__ n_out) {
+// The walk runs in blocks of kTbRows rows, wave-synchronously from the wave's
+// top row down: the block's nibble dwords (rows rb .. rb - kTbRows + 1 at the
+// dword the lane's band slot was in when the block before started) were
+// requested one block ahead and sit in LDS, one 256-byte row of the tile per
+// block row (lane L at dword L: every read is conflict-free whatever rows the
+// lanes are on).  A step whose cell is that dword of a block row reads it from
+// LDS; any other cell (an indel moved the slot across a dword, or the path left
+// the band) takes the direct load of the per-cell walk.  The per-row walk
+// waited on every row's load (137 us a 250k-task batch, 88 us with every load
+// an L2 hit, `r6u`); blocks of 4 rows run 101 us, of 8 / 16 rows 111 / 127 us
+// (lanes wait for the block's slowest path), two blocks ahead 112 us (`r6v`-`r6z`).
+constexpr int kTbRows = 4;
+__device__ __forceinline__ void glane_traceback(const GLayout& L, int qlen, int tlen, int w, int top,
+                                                uint32_t* __restrict__ tile, uint32_t* __restrict__ cg, int cap,
+                                                int32_t* __restrict__ n_out) {
+  const int lane = lane_id();
   const int n_col = min(qlen, 2 * w + 1);
   const long long zsize = (long long)n_col * tlen;
+  const int dmax = (2 * w) >> 3;  // the band's last nibble dword
   constexpr uint64_t T01 = glane_next01();
   constexpr uint32_t T2 = glane_next2();
   int crow = -1, cdw = -1;
@@ -353,53 +368,85 @@ __device__ __forceinline__ void glane_traceback(const GLayout& L, int qlen, int 
   uint32_t curlen = 0;
   int i = tlen - 1;
   int k = (i + w + 1 < qlen ? i + w + 1 : qlen) - 1;
-  while (i >= 0 && k >= 0) {
-    // bwa's byte (row i, band offset c = k - beg_i) is cell k - i + w of
-    // nibble row i; c past the row's band end reads 0, as bwa's zeroed bytes
-    // there do; a column left of the row's band start indexes bwa's flat
-    // matrix backwards into the rows above (row-major, n_col bytes a row)
-    // In band (|k - i| <= w; k < qlen always holds) the cell is slot
-    // k - i + w of nibble row i; only a path that left the band takes the
-    // general mapping below.
-    int r = i, kb = k - i + w;
-    bool have = (unsigned)kb <= (unsigned)(2 * w);
-    if (!have) {
-      int c = k - (i > w ? i - w : 0);
-      if (c < 0 || c >= n_col) {
-        const long long zi = (long long)i * n_col + c;
-        r = (zi < 0 || zi >= zsize) ? -1 : (int)(zi / n_col);
-        c = r < 0 ? 0 : (int)(zi - (long long)r * n_col);
+  // the first block's dwords, then each block's for the next
+  int rb = top;
+  int ndw = min(max((k - i + w) >> 3, 0), dmax);
+  uint32_t nx[kTbRows];
+  // global (not flat) loads: a flat load also counts in lgkmcnt, so every LDS
+  // read of the block would wait for the next block's requests
+  typedef const __attribute__((address_space(1))) uint32_t gu32;
+  gu32* const gbase = reinterpret_cast<gu32*>(reinterpret_cast<uintptr_t>(L.base));
+  auto request = [&](int row0, int dw) {
+    gu32* const p = gbase + dw * L.ds;
+#pragma unroll
+    for (int j = 0; j < kTbRows; ++j) nx[j] = p[(long long)min(max(row0 - j, 0), tlen - 1) * L.rs];
+  };
+  request(rb, ndw);
+  uint32_t* const mine = tile + lane;
+  bool live = i >= 0 && k >= 0;
+  while (__ballot(live) != 0ull) {
+#pragma unroll
+    for (int j = 0; j < kTbRows; ++j) mine[64 * j] = nx[j];
+    const int tdw = ndw;
+    ndw = min(max((k - i + w) >> 3, 0), dmax);
+    request(rb - kTbRows, ndw);
+    const int lo = rb - (kTbRows - 1);
+    for (;;) {
+      const bool act = live && i >= lo;
+      if (__ballot(act) == 0ull) break;
+      if (!act) continue;
+      // bwa's byte (row i, band offset c = k - beg_i) is cell k - i + w of
+      // nibble row i; c past the row's band end reads 0, as bwa's zeroed bytes
+      // there do; a column left of the row's band start indexes bwa's flat
+      // matrix backwards into the rows above (row-major, n_col bytes a row).
+      // In band (|k - i| <= w; k < qlen always holds) the cell is slot
+      // k - i + w of nibble row i; only a path that left the band takes the
+      // general mapping below.
+      int kb = k - i + w;
+      // the block row's dword from LDS (always inside the tile: lo <= i <= rb)
+      uint32_t nb = (mine[64 * (rb - i)] >> (28 - 4 * (kb & 7))) & 15u;
+      if (!((unsigned)kb <= (unsigned)(2 * w) && (kb >> 3) == tdw)) {
+        int r = i;
+        bool have = (unsigned)kb <= (unsigned)(2 * w);
+        if (!have) {
+          int c = k - (i > w ? i - w : 0);
+          if (c < 0 || c >= n_col) {
+            const long long zi = (long long)i * n_col + c;
+            r = (zi < 0 || zi >= zsize) ? -1 : (int)(zi / n_col);
+            c = r < 0 ? 0 : (int)(zi - (long long)r * n_col);
+          }
+          if (r >= 0) {
+            const int beg = r > w ? r - w : 0, end = r + w + 1 < qlen ? r + w + 1 : qlen;
+            have = beg + c < end;
+            kb = beg + c - r + w;
+          }
+        }
+        nb = 0;
+        if (have) {
+          const int dw = kb >> 3;
+          if (r != crow || dw != cdw) {
+            crow = r, cdw = dw;
+            cval = gbase[(long long)r * L.rs + dw * L.ds];
+          }
+          nb = (cval >> (28 - 4 * (kb & 7))) & 15u;
+        }
       }
-      if (r >= 0) {
-        const int beg = r > w ? r - w : 0, end = r + w + 1 < qlen ? r + w + 1 : qlen;
-        have = beg + c < end;
-        kb = beg + c - r + w;
-      }
-    }
-    uint32_t nb = 0;
-    if (have) {
-      const int dw = kb >> 3;
-      if (r != crow || dw != cdw) {
-        crow = r, cdw = dw;
-        cval = L.base[(long long)r * L.rs + dw * L.ds];
-      }
-      nb = (cval >> (28 - 4 * (kb & 7))) & 15u;
-    }
-    which = which == 2 ? (int)((T2 >> (2 * nb)) & 3u) : (int)((T01 >> (32 * which + 2 * nb)) & 3u);
-    // state M: diagonal (CIGAR M), E: up (D), F: left (I)
-    const int op = (int)((0x18u >> (2 * which)) & 3u);
-    i -= which != 2;
-    k -= which != 1;
-    if (op == curop) {
-      ++curlen;
-    } else {
-      if (curop >= 0) {
-        if (n < cap) cg[n] = curlen << 4 | (uint32_t)curop;
-        ++n;
-      }
+      // next state: one 32-bit table of 2-bit entries per state (no branch)
+      const uint32_t tbl = which == 0 ? (uint32_t)T01 : which == 1 ? (uint32_t)(T01 >> 32) : T2;
+      which = (int)((tbl >> (2 * nb)) & 3u);
+      // state M: diagonal (CIGAR M), E: up (D), F: left (I)
+      const int op = (int)((0x18u >> (2 * which)) & 3u);
+      i -= which != 2;
+      k -= which != 1;
+      live = i >= 0 && k >= 0;
+      // a run ends: stored while it fits (one branch around the store only)
+      const bool ends = op != curop && curop >= 0;
+      if (ends && n < cap) cg[n] = curlen << 4 | (uint32_t)curop;
+      n += ends;
+      curlen = op != curop ? 1u : curlen + 1u;
       curop = op;
-      curlen = 1;
     }
+    rb -= kTbRows;
   }
   auto push = [&](int op, int len) {
     if (op == curop) {
@@ -864,9 +911,11 @@ __global__ __launch_bounds__(64) void bsw_traceback_kernel(const BswDevBatch b, 
   // wave votes)
   const bool lane = exists && glane_ok(qlen, tlen, w, p.lane_ok != 0);
   const GLayout zl = glane_layout(b, p, zbuf, zoff, task, lane);
+  const int top = wave_max(lane ? tlen - 1 : -1);  // the lane walks' first block (every lane votes)
+  __shared__ uint32_t tile[kTbRows * 64];
   if (!exists) return;
   if (lane) {
-    glane_traceback(zl, qlen, tlen, w, cigar + cigar_off[task], cigar_cap[task], n_cigar + task);
+    glane_traceback(zl, qlen, tlen, w, top, tile, cigar + cigar_off[task], cigar_cap[task], n_cigar + task);
     return;
   }
   const int n_col = qlen < 2 * w + 1 ? qlen : 2 * w + 1;
