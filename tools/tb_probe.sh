@@ -8,7 +8,7 @@ cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT
 for f in in-tree "$@"; do
   n=$(basename $f .so)
   if [ $f = in-tree ]; then L=; else L=$PWD/$f; fi
-  FCSHIP_LIB=$L timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/$n -o run --output-format csv -- python tools/bsw_bench.py --which global > $O/$n.log 2>&1
+  FCSHIP_LIB=$L timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/$n -o run --output-format csv -- python tools/bsw_bench.py --which global ${BSW_ARGS:-} > $O/$n.log 2>&1
   rc=$?
   echo "$n rc=$rc"
   case $rc in 124|137|134|139) exit $rc;; esac
