@@ -103,7 +103,10 @@ def main():
                     "hbm_bytes_per_batch = 2 x FETCH_SIZE + WRITE_SIZE (the gfx950 FETCH_SIZE calibration, "
                     "profiles/fetch_calibration.json)")
     out["source"] = tag if "c3" not in prev or os.path.isdir(os.path.join(src, "bswpmc_c3")) else prev.get("source")
-    if "align" in out and not os.path.isdir(os.path.join(src, "bswpmc_c3")):
+    # per-section sources when a session collected only some sections
+    if os.path.isdir(gdir) and not os.path.isdir(os.path.join(src, "bswpmc_c3")):
+        out["global"]["source"] = tag
+    if os.path.isdir(adir) and not os.path.isdir(os.path.join(src, "bswpmc_c3")):
         out["align"]["source"] = tag
     json.dump(out, open(path, "w"), indent=1)
     print(json.dumps(out))
