@@ -19,10 +19,6 @@
 //     wave-uniform and every integer matches bwa bit for bit.
 #include <hip/hip_runtime.h>
 
-#include <algorithm>
-#include <atomic>
-#include <cstdlib>
-
 #include "bsw_scan.h"
 #include "fcship_internal.h"
 
@@ -763,8 +759,6 @@ __device__ void glane_run(const BswDevBatch& b, const BswParams& p, long long ta
 
 // One launch per band class (each with its own register budget): a wave runs
 // in the launch whose NB is the smallest of 17 / 33 / 65 holding its widest band.
-// t0: the launch's first task (a multiple of 64: the waves are the same 64-task
-// groups in every launch, see glane_layout).
 template <int NB, bool CIG>
 __global__ __launch_bounds__(64) void bsw_global_lane_kernel(const BswDevBatch b, const BswParams p,
                                                              int32_t* __restrict__ scores, uint8_t* __restrict__ zbuf,
@@ -772,8 +766,8 @@ __global__ __launch_bounds__(64) void bsw_global_lane_kernel(const BswDevBatch b
                                                              uint32_t* __restrict__ cigar,
                                                              const int64_t* __restrict__ cigar_off,
                                                              const int32_t* __restrict__ cigar_cap,
-                                                             int32_t* __restrict__ n_cigar, const long long t0) {
-  const long long task = t0 + (long long)blockIdx.x * 64 + threadIdx.x;
+                                                             int32_t* __restrict__ n_cigar) {
+  const long long task = (long long)blockIdx.x * 64 + threadIdx.x;
   bool ok = false;
   int w = -1;
   if (task < b.n) {
@@ -908,8 +902,8 @@ __global__ __launch_bounds__(64) void bsw_global_kernel(const BswDevBatch b, con
 __global__ __launch_bounds__(64) void bsw_traceback_kernel(const BswDevBatch b, const BswParams p, uint8_t* __restrict__ zbuf,
                                      const int64_t* __restrict__ zoff, uint32_t* __restrict__ cigar,
                                      const int64_t* __restrict__ cigar_off, const int32_t* __restrict__ cigar_cap,
-                                     int32_t* __restrict__ n_cigar, const long long t0) {
-  const long long task = t0 + (long long)blockIdx.x * blockDim.x + threadIdx.x;
+                                     int32_t* __restrict__ n_cigar) {
+  const long long task = (long long)blockIdx.x * blockDim.x + threadIdx.x;
   const bool exists = task < b.n;
   const int qlen = exists ? b.qlen[task] : 0, tlen = exists ? b.tlen[task] : 0, w = exists ? b.w[task] : 0;
   // lane-path tasks: their nibble rows, located as bsw_global_lane_kernel
@@ -972,27 +966,6 @@ __global__ __launch_bounds__(64) void bsw_traceback_kernel(const BswDevBatch b, 
   n_cigar[task] = n;
 }
 
-// Waves of one round of the lane DP on the current device (3 per SIMD, the
-// 33 class's occupancy); 0 turns the chunked CIGAR pass off (the A/B build
-// -DFCS_GLOBAL_PIPE=0).  FCS_GLOBAL_CHUNK_WAVES=n sets the chunk (the tests
-// run small batches as several chunks).
-long long global_pipe_chunk_waves() {
-#if defined(FCS_GLOBAL_PIPE) && FCS_GLOBAL_PIPE == 0
-  return 0;
-#else
-  if (const char* e = std::getenv("FCS_GLOBAL_CHUNK_WAVES")) return std::max(0LL, std::atoll(e));
-  static std::atomic<int> cus_of[64];
-  int dev = 0;
-  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 0;
-  int cus = cus_of[dev].load(std::memory_order_relaxed);
-  if (cus == 0) {
-    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0) return 0;
-    cus_of[dev].store(cus, std::memory_order_relaxed);
-  }
-  return (long long)cus * 4 * 3;
-#endif
-}
-
 int launch_bsw_global(const BswDevBatch& b, const BswParams& p, int max_qlen, int max_tlen, int32_t* scores,
                       uint8_t* zbuf, int64_t zbytes, const int64_t* zoff, uint32_t* cigar, const int64_t* cigar_off,
                       const int32_t* cigar_cap, int32_t* n_cigar, hipStream_t s) {
@@ -1010,57 +983,34 @@ int launch_bsw_global(const BswDevBatch& b, const BswParams& p, int max_qlen, in
   // narrow bands: one lane per task (64 consecutive tasks per wave)
   const long long lane_waves = (b.n + 63) / 64;
   if (lane_waves > 0x7FFFFFFFLL) return fail(FCS_ERR_UNSUPPORTED, "[E::fcship] ksw_global2: batch too large");
-  // lane waves [w0, w0 + nw) of the three band classes on stream st
-  auto lane_launch = [&](auto kern, long long w0, long long nw, hipStream_t st) -> int {
-    hipLaunchKernelGGL(kern, dim3((unsigned)nw), dim3(64), 0, st, b, p, scores, zbuf, zoff, cigar, cigar_off,
-                       cigar_cap, n_cigar, 64 * w0);
+  auto lane_launch = [&](auto kern) -> int {
+    hipLaunchKernelGGL(kern, dim3((unsigned)lane_waves), dim3(64), 0, s, b, p, scores, zbuf, zoff, cigar, cigar_off,
+                       cigar_cap, n_cigar);
     FCS_HIP_CHECK(hipGetLastError());
     return FCS_OK;
   };
-  auto lane_dp = [&](long long w0, long long nw) -> int {
-    int rc;
-    if (zbuf) {
-      if ((rc = lane_launch(bsw_global_lane_kernel<17, true>, w0, nw, s)) ||
-          (rc = lane_launch(bsw_global_lane_kernel<33, true>, w0, nw, s)) ||
-          (rc = lane_launch(bsw_global_lane_kernel<65, true>, w0, nw, s)))
-        return rc;
-    } else {
-      if ((rc = lane_launch(bsw_global_lane_kernel<17, false>, w0, nw, s)) ||
-          (rc = lane_launch(bsw_global_lane_kernel<33, false>, w0, nw, s)) ||
-          (rc = lane_launch(bsw_global_lane_kernel<65, false>, w0, nw, s)))
-        return rc;
-    }
-    return FCS_OK;
-  };
-  auto traceback = [&](long long w0, long long nw, hipStream_t st) -> int {
-    hipLaunchKernelGGL(bsw_traceback_kernel, dim3((unsigned)nw), dim3(64), 0, st, b, p, zbuf, zoff, cigar, cigar_off,
-                       cigar_cap, n_cigar, 64 * w0);
-    FCS_HIP_CHECK(hipGetLastError());
-    return FCS_OK;
-  };
-  // The wide-band tasks first: a traceback block covers every task of its
-  // waves, so their direction bytes must be written before any of it runs.
+  int rc;
+  if (zbuf) {
+    if ((rc = lane_launch(bsw_global_lane_kernel<17, true>)) || (rc = lane_launch(bsw_global_lane_kernel<33, true>)) ||
+        (rc = lane_launch(bsw_global_lane_kernel<65, true>)))
+      return rc;
+  } else {
+    if ((rc = lane_launch(bsw_global_lane_kernel<17, false>)) || (rc = lane_launch(bsw_global_lane_kernel<33, false>)) ||
+        (rc = lane_launch(bsw_global_lane_kernel<65, false>)))
+      return rc;
+  }
   if (max_qlen <= 255)
     hipLaunchKernelGGL(bsw_global_kernel<4>, dim3((unsigned)grid), dim3(64), lds, s, b, p, scores, zbuf, zoff);
   else
     hipLaunchKernelGGL(bsw_global_kernel<16>, dim3((unsigned)grid), dim3(64), lds, s, b, p, scores, zbuf, zoff);
   FCS_HIP_CHECK(hipGetLastError());
-  int rc;
-  const long long chunk = global_pipe_chunk_waves();
-  if (!cigar || chunk <= 0 || lane_waves <= chunk + chunk / 4) {
-    if ((rc = lane_dp(0, lane_waves))) return rc;
-    return cigar ? traceback(0, lane_waves, s) : FCS_OK;
+  if (cigar) {
+    const long long nb = (b.n + 63) / 64;
+    hipLaunchKernelGGL(bsw_traceback_kernel, dim3((unsigned)nb), dim3(64), 0, s, b, p, zbuf, zoff, cigar, cigar_off,
+                       cigar_cap, n_cigar);
+    FCS_HIP_CHECK(hipGetLastError());
   }
-  // A CIGAR pass longer than one round of resident DP waves runs as chunks of
-  // one round each: chunk c's traceback (a chain of dependent loads per lane,
-  // 41 VGPRs) runs on a side stream beside chunk c + 1's DP (issue-bound), so
-  // only the last chunk's traceback is exposed.
-  hipStream_t fs[kForkStreams];
-  for (long long w0 = 0; w0 < lane_waves; w0 += chunk) {
-    const long long nw = std::min(chunk, lane_waves - w0);
-    if ((rc = lane_dp(w0, nw)) || (rc = fork_streams(s, fs)) || (rc = traceback(w0, nw, fs[1]))) return rc;
-  }
-  return join_streams(s, fs);
+  return FCS_OK;
 }
 
 }  // namespace fcs

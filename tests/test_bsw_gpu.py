@@ -344,20 +344,6 @@ def test_global_dev_direction_layouts(gpu, gap):
         assert np.array_equal(got, rc), f"task {k}: {fcship.cigar_str(got)} != {fcship.cigar_str(rc)}"
 
 
-@pytest.mark.parametrize("chunk", [1, 2, 5])
-def test_global_chunked_cigar_pass(gpu, monkeypatch, chunk):
-    """A CIGAR pass longer than one round of resident DP waves runs in chunks,
-    each chunk's traceback on a side stream beside the next chunk's DP
-    (launch_bsw_global).  FCS_GLOBAL_CHUNK_WAVES forces small chunks so that
-    these batches (7 to 24 waves, mixed lane / wave paths, both direction
-    layouts, narrow bands) cross several chunk boundaries; still bit-exact."""
-    monkeypatch.setenv("FCS_GLOBAL_CHUNK_WAVES", str(chunk))
-    test_global_scores_and_cigars(gpu)
-    test_global_dev_direction_layouts(gpu, 0)
-    test_global_dev_direction_layouts(gpu, 24)
-    test_global_lane_kernel_narrow_bands(gpu, 16)
-
-
 def align_tasks(seed, n, qmin=20, qmax=200, tmin=40, tmax=700, related=0.7):
     """Mate-rescue-shaped ksw_align2 tasks: a query that is (mostly) a mutated
     piece of its target window, sometimes twice (score2), sometimes unrelated."""
